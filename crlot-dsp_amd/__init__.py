@@ -1,0 +1,297 @@
+"""crlot-dsp_amd -- MI355X-native batched STFT -> iSTFT -> OLA engine (Python host binding).
+
+Thin ctypes layer over the C ABI in include/crlot_dsp.h (libcrlot_dsp.so, built
+in-tree by __graft_entry__.build()).  PyTorch is used only for device memory and
+the current HIP stream.  Names and argument meanings follow the reference's
+C++ API (dsp::Framer / WindowLUT / fft::IFftPlan / OLAAccumulator); error codes
+map to the reference's exception types: CRLOT_EINVAL -> ValueError
+(std::invalid_argument), CRLOT_ERUNTIME / CRLOT_EHIP -> RuntimeError
+(std::runtime_error), CRLOT_ENOMEM -> MemoryError (std::bad_alloc),
+CRLOT_EUNSUPPORTED -> NotImplementedError.
+
+There is no CPU fallback: if the library cannot be loaded, every entry raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcrlot_dsp.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "crlot_dsp.h")
+
+# dsp::WindowType / NormalizationType / BoundaryMode ordinals
+HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS = range(5)
+NORM_NONE, NORM_SUM_TO_ONE, NORM_L2, NORM_OLA_UNITY_GAIN, NORM_OLA_SUM_WSQ = range(5)
+ZERO_PAD, DROP = 0, 1
+
+OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4, -5
+
+
+class PlanDesc(C.Structure):
+    """crlot_plan_desc (include/crlot_dsp.h)."""
+    _fields_ = [
+        ("frame_size", C.c_int32),
+        ("hop_size", C.c_int32),
+        ("window_type", C.c_int32),
+        ("periodic", C.c_int32),
+        ("window_norm", C.c_int32),
+        ("boundary_mode", C.c_int32),
+        ("analysis_window", C.c_int32),
+        ("apply_window_inside", C.c_int32),
+        ("eps", C.c_float),
+        ("ola_gain", C.c_float),
+        ("ring_len", C.c_int32),
+        ("device", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Load libcrlot_dsp.so (raises if it is missing: no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+    fp = C.POINTER(C.c_float)
+    sig = {
+        "crlot_last_error": ([], C.c_char_p),
+        "crlot_abi_version": ([], C.c_int),
+        "crlot_plan_create": ([C.POINTER(PlanDesc), C.POINTER(vp)], C.c_int),
+        "crlot_plan_destroy": ([vp], None),
+        "crlot_plan_upload_tables": ([vp, vp, vp], C.c_int),
+        "crlot_plan_set_spectral_gain": ([vp, vp], C.c_int),
+        "crlot_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "crlot_frame_count": ([vp, i64], i64),
+        "crlot_output_length": ([vp, i64], i64),
+        "crlot_workspace_bytes": ([vp, i32, i64], i64),
+        "crlot_plan_reserve": ([vp, i64], C.c_int),
+        "crlot_roundtrip": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
+        "crlot_roundtrip_stages": ([vp, vp, i32, i64, i64, vp, vp, vp], C.c_int),
+        "crlot_ola_gather": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
+        "crlot_rfft_batched": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_irfft_batched": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_stream_create": ([vp, i32, C.POINTER(vp)], C.c_int),
+        "crlot_stream_destroy": ([vp], None),
+        "crlot_stream_reset": ([vp], C.c_int),
+        "crlot_stream_push_hop": ([vp, vp, vp, C.POINTER(i32), vp], C.c_int),
+        "crlot_window_table": ([i32, i64, i32, i32, fp], C.c_int),
+        "crlot_ring_len": ([i64, i64], i64),
+        "crlot_norm_table": ([fp, i64, i64, i64, i32, f32, fp], C.c_int),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str = "") -> int:
+    if rc >= 0:
+        return rc
+    msg = lib().crlot_last_error().decode(errors="replace")
+    msg = f"{what}: {msg}" if what else msg
+    if rc == EINVAL:
+        raise ValueError(msg)
+    if rc == EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    if rc == ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+# ----------------------------------------------------------------- host tables
+def window_table(wtype: int, n: int, periodic: bool = False, norm: int = NORM_NONE) -> np.ndarray:
+    """WindowLUT(n, type, periodic, norm).data() (WindowLUT.cc:215-388)."""
+    out = np.zeros(max(n, 1), np.float32)
+    _check(lib().crlot_window_table(wtype, n, int(periodic), norm, _fptr(out)), "window")
+    return out[:n]
+
+
+def ring_len(frame_size: int, hop: int) -> int:
+    return _check(int(lib().crlot_ring_len(frame_size, hop)), "ring_len")
+
+
+def norm_table(window, frame_size: int, hop: int, ring: int | None = None,
+               apply_window_inside: bool = True, eps: float = 1e-8) -> np.ndarray:
+    ring = ring_len(frame_size, hop) if ring is None else ring
+    out = np.zeros(ring, np.float32)
+    w = None if window is None else np.ascontiguousarray(window, np.float32)
+    _check(lib().crlot_norm_table(None if w is None else _fptr(w), frame_size, hop, ring,
+                                  int(apply_window_inside), eps, _fptr(out)), "norm")
+    return out
+
+
+def header_symbols() -> list[str]:
+    """Every function the C header declares (for the ABI-surface test)."""
+    import re
+    txt = open(HEADER_PATH).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(crlot_[a-z0-9_]+)\s*\(", txt)))
+
+
+# ----------------------------------------------------------------- device plan
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_handle(tensor) -> int:
+    torch = _torch()
+    return int(torch.cuda.current_stream(tensor.device).cuda_stream)
+
+
+@dataclass
+class PlanConfig:
+    frame_size: int = 1024
+    hop_size: int = 256
+    window_type: int = HANN
+    periodic: bool = False
+    window_norm: int = NORM_NONE
+    boundary_mode: int = ZERO_PAD
+    analysis_window: bool = True
+    apply_window_inside: bool = True
+    eps: float = 1e-8
+    ola_gain: float = 1.0
+    ring_len: int = 0
+    device: int = -1
+
+
+class Plan:
+    """A device plan: tables resident in HBM, kernels dispatched per call.
+
+    The default configuration is the reference harness's round trip
+    (bench/e2e_benchmark.cc:42-76): symmetric Hann analysis window applied by the
+    caller, window applied again inside the OLA, ZERO_PAD whole-stream framing.
+    """
+
+    def __init__(self, cfg: PlanConfig | None = None, **kw):
+        cfg = cfg or PlanConfig(**kw)
+        self.cfg = cfg
+        d = PlanDesc(cfg.frame_size, cfg.hop_size, cfg.window_type, int(cfg.periodic),
+                     cfg.window_norm, cfg.boundary_mode, int(cfg.analysis_window),
+                     int(cfg.apply_window_inside), cfg.eps, cfg.ola_gain, cfg.ring_len,
+                     cfg.device)
+        h = C.c_void_p()
+        _check(lib().crlot_plan_create(C.byref(d), C.byref(h)), "crlot_plan_create")
+        self._h = h
+        n, hop, ring = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(lib().crlot_plan_info(self._h, C.byref(n), C.byref(hop), C.byref(ring)))
+        self.frame_size, self.hop_size, self.ring_len = n.value, hop.value, ring.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().crlot_plan_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    # -- sizes
+    def frame_count(self, T: int) -> int:
+        return _check(int(lib().crlot_frame_count(self._h, T)))
+
+    def output_length(self, T: int) -> int:
+        return _check(int(lib().crlot_output_length(self._h, T)))
+
+    def workspace_bytes(self, n_streams: int, T: int) -> int:
+        return _check(int(lib().crlot_workspace_bytes(self._h, n_streams, T)))
+
+    def reserve(self, nbytes: int):
+        _check(lib().crlot_plan_reserve(self._h, nbytes))
+
+    def upload_tables(self, window=None, norm=None):
+        w = None if window is None else np.ascontiguousarray(window, np.float32)
+        nm = None if norm is None else np.ascontiguousarray(norm, np.float32)
+        _check(lib().crlot_plan_upload_tables(self._h, None if w is None else w.ctypes.data,
+                                              None if nm is None else nm.ctypes.data))
+
+    def set_spectral_gain(self, gain=None):
+        g = None if gain is None else np.ascontiguousarray(gain, np.float32)
+        if g is not None and g.size != self.frame_size // 2 + 1:
+            raise ValueError("gain needs N/2+1 bins")
+        _check(lib().crlot_plan_set_spectral_gain(self._h, None if g is None else g.ctypes.data))
+
+    # -- hot path
+    def roundtrip(self, x, y=None, stream: int | None = None):
+        """x: (S, T) float32 CUDA tensor -> y: (S, F*H)."""
+        torch = _torch()
+        if x.dim() == 1:
+            return self.roundtrip(x[None], None if y is None else y[None], stream)[0]
+        if x.dtype != torch.float32 or not x.is_cuda:
+            raise ValueError("x must be a float32 device tensor")
+        S, T = x.shape
+        if x.stride(1) != 1:
+            raise ValueError("x rows must be contiguous")
+        L = self.output_length(T)
+        if y is None:
+            y = torch.empty((S, L), dtype=torch.float32, device=x.device)
+        if y.shape[0] != S or y.shape[1] < L or y.stride(1) != 1:
+            raise ValueError("bad y shape")
+        s = _stream_handle(x) if stream is None else stream
+        _check(lib().crlot_roundtrip(self._h, x.data_ptr(), y.data_ptr(), S, T, x.stride(0),
+                                     y.stride(0), s), "crlot_roundtrip")
+        return y
+
+    def stages(self, x, want_spec=True):
+        """Per-stage outputs: frames (S, F, N) push_frame_AoS inputs, spec (S, F, N/2+1)."""
+        torch = _torch()
+        S, T = x.shape
+        F = self.frame_count(T)
+        n = self.frame_size
+        frames = torch.empty((S, F, n), dtype=torch.float32, device=x.device)
+        spec = (torch.empty((S, F, n // 2 + 1), dtype=torch.complex64, device=x.device)
+                if want_spec else None)
+        _check(lib().crlot_roundtrip_stages(self._h, x.data_ptr(), S, T, x.stride(0),
+                                            frames.data_ptr(),
+                                            None if spec is None else spec.data_ptr(),
+                                            _stream_handle(x)), "crlot_roundtrip_stages")
+        return frames, spec
+
+    def ola_gather(self, frames, y=None):
+        """frames (S, F, N) -> y (S, F*H) through the bit-exact OLA kernel."""
+        torch = _torch()
+        S, F, n = frames.shape
+        if n != self.frame_size or frames.stride(2) != 1 or frames.stride(0) != F * frames.stride(1):
+            raise ValueError("frames must be (S, F, N) with contiguous (F, N) blocks")
+        L = F * self.hop_size
+        if y is None:
+            y = torch.empty((S, L), dtype=torch.float32, device=frames.device)
+        _check(lib().crlot_ola_gather(self._h, frames.data_ptr(), y.data_ptr(), S, F,
+                                      frames.stride(1), y.stride(0), _stream_handle(frames)),
+               "crlot_ola_gather")
+        return y
+
+    def rfft(self, x):
+        """(B, N) real -> (B, N/2+1) complex, KissFftPlan::forward semantics."""
+        torch = _torch()
+        B, n = x.shape
+        out = torch.empty((B, n // 2 + 1), dtype=torch.complex64, device=x.device)
+        _check(lib().crlot_rfft_batched(self._h, x.data_ptr(), out.data_ptr(), B, x.stride(0),
+                                        x.stride(1), 2 * out.stride(0), 1, _stream_handle(x)),
+               "crlot_rfft_batched")
+        return out
+
+    def irfft(self, X):
+        """(B, N/2+1) complex -> (B, N) real, KissFftPlan::inverse semantics."""
+        torch = _torch()
+        B, bins = X.shape
+        n = self.frame_size
+        X = X.contiguous()
+        out = torch.empty((B, n), dtype=torch.float32, device=X.device)
+        _check(lib().crlot_irfft_batched(self._h, X.data_ptr(), out.data_ptr(), B, 2 * X.stride(0),
+                                         1, out.stride(0), 1, _stream_handle(X)),
+               "crlot_irfft_batched")
+        return out

@@ -1,0 +1,411 @@
+// abi.cpp -- the C ABI (include/crlot_dsp.h): plans, validation, dispatch.
+//
+// A plan owns its device tables (window, synthesis window, max(norm, eps),
+// twiddles, super twiddles, optional spectral gain) built once on the host by
+// the reference formulas and uploaded at creation.  crlot_roundtrip picks the
+// fused kernel when the shape has one (N in 256..2048, H % 128 == 0, N % H == 0,
+// 8-byte aligned streams) and otherwise the staged synth + gather pair, which
+// handles any hop and N up to 4096 through a plan-owned frame workspace.
+// There is no CPU fallback: an unsupported shape is CRLOT_EUNSUPPORTED.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "crlot_dsp.h"
+#include "kernels.h"
+
+struct crlot_plan {
+    crlot_plan_desc desc{};
+    int device = 0;
+    crlot::Geometry geo;
+    int boundary = CRLOT_ZERO_PAD;
+    // host copies
+    std::vector<float> window, norm;
+    bool has_gain = false;
+    // device tables
+    float* d_wa = nullptr;
+    float* d_ws = nullptr;
+    float* d_den = nullptr;
+    float* d_tw = nullptr;
+    float* d_st = nullptr;
+    float* d_gain = nullptr;
+    // staged-path workspace
+    float* d_work = nullptr;
+    int64_t work_bytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(CRLOT_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+crlot::DevTables tables(const crlot_plan* p) {
+    crlot::DevTables t;
+    t.wa = p->d_wa;
+    t.ws = p->d_ws;
+    t.den = p->d_den;
+    t.tw = p->d_tw;
+    t.st = p->d_st;
+    t.gain = p->has_gain ? p->d_gain : nullptr;
+    return t;
+}
+
+void free_plan(crlot_plan* p) {
+    if (!p) return;
+    DeviceGuard g(p->device);
+    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work})
+        if (q) (void)hipFree(q);
+    delete p;
+}
+
+// Upload window-derived tables: analysis window, synthesis window, den.
+int upload_window_tables(crlot_plan* p) {
+    const int n = p->geo.n;
+    std::vector<float> ones(n, 1.0f);
+    const std::vector<float>& wa = p->desc.analysis_window ? p->window : ones;
+    // apply_window_inside: the OLA multiplies by its copy of the window
+    // (OLAAccumulator.cc:82-83); the harness passes window = nullptr, so
+    // without it the frames are added unwindowed.
+    const std::vector<float>& ws = p->desc.apply_window_inside ? p->window : ones;
+    std::vector<float> den(p->norm.size());
+    const float eps = p->desc.eps;
+    for (size_t i = 0; i < den.size(); ++i)
+        den[i] = (p->norm[i] > eps) ? p->norm[i] : eps;  // kernels.cc:32
+    hipError_t e;
+    if ((e = hipMemcpy(p->d_wa, wa.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(p->d_ws, ws.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(p->d_den, den.data(), sizeof(float) * den.size(), hipMemcpyHostToDevice)))
+        return hip_fail(e, "hipMemcpy(tables)");
+    return CRLOT_OK;
+}
+
+int ensure_workspace(crlot_plan* p, int64_t bytes) {
+    if (bytes <= p->work_bytes) return CRLOT_OK;
+    if (p->d_work) (void)hipFree(p->d_work);
+    p->d_work = nullptr;
+    p->work_bytes = 0;
+    hipError_t e = hipMalloc(&p->d_work, size_t(bytes));
+    if (e != hipSuccess) return fail(CRLOT_ENOMEM, "workspace hipMalloc failed");
+    p->work_bytes = bytes;
+    return CRLOT_OK;
+}
+
+int64_t frames_for(const crlot_plan* p, int64_t T) {
+    const int64_t n = p->geo.n, h = p->geo.h;
+    if (T <= 0) return 0;
+    if (p->boundary == CRLOT_ZERO_PAD) return (T + h - 1) / h;  // framer.cc:88-117, whole push
+    if (T < n) return 0;
+    return (T - n) / h + 1;
+}
+
+bool aligned8(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 7u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+const char* crlot_last_error(void) { return g_err.c_str(); }
+int crlot_abi_version(void) { return CRLOT_ABI_VERSION; }
+
+int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
+    if (!desc_in || !out) return fail(CRLOT_EINVAL, "null argument");
+    *out = nullptr;
+    crlot_plan_desc d = *desc_in;
+    if (d.eps == 0.0f) d.eps = 1e-8f;
+    if (d.ola_gain == 0.0f) d.ola_gain = 1.0f;
+    // OLAConfig::isValid (OLAAccumulator.h:25-28), Framer::set_params (framer.cc:15-35)
+    if (d.frame_size <= 0) return fail(CRLOT_EINVAL, "Frame size must be greater than 0");
+    if (d.hop_size <= 0) return fail(CRLOT_EINVAL, "Hop size must be greater than 0");
+    if (!(d.eps > 0.0f)) return fail(CRLOT_EINVAL, "Invalid OLA configuration (eps)");
+    // MakeFftPlan (kissfft_adapter.cc:44-46)
+    if (d.frame_size % 2 != 0) return fail(CRLOT_ERUNTIME, "FFT size must be even for real FFT");
+    if (d.window_type == CRLOT_WIN_BLACKMAN_HARRIS)
+        return fail(CRLOT_EINVAL, "Blackman-Harris window not yet implemented");
+    if (d.window_type < CRLOT_WIN_HANN || d.window_type > CRLOT_WIN_RECT)
+        return fail(CRLOT_EINVAL, "Unknown window type");
+    if (d.boundary_mode != CRLOT_ZERO_PAD && d.boundary_mode != CRLOT_DROP)
+        return fail(CRLOT_EINVAL, "Unknown boundary mode");
+    if (d.hop_size > d.frame_size)
+        return fail(CRLOT_EUNSUPPORTED, "hop larger than frame is not supported on the GPU path");
+    if (!is_pow2(d.frame_size) || d.frame_size < 256 || d.frame_size > 4096)
+        return fail(CRLOT_EUNSUPPORTED,
+                    "GPU path supports power-of-two frame sizes 256..4096, got " +
+                        std::to_string(d.frame_size));
+
+    crlot_plan* p = new crlot_plan();
+    p->desc = d;
+    p->boundary = d.boundary_mode;
+    if (d.device < 0) {
+        if (hipGetDevice(&p->device) != hipSuccess) {
+            delete p;
+            return fail(CRLOT_EHIP, "no HIP device");
+        }
+    } else {
+        p->device = d.device;
+    }
+    DeviceGuard guard(p->device);
+    const int n = d.frame_size, h = d.hop_size;
+    const int ring = d.ring_len > 0 ? d.ring_len : int(crlot_ring_len(n, h));
+    if (ring < n) {
+        delete p;
+        return fail(CRLOT_EINVAL, "ring_len must be >= frame_size");
+    }
+    p->geo.n = n;
+    p->geo.h = h;
+    p->geo.ring_len = ring;
+    p->geo.inv_n = 1.0f / float(n);  // kissfft_adapter.cc:154
+    p->geo.gain = d.ola_gain;
+    p->window.resize(n);
+    int rc = crlot_window_table(d.window_type, n, d.periodic, d.window_norm, p->window.data());
+    if (rc != CRLOT_OK) {
+        delete p;
+        return fail(rc, "window table");
+    }
+    p->norm.resize(ring);
+    crlot_norm_table(p->window.data(), n, h, ring, d.apply_window_inside, d.eps, p->norm.data());
+
+    const int P = n / 2;
+    std::vector<float> tw(2 * P), st(2 * P);
+    for (int t = 0; t < P; ++t) {
+        const double ph = -2.0 * M_PI * double(t) / double(P);
+        tw[2 * t] = float(std::cos(ph));
+        tw[2 * t + 1] = float(std::sin(ph));
+        const double ps = -M_PI * (double(t) / double(P) + 0.5);
+        st[2 * t] = float(std::cos(ps));
+        st[2 * t + 1] = float(std::sin(ps));
+    }
+    hipError_t e;
+    if ((e = hipMalloc(&p->d_wa, sizeof(float) * n)) ||
+        (e = hipMalloc(&p->d_ws, sizeof(float) * n)) ||
+        (e = hipMalloc(&p->d_den, sizeof(float) * ring)) ||
+        (e = hipMalloc(&p->d_tw, sizeof(float) * 2 * P)) ||
+        (e = hipMalloc(&p->d_st, sizeof(float) * 2 * P)) ||
+        (e = hipMalloc(&p->d_gain, sizeof(float) * (P + 1)))) {
+        free_plan(p);
+        return hip_fail(e, "hipMalloc(plan tables)");
+    }
+    if ((e = hipMemcpy(p->d_tw, tw.data(), sizeof(float) * 2 * P, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(p->d_st, st.data(), sizeof(float) * 2 * P, hipMemcpyHostToDevice))) {
+        free_plan(p);
+        return hip_fail(e, "hipMemcpy(twiddles)");
+    }
+    rc = upload_window_tables(p);
+    if (rc != CRLOT_OK) {
+        free_plan(p);
+        return rc;
+    }
+    *out = p;
+    return CRLOT_OK;
+}
+
+void crlot_plan_destroy(crlot_plan* plan) { free_plan(plan); }
+
+int crlot_plan_upload_tables(crlot_plan* p, const float* window, const float* norm) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    DeviceGuard g(p->device);
+    if (window) std::memcpy(p->window.data(), window, sizeof(float) * p->window.size());
+    if (norm) {
+        std::memcpy(p->norm.data(), norm, sizeof(float) * p->norm.size());
+    } else if (window) {
+        // OLAAccumulator::set_window re-derives the norm (OLAAccumulator.cc:50-51)
+        crlot_norm_table(p->window.data(), p->geo.n, p->geo.h, p->geo.ring_len,
+                         p->desc.apply_window_inside, p->desc.eps, p->norm.data());
+    }
+    return upload_window_tables(p);
+}
+
+int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    DeviceGuard g(p->device);
+    if (!gain) {
+        p->has_gain = false;
+        return CRLOT_OK;
+    }
+    const int bins = p->geo.n / 2 + 1;
+    hipError_t e = hipMemcpy(p->d_gain, gain, sizeof(float) * bins, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(gain)");
+    p->has_gain = true;
+    return CRLOT_OK;
+}
+
+int crlot_plan_info(const crlot_plan* p, int32_t* n, int32_t* h, int32_t* ring) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n) *n = p->geo.n;
+    if (h) *h = p->geo.h;
+    if (ring) *ring = p->geo.ring_len;
+    return CRLOT_OK;
+}
+
+int64_t crlot_frame_count(const crlot_plan* p, int64_t T) {
+    if (!p || T < 0) return fail(CRLOT_EINVAL, "bad argument");
+    return frames_for(p, T);
+}
+
+int64_t crlot_output_length(const crlot_plan* p, int64_t T) {
+    if (!p || T < 0) return fail(CRLOT_EINVAL, "bad argument");
+    return frames_for(p, T) * p->geo.h;
+}
+
+static bool use_fused(const crlot_plan* p, const float* x, const float* y, int64_t ld_x,
+                      int64_t ld_y) {
+    return crlot::fused_supported(p->geo.n, p->geo.h) && p->geo.ring_len % p->geo.h == 0 &&
+           aligned8(x) && aligned8(y) && ld_x % 2 == 0 && ld_y % 2 == 0;
+}
+
+int64_t crlot_workspace_bytes(const crlot_plan* p, int32_t n_streams, int64_t T) {
+    if (!p || n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "bad argument");
+    return int64_t(n_streams) * frames_for(p, T) * p->geo.n * int64_t(sizeof(float));
+}
+
+int crlot_plan_reserve(crlot_plan* p, int64_t bytes) {
+    if (!p || bytes < 0) return fail(CRLOT_EINVAL, "bad argument");
+    DeviceGuard g(p->device);
+    return ensure_workspace(p, bytes);
+}
+
+int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_streams, int64_t T,
+                    int64_t ld_x, int64_t ld_y, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "negative size");
+    if (n_streams == 0 || T == 0) return CRLOT_OK;
+    if (!d_x || !d_y) return fail(CRLOT_EINVAL, "null buffer");
+    const int64_t F = frames_for(p, T);
+    if (F == 0) return CRLOT_OK;  // DROP with T < N: the Framer never yields
+    const int64_t out_len = F * p->geo.h;
+    if (ld_x < T || ld_y < out_len) return fail(CRLOT_EINVAL, "leading dimension too small");
+    DeviceGuard g(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const crlot::DevTables t = tables(p);
+    hipError_t e;
+    if (use_fused(p, d_x, d_y, ld_x, ld_y)) {
+        e = crlot::launch_fused(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s);
+        if (e != hipSuccess) return hip_fail(e, "fused kernel launch");
+        return CRLOT_OK;
+    }
+    const int64_t need = int64_t(n_streams) * F * p->geo.n * int64_t(sizeof(float));
+    int rc = ensure_workspace(p, need);
+    if (rc != CRLOT_OK) return rc;
+    e = crlot::launch_synth_frames(p->geo, t, d_x, n_streams, T, ld_x, F, p->d_work, nullptr, s);
+    if (e != hipSuccess) return hip_fail(e, "synth kernel launch");
+    e = crlot::launch_ola_gather(p->geo, t, p->d_work, p->geo.n, d_y, n_streams, F, ld_y,
+                                 out_len, s);
+    if (e != hipSuccess) return hip_fail(e, "gather kernel launch");
+    return CRLOT_OK;
+}
+
+int crlot_roundtrip_stages(crlot_plan* p, const float* d_x, int32_t n_streams, int64_t T,
+                           int64_t ld_x, float* d_frames, float* d_spec, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_streams < 0 || T < 0 || ld_x < T) return fail(CRLOT_EINVAL, "bad size");
+    if (!d_x || !d_frames) return fail(CRLOT_EINVAL, "null buffer");
+    const int64_t F = frames_for(p, T);
+    if (F == 0 || n_streams == 0) return CRLOT_OK;
+    DeviceGuard g(p->device);
+    hipError_t e = crlot::launch_synth_frames(p->geo, tables(p), d_x, n_streams, T, ld_x, F,
+                                              d_frames, d_spec, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "synth kernel launch");
+    return CRLOT_OK;
+}
+
+int crlot_ola_gather(crlot_plan* p, const float* d_frames, float* d_y, int32_t n_streams,
+                     int64_t F, int64_t ld_frames, int64_t ld_y, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_streams < 0 || F < 0) return fail(CRLOT_EINVAL, "negative size");
+    if (n_streams == 0 || F == 0) return CRLOT_OK;
+    if (!d_frames || !d_y) return fail(CRLOT_EINVAL, "null buffer");
+    const int64_t out_len = F * p->geo.h;
+    if (ld_frames < p->geo.n || ld_y < out_len)
+        return fail(CRLOT_EINVAL, "leading dimension too small");
+    DeviceGuard g(p->device);
+    hipError_t e = crlot::launch_ola_gather(p->geo, tables(p), d_frames, ld_frames, d_y,
+                                            n_streams, F, ld_y, out_len,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "gather kernel launch");
+    return CRLOT_OK;
+}
+
+int crlot_rfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t batch,
+                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                       void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (batch < 0 || inc_in < 1 || inc_out < 1) return fail(CRLOT_EINVAL, "bad batch/stride");
+    if (batch == 0) return CRLOT_OK;
+    if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
+    DeviceGuard g(p->device);
+    hipError_t e = crlot::launch_rfft(p->geo, tables(p), d_in, d_out, batch, ld_in, inc_in, ld_out,
+                                      inc_out, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "rfft kernel launch");
+    return CRLOT_OK;
+}
+
+int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t batch,
+                        int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                        void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (batch < 0 || inc_in < 1 || inc_out < 1) return fail(CRLOT_EINVAL, "bad batch/stride");
+    if (batch == 0) return CRLOT_OK;
+    if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
+    DeviceGuard g(p->device);
+    hipError_t e = crlot::launch_irfft(p->geo, tables(p), d_in, d_out, batch, ld_in, inc_in,
+                                       ld_out, inc_out, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "irfft kernel launch");
+    return CRLOT_OK;
+}
+
+// ------------------------------------------------------------------ streaming
+struct crlot_stream {
+    crlot_plan* plan = nullptr;
+    int channels = 0;
+};
+
+int crlot_stream_create(crlot_plan* p, int32_t channels, crlot_stream** out) {
+    if (!p || !out || channels <= 0) return fail(CRLOT_EINVAL, "bad argument");
+    *out = nullptr;
+    return fail(CRLOT_EUNSUPPORTED, "streaming path not built yet");
+}
+
+void crlot_stream_destroy(crlot_stream* st) { delete st; }
+
+int crlot_stream_reset(crlot_stream* st) {
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    return fail(CRLOT_EUNSUPPORTED, "streaming path not built yet");
+}
+
+int crlot_stream_push_hop(crlot_stream* st, const float* d_in, float* d_out, int32_t* emitted,
+                          void* stream) {
+    (void)d_in;
+    (void)d_out;
+    (void)stream;
+    if (emitted) *emitted = 0;
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    return fail(CRLOT_EUNSUPPORTED, "streaming path not built yet");
+}
+
+}  // extern "C"

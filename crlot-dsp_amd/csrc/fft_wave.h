@@ -1,0 +1,239 @@
+// fft_wave.h -- one-wavefront complex FFT building blocks for gfx950 (CDNA4).
+//
+// A real frame of N samples is transformed as a complex sequence of P = N/2
+// points z[n] = x[2n] + i x[2n+1] (the kiss_fftr split, kiss_fftr.c), held by
+// ONE 64-lane wave: lane l owns z[l + 64 m], m = 0..E-1, E = P/64 ("lane-major").
+//
+// The complex FFT is a radix-8/4/2 Stockham autosort (decimation in time):
+//   pass with current sub-length Ns and radix R: butterfly j in [0, P/R) reads
+//   x[j + r P/R] (r < R), twiddles by W_{Ns R}^{r (j mod Ns)}, runs a length-R
+//   DFT and writes y[(j / Ns) Ns R + (j mod Ns) + r Ns].
+// With j = lane + 64 b every read is lane-major (no data movement), the first
+// pass (Ns = 1) needs no twiddles, and the LAST pass writes lane-major too, so a
+// P-point FFT costs (passes - 1) LDS exchanges and leaves its output in natural
+// order in registers.  Exchanges go through a per-wave LDS buffer padded by one
+// element every 8 (phys(i) = i + i/8) so the stride-R writes of early passes are
+// bank-conflict free for ds_write_b64.
+//
+// Arithmetic is IEEE f32; the translation unit is built with -ffp-contract=off,
+// so every FMA below is explicit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace crlot {
+namespace dev {
+
+struct cf {
+    float r, i;
+};
+
+__device__ __forceinline__ cf cadd(cf a, cf b) { return {a.r + b.r, a.i + b.i}; }
+__device__ __forceinline__ cf csub(cf a, cf b) { return {a.r - b.r, a.i - b.i}; }
+__device__ __forceinline__ cf conj(cf a) { return {a.r, -a.i}; }
+// a * w with two FMAs
+__device__ __forceinline__ cf cmul(cf a, cf w) {
+    return {__builtin_fmaf(a.r, w.r, -(a.i * w.i)), __builtin_fmaf(a.r, w.i, a.i * w.r)};
+}
+// a * conj(w)
+__device__ __forceinline__ cf cmulc(cf a, cf w) {
+    return {__builtin_fmaf(a.r, w.r, a.i * w.i), __builtin_fmaf(a.i, w.r, -(a.r * w.i))};
+}
+// multiply by -i (forward) / +i (inverse)
+template <bool INV>
+__device__ __forceinline__ cf mul_mi(cf a) {
+    return INV ? cf{-a.i, a.r} : cf{a.i, -a.r};
+}
+
+// ------------------------------------------------------------- small DFTs
+template <bool INV>
+__device__ __forceinline__ void dft2(cf& a, cf& b) {
+    cf t = a;
+    a = cadd(t, b);
+    b = csub(t, b);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(cf& x0, cf& x1, cf& x2, cf& x3) {
+    cf s0 = cadd(x0, x2), s1 = csub(x0, x2), s2 = cadd(x1, x3), s3 = csub(x1, x3);
+    cf t = mul_mi<INV>(s3);
+    x0 = cadd(s0, s2);
+    x2 = csub(s0, s2);
+    x1 = cadd(s1, t);
+    x3 = csub(s1, t);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft8(cf* x) {
+    constexpr float c = 0.70710678118654752440f;
+    cf a0 = x[0], a1 = x[2], a2 = x[4], a3 = x[6];
+    cf b0 = x[1], b1 = x[3], b2 = x[5], b3 = x[7];
+    dft4<INV>(a0, a1, a2, a3);
+    dft4<INV>(b0, b1, b2, b3);
+    // W8^k b_k
+    cf w1, w3;
+    if (!INV) {
+        w1 = {(b1.r + b1.i) * c, (b1.i - b1.r) * c};
+        w3 = {(b3.i - b3.r) * c, -(b3.r + b3.i) * c};
+    } else {
+        w1 = {(b1.r - b1.i) * c, (b1.r + b1.i) * c};
+        w3 = {-(b3.r + b3.i) * c, (b3.r - b3.i) * c};
+    }
+    cf w2 = mul_mi<INV>(b2);
+    x[0] = cadd(a0, b0);
+    x[4] = csub(a0, b0);
+    x[1] = cadd(a1, w1);
+    x[5] = csub(a1, w1);
+    x[2] = cadd(a2, w2);
+    x[6] = csub(a2, w2);
+    x[3] = cadd(a3, w3);
+    x[7] = csub(a3, w3);
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dftR(cf* x) {
+    if constexpr (R == 2) {
+        dft2<INV>(x[0], x[1]);
+    } else if constexpr (R == 4) {
+        dft4<INV>(x[0], x[1], x[2], x[3]);
+    } else {
+        static_assert(R == 8, "radix");
+        dft8<INV>(x);
+    }
+}
+
+// ------------------------------------------------------------- LDS exchange
+__device__ __forceinline__ int pad_idx(int i) { return i + (i >> 3); }
+
+// Orders this wave's LDS writes before its later LDS reads (and vice versa)
+// without a workgroup barrier: DS instructions of one wave execute in order,
+// the fences only stop the compiler from moving memory ops across.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int P>
+constexpr int radix_for(int rem, int e) {
+    // largest radix in {8,4,2} dividing what is left and not exceeding E
+    return (rem % 8 == 0 && e >= 8) ? 8 : (rem % 4 == 0 && e >= 4) ? 4 : 2;
+}
+
+// One Stockham pass on the lane-major registers v[E]; NS = current sub-length.
+// After the pass, if NS*R < P, the results are exchanged through LDS (buf) back
+// into lane-major order for the next pass.  tw: W_P^t table (forward sign).
+template <int E, int R, int NS, bool INV>
+__device__ __forceinline__ void stockham_pass(cf (&v)[E], cf* buf, const cf* tw, int lane) {
+    constexpr int P = 64 * E;
+    constexpr int B = E / R;  // butterflies per lane
+    constexpr int TWS = P / (NS * R);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        cf x[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) x[r] = v[b + r * B];
+        const int j = lane + 64 * b;
+        if constexpr (NS > 1) {
+            const int jm = j % NS;
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                cf w = tw[r * jm * TWS];
+                x[r] = INV ? cmulc(x[r], w) : cmul(x[r], w);
+            }
+        }
+        dftR<R, INV>(x);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[b + r * B] = x[r];
+    }
+    if constexpr (NS * R < P) {
+        // y[(j/NS) NS R + (j mod NS) + r NS]  ->  LDS ; then read x[lane + 64 m]
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const int j = lane + 64 * b;
+            const int base = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+            for (int r = 0; r < R; ++r) buf[pad_idx(base + r * NS)] = v[b + r * B];
+        }
+        wave_lds_fence();
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = buf[pad_idx(lane + 64 * m)];
+        wave_lds_fence();
+    }
+}
+
+template <int E, int NS, bool INV>
+__device__ __forceinline__ void fft_passes(cf (&v)[E], cf* buf, const cf* tw, int lane) {
+    constexpr int P = 64 * E;
+    if constexpr (NS < P) {
+        constexpr int R = radix_for<P>(P / NS, E);
+        stockham_pass<E, R, NS, INV>(v, buf, tw, lane);
+        fft_passes<E, NS * R, INV>(v, buf, tw, lane);
+    }
+}
+
+// In-place P-point complex FFT (unnormalised) of the lane-major registers.
+template <int E, bool INV>
+__device__ __forceinline__ void fft_wave(cf (&v)[E], cf* buf, const cf* tw, int lane) {
+    fft_passes<E, 1, INV>(v, buf, tw, lane);
+}
+
+// ------------------------------------------------------------- sanitize
+// KissFftPlan sanitize (kissfft_adapter.cc:102-110, 156-163):
+// NaN/Inf -> 0, |v| < 1e-30 -> 0.
+__device__ __forceinline__ float sanit(float v) {
+    const float a = __builtin_fabsf(v);
+    return (a >= 1e-30f && a <= 3.402823466e+38f) ? v : 0.0f;
+}
+
+// ------------------------------------------------------------- real split
+// Given Z = FFT_P(z) lane-major in v, produce the spectrum X[k] (k = 0..P) of
+// the real 2P-point frame (kiss_fftr), apply the optional real per-bin gain
+// (spectral hook, identity when gain == nullptr), then rebuild Z' such that
+// IFFT_P(Z') is the unnormalised inverse real FFT (kiss_fftri).  Each lane
+// works on its own k = lane + 64 m and needs Z[P-k], read from LDS.
+// st: super twiddles exp(-i pi (k/P + 1/2)), k in [0, P).
+// spec (optional): receives X[k] for k = lane + 64 m and X[P] from lane 0.
+template <int E, bool WRITE_SPEC>
+__device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const cf* st,
+                                                      const float* gain, int lane,
+                                                      cf* spec = nullptr) {
+    constexpr int P = 64 * E;
+#pragma unroll
+    for (int m = 0; m < E; ++m) buf[pad_idx(lane + 64 * m)] = v[m];
+    wave_lds_fence();
+    cf zp[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) zp[m] = buf[pad_idx((P - (lane + 64 * m)) & (P - 1))];
+    wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + 64 * m;
+        const cf w = st[k];
+        const cf zk = v[m];
+        const cf fpnk = conj(zp[m]);
+        const cf f1 = cadd(zk, fpnk);
+        const cf f2 = csub(zk, fpnk);
+        const cf t = cmul(f2, w);
+        cf xk = {(f1.r + t.r) * 0.5f, (f1.i + t.i) * 0.5f};
+        cf xpk = {(f1.r - t.r) * 0.5f, (t.i - f1.i) * 0.5f};  // X[P-k]
+        if (gain != nullptr) {
+            const float gk = gain[k], gpk = gain[P - k];
+            xk = {xk.r * gk, xk.i * gk};
+            xpk = {xpk.r * gpk, xpk.i * gpk};
+        }
+        if constexpr (WRITE_SPEC) {
+            spec[k] = xk;
+            if (k == 0) spec[P] = xpk;
+        }
+        // kiss_fftri merge for Z'[k]
+        const cf fnkc = conj(xpk);
+        const cf fek = cadd(xk, fnkc);
+        const cf tmp = csub(xk, fnkc);
+        const cf fok = cmulc(tmp, w);  // * conj(st) = inverse super twiddle
+        v[m] = cadd(fek, fok);
+    }
+}
+
+}  // namespace dev
+}  // namespace crlot

@@ -1,0 +1,52 @@
+// kernels.h -- host-side launch interface of the HIP kernels (internal).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace crlot {
+
+// Device-resident per-plan tables.
+struct DevTables {
+    const float* wa = nullptr;   // analysis window [N] (all ones if disabled)
+    const float* ws = nullptr;   // synthesis window [N] (all ones if none)
+    const float* den = nullptr;  // max(norm, eps) [ring_len]
+    const float* tw = nullptr;   // W_P^t, t < P, float pairs
+    const float* st = nullptr;   // exp(-i pi (k/P + 1/2)), k < P, float pairs
+    const float* gain = nullptr; // spectral gain [P+1] or nullptr
+};
+
+struct Geometry {
+    int n = 0;          // frame size N
+    int h = 0;          // hop H
+    int ring_len = 0;   // OLA ring length
+    float inv_n = 0.f;  // 1.0f / N (kissfft_adapter.cc:154)
+    float gain = 1.f;   // push gain
+};
+
+// Fused fast path: N in {256..2048}, H % 128 == 0, N % H == 0, ring_len % H == 0,
+// 8-byte aligned streams.  Returns false if this shape has no instantiation.
+bool fused_supported(int n, int h);
+hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, float* y,
+                        int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                        int64_t out_len, hipStream_t stream);
+
+// Staged general path.
+bool synth_supported(int n);
+hipError_t launch_synth_frames(const Geometry& g, const DevTables& t, const float* x,
+                               int n_streams, int64_t T, int64_t ld_x, int64_t F, float* frames,
+                               float* spec, hipStream_t stream);
+hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float* frames,
+                             int64_t ld_frames, float* y, int n_streams, int64_t F,
+                             int64_t ld_y, int64_t out_len, hipStream_t stream);
+
+// Batched adapter-semantics real FFTs.
+hipError_t launch_rfft(const Geometry& g, const DevTables& t, const float* in, float* out,
+                       int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                       int64_t inc_out, hipStream_t stream);
+hipError_t launch_irfft(const Geometry& g, const DevTables& t, const float* in, float* out,
+                        int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                        int64_t inc_out, hipStream_t stream);
+
+}  // namespace crlot

@@ -1,0 +1,568 @@
+// kernels.hip -- gfx950 kernels of the STFT -> iSTFT -> OLA round trip.
+//
+// K_fused  k_stft_ola_fused<E,S,NB>: one wave owns a run of consecutive frames
+//          of one stream (plus NB-1 warm-up frames) and walks them in order:
+//          the frame's input slides through registers (only H new samples are
+//          loaded per frame), the FFT/iFFT run in registers + per-wave LDS, and
+//          the overlap-add accumulates in registers, so HBM sees 4 B in and
+//          4 B out per sample.  Output block k (H samples) is final once frame k
+//          is added, exactly the reference's push(k) -> produce(H) order.
+// K_synth  k_synth_frames<E>: one wave per frame, any hop; writes the
+//          push_frame_AoS input (sanitized inverse output) per frame.
+// K_gather k_ola_gather: one thread per output sample, sums the frames in
+//          ascending k (the reference's accumulation order) and divides by
+//          max(norm, eps): bit-exact OLAAccumulator.
+// K_rfft / K_irfft: batched IFftPlan::forward / inverse (adapter semantics).
+//
+// Numerics (DESIGN.md "Parity"): the float steps the reference fixes are kept
+// operation-for-operation -- frame*w (e2e_benchmark.cc:155, a plain multiply),
+// sanitize (kissfft_adapter.cc:102-110,156-163), *1/N then sanitize, the OLA
+// update fma(fma(src, w, 0), g, dst) (kernels.cc:24-28) and the IEEE division
+// acc / max(norm, eps) (kernels.cc:30-36).  Built with -ffp-contract=off and
+// the default correctly-rounded f32 division; subnormals are preserved.
+#include "fft_wave.h"
+#include "kernels.h"
+
+namespace crlot {
+
+using dev::cf;
+
+namespace {
+
+constexpr int kWaves = 4;  // waves per 256-thread workgroup, each independent
+constexpr int kBlock = 64 * kWaves;
+
+template <int P>
+__host__ __device__ constexpr int xbuf_elems() {
+    return P + P / 8;
+}
+
+// LDS carve shared by the kernels: [tw P cf][st P cf][wa N f][ws N f][bufs]
+template <int E>
+struct Lds {
+    static constexpr int P = 64 * E;
+    static constexpr int N = 2 * P;
+    static constexpr size_t bytes =
+        sizeof(cf) * (2 * P) + sizeof(float) * (2 * N) + sizeof(cf) * kWaves * xbuf_elems<P>();
+};
+
+template <int E>
+__device__ __forceinline__ void load_tables(const DevTables& t, cf* tw, cf* st, float* wa,
+                                            float* ws, bool need_windows) {
+    constexpr int P = 64 * E, N = 2 * P;
+    const cf* gtw = reinterpret_cast<const cf*>(t.tw);
+    const cf* gst = reinterpret_cast<const cf*>(t.st);
+    for (int i = threadIdx.x; i < P; i += kBlock) {
+        tw[i] = gtw[i];
+        st[i] = gst[i];
+    }
+    if (need_windows) {
+        for (int i = threadIdx.x; i < N; i += kBlock) {
+            wa[i] = t.wa[i];
+            ws[i] = t.ws[i];
+        }
+    }
+    __syncthreads();
+}
+
+struct FusedArgs {
+    DevTables t;
+    const float* x;
+    float* y;
+    int64_t ld_x, ld_y, T, out_len;
+    int n_streams, F, n_chunks, M, ring_blocks;
+    float inv_n, gain;
+};
+
+// Frame input: lane owns complex samples z[lane + 64 m] = (x[2i], x[2i+1]).
+__device__ __forceinline__ float2 load_pair(const float* x, int64_t idx, int64_t T, bool full) {
+    if (full || idx + 1 < T) return *reinterpret_cast<const float2*>(x + idx);
+    if (idx < T) return make_float2(x[idx], 0.0f);
+    return make_float2(0.0f, 0.0f);
+}
+
+template <int E, int S, int NB>
+__global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
+    constexpr int P = 64 * E, N = 2 * P, H = 128 * S;
+    static_assert(NB * S == E, "N = NB * H");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    float* wa = reinterpret_cast<float*>(st + P);
+    float* ws = wa + N;
+    cf* bufs = reinterpret_cast<cf*>(ws + N);
+    load_tables<E>(a.t, tw, st, wa, ws, true);
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    const int64_t gw = int64_t(blockIdx.x) * kWaves + wave;
+    if (gw >= int64_t(a.n_streams) * a.n_chunks) return;
+    const int s = int(gw / a.n_chunks), c = int(gw % a.n_chunks);
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1));
+    const float* x = a.x + int64_t(s) * a.ld_x;
+    float* y = a.y + int64_t(s) * a.ld_y;
+    const float g = a.gain;
+
+    float2 xin[E];
+    float2 acc[NB][S];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[j][q] = make_float2(0.f, 0.f);
+
+    for (int k = fs; k < f1; ++k) {
+        const int64_t base = int64_t(k) * H;
+        const bool full = base + N <= a.T;
+        if (k == fs) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) xin[m] = load_pair(x, base + 2 * (lane + 64 * m), a.T, full);
+        } else {
+#pragma unroll
+            for (int m = 0; m < E - S; ++m) xin[m] = xin[m + S];
+#pragma unroll
+            for (int m = E - S; m < E; ++m)
+                xin[m] = load_pair(x, base + 2 * (lane + 64 * m), a.T, full);
+        }
+        // analysis window (harness: frame[i] * w[i]) + forward sanitize
+        cf v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int i0 = 2 * (lane + 64 * m);
+            const float2 w = *reinterpret_cast<const float2*>(wa + i0);
+            v[m].r = dev::sanit(xin[m].x * w.x);
+            v[m].i = dev::sanit(xin[m].y * w.y);
+        }
+        dev::fft_wave<E, false>(v, buf, tw, lane);
+        dev::real_split_hook_merge<E, false>(v, buf, st, a.t.gain, lane);
+        dev::fft_wave<E, true>(v, buf, tw, lane);
+        // *1/N, sanitize, synthesis window, OLA accumulate (ascending k)
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int i0 = 2 * (lane + 64 * m);
+            const float2 w = *reinterpret_cast<const float2*>(ws + i0);
+            const float o0 = dev::sanit(v[m].r * a.inv_n);
+            const float o1 = dev::sanit(v[m].i * a.inv_n);
+            float2& r = acc[m / S][m % S];
+            r.x = __builtin_fmaf(__builtin_fmaf(o0, w.x, 0.0f), g, r.x);
+            r.y = __builtin_fmaf(__builtin_fmaf(o1, w.y, 0.0f), g, r.y);
+        }
+        // block k is complete: produce(H)
+        if (k >= f0) {
+            const float* den = a.t.den + int64_t(k % a.ring_blocks) * H;
+#pragma unroll
+            for (int q = 0; q < S; ++q) {
+                const int pos = 128 * q + 2 * lane;
+                const float2 d = *reinterpret_cast<const float2*>(den + pos);
+                const float2 o = make_float2(acc[0][q].x / d.x, acc[0][q].y / d.y);
+                const int64_t n = base + pos;
+                if (n + 1 < a.out_len) {
+                    *reinterpret_cast<float2*>(y + n) = o;
+                } else if (n < a.out_len) {
+                    y[n] = o.x;
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < S; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[NB - 1][q] = make_float2(0.f, 0.f);
+    }
+}
+
+// ------------------------------------------------------------------ staged
+struct SynthArgs {
+    DevTables t;
+    const float* x;
+    float* frames;  // [s][k][N]
+    float* spec;    // [s][k][P+1] cf, optional
+    int64_t ld_x, T, F;
+    int h, n_streams;
+    float inv_n;
+};
+
+template <int E, bool SPEC>
+__global__ __launch_bounds__(kBlock) void k_synth_frames(const SynthArgs a) {
+    constexpr int P = 64 * E, N = 2 * P;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    float* wa = reinterpret_cast<float*>(st + P);
+    float* ws = wa + N;
+    cf* bufs = reinterpret_cast<cf*>(ws + N);
+    load_tables<E>(a.t, tw, st, wa, ws, true);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    const int64_t gw = int64_t(blockIdx.x) * kWaves + wave;
+    if (gw >= int64_t(a.n_streams) * a.F) return;
+    const int64_t s = gw / a.F, k = gw % a.F;
+    const float* x = a.x + s * a.ld_x;
+    const int64_t base = k * a.h;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int i0 = 2 * (lane + 64 * m);
+        const int64_t t0 = base + i0;
+        const float x0 = t0 < a.T ? x[t0] : 0.0f;
+        const float x1 = t0 + 1 < a.T ? x[t0 + 1] : 0.0f;
+        v[m].r = dev::sanit(x0 * wa[i0]);
+        v[m].i = dev::sanit(x1 * wa[i0 + 1]);
+    }
+    dev::fft_wave<E, false>(v, buf, tw, lane);
+    cf* spec = SPEC ? reinterpret_cast<cf*>(a.spec) + gw * (P + 1) : nullptr;
+    dev::real_split_hook_merge<E, SPEC>(v, buf, st, a.t.gain, lane, spec);
+    dev::fft_wave<E, true>(v, buf, tw, lane);
+    float* out = a.frames + gw * N;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int i0 = 2 * (lane + 64 * m);
+        *reinterpret_cast<float2*>(out + i0) =
+            make_float2(dev::sanit(v[m].r * a.inv_n), dev::sanit(v[m].i * a.inv_n));
+    }
+}
+
+struct GatherArgs {
+    const float* frames;
+    const float* ws;
+    const float* den;
+    float* y;
+    int64_t ld_frames, ld_y, F, out_len;
+    int n, h, ring_len, n_streams;
+    float gain;
+};
+
+__global__ __launch_bounds__(256) void k_ola_gather(const GatherArgs a) {
+    const int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t total = int64_t(a.n_streams) * a.out_len;
+    if (idx >= total) return;
+    const int64_t s = idx / a.out_len, n = idx % a.out_len;
+    // frames k with k*H <= n < k*H + N, ascending
+    int64_t kmax = n / a.h;
+    if (kmax > a.F - 1) kmax = a.F - 1;
+    int64_t kmin = n - a.n + 1 <= 0 ? 0 : (n - a.n + a.h) / a.h;
+    const float* fr = a.frames + s * a.F * a.ld_frames;
+    float acc = 0.0f;
+    for (int64_t k = kmin; k <= kmax; ++k) {
+        const int64_t off = n - k * a.h;
+        const float src = fr[k * a.ld_frames + off];
+        acc = __builtin_fmaf(__builtin_fmaf(src, a.ws[off], 0.0f), a.gain, acc);
+    }
+    const float d = a.den[n % a.ring_len];
+    a.y[s * a.ld_y + n] = acc / d;
+}
+
+// ------------------------------------------------------------------ rfft / irfft
+struct FftArgs {
+    DevTables t;
+    const float* in;
+    float* out;
+    int64_t ld_in, inc_in, ld_out, inc_out;
+    int batch;
+    float inv_n;
+};
+
+template <int E>
+__global__ __launch_bounds__(kBlock) void k_rfft(const FftArgs a) {
+    constexpr int P = 64 * E;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    cf* bufs = st + P;
+    load_tables<E>(a.t, tw, st, nullptr, nullptr, false);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    const int64_t b = int64_t(blockIdx.x) * kWaves + wave;
+    if (b >= a.batch) return;
+    const float* in = a.in + b * a.ld_in;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int64_t i0 = 2 * (lane + 64 * m);
+        v[m].r = dev::sanit(in[i0 * a.inc_in]);
+        v[m].i = dev::sanit(in[(i0 + 1) * a.inc_in]);
+    }
+    dev::fft_wave<E, false>(v, buf, tw, lane);
+    // split only (kiss_fftr): X[k] for own k, X[P] from k == 0
+#pragma unroll
+    for (int m = 0; m < E; ++m) buf[dev::pad_idx(lane + 64 * m)] = v[m];
+    dev::wave_lds_fence();
+    float* out = a.out + b * a.ld_out;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + 64 * m;
+        const cf zk = v[m];
+        const cf fpnk = dev::conj(buf[dev::pad_idx((P - k) & (P - 1))]);
+        const cf f1 = dev::cadd(zk, fpnk);
+        const cf f2 = dev::csub(zk, fpnk);
+        const cf t = dev::cmul(f2, st[k]);
+        out[int64_t(2 * k) * a.inc_out] = (f1.r + t.r) * 0.5f;
+        out[int64_t(2 * k) * a.inc_out + 1] = (f1.i + t.i) * 0.5f;
+        if (k == 0) {
+            out[int64_t(2 * P) * a.inc_out] = (f1.r - t.r) * 0.5f;
+            out[int64_t(2 * P) * a.inc_out + 1] = (t.i - f1.i) * 0.5f;
+        }
+    }
+}
+
+template <int E>
+__global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
+    constexpr int P = 64 * E;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    cf* bufs = st + P;
+    load_tables<E>(a.t, tw, st, nullptr, nullptr, false);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    const int64_t b = int64_t(blockIdx.x) * kWaves + wave;
+    if (b >= a.batch) return;
+    const float* in = a.in + b * a.ld_in;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + 64 * m;
+        const cf xk = {in[int64_t(2 * k) * a.inc_in], in[int64_t(2 * k) * a.inc_in + 1]};
+        const int pk = P - k;
+        const cf xpk = {in[int64_t(2 * pk) * a.inc_in], in[int64_t(2 * pk) * a.inc_in + 1]};
+        const cf w = st[k];
+        const cf fnkc = dev::conj(xpk);
+        const cf fek = dev::cadd(xk, fnkc);
+        const cf tmp = dev::csub(xk, fnkc);
+        const cf fok = dev::cmulc(tmp, w);
+        v[m] = dev::cadd(fek, fok);
+    }
+    dev::fft_wave<E, true>(v, buf, tw, lane);
+    float* out = a.out + b * a.ld_out;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int64_t i0 = 2 * (lane + 64 * m);
+        out[i0 * a.inc_out] = dev::sanit(v[m].r * a.inv_n);
+        out[(i0 + 1) * a.inc_out] = dev::sanit(v[m].i * a.inv_n);
+    }
+}
+
+// ------------------------------------------------------------------ dispatch
+template <int E>
+inline size_t lds_bytes_full() {
+    return Lds<E>::bytes;
+}
+template <int E>
+inline size_t lds_bytes_fft() {
+    constexpr int P = 64 * E;
+    return sizeof(cf) * (2 * P) + sizeof(cf) * kWaves * xbuf_elems<P>();
+}
+
+template <typename K>
+hipError_t set_lds(K kernel, size_t lds) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+}
+
+int e_of(int n) {
+    switch (n) {
+        case 256: return 2;
+        case 512: return 4;
+        case 1024: return 8;
+        case 2048: return 16;
+        case 4096: return 32;
+        default: return 0;
+    }
+}
+
+template <int E, int S>
+hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    constexpr int NB = E / S;
+    auto k = k_stft_ola_fused<E, S, NB>;
+    const size_t lds = Lds<E>::bytes;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
+    return hipGetLastError();
+}
+
+template <int E>
+hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    if constexpr (E >= 1) {
+        if (s == 1) return fused_es<E, 1>(a, grid, stream);
+    }
+    if constexpr (E >= 2) {
+        if (s == 2) return fused_es<E, 2>(a, grid, stream);
+    }
+    if constexpr (E >= 4) {
+        if (s == 4) return fused_es<E, 4>(a, grid, stream);
+    }
+    if constexpr (E >= 8) {
+        if (s == 8) return fused_es<E, 8>(a, grid, stream);
+    }
+    if constexpr (E >= 16) {
+        if (s == 16) return fused_es<E, 16>(a, grid, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+bool fused_supported(int n, int h) {
+    const int e = e_of(n);
+    if (e == 0 || e > 16) return false;
+    if (h % 128 != 0 || n % h != 0) return false;
+    const int s = h / 128;
+    return s == 1 || s == 2 || s == 4 || s == 8 || s == 16;
+}
+
+hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, float* y,
+                        int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                        int64_t out_len, hipStream_t stream) {
+    if (!fused_supported(g.n, g.h) || F <= 0 || n_streams <= 0) return hipErrorInvalidValue;
+    FusedArgs a;
+    a.t = t;
+    a.x = x;
+    a.y = y;
+    a.ld_x = ld_x;
+    a.ld_y = ld_y;
+    a.T = T;
+    a.out_len = out_len;
+    a.n_streams = n_streams;
+    a.F = int(F);
+    // chunk length: ~128 frames per wave (halo NB-1 frames recomputed), evened out
+    const int target = 128;
+    a.n_chunks = int((F + target - 1) / target);
+    a.M = int((F + a.n_chunks - 1) / a.n_chunks);
+    a.n_chunks = int((F + a.M - 1) / a.M);
+    a.ring_blocks = g.ring_len / g.h;
+    a.inv_n = g.inv_n;
+    a.gain = g.gain;
+    const int64_t waves = int64_t(n_streams) * a.n_chunks;
+    const int64_t grid = (waves + kWaves - 1) / kWaves;
+    const int e = e_of(g.n), s = g.h / 128;
+    switch (e) {
+        case 2: return fused_e<2>(s, a, grid, stream);
+        case 4: return fused_e<4>(s, a, grid, stream);
+        case 8: return fused_e<8>(s, a, grid, stream);
+        case 16: return fused_e<16>(s, a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+bool synth_supported(int n) { return e_of(n) != 0; }
+
+template <int E>
+static hipError_t synth_e(const SynthArgs& a, int64_t grid, hipStream_t stream) {
+    const size_t lds = Lds<E>::bytes;
+    if (a.spec) {
+        auto k = k_synth_frames<E, true>;
+        hipError_t e = set_lds(k, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
+    } else {
+        auto k = k_synth_frames<E, false>;
+        hipError_t e = set_lds(k, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_frames(const Geometry& g, const DevTables& t, const float* x,
+                               int n_streams, int64_t T, int64_t ld_x, int64_t F, float* frames,
+                               float* spec, hipStream_t stream) {
+    if (!synth_supported(g.n) || F <= 0 || n_streams <= 0) return hipErrorInvalidValue;
+    SynthArgs a;
+    a.t = t;
+    a.x = x;
+    a.frames = frames;
+    a.spec = spec;
+    a.ld_x = ld_x;
+    a.T = T;
+    a.F = F;
+    a.h = g.h;
+    a.n_streams = n_streams;
+    a.inv_n = g.inv_n;
+    const int64_t waves = int64_t(n_streams) * F;
+    const int64_t grid = (waves + kWaves - 1) / kWaves;
+    switch (e_of(g.n)) {
+        case 2: return synth_e<2>(a, grid, stream);
+        case 4: return synth_e<4>(a, grid, stream);
+        case 8: return synth_e<8>(a, grid, stream);
+        case 16: return synth_e<16>(a, grid, stream);
+        case 32: return synth_e<32>(a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float* frames,
+                             int64_t ld_frames, float* y, int n_streams, int64_t F,
+                             int64_t ld_y, int64_t out_len, hipStream_t stream) {
+    if (F <= 0 || n_streams <= 0 || out_len <= 0) return hipErrorInvalidValue;
+    GatherArgs a;
+    a.frames = frames;
+    a.ws = t.ws;
+    a.den = t.den;
+    a.y = y;
+    a.ld_frames = ld_frames;
+    a.ld_y = ld_y;
+    a.F = F;
+    a.out_len = out_len;
+    a.n = g.n;
+    a.h = g.h;
+    a.ring_len = g.ring_len;
+    a.n_streams = n_streams;
+    a.gain = g.gain;
+    const int64_t total = int64_t(n_streams) * out_len;
+    const int64_t grid = (total + 255) / 256;
+    hipLaunchKernelGGL(k_ola_gather, dim3(unsigned(grid)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <int E, bool INV>
+static hipError_t fft_e(const FftArgs& a, hipStream_t stream) {
+    const size_t lds = lds_bytes_fft<E>();
+    const int64_t grid = (int64_t(a.batch) + kWaves - 1) / kWaves;
+    auto k = INV ? k_irfft<E> : k_rfft<E>;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
+    return hipGetLastError();
+}
+
+template <bool INV>
+static hipError_t fft_dispatch(const Geometry& g, const DevTables& t, const float* in, float* out,
+                               int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                               int64_t inc_out, hipStream_t stream) {
+    if (batch <= 0) return hipErrorInvalidValue;
+    FftArgs a;
+    a.t = t;
+    a.in = in;
+    a.out = out;
+    a.ld_in = ld_in;
+    a.inc_in = inc_in;
+    a.ld_out = ld_out;
+    a.inc_out = inc_out;
+    a.batch = batch;
+    a.inv_n = g.inv_n;
+    switch (e_of(g.n)) {
+        case 2: return fft_e<2, INV>(a, stream);
+        case 4: return fft_e<4, INV>(a, stream);
+        case 8: return fft_e<8, INV>(a, stream);
+        case 16: return fft_e<16, INV>(a, stream);
+        case 32: return fft_e<32, INV>(a, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_rfft(const Geometry& g, const DevTables& t, const float* in, float* out,
+                       int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                       hipStream_t stream) {
+    return fft_dispatch<false>(g, t, in, out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+}
+
+hipError_t launch_irfft(const Geometry& g, const DevTables& t, const float* in, float* out,
+                        int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                        hipStream_t stream) {
+    return fft_dispatch<true>(g, t, in, out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+}
+
+}  // namespace crlot

@@ -1,0 +1,162 @@
+/*
+ * crlot_dsp.h -- C ABI of the MI355X (gfx950) batched STFT -> iSTFT -> OLA engine.
+ *
+ * Replaces, for the hot path, the reference's host objects (file:line in
+ * /root/reference):
+ *   dsp::Framer                  dsp/frame/framer.h:26-127, framer.cc:15-181
+ *   dsp::WindowLUT               dsp/window/WindowLUT.h:80-287, WindowLUT.cc:215-388
+ *   dsp::fft::IFftPlan           dsp/fft/api/fft_api.h:16-51,
+ *                                dsp/fft/backends/kissfft_adapter.cc:11-269
+ *   dsp::OLAAccumulator          dsp/ola/OLAAccumulator.h:15-217, OLAAccumulator.cc:13-295
+ *   dsp::ola::build_norm_linear  dsp/ola/norm_builder.cc:8-52
+ *   axpy_windowed / normalize_and_clear   dsp/ola/kernels.cc:18-52
+ * and the round trip the harness assembles from them
+ * (bench/e2e_benchmark.cc:138-186, streaming-interleaved order: push frame k,
+ * then produce(H)).
+ *
+ * Conventions: plain C types only.  Device pointers (d_*) are caller-owned HIP
+ * device memory; host pointers are plain host memory.  `stream` is a hipStream_t
+ * passed as void* (NULL = default stream).  Every entry returns 0 on success or
+ * a negative CRLOT_E* code; crlot_last_error() gives the message of the last
+ * failure on the calling thread.  Nothing throws across this boundary.
+ * A plan is not thread-safe (like KissFftPlan, whose scratch makes it
+ * non-reentrant: kissfft_adapter.cc:256-263); use one plan per host thread.
+ */
+#ifndef CRLOT_DSP_H_
+#define CRLOT_DSP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRLOT_ABI_VERSION 1
+
+/* error codes */
+#define CRLOT_OK 0
+#define CRLOT_EINVAL (-1)       /* bad argument (reference: std::invalid_argument) */
+#define CRLOT_EUNSUPPORTED (-2) /* valid for the reference, not on this device path */
+#define CRLOT_EHIP (-3)         /* HIP runtime error */
+#define CRLOT_ENOMEM (-4)       /* allocation failed (reference: std::bad_alloc) */
+#define CRLOT_ERUNTIME (-5)     /* reference: std::runtime_error */
+
+/* dsp::WindowType (WindowLUT.h:14-20) */
+#define CRLOT_WIN_HANN 0
+#define CRLOT_WIN_HAMMING 1
+#define CRLOT_WIN_BLACKMAN 2
+#define CRLOT_WIN_RECT 3
+#define CRLOT_WIN_BLACKMAN_HARRIS 4 /* rejected, as in WindowLUT.cc:241-242 */
+/* dsp::NormalizationType (WindowLUT.h:25-31) */
+#define CRLOT_NORM_NONE 0
+#define CRLOT_NORM_SUM_TO_ONE 1
+#define CRLOT_NORM_L2 2
+#define CRLOT_NORM_OLA_UNITY_GAIN 3
+#define CRLOT_NORM_OLA_SUM_WSQ 4
+/* dsp::BoundaryMode (framer.h:11-14) */
+#define CRLOT_ZERO_PAD 0
+#define CRLOT_DROP 1
+
+typedef struct crlot_plan crlot_plan;
+typedef struct crlot_stream crlot_stream;
+
+/* Plan description: the union of OLAConfig (OLAAccumulator.h:15-29), the
+ * Framer parameters (framer.h:46-47) and the window choice of the harness
+ * (e2e_benchmark.cc:48-64).  Zero-initialise, then set the fields. */
+typedef struct crlot_plan_desc {
+    int32_t frame_size;          /* N: even, power of two in [256, 4096] on this path */
+    int32_t hop_size;            /* H: 1..N */
+    int32_t window_type;         /* CRLOT_WIN_* */
+    int32_t periodic;            /* 0 = symmetric (reference default) */
+    int32_t window_norm;         /* CRLOT_NORM_* */
+    int32_t boundary_mode;       /* CRLOT_ZERO_PAD (whole-stream push) or CRLOT_DROP */
+    int32_t analysis_window;     /* 1: frame * w before forward (e2e_benchmark.cc:154-156) */
+    int32_t apply_window_inside; /* OLAConfig::apply_window_inside */
+    float eps;                   /* OLAConfig::eps; 0 -> 1e-8f */
+    float ola_gain;              /* push_frame_AoS gain; 0 -> 1.0f */
+    int32_t ring_len;            /* 0 -> (ceil(N/H)+20)*H (OLAAccumulator.cc:249-258) */
+    int32_t device;              /* HIP device ordinal, -1 = current */
+} crlot_plan_desc;
+
+const char* crlot_last_error(void);
+int crlot_abi_version(void);
+
+/* ---------------------------------------------------------------- plan */
+int crlot_plan_create(const crlot_plan_desc* desc, crlot_plan** out);
+void crlot_plan_destroy(crlot_plan* plan);
+/* Replace the plan's window (N floats) and/or COLA norm table (ring_len floats)
+ * with host-built ones (NULL keeps the plan's own, which are built on the host
+ * by the reference formulas, bit-exact). */
+int crlot_plan_upload_tables(crlot_plan* plan, const float* window, const float* norm);
+/* Spectral hook between rfft and irfft: real per-bin gain, N/2+1 host floats;
+ * NULL restores the identity step of the reference (e2e_benchmark.cc:161-162). */
+int crlot_plan_set_spectral_gain(crlot_plan* plan, const float* gain);
+int crlot_plan_info(const crlot_plan* plan, int32_t* frame_size, int32_t* hop_size,
+                    int32_t* ring_len);
+/* Frames a whole-stream push of T samples yields (Framer, framer.cc:88-117) */
+int64_t crlot_frame_count(const crlot_plan* plan, int64_t T);
+/* Samples the streaming-interleaved round trip emits: F*H */
+int64_t crlot_output_length(const crlot_plan* plan, int64_t T);
+/* Device workspace a non-fast-path crlot_roundtrip needs (bytes); reserve it
+ * up front so the launch itself never allocates (graph capture). */
+int64_t crlot_workspace_bytes(const crlot_plan* plan, int32_t n_streams, int64_t T);
+int crlot_plan_reserve(crlot_plan* plan, int64_t bytes);
+
+/* ---------------------------------------------------------------- hot path */
+/* The round trip for n_streams independent mono streams: stream s reads
+ * d_x[s*ld_x + t], t < T, and writes d_y[s*ld_y + n], n < crlot_output_length.
+ * Equals, per stream, Framer(push whole) -> pop -> *w -> IFftPlan::forward ->
+ * (spectral hook) -> IFftPlan::inverse -> OLAAccumulator::push_frame_AoS(k*H)
+ * -> produce(H), frame after frame. */
+int crlot_roundtrip(crlot_plan* plan, const float* d_x, float* d_y, int32_t n_streams, int64_t T,
+                    int64_t ld_x, int64_t ld_y, void* stream);
+
+/* Per-stage outputs of the same path (parity/debug): d_frames gets, per
+ * stream and frame, the N-sample push_frame_AoS input (sanitized inverse
+ * output, before the synthesis window), [s][k][N]; d_spec (optional) the
+ * forward spectrum [s][k][N/2+1] complex (float pairs). */
+int crlot_roundtrip_stages(crlot_plan* plan, const float* d_x, int32_t n_streams, int64_t T,
+                           int64_t ld_x, float* d_frames, float* d_spec, void* stream);
+
+/* OLAAccumulator over precomputed frames: d_frames [s][k][ld_frames] (k < F)
+ * pushed at k*H with the plan's synthesis window (apply_window_inside) and
+ * gain, normalised by max(norm, eps) and produced in H-sample steps:
+ * d_y[s*ld_y + n], n < F*H.  Bit-exact with the reference given equal frames. */
+int crlot_ola_gather(crlot_plan* plan, const float* d_frames, float* d_y, int32_t n_streams,
+                     int64_t F, int64_t ld_frames, int64_t ld_y, void* stream);
+
+/* Batched IFftPlan::forward / inverse with the adapter's semantics
+ * (kissfft_adapter.cc:83-168): forward sanitizes its input, inverse scales by
+ * 1/N and sanitizes its output.  Element i of batch b lives at
+ * [b*ld + i*inc] (float for real data, float pairs for spectra). */
+int crlot_rfft_batched(crlot_plan* plan, const float* d_in, float* d_out_complex, int32_t batch,
+                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                       void* stream);
+int crlot_irfft_batched(crlot_plan* plan, const float* d_in_complex, float* d_out, int32_t batch,
+                        int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                        void* stream);
+
+/* ---------------------------------------------------------------- streaming
+ * Low-latency per-hop path (BASELINE config 4): `channels` independent
+ * channels, Framer in DROP mode fed H samples per channel per call.  Each call
+ * consumes d_hop_in [channels][H] (channel-major) and, once N samples have
+ * arrived, emits the next H output samples per channel into d_hop_out
+ * [channels][H]; *emitted (host) gets 0 or H. Device rings persist across calls. */
+int crlot_stream_create(crlot_plan* plan, int32_t channels, crlot_stream** out);
+void crlot_stream_destroy(crlot_stream* st);
+int crlot_stream_reset(crlot_stream* st);
+int crlot_stream_push_hop(crlot_stream* st, const float* d_hop_in, float* d_hop_out,
+                          int32_t* emitted, void* stream);
+
+/* ---------------------------------------------------------------- host tables
+ * The reference's table builders, restated in the product's host code
+ * (bit-exact with WindowLUT.cc / norm_builder.cc / OLAAccumulator.cc). */
+int crlot_window_table(int32_t type, int64_t n, int32_t periodic, int32_t norm, float* out);
+int64_t crlot_ring_len(int64_t frame_size, int64_t hop);
+int crlot_norm_table(const float* window, int64_t frame_size, int64_t hop, int64_t ring_len,
+                     int32_t apply_window_inside, float eps, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRLOT_DSP_H_ */

@@ -1,0 +1,296 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this,
+and only as the checker (or the timed CPU baseline, "kind": "port").  The
+product package (crlot-dsp_amd/) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS = range(5)
+NORM_NONE, NORM_SUM_TO_ONE, NORM_L2, NORM_OLA_UNITY_GAIN, NORM_OLA_SUM_WSQ = range(5)
+ZERO_PAD, DROP = 0, 1
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_lib = None
+
+
+def build(native: bool = False) -> str:
+    target = "liboracle_native.so" if native else "liboracle.so"
+    subprocess.run(["make", "-s", "-C", HERE, target], check=True)
+    return os.path.join(HERE, target)
+
+
+def lib(native: bool = False):
+    global _lib
+    if _lib is not None and not native:
+        return _lib
+    path = os.path.join(HERE, "liboracle_native.so" if native else "liboracle.so")
+    if not os.path.exists(path):
+        build(native)
+    L = C.CDLL(path)
+    sz = C.c_size_t
+    L.or_window.argtypes = [C.c_int, sz, C.c_int, C.c_int, _f32p]
+    L.or_window.restype = C.c_int
+    L.or_ring_len.argtypes = [sz, sz]
+    L.or_ring_len.restype = sz
+    L.or_build_norm_linear.argtypes = [_f32p, _f32p, sz, sz, sz]
+    L.or_init_normalization.argtypes = [_f32p, C.c_void_p, sz, sz, sz, C.c_int, C.c_float]
+    L.or_framer_new.argtypes = [sz, sz, sz, C.c_int]
+    L.or_framer_new.restype = C.c_void_p
+    L.or_framer_free.argtypes = [C.c_void_p]
+    L.or_framer_push.argtypes = [C.c_void_p, _f32p, sz]
+    L.or_framer_pop.argtypes = [C.c_void_p, _f32p]
+    L.or_framer_available.argtypes = [C.c_void_p]
+    L.or_framer_available.restype = sz
+    for nm in ("or_kfft_alloc", "or_kfftr_alloc"):
+        getattr(L, nm).argtypes = [C.c_int, C.c_int]
+        getattr(L, nm).restype = C.c_void_p
+    L.or_kfft_free.argtypes = [C.c_void_p]
+    L.or_kfftr_free.argtypes = [C.c_void_p]
+    L.or_kfft.argtypes = [C.c_void_p, _f32p, _f32p]
+    L.or_kfftr.argtypes = [C.c_void_p, _f32p, _f32p]
+    L.or_kfftri.argtypes = [C.c_void_p, _f32p, _f32p]
+    L.or_adapter_forward.argtypes = [C.c_void_p, C.c_int, _f32p, _f32p]
+    L.or_adapter_inverse.argtypes = [C.c_void_p, C.c_int, _f32p, _f32p]
+    L.or_adapter_forward_complex.argtypes = [C.c_void_p, C.c_int, _f32p, _f32p]
+    L.or_adapter_inverse_complex.argtypes = [C.c_void_p, C.c_int, _f32p, _f32p]
+    L.or_ola_new.argtypes = [sz, sz, sz, C.c_float, C.c_int]
+    L.or_ola_new.restype = C.c_void_p
+    L.or_ola_free.argtypes = [C.c_void_p]
+    L.or_ola_set_window.argtypes = [C.c_void_p, _f32p]
+    L.or_ola_push_frame_aos.argtypes = [C.c_void_p, _f32p, C.c_void_p, sz, sz, sz, C.c_float]
+    L.or_ola_add_frame_soa.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, sz, sz, sz, C.c_float]
+    L.or_ola_produce.argtypes = [C.c_void_p, C.c_void_p, sz]
+    L.or_ola_produce.restype = sz
+    L.or_ola_ring_size.argtypes = [C.c_void_p]
+    L.or_ola_ring_size.restype = sz
+    L.or_ola_norm.argtypes = [C.c_void_p]
+    L.or_ola_norm.restype = C.POINTER(C.c_float)
+    L.or_frame_count.argtypes = [sz, sz, sz, C.c_int]
+    L.or_frame_count.restype = sz
+    L.or_roundtrip.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, _f32p, sz,
+                               C.c_void_p, C.c_void_p]
+    L.or_roundtrip.restype = C.c_long
+    L.or_roundtrip_batch.argtypes = [_f32p, sz, sz, sz, sz, sz, C.c_int, C.c_int, C.c_int, _f32p,
+                                     sz, C.c_int]
+    L.or_roundtrip_batch.restype = C.c_long
+    L.or_synth_fill.argtypes = [_f32p, sz, C.c_ulonglong]
+    if not native:
+        _lib = L
+    return L
+
+
+# --------------------------------------------------------------------- helpers
+
+def window(wtype: int, n: int, periodic: bool = False, norm: int = NORM_NONE) -> np.ndarray:
+    out = np.zeros(max(n, 1), np.float32)
+    rc = lib().or_window(wtype, n, int(periodic), norm, out)
+    if rc != 0:
+        raise ValueError(f"or_window rc={rc}")
+    return out[:n]
+
+
+def ring_len(n: int, h: int) -> int:
+    return int(lib().or_ring_len(n, h))
+
+
+def norm_table(win, n: int, h: int, apply_inside: bool = True, eps: float = 1e-8) -> np.ndarray:
+    r = ring_len(n, h)
+    out = np.zeros(r, np.float32)
+    wp = None if win is None else np.ascontiguousarray(win, np.float32)
+    lib().or_init_normalization(out, None if wp is None else wp.ctypes.data, r, n, h,
+                                int(apply_inside), eps)
+    return out
+
+
+def frame_count(T: int, n: int, h: int, mode: int = ZERO_PAD) -> int:
+    return int(lib().or_frame_count(T, n, h, mode))
+
+
+def framer_run(x: np.ndarray, T: int, C_: int, n: int, h: int, mode: int, chunk: int = 0):
+    """Push x (T frames x C_ channels, interleaved) in chunks, pop after every push."""
+    L = lib()
+    f = L.or_framer_new(n, h, C_, mode)
+    x = np.ascontiguousarray(x, np.float32)
+    buf = np.zeros(n * C_, np.float32)
+    frames, avail = [], []
+    pos = 0
+    chunk = chunk or T
+    while pos < T:
+        m = min(chunk, T - pos)
+        L.or_framer_push(f, np.ascontiguousarray(x[pos * C_:(pos + m) * C_]), m)
+        pos += m
+        avail.append(int(L.or_framer_available(f)))
+        while L.or_framer_pop(f, buf):
+            frames.append(buf.copy())
+    L.or_framer_free(f)
+    fr = np.concatenate(frames) if frames else np.zeros(0, np.float32)
+    return fr, np.array(avail, np.uint64)
+
+
+class KissR:
+    """kiss_fftr restatement plan (forward + inverse)."""
+
+    def __init__(self, nfft: int):
+        self.n = nfft
+        self.f = lib().or_kfftr_alloc(nfft, 0)
+        self.i = lib().or_kfftr_alloc(nfft, 1)
+
+    def __del__(self):
+        try:
+            lib().or_kfftr_free(self.f)
+            lib().or_kfftr_free(self.i)
+        except Exception:
+            pass
+
+    def rfft_raw(self, x):
+        out = np.zeros(self.n + 2, np.float32)
+        lib().or_kfftr(self.f, np.ascontiguousarray(x, np.float32), out)
+        return out.view(np.complex64)
+
+    def irfft_raw(self, X):
+        out = np.zeros(self.n, np.float32)
+        lib().or_kfftri(self.i, np.ascontiguousarray(X, np.complex64).view(np.float32), out)
+        return out
+
+    def forward(self, x):
+        """KissFftPlan::forward (sanitize + kiss_fftr)."""
+        out = np.zeros(self.n + 2, np.float32)
+        lib().or_adapter_forward(self.f, self.n, np.ascontiguousarray(x, np.float32), out)
+        return out.view(np.complex64)
+
+    def inverse(self, X):
+        """KissFftPlan::inverse (kiss_fftri, *1/N, sanitize)."""
+        out = np.zeros(self.n, np.float32)
+        lib().or_adapter_inverse(self.i, self.n,
+                                 np.ascontiguousarray(X, np.complex64).view(np.float32), out)
+        return out
+
+
+class KissC:
+    def __init__(self, nfft: int):
+        self.n = nfft
+        self.f = lib().or_kfft_alloc(nfft, 0)
+        self.i = lib().or_kfft_alloc(nfft, 1)
+
+    def __del__(self):
+        try:
+            lib().or_kfft_free(self.f)
+            lib().or_kfft_free(self.i)
+        except Exception:
+            pass
+
+    def forward(self, z):
+        out = np.zeros(2 * self.n, np.float32)
+        lib().or_adapter_forward_complex(self.f, self.n,
+                                         np.ascontiguousarray(z, np.complex64).view(np.float32), out)
+        return out.view(np.complex64)
+
+    def inverse(self, Z):
+        out = np.zeros(2 * self.n, np.float32)
+        lib().or_adapter_inverse_complex(self.i, self.n,
+                                         np.ascontiguousarray(Z, np.complex64).view(np.float32), out)
+        return out.view(np.complex64)
+
+
+class Ola:
+    """OLAAccumulator restatement (SoA channels)."""
+
+    def __init__(self, n, h, c=1, eps=1e-8, inside=True):
+        self.n, self.h, self.c = n, h, c
+        self.p = lib().or_ola_new(n, h, c, eps, int(inside))
+        if not self.p:
+            raise ValueError("invalid OLA config")
+
+    def __del__(self):
+        try:
+            lib().or_ola_free(self.p)
+        except Exception:
+            pass
+
+    def set_window(self, w):
+        lib().or_ola_set_window(self.p, np.ascontiguousarray(w, np.float32))
+
+    def push_frame_aos(self, x, start, off=0, size=None, gain=1.0, window=None):
+        size = self.n if size is None else size
+        x = np.ascontiguousarray(x, np.float32)
+        wp = None
+        if window is not None:
+            wp = np.ascontiguousarray(window, np.float32)
+        lib().or_ola_push_frame_aos(self.p, x, None if wp is None else wp.ctypes.data, start, off,
+                                    size, gain)
+
+    def produce(self, n):
+        outs = [np.zeros(n, np.float32) for _ in range(self.c)]
+        ptrs = (C.c_void_p * self.c)(*[o.ctypes.data for o in outs])
+        got = lib().or_ola_produce(self.p, ptrs, n)
+        return [o[:got] for o in outs]
+
+    @property
+    def ring_size(self):
+        return int(lib().or_ola_ring_size(self.p))
+
+    def norm(self):
+        r = self.ring_size
+        return np.ctypeslib.as_array(lib().or_ola_norm(self.p), shape=(r,)).copy()
+
+
+def roundtrip(x, n, h, wtype=HANN, periodic=False, mode=ZERO_PAD, want_frames=False,
+              want_spec=False):
+    """One stream through the reference hot path (streaming-interleaved).
+
+    Returns y (F*H samples) [, frames (F,N) sanitized inverse output] [, spec (F,N/2+1)]."""
+    x = np.ascontiguousarray(x, np.float32)
+    T = x.size
+    F = frame_count(T, n, h, mode)
+    y = np.zeros(max(F * h, 1), np.float32)
+    frames = np.zeros((max(F, 1), n), np.float32) if want_frames else None
+    spec = np.zeros((max(F, 1), n // 2 + 1), np.complex64) if want_spec else None
+    r = lib().or_roundtrip(x, T, n, h, wtype, int(periodic), mode, y, F * h,
+                           None if frames is None else frames.ctypes.data,
+                           None if spec is None else spec.ctypes.data)
+    if r < 0:
+        raise ValueError(f"or_roundtrip rc={r}")
+    assert r == F, (r, F)
+    out = [y[:F * h]]
+    if want_frames:
+        out.append(frames[:F])
+    if want_spec:
+        out.append(spec[:F])
+    return out[0] if len(out) == 1 else tuple(out)
+
+
+def roundtrip_batch(x2d, n, h, wtype=HANN, periodic=False, mode=ZERO_PAD, nthreads=1,
+                    native=False):
+    x2d = np.ascontiguousarray(x2d, np.float32)
+    S, T = x2d.shape
+    F = frame_count(T, n, h, mode)
+    y = np.zeros((S, max(F * h, 1)), np.float32)
+    r = lib(native).or_roundtrip_batch(x2d, S, T, T, n, h, wtype, int(periodic), mode, y,
+                                       y.shape[1], nthreads)
+    if r < 0:
+        raise ValueError(f"or_roundtrip_batch rc={r}")
+    return y[:, :F * h]
+
+
+def synth(n: int, seed: int) -> np.ndarray:
+    out = np.zeros(n, np.float32)
+    lib().or_synth_fill(out, n, seed)
+    return out
+
+
+def synth_streams(n_streams: int, T: int, config_id: int = 2, first_stream: int = 0):
+    """seed = 0xC0FFEE ^ (config_id << 32) ^ stream_id."""
+    x = np.zeros((n_streams, T), np.float32)
+    for s in range(n_streams):
+        sid = first_stream + s
+        x[s] = synth(T, 0xC0FFEE ^ (config_id << 32) ^ sid)
+    return x
