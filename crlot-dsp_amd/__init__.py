@@ -149,6 +149,12 @@ def _torch():
     return torch
 
 
+def _ld(t, dim: int, minimum: int) -> int:
+    """Leading dimension of `t` along `dim`; a size-1 dim's stride is meaningless
+    (numpy/torch may report 0), so use the dense value there."""
+    return int(t.stride(dim)) if t.shape[dim] > 1 else int(minimum)
+
+
 def _stream_handle(tensor) -> int:
     torch = _torch()
     return int(torch.cuda.current_stream(tensor.device).cuda_stream)
@@ -241,8 +247,8 @@ class Plan:
         if y.shape[0] != S or y.shape[1] < L or y.stride(1) != 1:
             raise ValueError("bad y shape")
         s = _stream_handle(x) if stream is None else stream
-        _check(lib().crlot_roundtrip(self._h, x.data_ptr(), y.data_ptr(), S, T, x.stride(0),
-                                     y.stride(0), s), "crlot_roundtrip")
+        _check(lib().crlot_roundtrip(self._h, x.data_ptr(), y.data_ptr(), S, T, _ld(x, 0, T),
+                                     _ld(y, 0, L), s), "crlot_roundtrip")
         return y
 
     def stages(self, x, want_spec=True):
@@ -254,7 +260,7 @@ class Plan:
         frames = torch.empty((S, F, n), dtype=torch.float32, device=x.device)
         spec = (torch.empty((S, F, n // 2 + 1), dtype=torch.complex64, device=x.device)
                 if want_spec else None)
-        _check(lib().crlot_roundtrip_stages(self._h, x.data_ptr(), S, T, x.stride(0),
+        _check(lib().crlot_roundtrip_stages(self._h, x.data_ptr(), S, T, _ld(x, 0, T),
                                             frames.data_ptr(),
                                             None if spec is None else spec.data_ptr(),
                                             _stream_handle(x)), "crlot_roundtrip_stages")
@@ -264,13 +270,14 @@ class Plan:
         """frames (S, F, N) -> y (S, F*H) through the bit-exact OLA kernel."""
         torch = _torch()
         S, F, n = frames.shape
-        if n != self.frame_size or frames.stride(2) != 1 or frames.stride(0) != F * frames.stride(1):
+        if n != self.frame_size or frames.stride(2) != 1 or (
+                S > 1 and frames.stride(0) != F * _ld(frames, 1, n)):
             raise ValueError("frames must be (S, F, N) with contiguous (F, N) blocks")
         L = F * self.hop_size
         if y is None:
             y = torch.empty((S, L), dtype=torch.float32, device=frames.device)
         _check(lib().crlot_ola_gather(self._h, frames.data_ptr(), y.data_ptr(), S, F,
-                                      frames.stride(1), y.stride(0), _stream_handle(frames)),
+                                      _ld(frames, 1, n), _ld(y, 0, L), _stream_handle(frames)),
                "crlot_ola_gather")
         return y
 
@@ -279,8 +286,8 @@ class Plan:
         torch = _torch()
         B, n = x.shape
         out = torch.empty((B, n // 2 + 1), dtype=torch.complex64, device=x.device)
-        _check(lib().crlot_rfft_batched(self._h, x.data_ptr(), out.data_ptr(), B, x.stride(0),
-                                        x.stride(1), 2 * out.stride(0), 1, _stream_handle(x)),
+        _check(lib().crlot_rfft_batched(self._h, x.data_ptr(), out.data_ptr(), B, _ld(x, 0, n),
+                                        x.stride(1), 2 * (n // 2 + 1), 1, _stream_handle(x)),
                "crlot_rfft_batched")
         return out
 
@@ -291,7 +298,7 @@ class Plan:
         n = self.frame_size
         X = X.contiguous()
         out = torch.empty((B, n), dtype=torch.float32, device=X.device)
-        _check(lib().crlot_irfft_batched(self._h, X.data_ptr(), out.data_ptr(), B, 2 * X.stride(0),
-                                         1, out.stride(0), 1, _stream_handle(X)),
+        _check(lib().crlot_irfft_batched(self._h, X.data_ptr(), out.data_ptr(), B, 2 * bins,
+                                         1, n, 1, _stream_handle(X)),
                "crlot_irfft_batched")
         return out

@@ -273,10 +273,14 @@ int64_t crlot_output_length(const crlot_plan* p, int64_t T) {
     return frames_for(p, T) * p->geo.h;
 }
 
+// The fused kernel addresses a stream with 32-bit buffer offsets: keep every
+// byte offset of a stream (input and output) below 2^31.
 static bool use_fused(const crlot_plan* p, const float* x, const float* y, int64_t ld_x,
-                      int64_t ld_y) {
+                      int64_t ld_y, int32_t n_streams, int64_t T, int64_t out_len) {
+    const int64_t lim = int64_t(1) << 29;
     return crlot::fused_supported(p->geo.n, p->geo.h) && p->geo.ring_len % p->geo.h == 0 &&
-           aligned8(x) && aligned8(y) && ld_x % 2 == 0 && ld_y % 2 == 0;
+           aligned8(x) && aligned8(y) && ld_x % 2 == 0 && ld_y % 2 == 0 && T < lim &&
+           out_len + 2 * p->geo.n < lim && int64_t(n_streams) * (T / p->geo.h + 1) < lim;
 }
 
 int64_t crlot_workspace_bytes(const crlot_plan* p, int32_t n_streams, int64_t T) {
@@ -294,17 +298,17 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
                     int64_t ld_x, int64_t ld_y, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "negative size");
-    if (n_streams == 0 || T == 0) return CRLOT_OK;
-    if (!d_x || !d_y) return fail(CRLOT_EINVAL, "null buffer");
     const int64_t F = frames_for(p, T);
-    if (F == 0) return CRLOT_OK;  // DROP with T < N: the Framer never yields
+    // nothing to emit (n_streams == 0, T == 0, or DROP with T < N: the Framer never yields)
+    if (n_streams == 0 || F == 0) return CRLOT_OK;
+    if (!d_x || !d_y) return fail(CRLOT_EINVAL, "null buffer");
     const int64_t out_len = F * p->geo.h;
     if (ld_x < T || ld_y < out_len) return fail(CRLOT_EINVAL, "leading dimension too small");
     DeviceGuard g(p->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const crlot::DevTables t = tables(p);
     hipError_t e;
-    if (use_fused(p, d_x, d_y, ld_x, ld_y)) {
+    if (use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len)) {
         e = crlot::launch_fused(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s);
         if (e != hipSuccess) return hip_fail(e, "fused kernel launch");
         return CRLOT_OK;

@@ -70,24 +70,28 @@ __device__ __forceinline__ void dft8(cf* x) {
     cf b0 = x[1], b1 = x[3], b2 = x[5], b3 = x[7];
     dft4<INV>(a0, a1, a2, a3);
     dft4<INV>(b0, b1, b2, b3);
-    // W8^k b_k
-    cf w1, w3;
+    // W8^1 b1 = (p1, q1) c and W8^3 b3 = (p3, q3) c, folded into FMAs
+    float p1, q1, p3, q3;
     if (!INV) {
-        w1 = {(b1.r + b1.i) * c, (b1.i - b1.r) * c};
-        w3 = {(b3.i - b3.r) * c, -(b3.r + b3.i) * c};
+        p1 = b1.r + b1.i;
+        q1 = b1.i - b1.r;
+        p3 = b3.i - b3.r;
+        q3 = -(b3.r + b3.i);
     } else {
-        w1 = {(b1.r - b1.i) * c, (b1.r + b1.i) * c};
-        w3 = {-(b3.r + b3.i) * c, (b3.r - b3.i) * c};
+        p1 = b1.r - b1.i;
+        q1 = b1.r + b1.i;
+        p3 = -(b3.r + b3.i);
+        q3 = b3.r - b3.i;
     }
     cf w2 = mul_mi<INV>(b2);
     x[0] = cadd(a0, b0);
     x[4] = csub(a0, b0);
-    x[1] = cadd(a1, w1);
-    x[5] = csub(a1, w1);
+    x[1] = {__builtin_fmaf(p1, c, a1.r), __builtin_fmaf(q1, c, a1.i)};
+    x[5] = {__builtin_fmaf(p1, -c, a1.r), __builtin_fmaf(q1, -c, a1.i)};
     x[2] = cadd(a2, w2);
     x[6] = csub(a2, w2);
-    x[3] = cadd(a3, w3);
-    x[7] = csub(a3, w3);
+    x[3] = {__builtin_fmaf(p3, c, a3.r), __builtin_fmaf(q3, c, a3.i)};
+    x[7] = {__builtin_fmaf(p3, -c, a3.r), __builtin_fmaf(q3, -c, a3.i)};
 }
 
 template <int R, bool INV>
@@ -189,15 +193,16 @@ __device__ __forceinline__ float sanit(float v) {
 // ------------------------------------------------------------- real split
 // Given Z = FFT_P(z) lane-major in v, produce the spectrum X[k] (k = 0..P) of
 // the real 2P-point frame (kiss_fftr), apply the optional real per-bin gain
-// (spectral hook, identity when gain == nullptr), then rebuild Z' such that
-// IFFT_P(Z') is the unnormalised inverse real FFT (kiss_fftri).  Each lane
+// (spectral hook; the reference's step is the identity), then rebuild Z' such
+// that IFFT_P(Z') is the unnormalised inverse real FFT (kiss_fftri).  Each lane
 // works on its own k = lane + 64 m and needs Z[P-k], read from LDS.
-// st: super twiddles exp(-i pi (k/P + 1/2)), k in [0, P).
+//   st : super twiddles exp(-i pi (k/P + 1/2)), k in [0, P)
+//   sth: 0.5 * st (exact), so X[k] = fma(f1, 1/2, f2 * sth) with no extra multiply
 // spec (optional): receives X[k] for k = lane + 64 m and X[P] from lane 0.
-template <int E, bool WRITE_SPEC>
+template <int E, bool HAS_GAIN, bool WRITE_SPEC>
 __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const cf* st,
-                                                      const float* gain, int lane,
-                                                      cf* spec = nullptr) {
+                                                      const cf* sth, const float* gain,
+                                                      int lane, cf* spec = nullptr) {
     constexpr int P = 64 * E;
 #pragma unroll
     for (int m = 0; m < E; ++m) buf[pad_idx(lane + 64 * m)] = v[m];
@@ -209,15 +214,14 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int k = lane + 64 * m;
-        const cf w = st[k];
         const cf zk = v[m];
         const cf fpnk = conj(zp[m]);
         const cf f1 = cadd(zk, fpnk);
         const cf f2 = csub(zk, fpnk);
-        const cf t = cmul(f2, w);
-        cf xk = {(f1.r + t.r) * 0.5f, (f1.i + t.i) * 0.5f};
-        cf xpk = {(f1.r - t.r) * 0.5f, (t.i - f1.i) * 0.5f};  // X[P-k]
-        if (gain != nullptr) {
+        const cf t = cmul(f2, sth[k]);  // 0.5 * f2 * st
+        cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
+        cf xpk = {__builtin_fmaf(f1.r, 0.5f, -t.r), __builtin_fmaf(f1.i, -0.5f, t.i)};  // X[P-k]
+        if constexpr (HAS_GAIN) {
             const float gk = gain[k], gpk = gain[P - k];
             xk = {xk.r * gk, xk.i * gk};
             xpk = {xpk.r * gpk, xpk.i * gpk};
@@ -226,13 +230,43 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
             spec[k] = xk;
             if (k == 0) spec[P] = xpk;
         }
-        // kiss_fftri merge for Z'[k]
-        const cf fnkc = conj(xpk);
-        const cf fek = cadd(xk, fnkc);
-        const cf tmp = csub(xk, fnkc);
-        const cf fok = cmulc(tmp, w);  // * conj(st) = inverse super twiddle
-        v[m] = cadd(fek, fok);
+        // kiss_fftri merge: Z'[k] = (X[k] + conj X[P-k]) + (X[k] - conj X[P-k]) conj(st)
+        const cf w = st[k];
+        const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+        const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+        v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
+        v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
     }
+}
+
+// ------------------------------------------------------------- buffer access
+// Raw buffer descriptors: 32-bit offsets, hardware range check (loads past
+// num_bytes return 0, stores past it are dropped).  Build them from
+// wave-uniform values only (readfirstlane'd), see cdna_hip_programming.md T20.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(a));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(a >> 32));
+    const uint64_t b = (uint64_t(hi) << 32) | lo;
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(b), 0,
+                                             int(__builtin_amdgcn_readfirstlane(bytes)),
+                                             0x00020000);
+}
+// NOTE (ROCm 7.2 clang): __builtin_bit_cast applied directly to an element of the
+// vector returned by raw_buffer_load_b64/b128 is miscompiled into a single-dword
+// load (upper half garbage); copying each element to a scalar first is correct.
+__device__ __forceinline__ float2 bload2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    const unsigned lo = v[0], hi = v[1];
+    return make_float2(__builtin_bit_cast(float, lo), __builtin_bit_cast(float, hi));
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ void bstore2(float2 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    u2 w = {__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y)};
+    __builtin_amdgcn_raw_buffer_store_b64(w, r, voff, soff, 0);
 }
 
 }  // namespace dev

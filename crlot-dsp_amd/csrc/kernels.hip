@@ -37,24 +37,26 @@ __host__ __device__ constexpr int xbuf_elems() {
     return P + P / 8;
 }
 
-// LDS carve shared by the kernels: [tw P cf][st P cf][wa N f][ws N f][bufs]
+// LDS carve shared by the kernels: [tw P cf][st P cf][sth P cf][wa N f][ws N f][bufs]
 template <int E>
 struct Lds {
     static constexpr int P = 64 * E;
     static constexpr int N = 2 * P;
     static constexpr size_t bytes =
-        sizeof(cf) * (2 * P) + sizeof(float) * (2 * N) + sizeof(cf) * kWaves * xbuf_elems<P>();
+        sizeof(cf) * (3 * P) + sizeof(float) * (2 * N) + sizeof(cf) * kWaves * xbuf_elems<P>();
 };
 
 template <int E>
-__device__ __forceinline__ void load_tables(const DevTables& t, cf* tw, cf* st, float* wa,
+__device__ __forceinline__ void load_tables(const DevTables& t, cf* tw, cf* st, cf* sth, float* wa,
                                             float* ws, bool need_windows) {
     constexpr int P = 64 * E, N = 2 * P;
     const cf* gtw = reinterpret_cast<const cf*>(t.tw);
     const cf* gst = reinterpret_cast<const cf*>(t.st);
     for (int i = threadIdx.x; i < P; i += kBlock) {
         tw[i] = gtw[i];
-        st[i] = gst[i];
+        const cf w = gst[i];
+        st[i] = w;
+        sth[i] = cf{w.r * 0.5f, w.i * 0.5f};  // exact
     }
     if (need_windows) {
         for (int i = threadIdx.x; i < N; i += kBlock) {
@@ -69,43 +71,59 @@ struct FusedArgs {
     DevTables t;
     const float* x;
     float* y;
-    int64_t ld_x, ld_y, T, out_len;
+    int64_t ld_x, ld_y;
+    int T, out_len;  // per stream, T * 4 and out_len * 4 < 2^31 (checked on the host)
     int n_streams, F, n_chunks, M, ring_blocks;
     float inv_n, gain;
 };
 
-// Frame input: lane owns complex samples z[lane + 64 m] = (x[2i], x[2i+1]).
-__device__ __forceinline__ float2 load_pair(const float* x, int64_t idx, int64_t T, bool full) {
-    if (full || idx + 1 < T) return *reinterpret_cast<const float2*>(x + idx);
-    if (idx < T) return make_float2(x[idx], 0.0f);
-    return make_float2(0.0f, 0.0f);
+// Hop loads: lane owns complex samples z[lane + 64 m] = (x[2i], x[2i+1]), i = lane + 64 m.
+// `full` (wave-uniform) = the whole frame lies inside the stream: one dwordx2 per
+// pair; otherwise two dword loads whose out-of-range halves read 0 (ZERO_PAD).
+template <int M0, int CNT, int E>
+__device__ __forceinline__ void load_pairs(float2 (&dst)[E], __amdgpu_buffer_rsrc_t rx, int lane,
+                                           int frame_byte, bool full) {
+    if (full) {
+#pragma unroll
+        for (int m = M0; m < M0 + CNT; ++m) dst[m] = dev::bload2(rx, lane * 8 + m * 512, frame_byte);
+    } else {
+#pragma unroll
+        for (int m = M0; m < M0 + CNT; ++m)
+            dst[m] = make_float2(dev::bload1(rx, lane * 8 + m * 512, frame_byte),
+                                 dev::bload1(rx, lane * 8 + m * 512 + 4, frame_byte));
+    }
 }
 
-template <int E, int S, int NB>
+template <int E, int S, int NB, bool HAS_GAIN>
 __global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
     constexpr int P = 64 * E, N = 2 * P, H = 128 * S;
     static_assert(NB * S == E, "N = NB * H");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     cf* st = tw + P;
-    float* wa = reinterpret_cast<float*>(st + P);
+    cf* sth = st + P;
+    float* wa = reinterpret_cast<float*>(sth + P);
     float* ws = wa + N;
     cf* bufs = reinterpret_cast<cf*>(ws + N);
-    load_tables<E>(a.t, tw, st, wa, ws, true);
+    load_tables<E>(a.t, tw, st, sth, wa, ws, true);
 
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     cf* buf = bufs + wave * xbuf_elems<P>();
-    const int64_t gw = int64_t(blockIdx.x) * kWaves + wave;
-    if (gw >= int64_t(a.n_streams) * a.n_chunks) return;
-    const int s = int(gw / a.n_chunks), c = int(gw % a.n_chunks);
+    const int gw = blockIdx.x * kWaves + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
     const int fs = max(0, f0 - (NB - 1));
-    const float* x = a.x + int64_t(s) * a.ld_x;
-    float* y = a.y + int64_t(s) * a.ld_y;
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
     const float g = a.gain;
 
     float2 xin[E];
+    load_pairs<0, E, E>(xin, rx, lane, fs * H * 4, fs * H + N <= a.T);
     float2 acc[NB][S];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
@@ -113,56 +131,42 @@ __global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
         for (int q = 0; q < S; ++q) acc[j][q] = make_float2(0.f, 0.f);
 
     for (int k = fs; k < f1; ++k) {
-        const int64_t base = int64_t(k) * H;
-        const bool full = base + N <= a.T;
-        if (k == fs) {
+        // prefetch: frame k+1's new hop and block k's normaliser, consumed at the
+        // end of this iteration, so their latency hides under the transforms
+        float2 nxt[E];
+        if (k + 1 < f1) load_pairs<E - S, S, E>(nxt, rx, lane, (k + 1) * H * 4, (k + 1) * H + N <= a.T);
+        float2 dn[S];
+        if (k >= f0) {
 #pragma unroll
-            for (int m = 0; m < E; ++m) xin[m] = load_pair(x, base + 2 * (lane + 64 * m), a.T, full);
-        } else {
-#pragma unroll
-            for (int m = 0; m < E - S; ++m) xin[m] = xin[m + S];
-#pragma unroll
-            for (int m = E - S; m < E; ++m)
-                xin[m] = load_pair(x, base + 2 * (lane + 64 * m), a.T, full);
+            for (int q = 0; q < S; ++q) dn[q] = dev::bload2(rd, lane * 8 + q * 512, (k % a.ring_blocks) * H * 4);
         }
         // analysis window (harness: frame[i] * w[i]) + forward sanitize
         cf v[E];
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const int i0 = 2 * (lane + 64 * m);
-            const float2 w = *reinterpret_cast<const float2*>(wa + i0);
+            const float2 w = *reinterpret_cast<const float2*>(wa + 2 * (lane + 64 * m));
             v[m].r = dev::sanit(xin[m].x * w.x);
             v[m].i = dev::sanit(xin[m].y * w.y);
         }
         dev::fft_wave<E, false>(v, buf, tw, lane);
-        dev::real_split_hook_merge<E, false>(v, buf, st, a.t.gain, lane);
+        dev::real_split_hook_merge<E, HAS_GAIN, false>(v, buf, st, sth, a.t.gain, lane);
         dev::fft_wave<E, true>(v, buf, tw, lane);
         // *1/N, sanitize, synthesis window, OLA accumulate (ascending k)
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const int i0 = 2 * (lane + 64 * m);
-            const float2 w = *reinterpret_cast<const float2*>(ws + i0);
+            const float2 w = *reinterpret_cast<const float2*>(ws + 2 * (lane + 64 * m));
             const float o0 = dev::sanit(v[m].r * a.inv_n);
             const float o1 = dev::sanit(v[m].i * a.inv_n);
             float2& r = acc[m / S][m % S];
             r.x = __builtin_fmaf(__builtin_fmaf(o0, w.x, 0.0f), g, r.x);
             r.y = __builtin_fmaf(__builtin_fmaf(o1, w.y, 0.0f), g, r.y);
         }
-        // block k is complete: produce(H)
+        // block k is complete: produce(H) = acc / max(norm, eps)
         if (k >= f0) {
-            const float* den = a.t.den + int64_t(k % a.ring_blocks) * H;
 #pragma unroll
-            for (int q = 0; q < S; ++q) {
-                const int pos = 128 * q + 2 * lane;
-                const float2 d = *reinterpret_cast<const float2*>(den + pos);
-                const float2 o = make_float2(acc[0][q].x / d.x, acc[0][q].y / d.y);
-                const int64_t n = base + pos;
-                if (n + 1 < a.out_len) {
-                    *reinterpret_cast<float2*>(y + n) = o;
-                } else if (n < a.out_len) {
-                    y[n] = o.x;
-                }
-            }
+            for (int q = 0; q < S; ++q)
+                dev::bstore2(make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y), ry,
+                             lane * 8 + q * 512, k * H * 4);
         }
 #pragma unroll
         for (int j = 0; j < NB - 1; ++j)
@@ -170,6 +174,10 @@ __global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
             for (int q = 0; q < S; ++q) acc[j][q] = acc[j + 1][q];
 #pragma unroll
         for (int q = 0; q < S; ++q) acc[NB - 1][q] = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int m = 0; m < E - S; ++m) xin[m] = xin[m + S];
+#pragma unroll
+        for (int m = E - S; m < E; ++m) xin[m] = nxt[m];
     }
 }
 
@@ -184,16 +192,17 @@ struct SynthArgs {
     float inv_n;
 };
 
-template <int E, bool SPEC>
+template <int E, bool HAS_GAIN, bool SPEC>
 __global__ __launch_bounds__(kBlock) void k_synth_frames(const SynthArgs a) {
     constexpr int P = 64 * E, N = 2 * P;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     cf* st = tw + P;
-    float* wa = reinterpret_cast<float*>(st + P);
+    cf* sth = st + P;
+    float* wa = reinterpret_cast<float*>(sth + P);
     float* ws = wa + N;
     cf* bufs = reinterpret_cast<cf*>(ws + N);
-    load_tables<E>(a.t, tw, st, wa, ws, true);
+    load_tables<E>(a.t, tw, st, sth, wa, ws, true);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     cf* buf = bufs + wave * xbuf_elems<P>();
     const int64_t gw = int64_t(blockIdx.x) * kWaves + wave;
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_synth_frames(const SynthArgs a) {
     }
     dev::fft_wave<E, false>(v, buf, tw, lane);
     cf* spec = SPEC ? reinterpret_cast<cf*>(a.spec) + gw * (P + 1) : nullptr;
-    dev::real_split_hook_merge<E, SPEC>(v, buf, st, a.t.gain, lane, spec);
+    dev::real_split_hook_merge<E, HAS_GAIN, SPEC>(v, buf, st, sth, a.t.gain, lane, spec);
     dev::fft_wave<E, true>(v, buf, tw, lane);
     float* out = a.frames + gw * N;
 #pragma unroll
@@ -270,8 +279,9 @@ __global__ __launch_bounds__(kBlock) void k_rfft(const FftArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     cf* st = tw + P;
-    cf* bufs = st + P;
-    load_tables<E>(a.t, tw, st, nullptr, nullptr, false);
+    cf* sth = st + P;
+    cf* bufs = sth + P;
+    load_tables<E>(a.t, tw, st, sth, nullptr, nullptr, false);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     cf* buf = bufs + wave * xbuf_elems<P>();
     const int64_t b = int64_t(blockIdx.x) * kWaves + wave;
@@ -297,12 +307,12 @@ __global__ __launch_bounds__(kBlock) void k_rfft(const FftArgs a) {
         const cf fpnk = dev::conj(buf[dev::pad_idx((P - k) & (P - 1))]);
         const cf f1 = dev::cadd(zk, fpnk);
         const cf f2 = dev::csub(zk, fpnk);
-        const cf t = dev::cmul(f2, st[k]);
-        out[int64_t(2 * k) * a.inc_out] = (f1.r + t.r) * 0.5f;
-        out[int64_t(2 * k) * a.inc_out + 1] = (f1.i + t.i) * 0.5f;
+        const cf t = dev::cmul(f2, sth[k]);
+        out[int64_t(2 * k) * a.inc_out] = __builtin_fmaf(f1.r, 0.5f, t.r);
+        out[int64_t(2 * k) * a.inc_out + 1] = __builtin_fmaf(f1.i, 0.5f, t.i);
         if (k == 0) {
-            out[int64_t(2 * P) * a.inc_out] = (f1.r - t.r) * 0.5f;
-            out[int64_t(2 * P) * a.inc_out + 1] = (t.i - f1.i) * 0.5f;
+            out[int64_t(2 * P) * a.inc_out] = __builtin_fmaf(f1.r, 0.5f, -t.r);
+            out[int64_t(2 * P) * a.inc_out + 1] = __builtin_fmaf(f1.i, -0.5f, t.i);
         }
     }
 }
@@ -313,8 +323,9 @@ __global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
     cf* st = tw + P;
-    cf* bufs = st + P;
-    load_tables<E>(a.t, tw, st, nullptr, nullptr, false);
+    cf* sth = st + P;
+    cf* bufs = sth + P;
+    load_tables<E>(a.t, tw, st, sth, nullptr, nullptr, false);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     cf* buf = bufs + wave * xbuf_elems<P>();
     const int64_t b = int64_t(blockIdx.x) * kWaves + wave;
@@ -328,11 +339,10 @@ __global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
         const int pk = P - k;
         const cf xpk = {in[int64_t(2 * pk) * a.inc_in], in[int64_t(2 * pk) * a.inc_in + 1]};
         const cf w = st[k];
-        const cf fnkc = dev::conj(xpk);
-        const cf fek = dev::cadd(xk, fnkc);
-        const cf tmp = dev::csub(xk, fnkc);
-        const cf fok = dev::cmulc(tmp, w);
-        v[m] = dev::cadd(fek, fok);
+        const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+        const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+        v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
+        v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
     }
     dev::fft_wave<E, true>(v, buf, tw, lane);
     float* out = a.out + b * a.ld_out;
@@ -352,7 +362,7 @@ inline size_t lds_bytes_full() {
 template <int E>
 inline size_t lds_bytes_fft() {
     constexpr int P = 64 * E;
-    return sizeof(cf) * (2 * P) + sizeof(cf) * kWaves * xbuf_elems<P>();
+    return sizeof(cf) * (3 * P) + sizeof(cf) * kWaves * xbuf_elems<P>();
 }
 
 template <typename K>
@@ -375,7 +385,7 @@ int e_of(int n) {
 template <int E, int S>
 hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     constexpr int NB = E / S;
-    auto k = k_stft_ola_fused<E, S, NB>;
+    auto k = a.t.gain ? k_stft_ola_fused<E, S, NB, true> : k_stft_ola_fused<E, S, NB, false>;
     const size_t lds = Lds<E>::bytes;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
@@ -423,8 +433,8 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.y = y;
     a.ld_x = ld_x;
     a.ld_y = ld_y;
-    a.T = T;
-    a.out_len = out_len;
+    a.T = int(T);
+    a.out_len = int(out_len);
     a.n_streams = n_streams;
     a.F = int(F);
     // chunk length: ~128 frames per wave (halo NB-1 frames recomputed), evened out
@@ -453,12 +463,12 @@ template <int E>
 static hipError_t synth_e(const SynthArgs& a, int64_t grid, hipStream_t stream) {
     const size_t lds = Lds<E>::bytes;
     if (a.spec) {
-        auto k = k_synth_frames<E, true>;
+        auto k = a.t.gain ? k_synth_frames<E, true, true> : k_synth_frames<E, false, true>;
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
     } else {
-        auto k = k_synth_frames<E, false>;
+        auto k = a.t.gain ? k_synth_frames<E, true, false> : k_synth_frames<E, false, false>;
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
