@@ -94,7 +94,7 @@ def load_pmc_traffic():
     best = None
     if os.path.isdir(pdir):
         for f in sorted(os.listdir(pdir)):
-            if f.endswith(".json") and "pmc" in f:
+            if f.endswith(".json") and "pmc" in f and not f.startswith("_"):
                 try:
                     d = json.load(open(os.path.join(pdir, f)))
                 except Exception:

@@ -20,7 +20,7 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcrlot_dsp.so")
+LIB_PATH = os.environ.get("CRLOT_LIB") or os.path.join(HERE, "libcrlot_dsp.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "crlot_dsp.h")
 
 # dsp::WindowType / NormalizationType / BoundaryMode ordinals

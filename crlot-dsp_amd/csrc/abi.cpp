@@ -192,11 +192,9 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     crlot_norm_table(p->window.data(), n, h, ring, d.apply_window_inside, d.eps, p->norm.data());
 
     const int P = n / 2;
-    std::vector<float> tw(2 * P), st(2 * P);
+    const std::vector<float> tw = crlot::build_pass_twiddles(n);
+    std::vector<float> st(2 * P);
     for (int t = 0; t < P; ++t) {
-        const double ph = -2.0 * M_PI * double(t) / double(P);
-        tw[2 * t] = float(std::cos(ph));
-        tw[2 * t + 1] = float(std::sin(ph));
         const double ps = -M_PI * (double(t) / double(P) + 0.5);
         st[2 * t] = float(std::cos(ps));
         st[2 * t + 1] = float(std::sin(ps));
@@ -205,13 +203,13 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     if ((e = hipMalloc(&p->d_wa, sizeof(float) * n)) ||
         (e = hipMalloc(&p->d_ws, sizeof(float) * n)) ||
         (e = hipMalloc(&p->d_den, sizeof(float) * ring)) ||
-        (e = hipMalloc(&p->d_tw, sizeof(float) * 2 * P)) ||
+        (e = hipMalloc(&p->d_tw, sizeof(float) * (tw.size() + 2))) ||
         (e = hipMalloc(&p->d_st, sizeof(float) * 2 * P)) ||
         (e = hipMalloc(&p->d_gain, sizeof(float) * (P + 1)))) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }
-    if ((e = hipMemcpy(p->d_tw, tw.data(), sizeof(float) * 2 * P, hipMemcpyHostToDevice)) ||
+    if ((e = hipMemcpy(p->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
         (e = hipMemcpy(p->d_st, st.data(), sizeof(float) * 2 * P, hipMemcpyHostToDevice))) {
         free_plan(p);
         return hip_fail(e, "hipMemcpy(twiddles)");

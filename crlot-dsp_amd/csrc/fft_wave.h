@@ -11,9 +11,8 @@
 // With j = lane + 64 b every read is lane-major (no data movement), the first
 // pass (Ns = 1) needs no twiddles, and the LAST pass writes lane-major too, so a
 // P-point FFT costs (passes - 1) LDS exchanges and leaves its output in natural
-// order in registers.  Exchanges go through a per-wave LDS buffer padded by one
-// element every 8 (phys(i) = i + i/8) so the stride-R writes of early passes are
-// bank-conflict free for ds_write_b64.
+// order in registers.  Exchanges go through a per-wave LDS buffer of P elements
+// under a per-exchange XOR swizzle that keeps them bank-conflict free.
 //
 // Arithmetic is IEEE f32; the translation unit is built with -ffp-contract=off,
 // so every FMA below is explicit.
@@ -107,7 +106,23 @@ __device__ __forceinline__ void dftR(cf* x) {
 }
 
 // ------------------------------------------------------------- LDS exchange
-__device__ __forceinline__ int pad_idx(int i) { return i + (i >> 3); }
+// Each exchange stores the pass outputs at their Stockham positions and reads
+// them back lane-major.  The XOR swizzle below (a permutation inside aligned
+// blocks, so the buffer stays P elements) makes both the ds_write_b64 scatter
+// and the ds_read_b64 gather bank-conflict free for every exchange of every
+// supported size; it was found by tools/swizzle_search.py with the gfx950 LDS
+// model in tools/lds_banks.py (ds_write_b64: 16-lane groups, 32 banks;
+// ds_read_b64: 32-lane groups, 64 banks).
+template <int NS, int R>
+__device__ __forceinline__ int swz(int i) {
+    if constexpr (NS == 1) return i ^ ((i >> 4) & (R - 1));
+    else if constexpr (NS == 2) return i ^ ((i >> 3) & 3);
+    else if constexpr (NS == 4 && R == 4) return i ^ (((i >> 4) & 3) << 2);
+    else if constexpr (NS == 4) return i ^ (((i >> 3) & 3) << 1);
+    else if constexpr (NS == 8 && R == 8) return i ^ (((i >> 4) & 7) << 1);
+    else if constexpr (NS == 8) return i ^ (((i >> 4) & 1) << 3);
+    else return i;
+}
 
 // Orders this wave's LDS writes before its later LDS reads (and vice versa)
 // without a workgroup barrier: DS instructions of one wave execute in order,
@@ -118,74 +133,155 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int P>
-constexpr int radix_for(int rem, int e) {
-    // largest radix in {8,4,2} dividing what is left and not exceeding E
+// Radix schedule: largest radix in {8,4,2} dividing what is left, not above E.
+__host__ __device__ constexpr int radix_for(int rem, int e) {
     return (rem % 8 == 0 && e >= 8) ? 8 : (rem % 4 == 0 && e >= 4) ? 4 : 2;
 }
 
+// Per-pass twiddle table layout (host + device): pass (NS > 1, R) owns
+// (R-1)*NS entries T[(r-1)*NS + jm] = W_{NS R}^{r jm}, jm = j mod NS, so a
+// wave's twiddle reads are contiguous (or broadcast) -- conflict free.
+__host__ __device__ constexpr int twiddle_table_size(int e) {
+    int p = 64 * e, ns = 1, n = 0;
+    while (ns < p) {
+        const int r = radix_for(p / ns, e);
+        if (ns > 1) n += (r - 1) * ns;
+        ns *= r;
+    }
+    return n;
+}
+
+// Per-lane twiddles of one pass: w[b][r-1] for butterfly j = lane + 64 b.
+template <int E, int R, int NS>
+struct PassTw {
+    cf w[E / R][R - 1];
+};
+
+template <int E, int R, int NS, int TOFF>
+__device__ __forceinline__ void load_pass_tw(PassTw<E, R, NS>& t, const cf* twp, int lane) {
+#pragma unroll
+    for (int b = 0; b < E / R; ++b)
+#pragma unroll
+        for (int r = 1; r < R; ++r) t.w[b][r - 1] = twp[TOFF + (r - 1) * NS + (lane + 64 * b) % NS];
+}
+
 // One Stockham pass on the lane-major registers v[E]; NS = current sub-length.
-// After the pass, if NS*R < P, the results are exchanged through LDS (buf) back
-// into lane-major order for the next pass.  tw: W_P^t table (forward sign).
+// Twiddles arrive pre-loaded in `tw` (unused when NS == 1).
 template <int E, int R, int NS, bool INV>
-__device__ __forceinline__ void stockham_pass(cf (&v)[E], cf* buf, const cf* tw, int lane) {
-    constexpr int P = 64 * E;
+__device__ __forceinline__ void stockham_compute(cf (&v)[E], const PassTw<E, R, NS>& tw) {
     constexpr int B = E / R;  // butterflies per lane
-    constexpr int TWS = P / (NS * R);
 #pragma unroll
     for (int b = 0; b < B; ++b) {
         cf x[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) x[r] = v[b + r * B];
-        const int j = lane + 64 * b;
         if constexpr (NS > 1) {
-            const int jm = j % NS;
 #pragma unroll
-            for (int r = 1; r < R; ++r) {
-                cf w = tw[r * jm * TWS];
-                x[r] = INV ? cmulc(x[r], w) : cmul(x[r], w);
-            }
+            for (int r = 1; r < R; ++r) x[r] = INV ? cmulc(x[r], tw.w[b][r - 1]) : cmul(x[r], tw.w[b][r - 1]);
         }
         dftR<R, INV>(x);
 #pragma unroll
         for (int r = 0; r < R; ++r) v[b + r * B] = x[r];
     }
-    if constexpr (NS * R < P) {
-        // y[(j/NS) NS R + (j mod NS) + r NS]  ->  LDS ; then read x[lane + 64 m]
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int j = lane + 64 * b;
-            const int base = (j / NS) * NS * R + (j % NS);
-#pragma unroll
-            for (int r = 0; r < R; ++r) buf[pad_idx(base + r * NS)] = v[b + r * B];
-        }
-        wave_lds_fence();
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = buf[pad_idx(lane + 64 * m)];
-        wave_lds_fence();
-    }
 }
 
-template <int E, int NS, bool INV>
-__device__ __forceinline__ void fft_passes(cf (&v)[E], cf* buf, const cf* tw, int lane) {
+// y[(j/NS) NS R + (j mod NS) + r NS] -> LDS, then read back x[lane + 64 m].
+template <int E, int R, int NS>
+__device__ __forceinline__ void stockham_exchange(cf (&v)[E], cf* buf, int lane) {
+    constexpr int B = E / R;
+#ifdef CRLOT_ABL_NOXCHG  // timing-only ablation: wrong results
+    return;
+#endif
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int j = lane + 64 * b;
+        const int base = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[swz<NS, R>(base + r * NS)] = v[b + r * B];
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < E; ++m) v[m] = buf[swz<NS, R>(lane + 64 * m)];
+    wave_lds_fence();
+}
+
+// Pass NS (twiddles already in `tw`); the next pass's twiddles are issued
+// BEFORE this pass's exchange so their LDS latency hides under it.
+template <int E, int NS, int TOFF, bool INV, typename TW>
+__device__ __forceinline__ void fft_passes(cf (&v)[E], cf* buf, const cf* twp, int lane,
+                                           const TW& tw) {
     constexpr int P = 64 * E;
     if constexpr (NS < P) {
-        constexpr int R = radix_for<P>(P / NS, E);
-        stockham_pass<E, R, NS, INV>(v, buf, tw, lane);
-        fft_passes<E, NS * R, INV>(v, buf, tw, lane);
+        constexpr int R = radix_for(P / NS, E);
+        stockham_compute<E, R, NS, INV>(v, tw);
+        if constexpr (NS * R < P) {
+            constexpr int NS2 = NS * R;
+            constexpr int R2 = radix_for(P / NS2, E);
+            constexpr int TOFF2 = TOFF + (NS > 1 ? (R - 1) * NS : 0);
+            PassTw<E, R2, NS2> tw2;
+            load_pass_tw<E, R2, NS2, TOFF2>(tw2, twp, lane);
+            stockham_exchange<E, R, NS>(v, buf, lane);
+            fft_passes<E, NS2, TOFF2, INV>(v, buf, twp, lane, tw2);
+        }
     }
 }
 
 // In-place P-point complex FFT (unnormalised) of the lane-major registers.
+// twp: per-pass forward twiddles (inverse uses their conjugates).
 template <int E, bool INV>
-__device__ __forceinline__ void fft_wave(cf (&v)[E], cf* buf, const cf* tw, int lane) {
-    fft_passes<E, 1, INV>(v, buf, tw, lane);
+__device__ __forceinline__ void fft_wave(cf (&v)[E], cf* buf, const cf* twp, int lane) {
+    constexpr int R = radix_for(64 * E, E);
+    PassTw<E, R, 1> none;
+    fft_passes<E, 1, 0, INV>(v, buf, twp, lane, none);
+}
+
+// All passes' per-lane twiddles held in registers (they do not depend on the
+// frame, so a wave that walks many frames loads them once).
+template <int E, int NS, bool END = (NS >= 64 * E)>
+struct TwChain {
+    static constexpr int R = radix_for(64 * E / NS, E);
+    PassTw<E, R, NS> here;
+    TwChain<E, NS * R> next;
+};
+template <int E, int NS>
+struct TwChain<E, NS, true> {};
+
+template <int E, int NS, int TOFF>
+__device__ __forceinline__ void load_chain(TwChain<E, NS>& c, const cf* twp, int lane) {
+    if constexpr (NS < 64 * E) {
+        constexpr int R = radix_for(64 * E / NS, E);
+        if constexpr (NS > 1) load_pass_tw<E, R, NS, TOFF>(c.here, twp, lane);
+        load_chain<E, NS * R, TOFF + (NS > 1 ? (R - 1) * NS : 0)>(c.next, twp, lane);
+    }
+}
+
+template <int E, int NS, bool INV>
+__device__ __forceinline__ void fft_passes_reg(cf (&v)[E], cf* buf, const TwChain<E, NS>& c,
+                                               int lane) {
+    constexpr int P = 64 * E;
+    if constexpr (NS < P) {
+        constexpr int R = radix_for(P / NS, E);
+        stockham_compute<E, R, NS, INV>(v, c.here);
+        if constexpr (NS * R < P) {
+            stockham_exchange<E, R, NS>(v, buf, lane);
+            fft_passes_reg<E, NS * R, INV>(v, buf, c.next, lane);
+        }
+    }
+}
+
+template <int E, bool INV>
+__device__ __forceinline__ void fft_wave_reg(cf (&v)[E], cf* buf, const TwChain<E, 1>& c,
+                                             int lane) {
+    fft_passes_reg<E, 1, INV>(v, buf, c, lane);
 }
 
 // ------------------------------------------------------------- sanitize
 // KissFftPlan sanitize (kissfft_adapter.cc:102-110, 156-163):
 // NaN/Inf -> 0, |v| < 1e-30 -> 0.
 __device__ __forceinline__ float sanit(float v) {
+#ifdef CRLOT_ABL_NOSANIT  // timing-only ablation
+    return v;
+#endif
     const float a = __builtin_fabsf(v);
     return (a >= 1e-30f && a <= 3.402823466e+38f) ? v : 0.0f;
 }
@@ -205,12 +301,16 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
                                                       int lane, cf* spec = nullptr) {
     constexpr int P = 64 * E;
 #pragma unroll
-    for (int m = 0; m < E; ++m) buf[pad_idx(lane + 64 * m)] = v[m];
+    for (int m = 0; m < E; ++m) buf[lane + 64 * m] = v[m];  // conflict free unswizzled
     wave_lds_fence();
     cf zp[E];
 #pragma unroll
-    for (int m = 0; m < E; ++m) zp[m] = buf[pad_idx((P - (lane + 64 * m)) & (P - 1))];
+    for (int m = 0; m < E; ++m) zp[m] = buf[(P - (lane + 64 * m)) & (P - 1)];
     wave_lds_fence();
+#ifdef CRLOT_ABL_NOSPLITX  // timing-only ablation: wrong results
+#pragma unroll
+    for (int m = 0; m < E; ++m) zp[m] = v[E - 1 - m];
+#endif
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int k = lane + 64 * m;

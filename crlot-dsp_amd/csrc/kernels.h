@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace crlot {
 
@@ -12,10 +13,15 @@ struct DevTables {
     const float* wa = nullptr;   // analysis window [N] (all ones if disabled)
     const float* ws = nullptr;   // synthesis window [N] (all ones if none)
     const float* den = nullptr;  // max(norm, eps) [ring_len]
-    const float* tw = nullptr;   // W_P^t, t < P, float pairs
+    const float* tw = nullptr;   // per-pass Stockham twiddles (build_pass_twiddles)
     const float* st = nullptr;   // exp(-i pi (k/P + 1/2)), k < P, float pairs
     const float* gain = nullptr; // spectral gain [P+1] or nullptr
 };
+
+// Per-pass Stockham twiddles for an N-point real frame (P = N/2 complex points),
+// laid out as the device reads them (fft_wave.h twiddle_table_size), computed in
+// double and rounded to float.  Returns float pairs.
+std::vector<float> build_pass_twiddles(int n);
 
 struct Geometry {
     int n = 0;          // frame size N

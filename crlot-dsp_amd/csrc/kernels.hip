@@ -20,6 +20,8 @@
 // update fma(fma(src, w, 0), g, dst) (kernels.cc:24-28) and the IEEE division
 // acc / max(norm, eps) (kernels.cc:30-36).  Built with -ffp-contract=off and
 // the default correctly-rounded f32 division; subnormals are preserved.
+#include <cmath>
+
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -34,7 +36,7 @@ constexpr int kBlock = 64 * kWaves;
 
 template <int P>
 __host__ __device__ constexpr int xbuf_elems() {
-    return P + P / 8;
+    return P;
 }
 
 // LDS carve shared by the kernels: [tw P cf][st P cf][sth P cf][wa N f][ws N f][bufs]
@@ -52,8 +54,8 @@ __device__ __forceinline__ void load_tables(const DevTables& t, cf* tw, cf* st, 
     constexpr int P = 64 * E, N = 2 * P;
     const cf* gtw = reinterpret_cast<const cf*>(t.tw);
     const cf* gst = reinterpret_cast<const cf*>(t.st);
+    for (int i = threadIdx.x; i < dev::twiddle_table_size(E); i += kBlock) tw[i] = gtw[i];
     for (int i = threadIdx.x; i < P; i += kBlock) {
-        tw[i] = gtw[i];
         const cf w = gst[i];
         st[i] = w;
         sth[i] = cf{w.r * 0.5f, w.i * 0.5f};  // exact
@@ -94,8 +96,11 @@ __device__ __forceinline__ void load_pairs(float2 (&dst)[E], __amdgpu_buffer_rsr
     }
 }
 
+#ifndef CRLOT_FUSED_MIN_WAVES
+#define CRLOT_FUSED_MIN_WAVES 1
+#endif
 template <int E, int S, int NB, bool HAS_GAIN>
-__global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
+__global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fused(const FusedArgs a) {
     constexpr int P = 64 * E, N = 2 * P, H = 128 * S;
     static_assert(NB * S == E, "N = NB * H");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -122,6 +127,24 @@ __global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
     const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
     const float g = a.gain;
 
+#ifndef CRLOT_TW_REGS
+#define CRLOT_TW_REGS 0
+#endif
+#ifndef CRLOT_WIN_REGS
+#define CRLOT_WIN_REGS 0
+#endif
+#if CRLOT_TW_REGS
+    dev::TwChain<E, 1> twc;
+    dev::load_chain<E, 1, 0>(twc, tw, lane);
+#endif
+#if CRLOT_WIN_REGS
+    float2 wreg_a[E], wreg_s[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wreg_a[m] = *reinterpret_cast<const float2*>(wa + 2 * (lane + 64 * m));
+        wreg_s[m] = *reinterpret_cast<const float2*>(ws + 2 * (lane + 64 * m));
+    }
+#endif
     float2 xin[E];
     load_pairs<0, E, E>(xin, rx, lane, fs * H * 4, fs * H + N <= a.T);
     float2 acc[NB][S];
@@ -144,17 +167,31 @@ __global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
         cf v[E];
 #pragma unroll
         for (int m = 0; m < E; ++m) {
+#if CRLOT_WIN_REGS
+            const float2 w = wreg_a[m];
+#else
             const float2 w = *reinterpret_cast<const float2*>(wa + 2 * (lane + 64 * m));
+#endif
             v[m].r = dev::sanit(xin[m].x * w.x);
             v[m].i = dev::sanit(xin[m].y * w.y);
         }
+#if CRLOT_TW_REGS
+        dev::fft_wave_reg<E, false>(v, buf, twc, lane);
+        dev::real_split_hook_merge<E, HAS_GAIN, false>(v, buf, st, sth, a.t.gain, lane);
+        dev::fft_wave_reg<E, true>(v, buf, twc, lane);
+#else
         dev::fft_wave<E, false>(v, buf, tw, lane);
         dev::real_split_hook_merge<E, HAS_GAIN, false>(v, buf, st, sth, a.t.gain, lane);
         dev::fft_wave<E, true>(v, buf, tw, lane);
+#endif
         // *1/N, sanitize, synthesis window, OLA accumulate (ascending k)
 #pragma unroll
         for (int m = 0; m < E; ++m) {
+#if CRLOT_WIN_REGS
+            const float2 w = wreg_s[m];
+#else
             const float2 w = *reinterpret_cast<const float2*>(ws + 2 * (lane + 64 * m));
+#endif
             const float o0 = dev::sanit(v[m].r * a.inv_n);
             const float o1 = dev::sanit(v[m].i * a.inv_n);
             float2& r = acc[m / S][m % S];
@@ -165,8 +202,13 @@ __global__ __launch_bounds__(kBlock) void k_stft_ola_fused(const FusedArgs a) {
         if (k >= f0) {
 #pragma unroll
             for (int q = 0; q < S; ++q)
+#ifdef CRLOT_ABL_NODIV  // timing-only ablation
+                dev::bstore2(make_float2(acc[0][q].x * dn[q].x, acc[0][q].y * dn[q].y), ry,
+                             lane * 8 + q * 512, k * H * 4);
+#else
                 dev::bstore2(make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y), ry,
                              lane * 8 + q * 512, k * H * 4);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < NB - 1; ++j)
@@ -297,14 +339,14 @@ __global__ __launch_bounds__(kBlock) void k_rfft(const FftArgs a) {
     dev::fft_wave<E, false>(v, buf, tw, lane);
     // split only (kiss_fftr): X[k] for own k, X[P] from k == 0
 #pragma unroll
-    for (int m = 0; m < E; ++m) buf[dev::pad_idx(lane + 64 * m)] = v[m];
+    for (int m = 0; m < E; ++m) buf[lane + 64 * m] = v[m];
     dev::wave_lds_fence();
     float* out = a.out + b * a.ld_out;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int k = lane + 64 * m;
         const cf zk = v[m];
-        const cf fpnk = dev::conj(buf[dev::pad_idx((P - k) & (P - 1))]);
+        const cf fpnk = dev::conj(buf[(P - k) & (P - 1)]);
         const cf f1 = dev::cadd(zk, fpnk);
         const cf f2 = dev::csub(zk, fpnk);
         const cf t = dev::cmul(f2, sth[k]);
@@ -414,6 +456,25 @@ hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) 
 }
 
 }  // namespace
+
+std::vector<float> build_pass_twiddles(int n) {
+    const int p = n / 2, e = p / 64;
+    std::vector<float> t;
+    int ns = 1;
+    while (ns < p) {
+        const int r = dev::radix_for(p / ns, e);
+        if (ns > 1) {
+            for (int q = 1; q < r; ++q)
+                for (int jm = 0; jm < ns; ++jm) {
+                    const double ph = -2.0 * M_PI * double(q) * double(jm) / double(ns * r);
+                    t.push_back(float(std::cos(ph)));
+                    t.push_back(float(std::sin(ph)));
+                }
+        }
+        ns *= r;
+    }
+    return t;
+}
 
 bool fused_supported(int n, int h) {
     const int e = e_of(n);

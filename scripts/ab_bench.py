@@ -1,0 +1,65 @@
+"""A/B timing of library variants (crlot-dsp_amd/variants/*.so) in ONE process,
+interleaved rounds (cdna_hip_programming.md 5.4 rule 24).  Each variant is
+loaded through its own ctypes handle; the workload is the headline one."""
+import ctypes as C
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+S, T, N, H = int(os.environ.get("AB_S", 1024)), 480000, int(os.environ.get("AB_N", 1024)), int(os.environ.get("AB_H", 256))
+libs = sorted(glob.glob(os.path.join(ROOT, "crlot-dsp_amd", "variants", "*.so")))
+base = os.path.join(ROOT, "crlot-dsp_amd", "libcrlot_dsp.so")
+libs = [base] + libs
+
+
+class Desc(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("frame_size", "hop_size", "window_type", "periodic",
+                                         "window_norm", "boundary_mode", "analysis_window",
+                                         "apply_window_inside")] + [
+        ("eps", C.c_float), ("ola_gain", C.c_float), ("ring_len", C.c_int32), ("device", C.c_int32)]
+
+
+g = torch.Generator(device="cuda").manual_seed(3)
+x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
+F = (T + H - 1) // H
+ys = {}
+plans = {}
+handles = {}
+for path in libs:
+    L = C.CDLL(path, mode=os.RTLD_LOCAL)
+    L.crlot_plan_create.argtypes = [C.POINTER(Desc), C.POINTER(C.c_void_p)]
+    L.crlot_roundtrip.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64,
+                                  C.c_int64, C.c_int64, C.c_void_p]
+    d = Desc(N, H, 0, 0, 0, 0, 1, 1, 1e-8, 1.0, 0, -1)
+    h = C.c_void_p()
+    assert L.crlot_plan_create(C.byref(d), C.byref(h)) == 0
+    handles[path], plans[path] = L, h
+    ys[path] = torch.empty((S, F * H), device="cuda")
+
+stream = torch.cuda.current_stream()
+times = {p: [] for p in libs}
+for rnd in range(5):
+    for p in libs:
+        L, h, y = handles[p], plans[p], ys[p]
+        for _ in range(2):
+            L.crlot_roundtrip(h, x.data_ptr(), y.data_ptr(), S, T, T, F * H, stream.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            L.crlot_roundtrip(h, x.data_ptr(), y.data_ptr(), S, T, T, F * H, stream.cuda_stream)
+        e1.record()
+        torch.cuda.synchronize()
+        times[p].append(e0.elapsed_time(e1) / 5)
+ref = ys[base]
+for p in libs:
+    t = sorted(times[p])
+    same = bool(torch.equal(ys[p], ref))
+    maxd = float((ys[p] - ref).abs().max())
+    print(json.dumps({"lib": os.path.basename(p), "ms_median": round(t[len(t) // 2], 4),
+                      "ms_min": round(t[0], 4), "Msamples_s": round(S * T / t[len(t) // 2] / 1e3, 1),
+                      "bitexact_vs_base": same, "maxdiff": maxd}))

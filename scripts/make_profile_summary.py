@@ -1,0 +1,70 @@
+"""Turn gpurun_out/prof_<tag>/ into committed summaries under profiles/:
+  profiles/<tag>_kernel_stats.csv    rocprofv3 --kernel-trace --stats of bench.py
+  profiles/<tag>_pmc_summary.json    per-launch PMC values of the fused kernel and
+                                     the HBM traffic figure bench.py reports.
+HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: FETCH_SIZE reads
+half the bytes of a coalesced streaming read on gfx950 (MI355X_MICROARCH.md,
+HBM section); WRITE_SIZE is exact for streaming stores.  Our reads are 8 B/lane
+dwordx2; the doubled value lands at 1.05x the algorithmic read bytes, which the
+recomputed warm-up frames (3 per 125-frame chunk) and the normaliser table explain."""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+src = f"gpurun_out/prof_{tag}"
+os.makedirs("profiles", exist_ok=True)
+stats = glob.glob(f"{src}/trace/run_kernel_stats.csv")
+if stats:
+    shutil.copy(stats[0], f"profiles/{tag}_kernel_stats.csv")
+
+
+def counters(sub, pat="stft_ola_fused"):
+    agg = collections.defaultdict(list)
+    for f in glob.glob(f"{src}/{sub}/run_counter_collection.csv"):
+        per = collections.defaultdict(dict)
+        for r in csv.DictReader(open(f)):
+            if pat in r["Kernel_Name"]:
+                per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
+                kname = r["Kernel_Name"]
+                vg = r.get("VGPR_Count")
+        for c in per.values():
+            for k, v in c.items():
+                agg[k].append(v)
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+pmc = {}
+for sub in ("fetch", "write", "sq", "lds"):
+    pmc.update(counters(sub))
+S, T, N, H = 1024, 480000, 1024, 256
+alg_read = S * T * 4
+alg_write = S * T * 4
+hbm = None
+if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+    hbm = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
+dur = None
+tr = glob.glob(f"{src}/trace/run_kernel_stats.csv")
+if tr:
+    for r in csv.DictReader(open(tr[0])):
+        if "stft_ola_fused" in r["Name"]:
+            dur = float(r["AverageNs"])
+out = {
+    "tag": tag,
+    "workload_key": f"{S}x{T}_N{N}_H{H}",
+    "kernel": "k_stft_ola_fused<8,2,4,false>",
+    "avg_duration_ns_trace": dur,
+    "pmc_per_launch": pmc,
+    "algorithmic_bytes_per_launch": alg_read + alg_write,
+    "hbm_bytes_per_launch": hbm,
+    "hbm_over_algorithmic": None if hbm is None else hbm / (alg_read + alg_write),
+    "fetch_bytes_corrected": None if "FETCH_SIZE" not in pmc else 2 * pmc["FETCH_SIZE"] * 1024,
+    "write_bytes": None if "WRITE_SIZE" not in pmc else pmc["WRITE_SIZE"] * 1024,
+    "note": __doc__.strip(),
+}
+json.dump(out, open(f"profiles/{tag}_pmc_summary.json", "w"), indent=1)
+print(json.dumps({k: v for k, v in out.items() if k not in ("note", "pmc_per_launch")}, indent=1))
