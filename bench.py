@@ -114,17 +114,13 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
-    from __graft_entry__ import load_pkg
+    from __graft_entry__ import load_pkg, load_dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    D = load_dist()
+    _, world, local = D.env_rank_world()
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
+    rank, world = D.init("nccl", dev)
 
     pkg = load_pkg()
     plan = pkg.Plan(frame_size=N_FFT, hop_size=HOP, device=dev.index)
@@ -141,8 +137,7 @@ def main():
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -150,15 +145,10 @@ def main():
         plan.roundtrip(x, y)
         ev[i][1].record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
+    elapsed_max = D.max_over_ranks(elapsed, dev)
 
     samples_step_rank = S * T
     total_samples = samples_step_rank * world * args.steps
@@ -220,8 +210,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    D.finalize()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,263 @@
+// crlot_dsp.hpp -- C++ host surface over the C ABI (header-only).
+//
+// Mirrors the reference's C++ API for the hot path so C++ callers drop in:
+//   crlot::dsp::WindowLUT          <- dsp::WindowLUT        (WindowLUT.h:80-199)
+//   crlot::dsp::fft::FftPlanDesc   <- dsp::fft::FftPlanDesc (fft_api.h:16-23)
+//   crlot::dsp::fft::IFftPlan      <- dsp::fft::IFftPlan    (fft_api.h:26-48)
+//   crlot::dsp::fft::MakeFftPlan   <- dsp::fft::MakeFftPlan (fft_api.h:51), HIP-backed
+//   crlot::StftEngine              <- the Framer -> window -> FFT -> iFFT -> OLA loop
+//                                     of bench/e2e_benchmark.cc:138-186, batched
+// Error codes become the reference's exception types: CRLOT_EINVAL ->
+// std::invalid_argument, CRLOT_ENOMEM -> std::bad_alloc, everything else ->
+// std::runtime_error.  Host-pointer calls stage through device buffers owned by
+// the object; device-pointer calls (suffix _device) take HBM-resident data.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <complex>
+#include <cstdint>
+#include <memory>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "crlot_dsp.h"
+
+namespace crlot {
+
+inline void check(int rc, const char* what) {
+    if (rc >= 0) return;
+    std::string msg = std::string(what) + ": " + crlot_last_error();
+    if (rc == CRLOT_EINVAL) throw std::invalid_argument(msg);
+    if (rc == CRLOT_ENOMEM) throw std::bad_alloc();
+    throw std::runtime_error(msg);
+}
+
+inline void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Device buffer (RAII).
+template <typename T>
+class DeviceBuffer {
+   public:
+    DeviceBuffer() = default;
+    explicit DeviceBuffer(size_t n) { resize(n); }
+    ~DeviceBuffer() {
+        if (p_) (void)hipFree(p_);
+    }
+    DeviceBuffer(const DeviceBuffer&) = delete;
+    DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+    void resize(size_t n) {
+        if (n <= n_) return;
+        if (p_) (void)hipFree(p_);
+        p_ = nullptr;
+        n_ = 0;
+        if (hipMalloc(&p_, n * sizeof(T)) != hipSuccess) throw std::bad_alloc();
+        n_ = n;
+    }
+    T* get() const { return p_; }
+    size_t size() const { return n_; }
+
+   private:
+    T* p_ = nullptr;
+    size_t n_ = 0;
+};
+
+// Owning plan handle.
+class Plan {
+   public:
+    explicit Plan(const crlot_plan_desc& d) { check(crlot_plan_create(&d, &p_), "crlot_plan_create"); }
+    ~Plan() { crlot_plan_destroy(p_); }
+    Plan(const Plan&) = delete;
+    Plan& operator=(const Plan&) = delete;
+    crlot_plan* get() const { return p_; }
+    int frame_size() const {
+        int32_t n = 0;
+        check(crlot_plan_info(p_, &n, nullptr, nullptr), "crlot_plan_info");
+        return n;
+    }
+    int hop_size() const {
+        int32_t h = 0;
+        check(crlot_plan_info(p_, nullptr, &h, nullptr), "crlot_plan_info");
+        return h;
+    }
+
+   private:
+    crlot_plan* p_ = nullptr;
+};
+
+// Batched round trip: n_streams mono streams, each T samples.
+class StftEngine {
+   public:
+    struct Config {
+        int frame_size = 1024, hop_size = 256;
+        int window_type = CRLOT_WIN_HANN;
+        bool periodic = false;
+        int boundary_mode = CRLOT_ZERO_PAD;
+        bool analysis_window = true, apply_window_inside = true;
+        float eps = 1e-8f, gain = 1.0f;
+        int device = -1;
+    };
+    explicit StftEngine(const Config& c) : plan_(desc(c)) {}
+    int64_t frame_count(int64_t T) const { return crlot_frame_count(plan_.get(), T); }
+    int64_t output_length(int64_t T) const { return crlot_output_length(plan_.get(), T); }
+    // d_x [n_streams][ld_x], d_y [n_streams][ld_y] device pointers
+    void roundtrip_device(const float* d_x, float* d_y, int n_streams, int64_t T, int64_t ld_x,
+                          int64_t ld_y, hipStream_t s = nullptr) {
+        check(crlot_roundtrip(plan_.get(), d_x, d_y, n_streams, T, ld_x, ld_y, s), "crlot_roundtrip");
+    }
+    // host convenience: x [n_streams][T] -> y [n_streams][output_length(T)]
+    std::vector<float> roundtrip(const std::vector<float>& x, int n_streams, int64_t T) {
+        const int64_t L = output_length(T);
+        dx_.resize(size_t(n_streams) * T);
+        dy_.resize(size_t(n_streams) * L);
+        hip_check(hipMemcpy(dx_.get(), x.data(), sizeof(float) * n_streams * T, hipMemcpyHostToDevice),
+                  "hipMemcpy");
+        roundtrip_device(dx_.get(), dy_.get(), n_streams, T, T, L);
+        std::vector<float> y(size_t(n_streams) * L);
+        hip_check(hipMemcpy(y.data(), dy_.get(), sizeof(float) * y.size(), hipMemcpyDeviceToHost),
+                  "hipMemcpy");
+        return y;
+    }
+    void set_spectral_gain(const float* gain_or_null) {
+        check(crlot_plan_set_spectral_gain(plan_.get(), gain_or_null), "set_spectral_gain");
+    }
+    crlot_plan* plan() const { return plan_.get(); }
+
+   private:
+    static crlot_plan_desc desc(const Config& c) {
+        crlot_plan_desc d{};
+        d.frame_size = c.frame_size;
+        d.hop_size = c.hop_size;
+        d.window_type = c.window_type;
+        d.periodic = c.periodic;
+        d.boundary_mode = c.boundary_mode;
+        d.analysis_window = c.analysis_window;
+        d.apply_window_inside = c.apply_window_inside;
+        d.eps = c.eps;
+        d.ola_gain = c.gain;
+        d.device = c.device;
+        return d;
+    }
+    Plan plan_;
+    DeviceBuffer<float> dx_, dy_;
+};
+
+namespace dsp {
+
+enum class WindowType { HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS };
+enum class NormalizationType { NONE, SUM_TO_ONE, L2_NORM, OLA_UNITY_GAIN, OLA_SUM_WSQ };
+
+// WindowLUT(nfft, type, periodic, norm).data(): the reference's tables, bit-exact.
+class WindowLUT {
+   public:
+    WindowLUT(size_t nfft, WindowType type, bool periodic = false,
+              NormalizationType norm = NormalizationType::NONE)
+        : data_(nfft) {
+        if (nfft == 0) throw std::invalid_argument("Window size must be greater than 0");
+        if (type == WindowType::BLACKMAN_HARRIS)
+            throw std::invalid_argument("Blackman-Harris window not yet implemented");
+        check(crlot_window_table(int32_t(type), int64_t(nfft), periodic, int32_t(norm), data_.data()),
+              "crlot_window_table");
+    }
+    const float* data() const { return data_.data(); }
+    size_t size() const { return data_.size(); }
+
+   private:
+    std::vector<float> data_;
+};
+
+namespace fft {
+
+enum class FftDomain { Real, Complex };
+
+struct FftPlanDesc {
+    FftDomain domain;
+    int nfft;
+    bool in_place;
+    int batch;
+    int stride_in;
+    int stride_out;
+};
+
+class IFftPlan {
+   public:
+    virtual ~IFftPlan() = default;
+    virtual void forward(const float* in, std::complex<float>* out, int batch = 1) = 0;
+    virtual void inverse(const std::complex<float>* in, float* out, int batch = 1) = 0;
+    virtual FftDomain domain() const = 0;
+    virtual int size() const = 0;
+    virtual bool supports_batch() const { return true; }
+    virtual int max_batch_size() const = 0;
+};
+
+// HIP-backed real FFT plan with KissFftPlan's semantics (sanitize on the forward
+// input; 1/N and sanitize on the inverse output; batch b at b*stride*N, element
+// i at i*stride).  Validation mirrors KissFftPlan (kissfft_adapter.cc:13-63)
+// except the batch ceiling, which the device path does not need.
+class HipRealFftPlan final : public IFftPlan {
+   public:
+    explicit HipRealFftPlan(const FftPlanDesc& d) : d_(d), plan_(pdesc(d)) {}
+    void forward(const float* in, std::complex<float>* out, int batch = 1) override {
+        if (batch < 1 || batch > d_.batch) throw std::runtime_error("Invalid batch size");
+        const int64_t n = d_.nfft, bins = n / 2 + 1;
+        const int64_t in_len = int64_t(batch) * d_.stride_in * n, out_len = int64_t(batch) * d_.stride_out * bins;
+        din_.resize(size_t(in_len));
+        dout_.resize(size_t(2 * out_len));
+        hip_check(hipMemcpy(din_.get(), in, sizeof(float) * in_len, hipMemcpyHostToDevice), "hipMemcpy");
+        // the reference only writes the strided elements: start from the caller's buffer
+        hip_check(hipMemcpy(dout_.get(), out, sizeof(float) * 2 * out_len, hipMemcpyHostToDevice),
+                  "hipMemcpy");
+        check(crlot_rfft_batched(plan_.get(), din_.get(), dout_.get(), batch, d_.stride_in * n,
+                                 d_.stride_in, 2 * d_.stride_out * bins, d_.stride_out, nullptr),
+              "crlot_rfft_batched");
+        hip_check(hipMemcpy(out, dout_.get(), sizeof(float) * 2 * out_len, hipMemcpyDeviceToHost),
+                  "hipMemcpy");
+    }
+    void inverse(const std::complex<float>* in, float* out, int batch = 1) override {
+        if (batch < 1 || batch > d_.batch) throw std::runtime_error("Invalid batch size");
+        const int64_t n = d_.nfft, bins = n / 2 + 1;
+        const int64_t in_len = int64_t(batch) * d_.stride_in * bins, out_len = int64_t(batch) * d_.stride_out * n;
+        din_.resize(size_t(2 * in_len));
+        dout_.resize(size_t(out_len));
+        hip_check(hipMemcpy(din_.get(), in, sizeof(float) * 2 * in_len, hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(hipMemcpy(dout_.get(), out, sizeof(float) * out_len, hipMemcpyHostToDevice), "hipMemcpy");
+        check(crlot_irfft_batched(plan_.get(), din_.get(), dout_.get(), batch, 2 * d_.stride_in * bins,
+                                  d_.stride_in, d_.stride_out * n, d_.stride_out, nullptr),
+              "crlot_irfft_batched");
+        hip_check(hipMemcpy(out, dout_.get(), sizeof(float) * out_len, hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    FftDomain domain() const override { return FftDomain::Real; }
+    int size() const override { return d_.nfft; }
+    int max_batch_size() const override { return d_.batch; }
+
+   private:
+    static crlot_plan_desc pdesc(const FftPlanDesc& d) {
+        if (d.domain != FftDomain::Real) throw std::runtime_error("Unsupported FFT domain");
+        if (d.batch < 1) throw std::runtime_error("Batch size must be at least 1");
+        if (d.stride_in < 1 || d.stride_out < 1) throw std::runtime_error("Stride must be at least 1");
+        if (d.in_place) throw std::runtime_error("In-place FFT is not yet supported");
+        if (d.nfft % 2 != 0) throw std::runtime_error("FFT size must be even for real FFT");
+        crlot_plan_desc p{};
+        p.frame_size = d.nfft;
+        p.hop_size = d.nfft / 4 > 0 ? d.nfft / 4 : 1;
+        p.analysis_window = 0;
+        p.apply_window_inside = 0;
+        p.device = -1;
+        return p;
+    }
+    FftPlanDesc d_;
+    Plan plan_;
+    DeviceBuffer<float> din_, dout_;
+};
+
+inline std::unique_ptr<IFftPlan> MakeFftPlan(const FftPlanDesc& d) {
+    return std::make_unique<HipRealFftPlan>(d);
+}
+
+}  // namespace fft
+}  // namespace dsp
+}  // namespace crlot

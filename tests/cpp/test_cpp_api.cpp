@@ -1,0 +1,123 @@
+// C++ drop-in surface test (runs on the GPU box): the reference's own
+// known-answer checks from tests/fft_test.cc and the e2e round trip, written
+// against crlot::dsp::* exactly as the reference tests use dsp::*.
+// Links the product (libcrlot_dsp.so) and, as the checker only, the oracle.
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <vector>
+
+#include "../../include/crlot_dsp.hpp"
+#include "../../oracle/crlot_oracle.h"
+
+using namespace crlot::dsp;
+using namespace crlot::dsp::fft;
+
+static int failures = 0;
+#define EXPECT(cond, ...)                                             \
+    do {                                                              \
+        if (!(cond)) {                                                \
+            ++failures;                                               \
+            std::printf("FAIL %s:%d: %s ", __FILE__, __LINE__, #cond); \
+            std::printf(__VA_ARGS__);                                 \
+            std::printf("\n");                                        \
+        }                                                             \
+    } while (0)
+
+static FftPlanDesc real_desc(int n, int batch = 1, int si = 1, int so = 1) {
+    return FftPlanDesc{FftDomain::Real, n, false, batch, si, so};
+}
+
+int main() {
+    // fft_test.cc:131-155 DC
+    {
+        auto plan = MakeFftPlan(real_desc(512));
+        std::vector<float> x(512, 1.0f);
+        std::vector<std::complex<float>> X(257);
+        plan->forward(x.data(), X.data());
+        EXPECT(std::fabs(std::abs(X[0]) - 512.0f) < 1e-3f, "DC %g", std::abs(X[0]));
+        for (int i = 1; i < 257; ++i) EXPECT(std::abs(X[i]) < 1e-3f, "bin %d %g", i, std::abs(X[i]));
+    }
+    // fft_test.cc:157-197 cos at bin 10, round trip
+    for (int n : {512, 1024, 2048}) {
+        auto plan = MakeFftPlan(real_desc(n));
+        std::vector<float> x(n), y(n);
+        for (int i = 0; i < n; ++i) x[i] = 2.0f * std::cos(2.0f * float(M_PI) * 10.0f * (float(i) / n));
+        std::vector<std::complex<float>> X(n / 2 + 1);
+        plan->forward(x.data(), X.data());
+        EXPECT(std::fabs(std::abs(X[10]) - float(n)) < 1e-3f * n / 512, "n=%d |X10|=%g", n, std::abs(X[10]));
+        EXPECT(std::fabs(std::arg(X[10])) < 1e-3f, "phase");
+        plan->inverse(X.data(), y.data());
+        double e = 0;
+        for (int i = 0; i < n; ++i) e += double(x[i] - y[i]) * (x[i] - y[i]);
+        EXPECT(std::sqrt(e / n) < 1e-5, "n=%d rms %g", n, std::sqrt(e / n));
+    }
+    // fft_test.cc:199-221 NaN / denormal / Inf
+    {
+        auto plan = MakeFftPlan(real_desc(512));
+        std::vector<float> x(512, 0.0f), y(512);
+        x[0] = NAN;
+        x[1] = 1e-40f;
+        x[2] = INFINITY;
+        std::vector<std::complex<float>> X(257);
+        plan->forward(x.data(), X.data());
+        plan->inverse(X.data(), y.data());
+        for (float v : y) EXPECT(std::isfinite(v), "non-finite");
+    }
+    // fft_test.cc:223-248 invalid configuration
+    {
+        bool threw = false;
+        try {
+            MakeFftPlan(real_desc(513));
+        } catch (const std::runtime_error&) {
+            threw = true;
+        }
+        EXPECT(threw, "odd N must throw");
+    }
+    // fft_test.cc:450-495 stride layout
+    {
+        const int n = 256, B = 3, st = 2;  // reference uses 128; device path starts at 256
+        auto plan = MakeFftPlan(real_desc(n, B, st, st));
+        std::vector<float> in(B * n * st, 0.0f), rec(B * n * st, 0.0f);
+        for (int b = 0; b < B; ++b)
+            for (int i = 0; i < n; ++i) in[b * n * st + i * st] = std::sin(2.0f * float(M_PI) * (b + 1) * i / n);
+        std::vector<std::complex<float>> out(B * (n / 2 + 1) * st);
+        plan->forward(in.data(), out.data(), B);
+        plan->inverse(out.data(), rec.data(), B);
+        for (int b = 0; b < B; ++b)
+            for (int i = 0; i < n; ++i)
+                EXPECT(std::fabs(in[b * n * st + i * st] - rec[b * n * st + i * st]) < 1e-4f, "stride b=%d i=%d", b, i);
+    }
+    // WindowLUT: the reference default (symmetric Hann) equals the oracle bit for bit
+    {
+        WindowLUT lut(1024, WindowType::HANN);
+        std::vector<float> ref(1024);
+        or_window(OR_HANN, 1024, 0, OR_NORM_NONE, ref.data());
+        for (int i = 0; i < 1024; ++i) EXPECT(lut.data()[i] == ref[i], "window %d", i);
+    }
+    // e2e round trip: StftEngine vs the oracle restatement of e2e_benchmark.cc
+    {
+        crlot::StftEngine::Config c;
+        crlot::StftEngine eng(c);
+        const int S = 3;
+        const int64_t T = 48000;
+        std::vector<float> x(S * T);
+        for (int s = 0; s < S; ++s) or_synth_fill(x.data() + s * T, T, 1000 + s);
+        auto y = eng.roundtrip(x, S, T);
+        const int64_t L = eng.output_length(T);
+        std::vector<float> ref(L);
+        for (int s = 0; s < S; ++s) {
+            or_roundtrip(x.data() + s * T, T, 1024, 256, OR_HANN, 0, OR_ZERO_PAD, ref.data(), L, nullptr, nullptr);
+            double num = 0, den = 0, mx = 0;
+            for (int64_t i = 0; i < L; ++i) {
+                double d = double(y[s * L + i]) - ref[i];
+                num += d * d;
+                den += double(ref[i]) * ref[i];
+                mx = std::fmax(mx, std::fabs(d));
+            }
+            EXPECT(std::sqrt(num / den) < 1e-6 && mx < 2e-6, "stream %d rel %g max %g", s, std::sqrt(num / den), mx);
+        }
+    }
+    std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
+    return failures ? 1 : 0;
+}

@@ -330,3 +330,18 @@ def test_full_size_properties(pkg, oracle, torch_cuda):
         assert_close(host(y1[s]), ref, 0.5, f"full-size stream {s}")
     del x, y1, y2, yp, y4
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------ C++ surface
+def test_cpp_api_binary(torch_cuda):
+    """tests/cpp/test_cpp_api: the reference's fft_test.cc known answers and the
+    e2e round trip through crlot::dsp::* (include/crlot_dsp.hpp)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "cpp", "test_cpp_api")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(root, "tests", "cpp")], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout

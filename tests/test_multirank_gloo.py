@@ -1,0 +1,76 @@
+"""world_size-2 coverage of the multi-rank path on CPU (gloo): stream sharding
+covers every stream exactly once, per-rank results equal a single-process run,
+and the timing reduction is the max over ranks.  The per-rank compute here is
+the oracle (CPU), standing in for the device kernel, which the GPU tests cover."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r'''
+import os, sys, json, time
+import numpy as np
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)
+import importlib.util
+spec = importlib.util.spec_from_file_location("crlot_dist", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+D = importlib.util.module_from_spec(spec); spec.loader.exec_module(D)
+import oracle as O
+rank, world = D.init("gloo")
+S_total, T = 6, 5000
+lo, hi = D.stream_range(S_total, world, rank)
+x = O.synth_streams(S_total, T, config_id=5)[lo:hi]
+D.barrier()
+t0 = time.perf_counter()
+y = O.roundtrip_batch(x, 1024, 256)
+dt = time.perf_counter() - t0 + 0.05 * rank   # make ranks differ
+D.barrier()
+mx = D.max_over_ranks(dt)
+np.save(os.path.join(OUT, f"y_{rank}.npy"), y)
+json.dump({"rank": rank, "lo": lo, "hi": hi, "dt": dt, "max": mx}, open(os.path.join(OUT, f"r_{rank}.json"), "w"))
+D.finalize()
+'''
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_sharding_gloo(tmp_path, oracle):
+    script = tmp_path / "worker.py"
+    script.write_text(f"ROOT = {ROOT!r}\nOUT = {str(tmp_path)!r}\n" + WORKER)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2")
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=e))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    import json
+    rs = [json.load(open(tmp_path / f"r_{r}.json")) for r in range(2)]
+    assert (rs[0]["lo"], rs[0]["hi"], rs[1]["lo"], rs[1]["hi"]) == (0, 3, 3, 6)
+    assert rs[0]["max"] == rs[1]["max"] == max(r["dt"] for r in rs)
+    y = np.concatenate([np.load(tmp_path / f"y_{r}.npy") for r in range(2)])
+    x = oracle.synth_streams(6, 5000, config_id=5)
+    ref = oracle.roundtrip_batch(x, 1024, 256)
+    assert np.array_equal(y, ref)
+
+
+def test_stream_range_partitions():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("crlot_dist", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+    D = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(D)
+    for total in (1, 7, 1024, 8192):
+        for world in (1, 2, 3, 4, 8):
+            ranges = [D.stream_range(total, world, r) for r in range(world)]
+            assert ranges[0][0] == 0 and ranges[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
