@@ -83,6 +83,7 @@ def lib():
         "crlot_stream_destroy": ([vp], None),
         "crlot_stream_reset": ([vp], C.c_int),
         "crlot_stream_push_hop": ([vp, vp, vp, C.POINTER(i32), vp], C.c_int),
+        "crlot_stream_set_layout": ([vp, i32], C.c_int),
         "crlot_window_table": ([i32, i64, i32, i32, fp], C.c_int),
         "crlot_ring_len": ([i64, i64], i64),
         "crlot_norm_table": ([fp, i64, i64, i64, i32, f32, fp], C.c_int),
@@ -302,3 +303,41 @@ class Plan:
                                          1, n, 1, _stream_handle(X)),
                "crlot_irfft_batched")
         return out
+
+
+class Stream:
+    """Low-latency per-hop path (config 4): DROP-mode framing of `channels`
+    channels fed one hop at a time; device state persists across calls."""
+
+    def __init__(self, plan: Plan, channels: int, interleaved: bool = False):
+        self.plan = plan
+        self.channels = channels
+        self.interleaved = interleaved
+        h = C.c_void_p()
+        _check(lib().crlot_stream_create(plan._h, channels, C.byref(h)), "crlot_stream_create")
+        self._h = h
+        _check(lib().crlot_stream_set_layout(self._h, int(interleaved)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().crlot_stream_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def reset(self):
+        _check(lib().crlot_stream_reset(self._h))
+
+    def push_hop(self, hop, out=None, stream: int | None = None) -> tuple:
+        """hop: (channels, H) float32 CUDA tensor ((H, channels) if interleaved).
+        Returns (out, emitted) where emitted is 0 or H."""
+        torch = _torch()
+        if not hop.is_contiguous():
+            raise ValueError("hop must be contiguous")
+        if out is None:
+            out = torch.empty_like(hop)
+        em = C.c_int32()
+        s = _stream_handle(hop) if stream is None else stream
+        _check(lib().crlot_stream_push_hop(self._h, hop.data_ptr(), out.data_ptr(), C.byref(em), s),
+               "crlot_stream_push_hop")
+        return out, em.value

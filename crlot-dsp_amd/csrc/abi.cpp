@@ -385,29 +385,77 @@ int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t 
 struct crlot_stream {
     crlot_plan* plan = nullptr;
     int channels = 0;
+    int interleaved = 0;
+    int64_t q = 0;  // hops pushed so far
+    float* d_hist = nullptr;
+    float* d_acc = nullptr;
 };
 
 int crlot_stream_create(crlot_plan* p, int32_t channels, crlot_stream** out) {
     if (!p || !out || channels <= 0) return fail(CRLOT_EINVAL, "bad argument");
     *out = nullptr;
-    return fail(CRLOT_EUNSUPPORTED, "streaming path not built yet");
+    if (!crlot::fused_supported(p->geo.n, p->geo.h))
+        return fail(CRLOT_EUNSUPPORTED, "streaming path needs H % 128 == 0, N % H == 0, N <= 2048");
+    DeviceGuard g(p->device);
+    crlot_stream* st = new crlot_stream();
+    st->plan = p;
+    st->channels = channels;
+    const size_t bytes = sizeof(float) * size_t(channels) * p->geo.n;
+    hipError_t e;
+    if ((e = hipMalloc(&st->d_hist, bytes)) || (e = hipMalloc(&st->d_acc, bytes))) {
+        crlot_stream_destroy(st);
+        return hip_fail(e, "hipMalloc(stream state)");
+    }
+    if ((e = hipMemset(st->d_hist, 0, bytes)) || (e = hipMemset(st->d_acc, 0, bytes))) {
+        crlot_stream_destroy(st);
+        return hip_fail(e, "hipMemset(stream state)");
+    }
+    *out = st;
+    return CRLOT_OK;
 }
 
-void crlot_stream_destroy(crlot_stream* st) { delete st; }
+void crlot_stream_destroy(crlot_stream* st) {
+    if (!st) return;
+    DeviceGuard g(st->plan->device);
+    if (st->d_hist) (void)hipFree(st->d_hist);
+    if (st->d_acc) (void)hipFree(st->d_acc);
+    delete st;
+}
 
 int crlot_stream_reset(crlot_stream* st) {
     if (!st) return fail(CRLOT_EINVAL, "null stream");
-    return fail(CRLOT_EUNSUPPORTED, "streaming path not built yet");
+    DeviceGuard g(st->plan->device);
+    const size_t bytes = sizeof(float) * size_t(st->channels) * st->plan->geo.n;
+    hipError_t e;
+    if ((e = hipMemset(st->d_hist, 0, bytes)) || (e = hipMemset(st->d_acc, 0, bytes)))
+        return hip_fail(e, "hipMemset(stream state)");
+    st->q = 0;
+    return CRLOT_OK;
+}
+
+int crlot_stream_set_layout(crlot_stream* st, int32_t interleaved) {
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    st->interleaved = interleaved ? 1 : 0;
+    return CRLOT_OK;
 }
 
 int crlot_stream_push_hop(crlot_stream* st, const float* d_in, float* d_out, int32_t* emitted,
                           void* stream) {
-    (void)d_in;
-    (void)d_out;
-    (void)stream;
     if (emitted) *emitted = 0;
     if (!st) return fail(CRLOT_EINVAL, "null stream");
-    return fail(CRLOT_EUNSUPPORTED, "streaming path not built yet");
+    if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
+    crlot_plan* p = st->plan;
+    DeviceGuard g(p->device);
+    const int64_t C = st->channels, H = p->geo.h;
+    const int64_t ld = st->interleaved ? 1 : H, inc = st->interleaved ? C : 1;
+    hipError_t e = crlot::launch_stream_hop(p->geo, tables(p), d_in, ld, inc, d_out, ld, inc,
+                                            st->d_hist, st->d_acc, st->channels, st->q,
+                                            static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "stream kernel launch");
+    const int64_t nb = p->geo.n / H;
+    if (emitted) *emitted = (st->q >= nb - 1) ? int32_t(H) : 0;
+    st->q += 1;
+    return CRLOT_OK;
 }
 
 }  // extern "C"

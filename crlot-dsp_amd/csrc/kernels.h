@@ -47,6 +47,11 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
                              int64_t ld_frames, float* y, int n_streams, int64_t F,
                              int64_t ld_y, int64_t out_len, hipStream_t stream);
 
+// Streaming per-hop path (shapes as the fused path).  hist/acc: [channels][N].
+hipError_t launch_stream_hop(const Geometry& g, const DevTables& t, const float* in, int64_t in_ld,
+                             int64_t in_inc, float* out, int64_t out_ld, int64_t out_inc,
+                             float* hist, float* acc, int channels, int64_t q, hipStream_t stream);
+
 // Batched adapter-semantics real FFTs.
 hipError_t launch_rfft(const Geometry& g, const DevTables& t, const float* in, float* out,
                        int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,

@@ -396,6 +396,101 @@ __global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ streaming
+// One hop of the low-latency path (BASELINE config 4): per channel, the last
+// NB = N/H hops live in `hist` (slot q mod NB holds hop q) and the OLA
+// accumulator blocks in `acc` (slot b mod NB holds output block b).  Call q
+// (0-based) brings hop q; once q >= NB-1 the DROP-mode Framer yields frame
+// f = q-NB+1 (hops f..q), which goes through the same transform and OLA
+// arithmetic as the batched kernels; block f is then complete and emitted.
+// The lane that owns frame sample i owns it in every frame (H % 128 == 0), so a
+// lane only ever touches its own acc words: no cross-lane hazards.
+struct StreamArgs {
+    DevTables t;
+    const float* in;   // hop input: channel c sample i at in[c*in_ld + i*in_inc]
+    float* out;        // hop output, same layout (out_ld, out_inc)
+    float* hist;       // [C][N]
+    float* acc;        // [C][N]
+    int64_t in_ld, in_inc, out_ld, out_inc;
+    int64_t q;         // index of the hop being pushed
+    int channels, ring_len;
+    float inv_n, gain;
+};
+
+template <int E, int S, bool HAS_GAIN>
+__global__ __launch_bounds__(kBlock) void k_stream_hop(const StreamArgs a) {
+    constexpr int P = 64 * E, N = 2 * P, H = 128 * S, NB = E / S;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    cf* sth = st + P;
+    float* wa = reinterpret_cast<float*>(sth + P);
+    float* ws = wa + N;
+    cf* bufs = reinterpret_cast<cf*>(ws + N);
+    load_tables<E>(a.t, tw, st, sth, wa, ws, true);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    const int c = blockIdx.x * kWaves + wave;
+    if (c >= a.channels) return;
+    const float* in = a.in + c * a.in_ld;
+    float* hist = a.hist + int64_t(c) * N;
+    float* acc = a.acc + int64_t(c) * N;
+    const int64_t q = a.q;
+    // the new hop: frame pairs m in [E-S, E) when a frame completes this call
+    float2 hop[S];
+#pragma unroll
+    for (int s2 = 0; s2 < S; ++s2) {
+        const int i0 = 2 * (lane + 64 * s2);
+        hop[s2] = make_float2(in[i0 * a.in_inc], in[(i0 + 1) * a.in_inc]);
+    }
+    if (q >= NB - 1) {
+        const int64_t f = q - (NB - 1);
+        cf v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int i0 = 2 * (lane + 64 * m);
+            float2 xv;
+            if (m >= E - S) {
+                xv = hop[m - (E - S)];
+            } else {  // hop f + m/S sits in slot (f + m/S) mod NB
+                const int slot = int((f + m / S) % NB);
+                xv = *reinterpret_cast<const float2*>(hist + slot * H + (i0 % H));
+            }
+            v[m].r = dev::sanit(xv.x * wa[i0]);
+            v[m].i = dev::sanit(xv.y * wa[i0 + 1]);
+        }
+        dev::fft_wave<E, false>(v, buf, tw, lane);
+        dev::real_split_hook_merge<E, HAS_GAIN, false>(v, buf, st, sth, a.t.gain, lane);
+        dev::fft_wave<E, true>(v, buf, tw, lane);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int i0 = 2 * (lane + 64 * m);
+            const float o0 = dev::sanit(v[m].r * a.inv_n);
+            const float o1 = dev::sanit(v[m].i * a.inv_n);
+            const int slot = int((f + m / S) % NB);
+            float2* r = reinterpret_cast<float2*>(acc + slot * H + (i0 % H));
+            float2 cur = *r;
+            cur.x = __builtin_fmaf(__builtin_fmaf(o0, ws[i0], 0.0f), a.gain, cur.x);
+            cur.y = __builtin_fmaf(__builtin_fmaf(o1, ws[i0 + 1], 0.0f), a.gain, cur.y);
+            if (m < S) {  // block f is complete: produce(H) and clear its slot
+                const int pos = i0 % H;
+                const int64_t n = f * H + pos;
+                const float d0 = a.t.den[n % a.ring_len], d1 = a.t.den[(n + 1) % a.ring_len];
+                float* o = a.out + c * a.out_ld;
+                o[pos * a.out_inc] = cur.x / d0;
+                o[(pos + 1) * a.out_inc] = cur.y / d1;
+                cur = make_float2(0.f, 0.f);
+            }
+            *r = cur;
+        }
+    }
+    // store the new hop into its slot for later frames
+    const int qslot = int(q % NB);
+#pragma unroll
+    for (int s2 = 0; s2 < S; ++s2)
+        *reinterpret_cast<float2*>(hist + qslot * H + 2 * (lane + 64 * s2)) = hop[s2];
+}
+
 // ------------------------------------------------------------------ dispatch
 template <int E>
 inline size_t lds_bytes_full() {
@@ -620,6 +715,67 @@ static hipError_t fft_dispatch(const Geometry& g, const DevTables& t, const floa
         case 8: return fft_e<8, INV>(a, stream);
         case 16: return fft_e<16, INV>(a, stream);
         case 32: return fft_e<32, INV>(a, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <int E, int S>
+static hipError_t stream_es(const StreamArgs& a, hipStream_t stream) {
+    auto k = a.t.gain ? k_stream_hop<E, S, true> : k_stream_hop<E, S, false>;
+    const size_t lds = Lds<E>::bytes;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned((a.channels + kWaves - 1) / kWaves)), dim3(kBlock), lds,
+                       stream, a);
+    return hipGetLastError();
+}
+
+template <int E>
+static hipError_t stream_e(int s, const StreamArgs& a, hipStream_t stream) {
+    if constexpr (E >= 1) {
+        if (s == 1) return stream_es<E, 1>(a, stream);
+    }
+    if constexpr (E >= 2) {
+        if (s == 2) return stream_es<E, 2>(a, stream);
+    }
+    if constexpr (E >= 4) {
+        if (s == 4) return stream_es<E, 4>(a, stream);
+    }
+    if constexpr (E >= 8) {
+        if (s == 8) return stream_es<E, 8>(a, stream);
+    }
+    if constexpr (E >= 16) {
+        if (s == 16) return stream_es<E, 16>(a, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_stream_hop(const Geometry& g, const DevTables& t, const float* in, int64_t in_ld,
+                             int64_t in_inc, float* out, int64_t out_ld, int64_t out_inc,
+                             float* hist, float* acc, int channels, int64_t q,
+                             hipStream_t stream) {
+    if (!fused_supported(g.n, g.h) || channels <= 0) return hipErrorInvalidValue;
+    StreamArgs a;
+    a.t = t;
+    a.in = in;
+    a.out = out;
+    a.hist = hist;
+    a.acc = acc;
+    a.in_ld = in_ld;
+    a.in_inc = in_inc;
+    a.out_ld = out_ld;
+    a.out_inc = out_inc;
+    a.q = q;
+    a.channels = channels;
+    a.ring_len = g.ring_len;
+    a.inv_n = g.inv_n;
+    a.gain = g.gain;
+    const int s = g.h / 128;
+    switch (e_of(g.n)) {
+        case 2: return stream_e<2>(s, a, stream);
+        case 4: return stream_e<4>(s, a, stream);
+        case 8: return stream_e<8>(s, a, stream);
+        case 16: return stream_e<16>(s, a, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -138,13 +138,19 @@ int crlot_irfft_batched(crlot_plan* plan, const float* d_in_complex, float* d_ou
 
 /* ---------------------------------------------------------------- streaming
  * Low-latency per-hop path (BASELINE config 4): `channels` independent
- * channels, Framer in DROP mode fed H samples per channel per call.  Each call
- * consumes d_hop_in [channels][H] (channel-major) and, once N samples have
- * arrived, emits the next H output samples per channel into d_hop_out
- * [channels][H]; *emitted (host) gets 0 or H. Device rings persist across calls. */
+ * channels, Framer in DROP mode fed H samples per channel per call
+ * (Framer::push of one hop then pop, OLAAccumulator push_frame_AoS + produce(H);
+ * framer.cc:37-117, OLAAccumulator.cc:124-221).  Each call consumes d_hop_in
+ * and, once N samples per channel have arrived, writes the next H output
+ * samples per channel into d_hop_out; *emitted (host) gets 0 or H.  Layout:
+ * channel-major [channels][H] by default, or interleaved [H][channels] (the
+ * reference's interleaved PCM) after crlot_stream_set_layout(st, 1).  Device
+ * state (last N input samples, OLA blocks) persists across calls; the shapes
+ * are those of the fused path (H % 128 == 0, N % H == 0, N <= 2048). */
 int crlot_stream_create(crlot_plan* plan, int32_t channels, crlot_stream** out);
 void crlot_stream_destroy(crlot_stream* st);
 int crlot_stream_reset(crlot_stream* st);
+int crlot_stream_set_layout(crlot_stream* st, int32_t interleaved);
 int crlot_stream_push_hop(crlot_stream* st, const float* d_hop_in, float* d_hop_out,
                           int32_t* emitted, void* stream);
 

@@ -1,0 +1,48 @@
+"""Throughput of the batched round trip for the BASELINE configs on one GPU
+(the headline is bench.py; these are the other shapes): Msamples/s and the
+algorithmic HBM fraction (8 B/sample vs 8 TB/s)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CONFIGS = [
+    ("config2: 256 streams, N=1024 H=256", 256, 480000, 1024, 256, 0),
+    ("headline: 1024 streams, N=1024 H=256", 1024, 480000, 1024, 256, 0),
+    ("config3: 1024 streams, N=4096 H=1024", 1024, 480000, 4096, 1024, 0),
+    ("e2e-harness hop: 1024 streams, N=1024 H=512", 1024, 480000, 1024, 512, 0),
+    ("config4 shape batched: 64 ch, N=512 H=128 DROP", 64, 480000, 512, 128, 1),
+    ("2048/512: 1024 streams", 1024, 480000, 2048, 512, 0),
+]
+
+
+def main():
+    import torch
+    from __graft_entry__ import load_pkg
+    pkg = load_pkg()
+    for name, S, T, N, H, mode in CONFIGS:
+        plan = pkg.Plan(frame_size=N, hop_size=H, boundary_mode=mode)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
+        y = torch.empty((S, plan.output_length(T)), device="cuda")
+        for _ in range(2):
+            plan.roundtrip(x, y)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record()
+        for _ in range(reps):
+            plan.roundtrip(x, y)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        rate = S * T / (ms * 1e-3)
+        print(json.dumps({"config": name, "ms": round(ms, 4), "Msamples_s": round(rate / 1e6, 1),
+                          "hbm_frac_algorithmic": round(8 * rate / 8e12, 4)}), flush=True)
+        del x, y
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -345,3 +345,41 @@ def test_cpp_api_binary(torch_cuda):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
+
+
+# ------------------------------------------------------------------ streaming (config 4)
+@pytest.mark.parametrize("n,h,interleaved,gain", [(512, 128, False, False), (512, 128, True, False),
+                                                   (1024, 256, False, True), (1024, 512, True, False)])
+def test_stream_per_hop_equals_batched_drop(pkg, oracle, torch_cuda, n, h, interleaved, gain):
+    """Per-hop pushes (DROP Framer, produce(H) after every frame) reproduce the
+    batched DROP round trip bit for bit (same float ops), hence the oracle."""
+    torch = torch_cuda
+    C_, hops = 64, 60
+    T = hops * h
+    x = oracle.synth_streams(C_, T, config_id=44)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP)
+    if gain:
+        plan.set_spectral_gain(np.linspace(1.0, 0.25, n // 2 + 1).astype(np.float32))
+    xd = dev(torch, x)
+    y_batch = host(plan.roundtrip(xd))
+    st = pkg.Stream(plan, C_, interleaved=interleaved)
+    outs = []
+    nb = n // h
+    for q in range(hops):
+        hop = xd[:, q * h:(q + 1) * h]
+        hop = hop.t().contiguous() if interleaved else hop.contiguous()
+        out, em = st.push_hop(hop)
+        assert em == (h if q >= nb - 1 else 0)
+        if em:
+            o = host(out)
+            outs.append(o.T if interleaved else o)
+    y_stream = np.concatenate(outs, axis=1)
+    assert y_stream.shape == y_batch.shape
+    assert np.array_equal(bits(y_stream), bits(y_batch))
+    if not gain:
+        ref = oracle.roundtrip_batch(x[:4], n, h, mode=oracle.DROP)
+        for s in range(4):
+            assert_close(y_stream[s], ref[s], 0.5, f"stream ch {s}")
+    st.reset()
+    out, em = st.push_hop(xd[:, :h].t().contiguous() if interleaved else xd[:, :h].contiguous())
+    assert em == (h if nb == 1 else 0)
