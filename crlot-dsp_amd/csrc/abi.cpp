@@ -276,7 +276,9 @@ int64_t crlot_output_length(const crlot_plan* p, int64_t T) {
 static bool use_fused(const crlot_plan* p, const float* x, const float* y, int64_t ld_x,
                       int64_t ld_y, int32_t n_streams, int64_t T, int64_t out_len) {
     const int64_t lim = int64_t(1) << 29;
-    return crlot::fused_supported(p->geo.n, p->geo.h) && p->geo.ring_len % p->geo.h == 0 &&
+    return (crlot::fused_supported(p->geo.n, p->geo.h) ||
+            crlot::fused_wg_supported(p->geo.n, p->geo.h)) &&
+           p->geo.ring_len % p->geo.h == 0 &&
            aligned8(x) && aligned8(y) && ld_x % 2 == 0 && ld_y % 2 == 0 && T < lim &&
            out_len + 2 * p->geo.n < lim && int64_t(n_streams) * (T / p->geo.h + 1) < lim;
 }
@@ -307,7 +309,9 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
     const crlot::DevTables t = tables(p);
     hipError_t e;
     if (use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len)) {
-        e = crlot::launch_fused(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s);
+        e = !crlot::fused_wg_supported(p->geo.n, p->geo.h)
+                ? crlot::launch_fused(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s)
+                : crlot::launch_fused_wg(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s);
         if (e != hipSuccess) return hip_fail(e, "fused kernel launch");
         return CRLOT_OK;
     }

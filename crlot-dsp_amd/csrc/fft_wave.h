@@ -275,6 +275,83 @@ __device__ __forceinline__ void fft_wave_reg(cf (&v)[E], cf* buf, const TwChain<
     fft_passes_reg<E, 1, INV>(v, buf, c, lane);
 }
 
+// ------------------------------------------------------------- workgroup FFT
+// The same Stockham schedule spread over L = 64 * W lanes of one workgroup
+// (lane t owns z[t + L m], m < E), for frames too large for one wave's
+// registers (N = 4096 at E = 8, L = 256).  All twiddles live in registers
+// (loaded once per kernel; they do not depend on the frame), exchanges go
+// through LDS with ONE workgroup barrier each: consecutive exchanges alternate
+// between two buffers, so a buffer is rewritten only after the next exchange's
+// barrier, which every wave reaches after finishing its reads of it.  The
+// per-wave XOR swizzles above stay bank-conflict free at L = 256
+// (tools/swizzle_search_wg.py).
+template <int E, int R, int NS, int L, int TOFF>
+__device__ __forceinline__ void load_pass_tw_wg(PassTw<E, R, NS>& t, const cf* twp, int lane) {
+#pragma unroll
+    for (int b = 0; b < E / R; ++b)
+#pragma unroll
+        for (int r = 1; r < R; ++r) t.w[b][r - 1] = twp[TOFF + (r - 1) * NS + (lane + L * b) % NS];
+}
+
+template <int E, int L, int NS, bool END = (NS >= L * E)>
+struct TwChainWg {
+    static constexpr int R = radix_for(L * E / NS, E);
+    PassTw<E, R, NS> here;
+    TwChainWg<E, L, NS * R> next;
+};
+template <int E, int L, int NS>
+struct TwChainWg<E, L, NS, true> {};
+
+template <int E, int L, int NS, int TOFF>
+__device__ __forceinline__ void load_chain_wg(TwChainWg<E, L, NS>& c, const cf* twp, int lane) {
+    if constexpr (NS < L * E) {
+        constexpr int R = radix_for(L * E / NS, E);
+        if constexpr (NS > 1) load_pass_tw_wg<E, R, NS, L, TOFF>(c.here, twp, lane);
+        load_chain_wg<E, L, NS * R, TOFF + (NS > 1 ? (R - 1) * NS : 0)>(c.next, twp, lane);
+    }
+}
+
+template <int E, int R, int NS, int L>
+__device__ __forceinline__ void stockham_exchange_wg(cf (&v)[E], cf* buf, int lane) {
+    constexpr int B = E / R;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int j = lane + L * b;
+        const int base = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+        for (int r = 0; r < R; ++r) buf[swz<NS, R>(base + r * NS)] = v[b + r * B];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < E; ++m) v[m] = buf[swz<NS, R>(lane + L * m)];
+}
+
+// XI = index of the next exchange; it uses buffer XI & 1.
+template <int E, int L, int NS, int XI, bool INV>
+__device__ __forceinline__ void fft_passes_wg(cf (&v)[E], cf* buf0, cf* buf1,
+                                              const TwChainWg<E, L, NS>& c, int lane) {
+    constexpr int P = L * E;
+    if constexpr (NS < P) {
+        constexpr int R = radix_for(P / NS, E);
+        stockham_compute<E, R, NS, INV>(v, c.here);
+        if constexpr (NS * R < P) {
+            stockham_exchange_wg<E, R, NS, L>(v, (XI & 1) ? buf1 : buf0, lane);
+            fft_passes_wg<E, L, NS * R, XI + 1, INV>(v, buf0, buf1, c.next, lane);
+        }
+    }
+}
+
+// Number of exchanges of one P-point FFT.
+__host__ __device__ constexpr int fft_exchanges(int p, int e) {
+    int ns = 1, n = 0;
+    while (ns < p) {
+        const int r = radix_for(p / ns, e);
+        if (ns * r < p) ++n;
+        ns *= r;
+    }
+    return n;
+}
+
 // ------------------------------------------------------------- sanitize
 // KissFftPlan sanitize (kissfft_adapter.cc:102-110, 156-163):
 // NaN/Inf -> 0, |v| < 1e-30 -> 0.
@@ -332,6 +409,42 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
         }
         // kiss_fftri merge: Z'[k] = (X[k] + conj X[P-k]) + (X[k] - conj X[P-k]) conj(st)
         const cf w = st[k];
+        const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+        const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+        v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
+        v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
+    }
+}
+
+// Workgroup form of the split/hook/merge: st[m] = st(k) for k = lane + L m in
+// registers (sth = 0.5 st is formed on the fly, exact), the partner Z[P-k]
+// exchanged through `buf` with one barrier.  Same arithmetic as above.
+template <int E, int L, bool HAS_GAIN>
+__device__ __forceinline__ void real_split_hook_merge_wg(cf (&v)[E], cf* buf, const cf (&st)[E],
+                                                         const float* gain, int lane) {
+    constexpr int P = L * E;
+#pragma unroll
+    for (int m = 0; m < E; ++m) buf[lane + L * m] = v[m];
+    __syncthreads();
+    cf zp[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) zp[m] = buf[(P - (lane + L * m)) & (P - 1)];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + L * m;
+        const cf zk = v[m];
+        const cf fpnk = conj(zp[m]);
+        const cf f1 = cadd(zk, fpnk);
+        const cf f2 = csub(zk, fpnk);
+        const cf w = st[m];
+        const cf t = cmul(f2, cf{w.r * 0.5f, w.i * 0.5f});
+        cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
+        cf xpk = {__builtin_fmaf(f1.r, 0.5f, -t.r), __builtin_fmaf(f1.i, -0.5f, t.i)};
+        if constexpr (HAS_GAIN) {
+            const float gk = gain[k], gpk = gain[P - k];
+            xk = {xk.r * gk, xk.i * gk};
+            xpk = {xpk.r * gpk, xpk.i * gpk};
+        }
         const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
         const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
         v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));

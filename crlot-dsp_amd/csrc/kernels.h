@@ -38,6 +38,13 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
                         int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
                         int64_t out_len, hipStream_t stream);
 
+// Fused workgroup-walker path for frames too large for one wave: N = 4096
+// (256 lanes per frame), H % 512 == 0, N % H == 0; same preconditions otherwise.
+bool fused_wg_supported(int n, int h);
+hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x, float* y,
+                           int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                           int64_t out_len, hipStream_t stream);
+
 // Staged general path.
 bool synth_supported(int n);
 hipError_t launch_synth_frames(const Geometry& g, const DevTables& t, const float* x,

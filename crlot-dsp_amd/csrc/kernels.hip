@@ -21,6 +21,7 @@
 // acc / max(norm, eps) (kernels.cc:30-36).  Built with -ffp-contract=off and
 // the default correctly-rounded f32 division; subnormals are preserved.
 #include <cmath>
+#include <cstdlib>
 
 #include "fft_wave.h"
 #include "kernels.h"
@@ -82,6 +83,20 @@ struct FusedArgs {
 // Hop loads: lane owns complex samples z[lane + 64 m] = (x[2i], x[2i+1]), i = lane + 64 m.
 // `full` (wave-uniform) = the whole frame lies inside the stream: one dwordx2 per
 // pair; otherwise two dword loads whose out-of-range halves read 0 (ZERO_PAD).
+template <int M0, int CNT, int E, int L>
+__device__ __forceinline__ void load_pairs_l(float2 (&dst)[E], __amdgpu_buffer_rsrc_t rx, int lane,
+                                             int frame_byte, bool full) {
+    if (full) {
+#pragma unroll
+        for (int m = M0; m < M0 + CNT; ++m) dst[m] = dev::bload2(rx, lane * 8 + m * 8 * L, frame_byte);
+    } else {
+#pragma unroll
+        for (int m = M0; m < M0 + CNT; ++m)
+            dst[m] = make_float2(dev::bload1(rx, lane * 8 + m * 8 * L, frame_byte),
+                                 dev::bload1(rx, lane * 8 + m * 8 * L + 4, frame_byte));
+    }
+}
+
 template <int M0, int CNT, int E>
 __device__ __forceinline__ void load_pairs(float2 (&dst)[E], __amdgpu_buffer_rsrc_t rx, int lane,
                                            int frame_byte, bool full) {
@@ -209,6 +224,98 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
                 dev::bstore2(make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y), ry,
                              lane * 8 + q * 512, k * H * 4);
 #endif
+        }
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < S; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[NB - 1][q] = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int m = 0; m < E - S; ++m) xin[m] = xin[m + S];
+#pragma unroll
+        for (int m = E - S; m < E; ++m) xin[m] = nxt[m];
+    }
+}
+
+// ------------------------------------------------------------------ fused, workgroup walker
+// K_fused_wg k_stft_ola_wg<L,S,NB>: the fused walk of K_fused for frames too big
+// for one wave (N = 16 L, E = 8): a workgroup of L lanes owns a run of frames
+// of one stream, lane t holding z[t + L m].  The frame-invariant tables
+// (analysis/synthesis window, super-twiddles, pass twiddles) sit in registers,
+// so LDS holds only the three exchange buffers (A/B alternate through the FFT
+// passes, C for the split); each exchange costs one s_barrier.
+template <int L, int S, int NB, bool HAS_GAIN>
+__global__ __launch_bounds__(L) void k_stft_ola_wg(const FusedArgs a) {
+    constexpr int E = 8, P = L * E, N = 2 * P, H = 2 * L * S;
+    static_assert(NB * S == E, "N = NB * H");
+    constexpr int NX = dev::fft_exchanges(P, E);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* bufA = reinterpret_cast<cf*>(smem);
+    cf* bufB = bufA + P;
+    cf* bufC = bufB + P;
+
+    const int t = threadIdx.x;
+    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1));
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
+    const float g = a.gain;
+
+    dev::TwChainWg<E, L, 1> twc;
+    dev::load_chain_wg<E, L, 1, 0>(twc, reinterpret_cast<const cf*>(a.t.tw), t);
+    float2 wa[E], ws[E];
+    cf st[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = *reinterpret_cast<const float2*>(a.t.wa + 2 * (t + L * m));
+        ws[m] = *reinterpret_cast<const float2*>(a.t.ws + 2 * (t + L * m));
+        st[m] = reinterpret_cast<const cf*>(a.t.st)[t + L * m];
+    }
+
+    float2 xin[E];
+    load_pairs_l<0, E, E, L>(xin, rx, t, fs * H * 4, fs * H + N <= a.T);
+    float2 acc[NB][S];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[j][q] = make_float2(0.f, 0.f);
+
+    for (int k = fs; k < f1; ++k) {
+        float2 nxt[E];
+        if (k + 1 < f1) load_pairs_l<E - S, S, E, L>(nxt, rx, t, (k + 1) * H * 4, (k + 1) * H + N <= a.T);
+        float2 dn[S];
+        if (k >= f0) {
+#pragma unroll
+            for (int q = 0; q < S; ++q)
+                dn[q] = dev::bload2(rd, t * 8 + q * 8 * L, (k % a.ring_blocks) * H * 4);
+        }
+        cf v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            v[m].r = dev::sanit(xin[m].x * wa[m].x);
+            v[m].i = dev::sanit(xin[m].y * wa[m].y);
+        }
+        dev::fft_passes_wg<E, L, 1, 0, false>(v, bufA, bufB, twc, t);
+        dev::real_split_hook_merge_wg<E, L, HAS_GAIN>(v, bufC, st, a.t.gain, t);
+        dev::fft_passes_wg<E, L, 1, (NX & 1), true>(v, bufA, bufB, twc, t);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float o0 = dev::sanit(v[m].r * a.inv_n);
+            const float o1 = dev::sanit(v[m].i * a.inv_n);
+            float2& r = acc[m / S][m % S];
+            r.x = __builtin_fmaf(__builtin_fmaf(o0, ws[m].x, 0.0f), g, r.x);
+            r.y = __builtin_fmaf(__builtin_fmaf(o1, ws[m].y, 0.0f), g, r.y);
+        }
+        if (k >= f0) {
+#pragma unroll
+            for (int q = 0; q < S; ++q)
+                dev::bstore2(make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y), ry,
+                             t * 8 + q * 8 * L, k * H * 4);
         }
 #pragma unroll
         for (int j = 0; j < NB - 1; ++j)
@@ -550,6 +657,16 @@ hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) 
     return hipErrorInvalidValue;
 }
 
+// frames per workgroup walk (halo NB-1 frames recomputed); CRLOT_WG_CHUNK overrides
+int wg_chunk_target() {
+    static const int v = [] {
+        const char* e = std::getenv("CRLOT_WG_CHUNK");
+        const int x = e ? std::atoi(e) : 0;
+        return x > 0 ? x : 128;
+    }();
+    return v;
+}
+
 }  // namespace
 
 std::vector<float> build_pass_twiddles(int n) {
@@ -609,6 +726,73 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
         case 4: return fused_e<4>(s, a, grid, stream);
         case 8: return fused_e<8>(s, a, grid, stream);
         case 16: return fused_e<16>(s, a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// Workgroup walker: N = 16 L (E = 8), H = 2 L S.
+template <int L, int S>
+static hipError_t fused_wg_ls(const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    constexpr int NB = 8 / S;
+    auto k = a.t.gain ? k_stft_ola_wg<L, S, NB, true> : k_stft_ola_wg<L, S, NB, false>;
+    const size_t lds = sizeof(cf) * 3 * 8 * L;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(L), lds, stream, a);
+    return hipGetLastError();
+}
+
+template <int L>
+static hipError_t fused_wg_l(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    switch (s) {
+        case 1: return fused_wg_ls<L, 1>(a, grid, stream);
+        case 2: return fused_wg_ls<L, 2>(a, grid, stream);
+        case 4: return fused_wg_ls<L, 4>(a, grid, stream);
+        case 8: return fused_wg_ls<L, 8>(a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// N = 4096 always; N = 2048 (L = 128) only when CRLOT_WG_2048=1 (A/B against the
+// per-wave E = 16 kernel, which is the default there).
+bool fused_wg_supported(int n, int h) {
+    static const bool wg2048 = [] {
+        const char* e = std::getenv("CRLOT_WG_2048");
+        return e && e[0] == '1';
+    }();
+    if (n != 4096 && !(n == 2048 && wg2048)) return false;
+    const int L = n / 16;
+    if (h % (2 * L) != 0 || n % h != 0) return false;
+    const int s = h / (2 * L);
+    return s == 1 || s == 2 || s == 4 || s == 8;
+}
+
+hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x, float* y,
+                           int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                           int64_t out_len, hipStream_t stream) {
+    if (!fused_wg_supported(g.n, g.h) || F <= 0 || n_streams <= 0) return hipErrorInvalidValue;
+    FusedArgs a;
+    a.t = t;
+    a.x = x;
+    a.y = y;
+    a.ld_x = ld_x;
+    a.ld_y = ld_y;
+    a.T = int(T);
+    a.out_len = int(out_len);
+    a.n_streams = n_streams;
+    a.F = int(F);
+    const int target = wg_chunk_target();
+    a.n_chunks = int((F + target - 1) / target);
+    a.M = int((F + a.n_chunks - 1) / a.n_chunks);
+    a.n_chunks = int((F + a.M - 1) / a.M);
+    a.ring_blocks = g.ring_len / g.h;
+    a.inv_n = g.inv_n;
+    a.gain = g.gain;
+    const int64_t grid = int64_t(n_streams) * a.n_chunks;
+    const int L = g.n / 16, s = g.h / (2 * L);
+    switch (L) {
+        case 128: return fused_wg_l<128>(s, a, grid, stream);
+        case 256: return fused_wg_l<256>(s, a, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -22,7 +22,10 @@ def main():
     import torch
     from __graft_entry__ import load_pkg
     pkg = load_pkg()
+    only = os.environ.get("BC_ONLY")
     for name, S, T, N, H, mode in CONFIGS:
+        if only and only not in name:
+            continue
         plan = pkg.Plan(frame_size=N, hop_size=H, boundary_mode=mode)
         g = torch.Generator(device="cuda").manual_seed(1)
         x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5

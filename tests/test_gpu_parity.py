@@ -82,7 +82,9 @@ CASES = [
     # N, H, mode, S, T
     (1024, 256, 0, 3, 48000),        # BASELINE config 2 shape (fused)
     (1024, 256, 0, 2, 480000),       # full-length streams, 15 chunks per stream
-    (4096, 1024, 0, 2, 40000),       # config 3 shape (staged, E=32)
+    (4096, 1024, 0, 2, 40000),       # config 3 shape (fused workgroup walker, L=256)
+    (4096, 512, 1, 2, 30000),        # workgroup walker S=1 NB=8, DROP
+    (4096, 2048, 0, 2, 30001),       # workgroup walker S=4, odd T
     (512, 128, 1, 3, 24000),         # config 4 shape, DROP framing (fused)
     (1024, 512, 0, 2, 30001),        # e2e harness hop, odd T (fused)
     (2048, 512, 0, 2, 20000),        # fused E=16
@@ -108,7 +110,8 @@ def test_roundtrip_vs_oracle(pkg, oracle, torch_cuda, n, h, mode, S, T):
         assert_close(y[s], ref[s], xmax, f"N={n} H={h} stream {s}")
 
 
-@pytest.mark.parametrize("n,h", [(1024, 256), (512, 128), (2048, 512), (1024, 512)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (512, 128), (2048, 512), (1024, 512),
+                                 (4096, 1024), (4096, 512), (4096, 4096)])
 def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
     """The fused kernel and the staged synth+gather pair run the same float ops:
     outputs must agree bit for bit (this also covers the fused chunk seams)."""
