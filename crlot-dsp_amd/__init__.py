@@ -27,6 +27,8 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "crlot_dsp.h")
 HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS = range(5)
 NORM_NONE, NORM_SUM_TO_ONE, NORM_L2, NORM_OLA_UNITY_GAIN, NORM_OLA_SUM_WSQ = range(5)
 ZERO_PAD, DROP = 0, 1
+# dsp::fft::FftDomain
+FFT_REAL, FFT_COMPLEX = 0, 1
 
 OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4, -5
 
@@ -47,6 +49,11 @@ class PlanDesc(C.Structure):
         ("ring_len", C.c_int32),
         ("device", C.c_int32),
     ]
+
+
+class FftDesc(C.Structure):
+    """crlot_fft_desc (include/crlot_dsp.h)."""
+    _fields_ = [("domain", C.c_int32), ("nfft", C.c_int32), ("device", C.c_int32)]
 
 
 _lib = None
@@ -79,6 +86,13 @@ def lib():
         "crlot_ola_gather": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
         "crlot_rfft_batched": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
         "crlot_irfft_batched": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_fft_plan_create": ([C.POINTER(FftDesc), C.POINTER(vp)], C.c_int),
+        "crlot_fft_plan_destroy": ([vp], None),
+        "crlot_fft_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "crlot_fft_forward": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_fft_inverse": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_fft_forward_complex": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_fft_inverse_complex": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
         "crlot_stream_create": ([vp, i32, C.POINTER(vp)], C.c_int),
         "crlot_stream_destroy": ([vp], None),
         "crlot_stream_reset": ([vp], C.c_int),
@@ -303,6 +317,71 @@ class Plan:
                                          1, n, 1, _stream_handle(X)),
                "crlot_irfft_batched")
         return out
+
+
+class FftPlan:
+    """dsp::fft::IFftPlan on the device (fft_api.h:26-48), both domains.
+
+    Batched over the leading dim of torch CUDA tensors; `forward`/`inverse` for a
+    Real plan, `forward_complex`/`inverse_complex` for a Complex plan (the other
+    domain's calls raise RuntimeError with the reference's message)."""
+
+    def __init__(self, nfft: int, domain: int = FFT_REAL, device: int = -1):
+        self.nfft, self.domain = nfft, domain
+        self._h = None
+        h = C.c_void_p()
+        _check(lib().crlot_fft_plan_create(C.byref(FftDesc(domain, nfft, device)), C.byref(h)),
+               "crlot_fft_plan_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib().crlot_fft_plan_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def size(self) -> int:
+        return self.nfft
+
+    def forward(self, x):
+        """(B, nfft) real -> (B, nfft/2+1) complex (sanitized input)."""
+        torch = _torch()
+        B, n = x.shape
+        bins = n // 2 + 1
+        out = torch.empty((B, bins), dtype=torch.complex64, device=x.device)
+        _check(lib().crlot_fft_forward(self._h, x.data_ptr(), out.data_ptr(), B, _ld(x, 0, n),
+                                       x.stride(1), 2 * bins, 1, _stream_handle(x)),
+               "forward")
+        return out
+
+    def inverse(self, X):
+        """(B, nfft/2+1) complex -> (B, nfft) real (*1/nfft, sanitize)."""
+        torch = _torch()
+        X = X.contiguous()
+        B, bins = X.shape
+        out = torch.empty((B, self.nfft), dtype=torch.float32, device=X.device)
+        _check(lib().crlot_fft_inverse(self._h, X.data_ptr(), out.data_ptr(), B, 2 * bins, 1,
+                                       self.nfft, 1, _stream_handle(X)),
+               "inverse")
+        return out
+
+    def _cplx(self, fn, name, Z):
+        torch = _torch()
+        B, n = Z.shape
+        out = torch.empty((B, n), dtype=torch.complex64, device=Z.device)
+        ld = 2 * Z.stride(0) if B > 1 else 2 * n
+        _check(fn(self._h, Z.data_ptr(), out.data_ptr(), B, ld, Z.stride(1), 2 * n, 1,
+                  _stream_handle(Z)), name)
+        return out
+
+    def forward_complex(self, Z):
+        """(B, nfft) complex64 -> (B, nfft) complex64, unnormalised."""
+        return self._cplx(lib().crlot_fft_forward_complex, "forward_complex", Z)
+
+    def inverse_complex(self, Z):
+        """(B, nfft) complex64 -> (B, nfft) complex64, *1/nfft, sanitize."""
+        return self._cplx(lib().crlot_fft_inverse_complex, "inverse_complex", Z)
 
 
 class Stream:

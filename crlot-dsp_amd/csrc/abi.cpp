@@ -385,6 +385,111 @@ int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t 
     return CRLOT_OK;
 }
 
+// ------------------------------------------------------------------ FFT plans
+// A real plan of nfft points owns an STFT plan of frame nfft; a complex plan of
+// nfft points owns one of frame 2*nfft, whose pass twiddles are those of an
+// nfft-point complex FFT.  Only the FFT tables of the inner plan are used.
+struct crlot_fft_plan {
+    int domain = CRLOT_FFT_REAL;
+    int nfft = 0;
+    crlot_plan* inner = nullptr;
+};
+
+int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
+    if (!d || !out) return fail(CRLOT_EINVAL, "null argument");
+    *out = nullptr;
+    // KissFftPlan ctor (kissfft_adapter.cc:13-63)
+    if (d->domain != CRLOT_FFT_REAL && d->domain != CRLOT_FFT_COMPLEX)
+        return fail(CRLOT_ERUNTIME, "Unsupported FFT domain");
+    if (d->domain == CRLOT_FFT_REAL && d->nfft % 2 != 0)
+        return fail(CRLOT_ERUNTIME, "FFT size must be even for real FFT");
+    const bool real = d->domain == CRLOT_FFT_REAL;
+    const int lo = real ? 256 : 128, hi = real ? 4096 : 2048;
+    if (!is_pow2(d->nfft) || d->nfft < lo || d->nfft > hi)
+        return fail(CRLOT_EUNSUPPORTED, std::string(real ? "real" : "complex") +
+                                            " FFT sizes on the GPU path are powers of two " +
+                                            std::to_string(lo) + ".." + std::to_string(hi) +
+                                            ", got " + std::to_string(d->nfft));
+    crlot_plan_desc pd{};
+    pd.frame_size = real ? d->nfft : 2 * d->nfft;
+    pd.hop_size = pd.frame_size / 4;
+    pd.window_type = CRLOT_WIN_RECT;
+    pd.device = d->device;
+    crlot_plan* inner = nullptr;
+    const int rc = crlot_plan_create(&pd, &inner);
+    if (rc != CRLOT_OK) return rc;
+    crlot_fft_plan* p = new crlot_fft_plan();
+    p->domain = d->domain;
+    p->nfft = d->nfft;
+    p->inner = inner;
+    *out = p;
+    return CRLOT_OK;
+}
+
+void crlot_fft_plan_destroy(crlot_fft_plan* p) {
+    if (!p) return;
+    crlot_plan_destroy(p->inner);
+    delete p;
+}
+
+int crlot_fft_plan_info(const crlot_fft_plan* p, int32_t* domain, int32_t* nfft) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (domain) *domain = p->domain;
+    if (nfft) *nfft = p->nfft;
+    return CRLOT_OK;
+}
+
+static int fft_domain_check(const crlot_fft_plan* p, int want) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (p->domain != want)
+        return fail(CRLOT_ERUNTIME, want == CRLOT_FFT_REAL
+                                        ? "Real FFT not supported for Complex domain plan"
+                                        : "Complex FFT not supported for Real domain plan");
+    return CRLOT_OK;
+}
+
+int crlot_fft_forward(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
+                      int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, void* stream) {
+    const int rc = fft_domain_check(p, CRLOT_FFT_REAL);
+    if (rc != CRLOT_OK) return rc;
+    return crlot_rfft_batched(p->inner, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+}
+
+int crlot_fft_inverse(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
+                      int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, void* stream) {
+    const int rc = fft_domain_check(p, CRLOT_FFT_REAL);
+    if (rc != CRLOT_OK) return rc;
+    return crlot_irfft_batched(p->inner, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+}
+
+static int cfft_common(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
+                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                       bool inverse, void* stream) {
+    int rc = fft_domain_check(p, CRLOT_FFT_COMPLEX);
+    if (rc != CRLOT_OK) return rc;
+    if (batch < 0 || inc_in < 1 || inc_out < 1) return fail(CRLOT_EINVAL, "bad batch/stride");
+    if (batch == 0) return CRLOT_OK;
+    if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
+    const crlot_plan* q = p->inner;
+    DeviceGuard g(q->device);
+    hipError_t e = crlot::launch_cfft(q->geo, tables(q), d_in, d_out, batch, ld_in, inc_in, ld_out,
+                                      inc_out, inverse, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "cfft kernel launch");
+    return CRLOT_OK;
+}
+
+int crlot_fft_forward_complex(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
+                              int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                              void* stream) {
+    return cfft_common(p, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, false, stream);
+}
+
+int crlot_fft_inverse_complex(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
+                              int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
+                              void* stream) {
+    return cfft_common(p, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, true, stream);
+}
+
 // ------------------------------------------------------------------ streaming
 struct crlot_stream {
     crlot_plan* plan = nullptr;

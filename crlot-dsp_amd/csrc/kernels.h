@@ -66,5 +66,9 @@ hipError_t launch_rfft(const Geometry& g, const DevTables& t, const float* in, f
 hipError_t launch_irfft(const Geometry& g, const DevTables& t, const float* in, float* out,
                         int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
                         int64_t inc_out, hipStream_t stream);
+// Batched complex FFT of P = g.n / 2 points (forward: raw DFT; inverse: *1/P, sanitize).
+hipError_t launch_cfft(const Geometry& g, const DevTables& t, const float* in, float* out, int batch,
+                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, bool inverse,
+                       hipStream_t stream);
 
 }  // namespace crlot

@@ -503,6 +503,46 @@ __global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ complex FFT
+// Batched IFftPlan::forward_complex / inverse_complex (kissfft_adapter.cc:171-246)
+// of P = 64 E points: forward is the plain unnormalised DFT (no sanitize);
+// inverse is the +i DFT, then *1/P and sanitize.  Element i of batch b is the
+// float pair at [b*ld + 2*i*inc].
+template <int E, bool INV>
+__global__ __launch_bounds__(kBlock) void k_cfft(const FftArgs a) {
+    constexpr int P = 64 * E;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    cf* sth = st + P;
+    cf* bufs = sth + P;
+    load_tables<E>(a.t, tw, st, sth, nullptr, nullptr, false);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    const int64_t b = int64_t(blockIdx.x) * kWaves + wave;
+    if (b >= a.batch) return;
+    const float* in = a.in + b * a.ld_in;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int64_t i = lane + 64 * m;
+        v[m] = {in[2 * i * a.inc_in], in[2 * i * a.inc_in + 1]};
+    }
+    dev::fft_wave<E, INV>(v, buf, tw, lane);
+    float* out = a.out + b * a.ld_out;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int64_t i = lane + 64 * m;
+        if constexpr (INV) {
+            out[2 * i * a.inc_out] = dev::sanit(v[m].r * a.inv_n);
+            out[2 * i * a.inc_out + 1] = dev::sanit(v[m].i * a.inv_n);
+        } else {
+            out[2 * i * a.inc_out] = v[m].r;
+            out[2 * i * a.inc_out + 1] = v[m].i;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ streaming
 // One hop of the low-latency path (BASELINE config 4): per channel, the last
 // NB = N/H hops live in `hist` (slot q mod NB holds hop q) and the OLA
@@ -867,18 +907,18 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
     return hipGetLastError();
 }
 
-template <int E, bool INV>
+template <int E, bool INV, bool CPLX = false>
 static hipError_t fft_e(const FftArgs& a, hipStream_t stream) {
     const size_t lds = lds_bytes_fft<E>();
     const int64_t grid = (int64_t(a.batch) + kWaves - 1) / kWaves;
-    auto k = INV ? k_irfft<E> : k_rfft<E>;
+    auto k = CPLX ? k_cfft<E, INV> : INV ? k_irfft<E> : k_rfft<E>;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
     return hipGetLastError();
 }
 
-template <bool INV>
+template <bool INV, bool CPLX = false>
 static hipError_t fft_dispatch(const Geometry& g, const DevTables& t, const float* in, float* out,
                                int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
                                int64_t inc_out, hipStream_t stream) {
@@ -892,13 +932,13 @@ static hipError_t fft_dispatch(const Geometry& g, const DevTables& t, const floa
     a.ld_out = ld_out;
     a.inc_out = inc_out;
     a.batch = batch;
-    a.inv_n = g.inv_n;
+    a.inv_n = CPLX ? 2.0f * g.inv_n : g.inv_n;  // 1/P for a P = N/2 point complex plan
     switch (e_of(g.n)) {
-        case 2: return fft_e<2, INV>(a, stream);
-        case 4: return fft_e<4, INV>(a, stream);
-        case 8: return fft_e<8, INV>(a, stream);
-        case 16: return fft_e<16, INV>(a, stream);
-        case 32: return fft_e<32, INV>(a, stream);
+        case 2: return fft_e<2, INV, CPLX>(a, stream);
+        case 4: return fft_e<4, INV, CPLX>(a, stream);
+        case 8: return fft_e<8, INV, CPLX>(a, stream);
+        case 16: return fft_e<16, INV, CPLX>(a, stream);
+        case 32: return fft_e<32, INV, CPLX>(a, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -968,6 +1008,13 @@ hipError_t launch_rfft(const Geometry& g, const DevTables& t, const float* in, f
                        int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
                        hipStream_t stream) {
     return fft_dispatch<false>(g, t, in, out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+}
+
+hipError_t launch_cfft(const Geometry& g, const DevTables& t, const float* in, float* out, int batch,
+                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, bool inverse,
+                       hipStream_t stream) {
+    return inverse ? fft_dispatch<true, true>(g, t, in, out, batch, ld_in, inc_in, ld_out, inc_out, stream)
+                   : fft_dispatch<false, true>(g, t, in, out, batch, ld_in, inc_in, ld_out, inc_out, stream);
 }
 
 hipError_t launch_irfft(const Geometry& g, const DevTables& t, const float* in, float* out,

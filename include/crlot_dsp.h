@@ -136,6 +136,41 @@ int crlot_irfft_batched(crlot_plan* plan, const float* d_in_complex, float* d_ou
                         int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out,
                         void* stream);
 
+/* ---------------------------------------------------------------- FFT plans
+ * dsp::fft::MakeFftPlan / IFftPlan (fft_api.h:16-51; kissfft_adapter.cc:11-269)
+ * as a device object of its own, both domains.  Semantics per entry point:
+ *   forward          real, sanitized input -> nfft/2+1 bins   (adapter :83-122)
+ *   inverse          nfft/2+1 bins -> real, *1/nfft, sanitize  (adapter :124-168)
+ *   forward_complex  complex -> complex, unnormalised, no sanitize (adapter :171-201)
+ *   inverse_complex  complex -> complex, *1/nfft, sanitize     (adapter :204-246)
+ * Calling the other domain's entry is CRLOT_ERUNTIME with the reference's
+ * message.  Element i of batch b is at [b*ld + i*inc] (ld in floats, inc in
+ * elements: floats for real data, float pairs for complex).  Sizes on this
+ * device path: real nfft = 256..4096, complex nfft = 128..2048, powers of two
+ * (others: CRLOT_EUNSUPPORTED).  No batch ceiling on the device path;
+ * MakeFftPlan's 1..16 rule is applied by the C++ layer (crlot_dsp.hpp). */
+#define CRLOT_FFT_REAL 0
+#define CRLOT_FFT_COMPLEX 1
+typedef struct crlot_fft_plan crlot_fft_plan;
+typedef struct crlot_fft_desc {
+    int32_t domain; /* CRLOT_FFT_REAL / CRLOT_FFT_COMPLEX (FftPlanDesc::domain) */
+    int32_t nfft;   /* FftPlanDesc::nfft */
+    int32_t device; /* HIP device ordinal, -1 = current */
+} crlot_fft_desc;
+int crlot_fft_plan_create(const crlot_fft_desc* desc, crlot_fft_plan** out);
+void crlot_fft_plan_destroy(crlot_fft_plan* plan);
+int crlot_fft_plan_info(const crlot_fft_plan* plan, int32_t* domain, int32_t* nfft);
+int crlot_fft_forward(crlot_fft_plan* plan, const float* d_in, float* d_out_complex, int32_t batch,
+                      int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, void* stream);
+int crlot_fft_inverse(crlot_fft_plan* plan, const float* d_in_complex, float* d_out, int32_t batch,
+                      int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, void* stream);
+int crlot_fft_forward_complex(crlot_fft_plan* plan, const float* d_in_complex, float* d_out_complex,
+                              int32_t batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                              int64_t inc_out, void* stream);
+int crlot_fft_inverse_complex(crlot_fft_plan* plan, const float* d_in_complex, float* d_out_complex,
+                              int32_t batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                              int64_t inc_out, void* stream);
+
 /* ---------------------------------------------------------------- streaming
  * Low-latency per-hop path (BASELINE config 4): `channels` independent
  * channels, Framer in DROP mode fed H samples per channel per call

@@ -4,6 +4,7 @@
 //   crlot::dsp::WindowLUT          <- dsp::WindowLUT        (WindowLUT.h:80-199)
 //   crlot::dsp::fft::FftPlanDesc   <- dsp::fft::FftPlanDesc (fft_api.h:16-23)
 //   crlot::dsp::fft::IFftPlan      <- dsp::fft::IFftPlan    (fft_api.h:26-48)
+//   crlot::dsp::fft::HipFftPlan    <- KissFftPlan (kissfft_adapter.cc:11-264), Real + Complex
 //   crlot::dsp::fft::MakeFftPlan   <- dsp::fft::MakeFftPlan (fft_api.h:51), HIP-backed
 //   crlot::StftEngine              <- the Framer -> window -> FFT -> iFFT -> OLA loop
 //                                     of bench/e2e_benchmark.cc:138-186, batched
@@ -183,79 +184,125 @@ struct FftPlanDesc {
     int stride_out;
 };
 
+// dsp::fft::IFftPlan (fft_api.h:26-48), same virtuals and defaults.
 class IFftPlan {
    public:
     virtual ~IFftPlan() = default;
     virtual void forward(const float* in, std::complex<float>* out, int batch = 1) = 0;
     virtual void inverse(const std::complex<float>* in, float* out, int batch = 1) = 0;
+    virtual void forward_complex(const std::complex<float>* in, std::complex<float>* out,
+                                 int batch = 1) = 0;
+    virtual void inverse_complex(const std::complex<float>* in, std::complex<float>* out,
+                                 int batch = 1) = 0;
     virtual FftDomain domain() const = 0;
     virtual int size() const = 0;
     virtual bool supports_batch() const { return true; }
-    virtual int max_batch_size() const = 0;
+    virtual int max_batch_size() const { return 16; }
 };
 
-// HIP-backed real FFT plan with KissFftPlan's semantics (sanitize on the forward
-// input; 1/N and sanitize on the inverse output; batch b at b*stride*N, element
-// i at i*stride).  Validation mirrors KissFftPlan (kissfft_adapter.cc:13-63)
-// except the batch ceiling, which the device path does not need.
-class HipRealFftPlan final : public IFftPlan {
+// HIP-backed plan with KissFftPlan's semantics in both domains
+// (kissfft_adapter.cc:83-246): real forward sanitizes its input; real and
+// complex inverse scale by 1/nfft and sanitize; complex forward is the raw DFT.
+// Batch b starts at b*stride*len, element i sits at i*stride (len = nfft, or
+// nfft/2+1 for the real spectrum).  Validation mirrors KissFftPlan
+// (kissfft_adapter.cc:13-63) except the batch ceiling, which the device path
+// does not need (MakeFftPlan below applies it).  Host pointers are staged
+// through device buffers owned by the plan, so calls are not reentrant (as in
+// the reference, whose plan owns scratch).
+class HipFftPlan final : public IFftPlan {
    public:
-    explicit HipRealFftPlan(const FftPlanDesc& d) : d_(d), plan_(pdesc(d)) {}
+    explicit HipFftPlan(const FftPlanDesc& d) : d_(validate(d)) {
+        crlot_fft_desc fd{d.domain == FftDomain::Real ? CRLOT_FFT_REAL : CRLOT_FFT_COMPLEX, d.nfft, -1};
+        check(crlot_fft_plan_create(&fd, &p_), "crlot_fft_plan_create");
+    }
+    ~HipFftPlan() override { crlot_fft_plan_destroy(p_); }
+    HipFftPlan(const HipFftPlan&) = delete;
+    HipFftPlan& operator=(const HipFftPlan&) = delete;
+
     void forward(const float* in, std::complex<float>* out, int batch = 1) override {
-        if (batch < 1 || batch > d_.batch) throw std::runtime_error("Invalid batch size");
+        if (d_.domain != FftDomain::Real)
+            throw std::runtime_error("Real FFT not supported for Complex domain plan");
+        check_batch(batch);
         const int64_t n = d_.nfft, bins = n / 2 + 1;
-        const int64_t in_len = int64_t(batch) * d_.stride_in * n, out_len = int64_t(batch) * d_.stride_out * bins;
-        din_.resize(size_t(in_len));
-        dout_.resize(size_t(2 * out_len));
-        hip_check(hipMemcpy(din_.get(), in, sizeof(float) * in_len, hipMemcpyHostToDevice), "hipMemcpy");
-        // the reference only writes the strided elements: start from the caller's buffer
-        hip_check(hipMemcpy(dout_.get(), out, sizeof(float) * 2 * out_len, hipMemcpyHostToDevice),
-                  "hipMemcpy");
-        check(crlot_rfft_batched(plan_.get(), din_.get(), dout_.get(), batch, d_.stride_in * n,
-                                 d_.stride_in, 2 * d_.stride_out * bins, d_.stride_out, nullptr),
-              "crlot_rfft_batched");
-        hip_check(hipMemcpy(out, dout_.get(), sizeof(float) * 2 * out_len, hipMemcpyDeviceToHost),
-                  "hipMemcpy");
+        run(in, 1, batch * d_.stride_in * n, reinterpret_cast<float*>(out), 2, batch * d_.stride_out * bins,
+            [&](const float* i, float* o) {
+                return crlot_fft_forward(p_, i, o, batch, d_.stride_in * n, d_.stride_in,
+                                         2 * d_.stride_out * bins, d_.stride_out, nullptr);
+            });
     }
     void inverse(const std::complex<float>* in, float* out, int batch = 1) override {
-        if (batch < 1 || batch > d_.batch) throw std::runtime_error("Invalid batch size");
+        if (d_.domain != FftDomain::Real)
+            throw std::runtime_error("Real FFT not supported for Complex domain plan");
+        check_batch(batch);
         const int64_t n = d_.nfft, bins = n / 2 + 1;
-        const int64_t in_len = int64_t(batch) * d_.stride_in * bins, out_len = int64_t(batch) * d_.stride_out * n;
-        din_.resize(size_t(2 * in_len));
-        dout_.resize(size_t(out_len));
-        hip_check(hipMemcpy(din_.get(), in, sizeof(float) * 2 * in_len, hipMemcpyHostToDevice), "hipMemcpy");
-        hip_check(hipMemcpy(dout_.get(), out, sizeof(float) * out_len, hipMemcpyHostToDevice), "hipMemcpy");
-        check(crlot_irfft_batched(plan_.get(), din_.get(), dout_.get(), batch, 2 * d_.stride_in * bins,
-                                  d_.stride_in, d_.stride_out * n, d_.stride_out, nullptr),
-              "crlot_irfft_batched");
-        hip_check(hipMemcpy(out, dout_.get(), sizeof(float) * out_len, hipMemcpyDeviceToHost), "hipMemcpy");
+        run(reinterpret_cast<const float*>(in), 2, batch * d_.stride_in * bins, out, 1,
+            batch * d_.stride_out * n, [&](const float* i, float* o) {
+                return crlot_fft_inverse(p_, i, o, batch, 2 * d_.stride_in * bins, d_.stride_in,
+                                         d_.stride_out * n, d_.stride_out, nullptr);
+            });
     }
-    FftDomain domain() const override { return FftDomain::Real; }
+    void forward_complex(const std::complex<float>* in, std::complex<float>* out, int batch = 1) override {
+        complex_call(in, out, batch, false);
+    }
+    void inverse_complex(const std::complex<float>* in, std::complex<float>* out, int batch = 1) override {
+        complex_call(in, out, batch, true);
+    }
+    FftDomain domain() const override { return d_.domain; }
     int size() const override { return d_.nfft; }
-    int max_batch_size() const override { return d_.batch; }
+    crlot_fft_plan* handle() const { return p_; }
 
    private:
-    static crlot_plan_desc pdesc(const FftPlanDesc& d) {
-        if (d.domain != FftDomain::Real) throw std::runtime_error("Unsupported FFT domain");
+    static FftPlanDesc validate(const FftPlanDesc& d) {
+        if (d.domain != FftDomain::Real && d.domain != FftDomain::Complex)
+            throw std::runtime_error("Unsupported FFT domain");
         if (d.batch < 1) throw std::runtime_error("Batch size must be at least 1");
         if (d.stride_in < 1 || d.stride_out < 1) throw std::runtime_error("Stride must be at least 1");
         if (d.in_place) throw std::runtime_error("In-place FFT is not yet supported");
-        if (d.nfft % 2 != 0) throw std::runtime_error("FFT size must be even for real FFT");
-        crlot_plan_desc p{};
-        p.frame_size = d.nfft;
-        p.hop_size = d.nfft / 4 > 0 ? d.nfft / 4 : 1;
-        p.analysis_window = 0;
-        p.apply_window_inside = 0;
-        p.device = -1;
-        return p;
+        if (d.domain == FftDomain::Real && d.nfft % 2 != 0)
+            throw std::runtime_error("FFT size must be even for real FFT");
+        return d;
+    }
+    void check_batch(int batch) const {
+        if (batch < 1 || batch > d_.batch) throw std::runtime_error("Invalid batch size");
+    }
+    void complex_call(const std::complex<float>* in, std::complex<float>* out, int batch, bool inv) {
+        if (d_.domain != FftDomain::Complex)
+            throw std::runtime_error("Complex FFT not supported for Real domain plan");
+        check_batch(batch);
+        const int64_t n = d_.nfft;
+        run(reinterpret_cast<const float*>(in), 2, batch * d_.stride_in * n,
+            reinterpret_cast<float*>(out), 2, batch * d_.stride_out * n, [&](const float* i, float* o) {
+                return (inv ? crlot_fft_inverse_complex : crlot_fft_forward_complex)(
+                    p_, i, o, batch, 2 * d_.stride_in * n, d_.stride_in, 2 * d_.stride_out * n,
+                    d_.stride_out, nullptr);
+            });
+    }
+    // stage host -> device, launch, device -> host.  The reference writes only
+    // the strided output elements, so the device output starts as a copy of the
+    // caller's buffer.
+    template <typename F>
+    void run(const float* in, int in_w, int64_t in_elems, float* out, int out_w, int64_t out_elems, F launch) {
+        const size_t in_f = size_t(in_w) * in_elems, out_f = size_t(out_w) * out_elems;
+        din_.resize(in_f);
+        dout_.resize(out_f);
+        hip_check(hipMemcpy(din_.get(), in, sizeof(float) * in_f, hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(hipMemcpy(dout_.get(), out, sizeof(float) * out_f, hipMemcpyHostToDevice), "hipMemcpy");
+        check(launch(din_.get(), dout_.get()), "fft");
+        hip_check(hipMemcpy(out, dout_.get(), sizeof(float) * out_f, hipMemcpyDeviceToHost), "hipMemcpy");
     }
     FftPlanDesc d_;
-    Plan plan_;
+    crlot_fft_plan* p_ = nullptr;
     DeviceBuffer<float> din_, dout_;
 };
+using HipRealFftPlan = HipFftPlan;  // earlier name
 
+// dsp::fft::MakeFftPlan (fft_api.h:51) with KissFftPlan's checks, including its
+// batch ceiling of 16 (kissfft_adapter.cc:21-23).
 inline std::unique_ptr<IFftPlan> MakeFftPlan(const FftPlanDesc& d) {
-    return std::make_unique<HipRealFftPlan>(d);
+    if (d.domain != FftDomain::Real && d.domain != FftDomain::Complex)
+        throw std::runtime_error("Unsupported FFT domain");
+    if (d.batch < 1 || d.batch > 16) throw std::runtime_error("Batch size must be between 1 and 16");
+    return std::make_unique<HipFftPlan>(d);
 }
 
 }  // namespace fft

@@ -88,6 +88,68 @@ int main() {
             for (int i = 0; i < n; ++i)
                 EXPECT(std::fabs(in[b * n * st + i * st] - rec[b * n * st + i * st]) < 1e-4f, "stride b=%d i=%d", b, i);
     }
+    // fft_test.cc:227-247 batch ceiling: 2 is fine, 17 throws
+    {
+        bool ok2 = true, threw17 = false;
+        try {
+            MakeFftPlan(real_desc(512, 2));
+        } catch (...) {
+            ok2 = false;
+        }
+        try {
+            MakeFftPlan(real_desc(512, 17));
+        } catch (const std::runtime_error&) {
+            threw17 = true;
+        }
+        EXPECT(ok2 && threw17, "batch 2 ok, 17 throws");
+    }
+    // fft_test.cc:251-288 complex tone round trip, and the complex DFT vs the oracle's kiss_fft
+    for (int n : {256, 128, 2048}) {
+        auto plan = MakeFftPlan(FftPlanDesc{FftDomain::Complex, n, false, 1, 1, 1});
+        EXPECT(plan->domain() == FftDomain::Complex && plan->size() == n, "complex plan info");
+        std::vector<std::complex<float>> in(n), X(n), back(n);
+        for (int i = 0; i < n; ++i) {
+            const float t = float(i) / float(n);
+            in[i] = {std::cos(2.0f * float(M_PI) * 10.0f * t), std::sin(2.0f * float(M_PI) * 10.0f * t)};
+        }
+        plan->forward_complex(in.data(), X.data());
+        plan->inverse_complex(X.data(), back.data());
+        float max_error = 0.0f;
+        for (int i = 0; i < n; ++i)
+            max_error = std::fmax(max_error, std::fmax(std::fabs(back[i].real() - in[i].real()),
+                                                       std::fabs(back[i].imag() - in[i].imag())));
+        EXPECT(max_error < 1e-5f, "complex n=%d round trip %g", n, max_error);
+        EXPECT(std::fabs(std::abs(X[10]) - float(n)) < 1e-3f * n, "complex n=%d |X10|=%g", n, std::abs(X[10]));
+        or_kfft_cfg* cfg = or_kfft_alloc(n, 0);
+        std::vector<std::complex<float>> ref(in);
+        or_kfft(cfg, reinterpret_cast<float*>(ref.data()), reinterpret_cast<float*>(ref.data()));
+        or_kfft_free(cfg);
+        double num = 0, den = 0;
+        for (int i = 0; i < n; ++i) {
+            num += std::norm(std::complex<double>(X[i]) - std::complex<double>(ref[i]));
+            den += std::norm(std::complex<double>(ref[i]));
+        }
+        EXPECT(std::sqrt(num / den) < 1e-6, "complex n=%d vs kiss rel %g", n, std::sqrt(num / den));
+    }
+    // domain mismatch: the reference's runtime_error both ways
+    {
+        auto rp = MakeFftPlan(real_desc(512));
+        auto cp = MakeFftPlan(FftPlanDesc{FftDomain::Complex, 256, false, 1, 1, 1});
+        std::vector<std::complex<float>> z(512);
+        std::vector<float> r(512);
+        int threw = 0;
+        try {
+            rp->forward_complex(z.data(), z.data());
+        } catch (const std::runtime_error&) {
+            ++threw;
+        }
+        try {
+            cp->forward(r.data(), z.data());
+        } catch (const std::runtime_error&) {
+            ++threw;
+        }
+        EXPECT(threw == 2, "domain mismatch must throw runtime_error");
+    }
     // WindowLUT: the reference default (symmetric Hann) equals the oracle bit for bit
     {
         WindowLUT lut(1024, WindowType::HANN);

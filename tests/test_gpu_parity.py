@@ -310,6 +310,79 @@ def test_rfft_strided_layout(pkg, oracle, torch_cuda):
         assert rel_l2(got, ref) < REL_L2
 
 
+# ------------------------------------------------------------------ complex domain
+@pytest.mark.parametrize("n", [128, 256, 512, 1024, 2048])
+def test_complex_fft_vs_oracle(pkg, oracle, torch_cuda, n):
+    """IFftPlan::forward_complex / inverse_complex (kissfft_adapter.cc:171-246)
+    against the kiss_fft restatement: raw forward, inverse *1/n + sanitize."""
+    torch = torch_cuda
+    rng = np.random.default_rng(n + 7)
+    B = 6
+    z = (rng.standard_normal((B, n)) + 1j * rng.standard_normal((B, n))).astype(np.complex64)
+    plan = pkg.FftPlan(n, pkg.FFT_COMPLEX)
+    Z = host(plan.forward_complex(dev(torch, z)))
+    k = oracle.KissC(n)
+    for b in range(B):
+        assert rel_l2(Z[b], k.forward(z[b])) < REL_L2, b
+    back = host(plan.inverse_complex(dev(torch, Z)))
+    for b in range(B):
+        assert rel_l2(back[b], k.inverse(Z[b])) < REL_L2, b
+        assert rel_l2(back[b], z[b]) < 2 * REL_L2, b
+    # fft_test.cc:251-288: tone at bin 10, round trip error < 1e-5
+    t = np.arange(n, dtype=np.float32) / np.float32(n)
+    tone = (np.cos(2 * np.pi * 10 * t) + 1j * np.sin(2 * np.pi * 10 * t)).astype(np.complex64)
+    T = host(plan.forward_complex(dev(torch, tone[None])))[0]
+    assert abs(abs(T[10]) - n) < 1e-3 * n
+    assert np.max(np.abs(host(plan.inverse_complex(dev(torch, T[None])))[0] - tone)) < 1e-5
+
+
+def test_complex_fft_sanitize_and_strides(pkg, oracle, torch_cuda):
+    torch = torch_cuda
+    n, B, st = 256, 3, 2
+    rng = np.random.default_rng(11)
+    buf = (rng.standard_normal(B * n * st) + 1j * rng.standard_normal(B * n * st)).astype(np.complex64)
+    buf[5 * st] = np.inf                      # inverse output is then all NaN/Inf -> 0
+    plan = pkg.FftPlan(n, pkg.FFT_COMPLEX)
+    L = pkg.lib()
+    d_in = dev(torch, buf.view(np.float32))
+    out = torch.zeros(2 * B * n * st, dtype=torch.float32, device="cuda")
+    pkg._check(L.crlot_fft_inverse_complex(plan._h, d_in.data_ptr(), out.data_ptr(), B,
+                                           2 * st * n, st, 2 * st * n, st, 0))
+    torch.cuda.synchronize()
+    o = host(out).view(np.complex64)
+    k = oracle.KissC(n)
+    for b in range(B):
+        ref = k.inverse(buf[b * n * st:(b + 1) * n * st:st])
+        got = o[b * n * st:(b + 1) * n * st:st]
+        assert np.all(np.isfinite(got))
+        if b == 0:
+            assert np.array_equal(got, ref)  # everything sanitized to 0 on both sides
+        else:
+            assert rel_l2(got, ref) < REL_L2
+        # untouched (odd) slots stay as they were
+        assert np.all(o[b * n * st + 1:(b + 1) * n * st:st] == 0)
+
+
+def test_fft_plan_domains(pkg, oracle, torch_cuda):
+    """Real plans through the FFT-plan object equal the STFT-plan rfft; the
+    other domain's calls raise the reference's runtime_error."""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((4, 1024)).astype(np.float32)
+    rp = pkg.FftPlan(1024, pkg.FFT_REAL)
+    X = rp.forward(dev(torch, x))
+    Xs = pkg.Plan(frame_size=1024, hop_size=256).rfft(dev(torch, x))
+    assert np.array_equal(host(X), host(Xs))
+    y = host(rp.inverse(X))
+    k = oracle.KissR(1024)
+    assert rel_l2(y[0], k.inverse(host(X)[0])) < REL_L2
+    with pytest.raises(RuntimeError, match="Complex FFT not supported"):
+        rp.forward_complex(X)
+    cp = pkg.FftPlan(512, pkg.FFT_COMPLEX)
+    with pytest.raises(RuntimeError, match="Real FFT not supported"):
+        cp.forward(dev(torch, x[:, :512]))
+
+
 # ------------------------------------------------------------------ size-independent properties
 def test_full_size_properties(pkg, oracle, torch_cuda):
     """At BASELINE scale (1024 streams x 480000, 2 GB in + 2 GB out): determinism,

@@ -94,5 +94,18 @@ def test_plan_validation_before_device(pkg, kw, exc):
         pkg.Plan(**cfg)
 
 
+@pytest.mark.parametrize("domain,nfft,exc", [
+    (2, 512, RuntimeError),            # "Unsupported FFT domain" (kissfft_adapter.cc:15-17)
+    (0, 513, RuntimeError),            # odd real size (kissfft_adapter.cc:36-40)
+    (0, 1000, NotImplementedError),    # valid for kissfft, not a device-path size
+    (1, 64, NotImplementedError),
+    (1, 4096, NotImplementedError),
+])
+def test_fft_plan_validation_before_device(pkg, domain, nfft, exc):
+    with pytest.raises(exc):
+        pkg.FftPlan(nfft, domain)
+
+
 def test_struct_layout_matches_header(pkg):
+    assert C.sizeof(pkg.FftDesc) == 3 * 4
     assert C.sizeof(pkg.PlanDesc) == 12 * 4
