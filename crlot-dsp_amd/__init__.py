@@ -26,7 +26,9 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "crlot_dsp.h")
 # dsp::WindowType / NormalizationType / BoundaryMode ordinals
 HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS = range(5)
 NORM_NONE, NORM_SUM_TO_ONE, NORM_L2, NORM_OLA_UNITY_GAIN, NORM_OLA_SUM_WSQ = range(5)
-ZERO_PAD, DROP = 0, 1
+ZERO_PAD, DROP, FRAMEQUEUE = 0, 1, 2
+# dsp::PadMode (FrameQueue.h:8-12)
+PAD_CONSTANT, PAD_REFLECT, PAD_EDGE = 0, 1, 2
 # dsp::fft::FftDomain
 FFT_REAL, FFT_COMPLEX = 0, 1
 
@@ -48,6 +50,8 @@ class PlanDesc(C.Structure):
         ("ola_gain", C.c_float),
         ("ring_len", C.c_int32),
         ("device", C.c_int32),
+        ("center", C.c_int32),
+        ("pad_mode", C.c_int32),
     ]
 
 
@@ -189,6 +193,8 @@ class PlanConfig:
     ola_gain: float = 1.0
     ring_len: int = 0
     device: int = -1
+    center: bool = True          # boundary_mode == FRAMEQUEUE only (FrameQueue default)
+    pad_mode: int = PAD_CONSTANT
 
 
 class Plan:
@@ -205,7 +211,7 @@ class Plan:
         d = PlanDesc(cfg.frame_size, cfg.hop_size, cfg.window_type, int(cfg.periodic),
                      cfg.window_norm, cfg.boundary_mode, int(cfg.analysis_window),
                      int(cfg.apply_window_inside), cfg.eps, cfg.ola_gain, cfg.ring_len,
-                     cfg.device)
+                     cfg.device, int(cfg.center), cfg.pad_mode)
         h = C.c_void_p()
         _check(lib().crlot_plan_create(C.byref(d), C.byref(h)), "crlot_plan_create")
         self._h = h

@@ -119,6 +119,12 @@ int ensure_workspace(crlot_plan* p, int64_t bytes) {
 
 int64_t frames_for(const crlot_plan* p, int64_t T) {
     const int64_t n = p->geo.n, h = p->geo.h;
+    if (p->boundary == CRLOT_FRAMEQUEUE) {  // FrameQueue.cc:98-115 on the padded length
+        const int64_t padded = T + 2 * int64_t(p->geo.pad);
+        if (padded < n) return 0;
+        const int64_t tail = n > h ? n - h : 0;
+        return (padded - tail) / h;
+    }
     if (T <= 0) return 0;
     if (p->boundary == CRLOT_ZERO_PAD) return (T + h - 1) / h;  // framer.cc:88-117, whole push
     if (T < n) return 0;
@@ -150,8 +156,12 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         return fail(CRLOT_EINVAL, "Blackman-Harris window not yet implemented");
     if (d.window_type < CRLOT_WIN_HANN || d.window_type > CRLOT_WIN_RECT)
         return fail(CRLOT_EINVAL, "Unknown window type");
-    if (d.boundary_mode != CRLOT_ZERO_PAD && d.boundary_mode != CRLOT_DROP)
+    if (d.boundary_mode != CRLOT_ZERO_PAD && d.boundary_mode != CRLOT_DROP &&
+        d.boundary_mode != CRLOT_FRAMEQUEUE)
         return fail(CRLOT_EINVAL, "Unknown boundary mode");
+    if (d.boundary_mode == CRLOT_FRAMEQUEUE &&
+        (d.pad_mode < CRLOT_PAD_CONSTANT || d.pad_mode > CRLOT_PAD_EDGE))
+        return fail(CRLOT_EINVAL, "Unknown pad mode");
     if (d.hop_size > d.frame_size)
         return fail(CRLOT_EUNSUPPORTED, "hop larger than frame is not supported on the GPU path");
     if (!is_pow2(d.frame_size) || d.frame_size < 256 || d.frame_size > 4096)
@@ -182,6 +192,10 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     p->geo.ring_len = ring;
     p->geo.inv_n = 1.0f / float(n);  // kissfft_adapter.cc:154
     p->geo.gain = d.ola_gain;
+    if (d.boundary_mode == CRLOT_FRAMEQUEUE) {
+        p->geo.pad = d.center ? n / 2 : 0;  // FrameQueue.cc:73
+        p->geo.pad_mode = d.pad_mode;
+    }
     p->window.resize(n);
     int rc = crlot_window_table(d.window_type, n, d.periodic, d.window_norm, p->window.data());
     if (rc != CRLOT_OK) {
@@ -301,7 +315,7 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
     const int64_t F = frames_for(p, T);
     // nothing to emit (n_streams == 0, T == 0, or DROP with T < N: the Framer never yields)
     if (n_streams == 0 || F == 0) return CRLOT_OK;
-    if (!d_x || !d_y) return fail(CRLOT_EINVAL, "null buffer");
+    if ((!d_x && T > 0) || !d_y) return fail(CRLOT_EINVAL, "null buffer");
     const int64_t out_len = F * p->geo.h;
     if (ld_x < T || ld_y < out_len) return fail(CRLOT_EINVAL, "leading dimension too small");
     DeviceGuard g(p->device);
@@ -330,7 +344,7 @@ int crlot_roundtrip_stages(crlot_plan* p, const float* d_x, int32_t n_streams, i
                            int64_t ld_x, float* d_frames, float* d_spec, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (n_streams < 0 || T < 0 || ld_x < T) return fail(CRLOT_EINVAL, "bad size");
-    if (!d_x || !d_frames) return fail(CRLOT_EINVAL, "null buffer");
+    if ((!d_x && T > 0) || !d_frames) return fail(CRLOT_EINVAL, "null buffer");
     const int64_t F = frames_for(p, T);
     if (F == 0 || n_streams == 0) return CRLOT_OK;
     DeviceGuard g(p->device);
@@ -503,6 +517,8 @@ struct crlot_stream {
 int crlot_stream_create(crlot_plan* p, int32_t channels, crlot_stream** out) {
     if (!p || !out || channels <= 0) return fail(CRLOT_EINVAL, "bad argument");
     *out = nullptr;
+    if (p->boundary == CRLOT_FRAMEQUEUE)
+        return fail(CRLOT_EINVAL, "FrameQueue framing is whole-signal; stream with ZERO_PAD/DROP");
     if (!crlot::fused_supported(p->geo.n, p->geo.h))
         return fail(CRLOT_EUNSUPPORTED, "streaming path needs H % 128 == 0, N % H == 0, N <= 2048");
     DeviceGuard g(p->device);

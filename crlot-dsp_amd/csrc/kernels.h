@@ -29,6 +29,11 @@ struct Geometry {
     int ring_len = 0;   // OLA ring length
     float inv_n = 0.f;  // 1.0f / N (kissfft_adapter.cc:154)
     float gain = 1.f;   // push gain
+    // framing source: frame k covers x[k*h - pad, k*h - pad + n); samples outside
+    // [0, T) come from pad_mode (0 zeros, 1 reflect101, 2 edge; FrameQueue,
+    // Indexing.h:18-70).  The Framer modes have pad = 0, pad_mode = 0.
+    int pad = 0;
+    int pad_mode = 0;
 };
 
 // Fused fast path: N in {256..2048}, H % 128 == 0, N % H == 0, ring_len % H == 0,

@@ -77,37 +77,59 @@ struct FusedArgs {
     int64_t ld_x, ld_y;
     int T, out_len;  // per stream, T * 4 and out_len * 4 < 2^31 (checked on the host)
     int n_streams, F, n_chunks, M, ring_blocks;
+    int pad, pad_mode;  // framing (Geometry)
     float inv_n, gain;
 };
 
-// Hop loads: lane owns complex samples z[lane + 64 m] = (x[2i], x[2i+1]), i = lane + 64 m.
-// `full` (wave-uniform) = the whole frame lies inside the stream: one dwordx2 per
-// pair; otherwise two dword loads whose out-of-range halves read 0 (ZERO_PAD).
-template <int M0, int CNT, int E, int L>
-__device__ __forceinline__ void load_pairs_l(float2 (&dst)[E], __amdgpu_buffer_rsrc_t rx, int lane,
-                                             int frame_byte, bool full) {
-    if (full) {
-#pragma unroll
-        for (int m = M0; m < M0 + CNT; ++m) dst[m] = dev::bload2(rx, lane * 8 + m * 8 * L, frame_byte);
-    } else {
-#pragma unroll
-        for (int m = M0; m < M0 + CNT; ++m)
-            dst[m] = make_float2(dev::bload1(rx, lane * 8 + m * 8 * L, frame_byte),
-                                 dev::bload1(rx, lane * 8 + m * 8 * L + 4, frame_byte));
-    }
+// FrameQueue padding (Indexing.h:18-37): left side i -> -i-1, right side
+// i -> 2n-2-i, repeated until inside.
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n <= 1) return 0;
+    while (i < 0 || i >= n) i = i < 0 ? -i - 1 : 2 * n - 2 - i;
+    return i;
 }
 
-template <int M0, int CNT, int E>
-__device__ __forceinline__ void load_pairs(float2 (&dst)[E], __amdgpu_buffer_rsrc_t rx, int lane,
-                                           int frame_byte, bool full) {
-    if (full) {
+// x[j] of a T-sample stream with the plan's padding outside [0, T)
+// (getPaddingValueSafe, Indexing.h:48-68): 0 zeros, 1 reflect101, 2 edge.
+__device__ __forceinline__ float fetch_x(__amdgpu_buffer_rsrc_t rx, int j, int T, int mode) {
+    if (mode == 1) j = reflect101(j, T);
+    else if (mode == 2) j = j < 0 ? 0 : (j >= T ? T - 1 : j);
+    const bool ok = j >= 0 && j < T;
+    const float v = dev::bload1(rx, (ok ? j : 0) * 4, 0);
+    return ok ? v : 0.0f;
+}
+
+// The same through a plain pointer and 64-bit indices (staged path).
+__device__ __forceinline__ float fetch_x64(const float* x, int64_t j, int64_t T, int mode) {
+    if (mode == 1) {
+        if (T <= 1) {
+            j = 0;
+        } else {
+            while (j < 0 || j >= T) j = j < 0 ? -j - 1 : 2 * T - 2 - j;
+        }
+    } else if (mode == 2) {
+        j = j < 0 ? 0 : (j >= T ? T - 1 : j);
+    }
+    return (j >= 0 && j < T) ? x[j] : 0.0f;
+}
+
+// Frame loads: lane owns complex samples z[lane + L m] = (x[o + 2i], x[o + 2i + 1]),
+// i = lane + L m, o = the frame's origin in x (k*H - pad).  A frame wholly inside
+// the stream takes one dwordx2 per pair; an edge frame maps every sample
+// through the padding rule (ZERO_PAD tails, FrameQueue centre padding).
+template <int M0, int CNT, int E, int L>
+__device__ __forceinline__ void load_pairs_l(float2 (&dst)[E], __amdgpu_buffer_rsrc_t rx, int lane,
+                                             int origin, int T, int mode) {
+    constexpr int N = 2 * L * E;
+    if (origin >= 0 && origin + N <= T) {
 #pragma unroll
-        for (int m = M0; m < M0 + CNT; ++m) dst[m] = dev::bload2(rx, lane * 8 + m * 512, frame_byte);
+        for (int m = M0; m < M0 + CNT; ++m) dst[m] = dev::bload2(rx, lane * 8 + m * 8 * L, origin * 4);
     } else {
 #pragma unroll
-        for (int m = M0; m < M0 + CNT; ++m)
-            dst[m] = make_float2(dev::bload1(rx, lane * 8 + m * 512, frame_byte),
-                                 dev::bload1(rx, lane * 8 + m * 512 + 4, frame_byte));
+        for (int m = M0; m < M0 + CNT; ++m) {
+            const int j = origin + 2 * (lane + L * m);
+            dst[m] = make_float2(fetch_x(rx, j, T, mode), fetch_x(rx, j + 1, T, mode));
+        }
     }
 }
 
@@ -161,7 +183,7 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
     }
 #endif
     float2 xin[E];
-    load_pairs<0, E, E>(xin, rx, lane, fs * H * 4, fs * H + N <= a.T);
+    load_pairs_l<0, E, E, 64>(xin, rx, lane, fs * H - a.pad, a.T, a.pad_mode);
     float2 acc[NB][S];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
@@ -172,7 +194,7 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
         // prefetch: frame k+1's new hop and block k's normaliser, consumed at the
         // end of this iteration, so their latency hides under the transforms
         float2 nxt[E];
-        if (k + 1 < f1) load_pairs<E - S, S, E>(nxt, rx, lane, (k + 1) * H * 4, (k + 1) * H + N <= a.T);
+        if (k + 1 < f1) load_pairs_l<E - S, S, E, 64>(nxt, rx, lane, (k + 1) * H - a.pad, a.T, a.pad_mode);
         float2 dn[S];
         if (k >= f0) {
 #pragma unroll
@@ -247,7 +269,7 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
 // passes, C for the split); each exchange costs one s_barrier.
 template <int L, int S, int NB, bool HAS_GAIN>
 __global__ __launch_bounds__(L) void k_stft_ola_wg(const FusedArgs a) {
-    constexpr int E = 8, P = L * E, N = 2 * P, H = 2 * L * S;
+    constexpr int E = 8, P = L * E, H = 2 * L * S;
     static_assert(NB * S == E, "N = NB * H");
     constexpr int NX = dev::fft_exchanges(P, E);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -278,7 +300,7 @@ __global__ __launch_bounds__(L) void k_stft_ola_wg(const FusedArgs a) {
     }
 
     float2 xin[E];
-    load_pairs_l<0, E, E, L>(xin, rx, t, fs * H * 4, fs * H + N <= a.T);
+    load_pairs_l<0, E, E, L>(xin, rx, t, fs * H - a.pad, a.T, a.pad_mode);
     float2 acc[NB][S];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
@@ -287,7 +309,7 @@ __global__ __launch_bounds__(L) void k_stft_ola_wg(const FusedArgs a) {
 
     for (int k = fs; k < f1; ++k) {
         float2 nxt[E];
-        if (k + 1 < f1) load_pairs_l<E - S, S, E, L>(nxt, rx, t, (k + 1) * H * 4, (k + 1) * H + N <= a.T);
+        if (k + 1 < f1) load_pairs_l<E - S, S, E, L>(nxt, rx, t, (k + 1) * H - a.pad, a.T, a.pad_mode);
         float2 dn[S];
         if (k >= f0) {
 #pragma unroll
@@ -337,7 +359,7 @@ struct SynthArgs {
     float* frames;  // [s][k][N]
     float* spec;    // [s][k][P+1] cf, optional
     int64_t ld_x, T, F;
-    int h, n_streams;
+    int h, n_streams, pad, pad_mode;
     float inv_n;
 };
 
@@ -358,14 +380,21 @@ __global__ __launch_bounds__(kBlock) void k_synth_frames(const SynthArgs a) {
     if (gw >= int64_t(a.n_streams) * a.F) return;
     const int64_t s = gw / a.F, k = gw % a.F;
     const float* x = a.x + s * a.ld_x;
-    const int64_t base = k * a.h;
+    const int64_t base = k * a.h - a.pad;
+    const bool inside = base >= 0 && base + N <= a.T;
     cf v[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int i0 = 2 * (lane + 64 * m);
         const int64_t t0 = base + i0;
-        const float x0 = t0 < a.T ? x[t0] : 0.0f;
-        const float x1 = t0 + 1 < a.T ? x[t0 + 1] : 0.0f;
+        float x0, x1;
+        if (inside) {
+            x0 = x[t0];
+            x1 = x[t0 + 1];
+        } else {
+            x0 = fetch_x64(x, t0, a.T, a.pad_mode);
+            x1 = fetch_x64(x, t0 + 1, a.T, a.pad_mode);
+        }
         v[m].r = dev::sanit(x0 * wa[i0]);
         v[m].i = dev::sanit(x1 * wa[i0 + 1]);
     }
@@ -756,6 +785,8 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.M = int((F + a.n_chunks - 1) / a.n_chunks);
     a.n_chunks = int((F + a.M - 1) / a.M);
     a.ring_blocks = g.ring_len / g.h;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     a.gain = g.gain;
     const int64_t waves = int64_t(n_streams) * a.n_chunks;
@@ -826,6 +857,8 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
     a.M = int((F + a.n_chunks - 1) / a.n_chunks);
     a.n_chunks = int((F + a.M - 1) / a.M);
     a.ring_blocks = g.ring_len / g.h;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     a.gain = g.gain;
     const int64_t grid = int64_t(n_streams) * a.n_chunks;
@@ -870,6 +903,8 @@ hipError_t launch_synth_frames(const Geometry& g, const DevTables& t, const floa
     a.F = F;
     a.h = g.h;
     a.n_streams = n_streams;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     const int64_t waves = int64_t(n_streams) * F;
     const int64_t grid = (waves + kWaves - 1) / kWaves;

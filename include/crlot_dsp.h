@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define CRLOT_ABI_VERSION 1
+#define CRLOT_ABI_VERSION 2
 
 /* error codes */
 #define CRLOT_OK 0
@@ -53,9 +53,15 @@ extern "C" {
 #define CRLOT_NORM_L2 2
 #define CRLOT_NORM_OLA_UNITY_GAIN 3
 #define CRLOT_NORM_OLA_SUM_WSQ 4
-/* dsp::BoundaryMode (framer.h:11-14) */
+/* framing source: dsp::BoundaryMode (framer.h:11-14) of a whole-stream Framer
+ * push, or dsp::FrameQueue (FrameQueue.h:26-96) with center / pad_mode */
 #define CRLOT_ZERO_PAD 0
 #define CRLOT_DROP 1
+#define CRLOT_FRAMEQUEUE 2
+/* dsp::PadMode (FrameQueue.h:8-12) */
+#define CRLOT_PAD_CONSTANT 0
+#define CRLOT_PAD_REFLECT 1
+#define CRLOT_PAD_EDGE 2
 
 typedef struct crlot_plan crlot_plan;
 typedef struct crlot_stream crlot_stream;
@@ -69,13 +75,15 @@ typedef struct crlot_plan_desc {
     int32_t window_type;         /* CRLOT_WIN_* */
     int32_t periodic;            /* 0 = symmetric (reference default) */
     int32_t window_norm;         /* CRLOT_NORM_* */
-    int32_t boundary_mode;       /* CRLOT_ZERO_PAD (whole-stream push) or CRLOT_DROP */
+    int32_t boundary_mode;       /* CRLOT_ZERO_PAD / CRLOT_DROP (Framer) or CRLOT_FRAMEQUEUE */
     int32_t analysis_window;     /* 1: frame * w before forward (e2e_benchmark.cc:154-156) */
     int32_t apply_window_inside; /* OLAConfig::apply_window_inside */
     float eps;                   /* OLAConfig::eps; 0 -> 1e-8f */
     float ola_gain;              /* push_frame_AoS gain; 0 -> 1.0f */
     int32_t ring_len;            /* 0 -> (ceil(N/H)+20)*H (OLAAccumulator.cc:249-258) */
     int32_t device;              /* HIP device ordinal, -1 = current */
+    int32_t center;              /* CRLOT_FRAMEQUEUE: pad N/2 both sides (FrameQueue default: 1) */
+    int32_t pad_mode;            /* CRLOT_FRAMEQUEUE: CRLOT_PAD_* */
 } crlot_plan_desc;
 
 const char* crlot_last_error(void);
@@ -93,7 +101,8 @@ int crlot_plan_upload_tables(crlot_plan* plan, const float* window, const float*
 int crlot_plan_set_spectral_gain(crlot_plan* plan, const float* gain);
 int crlot_plan_info(const crlot_plan* plan, int32_t* frame_size, int32_t* hop_size,
                     int32_t* ring_len);
-/* Frames a whole-stream push of T samples yields (Framer, framer.cc:88-117) */
+/* Frames of a T-sample stream: Framer whole push (framer.cc:88-117) or
+ * FrameQueue::calculateNumFrames on the padded length (FrameQueue.cc:98-115) */
 int64_t crlot_frame_count(const crlot_plan* plan, int64_t T);
 /* Samples the streaming-interleaved round trip emits: F*H */
 int64_t crlot_output_length(const crlot_plan* plan, int64_t T);
@@ -107,7 +116,10 @@ int crlot_plan_reserve(crlot_plan* plan, int64_t bytes);
  * d_x[s*ld_x + t], t < T, and writes d_y[s*ld_y + n], n < crlot_output_length.
  * Equals, per stream, Framer(push whole) -> pop -> *w -> IFftPlan::forward ->
  * (spectral hook) -> IFftPlan::inverse -> OLAAccumulator::push_frame_AoS(k*H)
- * -> produce(H), frame after frame. */
+ * -> produce(H), frame after frame.  With CRLOT_FRAMEQUEUE the frames are
+ * FrameQueue(x, T, N, H, center, pad_mode).getFrame(k) (output sample n is at
+ * padded position n) -- the performance_benchmark.cc:174-246 pipeline, with
+ * analysis_window = 0 there.  d_x may be NULL when T == 0. */
 int crlot_roundtrip(crlot_plan* plan, const float* d_x, float* d_y, int32_t n_streams, int64_t T,
                     int64_t ld_x, int64_t ld_y, void* stream);
 

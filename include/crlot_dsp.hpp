@@ -101,6 +101,8 @@ class StftEngine {
         bool analysis_window = true, apply_window_inside = true;
         float eps = 1e-8f, gain = 1.0f;
         int device = -1;
+        bool center = true;                  // boundary_mode == CRLOT_FRAMEQUEUE
+        int pad_mode = CRLOT_PAD_CONSTANT;   // (dsp::FrameQueue defaults)
     };
     explicit StftEngine(const Config& c) : plan_(desc(c)) {}
     int64_t frame_count(int64_t T) const { return crlot_frame_count(plan_.get(), T); }
@@ -141,6 +143,8 @@ class StftEngine {
         d.eps = c.eps;
         d.ola_gain = c.gain;
         d.device = c.device;
+        d.center = c.center;
+        d.pad_mode = c.pad_mode;
         return d;
     }
     Plan plan_;

@@ -788,15 +788,97 @@ size_t or_frame_count(size_t T, size_t n, size_t h, int mode) {
     return (T - n) / h + 1;
 }
 
+/* ======================================================================== */
+/* FrameQueue (dsp/frame/FrameQueue.cc, dsp/frame/Indexing.h)               */
+/* ======================================================================== */
+
+/* Indexing.h:18-37: left side i -> -i-1 (-1 -> 0), right side i -> 2n-2-i
+ * (n -> n-2), repeated until inside. */
+int or_fq_reflect101(int i, int n) {
+    if (n <= 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0)
+            i = -i - 1;
+        else
+            i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+/* Indexing.h:48-68 getPaddingValueSafe */
+float or_fq_pad_value(const float* data, int len, int idx, int pad_mode) {
+    if (len <= 0) return 0.0f;
+    switch (pad_mode) {
+        case 0: return 0.0f;
+        case 2: return idx < 0 ? data[0] : idx >= len ? data[len - 1] : data[idx];
+        case 1: return data[or_fq_reflect101(idx, len)];
+        default: return 0.0f;
+    }
+}
+
+/* FrameQueue.cc:98-115 calculateNumFrames on the padded length */
+size_t or_fq_count(size_t T, size_t n, size_t h, int center) {
+    const size_t padded = T + (center ? 2 * (n / 2) : 0);
+    if (padded < n) return 0;
+    const size_t tail = n > h ? n - h : 0;
+    if (padded < tail) return 0;
+    return (padded - tail) / h;
+}
+
+/* FrameQueue.cc:9-45 + createPaddedInput (:66-96) */
+size_t or_fq_frames(const float* x, size_t T, size_t n, size_t h, int center, int pad_mode,
+                    float* frames) {
+    const size_t pad = center ? n / 2 : 0;
+    const size_t padded_len = T + 2 * pad;
+    float* padded = (float*)malloc(sizeof(float) * (padded_len ? padded_len : 1));
+    if (!center) {
+        if (T) memcpy(padded, x, sizeof(float) * T);
+    } else {
+        const int sl = (int)T, sp = (int)pad;
+        for (int i = -sp; i < sl + sp; ++i)
+            padded[i + sp] = (i >= 0 && i < sl) ? x[i] : or_fq_pad_value(x, sl, i, pad_mode);
+    }
+    const size_t F = or_fq_count(T, n, h, center);
+    if (frames) {
+        for (size_t k = 0; k < F; ++k)
+            for (size_t i = 0; i < n; ++i) {
+                const size_t idx = k * h + i;
+                frames[k * n + i] = idx < padded_len
+                                        ? padded[idx]
+                                        : or_fq_pad_value(padded, (int)padded_len, (int)idx, pad_mode);
+            }
+    }
+    free(padded);
+    return F;
+}
+
 long or_roundtrip(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic, int mode,
                   float* y, size_t y_cap, float* frames_out, float* spec_out) {
+    return or_roundtrip_ex(x, T, n, h, wtype, periodic, mode, 0, 0, 1, y, y_cap, frames_out,
+                           spec_out);
+}
+
+long or_roundtrip_ex(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
+                     int framing, int center, int pad_mode, int analysis_window, float* y,
+                     size_t y_cap, float* frames_out, float* spec_out) {
     if (n == 0 || h == 0 || (n & 1)) return -1;
+    if (framing < 0 || framing > 2) return -3;
     float* w = (float*)malloc(sizeof(float) * n);
     if (or_window(wtype, n, periodic, OR_NORM_NONE, w) != 0) {
         free(w);
         return -2;
     }
-    or_framer* fr = or_framer_new(n, h, 1, mode);
+    or_framer* fr = NULL;
+    float* fq = NULL;
+    size_t fq_n = 0;
+    if (framing == 2) {
+        fq_n = or_fq_count(T, n, h, center);
+        fq = (float*)malloc(sizeof(float) * (fq_n * n + 1));
+        or_fq_frames(x, T, n, h, center, pad_mode, fq);
+    } else {
+        fr = or_framer_new(n, h, 1, framing);
+        or_framer_push(fr, x, T);
+    }
     or_ola* ola = or_ola_new(n, h, 1, 1e-8f, 1);
     or_ola_set_window(ola, w);
     or_kfftr_cfg* fwd = or_kfftr_alloc((int)n, 0);
@@ -804,49 +886,41 @@ long or_roundtrip(const float* x, size_t T, size_t n, size_t h, int wtype, int p
     float* frame = (float*)malloc(sizeof(float) * n);
     float* proc = (float*)malloc(sizeof(float) * n);
     float* spec = (float*)malloc(sizeof(float) * (n + 2));
-    or_framer_push(fr, x, T);
+    float* tmp = (float*)malloc(sizeof(float) * h);
     size_t k = 0, out_pos = 0;
-    while (or_framer_pop(fr, frame)) {
-        for (size_t i = 0; i < n; ++i) proc[i] = frame[i] * w[i]; /* e2e_benchmark.cc:154-156 */
+    for (;;) {
+        if (fr) {
+            if (!or_framer_pop(fr, frame)) break;
+        } else {
+            if (k >= fq_n) break;
+            memcpy(frame, fq + k * n, sizeof(float) * n); /* FrameQueue::getFrame */
+        }
+        for (size_t i = 0; i < n; ++i) /* e2e_benchmark.cc:154-156 (analysis window) */
+            proc[i] = analysis_window ? frame[i] * w[i] : frame[i];
         or_adapter_forward(fwd, (int)n, proc, spec);
         if (spec_out) memcpy(spec_out + k * (n + 2), spec, sizeof(float) * (n + 2));
         or_adapter_inverse(inv, (int)n, spec, proc);
         if (frames_out) memcpy(frames_out + k * n, proc, sizeof(float) * n);
         or_ola_push_frame_aos(ola, proc, NULL, k * h, 0, n, 1.0f);
-        float tmp_out[1];
-        (void)tmp_out;
+        float* chp[1] = {tmp};
+        const size_t got = or_ola_produce(ola, chp, h);
         if (out_pos < y_cap) {
-            float* dst = y + out_pos;
-            size_t want = h;
-            if (out_pos + want > y_cap) {
-                /* produce into a temp then clip */
-                float* t = (float*)malloc(sizeof(float) * h);
-                float* chp[1] = {t};
-                size_t got = or_ola_produce(ola, chp, h);
-                size_t cp = y_cap - out_pos < got ? y_cap - out_pos : got;
-                memcpy(dst, t, sizeof(float) * cp);
-                out_pos += got;
-                free(t);
-            } else {
-                float* chp[1] = {dst};
-                out_pos += or_ola_produce(ola, chp, want);
-            }
-        } else {
-            float* t = (float*)malloc(sizeof(float) * h);
-            float* chp[1] = {t};
-            out_pos += or_ola_produce(ola, chp, h);
-            free(t);
+            const size_t cp = y_cap - out_pos < got ? y_cap - out_pos : got;
+            memcpy(y + out_pos, tmp, sizeof(float) * cp);
         }
+        out_pos += got;
         ++k;
     }
     free(frame);
     free(proc);
     free(spec);
+    free(tmp);
     free(w);
+    free(fq);
     or_kfftr_free(fwd);
     or_kfftr_free(inv);
     or_ola_free(ola);
-    or_framer_free(fr);
+    if (fr) or_framer_free(fr);
     return (long)k;
 }
 
@@ -854,7 +928,7 @@ typedef struct {
     const float* x;
     float* y;
     size_t s0, s1, T, ld_x, ld_y, n, h;
-    int wtype, periodic, mode;
+    int wtype, periodic, mode, center, pad_mode, analysis_window;
     long ret;
 } batch_job;
 
@@ -862,8 +936,9 @@ static void* batch_worker(void* arg) {
     batch_job* j = (batch_job*)arg;
     j->ret = 0;
     for (size_t s = j->s0; s < j->s1; ++s) {
-        long r = or_roundtrip(j->x + s * j->ld_x, j->T, j->n, j->h, j->wtype, j->periodic, j->mode,
-                              j->y + s * j->ld_y, j->ld_y, NULL, NULL);
+        long r = or_roundtrip_ex(j->x + s * j->ld_x, j->T, j->n, j->h, j->wtype, j->periodic,
+                                 j->mode, j->center, j->pad_mode, j->analysis_window,
+                                 j->y + s * j->ld_y, j->ld_y, NULL, NULL);
         if (r < 0) {
             j->ret = r;
             break;
@@ -876,6 +951,13 @@ static void* batch_worker(void* arg) {
 long or_roundtrip_batch(const float* x, size_t n_streams, size_t T, size_t ld_x, size_t n,
                         size_t h, int wtype, int periodic, int mode, float* y, size_t ld_y,
                         int nthreads) {
+    return or_roundtrip_batch_ex(x, n_streams, T, ld_x, n, h, wtype, periodic, mode, 0, 0, 1, y,
+                                 ld_y, nthreads);
+}
+
+long or_roundtrip_batch_ex(const float* x, size_t n_streams, size_t T, size_t ld_x, size_t n,
+                           size_t h, int wtype, int periodic, int mode, int center, int pad_mode,
+                           int analysis_window, float* y, size_t ld_y, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if ((size_t)nthreads > n_streams) nthreads = (int)(n_streams ? n_streams : 1);
     batch_job* jobs = (batch_job*)calloc((size_t)nthreads, sizeof(batch_job));
@@ -894,6 +976,9 @@ long or_roundtrip_batch(const float* x, size_t n_streams, size_t T, size_t ld_x,
         j->wtype = wtype;
         j->periodic = periodic;
         j->mode = mode;
+        j->center = center;
+        j->pad_mode = pad_mode;
+        j->analysis_window = analysis_window;
         pthread_create(&th[t], NULL, batch_worker, j);
     }
     long ret = 0;

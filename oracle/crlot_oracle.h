@@ -117,6 +117,28 @@ long or_roundtrip_batch(const float* x, size_t n_streams, size_t T, size_t ld_x,
                         size_t hop, int window_type, int periodic, int mode, float* y,
                         size_t ld_y, int nthreads);
 
+/* ---- FrameQueue (dsp/frame/FrameQueue.cc:9-115, Indexing.h:18-70) ----
+ * pad_mode: 0 CONSTANT, 1 REFLECT, 2 EDGE (dsp::PadMode ordinals).
+ * or_fq_count: frames of a len-T signal; or_fq_frames writes them [F][N]. */
+int or_fq_reflect101(int i, int n);
+float or_fq_pad_value(const float* data, int len, int idx, int pad_mode);
+size_t or_fq_count(size_t T, size_t frame_size, size_t hop, int center);
+size_t or_fq_frames(const float* x, size_t T, size_t frame_size, size_t hop, int center,
+                    int pad_mode, float* frames);
+
+/* Generalised round trip: framing = 0/1 Framer ZERO_PAD/DROP whole push, 2 =
+ * FrameQueue(center, pad_mode); analysis_window = multiply frames by w before
+ * forward (e2e harness) or not (performance_benchmark.cc:174-246 pipeline).
+ * The OLA side is unchanged: add at k*H with the window inside, produce(H)
+ * after each frame.  Returns F. */
+long or_roundtrip_ex(const float* x, size_t T, size_t frame_size, size_t hop, int window_type,
+                     int periodic, int framing, int center, int pad_mode, int analysis_window,
+                     float* y, size_t y_cap, float* frames_out, float* spec_out);
+long or_roundtrip_batch_ex(const float* x, size_t n_streams, size_t T, size_t ld_x,
+                           size_t frame_size, size_t hop, int window_type, int periodic,
+                           int framing, int center, int pad_mode, int analysis_window, float* y,
+                           size_t ld_y, int nthreads);
+
 /* splitmix64-based synthetic input: uniform [-1,1) * 0.5 */
 void or_synth_fill(float* x, size_t n, unsigned long long seed);
 

@@ -17,6 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS = range(5)
 NORM_NONE, NORM_SUM_TO_ONE, NORM_L2, NORM_OLA_UNITY_GAIN, NORM_OLA_SUM_WSQ = range(5)
 ZERO_PAD, DROP = 0, 1
+FRAMEQUEUE = 2                      # framing source: dsp::FrameQueue (center, pad_mode)
+PAD_CONSTANT, PAD_REFLECT, PAD_EDGE = 0, 1, 2
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
 _lib = None
@@ -83,6 +85,18 @@ def lib(native: bool = False):
                                      sz, C.c_int]
     L.or_roundtrip_batch.restype = C.c_long
     L.or_synth_fill.argtypes = [_f32p, sz, C.c_ulonglong]
+    L.or_fq_reflect101.argtypes = [C.c_int, C.c_int]
+    L.or_fq_reflect101.restype = C.c_int
+    L.or_fq_count.argtypes = [sz, sz, sz, C.c_int]
+    L.or_fq_count.restype = sz
+    L.or_fq_frames.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_void_p]
+    L.or_fq_frames.restype = sz
+    L.or_roundtrip_ex.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, _f32p, sz, C.c_void_p, C.c_void_p]
+    L.or_roundtrip_ex.restype = C.c_long
+    L.or_roundtrip_batch_ex.argtypes = [_f32p, sz, sz, sz, sz, sz, C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_int, C.c_int, _f32p, sz, C.c_int]
+    L.or_roundtrip_batch_ex.restype = C.c_long
     if not native:
         _lib = L
     return L
@@ -278,6 +292,55 @@ def roundtrip_batch(x2d, n, h, wtype=HANN, periodic=False, mode=ZERO_PAD, nthrea
                                        y.shape[1], nthreads)
     if r < 0:
         raise ValueError(f"or_roundtrip_batch rc={r}")
+    return y[:, :F * h]
+
+
+def fq_count(T, n, h, center=True):
+    return int(lib().or_fq_count(T, n, h, int(center)))
+
+
+def fq_frames(x, n, h, center=True, pad_mode=PAD_CONSTANT):
+    """dsp::FrameQueue(x, T, n, h, center, pad_mode).getAllFrames() as (F, n)."""
+    x = np.ascontiguousarray(x, np.float32)
+    F = fq_count(x.size, n, h, center)
+    out = np.zeros((max(F, 1), n), np.float32)
+    lib().or_fq_frames(x if x.size else np.zeros(1, np.float32), x.size, n, h, int(center),
+                       pad_mode, out.ctypes.data)
+    return out[:F]
+
+
+def frames_for(T, n, h, mode=ZERO_PAD, center=True):
+    return fq_count(T, n, h, center) if mode == FRAMEQUEUE else frame_count(T, n, h, mode)
+
+
+def roundtrip_ex(x, n, h, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT, analysis_window=True,
+                 wtype=HANN, periodic=False, want_frames=False):
+    """or_roundtrip_ex: any framing source (Framer modes or FrameQueue), analysis
+    window on/off; returns y (F*H) [, frames (F, N)]."""
+    x = np.ascontiguousarray(x, np.float32)
+    T = x.size
+    F = frames_for(T, n, h, mode, center)
+    y = np.zeros(max(F * h, 1), np.float32)
+    frames = np.zeros((max(F, 1), n), np.float32) if want_frames else None
+    r = lib().or_roundtrip_ex(x if T else np.zeros(1, np.float32), T, n, h, wtype, int(periodic),
+                              mode, int(center), pad_mode, int(analysis_window), y, F * h,
+                              None if frames is None else frames.ctypes.data, None)
+    if r < 0:
+        raise ValueError(f"or_roundtrip_ex rc={r}")
+    assert r == F, (r, F)
+    return (y[:F * h], frames[:F]) if want_frames else y[:F * h]
+
+
+def roundtrip_batch_ex(x2d, n, h, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT,
+                       analysis_window=True, wtype=HANN, periodic=False, nthreads=1):
+    x2d = np.ascontiguousarray(x2d, np.float32)
+    S, T = x2d.shape
+    F = frames_for(T, n, h, mode, center)
+    y = np.zeros((S, max(F * h, 1)), np.float32)
+    r = lib().or_roundtrip_batch_ex(x2d, S, T, T, n, h, wtype, int(periodic), mode, int(center),
+                                    pad_mode, int(analysis_window), y, y.shape[1], nthreads)
+    if r < 0:
+        raise ValueError(f"or_roundtrip_batch_ex rc={r}")
     return y[:, :F * h]
 
 

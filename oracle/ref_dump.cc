@@ -1,10 +1,10 @@
 // ref_dump.cc -- fixture generator linked against the REFERENCE's own sources.
 //
 // TEST INFRASTRUCTURE ONLY.  Built by oracle/Makefile (target `ref`) from
-// /root/reference/dsp/window/WindowLUT.cc, dsp/ola/norm_builder.cc and
-// dsp/frame/framer.cc compiled unchanged with the reference's release flags
+// /root/reference/dsp/window/WindowLUT.cc, dsp/ola/norm_builder.cc,
+// dsp/frame/framer.cc and dsp/frame/FrameQueue.cc compiled unchanged with the reference's release flags
 // (-std=c++17 -O3 -DNDEBUG -march=native, scripts/run_all.sh:12).  No stand-in
-// headers or libraries are involved: those three translation units need only
+// headers or libraries are involved: those translation units need only
 // the C++ standard library.  Output goes to a directory of raw little-endian
 // float32 / uint64 files plus a manifest consumed by tests/golden/make_golden.py.
 //
@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "dsp/frame/FrameQueue.h"
 #include "dsp/frame/framer.h"
 #include "dsp/ola/norm_builder.h"
 #include "dsp/window/WindowLUT.h"
@@ -142,6 +143,37 @@ static void framers() {
     }
 }
 
+// FrameQueue (FrameQueue.cc:9-115, Indexing.h:18-70): every pad mode, center
+// on/off, signals shorter than the pad (multi-bounce reflect101), odd sizes.
+static void framequeues() {
+    const dsp::PadMode modes[] = {dsp::PadMode::CONSTANT, dsp::PadMode::REFLECT, dsp::PadMode::EDGE};
+    const char* mnames[] = {"constant", "reflect", "edge"};
+    struct Case {
+        size_t T, N, H;
+    };
+    const Case cases[] = {{20, 8, 2},   {5, 8, 2},      {1, 8, 4},      {2, 16, 4},  {3, 16, 16},
+                          {0, 8, 2},    {1000, 100, 30}, {3000, 512, 128}, {4100, 1024, 256},
+                          {9000, 1024, 512}, {6000, 4096, 1024}, {7, 6, 9}};
+    for (const Case& c : cases) {
+        std::vector<float> x(c.T);
+        for (size_t i = 0; i < c.T; ++i) x[i] = float(i % 1000) / 1024.0f - 0.5f + float(i / 1000);
+        for (int center = 0; center < 2; ++center)
+            for (int m = 0; m < 3; ++m) {
+                if (!center && m > 0) continue;  // padding is never consulted without center
+                dsp::FrameQueue fq(c.T ? x.data() : nullptr, c.T, c.N, c.H, center != 0, modes[m]);
+                char name[160];
+                std::snprintf(name, sizeof name, "fq_t%zu_n%zu_h%zu_c%d_%s", c.T, c.N, c.H, center,
+                              mnames[m]);
+                dump_u64(std::string(name) + "_meta",
+                         {uint64_t(c.T), uint64_t(c.N), uint64_t(c.H), uint64_t(center), uint64_t(m),
+                          uint64_t(fq.getNumFrames())});
+                dump_f32(std::string(name) + "_x", x.data(), x.size());
+                dump_f32(std::string(name) + "_frames", fq.getAllFrames().data(),
+                         fq.getAllFrames().size());
+            }
+    }
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: ref_dump OUTDIR\n");
@@ -153,6 +185,7 @@ int main(int argc, char** argv) {
     windows();
     norms();
     framers();
+    framequeues();
     std::fclose(g_manifest);
     return 0;
 }

@@ -21,7 +21,8 @@ class Desc(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("frame_size", "hop_size", "window_type", "periodic",
                                          "window_norm", "boundary_mode", "analysis_window",
                                          "apply_window_inside")] + [
-        ("eps", C.c_float), ("ola_gain", C.c_float), ("ring_len", C.c_int32), ("device", C.c_int32)]
+        ("eps", C.c_float), ("ola_gain", C.c_float), ("ring_len", C.c_int32), ("device", C.c_int32),
+        ("center", C.c_int32), ("pad_mode", C.c_int32)]
 
 
 g = torch.Generator(device="cuda").manual_seed(3)

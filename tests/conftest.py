@@ -64,6 +64,11 @@ def e2e_gold():
 
 
 @pytest.fixture(scope="session")
+def fq_gold():
+    return _npz("fq_oracle.npz")
+
+
+@pytest.fixture(scope="session")
 def torch_cuda():
     import torch
     if not torch.cuda.is_available():

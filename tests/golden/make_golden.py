@@ -15,6 +15,10 @@ kiss_gst.npz     kissfft float32 real transforms computed by the kissfft build
                  algorithm the reference calls (kissfft 131.1.0 is absent:
                  empty submodule).  Pins oracle/crlot_oracle.c's kissfft
                  restatement bit for bit.  Skipped if the library is absent.
+fq_oracle.npz    FrameQueue-framed round trips (performance_benchmark.cc:174-246
+                 pipeline: centre padding, no analysis window) from the oracle,
+                 whose FrameQueue restatement ref_tables.npz pins (fq_* arrays,
+                 dumped from the reference's own FrameQueue.cc).
 e2e_oracle.npz   round-trip vectors (input, per-stage frames/spectra, output)
                  from the pinned oracle for the BASELINE configs at small T,
                  plus sanitizer cases (NaN / Inf / 1e-40 inputs).
@@ -115,8 +119,39 @@ def e2e_oracle():
     print("e2e_oracle.npz:", len(out), "arrays")
 
 
+# (name, N, H, center, pad_mode, analysis_window, n_streams, T)
+FQ_CASES = [
+    ("perf_1024_512_const", 1024, 512, 1, O.PAD_CONSTANT, 0, 1, 9000),
+    ("c_1024_256_reflect", 1024, 256, 1, O.PAD_REFLECT, 0, 2, 5000),
+    ("c_512_128_edge_win", 512, 128, 1, O.PAD_EDGE, 1, 2, 3001),
+    ("c_4096_1024_reflect", 4096, 1024, 1, O.PAD_REFLECT, 0, 1, 9000),
+    ("c_1024_300_edge", 1024, 300, 1, O.PAD_EDGE, 0, 1, 4000),
+    ("nc_1024_256", 1024, 256, 0, O.PAD_CONSTANT, 0, 1, 5000),
+    ("short_reflect", 1024, 256, 1, O.PAD_REFLECT, 0, 1, 7),
+]
+
+
+def fq_oracle():
+    out = {}
+    for cid, (name, n, h, center, pm, aw, S, T) in enumerate(FQ_CASES):
+        x = O.synth_streams(S, T, config_id=200 + cid)
+        ys, frs = [], []
+        for s in range(S):
+            y, fr = O.roundtrip_ex(x[s], n, h, mode=O.FRAMEQUEUE, center=bool(center), pad_mode=pm,
+                                   analysis_window=bool(aw), want_frames=True)
+            ys.append(y)
+            frs.append(fr)
+        out[f"{name}/x"] = x
+        out[f"{name}/y"] = np.stack(ys)
+        out[f"{name}/frames"] = np.stack(frs)
+        out[f"{name}/meta"] = np.array([n, h, center, pm, aw, S, T], np.int64)
+    np.savez_compressed(os.path.join(GOLD, "fq_oracle.npz"), **out)
+    print("fq_oracle.npz:", len(out), "arrays")
+
+
 if __name__ == "__main__":
     O.build()
     ref_tables()
     kiss_gst()
     e2e_oracle()
+    fq_oracle()

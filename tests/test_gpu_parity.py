@@ -310,6 +310,83 @@ def test_rfft_strided_layout(pkg, oracle, torch_cuda):
         assert rel_l2(got, ref) < REL_L2
 
 
+# ------------------------------------------------------------------ FrameQueue framing
+def _fq_plan(pkg, n, h, center, pm, aw):
+    return pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.FRAMEQUEUE, center=bool(center),
+                    pad_mode=pm, analysis_window=bool(aw))
+
+
+def test_framequeue_golden(pkg, torch_cuda, fq_gold):
+    """FrameQueue-framed round trips (centre padding in all three pad modes,
+    with and without the analysis window) vs the pinned oracle fixtures; the
+    per-frame synthesis input too, and the OLA stage bit-exact."""
+    torch = torch_cuda
+    names = sorted({k.split("/")[0] for k in fq_gold.files})
+    for name in names:
+        n, h, c, pm, aw, S, T = (int(v) for v in fq_gold[f"{name}/meta"])
+        x = fq_gold[f"{name}/x"]
+        plan = _fq_plan(pkg, n, h, c, pm, aw)
+        F = fq_gold[f"{name}/frames"].shape[1]
+        assert plan.frame_count(T) == F, name
+        xd = dev(torch, x)
+        y = host(plan.roundtrip(xd))
+        xmax = float(np.max(np.abs(x)))
+        for s in range(S):
+            assert_close(y[s], fq_gold[f"{name}/y"][s], xmax, f"{name}[{s}] y")
+        frames, _ = plan.stages(xd, want_spec=False)
+        frames = host(frames)
+        for s in range(S):
+            assert_close(frames[s], fq_gold[f"{name}/frames"][s], xmax, f"{name}[{s}] frames")
+        yg = host(plan.ola_gather(dev(torch, fq_gold[f"{name}/frames"])))
+        assert np.array_equal(yg, fq_gold[f"{name}/y"]), f"{name} ola_gather"
+
+
+@pytest.mark.parametrize("n,h,pm", [(1024, 256, 1), (1024, 256, 2), (1024, 256, 0), (512, 128, 1),
+                                    (4096, 1024, 1), (2048, 512, 2)])
+def test_framequeue_fused_equals_staged(pkg, oracle, torch_cuda, n, h, pm):
+    """Edge frames go through the padding map in both kernels: fused == staged
+    bit for bit, and both match the oracle on a long stream."""
+    torch = torch_cuda
+    T = 60_001
+    x = oracle.synth_streams(2, T, config_id=300 + pm)
+    plan = _fq_plan(pkg, n, h, 1, pm, 0)
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    frames, _ = plan.stages(xd, want_spec=False)
+    assert np.array_equal(bits(y), bits(host(plan.ola_gather(frames))))
+    ref = oracle.roundtrip_batch_ex(x, n, h, mode=oracle.FRAMEQUEUE, center=True, pad_mode=pm,
+                                    analysis_window=False, nthreads=2)
+    for s in range(2):
+        assert_close(y[s], ref[s], float(np.max(np.abs(x))), f"N={n} H={h} pm={pm} stream {s}")
+
+
+@pytest.mark.parametrize("T", [0, 1, 2, 5, 511, 513, 2048])
+def test_framequeue_short_signals(pkg, oracle, torch_cuda, T):
+    """Signals shorter than the pad: reflect101 bounces several times, edge
+    repeats x[0]/x[T-1], T = 0 gives one all-zero frame (d_x may be NULL)."""
+    torch = torch_cuda
+    n, h = 1024, 256
+    x = oracle.synth(max(T, 1), 40 + T)[:T]
+    for pm in (0, 1, 2):
+        plan = _fq_plan(pkg, n, h, 1, pm, 0)
+        F = oracle.fq_count(T, n, h, True)
+        assert plan.frame_count(T) == F
+        ref = oracle.roundtrip_ex(x, n, h, mode=oracle.FRAMEQUEUE, center=True, pad_mode=pm,
+                                  analysis_window=False)
+        if T == 0:
+            y = torch.empty((1, F * h), device="cuda")
+            pkg._check(pkg.lib().crlot_roundtrip(plan._h, None, y.data_ptr(), 1, 0, 0, F * h, 0))
+            torch.cuda.synchronize()
+            y = host(y)
+        else:
+            y = host(plan.roundtrip(dev(torch, x[None])))
+        assert y.shape == (1, F * h)
+        # the output window can hold only rounding noise (T=2: the samples sit at
+        # padded 512..513, beyond F*H = 256), so scale the error by ||x||
+        xs = max(float(np.max(np.abs(x))) if T else 1.0, 1e-3)
+        assert_close(y[0], ref, xs, f"T={T} pm={pm}", xnorm=float(np.linalg.norm(x)) if T else 1.0)
+
+
 # ------------------------------------------------------------------ complex domain
 @pytest.mark.parametrize("n", [128, 256, 512, 1024, 2048])
 def test_complex_fft_vs_oracle(pkg, oracle, torch_cuda, n):

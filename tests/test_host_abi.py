@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol(pkg):
                          text=True, check=True).stdout
     exported = set(re.findall(r"\b(crlot_[a-z0-9_]+)\b", out))
     assert set(syms) <= exported
-    assert L.crlot_abi_version() == 1
+    assert L.crlot_abi_version() == 2
 
 
 def test_library_has_gfx950_code_object(pkg):
@@ -86,6 +86,8 @@ def test_window_rejects_like_reference(pkg):
     (dict(frame_size=513), RuntimeError),        # MakeFftPlan: odd N (kissfft_adapter.cc:44-46)
     (dict(frame_size=1000, hop_size=250), NotImplementedError),  # not a GPU-path size
     (dict(window_type=4), ValueError),           # BLACKMAN_HARRIS
+    (dict(boundary_mode=2, pad_mode=7), ValueError),  # unknown dsp::PadMode
+    (dict(boundary_mode=3), ValueError),
 ])
 def test_plan_validation_before_device(pkg, kw, exc):
     cfg = dict(frame_size=1024, hop_size=256)
@@ -108,4 +110,4 @@ def test_fft_plan_validation_before_device(pkg, domain, nfft, exc):
 
 def test_struct_layout_matches_header(pkg):
     assert C.sizeof(pkg.FftDesc) == 3 * 4
-    assert C.sizeof(pkg.PlanDesc) == 12 * 4
+    assert C.sizeof(pkg.PlanDesc) == 14 * 4

@@ -101,6 +101,49 @@ def test_framer_counts_match_formula(oracle, ref_tables):
             assert fr.size // 1024 == oracle.frame_count(T, 1024, 256, mode)
 
 
+# ----------------------------------------------------------------- FrameQueue
+def _fq_cases(ref_tables):
+    for key in sorted(ref_tables.files):
+        if key.startswith("fq_") and key.endswith("_meta"):
+            base = key[:-5]
+            T, N, H, c, m, F = (int(v) for v in ref_tables[key])
+            yield base, T, N, H, c, m, F
+
+
+def test_framequeue_bit_exact_vs_reference(oracle, ref_tables):
+    """FrameQueue.cc / Indexing.h restatement vs the reference's own FrameQueue
+    (ref_dump): frame counts and every frame value, all pad modes, centre on/off,
+    signals shorter than the pad (multi-bounce reflect101), T = 0."""
+    n = 0
+    for base, T, N, H, c, m, F in _fq_cases(ref_tables):
+        x = ref_tables[base + "_x"]
+        assert oracle.fq_count(T, N, H, bool(c)) == F, base
+        got = oracle.fq_frames(x, N, H, bool(c), m)
+        assert np.array_equal(got.reshape(-1), ref_tables[base + "_frames"]), base
+        n += 1
+    assert n == 48
+
+
+def test_reflect101_is_the_reference_mixed_rule(oracle):
+    """Indexing.h:18-37 as written: the left side reflects about -1/2 (-1 -> 0),
+    the right side about n-1 (n -> n-2); the doc comment's example differs."""
+    L = oracle.lib()
+    assert [L.or_fq_reflect101(i, 4) for i in range(-4, 8)] == [3, 2, 1, 0, 0, 1, 2, 3, 2, 1, 0, 0]
+    assert L.or_fq_reflect101(-9, 1) == 0 and L.or_fq_reflect101(5, 0) == 0
+
+
+def test_framequeue_golden_reproduces(oracle, fq_gold):
+    names = sorted({k.split("/")[0] for k in fq_gold.files})
+    for name in names:
+        n, h, c, pm, aw, S, T = (int(v) for v in fq_gold[f"{name}/meta"])
+        x = fq_gold[f"{name}/x"]
+        for s in range(S):
+            y, fr = oracle.roundtrip_ex(x[s], n, h, mode=oracle.FRAMEQUEUE, center=bool(c),
+                                        pad_mode=pm, analysis_window=bool(aw), want_frames=True)
+            assert np.array_equal(y, fq_gold[f"{name}/y"][s]), name
+            assert np.array_equal(fr, fq_gold[f"{name}/frames"][s]), name
+
+
 # ----------------------------------------------------------------- kissfft
 def test_kissfft_bit_exact_vs_independent_build(oracle, kiss_gst):
     for key in kiss_gst.files:
