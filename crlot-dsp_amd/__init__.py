@@ -70,6 +70,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build()")
+    # torch ships its own libamdhip64.so.7 and loads it by path; if this library
+    # bound /opt/rocm's copy first, the process would hold two HIP runtimes
+    # that do not share devices, streams or allocations.  Load torch's first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i32, i64, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
     fp = C.POINTER(C.c_float)
@@ -102,6 +109,16 @@ def lib():
         "crlot_stream_reset": ([vp], C.c_int),
         "crlot_stream_push_hop": ([vp, vp, vp, C.POINTER(i32), vp], C.c_int),
         "crlot_stream_set_layout": ([vp, i32], C.c_int),
+        "crlot_wav_reader_open": ([C.c_char_p, C.POINTER(vp)], C.c_int),
+        "crlot_wav_reader_close": ([vp], None),
+        "crlot_wav_reader_info": ([vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                   C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(i32)],
+                                  C.c_int),
+        "crlot_wav_reader_read": ([vp, fp, C.c_uint64, C.POINTER(C.c_uint64)], C.c_int),
+        "crlot_wav_writer_open": ([C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, i32,
+                                   C.POINTER(vp)], C.c_int),
+        "crlot_wav_writer_write": ([vp, fp, C.c_uint64, C.POINTER(C.c_uint64)], C.c_int),
+        "crlot_wav_writer_close": ([vp], C.c_int),
         "crlot_window_table": ([i32, i64, i32, i32, fp], C.c_int),
         "crlot_ring_len": ([i64, i64], i64),
         "crlot_norm_table": ([fp, i64, i64, i64, i32, f32, fp], C.c_int),
@@ -224,7 +241,11 @@ class Plan:
             lib().crlot_plan_destroy(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
     # -- sizes
     def frame_count(self, T: int) -> int:
@@ -345,7 +366,11 @@ class FftPlan:
             lib().crlot_fft_plan_destroy(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def size(self) -> int:
         return self.nfft
@@ -408,7 +433,11 @@ class Stream:
             lib().crlot_stream_destroy(self._h)
             self._h = None
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
     def reset(self):
         _check(lib().crlot_stream_reset(self._h))
@@ -426,3 +455,129 @@ class Stream:
         _check(lib().crlot_stream_push_hop(self._h, hop.data_ptr(), out.data_ptr(), C.byref(em), s),
                "crlot_stream_push_hop")
         return out, em.value
+
+
+# ----------------------------------------------------------------- WAV I/O
+class WavReader:
+    """io/wav.h WavReader (host): open() -> bool, read_all() -> interleaved float32."""
+
+    def __init__(self):
+        self._h = None
+        self.last_error = ""
+
+    def open(self, filename) -> bool:
+        self.close()
+        h = C.c_void_p()
+        rc = lib().crlot_wav_reader_open(os.fsencode(filename), C.byref(h))
+        if rc == ERUNTIME:
+            self.last_error = lib().crlot_last_error().decode(errors="replace")
+            return False
+        _check(rc, "crlot_wav_reader_open")
+        self._h = h
+        ch, sr, bps = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        tf, fl = C.c_uint64(), C.c_int32()
+        _check(lib().crlot_wav_reader_info(h, C.byref(ch), C.byref(sr), C.byref(tf), C.byref(bps),
+                                           C.byref(fl)))
+        self._info = (ch.value, sr.value, tf.value, bps.value, bool(fl.value))
+        return True
+
+    def close(self):
+        if self._h:
+            lib().crlot_wav_reader_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def is_open(self) -> bool:
+        return bool(self._h)
+
+    def get_channels(self) -> int:
+        return self._info[0] if self._h else 0
+
+    def get_sample_rate(self) -> int:
+        return self._info[1] if self._h else 0
+
+    def get_total_frames(self) -> int:
+        return self._info[2] if self._h else 0
+
+    def get_bits_per_sample(self) -> int:
+        return self._info[3] if self._h else 0
+
+    def read(self, frames: int) -> np.ndarray:
+        """Next `frames` frames (fewer at the end), interleaved float32."""
+        if not self._h:
+            return np.zeros(0, np.float32)
+        out = np.zeros(max(frames, 0) * self.get_channels(), np.float32)
+        got = C.c_uint64()
+        _check(lib().crlot_wav_reader_read(self._h, _fptr(out) if out.size else None, frames,
+                                           C.byref(got)), "crlot_wav_reader_read")
+        return out[:got.value * self.get_channels()]
+
+    def read_all(self) -> np.ndarray:
+        return self.read(self.get_total_frames())
+
+
+class WavWriter:
+    """io/wav.h WavWriter (host): open(path, channels, sample_rate, bits=16, float_format=False)."""
+
+    def __init__(self):
+        self._h = None
+        self.last_error = ""
+
+    def open(self, filename, channels: int, sample_rate: int, bits_per_sample: int = 16,
+             float_format: bool = False) -> bool:
+        self.close()
+        h = C.c_void_p()
+        rc = lib().crlot_wav_writer_open(os.fsencode(filename), channels, sample_rate,
+                                         bits_per_sample, int(float_format), C.byref(h))
+        if rc == ERUNTIME:
+            self.last_error = lib().crlot_last_error().decode(errors="replace")
+            return False
+        _check(rc, "crlot_wav_writer_open")
+        self._h = h
+        self.channels = channels
+        return True
+
+    def write(self, data) -> int:
+        """Interleaved float32 frames; returns the frames written."""
+        if not self._h:
+            return 0
+        a = np.ascontiguousarray(data, np.float32).reshape(-1)
+        frames = a.size // self.channels
+        put = C.c_uint64()
+        _check(lib().crlot_wav_writer_write(self._h, _fptr(a) if a.size else None, frames,
+                                            C.byref(put)), "crlot_wav_writer_write")
+        return put.value
+
+    def close(self):
+        if self._h:
+            h, self._h = self._h, None
+            _check(lib().crlot_wav_writer_close(h), "crlot_wav_writer_close")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def is_open(self) -> bool:
+        return bool(self._h)
+
+
+def load_wav_mono(filename) -> tuple[np.ndarray, int]:
+    """WavReader.read_all() mixed down to mono the way main/main.cc:155-160 does
+    (sum the channels in float, divide by the channel count); returns (x, rate)."""
+    r = WavReader()
+    if not r.open(filename):
+        raise RuntimeError(r.last_error)
+    ch, sr = r.get_channels(), r.get_sample_rate()
+    pcm = r.read_all().reshape(-1, ch)
+    r.close()
+    acc = np.zeros(pcm.shape[0], np.float32)
+    for c in range(ch):
+        acc = (acc + pcm[:, c]).astype(np.float32)
+    return (acc / np.float32(ch)).astype(np.float32), sr

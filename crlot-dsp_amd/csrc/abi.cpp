@@ -135,6 +135,10 @@ bool aligned8(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 7u) 
 
 }  // namespace
 
+namespace crlot {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace crlot
+
 extern "C" {
 
 const char* crlot_last_error(void) { return g_err.c_str(); }

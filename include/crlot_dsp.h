@@ -201,6 +201,27 @@ int crlot_stream_set_layout(crlot_stream* st, int32_t interleaved);
 int crlot_stream_push_hop(crlot_stream* st, const float* d_hop_in, float* d_hop_out,
                           int32_t* emitted, void* stream);
 
+/* ---------------------------------------------------------------- WAV I/O
+ * io/wav.{h,cc} (WavReader / WavWriter over dr_wav): RIFF WAVE, 1 or 2
+ * channels, 16/24/32-bit PCM or 32-bit IEEE float (wav.cc:26-55 guards; a
+ * rejected file is CRLOT_ERUNTIME, the reference's `false`).  Samples are
+ * interleaved float frames with dr_wav's conversions: s16 * 2^-15,
+ * s24 * 2^-23, s32 / 2^31 on read; drwav_f32_to_s16 / the reference's 24-bit
+ * packer (wav.cc:233-246) / 2^31 * x (clamped) on write.  Host memory only. */
+typedef struct crlot_wav_reader crlot_wav_reader;
+typedef struct crlot_wav_writer crlot_wav_writer;
+int crlot_wav_reader_open(const char* path, crlot_wav_reader** out);
+void crlot_wav_reader_close(crlot_wav_reader* r);
+int crlot_wav_reader_info(const crlot_wav_reader* r, uint32_t* channels, uint32_t* sample_rate,
+                          uint64_t* total_frames, uint32_t* bits_per_sample, int32_t* is_float);
+/* reads up to `frames` frames from the current position; *frames_read < frames at the end */
+int crlot_wav_reader_read(crlot_wav_reader* r, float* out, uint64_t frames, uint64_t* frames_read);
+int crlot_wav_writer_open(const char* path, uint32_t channels, uint32_t sample_rate,
+                          uint32_t bits_per_sample, int32_t float_format, crlot_wav_writer** out);
+int crlot_wav_writer_write(crlot_wav_writer* w, const float* in, uint64_t frames, uint64_t* written);
+/* patches the RIFF/data sizes and closes the file */
+int crlot_wav_writer_close(crlot_wav_writer* w);
+
 /* ---------------------------------------------------------------- host tables
  * The reference's table builders, restated in the product's host code
  * (bit-exact with WindowLUT.cc / norm_builder.cc / OLAAccumulator.cc). */

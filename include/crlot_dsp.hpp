@@ -6,6 +6,7 @@
 //   crlot::dsp::fft::IFftPlan      <- dsp::fft::IFftPlan    (fft_api.h:26-48)
 //   crlot::dsp::fft::HipFftPlan    <- KissFftPlan (kissfft_adapter.cc:11-264), Real + Complex
 //   crlot::dsp::fft::MakeFftPlan   <- dsp::fft::MakeFftPlan (fft_api.h:51), HIP-backed
+//   crlot::io::WavReader/WavWriter <- WavReader / WavWriter  (io/wav.h:11-72)
 //   crlot::StftEngine              <- the Framer -> window -> FFT -> iFFT -> OLA loop
 //                                     of bench/e2e_benchmark.cc:138-186, batched
 // Error codes become the reference's exception types: CRLOT_EINVAL ->
@@ -150,6 +151,84 @@ class StftEngine {
     Plan plan_;
     DeviceBuffer<float> dx_, dy_;
 };
+
+// io/wav.h WavReader / WavWriter (same methods; open() returns false on a
+// file the reference would reject, crlot_last_error() says why).
+namespace io {
+
+class WavReader {
+   public:
+    WavReader() = default;
+    ~WavReader() { close(); }
+    WavReader(const WavReader&) = delete;
+    WavReader& operator=(const WavReader&) = delete;
+    bool open(const std::string& filename) {
+        close();
+        if (crlot_wav_reader_open(filename.c_str(), &r_) != CRLOT_OK) return false;
+        crlot_wav_reader_info(r_, &ch_, &rate_, &frames_, &bits_, nullptr);
+        return true;
+    }
+    void close() {
+        if (r_) crlot_wav_reader_close(r_);
+        r_ = nullptr;
+    }
+    bool read(float* buffer, size_t frames_to_read, size_t* frames_read = nullptr) {
+        if (!r_) return false;
+        uint64_t got = 0;
+        if (crlot_wav_reader_read(r_, buffer, frames_to_read, &got) != CRLOT_OK) return false;
+        if (frames_read) *frames_read = size_t(got);
+        return got > 0 || frames_to_read == 0;
+    }
+    std::vector<float> read_all() {
+        if (!r_) return {};
+        std::vector<float> v(size_t(frames_) * ch_);
+        uint64_t got = 0;
+        if (!v.empty()) crlot_wav_reader_read(r_, v.data(), frames_, &got);
+        v.resize(size_t(got) * ch_);
+        return v;
+    }
+    uint32_t get_channels() const { return r_ ? ch_ : 0; }
+    uint32_t get_sample_rate() const { return r_ ? rate_ : 0; }
+    uint64_t get_total_frames() const { return r_ ? frames_ : 0; }
+    uint32_t get_bits_per_sample() const { return r_ ? bits_ : 0; }
+    bool is_open() const { return r_ != nullptr; }
+
+   private:
+    crlot_wav_reader* r_ = nullptr;
+    uint32_t ch_ = 0, rate_ = 0, bits_ = 0;
+    uint64_t frames_ = 0;
+};
+
+class WavWriter {
+   public:
+    WavWriter() = default;
+    ~WavWriter() { close(); }
+    WavWriter(const WavWriter&) = delete;
+    WavWriter& operator=(const WavWriter&) = delete;
+    bool open(const std::string& filename, uint32_t channels, uint32_t sample_rate,
+              uint32_t bits_per_sample = 16, bool float_format = false) {
+        close();
+        return crlot_wav_writer_open(filename.c_str(), channels, sample_rate, bits_per_sample,
+                                     float_format, &w_) == CRLOT_OK;
+    }
+    void close() {
+        if (w_) crlot_wav_writer_close(w_);
+        w_ = nullptr;
+    }
+    bool write(const float* buffer, size_t frames_to_write, size_t* frames_written = nullptr) {
+        if (!w_) return false;
+        uint64_t put = 0;
+        const int rc = crlot_wav_writer_write(w_, buffer, frames_to_write, &put);
+        if (frames_written) *frames_written = size_t(put);
+        return rc == CRLOT_OK && put == frames_to_write;
+    }
+    bool is_open() const { return w_ != nullptr; }
+
+   private:
+    crlot_wav_writer* w_ = nullptr;
+};
+
+}  // namespace io
 
 namespace dsp {
 

@@ -13,6 +13,10 @@
 using namespace crlot::dsp;
 using namespace crlot::dsp::fft;
 
+#ifndef CRLOT_GOLDEN_DIR
+#define CRLOT_GOLDEN_DIR "tests/golden"  // run from the repository root
+#endif
+
 static int failures = 0;
 #define EXPECT(cond, ...)                                             \
     do {                                                              \
@@ -179,6 +183,33 @@ int main() {
             }
             EXPECT(std::sqrt(num / den) < 1e-6 && mx < 2e-6, "stream %d rel %g max %g", s, std::sqrt(num / den), mx);
         }
+    }
+    // io::WavReader / WavWriter (wav_io_test.cc WriteAndRead) + the oboe fixture
+    {
+        crlot::io::WavReader r;
+        EXPECT(!r.open("nonexistent.wav") && !r.is_open(), "nonexistent");
+        if (r.open(CRLOT_GOLDEN_DIR "/oboe.wav")) {
+            EXPECT(r.get_channels() == 2 && r.get_sample_rate() == 44100 && r.get_bits_per_sample() == 16 &&
+                       r.get_total_frames() == 285315,
+                   "oboe info");
+            EXPECT(r.read_all().size() == 285315u * 2, "oboe read_all");
+        } else {
+            EXPECT(false, "oboe.wav fixture missing");
+        }
+        const char* path = "/tmp/crlot_cpp_wav_test.wav";
+        std::vector<float> d(2 * 1000);
+        for (size_t i = 0; i < d.size(); ++i) d[i] = 0.4f * std::sin(0.01f * float(i));
+        crlot::io::WavWriter w;
+        size_t put = 0;
+        EXPECT(w.open(path, 2, 48000, 24) && w.write(d.data(), 1000, &put) && put == 1000, "wav write");
+        w.close();
+        crlot::io::WavReader r2;
+        EXPECT(r2.open(path) && r2.get_total_frames() == 1000 && r2.get_bits_per_sample() == 24, "wav reopen");
+        auto back = r2.read_all();
+        float mx = 0;
+        for (size_t i = 0; i < d.size(); ++i) mx = std::fmax(mx, std::fabs(back[i] - d[i]));
+        EXPECT(back.size() == d.size() && mx < 1e-4f, "24-bit round trip %g", mx);
+        std::remove(path);
     }
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "OK", failures);
     return failures ? 1 : 0;

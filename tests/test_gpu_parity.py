@@ -387,6 +387,21 @@ def test_framequeue_short_signals(pkg, oracle, torch_cuda, T):
         assert_close(y[0], ref, xs, f"T={T} pm={pm}", xnorm=float(np.linalg.norm(x)) if T else 1.0)
 
 
+def test_oboe_wav_roundtrip(pkg, oracle, torch_cuda):
+    """BASELINE config 1's input (the reference's assets/oboe.wav) read by the
+    product's WavReader, mixed to mono like main.cc, through the device round
+    trip: parity with the oracle on a real recording."""
+    import os
+    torch = torch_cuda
+    x, sr = pkg.load_wav_mono(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                           "oboe.wav"))
+    assert sr == 44100 and x.size == 285315
+    plan = pkg.Plan(frame_size=1024, hop_size=256)
+    y = host(plan.roundtrip(dev(torch, x[None])))[0]
+    ref = oracle.roundtrip(x, 1024, 256)
+    assert_close(y, ref, float(np.max(np.abs(x))), "oboe")
+
+
 # ------------------------------------------------------------------ complex domain
 @pytest.mark.parametrize("n", [128, 256, 512, 1024, 2048])
 def test_complex_fft_vs_oracle(pkg, oracle, torch_cuda, n):
@@ -495,7 +510,7 @@ def test_cpp_api_binary(torch_cuda):
     exe = os.path.join(root, "tests", "cpp", "test_cpp_api")
     if not os.path.exists(exe):
         subprocess.run(["make", "-C", os.path.join(root, "tests", "cpp")], check=True)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, cwd=root)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout
 
