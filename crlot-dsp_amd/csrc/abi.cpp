@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -34,6 +35,9 @@ struct crlot_plan {
     float* d_tw = nullptr;
     float* d_st = nullptr;
     float* d_gain = nullptr;
+    float* d_wsn = nullptr;   // ws * (1/N)
+    float* d_rden = nullptr;  // RN(1 / den)
+    bool fast_ok = false;     // both exact rewrites valid for the current tables
     // staged-path workspace
     float* d_work = nullptr;
     int64_t work_bytes = 0;
@@ -74,13 +78,22 @@ crlot::DevTables tables(const crlot_plan* p) {
     t.tw = p->d_tw;
     t.st = p->d_st;
     t.gain = p->has_gain ? p->d_gain : nullptr;
+    static const bool exact_div = [] {
+        const char* e = std::getenv("CRLOT_EXACT_DIV");
+        return e && e[0] == '1';
+    }();
+    if (p->fast_ok && !exact_div) {
+        t.wsn = p->d_wsn;
+        t.rden = p->d_rden;
+    }
     return t;
 }
 
 void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
-    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work})
+    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
+                     p->d_rden})
         if (q) (void)hipFree(q);
     delete p;
 }
@@ -98,11 +111,26 @@ int upload_window_tables(crlot_plan* p) {
     const float eps = p->desc.eps;
     for (size_t i = 0; i < den.size(); ++i)
         den[i] = (p->norm[i] > eps) ? p->norm[i] : eps;  // kernels.cc:32
+    // Exact rewrites of the fused kernels (kernels.hip mk_div / sanit_scaled):
+    // ws * 2^-k must be exact (zero or normal) and den must lie in [2^-40, 2^40].
+    std::vector<float> wsn(n), rden(den.size());
+    bool ok = is_pow2(n);
+    for (int i = 0; i < n; ++i) {
+        wsn[i] = ws[i] * p->geo.inv_n;
+        if (ws[i] != 0.0f && !(std::fabs(wsn[i]) >= 0x1p-126f)) ok = false;
+    }
+    for (size_t i = 0; i < den.size(); ++i) {
+        if (!(den[i] >= 0x1p-40f && den[i] <= 0x1p40f)) ok = false;
+        rden[i] = 1.0f / den[i];
+    }
     hipError_t e;
     if ((e = hipMemcpy(p->d_wa, wa.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
         (e = hipMemcpy(p->d_ws, ws.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(p->d_den, den.data(), sizeof(float) * den.size(), hipMemcpyHostToDevice)))
+        (e = hipMemcpy(p->d_den, den.data(), sizeof(float) * den.size(), hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(p->d_wsn, wsn.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
+        (e = hipMemcpy(p->d_rden, rden.data(), sizeof(float) * den.size(), hipMemcpyHostToDevice)))
         return hip_fail(e, "hipMemcpy(tables)");
+    p->fast_ok = ok;
     return CRLOT_OK;
 }
 
@@ -223,7 +251,9 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         (e = hipMalloc(&p->d_den, sizeof(float) * ring)) ||
         (e = hipMalloc(&p->d_tw, sizeof(float) * (tw.size() + 2))) ||
         (e = hipMalloc(&p->d_st, sizeof(float) * 2 * P)) ||
-        (e = hipMalloc(&p->d_gain, sizeof(float) * (P + 1)))) {
+        (e = hipMalloc(&p->d_gain, sizeof(float) * (P + 1))) ||
+        (e = hipMalloc(&p->d_wsn, sizeof(float) * n)) ||
+        (e = hipMalloc(&p->d_rden, sizeof(float) * ring))) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }

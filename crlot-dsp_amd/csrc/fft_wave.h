@@ -363,6 +363,19 @@ __device__ __forceinline__ float sanit(float v) {
     return (a >= 1e-30f && a <= 3.402823466e+38f) ? v : 0.0f;
 }
 
+// sanit(v * 2^-k) == sanit_scaled<2^k>(v) * 2^-k exactly (v * 2^-k is exact for
+// every v the threshold keeps; inf/NaN still map to 0): lets the fused kernels
+// fold the inverse's 1/N into the synthesis window.
+template <int NPOW2>
+__device__ __forceinline__ float sanit_scaled(float v) {
+#ifdef CRLOT_ABL_NOSANIT
+    return v;
+#endif
+    constexpr float lo = 1e-30f * float(NPOW2);
+    const float a = __builtin_fabsf(v);
+    return (a >= lo && a <= 3.402823466e+38f) ? v : 0.0f;
+}
+
 // ------------------------------------------------------------- real split
 // Given Z = FFT_P(z) lane-major in v, produce the spectrum X[k] (k = 0..P) of
 // the real 2P-point frame (kiss_fftr), apply the optional real per-bin gain

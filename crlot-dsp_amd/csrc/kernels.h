@@ -16,6 +16,10 @@ struct DevTables {
     const float* tw = nullptr;   // per-pass Stockham twiddles (build_pass_twiddles)
     const float* st = nullptr;   // exp(-i pi (k/P + 1/2)), k < P, float pairs
     const float* gain = nullptr; // spectral gain [P+1] or nullptr
+    // Exact-rewrite tables of the fused kernels (nullptr when the plan's tables
+    // fall outside the ranges where the rewrites are bit-identical):
+    const float* wsn = nullptr;  // ws * (1/N): folds the inverse's 1/N into the window
+    const float* rden = nullptr; // RN(1 / den): Markstein division
 };
 
 // Per-pass Stockham twiddles for an N-point real frame (P = N/2 complex points),

@@ -51,7 +51,7 @@ struct Lds {
 
 template <int E>
 __device__ __forceinline__ void load_tables(const DevTables& t, cf* tw, cf* st, cf* sth, float* wa,
-                                            float* ws, bool need_windows) {
+                                            float* ws, bool need_windows, const float* ws_src = nullptr) {
     constexpr int P = 64 * E, N = 2 * P;
     const cf* gtw = reinterpret_cast<const cf*>(t.tw);
     const cf* gst = reinterpret_cast<const cf*>(t.st);
@@ -62,9 +62,10 @@ __device__ __forceinline__ void load_tables(const DevTables& t, cf* tw, cf* st, 
         sth[i] = cf{w.r * 0.5f, w.i * 0.5f};  // exact
     }
     if (need_windows) {
+        const float* gws = ws_src ? ws_src : t.ws;
         for (int i = threadIdx.x; i < N; i += kBlock) {
             wa[i] = t.wa[i];
-            ws[i] = t.ws[i];
+            ws[i] = gws[i];
         }
     }
     __syncthreads();
@@ -136,7 +137,20 @@ __device__ __forceinline__ void load_pairs_l(float2 (&dst)[E], __amdgpu_buffer_r
 #ifndef CRLOT_FUSED_MIN_WAVES
 #define CRLOT_FUSED_MIN_WAVES 1
 #endif
-template <int E, int S, int NB, bool HAS_GAIN>
+// Division acc / den by Markstein's correction with r = RN(1/den): exact (equal
+// to the IEEE quotient) for den in [2^-40, 2^40] (host-checked) and acc = 0 or
+// |acc| in [2^-64, 2^64]; any other value sends the whole wave to the IEEE
+// division.  Verified exhaustively over den significands.
+__device__ __forceinline__ bool mk_ok(float a) {
+    const float t = __builtin_fabsf(a);
+    return t <= 0x1p64f && (t >= 0x1p-64f || t == 0.0f);
+}
+__device__ __forceinline__ float mk_div(float a, float d, float r) {
+    const float q = a * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, d, a), r, q);
+}
+
+template <int E, int S, int NB, bool HAS_GAIN, bool FAST = false>
 __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fused(const FusedArgs a) {
     constexpr int P = 64 * E, N = 2 * P, H = 128 * S;
     static_assert(NB * S == E, "N = NB * H");
@@ -147,7 +161,7 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
     float* wa = reinterpret_cast<float*>(sth + P);
     float* ws = wa + N;
     cf* bufs = reinterpret_cast<cf*>(ws + N);
-    load_tables<E>(a.t, tw, st, sth, wa, ws, true);
+    load_tables<E>(a.t, tw, st, sth, wa, ws, true, FAST ? a.t.wsn : nullptr);
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -162,6 +176,8 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
     const __amdgpu_buffer_rsrc_t ry =
         dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
+    const __amdgpu_buffer_rsrc_t rr =
+        dev::make_rsrc(FAST ? a.t.rden : a.t.den, uint32_t(a.ring_blocks * H) * 4u);
     const float g = a.gain;
 
 #ifndef CRLOT_TW_REGS
@@ -195,10 +211,13 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
         // end of this iteration, so their latency hides under the transforms
         float2 nxt[E];
         if (k + 1 < f1) load_pairs_l<E - S, S, E, 64>(nxt, rx, lane, (k + 1) * H - a.pad, a.T, a.pad_mode);
-        float2 dn[S];
+        float2 dn[S], rn[S];
         if (k >= f0) {
 #pragma unroll
-            for (int q = 0; q < S; ++q) dn[q] = dev::bload2(rd, lane * 8 + q * 512, (k % a.ring_blocks) * H * 4);
+            for (int q = 0; q < S; ++q) {
+                dn[q] = dev::bload2(rd, lane * 8 + q * 512, (k % a.ring_blocks) * H * 4);
+                if constexpr (FAST) rn[q] = dev::bload2(rr, lane * 8 + q * 512, (k % a.ring_blocks) * H * 4);
+            }
         }
         // analysis window (harness: frame[i] * w[i]) + forward sanitize
         cf v[E];
@@ -229,14 +248,31 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
 #else
             const float2 w = *reinterpret_cast<const float2*>(ws + 2 * (lane + 64 * m));
 #endif
-            const float o0 = dev::sanit(v[m].r * a.inv_n);
-            const float o1 = dev::sanit(v[m].i * a.inv_n);
+            // FAST: w = ws / N and the 1/N is folded out of the sanitize (exact)
+            const float o0 = FAST ? dev::sanit_scaled<N>(v[m].r) : dev::sanit(v[m].r * a.inv_n);
+            const float o1 = FAST ? dev::sanit_scaled<N>(v[m].i) : dev::sanit(v[m].i * a.inv_n);
             float2& r = acc[m / S][m % S];
             r.x = __builtin_fmaf(__builtin_fmaf(o0, w.x, 0.0f), g, r.x);
             r.y = __builtin_fmaf(__builtin_fmaf(o1, w.y, 0.0f), g, r.y);
         }
         // block k is complete: produce(H) = acc / max(norm, eps)
-        if (k >= f0) {
+        if (FAST && k >= f0) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < S; ++q) ok = ok && mk_ok(acc[0][q].x) && mk_ok(acc[0][q].y);
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+#pragma unroll
+                for (int q = 0; q < S; ++q)
+                    dev::bstore2(make_float2(mk_div(acc[0][q].x, dn[q].x, rn[q].x),
+                                             mk_div(acc[0][q].y, dn[q].y, rn[q].y)),
+                                 ry, lane * 8 + q * 512, k * H * 4);
+            } else {
+#pragma unroll
+                for (int q = 0; q < S; ++q)
+                    dev::bstore2(make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y), ry,
+                                 lane * 8 + q * 512, k * H * 4);
+            }
+        } else if (k >= f0) {
 #pragma unroll
             for (int q = 0; q < S; ++q)
 #ifdef CRLOT_ABL_NODIV  // timing-only ablation
@@ -698,7 +734,13 @@ int e_of(int n) {
 template <int E, int S>
 hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     constexpr int NB = E / S;
-    auto k = a.t.gain ? k_stft_ola_fused<E, S, NB, true> : k_stft_ola_fused<E, S, NB, false>;
+#ifdef CRLOT_NO_FAST  // A/B builds
+    const bool fast = false;
+#else
+    const bool fast = a.t.wsn && a.t.rden;
+#endif
+    auto k = a.t.gain ? (fast ? k_stft_ola_fused<E, S, NB, true, true> : k_stft_ola_fused<E, S, NB, true, false>)
+                      : (fast ? k_stft_ola_fused<E, S, NB, false, true> : k_stft_ola_fused<E, S, NB, false, false>);
     const size_t lds = Lds<E>::bytes;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;

@@ -131,6 +131,23 @@ def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
     assert np.array_equal(bits(y_unaligned), bits(y_fused))
 
 
+@pytest.mark.parametrize("scale", [1e-25, 1e25, 1.0])
+def test_fused_fast_division_and_fold_exact(pkg, oracle, torch_cuda, scale):
+    """The fused kernel's exact rewrites (1/N folded into the window, Markstein
+    division with a per-wave IEEE fallback) give the staged path's bits: tiny and
+    huge accumulators exercise the fallback, unit scale the fast path."""
+    torch = torch_cuda
+    T = 50_000
+    x = (oracle.synth_streams(2, T, config_id=91) * np.float32(scale)).astype(np.float32)
+    x[0, 1000:1100] = 0.0  # exact zeros inside a stream
+    for n, h in ((1024, 256), (512, 128)):
+        plan = pkg.Plan(frame_size=n, hop_size=h)
+        xd = dev(torch, x)
+        y = host(plan.roundtrip(xd))
+        frames, _ = plan.stages(xd, want_spec=False)
+        assert np.array_equal(bits(y), bits(host(plan.ola_gather(frames)))), (n, scale)
+
+
 def test_ola_gather_bit_exact_random_frames(pkg, oracle, torch_cuda):
     """OLAAccumulator given identical frames: bit-exact (push_frame_AoS + produce(H))."""
     torch = torch_cuda
