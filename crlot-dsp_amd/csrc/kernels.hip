@@ -20,6 +20,7 @@
 // update fma(fma(src, w, 0), g, dst) (kernels.cc:24-28) and the IEEE division
 // acc / max(norm, eps) (kernels.cc:30-36).  Built with -ffp-contract=off and
 // the default correctly-rounded f32 division; subnormals are preserved.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 
@@ -768,6 +769,38 @@ hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) 
     return hipErrorInvalidValue;
 }
 
+// Waves of K_fused the device holds at once: 4 per SIMD (<= 128 VGPRs), 4 SIMDs
+// per CU.
+int fused_resident_waves() {
+    static const int v = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        return 16 * cus;
+    }();
+    return v;
+}
+
+// Split each stream's F frames into n chunks (one wave each; NB-1 halo frames
+// recomputed per chunk).  Measured on MI355X (scripts/sweep_chunks.sh): ~128-frame
+// chunks are right while the grid is several resident rounds deep (headline:
+// flat for 12..24 chunks), but a small batch must still fill the device -- at
+// least one resident round of waves, two when chunks stay >= 48 frames (config 2:
+// +5 %, config 4 batched: +20 % over fixed 128-frame chunks).
+void choose_chunks(int64_t F, int n_streams, int nb, int resident, int& n_chunks, int& m) {
+    (void)nb;
+    const int64_t S = std::max(1, n_streams);
+    int64_t n = (F + 127) / 128;
+    n = std::max<int64_t>(n, (resident + S - 1) / S);
+    const int64_t two = (2 * resident + S - 1) / S;
+    if (two > n && F / two >= 48) n = two;
+    n = std::max<int64_t>(1, std::min<int64_t>(n, std::max<int64_t>(1, F / 32)));
+    m = int((F + n - 1) / n);
+    n_chunks = int((F + m - 1) / m);
+}
+
 // frames per workgroup walk (halo NB-1 frames recomputed); CRLOT_WG_CHUNK overrides
 int wg_chunk_target() {
     static const int v = [] {
@@ -821,11 +854,19 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.out_len = int(out_len);
     a.n_streams = n_streams;
     a.F = int(F);
-    // chunk length: ~128 frames per wave (halo NB-1 frames recomputed), evened out
+#ifdef CRLOT_OLD_CHUNKS  // A/B builds: fixed ~128-frame chunks
     const int target = 128;
     a.n_chunks = int((F + target - 1) / target);
     a.M = int((F + a.n_chunks - 1) / a.n_chunks);
     a.n_chunks = int((F + a.M - 1) / a.M);
+#else
+    choose_chunks(F, n_streams, g.n / g.h, fused_resident_waves(), a.n_chunks, a.M);
+    if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
+        const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
+        a.M = int((F + n - 1) / n);
+        a.n_chunks = int((F + a.M - 1) / a.M);
+    }
+#endif
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
     a.pad_mode = g.pad_mode;

@@ -4,6 +4,7 @@ algorithmic HBM fraction (8 B/sample vs 8 TB/s)."""
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -30,16 +31,22 @@ def main():
         g = torch.Generator(device="cuda").manual_seed(1)
         x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
         y = torch.empty((S, plan.output_length(T)), device="cuda")
-        for _ in range(2):
+        # warm up for >= 200 ms (clocks ramp), then the median of 5 groups of 10
+        t_end = time.perf_counter() + 0.2
+        while time.perf_counter() < t_end:
             plan.roundtrip(x, y)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 10
-        e0.record()
-        for _ in range(reps):
-            plan.roundtrip(x, y)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / reps
+            torch.cuda.synchronize()
+        groups = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 10
+            e0.record()
+            for _ in range(reps):
+                plan.roundtrip(x, y)
+            e1.record()
+            torch.cuda.synchronize()
+            groups.append(e0.elapsed_time(e1) / reps)
+        ms = sorted(groups)[len(groups) // 2]
         rate = S * T / (ms * 1e-3)
         print(json.dumps({"config": name, "ms": round(ms, 4), "Msamples_s": round(rate / 1e6, 1),
                           "hbm_frac_algorithmic": round(8 * rate / 8e12, 4)}), flush=True)
