@@ -45,7 +45,7 @@ def flop_per_sample(n: int, h: int) -> float:
     return 2 * 2.5 * n * math.log2(n) / h + 6
 
 
-def cpu_baseline(n_streams: int = 256, threads: int = 16):
+def cpu_baseline(n_streams: int = 1024, threads: int = 16):
     """Oracle restatement of the reference CPU path on this host (kind "port")."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -80,7 +80,7 @@ def cpu_baseline(n_streams: int = 256, threads: int = 16):
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n_streams} of the 1024 streams x {T_LEN} samples, {threads} pthreads, "
+        "sample": f"{n_streams} of the 1024 streams x {T_LEN} samples (the N=1 workload), {threads} pthreads, "
                   f"oracle/crlot_oracle.c -O3{' -march=native' if native else ''} "
                   f"(kissfft-algorithm + scalar-FMA OLA restatement), {dt:.2f} s",
         "single_thread_value": round(4 * T_LEN / dt1 / 1e6, 3),

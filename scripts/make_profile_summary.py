@@ -53,10 +53,24 @@ if tr:
     for r in csv.DictReader(open(tr[0])):
         if "stft_ola_fused" in r["Name"]:
             dur = float(r["AverageNs"])
+# per-dispatch durations of the fused kernel (the stats average includes warm-up launches)
+kname, med, mn = "k_stft_ola_fused", None, None
+kt = glob.glob(f"{src}/trace/run_kernel_trace.csv")
+if kt:
+    ds = []
+    for r in csv.DictReader(open(kt[0])):
+        if "stft_ola_fused" in r["Kernel_Name"]:
+            kname = r["Kernel_Name"]
+            ds.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    if ds:
+        ds.sort()
+        med, mn = ds[len(ds) // 2], ds[0]
 out = {
     "tag": tag,
     "workload_key": f"{S}x{T}_N{N}_H{H}",
-    "kernel": "k_stft_ola_fused<8,2,4,false>",
+    "kernel": kname,
+    "median_duration_ns_trace": med,
+    "min_duration_ns_trace": mn,
     "avg_duration_ns_trace": dur,
     "pmc_per_launch": pmc,
     "algorithmic_bytes_per_launch": alg_read + alg_write,
