@@ -38,6 +38,8 @@ struct crlot_plan {
     float* d_wsn = nullptr;   // ws * (1/N)
     float* d_rden = nullptr;  // RN(1 / den)
     bool fast_ok = false;     // both exact rewrites valid for the current tables
+    bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
+    float* d_twany = nullptr; // W_P^k (generic path)
     // staged-path workspace
     float* d_work = nullptr;
     int64_t work_bytes = 0;
@@ -93,7 +95,7 @@ void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
-                     p->d_rden})
+                     p->d_rden})  // d_twany aliases d_tw
         if (q) (void)hipFree(q);
     delete p;
 }
@@ -196,13 +198,17 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         return fail(CRLOT_EINVAL, "Unknown pad mode");
     if (d.hop_size > d.frame_size)
         return fail(CRLOT_EUNSUPPORTED, "hop larger than frame is not supported on the GPU path");
-    if (!is_pow2(d.frame_size) || d.frame_size < 256 || d.frame_size > 4096)
+    // power-of-two 256..4096: register-resident kernels; any other even size up to
+    // 16384: the mixed-radix path (fft_any.h)
+    const bool generic = !(is_pow2(d.frame_size) && d.frame_size >= 256 && d.frame_size <= 4096);
+    if (generic && (d.frame_size > 16384 || !crlot::any_supported(d.frame_size / 2)))
         return fail(CRLOT_EUNSUPPORTED,
-                    "GPU path supports power-of-two frame sizes 256..4096, got " +
+                    "GPU path supports even frame sizes up to 16384, got " +
                         std::to_string(d.frame_size));
 
     crlot_plan* p = new crlot_plan();
     p->desc = d;
+    p->generic = generic;
     p->boundary = d.boundary_mode;
     if (d.device < 0) {
         if (hipGetDevice(&p->device) != hipSuccess) {
@@ -238,7 +244,7 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     crlot_norm_table(p->window.data(), n, h, ring, d.apply_window_inside, d.eps, p->norm.data());
 
     const int P = n / 2;
-    const std::vector<float> tw = crlot::build_pass_twiddles(n);
+    const std::vector<float> tw = generic ? crlot::build_any_twiddles(P) : crlot::build_pass_twiddles(n);
     std::vector<float> st(2 * P);
     for (int t = 0; t < P; ++t) {
         const double ps = -M_PI * (double(t) / double(P) + 0.5);
@@ -257,6 +263,7 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }
+    if (generic) p->d_twany = p->d_tw;  // the same allocation: W_P^k
     if ((e = hipMemcpy(p->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
         (e = hipMemcpy(p->d_st, st.data(), sizeof(float) * 2 * P, hipMemcpyHostToDevice))) {
         free_plan(p);
@@ -366,7 +373,10 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
     const int64_t need = int64_t(n_streams) * F * p->geo.n * int64_t(sizeof(float));
     int rc = ensure_workspace(p, need);
     if (rc != CRLOT_OK) return rc;
-    e = crlot::launch_synth_frames(p->geo, t, d_x, n_streams, T, ld_x, F, p->d_work, nullptr, s);
+    e = p->generic ? crlot::launch_synth_any(p->geo, t, p->d_twany, d_x, n_streams, T, ld_x, F,
+                                             p->d_work, nullptr, s)
+                   : crlot::launch_synth_frames(p->geo, t, d_x, n_streams, T, ld_x, F, p->d_work,
+                                                nullptr, s);
     if (e != hipSuccess) return hip_fail(e, "synth kernel launch");
     e = crlot::launch_ola_gather(p->geo, t, p->d_work, p->geo.n, d_y, n_streams, F, ld_y,
                                  out_len, s);
@@ -382,8 +392,12 @@ int crlot_roundtrip_stages(crlot_plan* p, const float* d_x, int32_t n_streams, i
     const int64_t F = frames_for(p, T);
     if (F == 0 || n_streams == 0) return CRLOT_OK;
     DeviceGuard g(p->device);
-    hipError_t e = crlot::launch_synth_frames(p->geo, tables(p), d_x, n_streams, T, ld_x, F,
-                                              d_frames, d_spec, static_cast<hipStream_t>(stream));
+    hipError_t e = p->generic
+                       ? crlot::launch_synth_any(p->geo, tables(p), p->d_twany, d_x, n_streams, T,
+                                                 ld_x, F, d_frames, d_spec,
+                                                 static_cast<hipStream_t>(stream))
+                       : crlot::launch_synth_frames(p->geo, tables(p), d_x, n_streams, T, ld_x, F,
+                                                    d_frames, d_spec, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "synth kernel launch");
     return CRLOT_OK;
 }
@@ -413,8 +427,12 @@ int crlot_rfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t b
     if (batch == 0) return CRLOT_OK;
     if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
     DeviceGuard g(p->device);
-    hipError_t e = crlot::launch_rfft(p->geo, tables(p), d_in, d_out, batch, ld_in, inc_in, ld_out,
-                                      inc_out, static_cast<hipStream_t>(stream));
+    hipError_t e = p->generic
+                       ? crlot::launch_fft_any(0, p->geo.n / 2, p->geo.inv_n, tables(p), p->d_twany,
+                                               d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out,
+                                               static_cast<hipStream_t>(stream))
+                       : crlot::launch_rfft(p->geo, tables(p), d_in, d_out, batch, ld_in, inc_in,
+                                            ld_out, inc_out, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "rfft kernel launch");
     return CRLOT_OK;
 }
@@ -427,8 +445,12 @@ int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t 
     if (batch == 0) return CRLOT_OK;
     if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
     DeviceGuard g(p->device);
-    hipError_t e = crlot::launch_irfft(p->geo, tables(p), d_in, d_out, batch, ld_in, inc_in,
-                                       ld_out, inc_out, static_cast<hipStream_t>(stream));
+    hipError_t e = p->generic
+                       ? crlot::launch_fft_any(1, p->geo.n / 2, p->geo.inv_n, tables(p), p->d_twany,
+                                               d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out,
+                                               static_cast<hipStream_t>(stream))
+                       : crlot::launch_irfft(p->geo, tables(p), d_in, d_out, batch, ld_in, inc_in,
+                                             ld_out, inc_out, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "irfft kernel launch");
     return CRLOT_OK;
 }
@@ -452,15 +474,14 @@ int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
     if (d->domain == CRLOT_FFT_REAL && d->nfft % 2 != 0)
         return fail(CRLOT_ERUNTIME, "FFT size must be even for real FFT");
     const bool real = d->domain == CRLOT_FFT_REAL;
-    const int lo = real ? 256 : 128, hi = real ? 4096 : 2048;
-    if (!is_pow2(d->nfft) || d->nfft < lo || d->nfft > hi)
+    const int hi = real ? 16384 : 8192;
+    if (d->nfft < (real ? 2 : 1) || d->nfft > hi)
         return fail(CRLOT_EUNSUPPORTED, std::string(real ? "real" : "complex") +
-                                            " FFT sizes on the GPU path are powers of two " +
-                                            std::to_string(lo) + ".." + std::to_string(hi) +
-                                            ", got " + std::to_string(d->nfft));
+                                            " FFT sizes on the GPU path are 1.." +
+                                            std::to_string(hi) + ", got " + std::to_string(d->nfft));
     crlot_plan_desc pd{};
     pd.frame_size = real ? d->nfft : 2 * d->nfft;
-    pd.hop_size = pd.frame_size / 4;
+    pd.hop_size = pd.frame_size / 4 > 0 ? pd.frame_size / 4 : 1;
     pd.window_type = CRLOT_WIN_RECT;
     pd.device = d->device;
     crlot_plan* inner = nullptr;
@@ -520,8 +541,12 @@ static int cfft_common(crlot_fft_plan* p, const float* d_in, float* d_out, int32
     if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
     const crlot_plan* q = p->inner;
     DeviceGuard g(q->device);
-    hipError_t e = crlot::launch_cfft(q->geo, tables(q), d_in, d_out, batch, ld_in, inc_in, ld_out,
-                                      inc_out, inverse, static_cast<hipStream_t>(stream));
+    hipError_t e = q->generic
+                       ? crlot::launch_fft_any(inverse ? 3 : 2, p->nfft, 1.0f / float(p->nfft),
+                                               tables(q), q->d_twany, d_in, d_out, batch, ld_in,
+                                               inc_in, ld_out, inc_out, static_cast<hipStream_t>(stream))
+                       : crlot::launch_cfft(q->geo, tables(q), d_in, d_out, batch, ld_in, inc_in,
+                                            ld_out, inc_out, inverse, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return hip_fail(e, "cfft kernel launch");
     return CRLOT_OK;
 }

@@ -1,0 +1,170 @@
+// fft_any.h -- mixed-radix complex FFT of ANY length P, one wave per transform.
+//
+// The power-of-two sizes of the hot path use the register-resident kernels of
+// fft_wave.h; this is the general path behind the same entry points for every
+// other frame size kissfft accepts (kiss_fft.c factors any n): N = 960 / 480
+// (20 / 10 ms at 48 kHz), N < 256, odd P = N/2, primes.
+//
+// Stockham autosort passes through two LDS buffers of P elements: the pass with
+// radix R and current sub-length Ns runs butterflies j < P/R (strided over the
+// wave's 64 lanes): x_r = src[j + r P/R] * W_{Ns R}^{r (j mod Ns)}, a length-R
+// DFT, dst[(j / Ns) Ns R + j mod Ns + r Ns] = y.  Factors follow kiss_fft's
+// kf_factor order (4s, then 2s, then odd primes).  Radix 2/3/4/5 butterflies
+// are written out (the kf_bfly2/3/4/5 formulas); any other prime R uses an
+// O(R^2) DFT that streams its inputs from LDS, so no size is excluded.
+// Twiddles come from one table W_P^k (k < P, forward sign) in global memory;
+// the inverse conjugates them.  IEEE f32, explicit FMAs.
+#pragma once
+
+#include "fft_wave.h"
+
+namespace crlot {
+namespace dev {
+namespace any {
+
+constexpr int kMaxPasses = 24;
+
+struct Plan {
+    int p;                  // complex points
+    int n_pass;
+    int radix[kMaxPasses];
+};
+
+// W_P^k (forward) or its conjugate
+template <bool INV>
+__device__ __forceinline__ cf twid(const cf* tw, int k) {
+    const cf w = tw[k];
+    return INV ? cf{w.r, -w.i} : w;
+}
+
+template <bool INV>
+__device__ __forceinline__ cf tmul(cf a, const cf* tw, int k) {
+    return k == 0 ? a : cmul(a, twid<INV>(tw, k));
+}
+
+// One Stockham pass, src -> dst.
+template <bool INV>
+__device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p, int ns, int r,
+                                     int lane) {
+    const int m = p / r;           // butterflies
+    const int stride = p / (ns * r);  // W_{Ns R}^e = W_P^{e * stride}
+    for (int j = lane; j < m; j += 64) {
+        const int jm = j % ns;
+        const int ob = (j / ns) * ns * r + jm;
+        const int tstep = jm * stride;  // twiddle exponent of x_1, < p
+        if (r == 2) {
+            const cf a = src[j], b = tmul<INV>(src[j + m], tw, tstep);
+            dst[ob] = cadd(a, b);
+            dst[ob + ns] = csub(a, b);
+        } else if (r == 4) {
+            cf x0 = src[j], x1 = tmul<INV>(src[j + m], tw, tstep);
+            cf x2 = tmul<INV>(src[j + 2 * m], tw, (2 * tstep) % p);
+            cf x3 = tmul<INV>(src[j + 3 * m], tw, (3 * tstep) % p);
+            dft4<INV>(x0, x1, x2, x3);
+            dst[ob] = x0;
+            dst[ob + ns] = x1;
+            dst[ob + 2 * ns] = x2;
+            dst[ob + 3 * ns] = x3;
+        } else if (r == 3) {
+            // kf_bfly3: y0 = a + b + c, y1/2 = a - (b + c)/2 -/+ i sin(2pi/3) (b - c)
+            const cf a = src[j], b = tmul<INV>(src[j + m], tw, tstep);
+            const cf c = tmul<INV>(src[j + 2 * m], tw, (2 * tstep) % p);
+            constexpr float s3 = 0.86602540378443864676f;
+            const cf s = cadd(b, c), d = csub(b, c);
+            const cf h = {__builtin_fmaf(s.r, -0.5f, a.r), __builtin_fmaf(s.i, -0.5f, a.i)};
+            const cf e = mul_mi<INV>(cf{d.r * s3, d.i * s3});  // -i sin(2pi/3) (b - c) forward
+            dst[ob] = cadd(a, s);
+            dst[ob + ns] = cadd(h, e);
+            dst[ob + 2 * ns] = csub(h, e);
+        } else if (r == 5) {
+            // kf_bfly5 with ya = W5^1, yb = W5^2
+            constexpr float c1 = 0.30901699437494742410f, s1 = 0.95105651629515357212f;
+            constexpr float c2 = -0.80901699437494742410f, s2 = 0.58778525229247312917f;
+            const cf x0 = src[j];
+            const cf x1 = tmul<INV>(src[j + m], tw, tstep);
+            const cf x2 = tmul<INV>(src[j + 2 * m], tw, (2 * tstep) % p);
+            const cf x3 = tmul<INV>(src[j + 3 * m], tw, (3 * tstep) % p);
+            const cf x4 = tmul<INV>(src[j + 4 * m], tw, (4 * tstep) % p);
+            const cf s7 = cadd(x1, x4), s10 = csub(x1, x4), s8 = cadd(x2, x3), s9 = csub(x2, x3);
+            const float sg = INV ? -1.0f : 1.0f;  // forward W5 = c - i s
+            const cf s5 = {__builtin_fmaf(s7.r, c1, __builtin_fmaf(s8.r, c2, x0.r)),
+                           __builtin_fmaf(s7.i, c1, __builtin_fmaf(s8.i, c2, x0.i))};
+            const cf s6 = {sg * __builtin_fmaf(s10.i, s1, s9.i * s2),
+                           -sg * __builtin_fmaf(s10.r, s1, s9.r * s2)};
+            const cf s11 = {__builtin_fmaf(s7.r, c2, __builtin_fmaf(s8.r, c1, x0.r)),
+                            __builtin_fmaf(s7.i, c2, __builtin_fmaf(s8.i, c1, x0.i))};
+            const cf s12 = {sg * __builtin_fmaf(s9.i, -s1, s10.i * s2),
+                            -sg * __builtin_fmaf(s9.r, -s1, s10.r * s2)};
+            dst[ob] = {x0.r + s7.r + s8.r, x0.i + s7.i + s8.i};
+            dst[ob + ns] = cadd(s5, s6);
+            dst[ob + 4 * ns] = csub(s5, s6);
+            dst[ob + 2 * ns] = cadd(s11, s12);
+            dst[ob + 3 * ns] = csub(s11, s12);
+        } else {
+            // generic prime radix: y_s = sum_q x_q W_R^{q s}, inputs re-read per output
+            const int wr = p / r;  // W_R = W_P^{p / r}
+            for (int s = 0; s < r; ++s) {
+                cf acc = src[j];
+                for (int q = 1; q < r; ++q) {
+                    const cf xq = tmul<INV>(src[j + q * m], tw, int((int64_t(q) * tstep) % p));
+                    acc = cadd(acc, tmul<INV>(xq, tw, int((int64_t(q) * s % r) * wr)));
+                }
+                dst[ob + s * ns] = acc;
+            }
+        }
+    }
+}
+
+// In-place (from the caller's view) P-point FFT of buf a; returns the buffer
+// holding the result (a or b).  Every pass is followed by a wave fence.
+template <bool INV>
+__device__ __forceinline__ cf* fft(cf* a, cf* b, const Plan& pl, const cf* tw, int lane) {
+    int ns = 1;
+    for (int i = 0; i < pl.n_pass; ++i) {
+        const int r = pl.radix[i];
+        pass<INV>(a, b, tw, pl.p, ns, r, lane);
+        wave_lds_fence();
+        cf* t = a;
+        a = b;
+        b = t;
+        ns *= r;
+    }
+    return a;
+}
+
+// kiss_fftr split -> gain -> kiss_fftri merge, src (Z) -> dst (Z'), with the
+// arithmetic of fft_wave.h real_split_hook_merge.  spec (optional) gets X[k],
+// k <= P.  st: exp(-i pi (k/P + 1/2)), k < P.
+template <bool HAS_GAIN>
+__device__ __forceinline__ void split_merge(const cf* src, cf* dst, int p, const cf* st,
+                                            const float* gain, cf* spec, int lane) {
+    for (int k = lane; k < p; k += 64) {
+        const cf zk = src[k];
+        const cf fpnk = conj(src[(p - k) % p]);
+        const cf f1 = cadd(zk, fpnk);
+        const cf f2 = csub(zk, fpnk);
+        const cf w = st[k];
+        const cf t = cmul(f2, cf{w.r * 0.5f, w.i * 0.5f});
+        cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
+        cf xpk = {__builtin_fmaf(f1.r, 0.5f, -t.r), __builtin_fmaf(f1.i, -0.5f, t.i)};
+        if (k == 0) dc_split(zk, xk, xpk);
+        if constexpr (HAS_GAIN) {
+            const float gk = gain[k], gpk = gain[p - k];
+            xk = {xk.r * gk, xk.i * gk};
+            xpk = {xpk.r * gpk, xpk.i * gpk};
+        }
+        if (spec) {
+            spec[k] = xk;
+            if (k == 0) spec[p] = xpk;
+        }
+        const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+        const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+        dst[k] = k == 0 ? dc_merge(xk, xpk)
+                        : cf{__builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r)),
+                             __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i))};
+    }
+}
+
+}  // namespace any
+}  // namespace dev
+}  // namespace crlot

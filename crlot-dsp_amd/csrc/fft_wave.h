@@ -377,6 +377,15 @@ __device__ __forceinline__ float sanit_scaled(float v) {
 }
 
 // ------------------------------------------------------------- real split
+// DC / Nyquist bins exactly as kissfft forms them: kiss_fftr sets
+// X[0] = (Z0.r + Z0.i, 0), X[P] = (Z0.r - Z0.i, 0); kiss_fftri rebuilds
+// Z'[0] = (X0.r + XP.r, X0.r - XP.r) from the REAL parts only (kiss_fftr.c).
+__device__ __forceinline__ void dc_split(cf z0, cf& x0, cf& xp) {
+    x0 = {z0.r + z0.i, 0.0f};
+    xp = {z0.r - z0.i, 0.0f};
+}
+__device__ __forceinline__ cf dc_merge(cf x0, cf xp) { return {x0.r + xp.r, x0.r - xp.r}; }
+
 // Given Z = FFT_P(z) lane-major in v, produce the spectrum X[k] (k = 0..P) of
 // the real 2P-point frame (kiss_fftr), apply the optional real per-bin gain
 // (spectral hook; the reference's step is the identity), then rebuild Z' such
@@ -411,6 +420,7 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
         const cf t = cmul(f2, sth[k]);  // 0.5 * f2 * st
         cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
         cf xpk = {__builtin_fmaf(f1.r, 0.5f, -t.r), __builtin_fmaf(f1.i, -0.5f, t.i)};  // X[P-k]
+        if (m == 0 && lane == 0) dc_split(zk, xk, xpk);
         if constexpr (HAS_GAIN) {
             const float gk = gain[k], gpk = gain[P - k];
             xk = {xk.r * gk, xk.i * gk};
@@ -426,6 +436,7 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
         const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
         v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
         v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
+        if (m == 0 && lane == 0) v[0] = dc_merge(xk, xpk);
     }
 }
 
@@ -453,6 +464,7 @@ __device__ __forceinline__ void real_split_hook_merge_wg(cf (&v)[E], cf* buf, co
         const cf t = cmul(f2, cf{w.r * 0.5f, w.i * 0.5f});
         cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
         cf xpk = {__builtin_fmaf(f1.r, 0.5f, -t.r), __builtin_fmaf(f1.i, -0.5f, t.i)};
+        if (m == 0 && lane == 0) dc_split(zk, xk, xpk);
         if constexpr (HAS_GAIN) {
             const float gk = gain[k], gpk = gain[P - k];
             xk = {xk.r * gk, xk.i * gk};
@@ -462,6 +474,7 @@ __device__ __forceinline__ void real_split_hook_merge_wg(cf (&v)[E], cf* buf, co
         const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
         v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
         v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
+        if (m == 0 && lane == 0) v[0] = dc_merge(xk, xpk);
     }
 }
 

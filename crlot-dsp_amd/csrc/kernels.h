@@ -63,6 +63,18 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
                              int64_t ld_frames, float* y, int n_streams, int64_t F,
                              int64_t ld_y, int64_t out_len, hipStream_t stream);
 
+// Any-size path (fft_any.h): any P = N/2 in 1..8192.  twany = build_any_twiddles(P)
+// on device.  kind: 0 rfft, 1 irfft, 2 cfft, 3 icfft; p = complex points of the
+// transform (N/2 for the real kinds, nfft for the complex ones); inv_scale = 1/nfft.
+bool any_supported(int p);
+std::vector<float> build_any_twiddles(int p);
+hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* twany,
+                            const float* x, int n_streams, int64_t T, int64_t ld_x, int64_t F,
+                            float* frames, float* spec, hipStream_t stream);
+hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
+                          const float* in, float* out, int batch, int64_t ld_in, int64_t inc_in,
+                          int64_t ld_out, int64_t inc_out, hipStream_t stream);
+
 // Streaming per-hop path (shapes as the fused path).  hist/acc: [channels][N].
 hipError_t launch_stream_hop(const Geometry& g, const DevTables& t, const float* in, int64_t in_ld,
                              int64_t in_inc, float* out, int64_t out_ld, int64_t out_inc,

@@ -24,6 +24,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "fft_any.h"
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -523,11 +524,13 @@ __global__ __launch_bounds__(kBlock) void k_rfft(const FftArgs a) {
         const cf f1 = dev::cadd(zk, fpnk);
         const cf f2 = dev::csub(zk, fpnk);
         const cf t = dev::cmul(f2, sth[k]);
-        out[int64_t(2 * k) * a.inc_out] = __builtin_fmaf(f1.r, 0.5f, t.r);
-        out[int64_t(2 * k) * a.inc_out + 1] = __builtin_fmaf(f1.i, 0.5f, t.i);
+        cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)}, xp;
+        if (k == 0) dev::dc_split(zk, xk, xp);
+        out[int64_t(2 * k) * a.inc_out] = xk.r;
+        out[int64_t(2 * k) * a.inc_out + 1] = xk.i;
         if (k == 0) {
-            out[int64_t(2 * P) * a.inc_out] = __builtin_fmaf(f1.r, 0.5f, -t.r);
-            out[int64_t(2 * P) * a.inc_out + 1] = __builtin_fmaf(f1.i, -0.5f, t.i);
+            out[int64_t(2 * P) * a.inc_out] = xp.r;
+            out[int64_t(2 * P) * a.inc_out + 1] = xp.i;
         }
     }
 }
@@ -558,6 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
         const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
         v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
         v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
+        if (k == 0) v[m] = dev::dc_merge(xk, xpk);
     }
     dev::fft_wave<E, true>(v, buf, tw, lane);
     float* out = a.out + b * a.ld_out;
@@ -605,6 +609,131 @@ __global__ __launch_bounds__(kBlock) void k_cfft(const FftArgs a) {
         } else {
             out[2 * i * a.inc_out] = v[m].r;
             out[2 * i * a.inc_out + 1] = v[m].i;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ any size
+// General-size path (fft_any.h): one wave per frame / transform, two LDS
+// buffers of P elements per wave, tables read from global memory (L1/L2).
+struct AnyArgs {
+    DevTables t;
+    const float* twany;  // W_P^k, k < P
+    dev::any::Plan pl;
+    const float* in;
+    float* out;
+    float* spec;
+    int64_t ld_in, inc_in, ld_out, inc_out;  // FFT kernels
+    int64_t T, F;                            // synth kernel
+    int h, n_streams, batch, pad, pad_mode, waves_per_block;
+    float inv_n;
+};
+
+__device__ __forceinline__ cf* any_bufs(int p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int wave = threadIdx.x >> 6;
+    return reinterpret_cast<cf*>(smem) + size_t(wave) * 2 * p;
+}
+
+// K_synth for any N: the push_frame_AoS input of every frame (and optionally the
+// forward spectrum), the same steps as k_synth_frames.
+template <bool HAS_GAIN>
+__global__ __launch_bounds__(256) void k_synth_any(const AnyArgs a) {
+    const int p = a.pl.p, n = 2 * p;
+    const int lane = threadIdx.x & 63;
+    cf* A = any_bufs(p);
+    cf* B = A + p;
+    const int64_t gw = int64_t(blockIdx.x) * a.waves_per_block + (threadIdx.x >> 6);
+    if (gw >= int64_t(a.n_streams) * a.F) return;
+    const int64_t s = gw / a.F, k = gw % a.F;
+    const float* x = a.in + s * a.ld_in;
+    const int64_t base = k * a.h - a.pad;
+    const cf* tw = reinterpret_cast<const cf*>(a.twany);
+    for (int i = lane; i < p; i += 64) {
+        const int64_t t0 = base + 2 * i;
+        const float x0 = fetch_x64(x, t0, a.T, a.pad_mode), x1 = fetch_x64(x, t0 + 1, a.T, a.pad_mode);
+        A[i] = {dev::sanit(x0 * a.t.wa[2 * i]), dev::sanit(x1 * a.t.wa[2 * i + 1])};
+    }
+    dev::wave_lds_fence();
+    cf* z = dev::any::fft<false>(A, B, a.pl, tw, lane);
+    cf* zo = z == A ? B : A;
+    cf* spec = a.spec ? reinterpret_cast<cf*>(a.spec) + gw * (p + 1) : nullptr;
+    dev::any::split_merge<HAS_GAIN>(z, zo, p, reinterpret_cast<const cf*>(a.t.st), a.t.gain, spec, lane);
+    dev::wave_lds_fence();
+    cf* r = dev::any::fft<true>(zo, z, a.pl, tw, lane);
+    float* out = a.out + gw * n;
+    for (int i = lane; i < p; i += 64) {
+        const cf v = r[i];
+        out[2 * i] = dev::sanit(v.r * a.inv_n);
+        out[2 * i + 1] = dev::sanit(v.i * a.inv_n);
+    }
+}
+
+// batched IFftPlan::forward / inverse / forward_complex / inverse_complex, any size
+template <int KIND>  // 0 rfft, 1 irfft, 2 cfft, 3 icfft
+__global__ __launch_bounds__(256) void k_fft_any(const AnyArgs a) {
+    const int p = a.pl.p;
+    const int lane = threadIdx.x & 63;
+    cf* A = any_bufs(p);
+    cf* B = A + p;
+    const int64_t b = int64_t(blockIdx.x) * a.waves_per_block + (threadIdx.x >> 6);
+    if (b >= a.batch) return;
+    const float* in = a.in + b * a.ld_in;
+    float* out = a.out + b * a.ld_out;
+    const cf* tw = reinterpret_cast<const cf*>(a.twany);
+    const cf* st = reinterpret_cast<const cf*>(a.t.st);
+    if (KIND == 0) {
+        for (int i = lane; i < p; i += 64)
+            A[i] = {dev::sanit(in[int64_t(2 * i) * a.inc_in]), dev::sanit(in[int64_t(2 * i + 1) * a.inc_in])};
+    } else if (KIND == 1) {
+        // kiss_fftri merge of the caller's bins X[0..P]
+        for (int k = lane; k < p; k += 64) {
+            const cf xk = {in[int64_t(2 * k) * a.inc_in], in[int64_t(2 * k) * a.inc_in + 1]};
+            const int pk = p - k;
+            const cf xpk = {in[int64_t(2 * pk) * a.inc_in], in[int64_t(2 * pk) * a.inc_in + 1]};
+            const cf w = st[k];
+            const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+            const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+            A[k] = k == 0 ? dev::dc_merge(xk, xpk)
+                          : cf{__builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r)),
+                               __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i))};
+        }
+    } else {
+        for (int i = lane; i < p; i += 64)
+            A[i] = {in[int64_t(2 * i) * a.inc_in], in[int64_t(2 * i) * a.inc_in + 1]};
+    }
+    dev::wave_lds_fence();
+    cf* z = dev::any::fft<(KIND == 1 || KIND == 3)>(A, B, a.pl, tw, lane);
+    if (KIND == 0) {  // kiss_fftr split: X[k], k <= P
+        for (int k = lane; k < p; k += 64) {
+            const cf zk = z[k];
+            const cf fpnk = dev::conj(z[(p - k) % p]);
+            const cf f1 = dev::cadd(zk, fpnk), f2 = dev::csub(zk, fpnk);
+            const cf w = st[k];
+            const cf t = dev::cmul(f2, cf{w.r * 0.5f, w.i * 0.5f});
+            cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)}, xp;
+            if (k == 0) dev::dc_split(zk, xk, xp);
+            out[int64_t(2 * k) * a.inc_out] = xk.r;
+            out[int64_t(2 * k) * a.inc_out + 1] = xk.i;
+            if (k == 0) {
+                out[int64_t(2 * p) * a.inc_out] = xp.r;
+                out[int64_t(2 * p) * a.inc_out + 1] = xp.i;
+            }
+        }
+    } else if (KIND == 1) {
+        for (int i = lane; i < p; i += 64) {
+            out[int64_t(2 * i) * a.inc_out] = dev::sanit(z[i].r * a.inv_n);
+            out[int64_t(2 * i + 1) * a.inc_out] = dev::sanit(z[i].i * a.inv_n);
+        }
+    } else if (KIND == 2) {
+        for (int i = lane; i < p; i += 64) {
+            out[int64_t(2 * i) * a.inc_out] = z[i].r;
+            out[int64_t(2 * i) * a.inc_out + 1] = z[i].i;
+        }
+    } else {
+        for (int i = lane; i < p; i += 64) {
+            out[int64_t(2 * i) * a.inc_out] = dev::sanit(z[i].r * a.inv_n);
+            out[int64_t(2 * i) * a.inc_out + 1] = dev::sanit(z[i].i * a.inv_n);
         }
     }
 }
@@ -954,6 +1083,112 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
 }
 
 bool synth_supported(int n) { return e_of(n) != 0; }
+
+// ---- any-size path
+dev::any::Plan make_any_plan(int p) {
+    dev::any::Plan pl{};
+    pl.p = p;
+    int n = p;
+    auto push = [&](int r) { pl.radix[pl.n_pass++] = r; };
+    while (n % 4 == 0 && n > 1) {  // kf_factor order: 4s, then 2s, then odd primes
+        push(4);
+        n /= 4;
+    }
+    while (n % 2 == 0 && n > 1) {
+        push(2);
+        n /= 2;
+    }
+    for (int f = 3; n > 1;) {
+        if (f * f > n) f = n;
+        if (n % f == 0) {
+            push(f);
+            n /= f;
+        } else {
+            f += 2;
+        }
+    }
+    return pl;
+}
+
+bool any_supported(int p) {
+    const dev::any::Plan pl = make_any_plan(p);
+    return p >= 1 && p <= 8192 && pl.n_pass <= dev::any::kMaxPasses;
+}
+
+std::vector<float> build_any_twiddles(int p) {
+    std::vector<float> t(2 * size_t(p));
+    for (int k = 0; k < p; ++k) {
+        const double ph = -2.0 * M_PI * double(k) / double(p);
+        t[2 * k] = float(std::cos(ph));
+        t[2 * k + 1] = float(std::sin(ph));
+    }
+    return t;
+}
+
+static int any_waves_per_block(int p) {
+    const int per = 16 * p;  // two buffers of P float pairs
+    return std::max(1, std::min(4, (128 * 1024) / per));
+}
+
+template <typename K>
+static hipError_t launch_any(K kernel, AnyArgs& a, int64_t items, hipStream_t stream) {
+    a.waves_per_block = any_waves_per_block(a.pl.p);
+    const size_t lds = size_t(a.waves_per_block) * 16 * a.pl.p;
+    hipError_t e = set_lds(kernel, lds);
+    if (e != hipSuccess) return e;
+    const int64_t grid = (items + a.waves_per_block - 1) / a.waves_per_block;
+    hipLaunchKernelGGL(kernel, dim3(unsigned(grid)), dim3(64 * a.waves_per_block), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* twany,
+                            const float* x, int n_streams, int64_t T, int64_t ld_x, int64_t F,
+                            float* frames, float* spec, hipStream_t stream) {
+    if (F <= 0 || n_streams <= 0 || !any_supported(g.n / 2)) return hipErrorInvalidValue;
+    AnyArgs a{};
+    a.t = t;
+    a.twany = twany;
+    a.pl = make_any_plan(g.n / 2);
+    a.in = x;
+    a.out = frames;
+    a.spec = spec;
+    a.ld_in = ld_x;
+    a.T = T;
+    a.F = F;
+    a.h = g.h;
+    a.n_streams = n_streams;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
+    a.inv_n = g.inv_n;
+    const int64_t items = int64_t(n_streams) * F;
+    return t.gain ? launch_any(k_synth_any<true>, a, items, stream)
+                  : launch_any(k_synth_any<false>, a, items, stream);
+}
+
+hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
+                          const float* in, float* out, int batch, int64_t ld_in, int64_t inc_in,
+                          int64_t ld_out, int64_t inc_out, hipStream_t stream) {
+    if (batch <= 0 || !any_supported(p)) return hipErrorInvalidValue;
+    AnyArgs a{};
+    a.t = t;
+    a.twany = twany;
+    a.pl = make_any_plan(p);
+    a.in = in;
+    a.out = out;
+    a.ld_in = ld_in;
+    a.inc_in = inc_in;
+    a.ld_out = ld_out;
+    a.inc_out = inc_out;
+    a.batch = batch;
+    a.inv_n = inv_scale;
+    switch (kind) {
+        case 0: return launch_any(k_fft_any<0>, a, batch, stream);
+        case 1: return launch_any(k_fft_any<1>, a, batch, stream);
+        case 2: return launch_any(k_fft_any<2>, a, batch, stream);
+        case 3: return launch_any(k_fft_any<3>, a, batch, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 template <int E>
 static hipError_t synth_e(const SynthArgs& a, int64_t grid, hipStream_t stream) {

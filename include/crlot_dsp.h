@@ -70,7 +70,8 @@ typedef struct crlot_stream crlot_stream;
  * Framer parameters (framer.h:46-47) and the window choice of the harness
  * (e2e_benchmark.cc:48-64).  Zero-initialise, then set the fields. */
 typedef struct crlot_plan_desc {
-    int32_t frame_size;          /* N: even, power of two in [256, 4096] on this path */
+    int32_t frame_size;          /* N: even, <= 16384 (powers of two 256..4096 run the
+                                    register-resident kernels, other sizes the mixed-radix path) */
     int32_t hop_size;            /* H: 1..N */
     int32_t window_type;         /* CRLOT_WIN_* */
     int32_t periodic;            /* 0 = symmetric (reference default) */
@@ -157,9 +158,9 @@ int crlot_irfft_batched(crlot_plan* plan, const float* d_in_complex, float* d_ou
  *   inverse_complex  complex -> complex, *1/nfft, sanitize     (adapter :204-246)
  * Calling the other domain's entry is CRLOT_ERUNTIME with the reference's
  * message.  Element i of batch b is at [b*ld + i*inc] (ld in floats, inc in
- * elements: floats for real data, float pairs for complex).  Sizes on this
- * device path: real nfft = 256..4096, complex nfft = 128..2048, powers of two
- * (others: CRLOT_EUNSUPPORTED).  No batch ceiling on the device path;
+ * elements: floats for real data, float pairs for complex).  Sizes: real nfft
+ * even in 2..16384, complex nfft 1..8192 (any factorisation, as kiss_fft);
+ * larger sizes are CRLOT_EUNSUPPORTED.  No batch ceiling on the device path;
  * MakeFftPlan's 1..16 rule is applied by the C++ layer (crlot_dsp.hpp). */
 #define CRLOT_FFT_REAL 0
 #define CRLOT_FFT_COMPLEX 1

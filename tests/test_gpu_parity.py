@@ -419,6 +419,76 @@ def test_oboe_wav_roundtrip(pkg, oracle, torch_cuda):
     assert_close(y, ref, float(np.max(np.abs(x))), "oboe")
 
 
+# ------------------------------------------------------------------ any frame size
+@pytest.mark.parametrize("n,h,mode", [(960, 240, 0), (480, 120, 1), (1000, 250, 0), (998, 499, 0),
+                                      (128, 32, 0), (6, 2, 0), (1536, 384, 0), (6000, 1500, 0)])
+def test_roundtrip_any_size_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
+    """Frame sizes kissfft accepts beyond the power-of-two kernels (20 / 10 ms at
+    48 kHz, P = 499 prime, N < 256, N > 4096) through the mixed-radix path."""
+    torch = torch_cuda
+    T = 20_000
+    x = oracle.synth_streams(2, T, config_id=n + h)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode)
+    F = oracle.frame_count(T, n, h, mode)
+    assert plan.frame_count(T) == F
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    ref = oracle.roundtrip_batch(x, n, h, mode=mode, nthreads=2)
+    for s in range(2):
+        assert_close(y[s], ref[s], float(np.max(np.abs(x))), f"N={n} H={h} stream {s}")
+    frames, spec = plan.stages(xd)
+    assert np.array_equal(bits(y), bits(host(plan.ola_gather(frames))))
+    _, fr_ref, sp_ref = oracle.roundtrip(x[0], n, h, mode=mode, want_frames=True, want_spec=True)
+    assert rel_l2(host(spec)[0], sp_ref) <= REL_L2
+
+
+def test_framequeue_any_size(pkg, oracle, torch_cuda):
+    torch = torch_cuda
+    n, h, T = 960, 480, 9001
+    x = oracle.synth_streams(1, T, config_id=17)
+    for pm in (0, 1, 2):
+        plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.FRAMEQUEUE, pad_mode=pm,
+                        analysis_window=False)
+        y = host(plan.roundtrip(dev(torch, x)))[0]
+        ref = oracle.roundtrip_ex(x[0], n, h, mode=oracle.FRAMEQUEUE, center=True, pad_mode=pm,
+                                  analysis_window=False)
+        assert_close(y, ref, float(np.max(np.abs(x))), f"FrameQueue N={n} pm={pm}")
+
+
+@pytest.mark.parametrize("n", [2, 6, 30, 96, 100, 998, 1000, 4410, 12000])
+def test_rfft_irfft_any_size(pkg, oracle, torch_cuda, n):
+    torch = torch_cuda
+    rng = np.random.default_rng(n)
+    B = 5
+    x = rng.standard_normal((B, n)).astype(np.float32)
+    x[0, 0] = np.inf
+    plan = pkg.FftPlan(n, pkg.FFT_REAL)
+    X = host(plan.forward(dev(torch, x)))
+    k = oracle.KissR(n)
+    for b in range(B):
+        assert rel_l2(X[b], k.forward(x[b])) < REL_L2, b
+    Y = (rng.standard_normal((B, n // 2 + 1)) + 1j * rng.standard_normal((B, n // 2 + 1))).astype(np.complex64)
+    y = host(plan.inverse(dev(torch, Y)))
+    for b in range(B):
+        assert rel_l2(y[b], k.inverse(Y[b])) < REL_L2, b
+
+
+@pytest.mark.parametrize("n", [1, 3, 5, 7, 12, 100, 499, 1000, 3000, 4096, 8192])
+def test_complex_fft_any_size(pkg, oracle, torch_cuda, n):
+    torch = torch_cuda
+    rng = np.random.default_rng(n + 1)
+    B = 3
+    z = (rng.standard_normal((B, n)) + 1j * rng.standard_normal((B, n))).astype(np.complex64)
+    plan = pkg.FftPlan(n, pkg.FFT_COMPLEX)
+    Z = host(plan.forward_complex(dev(torch, z)))
+    k = oracle.KissC(n)
+    for b in range(B):
+        assert rel_l2(Z[b], k.forward(z[b])) < REL_L2, b
+    back = host(plan.inverse_complex(dev(torch, Z)))
+    for b in range(B):
+        assert rel_l2(back[b], k.inverse(Z[b])) < REL_L2, b
+
+
 # ------------------------------------------------------------------ complex domain
 @pytest.mark.parametrize("n", [128, 256, 512, 1024, 2048])
 def test_complex_fft_vs_oracle(pkg, oracle, torch_cuda, n):

@@ -84,7 +84,7 @@ def test_window_rejects_like_reference(pkg):
     (dict(hop_size=0), ValueError),
     (dict(eps=-1.0), ValueError),
     (dict(frame_size=513), RuntimeError),        # MakeFftPlan: odd N (kissfft_adapter.cc:44-46)
-    (dict(frame_size=1000, hop_size=250), NotImplementedError),  # not a GPU-path size
+    (dict(frame_size=20000, hop_size=5000), NotImplementedError),  # beyond the device path
     (dict(window_type=4), ValueError),           # BLACKMAN_HARRIS
     (dict(boundary_mode=2, pad_mode=7), ValueError),  # unknown dsp::PadMode
     (dict(boundary_mode=3), ValueError),
@@ -99,9 +99,9 @@ def test_plan_validation_before_device(pkg, kw, exc):
 @pytest.mark.parametrize("domain,nfft,exc", [
     (2, 512, RuntimeError),            # "Unsupported FFT domain" (kissfft_adapter.cc:15-17)
     (0, 513, RuntimeError),            # odd real size (kissfft_adapter.cc:36-40)
-    (0, 1000, NotImplementedError),    # valid for kissfft, not a device-path size
-    (1, 64, NotImplementedError),
-    (1, 4096, NotImplementedError),
+    (0, 20000, NotImplementedError),   # valid for kissfft, beyond the device path
+    (0, 0, NotImplementedError),
+    (1, 10000, NotImplementedError),
 ])
 def test_fft_plan_validation_before_device(pkg, domain, nfft, exc):
     with pytest.raises(exc):
