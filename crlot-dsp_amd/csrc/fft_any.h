@@ -12,8 +12,9 @@
 // kf_factor order (4s, then 2s, then odd primes).  Radix 2/3/4/5 butterflies
 // are written out (the kf_bfly2/3/4/5 formulas); any other prime R uses an
 // O(R^2) DFT that streams its inputs from LDS, so no size is excluded.
-// Twiddles come from one table W_P^k (k < P, forward sign) in global memory;
-// the inverse conjugates them.  IEEE f32, explicit FMAs.
+// Twiddles come from per-pass tables in global memory (L1/L2-resident; no
+// integer division or modulo in the butterfly loop); the inverse conjugates
+// them.  IEEE f32, explicit FMAs.
 #pragma once
 
 #include "fft_wave.h"
@@ -24,42 +25,54 @@ namespace any {
 
 constexpr int kMaxPasses = 24;
 
-struct Plan {
-    int p;                  // complex points
-    int n_pass;
-    int radix[kMaxPasses];
+// Per-pass constants, built on the host (kernels.hip make_any_plan):
+// twiddles of pass i live at tw[off + (q-1) ns + jm] = W_{ns r}^{q jm} (q < r);
+// a generic prime radix also has W_r^e at tw[woff + e], e < r.
+struct PassDesc {
+    int r, ns, off, woff;
+    float rcp_ns;  // 1 / ns, for the quotient j / ns
 };
 
-// W_P^k (forward) or its conjugate
-template <bool INV>
-__device__ __forceinline__ cf twid(const cf* tw, int k) {
-    const cf w = tw[k];
-    return INV ? cf{w.r, -w.i} : w;
+struct Plan {
+    int p;  // complex points
+    int n_pass;
+    PassDesc pass[kMaxPasses];
+};
+
+// floor(j / ns) for 0 <= j < 2^23 from a float reciprocal, corrected to exact.
+__device__ __forceinline__ int fdiv(int j, int ns, float rcp) {
+    int q = int(float(j) * rcp);
+    q -= (q * ns > j);
+    q += ((q + 1) * ns <= j);
+    return q;
 }
 
 template <bool INV>
-__device__ __forceinline__ cf tmul(cf a, const cf* tw, int k) {
-    return k == 0 ? a : cmul(a, twid<INV>(tw, k));
+__device__ __forceinline__ cf twv(const cf* tw, int i) {
+    const cf w = tw[i];
+    return INV ? cf{w.r, -w.i} : w;
 }
 
 // One Stockham pass, src -> dst.
 template <bool INV>
-__device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p, int ns, int r,
+__device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p, const PassDesc& d,
                                      int lane) {
-    const int m = p / r;           // butterflies
-    const int stride = p / (ns * r);  // W_{Ns R}^e = W_P^{e * stride}
+    const int r = d.r, ns = d.ns;
+    const int m = p / r;  // butterflies
     for (int j = lane; j < m; j += 64) {
-        const int jm = j % ns;
-        const int ob = (j / ns) * ns * r + jm;
-        const int tstep = jm * stride;  // twiddle exponent of x_1, < p
+        const int jb = fdiv(j, ns, d.rcp_ns);
+        const int jm = j - jb * ns;
+        const int ob = jb * ns * r + jm;
+        const cf* t = tw + d.off + jm;  // t[(q-1) ns] = W^{q jm}
         if (r == 2) {
-            const cf a = src[j], b = tmul<INV>(src[j + m], tw, tstep);
+            const cf a = src[j], b = cmul(src[j + m], twv<INV>(t, 0));
             dst[ob] = cadd(a, b);
             dst[ob + ns] = csub(a, b);
         } else if (r == 4) {
-            cf x0 = src[j], x1 = tmul<INV>(src[j + m], tw, tstep);
-            cf x2 = tmul<INV>(src[j + 2 * m], tw, (2 * tstep) % p);
-            cf x3 = tmul<INV>(src[j + 3 * m], tw, (3 * tstep) % p);
+            cf x0 = src[j];
+            cf x1 = cmul(src[j + m], twv<INV>(t, 0));
+            cf x2 = cmul(src[j + 2 * m], twv<INV>(t, ns));
+            cf x3 = cmul(src[j + 3 * m], twv<INV>(t, 2 * ns));
             dft4<INV>(x0, x1, x2, x3);
             dst[ob] = x0;
             dst[ob + ns] = x1;
@@ -67,12 +80,12 @@ __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p
             dst[ob + 3 * ns] = x3;
         } else if (r == 3) {
             // kf_bfly3: y0 = a + b + c, y1/2 = a - (b + c)/2 -/+ i sin(2pi/3) (b - c)
-            const cf a = src[j], b = tmul<INV>(src[j + m], tw, tstep);
-            const cf c = tmul<INV>(src[j + 2 * m], tw, (2 * tstep) % p);
+            const cf a = src[j], b = cmul(src[j + m], twv<INV>(t, 0));
+            const cf c = cmul(src[j + 2 * m], twv<INV>(t, ns));
             constexpr float s3 = 0.86602540378443864676f;
-            const cf s = cadd(b, c), d = csub(b, c);
+            const cf s = cadd(b, c), dd = csub(b, c);
             const cf h = {__builtin_fmaf(s.r, -0.5f, a.r), __builtin_fmaf(s.i, -0.5f, a.i)};
-            const cf e = mul_mi<INV>(cf{d.r * s3, d.i * s3});  // -i sin(2pi/3) (b - c) forward
+            const cf e = mul_mi<INV>(cf{dd.r * s3, dd.i * s3});  // -i sin(2pi/3) (b - c) forward
             dst[ob] = cadd(a, s);
             dst[ob + ns] = cadd(h, e);
             dst[ob + 2 * ns] = csub(h, e);
@@ -81,10 +94,10 @@ __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p
             constexpr float c1 = 0.30901699437494742410f, s1 = 0.95105651629515357212f;
             constexpr float c2 = -0.80901699437494742410f, s2 = 0.58778525229247312917f;
             const cf x0 = src[j];
-            const cf x1 = tmul<INV>(src[j + m], tw, tstep);
-            const cf x2 = tmul<INV>(src[j + 2 * m], tw, (2 * tstep) % p);
-            const cf x3 = tmul<INV>(src[j + 3 * m], tw, (3 * tstep) % p);
-            const cf x4 = tmul<INV>(src[j + 4 * m], tw, (4 * tstep) % p);
+            const cf x1 = cmul(src[j + m], twv<INV>(t, 0));
+            const cf x2 = cmul(src[j + 2 * m], twv<INV>(t, ns));
+            const cf x3 = cmul(src[j + 3 * m], twv<INV>(t, 2 * ns));
+            const cf x4 = cmul(src[j + 4 * m], twv<INV>(t, 3 * ns));
             const cf s7 = cadd(x1, x4), s10 = csub(x1, x4), s8 = cadd(x2, x3), s9 = csub(x2, x3);
             const float sg = INV ? -1.0f : 1.0f;  // forward W5 = c - i s
             const cf s5 = {__builtin_fmaf(s7.r, c1, __builtin_fmaf(s8.r, c2, x0.r)),
@@ -101,13 +114,16 @@ __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p
             dst[ob + 2 * ns] = cadd(s11, s12);
             dst[ob + 3 * ns] = csub(s11, s12);
         } else {
-            // generic prime radix: y_s = sum_q x_q W_R^{q s}, inputs re-read per output
-            const int wr = p / r;  // W_R = W_P^{p / r}
+            // generic prime radix: y_s = sum_q (x_q W^{q jm}) W_r^{q s}, inputs re-read per output
+            const cf* wr = tw + d.woff;
             for (int s = 0; s < r; ++s) {
                 cf acc = src[j];
+                int e = 0;  // (q s) mod r
                 for (int q = 1; q < r; ++q) {
-                    const cf xq = tmul<INV>(src[j + q * m], tw, int((int64_t(q) * tstep) % p));
-                    acc = cadd(acc, tmul<INV>(xq, tw, int((int64_t(q) * s % r) * wr)));
+                    e += s;
+                    if (e >= r) e -= r;
+                    const cf xq = cmul(src[j + q * m], twv<INV>(t, (q - 1) * ns));
+                    acc = cadd(acc, cmul(xq, twv<INV>(wr, e)));
                 }
                 dst[ob + s * ns] = acc;
             }
@@ -119,15 +135,12 @@ __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p
 // holding the result (a or b).  Every pass is followed by a wave fence.
 template <bool INV>
 __device__ __forceinline__ cf* fft(cf* a, cf* b, const Plan& pl, const cf* tw, int lane) {
-    int ns = 1;
     for (int i = 0; i < pl.n_pass; ++i) {
-        const int r = pl.radix[i];
-        pass<INV>(a, b, tw, pl.p, ns, r, lane);
+        pass<INV>(a, b, tw, pl.p, pl.pass[i], lane);
         wave_lds_fence();
         cf* t = a;
         a = b;
         b = t;
-        ns *= r;
     }
     return a;
 }

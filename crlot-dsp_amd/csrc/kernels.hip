@@ -626,39 +626,86 @@ struct AnyArgs {
     int64_t ld_in, inc_in, ld_out, inc_out;  // FFT kernels
     int64_t T, F;                            // synth kernel
     int h, n_streams, batch, pad, pad_mode, waves_per_block;
+    int tw_len;  // float pairs in twany
     float inv_n;
 };
 
-__device__ __forceinline__ cf* any_bufs(int p) {
+// LDS of the any-size kernels: [tw tw_len cf][st P cf][wa 2P f][per wave: 2 x P cf]
+struct AnyLds {
+    cf* tw;
+    cf* st;
+    float* wa;
+    cf* A;
+    cf* B;
+};
+
+template <bool LDS_TABLES>
+__device__ __forceinline__ AnyLds any_lds(const AnyArgs& a, bool need_wa) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int wave = threadIdx.x >> 6;
-    return reinterpret_cast<cf*>(smem) + size_t(wave) * 2 * p;
+    const int p = a.pl.p;
+    AnyLds l;
+    if constexpr (!LDS_TABLES) {  // large P: tables stay in global memory (L1/L2)
+        l.tw = const_cast<cf*>(reinterpret_cast<const cf*>(a.twany));
+        l.st = const_cast<cf*>(reinterpret_cast<const cf*>(a.t.st));
+        l.wa = const_cast<float*>(a.t.wa);
+        l.A = reinterpret_cast<cf*>(smem) + size_t(threadIdx.x >> 6) * 2 * p;
+        l.B = l.A + p;
+        return l;
+    }
+    l.tw = reinterpret_cast<cf*>(smem);
+    l.st = l.tw + a.tw_len;
+    l.wa = reinterpret_cast<float*>(l.st + p);
+    l.A = reinterpret_cast<cf*>(l.wa + 2 * p) + size_t(threadIdx.x >> 6) * 2 * p;
+    l.B = l.A + p;
+    const int nt = blockDim.x;
+    const cf* gtw = reinterpret_cast<const cf*>(a.twany);
+    const cf* gst = reinterpret_cast<const cf*>(a.t.st);
+    for (int i = threadIdx.x; i < a.tw_len; i += nt) l.tw[i] = gtw[i];
+    for (int i = threadIdx.x; i < p; i += nt) l.st[i] = gst[i];
+    if (need_wa)
+        for (int i = threadIdx.x; i < 2 * p; i += nt) l.wa[i] = a.t.wa[i];
+    __syncthreads();
+    return l;
+}
+
+static size_t any_lds_bytes(int p, int tw_len, int waves, bool tables) {
+    const size_t bufs = size_t(waves) * 2 * p * sizeof(cf);
+    return tables ? sizeof(cf) * (size_t(tw_len) + p) + sizeof(float) * 2 * p + bufs : bufs;
 }
 
 // K_synth for any N: the push_frame_AoS input of every frame (and optionally the
 // forward spectrum), the same steps as k_synth_frames.
-template <bool HAS_GAIN>
-__global__ __launch_bounds__(256) void k_synth_any(const AnyArgs a) {
+template <bool HAS_GAIN, bool LDS_TABLES>
+__global__ __launch_bounds__(512) void k_synth_any(const AnyArgs a) {
     const int p = a.pl.p, n = 2 * p;
     const int lane = threadIdx.x & 63;
-    cf* A = any_bufs(p);
-    cf* B = A + p;
+    const AnyLds l = any_lds<LDS_TABLES>(a, true);
+    cf* A = l.A;
+    cf* B = l.B;
     const int64_t gw = int64_t(blockIdx.x) * a.waves_per_block + (threadIdx.x >> 6);
     if (gw >= int64_t(a.n_streams) * a.F) return;
     const int64_t s = gw / a.F, k = gw % a.F;
     const float* x = a.in + s * a.ld_in;
     const int64_t base = k * a.h - a.pad;
-    const cf* tw = reinterpret_cast<const cf*>(a.twany);
+    const cf* tw = l.tw;
+    const bool inside = base >= 0 && base + n <= a.T;
     for (int i = lane; i < p; i += 64) {
         const int64_t t0 = base + 2 * i;
-        const float x0 = fetch_x64(x, t0, a.T, a.pad_mode), x1 = fetch_x64(x, t0 + 1, a.T, a.pad_mode);
-        A[i] = {dev::sanit(x0 * a.t.wa[2 * i]), dev::sanit(x1 * a.t.wa[2 * i + 1])};
+        float x0, x1;
+        if (inside) {
+            x0 = x[t0];
+            x1 = x[t0 + 1];
+        } else {
+            x0 = fetch_x64(x, t0, a.T, a.pad_mode);
+            x1 = fetch_x64(x, t0 + 1, a.T, a.pad_mode);
+        }
+        A[i] = {dev::sanit(x0 * l.wa[2 * i]), dev::sanit(x1 * l.wa[2 * i + 1])};
     }
     dev::wave_lds_fence();
     cf* z = dev::any::fft<false>(A, B, a.pl, tw, lane);
     cf* zo = z == A ? B : A;
     cf* spec = a.spec ? reinterpret_cast<cf*>(a.spec) + gw * (p + 1) : nullptr;
-    dev::any::split_merge<HAS_GAIN>(z, zo, p, reinterpret_cast<const cf*>(a.t.st), a.t.gain, spec, lane);
+    dev::any::split_merge<HAS_GAIN>(z, zo, p, l.st, a.t.gain, spec, lane);
     dev::wave_lds_fence();
     cf* r = dev::any::fft<true>(zo, z, a.pl, tw, lane);
     float* out = a.out + gw * n;
@@ -670,18 +717,19 @@ __global__ __launch_bounds__(256) void k_synth_any(const AnyArgs a) {
 }
 
 // batched IFftPlan::forward / inverse / forward_complex / inverse_complex, any size
-template <int KIND>  // 0 rfft, 1 irfft, 2 cfft, 3 icfft
-__global__ __launch_bounds__(256) void k_fft_any(const AnyArgs a) {
+template <int KIND, bool LDS_TABLES>  // KIND: 0 rfft, 1 irfft, 2 cfft, 3 icfft
+__global__ __launch_bounds__(512) void k_fft_any(const AnyArgs a) {
     const int p = a.pl.p;
     const int lane = threadIdx.x & 63;
-    cf* A = any_bufs(p);
-    cf* B = A + p;
+    const AnyLds l = any_lds<LDS_TABLES>(a, false);
+    cf* A = l.A;
+    cf* B = l.B;
     const int64_t b = int64_t(blockIdx.x) * a.waves_per_block + (threadIdx.x >> 6);
     if (b >= a.batch) return;
     const float* in = a.in + b * a.ld_in;
     float* out = a.out + b * a.ld_out;
-    const cf* tw = reinterpret_cast<const cf*>(a.twany);
-    const cf* st = reinterpret_cast<const cf*>(a.t.st);
+    const cf* tw = l.tw;
+    const cf* st = l.st;
     if (KIND == 0) {
         for (int i = lane; i < p; i += 64)
             A[i] = {dev::sanit(in[int64_t(2 * i) * a.inc_in]), dev::sanit(in[int64_t(2 * i + 1) * a.inc_in])};
@@ -1085,55 +1133,92 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
 bool synth_supported(int n) { return e_of(n) != 0; }
 
 // ---- any-size path
-dev::any::Plan make_any_plan(int p) {
-    dev::any::Plan pl{};
-    pl.p = p;
+// kf_factor order: 4s, then 2s, then odd primes; per-pass twiddle tables laid out
+// as fft_any.h PassDesc describes (the device table = build_any_twiddles(p)).
+static std::vector<int> any_factors(int p) {
+    std::vector<int> f;
     int n = p;
-    auto push = [&](int r) { pl.radix[pl.n_pass++] = r; };
-    while (n % 4 == 0 && n > 1) {  // kf_factor order: 4s, then 2s, then odd primes
-        push(4);
+    while (n % 4 == 0 && n > 1) {
+        f.push_back(4);
         n /= 4;
     }
     while (n % 2 == 0 && n > 1) {
-        push(2);
+        f.push_back(2);
         n /= 2;
     }
-    for (int f = 3; n > 1;) {
-        if (f * f > n) f = n;
-        if (n % f == 0) {
-            push(f);
-            n /= f;
+    for (int d = 3; n > 1;) {
+        if (d * d > n) d = n;
+        if (n % d == 0) {
+            f.push_back(d);
+            n /= d;
         } else {
-            f += 2;
+            d += 2;
         }
+    }
+    return f;
+}
+
+dev::any::Plan make_any_plan(int p) {
+    dev::any::Plan pl{};
+    pl.p = p;
+    const std::vector<int> f = any_factors(p);
+    int ns = 1, off = 0;
+    for (size_t i = 0; i < f.size() && int(i) < dev::any::kMaxPasses; ++i) {
+        dev::any::PassDesc& d = pl.pass[pl.n_pass++];
+        d.r = f[i];
+        d.ns = ns;
+        d.off = off;
+        d.rcp_ns = 1.0f / float(ns);
+        off += (d.r - 1) * ns;
+        const bool special = d.r == 2 || d.r == 3 || d.r == 4 || d.r == 5;
+        d.woff = special ? 0 : off;
+        if (!special) off += d.r;
+        ns *= d.r;
     }
     return pl;
 }
 
 bool any_supported(int p) {
-    const dev::any::Plan pl = make_any_plan(p);
-    return p >= 1 && p <= 8192 && pl.n_pass <= dev::any::kMaxPasses;
+    return p >= 1 && p <= 8192 && any_factors(p).size() <= size_t(dev::any::kMaxPasses);
 }
 
 std::vector<float> build_any_twiddles(int p) {
-    std::vector<float> t(2 * size_t(p));
-    for (int k = 0; k < p; ++k) {
-        const double ph = -2.0 * M_PI * double(k) / double(p);
-        t[2 * k] = float(std::cos(ph));
-        t[2 * k + 1] = float(std::sin(ph));
+    std::vector<float> t;
+    const std::vector<int> f = any_factors(p);
+    int ns = 1;
+    auto push = [&](double ph) {
+        t.push_back(float(std::cos(ph)));
+        t.push_back(float(std::sin(ph)));
+    };
+    for (int r : f) {
+        for (int q = 1; q < r; ++q)
+            for (int jm = 0; jm < ns; ++jm) push(-2.0 * M_PI * double(q) * double(jm) / double(ns * r));
+        if (!(r == 2 || r == 3 || r == 4 || r == 5))
+            for (int e = 0; e < r; ++e) push(-2.0 * M_PI * double(e) / double(r));
+        ns *= r;
     }
+    if (t.empty()) push(0.0);  // P = 1: no passes
     return t;
 }
 
+// Waves per workgroup: up to 8 sharing one copy of the LDS tables, sized so two
+// workgroups fit a CU's 160 KB when the tables are in LDS (P <= ~1000).
 static int any_waves_per_block(int p) {
-    const int per = 16 * p;  // two buffers of P float pairs
-    return std::max(1, std::min(4, (128 * 1024) / per));
+    const int per = 16 * p;               // two buffers of P float pairs per wave
+    const int tables = 24 * p + 8 * 64;   // twiddles ~P, st P, wa 2P (float pairs / floats)
+    const int budget = p <= 1024 ? 78 * 1024 - tables : 96 * 1024;
+    return std::max(1, std::min(8, budget / per));
+}
+
+// tables in LDS when they fit beside the wave buffers (P <= 2048 or so)
+static bool any_lds_tables(int p, int tw_len) {
+    return any_lds_bytes(p, tw_len, any_waves_per_block(p), true) <= 150 * 1024;
 }
 
 template <typename K>
-static hipError_t launch_any(K kernel, AnyArgs& a, int64_t items, hipStream_t stream) {
+static hipError_t launch_any(K kernel, AnyArgs& a, int64_t items, hipStream_t stream, bool tables) {
     a.waves_per_block = any_waves_per_block(a.pl.p);
-    const size_t lds = size_t(a.waves_per_block) * 16 * a.pl.p;
+    const size_t lds = any_lds_bytes(a.pl.p, a.tw_len, a.waves_per_block, tables);
     hipError_t e = set_lds(kernel, lds);
     if (e != hipSuccess) return e;
     const int64_t grid = (items + a.waves_per_block - 1) / a.waves_per_block;
@@ -1161,8 +1246,13 @@ hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* 
     a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     const int64_t items = int64_t(n_streams) * F;
-    return t.gain ? launch_any(k_synth_any<true>, a, items, stream)
-                  : launch_any(k_synth_any<false>, a, items, stream);
+    a.tw_len = int(build_any_twiddles(a.pl.p).size() / 2);
+    const bool tb = any_lds_tables(a.pl.p, a.tw_len);
+    if (tb)
+        return t.gain ? launch_any(k_synth_any<true, true>, a, items, stream, true)
+                      : launch_any(k_synth_any<false, true>, a, items, stream, true);
+    return t.gain ? launch_any(k_synth_any<true, false>, a, items, stream, false)
+                  : launch_any(k_synth_any<false, false>, a, items, stream, false);
 }
 
 hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
@@ -1181,11 +1271,17 @@ hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, 
     a.inc_out = inc_out;
     a.batch = batch;
     a.inv_n = inv_scale;
-    switch (kind) {
-        case 0: return launch_any(k_fft_any<0>, a, batch, stream);
-        case 1: return launch_any(k_fft_any<1>, a, batch, stream);
-        case 2: return launch_any(k_fft_any<2>, a, batch, stream);
-        case 3: return launch_any(k_fft_any<3>, a, batch, stream);
+    a.tw_len = int(build_any_twiddles(p).size() / 2);
+    const bool tb = any_lds_tables(p, a.tw_len);
+    switch (kind * 2 + (tb ? 1 : 0)) {
+        case 0: return launch_any(k_fft_any<0, false>, a, batch, stream, false);
+        case 1: return launch_any(k_fft_any<0, true>, a, batch, stream, true);
+        case 2: return launch_any(k_fft_any<1, false>, a, batch, stream, false);
+        case 3: return launch_any(k_fft_any<1, true>, a, batch, stream, true);
+        case 4: return launch_any(k_fft_any<2, false>, a, batch, stream, false);
+        case 5: return launch_any(k_fft_any<2, true>, a, batch, stream, true);
+        case 6: return launch_any(k_fft_any<3, false>, a, batch, stream, false);
+        case 7: return launch_any(k_fft_any<3, true>, a, batch, stream, true);
         default: return hipErrorInvalidValue;
     }
 }

@@ -16,6 +16,8 @@ CONFIGS = [
     ("e2e-harness hop: 1024 streams, N=1024 H=512", 1024, 480000, 1024, 512, 0),
     ("config4 shape batched: 64 ch, N=512 H=128 DROP", 64, 480000, 512, 128, 1),
     ("2048/512: 1024 streams", 1024, 480000, 2048, 512, 0),
+    ("any-size 960/240 (20 ms @ 48 kHz): 1024 streams", 1024, 480000, 960, 240, 0),
+    ("any-size 480/120 (10 ms @ 48 kHz): 1024 streams", 1024, 480000, 480, 120, 0),
 ]
 
 
