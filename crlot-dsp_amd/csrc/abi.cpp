@@ -370,6 +370,11 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
         if (e != hipSuccess) return hip_fail(e, "fused kernel launch");
         return CRLOT_OK;
     }
+    if (p->generic && crlot::fused_any_fits(p->geo.n, p->geo.h) && ld_x < (int64_t(1) << 40)) {
+        e = crlot::launch_fused_any(p->geo, t, p->d_twany, d_x, d_y, n_streams, T, ld_x, ld_y, F, s);
+        if (e != hipSuccess) return hip_fail(e, "fused (any size) kernel launch");
+        return CRLOT_OK;
+    }
     const int64_t need = int64_t(n_streams) * F * p->geo.n * int64_t(sizeof(float));
     int rc = ensure_workspace(p, need);
     if (rc != CRLOT_OK) return rc;

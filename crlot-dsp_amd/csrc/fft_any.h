@@ -53,53 +53,45 @@ __device__ __forceinline__ cf twv(const cf* tw, int i) {
     return INV ? cf{w.r, -w.i} : w;
 }
 
-// One Stockham pass, src -> dst.
-template <bool INV>
-__device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p, const PassDesc& d,
-                                     int lane) {
-    const int r = d.r, ns = d.ns;
-    const int m = p / r;  // butterflies
+// One Stockham pass with a compile-time radix R (2, 3, 4, 5), src -> dst.
+template <bool INV, int R>
+__device__ __forceinline__ void pass_r(const cf* __restrict__ src, cf* __restrict__ dst,
+                                       const cf* __restrict__ tw, int p, const PassDesc& d,
+                                       int lane) {
+    const int ns = d.ns;
+    const int m = p / R;  // butterflies
+    const cf* twp = tw + d.off;
     for (int j = lane; j < m; j += 64) {
         const int jb = fdiv(j, ns, d.rcp_ns);
         const int jm = j - jb * ns;
-        const int ob = jb * ns * r + jm;
-        const cf* t = tw + d.off + jm;  // t[(q-1) ns] = W^{q jm}
-        if (r == 2) {
-            const cf a = src[j], b = cmul(src[j + m], twv<INV>(t, 0));
-            dst[ob] = cadd(a, b);
-            dst[ob + ns] = csub(a, b);
-        } else if (r == 4) {
-            cf x0 = src[j];
-            cf x1 = cmul(src[j + m], twv<INV>(t, 0));
-            cf x2 = cmul(src[j + 2 * m], twv<INV>(t, ns));
-            cf x3 = cmul(src[j + 3 * m], twv<INV>(t, 2 * ns));
-            dft4<INV>(x0, x1, x2, x3);
-            dst[ob] = x0;
-            dst[ob + ns] = x1;
-            dst[ob + 2 * ns] = x2;
-            dst[ob + 3 * ns] = x3;
-        } else if (r == 3) {
+        const int ob = jb * ns * R + jm;
+        const cf* t = twp + jm;  // t[(q-1) ns] = W^{q jm}
+        cf x[R];
+        x[0] = src[j];
+#pragma unroll
+        for (int q = 1; q < R; ++q) x[q] = cmul(src[j + q * m], twv<INV>(t, (q - 1) * ns));
+        if constexpr (R == 2) {
+            dft2<INV>(x[0], x[1]);
+        } else if constexpr (R == 4) {
+            dft4<INV>(x[0], x[1], x[2], x[3]);
+        } else if constexpr (R == 3) {
             // kf_bfly3: y0 = a + b + c, y1/2 = a - (b + c)/2 -/+ i sin(2pi/3) (b - c)
-            const cf a = src[j], b = cmul(src[j + m], twv<INV>(t, 0));
-            const cf c = cmul(src[j + 2 * m], twv<INV>(t, ns));
             constexpr float s3 = 0.86602540378443864676f;
-            const cf s = cadd(b, c), dd = csub(b, c);
-            const cf h = {__builtin_fmaf(s.r, -0.5f, a.r), __builtin_fmaf(s.i, -0.5f, a.i)};
+            const cf s = cadd(x[1], x[2]), dd = csub(x[1], x[2]);
+            const cf h = {__builtin_fmaf(s.r, -0.5f, x[0].r), __builtin_fmaf(s.i, -0.5f, x[0].i)};
             const cf e = mul_mi<INV>(cf{dd.r * s3, dd.i * s3});  // -i sin(2pi/3) (b - c) forward
-            dst[ob] = cadd(a, s);
-            dst[ob + ns] = cadd(h, e);
-            dst[ob + 2 * ns] = csub(h, e);
-        } else if (r == 5) {
+            x[0] = cadd(x[0], s);
+            x[1] = cadd(h, e);
+            x[2] = csub(h, e);
+        } else {
+            static_assert(R == 5, "radix");
             // kf_bfly5 with ya = W5^1, yb = W5^2
             constexpr float c1 = 0.30901699437494742410f, s1 = 0.95105651629515357212f;
             constexpr float c2 = -0.80901699437494742410f, s2 = 0.58778525229247312917f;
-            const cf x0 = src[j];
-            const cf x1 = cmul(src[j + m], twv<INV>(t, 0));
-            const cf x2 = cmul(src[j + 2 * m], twv<INV>(t, ns));
-            const cf x3 = cmul(src[j + 3 * m], twv<INV>(t, 2 * ns));
-            const cf x4 = cmul(src[j + 4 * m], twv<INV>(t, 3 * ns));
-            const cf s7 = cadd(x1, x4), s10 = csub(x1, x4), s8 = cadd(x2, x3), s9 = csub(x2, x3);
-            const float sg = INV ? -1.0f : 1.0f;  // forward W5 = c - i s
+            const cf x0 = x[0];
+            const cf s7 = cadd(x[1], x[4]), s10 = csub(x[1], x[4]);
+            const cf s8 = cadd(x[2], x[3]), s9 = csub(x[2], x[3]);
+            constexpr float sg = INV ? -1.0f : 1.0f;  // forward W5 = c - i s
             const cf s5 = {__builtin_fmaf(s7.r, c1, __builtin_fmaf(s8.r, c2, x0.r)),
                            __builtin_fmaf(s7.i, c1, __builtin_fmaf(s8.i, c2, x0.i))};
             const cf s6 = {sg * __builtin_fmaf(s10.i, s1, s9.i * s2),
@@ -108,26 +100,52 @@ __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p
                             __builtin_fmaf(s7.i, c2, __builtin_fmaf(s8.i, c1, x0.i))};
             const cf s12 = {sg * __builtin_fmaf(s9.i, -s1, s10.i * s2),
                             -sg * __builtin_fmaf(s9.r, -s1, s10.r * s2)};
-            dst[ob] = {x0.r + s7.r + s8.r, x0.i + s7.i + s8.i};
-            dst[ob + ns] = cadd(s5, s6);
-            dst[ob + 4 * ns] = csub(s5, s6);
-            dst[ob + 2 * ns] = cadd(s11, s12);
-            dst[ob + 3 * ns] = csub(s11, s12);
-        } else {
-            // generic prime radix: y_s = sum_q (x_q W^{q jm}) W_r^{q s}, inputs re-read per output
-            const cf* wr = tw + d.woff;
-            for (int s = 0; s < r; ++s) {
-                cf acc = src[j];
-                int e = 0;  // (q s) mod r
-                for (int q = 1; q < r; ++q) {
-                    e += s;
-                    if (e >= r) e -= r;
-                    const cf xq = cmul(src[j + q * m], twv<INV>(t, (q - 1) * ns));
-                    acc = cadd(acc, cmul(xq, twv<INV>(wr, e)));
-                }
-                dst[ob + s * ns] = acc;
-            }
+            x[0] = {x0.r + s7.r + s8.r, x0.i + s7.i + s8.i};
+            x[1] = cadd(s5, s6);
+            x[4] = csub(s5, s6);
+            x[2] = cadd(s11, s12);
+            x[3] = csub(s11, s12);
         }
+#pragma unroll
+        for (int q = 0; q < R; ++q) dst[ob + q * ns] = x[q];
+    }
+}
+
+// Any other (prime) radix: y_s = sum_q (x_q W^{q jm}) W_r^{q s}, inputs re-read per output.
+template <bool INV>
+__device__ __noinline__ void pass_generic(const cf* src, cf* dst, const cf* tw, int p,
+                                          const PassDesc d, int lane) {
+    const int r = d.r, ns = d.ns;
+    const int m = p / r;
+    const cf* wr = tw + d.woff;
+    for (int j = lane; j < m; j += 64) {
+        const int jb = fdiv(j, ns, d.rcp_ns);
+        const int jm = j - jb * ns;
+        const int ob = jb * ns * r + jm;
+        const cf* t = tw + d.off + jm;
+        for (int s = 0; s < r; ++s) {
+            cf acc = src[j];
+            int e = 0;  // (q s) mod r
+            for (int q = 1; q < r; ++q) {
+                e += s;
+                if (e >= r) e -= r;
+                const cf xq = cmul(src[j + q * m], twv<INV>(t, (q - 1) * ns));
+                acc = cadd(acc, cmul(xq, twv<INV>(wr, e)));
+            }
+            dst[ob + s * ns] = acc;
+        }
+    }
+}
+
+template <bool INV>
+__device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p, const PassDesc& d,
+                                     int lane) {
+    switch (d.r) {
+        case 2: pass_r<INV, 2>(src, dst, tw, p, d, lane); break;
+        case 3: pass_r<INV, 3>(src, dst, tw, p, d, lane); break;
+        case 4: pass_r<INV, 4>(src, dst, tw, p, d, lane); break;
+        case 5: pass_r<INV, 5>(src, dst, tw, p, d, lane); break;
+        default: pass_generic<INV>(src, dst, tw, p, d, lane); break;
     }
 }
 

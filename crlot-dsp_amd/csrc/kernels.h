@@ -71,6 +71,11 @@ std::vector<float> build_any_twiddles(int p);
 hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* twany,
                             const float* x, int n_streams, int64_t T, int64_t ld_x, int64_t F,
                             float* frames, float* spec, hipStream_t stream);
+// Fused any-size walker (OLA ring in LDS): bit-identical to synth_any + ola_gather.
+bool fused_any_fits(int n, int h);
+hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,
+                            const float* x, float* y, int n_streams, int64_t T, int64_t ld_x,
+                            int64_t ld_y, int64_t F, hipStream_t stream);
 hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
                           const float* in, float* out, int batch, int64_t ld_in, int64_t inc_in,
                           int64_t ld_out, int64_t inc_out, hipStream_t stream);

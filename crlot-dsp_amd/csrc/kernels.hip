@@ -716,6 +716,92 @@ __global__ __launch_bounds__(512) void k_synth_any(const AnyArgs a) {
     }
 }
 
+// K_fused_any: the fused walk for any N.  A wave owns a run of consecutive frames
+// of one stream (+ warm-up frames); the OLA accumulates in a per-wave LDS ring
+// of RL = H ceil(N/H) floats in ascending k (k_ola_gather's arithmetic, so the
+// result equals the staged path bit for bit); block k is divided by max(norm,
+// eps) and stored right after frame k.  Tables are staged once per workgroup.
+struct AnyFusedArgs {
+    AnyArgs a;        // tables, plan, x (in), y (out), T, pad
+    int64_t ld_y;
+    int out_len_i, n_chunks, M, F, rl;  // rl = ring floats per wave
+    int ring_len;
+    float gain;
+};
+
+template <bool HAS_GAIN>
+__global__ __launch_bounds__(1024) void k_stft_ola_any(const AnyFusedArgs f) {
+    const AnyArgs& a = f.a;
+    const int p = a.pl.p, n = 2 * p, H = a.h;
+    const int lane = threadIdx.x & 63;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    // [tables (any_lds layout)][per wave: A, B (2P cf)][per wave: ring (rl f)]
+    const AnyLds l = any_lds<true>(a, true);
+    const int wave = threadIdx.x >> 6;
+    float* ws = reinterpret_cast<float*>(l.A - size_t(wave) * 2 * p + size_t(a.waves_per_block) * 2 * p);
+    float* ring = ws + 2 * p + size_t(wave) * f.rl;
+    if (wave == 0)
+        for (int i = lane; i < 2 * p; i += 64) ws[i] = a.t.ws[i];
+    __syncthreads();
+    const int64_t gw = int64_t(blockIdx.x) * a.waves_per_block + wave;
+    if (gw >= int64_t(a.n_streams) * f.n_chunks) return;
+    const int64_t s = gw / f.n_chunks, c = gw - s * f.n_chunks;
+    const int nbr = f.rl / H;
+    const int f0 = int(c) * f.M;
+    const int f1 = min(f.F, f0 + f.M);
+    const int fs = max(0, f0 - (nbr - 1));
+    const float* x = a.in + s * a.ld_in;
+    float* y = a.out + s * f.ld_y;
+    cf* A = l.A;
+    cf* B = l.B;
+    for (int i = lane; i < f.rl; i += 64) ring[i] = 0.0f;
+    for (int k = fs; k < f1; ++k) {
+        const int64_t base = int64_t(k) * H - a.pad;
+        const bool inside = base >= 0 && base + n <= a.T;
+        for (int i = lane; i < p; i += 64) {
+            const int64_t t0 = base + 2 * i;
+            float x0, x1;
+            if (inside) {
+                x0 = x[t0];
+                x1 = x[t0 + 1];
+            } else {
+                x0 = fetch_x64(x, t0, a.T, a.pad_mode);
+                x1 = fetch_x64(x, t0 + 1, a.T, a.pad_mode);
+            }
+            A[i] = {dev::sanit(x0 * l.wa[2 * i]), dev::sanit(x1 * l.wa[2 * i + 1])};
+        }
+        dev::wave_lds_fence();
+        cf* z = dev::any::fft<false>(A, B, a.pl, l.tw, lane);
+        cf* zo = z == A ? B : A;
+        dev::any::split_merge<HAS_GAIN>(z, zo, p, l.st, a.t.gain, nullptr, lane);
+        dev::wave_lds_fence();
+        const cf* r = dev::any::fft<true>(zo, z, a.pl, l.tw, lane);
+        // push_frame_AoS(k*H): ring[(kH + i) mod rl] = fma(fma(src, w, 0), g, ring)
+        const int rb = (k % nbr) * H;
+        for (int i = lane; i < n; i += 64) {
+            const cf v = r[i >> 1];
+            const float src = dev::sanit(((i & 1) ? v.i : v.r) * a.inv_n);
+            int pos = rb + i;
+            if (pos >= f.rl) pos -= f.rl;
+            ring[pos] = __builtin_fmaf(__builtin_fmaf(src, ws[i], 0.0f), f.gain, ring[pos]);
+        }
+        dev::wave_lds_fence();
+        // produce(H): block k is complete
+        const int64_t ob = int64_t(k) * H;
+        int di = int(ob % f.ring_len);
+        for (int i = lane; i < H; i += 64) {
+            const int pos = rb + i;
+            if (k >= f0) {
+                int d = di + i;
+                if (d >= f.ring_len) d -= f.ring_len;
+                y[ob + i] = ring[pos] / a.t.den[d];
+            }
+            ring[pos] = 0.0f;
+        }
+        dev::wave_lds_fence();
+    }
+}
+
 // batched IFftPlan::forward / inverse / forward_complex / inverse_complex, any size
 template <int KIND, bool LDS_TABLES>  // KIND: 0 rfft, 1 irfft, 2 cfft, 3 icfft
 __global__ __launch_bounds__(512) void k_fft_any(const AnyArgs a) {
@@ -1253,6 +1339,65 @@ hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* 
                       : launch_any(k_synth_any<false, true>, a, items, stream, true);
     return t.gain ? launch_any(k_synth_any<true, false>, a, items, stream, false)
                   : launch_any(k_synth_any<false, false>, a, items, stream, false);
+}
+
+hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,
+                            const float* x, float* y, int n_streams, int64_t T, int64_t ld_x,
+                            int64_t ld_y, int64_t F, hipStream_t stream) {
+    const int p = g.n / 2;
+    if (F <= 0 || n_streams <= 0 || !any_supported(p)) return hipErrorInvalidValue;
+    AnyFusedArgs f{};
+    AnyArgs& a = f.a;
+    a.t = t;
+    a.twany = twany;
+    a.pl = make_any_plan(p);
+    a.in = x;
+    a.out = y;
+    a.ld_in = ld_x;
+    a.T = T;
+    a.h = g.h;
+    a.n_streams = n_streams;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
+    a.inv_n = g.inv_n;
+    a.tw_len = int(build_any_twiddles(p).size() / 2);
+    f.ld_y = ld_y;
+    f.F = int(F);
+    f.rl = g.h * ((g.n + g.h - 1) / g.h);
+    f.ring_len = g.ring_len;
+    f.gain = g.gain;
+    const size_t tables = sizeof(cf) * (size_t(a.tw_len) + p) + sizeof(float) * 4 * p;  // + ws
+    const size_t per_wave = sizeof(cf) * 2 * p + sizeof(float) * f.rl;
+    // two workgroups per CU when each still holds >= 3 walkers (their tails overlap),
+    // else one workgroup with as many walkers as the LDS takes (tables shared)
+    int per_cu = 2;
+    int w = int(std::min<size_t>(8, (75 * 1024 - std::min<size_t>(tables, 75 * 1024)) / per_wave));
+    if (w < 3) {
+        per_cu = 1;
+        w = int(std::min<size_t>(16, (150 * 1024 - std::min<size_t>(tables, 150 * 1024)) / per_wave));
+    }
+    if (w < 1) return hipErrorInvalidValue;  // too large for one CU: staged path
+    a.waves_per_block = w;
+    const int nb = (g.n + g.h - 1) / g.h;
+    const int resident = fused_resident_waves() / 16 * per_cu * w;  // CUs x walkers per CU
+    choose_chunks(F, n_streams, nb, resident, f.n_chunks, f.M);
+    const size_t lds = tables + size_t(w) * per_wave;
+    const int64_t waves = int64_t(n_streams) * f.n_chunks;
+    const int64_t grid = (waves + w - 1) / w;
+    auto k = t.gain ? k_stft_ola_any<true> : k_stft_ola_any<false>;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * w), lds, stream, f);
+    return hipGetLastError();
+}
+
+bool fused_any_fits(int n, int h) {
+    const int p = n / 2;
+    if (!any_supported(p) || h <= 0) return false;
+    const size_t tw_len = build_any_twiddles(p).size() / 2;
+    const size_t tables = sizeof(cf) * (tw_len + p) + sizeof(float) * 4 * p;
+    const size_t per_wave = sizeof(cf) * 2 * p + sizeof(float) * (h * ((n + h - 1) / h));
+    return tables + per_wave <= 150 * 1024;
 }
 
 hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
