@@ -39,7 +39,8 @@ struct crlot_plan {
     float* d_rden = nullptr;  // RN(1 / den)
     bool fast_ok = false;     // both exact rewrites valid for the current tables
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
-    float* d_twany = nullptr; // W_P^k (generic path)
+    float* d_twany = nullptr; // per-pass twiddles of the mixed-radix path (aliases d_tw when generic)
+    float* d_twany_own = nullptr;  // ... or its own table (power-of-two plans, any-shape streams)
     // staged-path workspace
     float* d_work = nullptr;
     int64_t work_bytes = 0;
@@ -95,7 +96,7 @@ void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
-                     p->d_rden})  // d_twany aliases d_tw
+                     p->d_rden, p->d_twany_own})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
     delete p;
 }
@@ -573,29 +574,49 @@ struct crlot_stream {
     crlot_plan* plan = nullptr;
     int channels = 0;
     int interleaved = 0;
-    int64_t q = 0;  // hops pushed so far
+    bool any = false;  // any-shape kernel (fft_any.h) instead of k_stream_hop
+    int64_t q = 0;     // hops pushed so far
     float* d_hist = nullptr;
     float* d_acc = nullptr;
+    size_t hist_floats = 0, acc_floats = 0;
 };
+
+// frames a DROP Framer has produced after q+1 hops of H samples (framer.cc:88-117)
+static int64_t drop_frames_after(int64_t hops, int64_t n, int64_t h) {
+    const int64_t t = hops * h;
+    return t >= n ? (t - n) / h + 1 : 0;
+}
 
 int crlot_stream_create(crlot_plan* p, int32_t channels, crlot_stream** out) {
     if (!p || !out || channels <= 0) return fail(CRLOT_EINVAL, "bad argument");
     *out = nullptr;
     if (p->boundary == CRLOT_FRAMEQUEUE)
         return fail(CRLOT_EINVAL, "FrameQueue framing is whole-signal; stream with ZERO_PAD/DROP");
-    if (!crlot::fused_supported(p->geo.n, p->geo.h))
-        return fail(CRLOT_EUNSUPPORTED, "streaming path needs H % 128 == 0, N % H == 0, N <= 2048");
     DeviceGuard g(p->device);
+    const bool any = !crlot::fused_supported(p->geo.n, p->geo.h);
+    if (any && !crlot::any_supported(p->geo.n / 2))
+        return fail(CRLOT_EUNSUPPORTED, "frame size not supported on the streaming path");
+    hipError_t e;
+    if (any && !p->d_twany) {  // power-of-two plan streaming with a non-fused hop
+        const std::vector<float> tw = crlot::build_any_twiddles(p->geo.n / 2);
+        if ((e = hipMalloc(&p->d_twany_own, sizeof(float) * tw.size())) ||
+            (e = hipMemcpy(p->d_twany_own, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)))
+            return hip_fail(e, "twiddles (any-shape stream)");
+        p->d_twany = p->d_twany_own;
+    }
     crlot_stream* st = new crlot_stream();
     st->plan = p;
     st->channels = channels;
-    const size_t bytes = sizeof(float) * size_t(channels) * p->geo.n;
-    hipError_t e;
-    if ((e = hipMalloc(&st->d_hist, bytes)) || (e = hipMalloc(&st->d_acc, bytes))) {
+    st->any = any;
+    st->hist_floats = size_t(channels) * (any ? crlot::stream_any_hist_len(p->geo.n, p->geo.h) : p->geo.n);
+    st->acc_floats = size_t(channels) * (any ? crlot::stream_any_ring_len(p->geo.n, p->geo.h) : p->geo.n);
+    if ((e = hipMalloc(&st->d_hist, sizeof(float) * st->hist_floats)) ||
+        (e = hipMalloc(&st->d_acc, sizeof(float) * st->acc_floats))) {
         crlot_stream_destroy(st);
         return hip_fail(e, "hipMalloc(stream state)");
     }
-    if ((e = hipMemset(st->d_hist, 0, bytes)) || (e = hipMemset(st->d_acc, 0, bytes))) {
+    if ((e = hipMemset(st->d_hist, 0, sizeof(float) * st->hist_floats)) ||
+        (e = hipMemset(st->d_acc, 0, sizeof(float) * st->acc_floats))) {
         crlot_stream_destroy(st);
         return hip_fail(e, "hipMemset(stream state)");
     }
@@ -614,9 +635,9 @@ void crlot_stream_destroy(crlot_stream* st) {
 int crlot_stream_reset(crlot_stream* st) {
     if (!st) return fail(CRLOT_EINVAL, "null stream");
     DeviceGuard g(st->plan->device);
-    const size_t bytes = sizeof(float) * size_t(st->channels) * st->plan->geo.n;
     hipError_t e;
-    if ((e = hipMemset(st->d_hist, 0, bytes)) || (e = hipMemset(st->d_acc, 0, bytes)))
+    if ((e = hipMemset(st->d_hist, 0, sizeof(float) * st->hist_floats)) ||
+        (e = hipMemset(st->d_acc, 0, sizeof(float) * st->acc_floats)))
         return hip_fail(e, "hipMemset(stream state)");
     st->q = 0;
     return CRLOT_OK;
@@ -637,6 +658,18 @@ int crlot_stream_push_hop(crlot_stream* st, const float* d_in, float* d_out, int
     DeviceGuard g(p->device);
     const int64_t C = st->channels, H = p->geo.h;
     const int64_t ld = st->interleaved ? 1 : H, inc = st->interleaved ? C : 1;
+    if (st->any) {
+        const int64_t n = p->geo.n;
+        const int64_t fc = drop_frames_after(st->q + 1, n, H), fp = drop_frames_after(st->q, n, H);
+        const int64_t k = fc > fp ? fc - 1 : -1;
+        hipError_t e = crlot::launch_stream_any(p->geo, tables(p), p->d_twany, d_in, ld, inc, d_out, ld,
+                                                inc, st->d_hist, st->d_acc, st->channels, st->q, k,
+                                                static_cast<hipStream_t>(stream));
+        if (e != hipSuccess) return hip_fail(e, "stream kernel launch");
+        if (emitted) *emitted = k >= 0 ? int32_t(H) : 0;
+        st->q += 1;
+        return CRLOT_OK;
+    }
     hipError_t e = crlot::launch_stream_hop(p->geo, tables(p), d_in, ld, inc, d_out, ld, inc,
                                             st->d_hist, st->d_acc, st->channels, st->q,
                                             static_cast<hipStream_t>(stream));

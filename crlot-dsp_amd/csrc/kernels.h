@@ -71,6 +71,15 @@ std::vector<float> build_any_twiddles(int p);
 hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* twany,
                             const float* x, int n_streams, int64_t T, int64_t ld_x, int64_t F,
                             float* frames, float* spec, hipStream_t stream);
+// Any-shape streaming hop (DROP Framer, one wave per channel).  hist: [C][hl],
+// acc: [C][rl] floats (zeroed at creation); k = frame completed by hop q or -1.
+int stream_any_hist_len(int n, int h);
+int stream_any_ring_len(int n, int h);
+hipError_t launch_stream_any(const Geometry& g, const DevTables& t, const float* twany,
+                             const float* in, int64_t in_ld, int64_t in_inc, float* out,
+                             int64_t out_ld, int64_t out_inc, float* hist, float* acc, int channels,
+                             int64_t q, int64_t k, hipStream_t stream);
+
 // Fused any-size walker (OLA ring in LDS): bit-identical to synth_any + ola_gather.
 bool fused_any_fits(int n, int h);
 hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,

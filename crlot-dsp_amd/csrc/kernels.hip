@@ -802,6 +802,76 @@ __global__ __launch_bounds__(1024) void k_stft_ola_any(const AnyFusedArgs f) {
     }
 }
 
+// K_stream_any: one hop of the per-hop streaming path for any N, H (DROP Framer).
+// Per channel: `hist` holds the last hl >= N + H samples (hop q at (qH) mod hl),
+// `acc` the OLA ring of rl = H ceil(N/H) floats.  When this hop completes frame
+// k (host-decided: wave-uniform), the frame runs through the same arithmetic as
+// K_fused_any and block k (H samples) is emitted.
+struct StreamAnyArgs {
+    AnyArgs a;                       // tables, plan, in (hop), out (hop), inv_n, h
+    float* hist;
+    float* acc;
+    int64_t in_ld, in_inc, out_ld, out_inc;
+    int64_t q, k;                    // hop index; frame completed by it (-1: none)
+    int channels, hl, rl, ring_len;
+    float gain;
+};
+
+template <bool HAS_GAIN>
+__global__ __launch_bounds__(512) void k_stream_any(const StreamAnyArgs f) {
+    const AnyArgs& a = f.a;
+    const int p = a.pl.p, n = 2 * p, H = a.h;
+    const int lane = threadIdx.x & 63;
+    const AnyLds l = any_lds<true>(a, true);
+    const int wave = threadIdx.x >> 6;
+    float* ws = reinterpret_cast<float*>(l.A - size_t(wave) * 2 * p + size_t(a.waves_per_block) * 2 * p);
+    if (wave == 0)
+        for (int i = lane; i < n; i += 64) ws[i] = a.t.ws[i];
+    __syncthreads();
+    const int c = blockIdx.x * a.waves_per_block + wave;
+    if (c >= f.channels) return;
+    float* hist = f.hist + int64_t(c) * f.hl;
+    float* acc = f.acc + int64_t(c) * f.rl;
+    // store the hop
+    const int hb = int((f.q * H) % f.hl);
+    for (int i = lane; i < H; i += 64) hist[hb + i] = a.in[c * f.in_ld + i * f.in_inc];
+    if (f.k < 0) return;
+    __threadfence();  // the hop written by other lanes of this wave is read back below
+    const int64_t k = f.k;
+    const int fb = int((k * H) % f.hl);
+    cf* A = l.A;
+    cf* B = l.B;
+    for (int i = lane; i < p; i += 64) {
+        int j0 = fb + 2 * i, j1 = j0 + 1;
+        if (j0 >= f.hl) j0 -= f.hl;
+        if (j1 >= f.hl) j1 -= f.hl;
+        A[i] = {dev::sanit(hist[j0] * l.wa[2 * i]), dev::sanit(hist[j1] * l.wa[2 * i + 1])};
+    }
+    dev::wave_lds_fence();
+    cf* z = dev::any::fft<false>(A, B, a.pl, l.tw, lane);
+    cf* zo = z == A ? B : A;
+    dev::any::split_merge<HAS_GAIN>(z, zo, p, l.st, a.t.gain, nullptr, lane);
+    dev::wave_lds_fence();
+    const cf* r = dev::any::fft<true>(zo, z, a.pl, l.tw, lane);
+    const int nbr = f.rl / H;
+    const int rb = int(k % nbr) * H;
+    for (int i = lane; i < n; i += 64) {
+        const cf v = r[i >> 1];
+        const float src = dev::sanit(((i & 1) ? v.i : v.r) * a.inv_n);
+        int pos = rb + i;
+        if (pos >= f.rl) pos -= f.rl;
+        acc[pos] = __builtin_fmaf(__builtin_fmaf(src, ws[i], 0.0f), f.gain, acc[pos]);
+    }
+    __threadfence_block();
+    const int di = int((k * H) % f.ring_len);
+    for (int i = lane; i < H; i += 64) {
+        int d = di + i;
+        if (d >= f.ring_len) d -= f.ring_len;
+        a.out[c * f.out_ld + i * f.out_inc] = acc[rb + i] / a.t.den[d];
+        acc[rb + i] = 0.0f;
+    }
+}
+
 // batched IFftPlan::forward / inverse / forward_complex / inverse_complex, any size
 template <int KIND, bool LDS_TABLES>  // KIND: 0 rfft, 1 irfft, 2 cfft, 3 icfft
 __global__ __launch_bounds__(512) void k_fft_any(const AnyArgs a) {
@@ -1219,6 +1289,8 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
 bool synth_supported(int n) { return e_of(n) != 0; }
 
 // ---- any-size path
+int stream_any_hist_len(int n, int h) { return h * ((n + h + h - 1) / h); }  // >= N + H, H multiple
+int stream_any_ring_len(int n, int h) { return h * ((n + h - 1) / h); }
 // kf_factor order: 4s, then 2s, then odd primes; per-pass twiddle tables laid out
 // as fft_any.h PassDesc describes (the device table = build_any_twiddles(p)).
 static std::vector<int> any_factors(int p) {
@@ -1388,6 +1460,48 @@ hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* 
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * w), lds, stream, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_any(const Geometry& g, const DevTables& t, const float* twany,
+                             const float* in, int64_t in_ld, int64_t in_inc, float* out,
+                             int64_t out_ld, int64_t out_inc, float* hist, float* acc, int channels,
+                             int64_t q, int64_t k, hipStream_t stream) {
+    const int p = g.n / 2;
+    if (channels <= 0 || !any_supported(p)) return hipErrorInvalidValue;
+    StreamAnyArgs f{};
+    AnyArgs& a = f.a;
+    a.t = t;
+    a.twany = twany;
+    a.pl = make_any_plan(p);
+    a.in = in;
+    a.out = out;
+    a.h = g.h;
+    a.inv_n = g.inv_n;
+    a.tw_len = int(build_any_twiddles(p).size() / 2);
+    f.hist = hist;
+    f.acc = acc;
+    f.in_ld = in_ld;
+    f.in_inc = in_inc;
+    f.out_ld = out_ld;
+    f.out_inc = out_inc;
+    f.q = q;
+    f.k = k;
+    f.channels = channels;
+    f.hl = stream_any_hist_len(g.n, g.h);
+    f.rl = stream_any_ring_len(g.n, g.h);
+    f.ring_len = g.ring_len;
+    f.gain = g.gain;
+    const size_t tables = sizeof(cf) * (size_t(a.tw_len) + p) + sizeof(float) * 4 * p;
+    const size_t per_wave = sizeof(cf) * 2 * p;
+    int w = int(std::min<size_t>(8, (150 * 1024 - std::min<size_t>(tables, 150 * 1024)) / per_wave));
+    if (w < 1) return hipErrorInvalidValue;
+    a.waves_per_block = w;
+    const size_t lds = tables + size_t(w) * per_wave;
+    auto kern = t.gain ? k_stream_any<true> : k_stream_any<false>;
+    hipError_t e = set_lds(kern, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(unsigned((channels + w - 1) / w)), dim3(64 * w), lds, stream, f);
     return hipGetLastError();
 }
 

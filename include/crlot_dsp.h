@@ -193,8 +193,9 @@ int crlot_fft_inverse_complex(crlot_fft_plan* plan, const float* d_in_complex, f
  * samples per channel into d_hop_out; *emitted (host) gets 0 or H.  Layout:
  * channel-major [channels][H] by default, or interleaved [H][channels] (the
  * reference's interleaved PCM) after crlot_stream_set_layout(st, 1).  Device
- * state (last N input samples, OLA blocks) persists across calls; the shapes
- * are those of the fused path (H % 128 == 0, N % H == 0, N <= 2048). */
+ * state (the recent input samples, the OLA blocks) persists across calls.  Any
+ * N / H the plan accepts: H % 128 == 0, N % H == 0, N <= 2048 run the
+ * register-resident per-hop kernel, other shapes the mixed-radix one. */
 int crlot_stream_create(crlot_plan* plan, int32_t channels, crlot_stream** out);
 void crlot_stream_destroy(crlot_stream* st);
 int crlot_stream_reset(crlot_stream* st);
