@@ -107,8 +107,8 @@ def load_pmc_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=50)  # ~130 ms: lets the clocks ramp
     ap.add_argument("--streams", type=int, default=STREAMS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
