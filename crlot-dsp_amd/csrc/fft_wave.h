@@ -235,6 +235,59 @@ __device__ __forceinline__ void fft_wave(cf (&v)[E], cf* buf, const cf* twp, int
     fft_passes<E, 1, 0, INV>(v, buf, twp, lane, none);
 }
 
+// ---- two frames per wave: the same passes on v0 and v1, sharing the twiddle
+// loads and one fence pair per exchange, so the two instruction streams interleave.
+template <int E, int R, int NS>
+__device__ __forceinline__ void stockham_exchange2(cf (&v0)[E], cf (&v1)[E], cf* buf0, cf* buf1,
+                                                   int lane) {
+    constexpr int B = E / R;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int j = lane + 64 * b;
+        const int base = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            buf0[swz<NS, R>(base + r * NS)] = v0[b + r * B];
+            buf1[swz<NS, R>(base + r * NS)] = v1[b + r * B];
+        }
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        v0[m] = buf0[swz<NS, R>(lane + 64 * m)];
+        v1[m] = buf1[swz<NS, R>(lane + 64 * m)];
+    }
+    wave_lds_fence();
+}
+
+template <int E, int NS, int TOFF, bool INV, typename TW>
+__device__ __forceinline__ void fft_passes2(cf (&v0)[E], cf (&v1)[E], cf* buf0, cf* buf1,
+                                            const cf* twp, int lane, const TW& tw) {
+    constexpr int P = 64 * E;
+    if constexpr (NS < P) {
+        constexpr int R = radix_for(P / NS, E);
+        stockham_compute<E, R, NS, INV>(v0, tw);
+        stockham_compute<E, R, NS, INV>(v1, tw);
+        if constexpr (NS * R < P) {
+            constexpr int NS2 = NS * R;
+            constexpr int R2 = radix_for(P / NS2, E);
+            constexpr int TOFF2 = TOFF + (NS > 1 ? (R - 1) * NS : 0);
+            PassTw<E, R2, NS2> tw2;
+            load_pass_tw<E, R2, NS2, TOFF2>(tw2, twp, lane);
+            stockham_exchange2<E, R, NS>(v0, v1, buf0, buf1, lane);
+            fft_passes2<E, NS2, TOFF2, INV>(v0, v1, buf0, buf1, twp, lane, tw2);
+        }
+    }
+}
+
+template <int E, bool INV>
+__device__ __forceinline__ void fft_wave2(cf (&v0)[E], cf (&v1)[E], cf* buf0, cf* buf1,
+                                          const cf* twp, int lane) {
+    constexpr int R = radix_for(64 * E, E);
+    PassTw<E, R, 1> none;
+    fft_passes2<E, 1, 0, INV>(v0, v1, buf0, buf1, twp, lane, none);
+}
+
 // All passes' per-lane twiddles held in registers (they do not depend on the
 // frame, so a wave that walks many frames loads them once).
 template <int E, int NS, bool END = (NS >= 64 * E)>
@@ -437,6 +490,60 @@ __device__ __forceinline__ void real_split_hook_merge(cf (&v)[E], cf* buf, const
         v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
         v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
         if (m == 0 && lane == 0) v[0] = dc_merge(xk, xpk);
+    }
+}
+
+// One element of the split -> gain -> merge (the arithmetic of real_split_hook_merge).
+template <bool HAS_GAIN>
+__device__ __forceinline__ cf split_merge_elem(cf zk, cf zp, cf w, cf wh, const float* gain, int k,
+                                               int P, bool dc) {
+    const cf fpnk = conj(zp);
+    const cf f1 = cadd(zk, fpnk);
+    const cf f2 = csub(zk, fpnk);
+    const cf t = cmul(f2, wh);
+    cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
+    cf xpk = {__builtin_fmaf(f1.r, 0.5f, -t.r), __builtin_fmaf(f1.i, -0.5f, t.i)};
+    if (dc) dc_split(zk, xk, xpk);
+    if constexpr (HAS_GAIN) {
+        const float gk = gain[k], gpk = gain[P - k];
+        xk = {xk.r * gk, xk.i * gk};
+        xpk = {xpk.r * gpk, xpk.i * gpk};
+    }
+    const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+    const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+    cf o = {__builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r)),
+            __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i))};
+    if (dc) o = dc_merge(xk, xpk);
+    return o;
+}
+
+// Two frames at once (fft_wave2 companion): the st/sth reads are shared.
+template <int E, bool HAS_GAIN>
+__device__ __forceinline__ void real_split_hook_merge2(cf (&v0)[E], cf (&v1)[E], cf* buf0, cf* buf1,
+                                                       const cf* st, const cf* sth,
+                                                       const float* gain, int lane) {
+    constexpr int P = 64 * E;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        buf0[lane + 64 * m] = v0[m];
+        buf1[lane + 64 * m] = v1[m];
+    }
+    wave_lds_fence();
+    cf zp0[E], zp1[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int pk = (P - (lane + 64 * m)) & (P - 1);
+        zp0[m] = buf0[pk];
+        zp1[m] = buf1[pk];
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + 64 * m;
+        const cf w = st[k], wh = sth[k];
+        const bool dc = m == 0 && lane == 0;
+        v0[m] = split_merge_elem<HAS_GAIN>(v0[m], zp0[m], w, wh, gain, k, P, dc);
+        v1[m] = split_merge_elem<HAS_GAIN>(v1[m], zp1[m], w, wh, gain, k, P, dc);
     }
 }
 

@@ -298,6 +298,150 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED_MIN_WAVES) void k_stft_ola_fuse
     }
 }
 
+// ------------------------------------------------------------------ fused, two frames per wave
+// K_fused2 k_stft_ola_fused2<E,S,NB>: K_fused with frames k and k+1 in flight
+// per iteration (fft_wave2: shared twiddle/window/super-twiddle reads, one
+// fence pair per exchange for both frames).  xin holds hops k..k+NB; the OLA
+// adds frame k, emits block k, then adds frame k+1 -- the same ascending-k
+// arithmetic, so results equal K_fused bit for bit.  Exact-rewrite numerics only.
+template <int S, int E>
+__device__ __forceinline__ void load_hop(float2* dst, __amdgpu_buffer_rsrc_t rx, int lane, int origin,
+                                         int T, int mode) {
+    constexpr int H = 128 * S;
+    if (origin >= 0 && origin + H <= T) {
+#pragma unroll
+        for (int q = 0; q < S; ++q) dst[q] = dev::bload2(rx, lane * 8 + q * 512, origin * 4);
+    } else {
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+            const int j = origin + 2 * (lane + 64 * q);
+            dst[q] = make_float2(fetch_x(rx, j, T, mode), fetch_x(rx, j + 1, T, mode));
+        }
+    }
+}
+
+#ifndef CRLOT_FUSED2_MIN_WAVES
+#define CRLOT_FUSED2_MIN_WAVES 1
+#endif
+template <int E, int S, int NB, bool HAS_GAIN>
+__global__ __launch_bounds__(kBlock, CRLOT_FUSED2_MIN_WAVES) void k_stft_ola_fused2(const FusedArgs a) {
+    constexpr int P = 64 * E, N = 2 * P, H = 128 * S;
+    static_assert(NB * S == E, "N = NB * H");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    cf* sth = st + P;
+    float* wa = reinterpret_cast<float*>(sth + P);
+    float* ws = wa + N;
+    cf* bufs = reinterpret_cast<cf*>(ws + N);
+    load_tables<E>(a.t, tw, st, sth, wa, ws, true, a.t.wsn);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    cf* buf0 = bufs + wave * 2 * P;
+    cf* buf1 = buf0 + P;
+    const int gw = blockIdx.x * kWaves + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1));
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
+    const __amdgpu_buffer_rsrc_t rr = dev::make_rsrc(a.t.rden, uint32_t(a.ring_blocks * H) * 4u);
+    const float g = a.gain;
+
+    // xin[h*S + q]: hop (k + h), pair q, h = 0..NB
+    float2 xin[E + S];
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) load_hop<S, E>(xin + h * S, rx, lane, (fs + h) * H - a.pad, a.T, a.pad_mode);
+    float2 acc[NB][S];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[j][q] = make_float2(0.f, 0.f);
+
+    auto windowed = [&](cf (&v)[E], int off) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float2 w = *reinterpret_cast<const float2*>(wa + 2 * (lane + 64 * m));
+            v[m].r = dev::sanit(xin[off + m].x * w.x);
+            v[m].i = dev::sanit(xin[off + m].y * w.y);
+        }
+    };
+    auto accumulate = [&](const cf (&v)[E]) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float2 w = *reinterpret_cast<const float2*>(ws + 2 * (lane + 64 * m));
+            const float o0 = dev::sanit_scaled<N>(v[m].r);
+            const float o1 = dev::sanit_scaled<N>(v[m].i);
+            float2& r = acc[m / S][m % S];
+            r.x = __builtin_fmaf(__builtin_fmaf(o0, w.x, 0.0f), g, r.x);
+            r.y = __builtin_fmaf(__builtin_fmaf(o1, w.y, 0.0f), g, r.y);
+        }
+    };
+    auto emit = [&](int k) {  // produce(H) of block k, then shift the accumulators
+        if (k >= f0) {
+            float2 dn[S], rn[S];
+#pragma unroll
+            for (int q = 0; q < S; ++q) {
+                dn[q] = dev::bload2(rd, lane * 8 + q * 512, (k % a.ring_blocks) * H * 4);
+                rn[q] = dev::bload2(rr, lane * 8 + q * 512, (k % a.ring_blocks) * H * 4);
+            }
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < S; ++q) ok = ok && mk_ok(acc[0][q].x) && mk_ok(acc[0][q].y);
+            const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
+#pragma unroll
+            for (int q = 0; q < S; ++q) {
+                const float2 o = fast ? make_float2(mk_div(acc[0][q].x, dn[q].x, rn[q].x),
+                                                    mk_div(acc[0][q].y, dn[q].y, rn[q].y))
+                                      : make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y);
+                dev::bstore2(o, ry, lane * 8 + q * 512, k * H * 4);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < S; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[NB - 1][q] = make_float2(0.f, 0.f);
+    };
+
+    int k = fs;
+    for (; k + 1 < f1; k += 2) {
+        // prefetch hops k+NB+1, k+NB+2 for the next pair
+        float2 nxt[2 * S];
+        load_hop<S, E>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
+        load_hop<S, E>(nxt + S, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        cf v0[E], v1[E];
+        windowed(v0, 0);
+        windowed(v1, S);
+        dev::fft_wave2<E, false>(v0, v1, buf0, buf1, tw, lane);
+        dev::real_split_hook_merge2<E, HAS_GAIN>(v0, v1, buf0, buf1, st, sth, a.t.gain, lane);
+        dev::fft_wave2<E, true>(v0, v1, buf0, buf1, tw, lane);
+        accumulate(v0);
+        emit(k);
+        accumulate(v1);
+        emit(k + 1);
+#pragma unroll
+        for (int m = 0; m < E - S; ++m) xin[m] = xin[m + 2 * S];
+#pragma unroll
+        for (int q = 0; q < 2 * S; ++q) xin[E - S + q] = nxt[q];
+    }
+    if (k < f1) {  // odd count: the last frame alone
+        cf v0[E];
+        windowed(v0, 0);
+        dev::fft_wave<E, false>(v0, buf0, tw, lane);
+        dev::real_split_hook_merge<E, HAS_GAIN, false>(v0, buf0, st, sth, a.t.gain, lane);
+        dev::fft_wave<E, true>(v0, buf0, tw, lane);
+        accumulate(v0);
+        emit(k);
+    }
+}
+
 // ------------------------------------------------------------------ fused, workgroup walker
 // K_fused_wg k_stft_ola_wg<L,S,NB>: the fused walk of K_fused for frames too big
 // for one wave (N = 16 L, E = 8): a workgroup of L lanes owns a run of frames
@@ -1065,6 +1209,16 @@ int e_of(int n) {
     }
 }
 
+// K_fused2 (two frames per wave) where its registers keep the occupancy: E = 4
+// (97-111 VGPRs, 4 waves/SIMD) and E = 8 with S = 2 (168: 3 waves/SIMD, the
+// headline); the other E = 8 hops need 170-197 VGPRs (2 waves/SIMD) and lose.
+constexpr bool fused2_used(int e, int s, bool fast) {
+#ifdef CRLOT_NO_FUSED2
+    return false;
+#endif
+    return fast && (e == 4 || (e == 8 && s == 2));
+}
+
 template <int E, int S>
 hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     constexpr int NB = E / S;
@@ -1072,6 +1226,16 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     const bool fast = false;
 #else
     const bool fast = a.t.wsn && a.t.rden;
+#endif
+#ifndef CRLOT_NO_FUSED2  // A/B builds: single-frame K_fused everywhere
+    if (fused2_used(E, S, fast)) {
+        auto k2 = a.t.gain ? k_stft_ola_fused2<E, S, NB, true> : k_stft_ola_fused2<E, S, NB, false>;
+        const size_t lds2 = Lds<E>::bytes + sizeof(cf) * kWaves * 64 * E;
+        hipError_t e2 = set_lds(k2, lds2);
+        if (e2 != hipSuccess) return e2;
+        hipLaunchKernelGGL(k2, dim3(unsigned(grid)), dim3(kBlock), lds2, stream, a);
+        return hipGetLastError();
+    }
 #endif
     auto k = a.t.gain ? (fast ? k_stft_ola_fused<E, S, NB, true, true> : k_stft_ola_fused<E, S, NB, true, false>)
                       : (fast ? k_stft_ola_fused<E, S, NB, false, true> : k_stft_ola_fused<E, S, NB, false, false>);
@@ -1193,7 +1357,11 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.M = int((F + a.n_chunks - 1) / a.n_chunks);
     a.n_chunks = int((F + a.M - 1) / a.M);
 #else
-    choose_chunks(F, n_streams, g.n / g.h, fused_resident_waves(), a.n_chunks, a.M);
+    // K_fused keeps 4 waves/SIMD resident, K_fused2 3
+    const int e = e_of(g.n);
+    const bool pair = fused2_used(e, g.h / 128, t.wsn && t.rden);
+    const int resident = pair && e == 8 ? fused_resident_waves() * 3 / 4 : fused_resident_waves();
+    choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
     if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
         const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
         a.M = int((F + n - 1) / n);
@@ -1207,7 +1375,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.gain = g.gain;
     const int64_t waves = int64_t(n_streams) * a.n_chunks;
     const int64_t grid = (waves + kWaves - 1) / kWaves;
-    const int e = e_of(g.n), s = g.h / 128;
+    const int s = g.h / 128;
     switch (e) {
         case 2: return fused_e<2>(s, a, grid, stream);
         case 4: return fused_e<4>(s, a, grid, stream);
