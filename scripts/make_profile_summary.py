@@ -65,6 +65,13 @@ if kt:
     if ds:
         ds.sort()
         med, mn = ds[len(ds) // 2], ds[0]
+# bench.py's own HIP-event kernel time from the same profiled run (trace.log)
+bench_ms = None
+for lf in (f"{src}/trace.log",):
+    if os.path.exists(lf):
+        for line in open(lf):
+            if line.startswith("{"):
+                bench_ms = json.loads(line)["roofline"]["kernel_ms"]
 out = {
     "tag": tag,
     "workload_key": f"{S}x{T}_N{N}_H{H}",
@@ -72,6 +79,7 @@ out = {
     "median_duration_ns_trace": med,
     "min_duration_ns_trace": mn,
     "avg_duration_ns_trace": dur,
+    "bench_event_ms_same_run": bench_ms,
     "pmc_per_launch": pmc,
     "algorithmic_bytes_per_launch": alg_read + alg_write,
     "hbm_bytes_per_launch": hbm,

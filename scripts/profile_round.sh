@@ -15,7 +15,7 @@ run() {  # name secs cmd...
   local rc=$?; echo "   rc=$rc"
   if [ $rc -ne 0 ]; then tail -n 20 $OUT/$name.log; exit $rc; fi
 }
-run trace 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+run trace 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 20 --warmup 50 --no-cpu-baseline
 run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d $OUT/fetch -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
 run write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats -d $OUT/write -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
 run sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY --kernel-trace --stats -d $OUT/sq -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
