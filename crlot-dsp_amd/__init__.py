@@ -87,6 +87,7 @@ def lib():
         "crlot_plan_destroy": ([vp], None),
         "crlot_plan_upload_tables": ([vp, vp, vp], C.c_int),
         "crlot_plan_set_spectral_gain": ([vp, vp], C.c_int),
+        "crlot_plan_set_frame_pairing": ([vp, i32], C.c_int),
         "crlot_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "crlot_frame_count": ([vp, i64], i64),
         "crlot_output_length": ([vp, i64], i64),
@@ -212,6 +213,7 @@ class PlanConfig:
     device: int = -1
     center: bool = True          # boundary_mode == FRAMEQUEUE only (FrameQueue default)
     pad_mode: int = PAD_CONSTANT
+    frame_pairing: bool = True   # crlot_plan_set_frame_pairing (N = 1024 fused path)
 
 
 class Plan:
@@ -235,6 +237,7 @@ class Plan:
         n, hop, ring = C.c_int32(), C.c_int32(), C.c_int32()
         _check(lib().crlot_plan_info(self._h, C.byref(n), C.byref(hop), C.byref(ring)))
         self.frame_size, self.hop_size, self.ring_len = n.value, hop.value, ring.value
+        self.set_frame_pairing(cfg.frame_pairing)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -265,6 +268,11 @@ class Plan:
         nm = None if norm is None else np.ascontiguousarray(norm, np.float32)
         _check(lib().crlot_plan_upload_tables(self._h, None if w is None else w.ctypes.data,
                                               None if nm is None else nm.ctypes.data))
+
+    def set_frame_pairing(self, enable: bool = True):
+        """Two frames per complex transform on the fused round trip (default);
+        False selects the per-frame kernels, bit-identical to stages + ola_gather."""
+        _check(lib().crlot_plan_set_frame_pairing(self._h, int(bool(enable))))
 
     def set_spectral_gain(self, gain=None):
         g = None if gain is None else np.ascontiguousarray(gain, np.float32)

@@ -37,6 +37,8 @@ struct crlot_plan {
     float* d_gain = nullptr;
     float* d_wsn = nullptr;   // ws * (1/N)
     float* d_rden = nullptr;  // RN(1 / den)
+    float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
+    bool pairing = true;      // crlot_plan_set_frame_pairing
     bool fast_ok = false;     // both exact rewrites valid for the current tables
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
     float* d_twany = nullptr; // per-pass twiddles of the mixed-radix path (aliases d_tw when generic)
@@ -89,6 +91,7 @@ crlot::DevTables tables(const crlot_plan* p) {
         t.wsn = p->d_wsn;
         t.rden = p->d_rden;
     }
+    if (p->pairing) t.ptw = p->d_ptw;
     return t;
 }
 
@@ -96,7 +99,7 @@ void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
-                     p->d_rden, p->d_twany_own})  // d_twany aliases d_tw or d_twany_own
+                     p->d_rden, p->d_twany_own, p->d_ptw})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
     delete p;
 }
@@ -264,6 +267,14 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }
+    if (n == 1024) {  // K_pair tables
+        const std::vector<float> ptw = crlot::build_pair_twiddles();
+        if ((e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
+            (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {
+            free_plan(p);
+            return hip_fail(e, "pair twiddles");
+        }
+    }
     if (generic) p->d_twany = p->d_tw;  // the same allocation: W_P^k
     if ((e = hipMemcpy(p->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
         (e = hipMemcpy(p->d_st, st.data(), sizeof(float) * 2 * P, hipMemcpyHostToDevice))) {
@@ -306,6 +317,12 @@ int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
     hipError_t e = hipMemcpy(p->d_gain, gain, sizeof(float) * bins, hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy(gain)");
     p->has_gain = true;
+    return CRLOT_OK;
+}
+
+int crlot_plan_set_frame_pairing(crlot_plan* p, int32_t enable) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    p->pairing = enable != 0;
     return CRLOT_OK;
 }
 

@@ -20,7 +20,13 @@ struct DevTables {
     // fall outside the ranges where the rewrites are bit-identical):
     const float* wsn = nullptr;  // ws * (1/N): folds the inverse's 1/N into the window
     const float* rden = nullptr; // RN(1 / den): Markstein division
+    // Frame-pair transform tables (N = 1024 plans with pairing on, else nullptr):
+    // W1024^{l k1} (15 x 64, fft_pair.h pair_t1_index) then W64^{b c} [c-1][b] (3 x 16), float pairs.
+    const float* ptw = nullptr;
 };
+
+// Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.
+std::vector<float> build_pair_twiddles();
 
 // Per-pass Stockham twiddles for an N-point real frame (P = N/2 complex points),
 // laid out as the device reads them (fft_wave.h twiddle_table_size), computed in

@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "fft_any.h"
+#include "fft_pair.h"
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -439,6 +440,225 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED2_MIN_WAVES) void k_stft_ola_fus
         dev::fft_wave<E, true>(v0, buf0, tw, lane);
         accumulate(v0);
         emit(k);
+    }
+}
+
+// ------------------------------------------------------------------ fused, frame pairs (N = 1024)
+// K_pair k_stft_ola_pair<SH,NB,W>: the fused walk with frames 2j and 2j+1 of a
+// stream packed into ONE 1024-point complex transform (fft_pair.h):
+// z = sanit(x_2j * w) + i sanit(x_2j+1 * w); the round trip's real part is frame
+// 2j's push_frame_AoS input and the imaginary part frame 2j+1's.  Pairs are
+// aligned to even frame indices whatever the chunking (a chunk's warm-up starts
+// on an even frame and a pair straddling its end still transforms the real
+// partner), so every frame's bits depend only on the stream.  Lane l holds
+// samples l + 64 m of the frame; a hop is SH = H/64 floats per lane.
+// Everything after the inverse is K_fused2's: folded 1/N, sanitize, OLA in
+// ascending k, Markstein division with a per-wave IEEE fallback.
+template <int SH>
+__device__ __forceinline__ void load_hop1(float* dst, __amdgpu_buffer_rsrc_t rx, int lane, int origin,
+                                          int T, int mode) {
+    constexpr int H = 64 * SH;
+#ifdef CRLOT_ABL_NOLOAD  // timing-only ablation: wrong results
+#pragma unroll
+    for (int q = 0; q < SH; ++q) dst[q] = float(lane + q + origin) * 1e-3f;
+    return;
+#endif
+    if (origin >= 0 && origin + H <= T) {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, lane * 4 + q * 256, origin * 4);
+    } else {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = fetch_x(rx, origin + lane + 64 * q, T, mode);
+    }
+}
+
+// LDS: t1 [15*64 cf] | wa4 [1024 f] | ws4 [1024 f] | per-wave transpose buffers.
+// Windows are stored [m/4][lane][m%4] so one ds_read_b128 gives a lane 4 taps.
+template <int W>
+struct PairLds {
+    static constexpr size_t t1 = 0;
+    static constexpr size_t wa = t1 + sizeof(cf) * 15 * 64;
+    static constexpr size_t ws = wa + sizeof(float) * 1024;
+    static constexpr size_t bufs = ws + sizeof(float) * 1024;
+    static constexpr size_t bytes = bufs + sizeof(cf) * dev::kPairXbuf * W;
+};
+
+#ifndef CRLOT_PAIR_MIN_WAVES
+#define CRLOT_PAIR_MIN_WAVES 4
+#endif
+template <int SH, int NB, int W, bool HAS_GAIN>
+__global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
+    constexpr int E = 16, N = 1024, H = 64 * SH;
+    static_assert(NB * SH == E, "N = NB * H");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* t1 = reinterpret_cast<cf*>(smem + PairLds<W>::t1);
+    float* wa4 = reinterpret_cast<float*>(smem + PairLds<W>::wa);
+    float* ws4 = reinterpret_cast<float*>(smem + PairLds<W>::ws);
+    {
+        const cf* g1 = reinterpret_cast<const cf*>(a.t.ptw);
+        for (int i = threadIdx.x; i < 15 * 64; i += 64 * W) t1[i] = g1[i];
+        for (int i = threadIdx.x; i < N; i += 64 * W) {
+            const int l = i & 63, m = i >> 6;  // tap n = l + 64 m
+            const int d = (m >> 2) * 256 + l * 4 + (m & 3);
+            wa4[d] = a.t.wa[i];
+            ws4[d] = a.t.wsn[i];
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    cf* buf = reinterpret_cast<cf*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
+    const int gw = blockIdx.x * W + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
+    const __amdgpu_buffer_rsrc_t rr = dev::make_rsrc(a.t.rden, uint32_t(a.ring_blocks * H) * 4u);
+    const float g = a.gain;
+    cf t2[3];
+    {
+        const cf* g2 = reinterpret_cast<const cf*>(a.t.ptw) + 15 * 64;
+#pragma unroll
+        for (int c2 = 0; c2 < 3; ++c2) t2[c2] = g2[c2 * 16 + (lane & 15)];
+    }
+    const int gbase = dev::pair_bin_lane(lane);
+
+    // xin[h*SH + q]: hop (k + h), h = 0..NB, sample lane + 64 q of the hop
+    float xin[E + SH];
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) load_hop1<SH>(xin + h * SH, rx, lane, (fs + h) * H - a.pad, a.T, a.pad_mode);
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+
+    auto accumulate = [&](const cf (&v)[E], bool imag) {
+#pragma unroll
+        for (int m4 = 0; m4 < E / 4; ++m4) {
+            const float4 w = *reinterpret_cast<const float4*>(ws4 + m4 * 256 + lane * 4);
+            const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int m = 4 * m4 + u;
+                const float o = dev::sanit_scaled<N>(imag ? v[m].i : v[m].r);
+                float& r = acc[m / SH][m % SH];
+                r = __builtin_fmaf(__builtin_fmaf(o, wv[u], 0.0f), g, r);
+            }
+        }
+    };
+    auto emit = [&](int k) {  // produce(H) of block k, then shift the accumulators
+        if (k >= f0) {
+            float dn[SH], rn[SH];
+#pragma unroll
+            for (int q = 0; q < SH; ++q) {
+                dn[q] = dev::bload1(rd, lane * 4 + q * 256, (k % a.ring_blocks) * H * 4);
+                rn[q] = dev::bload1(rr, lane * 4 + q * 256, (k % a.ring_blocks) * H * 4);
+            }
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < SH; ++q) ok = ok && mk_ok(acc[0][q]);
+            const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
+#pragma unroll
+            for (int q = 0; q < SH; ++q) {
+#ifdef CRLOT_ABL_NODIV  // timing-only ablation
+                const float o = acc[0][q] * rn[q];
+#else
+                const float o = fast ? mk_div(acc[0][q], dn[q], rn[q]) : acc[0][q] / dn[q];
+#endif
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry,
+                                                      lane * 4 + q * 256, k * H * 4, 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < SH; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
+    };
+
+    for (int k = fs; k < f1; k += 2) {
+        // prefetch hops k+NB+1, k+NB+2 for the next pair
+        float nxt[2 * SH];
+        load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
+        load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        const bool partner = k + 1 < a.F;  // frame k+1 exists (even past this chunk)
+        cf v[E];
+#pragma unroll
+        for (int m4 = 0; m4 < E / 4; ++m4) {
+            const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
+            const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int m = 4 * m4 + u;
+                v[m].r = dev::sanit(xin[m] * wv[u]);
+                v[m].i = partner ? dev::sanit(xin[m + SH] * wv[u]) : 0.0f;
+            }
+        }
+        dev::pair_fft_fwd(v, buf, t1, t2, lane);
+        if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins
+#pragma unroll
+            for (int d = 0; d < E; ++d) {
+                const int kb = gbase + 64 * d;
+                const float gk = a.t.gain[kb <= N / 2 ? kb : N - kb];
+                v[d] = cf{v[d].r * gk, v[d].i * gk};
+            }
+        }
+        dev::pair_fft_inv(v, buf, t1, t2, lane);
+#ifdef CRLOT_ABL_DUMMY  // timing-only: CRLOT_ABL_DUMMY extra independent VALU ops per pair
+        {
+            float d[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d[i] = v[i].r;
+#pragma unroll
+            for (int i = 0; i < CRLOT_ABL_DUMMY; ++i)
+#if defined(CRLOT_ABL_DUMMY_PK)
+                asm volatile("v_pk_add_f32 %0, %0, %0" : "+v"(*reinterpret_cast<double*>(&d[2 * (i & 3)])));
+#elif defined(CRLOT_ABL_DUMMY_CMP)
+            {
+                unsigned long long m;
+                asm volatile("v_cmp_ge_f32_e64 %0, |%1|, %1" : "=s"(m) : "v"(d[i & 7]));
+            }
+#elif defined(CRLOT_ABL_DUMMY_CND)
+                asm volatile("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(d[i & 7]) : "s"(__builtin_amdgcn_read_exec()));
+#elif defined(CRLOT_ABL_DUMMY_FMA3)
+                asm volatile("v_fma_f32 %0, %0, %0, %0" : "+v"(d[i & 7]));
+#elif defined(CRLOT_ABL_DUMMY_PERM)
+            if ((i & 1) == 0) {
+                const unsigned a0 = __builtin_bit_cast(unsigned, d[i & 7]), b0 = __builtin_bit_cast(unsigned, d[(i + 1) & 7]);
+                const auto r = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+                const unsigned r0 = r[0], r1 = r[1];
+                d[i & 7] = __builtin_bit_cast(float, r0);
+                d[(i + 1) & 7] = __builtin_bit_cast(float, r1);
+            }
+#elif defined(CRLOT_ABL_DUMMY_SALU)
+            {
+                unsigned long long m = __builtin_amdgcn_read_exec();
+                asm volatile("s_and_b64 %0, %0, %0" : "+s"(m));
+            }
+#else
+                asm volatile("v_add_f32 %0, %0, %0" : "+v"(d[i & 7]));
+#endif
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i].r = d[i];
+        }
+#endif
+        accumulate(v, false);
+        emit(k);
+        if (k + 1 < f1) {
+            accumulate(v, true);
+            emit(k + 1);
+        }
+#pragma unroll
+        for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
+#pragma unroll
+        for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
     }
 }
 
@@ -1246,6 +1466,41 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// K_pair: N = 1024, H = 64 * SH.  W waves per workgroup (16: one workgroup of
+// 155 KB LDS per CU, 4 waves/SIMD at <= 128 VGPRs).
+#ifndef CRLOT_PAIR_WAVES
+#define CRLOT_PAIR_WAVES 16
+#endif
+constexpr int kPairWaves = CRLOT_PAIR_WAVES;
+
+// Waves of K_pair a CU holds: whole workgroups within 160 KiB of LDS, at most
+// CRLOT_PAIR_MIN_WAVES per SIMD.
+constexpr int pair_waves_per_cu() {
+    return std::min(int(163840 / PairLds<kPairWaves>::bytes) * kPairWaves, 4 * CRLOT_PAIR_MIN_WAVES);
+}
+
+template <int SH>
+hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
+    constexpr int NB = 16 / SH, W = kPairWaves;
+    auto k = a.t.gain ? k_stft_ola_pair<SH, NB, W, true> : k_stft_ola_pair<SH, NB, W, false>;
+    const size_t lds = PairLds<W>::bytes;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    const int64_t grid = (waves + W - 1) / W;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream) {
+    switch (sh) {
+        case 2: return pair_sh<2>(a, waves, stream);
+        case 4: return pair_sh<4>(a, waves, stream);
+        case 8: return pair_sh<8>(a, waves, stream);
+        case 16: return pair_sh<16>(a, waves, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 template <int E>
 hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) {
     if constexpr (E >= 1) {
@@ -1310,6 +1565,24 @@ int wg_chunk_target() {
 
 }  // namespace
 
+std::vector<float> build_pair_twiddles() {
+    std::vector<float> t(2 * dev::kPairT1);
+    for (int k1 = 1; k1 < 16; ++k1)
+        for (int l = 0; l < 64; ++l) {
+            const double ph = -2.0 * M_PI * double(l * k1) / 1024.0;
+            const int i = dev::pair_t1_index(k1, l);
+            t[2 * i] = float(std::cos(ph));
+            t[2 * i + 1] = float(std::sin(ph));
+        }
+    for (int c = 1; c < 4; ++c)
+        for (int b = 0; b < 16; ++b) {
+            const double ph = -2.0 * M_PI * double(b * c) / 64.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    return t;
+}
+
 std::vector<float> build_pass_twiddles(int n) {
     const int p = n / 2, e = p / 64;
     std::vector<float> t;
@@ -1351,16 +1624,23 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.out_len = int(out_len);
     a.n_streams = n_streams;
     a.F = int(F);
+    const int e = e_of(g.n);
+    const bool fast = t.wsn && t.rden;
+#ifdef CRLOT_NO_PAIR  // A/B builds: per-frame kernels only
+    const bool use_pair = false;
+#else
+    const bool use_pair = g.n == 1024 && t.ptw && fast;
+#endif
 #ifdef CRLOT_OLD_CHUNKS  // A/B builds: fixed ~128-frame chunks
     const int target = 128;
     a.n_chunks = int((F + target - 1) / target);
     a.M = int((F + a.n_chunks - 1) / a.n_chunks);
     a.n_chunks = int((F + a.M - 1) / a.M);
 #else
-    // K_fused keeps 4 waves/SIMD resident, K_fused2 3
-    const int e = e_of(g.n);
-    const bool pair = fused2_used(e, g.h / 128, t.wsn && t.rden);
-    const int resident = pair && e == 8 ? fused_resident_waves() * 3 / 4 : fused_resident_waves();
+    // K_fused and K_pair keep 4 waves/SIMD resident, K_fused2 3
+    const bool pair = !use_pair && fused2_used(e, g.h / 128, fast);
+    const int resident = use_pair ? fused_resident_waves() * pair_waves_per_cu() / 16
+                         : pair && e == 8 ? fused_resident_waves() * 3 / 4 : fused_resident_waves();
     choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
     if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
         const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
@@ -1374,6 +1654,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.inv_n = g.inv_n;
     a.gain = g.gain;
     const int64_t waves = int64_t(n_streams) * a.n_chunks;
+    if (use_pair) return launch_pair(g.h / 64, a, waves, stream);
     const int64_t grid = (waves + kWaves - 1) / kWaves;
     const int s = g.h / 128;
     switch (e) {

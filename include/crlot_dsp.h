@@ -100,6 +100,14 @@ int crlot_plan_upload_tables(crlot_plan* plan, const float* window, const float*
 /* Spectral hook between rfft and irfft: real per-bin gain, N/2+1 host floats;
  * NULL restores the identity step of the reference (e2e_benchmark.cc:161-162). */
 int crlot_plan_set_spectral_gain(crlot_plan* plan, const float* gain);
+/* Frame pairing on the fused round trip (default on): two consecutive frames
+ * (2j, 2j+1) of a stream share one complex FFT, z = frame_2j + i frame_2j+1,
+ * whose real and imaginary round-trip outputs are the two frames' (exact for
+ * the real, bin-symmetric spectral gain).  Used where that kernel exists
+ * (N = 1024); results equal the per-frame kissfft formulation within float32
+ * rounding, not bit for bit.  0 selects the per-frame (kiss_fftr split)
+ * kernels, bit-identical to crlot_roundtrip_stages + crlot_ola_gather. */
+int crlot_plan_set_frame_pairing(crlot_plan* plan, int32_t enable);
 int crlot_plan_info(const crlot_plan* plan, int32_t* frame_size, int32_t* hop_size,
                     int32_t* ring_len);
 /* Frames of a T-sample stream: Framer whole push (framer.cc:88-117) or

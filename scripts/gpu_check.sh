@@ -22,6 +22,10 @@ step() {  # step NAME SECONDS CMD...
   return $rc
 }
 MODE=${1:-all}
+if [[ $MODE == sel ]]; then  # sel "<pytest -k expr>": selected GPU tests, then the bench
+  step pytest_sel 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread -k "$2"
+  step bench 600 python bench.py --no-cpu-baseline
+fi
 if [[ $MODE == all || $MODE == test ]]; then
   step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 fi

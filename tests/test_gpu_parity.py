@@ -118,7 +118,7 @@ def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
     torch = torch_cuda
     T = 200_000
     x = oracle.synth_streams(3, T, config_id=77)
-    plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan = pkg.Plan(frame_size=n, hop_size=h, frame_pairing=False)
     xd = dev(torch, x)
     y_fused = host(plan.roundtrip(xd))
     frames, _ = plan.stages(xd, want_spec=False)
@@ -131,6 +131,44 @@ def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
     assert np.array_equal(bits(y_unaligned), bits(y_fused))
 
 
+@pytest.mark.parametrize("h,mode", [(256, 0), (128, 0), (512, 1), (1024, 0), (256, 1)])
+def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, h, mode):
+    """K_pair (two frames per 1024-point complex transform) against the oracle's
+    per-frame kissfft chain and against the per-frame kernel, odd and even frame
+    counts, every hop the kernel takes."""
+    torch = torch_cuda
+    n = 1024
+    for T in (100_002, 99_998 + h):  # even T: 8-byte aligned rows take the fused path
+        x = oracle.synth_streams(3, T, config_id=h + mode + T % 7)
+        xd = dev(torch, x)
+        y = host(pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode).roundtrip(xd))
+        yu = host(pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode,
+                           frame_pairing=False).roundtrip(xd))
+        ref = oracle.roundtrip_batch(x, n, h, mode=mode, nthreads=4)
+        xmax = float(np.max(np.abs(x)))
+        for s in range(3):
+            assert_close(y[s], ref[s], xmax, f"pair H={h} T={T} stream {s}")
+            assert_close(y[s], yu[s], xmax, f"pair vs per-frame H={h} T={T} stream {s}")
+        assert not np.array_equal(bits(y), bits(yu))  # the pair kernel really ran
+
+
+def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch):
+    """Pairs are aligned to even frames, so a stream's output bits do not depend on
+    how its frames are chunked over waves nor on the batch it is processed in."""
+    torch = torch_cuda
+    n, h, T = 1024, 256, 60_000
+    x = oracle.synth_streams(5, T, config_id=12)
+    xd = dev(torch, x)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    y = host(plan.roundtrip(xd))
+    for s in (0, 3):
+        assert np.array_equal(bits(host(plan.roundtrip(xd[s:s + 1].contiguous()))[0]), bits(y[s]))
+    for chunks in ("1", "2", "3", "7", "40"):
+        monkeypatch.setenv("CRLOT_CHUNKS", chunks)
+        assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(y)), chunks
+    monkeypatch.delenv("CRLOT_CHUNKS")
+
+
 @pytest.mark.parametrize("scale", [1e-25, 1e25, 1.0])
 def test_fused_fast_division_and_fold_exact(pkg, oracle, torch_cuda, scale):
     """The fused kernel's exact rewrites (1/N folded into the window, Markstein
@@ -141,11 +179,17 @@ def test_fused_fast_division_and_fold_exact(pkg, oracle, torch_cuda, scale):
     x = (oracle.synth_streams(2, T, config_id=91) * np.float32(scale)).astype(np.float32)
     x[0, 1000:1100] = 0.0  # exact zeros inside a stream
     for n, h in ((1024, 256), (512, 128)):
-        plan = pkg.Plan(frame_size=n, hop_size=h)
+        plan = pkg.Plan(frame_size=n, hop_size=h, frame_pairing=False)
         xd = dev(torch, x)
         y = host(plan.roundtrip(xd))
         frames, _ = plan.stages(xd, want_spec=False)
         assert np.array_equal(bits(y), bits(host(plan.ola_gather(frames)))), (n, scale)
+        # the frame-pair kernel runs the same rewrites after its transforms
+        yp = host(pkg.Plan(frame_size=n, hop_size=h).roundtrip(xd))
+        xm = float(np.max(np.abs(x)))
+        for s in range(2):
+            assert_close(yp[s], y[s], xm, f"pair N={n} scale={scale}",
+                         xnorm=float(np.linalg.norm(x[s].astype(np.float64))))
 
 
 def test_ola_gather_bit_exact_random_frames(pkg, oracle, torch_cuda):
@@ -266,8 +310,13 @@ def test_spectral_gain_hook(pkg, oracle, torch_cuda):
         X = np.fft.rfft(seg * w) * g
         assert rel_l2(spec[f], X) < REL_L2
         assert rel_l2(frames[f], np.fft.irfft(X, n)) < 2 * REL_L2
+    y_ola = host(plan.ola_gather(dev(torch, frames[None])))[0]
+    y = host(plan.roundtrip(dev(torch, x[None])))[0]  # frame pairs: gain applied per complex bin
+    assert_close(y, y_ola, 0.5, "paired gain vs per-frame gain")
+    plan.set_frame_pairing(False)
     y = host(plan.roundtrip(dev(torch, x[None])))[0]
-    assert np.array_equal(bits(y), bits(host(plan.ola_gather(dev(torch, frames[None])))[0]))
+    assert np.array_equal(bits(y), bits(y_ola))
+    plan.set_frame_pairing(True)
     plan.set_spectral_gain(None)
     y0 = host(plan.roundtrip(dev(torch, x[None])))[0]
     assert_close(y0, oracle.roundtrip(x, n, h), 0.5, "identity restored")
@@ -368,9 +417,12 @@ def test_framequeue_fused_equals_staged(pkg, oracle, torch_cuda, n, h, pm):
     x = oracle.synth_streams(2, T, config_id=300 + pm)
     plan = _fq_plan(pkg, n, h, 1, pm, 0)
     xd = dev(torch, x)
+    plan.set_frame_pairing(False)
     y = host(plan.roundtrip(xd))
     frames, _ = plan.stages(xd, want_spec=False)
     assert np.array_equal(bits(y), bits(host(plan.ola_gather(frames))))
+    plan.set_frame_pairing(True)
+    y = host(plan.roundtrip(xd))  # the frame-pair kernel where N = 1024
     ref = oracle.roundtrip_batch_ex(x, n, h, mode=oracle.FRAMEQUEUE, center=True, pad_mode=pm,
                                     analysis_window=False, nthreads=2)
     for s in range(2):
@@ -646,7 +698,7 @@ def test_stream_per_hop_equals_batched_drop(pkg, oracle, torch_cuda, n, h, inter
     C_, hops = 64, 60
     T = hops * h
     x = oracle.synth_streams(C_, T, config_id=44)
-    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP, frame_pairing=False)
     if gain:
         plan.set_spectral_gain(np.linspace(1.0, 0.25, n // 2 + 1).astype(np.float32))
     xd = dev(torch, x)
