@@ -38,6 +38,9 @@ struct crlot_plan {
     float* d_wsn = nullptr;   // ws * (1/N)
     float* d_rden = nullptr;  // RN(1 / den)
     float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
+    float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024)
+    float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
+    float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
     bool fast_ok = false;     // both exact rewrites valid for the current tables
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
@@ -91,7 +94,13 @@ crlot::DevTables tables(const crlot_plan* p) {
         t.wsn = p->d_wsn;
         t.rden = p->d_rden;
     }
-    if (p->pairing) t.ptw = p->d_ptw;
+    if (p->pairing) {
+        t.ptw = p->d_ptw;
+        t.pden = p->d_pden;
+        t.px_lo = p->px_lo;
+        // no transform can overflow: |x w| <= 2^64 / max gain, so |X| < 2^75, |ifft| < 2^86
+        t.px_hi = p->px_hi / std::max(1.0f, p->has_gain ? p->gain_max : 1.0f);
+    }
     return t;
 }
 
@@ -99,7 +108,7 @@ void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
-                     p->d_rden, p->d_twany_own, p->d_ptw})  // d_twany aliases d_tw or d_twany_own
+                     p->d_rden, p->d_twany_own, p->d_ptw, p->d_pden})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
     delete p;
 }
@@ -128,6 +137,30 @@ int upload_window_tables(crlot_plan* p) {
     for (size_t i = 0; i < den.size(); ++i) {
         if (!(den[i] >= 0x1p-40f && den[i] <= 0x1p40f)) ok = false;
         rden[i] = 1.0f / den[i];
+    }
+    // K_pair: the paired regime needs sanitize(x * wa) == x * wa (up to the sign of
+    // a zero) for x == 0 or px_lo <= |x| <= px_hi: every nonzero product at least
+    // 1e-30 (px_lo rounded up) and bounded so no transform overflows.
+    double wmin = 0.0, wmax = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double w = std::fabs(double(wa[i]));
+        if (w > 0.0 && (wmin == 0.0 || w < wmin)) wmin = w;
+        wmax = std::max(wmax, w);
+    }
+    p->px_lo = wmin > 0.0 ? std::nextafter(float(double(1e-30f) / wmin * (1.0 + 0x1p-20)), INFINITY) : 0.0f;
+    p->px_hi = float(0x1p64 / std::max(1.0, wmax));
+    if (p->d_pden) {  // [block][lane][den SH | rden SH]
+        const int h = p->geo.h, sh = h / 64, blocks = int(den.size()) / h;
+        std::vector<float> pd(2 * den.size());
+        for (int b = 0; b < blocks; ++b)
+            for (int l = 0; l < 64; ++l)
+                for (int q = 0; q < sh; ++q) {
+                    const size_t at = (size_t(b) * 64 + l) * 2 * sh;
+                    pd[at + q] = den[size_t(b) * h + l + 64 * q];
+                    pd[at + sh + q] = rden[size_t(b) * h + l + 64 * q];
+                }
+        hipError_t e = hipMemcpy(p->d_pden, pd.data(), sizeof(float) * pd.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pair den)");
     }
     hipError_t e;
     if ((e = hipMemcpy(p->d_wa, wa.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
@@ -267,9 +300,10 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }
-    if (n == 1024) {  // K_pair tables
+    if (n == 1024 && h % 128 == 0 && ring % h == 0) {  // K_pair tables
         const std::vector<float> ptw = crlot::build_pair_twiddles();
-        if ((e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
+        if ((e = hipMalloc(&p->d_pden, sizeof(float) * 2 * ring)) ||
+            (e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
             (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {
             free_plan(p);
             return hip_fail(e, "pair twiddles");
@@ -317,6 +351,9 @@ int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
     hipError_t e = hipMemcpy(p->d_gain, gain, sizeof(float) * bins, hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy(gain)");
     p->has_gain = true;
+    float gm = 0.0f;
+    for (int i = 0; i < bins; ++i) gm = std::isnan(gain[i]) ? INFINITY : std::max(gm, std::fabs(gain[i]));
+    p->gain_max = gm;
     return CRLOT_OK;
 }
 

@@ -152,9 +152,8 @@ __device__ __forceinline__ void pair_t1_apply(cf (&v)[16], const cf* t1, int lan
 }
 
 // Forward: natural z[lane + 64 m] -> bin-scrambled X (pair_bin).
-//   t1: W1024^{l k1} (pair_t1_index), t2[c - 1] = W64^{(lane & 15) c}.
-__device__ __forceinline__ void pair_fft_fwd(cf (&v)[16], cf* buf, const cf* t1, const cf (&t2)[3],
-                                             int lane) {
+//   t1: W1024^{l k1} (pair_t1_index), t2[16 (c - 1)] = W64^{(lane & 15) c} (LDS).
+__device__ __forceinline__ void pair_fft_fwd(cf (&v)[16], cf* buf, const cf* t1, const cf* t2, int lane) {
     dft16<false>(v);
     pair_t1_apply<false>(v, t1, lane);
     lane_reg_swap(v);
@@ -163,20 +162,19 @@ __device__ __forceinline__ void pair_fft_fwd(cf (&v)[16], cf* buf, const cf* t1,
 #pragma unroll
     for (int c = 1; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = cmul(v[j + 4 * c], t2[c - 1]);
+        for (int j = 0; j < 4; ++j) v[j + 4 * c] = cmul(v[j + 4 * c], t2[16 * (c - 1)]);
     transpose16(v, buf, lane);
     dft16<false>(v);
 }
 
 // Inverse (unnormalised): bin-scrambled Y -> natural y[lane + 64 m].
-__device__ __forceinline__ void pair_fft_inv(cf (&v)[16], cf* buf, const cf* t1, const cf (&t2)[3],
-                                             int lane) {
+__device__ __forceinline__ void pair_fft_inv(cf (&v)[16], cf* buf, const cf* t1, const cf* t2, int lane) {
     dft16<true>(v);
     transpose16(v, buf, lane);
 #pragma unroll
     for (int c = 1; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = cmulc(v[j + 4 * c], t2[c - 1]);
+        for (int j = 0; j < 4; ++j) v[j + 4 * c] = cmulc(v[j + 4 * c], t2[16 * (c - 1)]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) dft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
     lane_reg_swap(v);

@@ -428,6 +428,15 @@ __device__ __forceinline__ float sanit_scaled(float v) {
     const float a = __builtin_fabsf(v);
     return (a >= lo && a <= 3.402823466e+38f) ? v : 0.0f;
 }
+// sanit_scaled for a v known to be finite (K_pair's paired regime): the threshold alone.
+template <int NPOW2>
+__device__ __forceinline__ float sanit_scaled_finite(float v) {
+#ifdef CRLOT_ABL_NOSANIT
+    return v;
+#endif
+    constexpr float lo = 1e-30f * float(NPOW2);
+    return __builtin_fabsf(v) >= lo ? v : 0.0f;
+}
 
 // ------------------------------------------------------------- real split
 // DC / Nyquist bins exactly as kissfft forms them: kiss_fftr sets

@@ -23,6 +23,12 @@ struct DevTables {
     // Frame-pair transform tables (N = 1024 plans with pairing on, else nullptr):
     // W1024^{l k1} (15 x 64, fft_pair.h pair_t1_index) then W64^{b c} [c-1][b] (3 x 16), float pairs.
     const float* ptw = nullptr;
+    // K_pair per-block divisors: [ring_len/H][64 lanes][den (SH) | rden (SH)], SH = H/64,
+    // den at block offset lane + 64 q (nullptr when the pair kernel is off).
+    const float* pden = nullptr;
+    // K_pair paired regime: samples x with x == 0 or px_lo <= |x| <= px_hi keep
+    // sanitize(x * wa) == x * wa and the transforms finite (kernels.hip K_pair).
+    float px_lo = 0.f, px_hi = 0.f;
 };
 
 // Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.

@@ -446,14 +446,27 @@ __global__ __launch_bounds__(kBlock, CRLOT_FUSED2_MIN_WAVES) void k_stft_ola_fus
 // ------------------------------------------------------------------ fused, frame pairs (N = 1024)
 // K_pair k_stft_ola_pair<SH,NB,W>: the fused walk with frames 2j and 2j+1 of a
 // stream packed into ONE 1024-point complex transform (fft_pair.h):
-// z = sanit(x_2j * w) + i sanit(x_2j+1 * w); the round trip's real part is frame
-// 2j's push_frame_AoS input and the imaginary part frame 2j+1's.  Pairs are
-// aligned to even frame indices whatever the chunking (a chunk's warm-up starts
-// on an even frame and a pair straddling its end still transforms the real
-// partner), so every frame's bits depend only on the stream.  Lane l holds
-// samples l + 64 m of the frame; a hop is SH = H/64 floats per lane.
-// Everything after the inverse is K_fused2's: folded 1/N, sanitize, OLA in
-// ascending k, Markstein division with a per-wave IEEE fallback.
+// z = x_2j * w + i x_2j+1 * w; the round trip's real part is frame 2j's
+// push_frame_AoS input and the imaginary part frame 2j+1's.  Pairs are aligned
+// to even frame indices whatever the chunking (a chunk's warm-up starts on an
+// even frame and a pair straddling its end still transforms the real partner),
+// so every frame's bits depend only on the stream.  Lane l holds samples
+// l + 64 m of the frame; a hop is SH = H/64 floats per lane.
+//
+// Two regimes per pair, chosen from the pair's own hops (k .. k+NB), so again
+// independent of the chunking:
+//  * paired: every sample is 0 or px_lo <= |x| <= px_hi (DevTables, set on the
+//    host from the window and the spectral gain).  Then sanitize(x*w) == x*w up
+//    to the sign of a zero, which no output bit can see (a nonzero value plus a
+//    zero of either sign is exact, and the output sanitize maps both zeros to
+//    +0); no transform can overflow; and the output sanitize reduces to its
+//    threshold test.
+//  * unpaired (a NaN, Inf, huge or tiny sample): each frame gets a transform of
+//    its own (imaginary part zero) with the full sanitize on both sides, so a
+//    frame whose spectrum overflows cannot leak into its neighbour -- the
+//    reference transforms every frame alone (kissfft_adapter.cc:83-168).
+// Everything after the inverse is K_fused2's: folded 1/N, OLA in ascending k,
+// Markstein division with a per-wave IEEE fallback.
 template <int SH>
 __device__ __forceinline__ void load_hop1(float* dst, __amdgpu_buffer_rsrc_t rx, int lane, int origin,
                                           int T, int mode) {
@@ -465,19 +478,55 @@ __device__ __forceinline__ void load_hop1(float* dst, __amdgpu_buffer_rsrc_t rx,
 #endif
     if (origin >= 0 && origin + H <= T) {
 #pragma unroll
-        for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, lane * 4 + q * 256, origin * 4);
+        for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, lane * 4, origin * 4 + q * 256);
     } else {
 #pragma unroll
         for (int q = 0; q < SH; ++q) dst[q] = fetch_x(rx, origin + lane + 64 * q, T, mode);
     }
 }
 
-// LDS: t1 [15*64 cf] | wa4 [1024 f] | ws4 [1024 f] | per-wave transpose buffers.
-// Windows are stored [m/4][lane][m%4] so one ds_read_b128 gives a lane 4 taps.
+// 1 when every sample of the hop (SH per lane, whole wave) keeps the paired regime.
+template <int SH>
+__device__ __forceinline__ uint32_t hop_ok(const float* h, float lo, float hi) {
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        const float t = __builtin_fabsf(h[q]);
+        bad |= !((t >= lo) & (t <= hi)) & (t != 0.0f);
+    }
+    return __builtin_amdgcn_ballot_w64(bad) == 0 ? 1u : 0u;
+}
+
+// den / rden of OLA block b for this lane (DevTables::pden: [block][lane][den SH | rden SH]).
+template <int SH>
+__device__ __forceinline__ void load_den(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int lane, int b) {
+#ifdef CRLOT_ABL_NODEN  // timing-only ablation: wrong results
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        dr[q] = 1.5f;
+        dr[SH + q] = 0.6666667f;
+    }
+    return;
+#endif
+#pragma unroll
+    for (int j = 0; j < 2 * SH / 4; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, lane * (8 * SH), b * (512 * SH) + 16 * j, 0);
+        const unsigned u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];  // (see bload2)
+        dr[4 * j] = __builtin_bit_cast(float, u0);
+        dr[4 * j + 1] = __builtin_bit_cast(float, u1);
+        dr[4 * j + 2] = __builtin_bit_cast(float, u2);
+        dr[4 * j + 3] = __builtin_bit_cast(float, u3);
+    }
+}
+
+// LDS: t1 [15*64 cf] | t2 [3*16 cf] | wa4 [1024 f] | ws4 [1024 f] | per-wave
+// transpose buffers.  Windows are stored [m/4][lane][m%4] so one ds_read_b128
+// gives a lane 4 taps.
 template <int W>
 struct PairLds {
     static constexpr size_t t1 = 0;
-    static constexpr size_t wa = t1 + sizeof(cf) * 15 * 64;
+    static constexpr size_t t2 = t1 + sizeof(cf) * 15 * 64;
+    static constexpr size_t wa = t2 + sizeof(cf) * 3 * 16;
     static constexpr size_t ws = wa + sizeof(float) * 1024;
     static constexpr size_t bufs = ws + sizeof(float) * 1024;
     static constexpr size_t bytes = bufs + sizeof(cf) * dev::kPairXbuf * W;
@@ -490,13 +539,15 @@ template <int SH, int NB, int W, bool HAS_GAIN>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
     constexpr int E = 16, N = 1024, H = 64 * SH;
     static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cf* t1 = reinterpret_cast<cf*>(smem + PairLds<W>::t1);
+    cf* t2s = reinterpret_cast<cf*>(smem + PairLds<W>::t2);
     float* wa4 = reinterpret_cast<float*>(smem + PairLds<W>::wa);
     float* ws4 = reinterpret_cast<float*>(smem + PairLds<W>::ws);
     {
         const cf* g1 = reinterpret_cast<const cf*>(a.t.ptw);
-        for (int i = threadIdx.x; i < 15 * 64; i += 64 * W) t1[i] = g1[i];
+        for (int i = threadIdx.x; i < 15 * 64 + 3 * 16; i += 64 * W) t1[i] = g1[i];  // t1 | t2
         for (int i = threadIdx.x; i < N; i += 64 * W) {
             const int l = i & 63, m = i >> 6;  // tap n = l + 64 m
             const int d = (m >> 2) * 256 + l * 4 + (m & 3);
@@ -508,6 +559,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     cf* buf = reinterpret_cast<cf*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
+    const cf* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
     const int gw = blockIdx.x * W + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
@@ -517,28 +569,27 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
     const __amdgpu_buffer_rsrc_t ry =
         dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
-    const __amdgpu_buffer_rsrc_t rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
-    const __amdgpu_buffer_rsrc_t rr = dev::make_rsrc(a.t.rden, uint32_t(a.ring_blocks * H) * 4u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
     const float g = a.gain;
-    cf t2[3];
-    {
-        const cf* g2 = reinterpret_cast<const cf*>(a.t.ptw) + 15 * 64;
-#pragma unroll
-        for (int c2 = 0; c2 < 3; ++c2) t2[c2] = g2[c2 * 16 + (lane & 15)];
-    }
-    const int gbase = dev::pair_bin_lane(lane);
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
-    // xin[h*SH + q]: hop (k + h), h = 0..NB, sample lane + 64 q of the hop
+    // xin[h*SH + q]: hop (k + h), h = 0..NB, sample lane + 64 q of the hop;
+    // bit h of hopok: hop k + h keeps the paired regime
     float xin[E + SH];
+    uint32_t hopok = 0;
 #pragma unroll
-    for (int h = 0; h <= NB; ++h) load_hop1<SH>(xin + h * SH, rx, lane, (fs + h) * H - a.pad, a.T, a.pad_mode);
+    for (int h = 0; h <= NB; ++h) {
+        load_hop1<SH>(xin + h * SH, rx, lane, (fs + h) * H - a.pad, a.T, a.pad_mode);
+        hopok |= hop_ok<SH>(xin + h * SH, xlo, xhi) << h;
+    }
     float acc[NB][SH];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
 #pragma unroll
         for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
 
-    auto accumulate = [&](const cf (&v)[E], bool imag) {
+    // push_frame_AoS of one frame: (sanitized) inverse output, folded 1/N, window, gain
+    auto accumulate = [&](const cf (&v)[E], bool imag, bool paired) {
 #pragma unroll
         for (int m4 = 0; m4 < E / 4; ++m4) {
             const float4 w = *reinterpret_cast<const float4*>(ws4 + m4 * 256 + lane * 4);
@@ -546,33 +597,33 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int m = 4 * m4 + u;
-                const float o = dev::sanit_scaled<N>(imag ? v[m].i : v[m].r);
+                const float x = imag ? v[m].i : v[m].r;
+                const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
                 float& r = acc[m / SH][m % SH];
                 r = __builtin_fmaf(__builtin_fmaf(o, wv[u], 0.0f), g, r);
             }
         }
     };
-    auto emit = [&](int k) {  // produce(H) of block k, then shift the accumulators
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
         if (k >= f0) {
-            float dn[SH], rn[SH];
+            float mx = 0.0f, mn = 0x1p127f;
 #pragma unroll
             for (int q = 0; q < SH; ++q) {
-                dn[q] = dev::bload1(rd, lane * 4 + q * 256, (k % a.ring_blocks) * H * 4);
-                rn[q] = dev::bload1(rr, lane * 4 + q * 256, (k % a.ring_blocks) * H * 4);
+                const float t = __builtin_fabsf(acc[0][q]);
+                mx = __builtin_fmaxf(mx, t);
+                mn = __builtin_fminf(mn, t);
             }
-            bool ok = true;
-#pragma unroll
-            for (int q = 0; q < SH; ++q) ok = ok && mk_ok(acc[0][q]);
+            const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
             const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
 #pragma unroll
             for (int q = 0; q < SH; ++q) {
 #ifdef CRLOT_ABL_NODIV  // timing-only ablation
-                const float o = acc[0][q] * rn[q];
+                const float o = acc[0][q] * dr[SH + q];
 #else
-                const float o = fast ? mk_div(acc[0][q], dn[q], rn[q]) : acc[0][q] / dn[q];
+                const float o = fast ? mk_div(acc[0][q], dr[q], dr[SH + q]) : acc[0][q] / dr[q];
 #endif
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry,
-                                                      lane * 4 + q * 256, k * H * 4, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry, lane * 4,
+                                                      k * (4 * H) + q * 256, 0);
             }
         }
 #pragma unroll
@@ -583,26 +634,10 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
     };
 
-    for (int k = fs; k < f1; k += 2) {
-        // prefetch hops k+NB+1, k+NB+2 for the next pair
-        float nxt[2 * SH];
-        load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
-        load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
-        const bool partner = k + 1 < a.F;  // frame k+1 exists (even past this chunk)
-        cf v[E];
-#pragma unroll
-        for (int m4 = 0; m4 < E / 4; ++m4) {
-            const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
-            const float wv[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int m = 4 * m4 + u;
-                v[m].r = dev::sanit(xin[m] * wv[u]);
-                v[m].i = partner ? dev::sanit(xin[m + SH] * wv[u]) : 0.0f;
-            }
-        }
+    auto transform = [&](cf (&v)[E]) {  // forward, spectral gain, inverse (unnormalised)
         dev::pair_fft_fwd(v, buf, t1, t2, lane);
         if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins
+            const int gbase = dev::pair_bin_lane(lane);
 #pragma unroll
             for (int d = 0; d < E; ++d) {
                 const int kb = gbase + 64 * d;
@@ -611,50 +646,96 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             }
         }
         dev::pair_fft_inv(v, buf, t1, t2, lane);
-#ifdef CRLOT_ABL_DUMMY  // timing-only: CRLOT_ABL_DUMMY extra independent VALU ops per pair
+#ifdef CRLOT_ABL_DUMMY  // timing-only: CRLOT_ABL_DUMMY extra independent VALU ops per transform
         {
             float d[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) d[i] = v[i].r;
 #pragma unroll
-            for (int i = 0; i < CRLOT_ABL_DUMMY; ++i)
-#if defined(CRLOT_ABL_DUMMY_PK)
-                asm volatile("v_pk_add_f32 %0, %0, %0" : "+v"(*reinterpret_cast<double*>(&d[2 * (i & 3)])));
-#elif defined(CRLOT_ABL_DUMMY_CMP)
-            {
-                unsigned long long m;
-                asm volatile("v_cmp_ge_f32_e64 %0, |%1|, %1" : "=s"(m) : "v"(d[i & 7]));
-            }
-#elif defined(CRLOT_ABL_DUMMY_CND)
-                asm volatile("v_cndmask_b32_e64 %0, 0, %0, %1" : "+v"(d[i & 7]) : "s"(__builtin_amdgcn_read_exec()));
-#elif defined(CRLOT_ABL_DUMMY_FMA3)
-                asm volatile("v_fma_f32 %0, %0, %0, %0" : "+v"(d[i & 7]));
-#elif defined(CRLOT_ABL_DUMMY_PERM)
-            if ((i & 1) == 0) {
-                const unsigned a0 = __builtin_bit_cast(unsigned, d[i & 7]), b0 = __builtin_bit_cast(unsigned, d[(i + 1) & 7]);
-                const auto r = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
-                const unsigned r0 = r[0], r1 = r[1];
-                d[i & 7] = __builtin_bit_cast(float, r0);
-                d[(i + 1) & 7] = __builtin_bit_cast(float, r1);
-            }
-#elif defined(CRLOT_ABL_DUMMY_SALU)
-            {
-                unsigned long long m = __builtin_amdgcn_read_exec();
-                asm volatile("s_and_b64 %0, %0, %0" : "+s"(m));
-            }
+            for (int i = 0; i < CRLOT_ABL_DUMMY; ++i) {
+#if defined(CRLOT_ABL_DUMMY_PERM)
+                if ((i & 1) == 0) {
+                    const unsigned a0 = __builtin_bit_cast(unsigned, d[i & 7]);
+                    const unsigned b0 = __builtin_bit_cast(unsigned, d[(i + 1) & 7]);
+                    const auto r = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+                    const unsigned r0 = r[0], r1 = r[1];
+                    d[i & 7] = __builtin_bit_cast(float, r0);
+                    d[(i + 1) & 7] = __builtin_bit_cast(float, r1);
+                }
 #else
                 asm volatile("v_add_f32 %0, %0, %0" : "+v"(d[i & 7]));
 #endif
+            }
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i].r = d[i];
         }
 #endif
-        accumulate(v, false);
-        emit(k);
-        if (k + 1 < f1) {
-            accumulate(v, true);
-            emit(k + 1);
+    };
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
+    for (int k = fs; k < f1; k += 2) {
+        // prefetch hops k+NB+1, k+NB+2 for the next pair
+        float nxt[2 * SH];
+        load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
+        load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        const bool paired = (hopok & kPairHops) == kPairHops;
+        if (paired) {
+            const bool partner = k + 1 < a.F;  // frame k+1 exists (even past this chunk)
+            cf v[E];
+#pragma unroll
+            for (int m4 = 0; m4 < E / 4; ++m4) {
+                const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
+                const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int m = 4 * m4 + u;
+                    v[m].r = xin[m] * wv[u];
+                    v[m].i = partner ? xin[m + SH] * wv[u] : 0.0f;
+                }
+            }
+            transform(v);
+            float dr[2 * SH];
+#ifdef CRLOT_PAIR_DEN_LATE
+            accumulate(v, false, true);
+            load_den<SH>(dr, rp, lane, k % a.ring_blocks);
+            emit(k, dr);
+            if (k + 1 < f1) {
+                accumulate(v, true, true);
+                load_den<SH>(dr, rp, lane, (k + 1) % a.ring_blocks);
+                emit(k + 1, dr);
+            }
+#else
+            load_den<SH>(dr, rp, lane, k % a.ring_blocks);
+            accumulate(v, false, true);
+            emit(k, dr);
+            if (k + 1 < f1) {
+                load_den<SH>(dr, rp, lane, (k + 1) % a.ring_blocks);
+                accumulate(v, true, true);
+                emit(k + 1, dr);
+            }
+#endif
+        } else {  // unpaired: frames k and k+1 alone, full sanitize (never taken on finite audio)
+            const int npass = min(2, f1 - k);
+            for (int p = 0; p < npass; ++p) {
+                cf v[E];
+#pragma unroll
+                for (int m4 = 0; m4 < E / 4; ++m4) {
+                    const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
+                    const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int m = 4 * m4 + u;
+                        v[m].r = dev::sanit((p ? xin[m + SH] : xin[m]) * wv[u]);
+                        v[m].i = 0.0f;
+                    }
+                }
+                transform(v);
+                float dr[2 * SH];
+                load_den<SH>(dr, rp, lane, (k + p) % a.ring_blocks);
+                accumulate(v, false, false);
+                emit(k + p, dr);
+            }
         }
+        hopok = (hopok | hop_ok<SH>(nxt, xlo, xhi) << (NB + 1) | hop_ok<SH>(nxt + SH, xlo, xhi) << (NB + 2)) >> 2;
 #pragma unroll
         for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
 #pragma unroll
@@ -1553,6 +1634,25 @@ void choose_chunks(int64_t F, int n_streams, int nb, int resident, int& n_chunks
     n_chunks = int((F + m - 1) / m);
 }
 
+// K_pair: whole resident rounds.  Its 16-wave workgroups only free a CU when
+// all 16 finish, so a grid that ends in a partial round idles the device for a
+// whole chunk's time (measured at the headline: 15 chunks = 3.75 rounds
+// 219k Msamples/s, 8 chunks = 2 rounds 232k).  At least two rounds, chunks of
+// 48..256 frames, and among those the fewest rounds x (frames + halo) per wave.
+void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m) {
+    const int64_t S = std::max(1, n_streams), R = std::max(1, resident);
+    const int64_t hi = std::max<int64_t>(1, F / 48);
+    const int64_t lo = std::min(hi, std::max((2 * R + S - 1) / S, (F + 255) / 256));
+    int64_t best_n = lo, best_cost = INT64_MAX;
+    for (int64_t n = lo; n <= std::min(hi, 2 * lo); ++n) {
+        const int64_t mm = (F + n - 1) / n, nc = (F + mm - 1) / mm;
+        const int64_t cost = ((S * nc + R - 1) / R) * (mm + halo);
+        if (cost < best_cost) best_cost = cost, best_n = n;
+    }
+    m = int((F + best_n - 1) / best_n);
+    n_chunks = int((F + m - 1) / m);
+}
+
 // frames per workgroup walk (halo NB-1 frames recomputed); CRLOT_WG_CHUNK overrides
 int wg_chunk_target() {
     static const int v = [] {
@@ -1629,7 +1729,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
 #ifdef CRLOT_NO_PAIR  // A/B builds: per-frame kernels only
     const bool use_pair = false;
 #else
-    const bool use_pair = g.n == 1024 && t.ptw && fast;
+    const bool use_pair = g.n == 1024 && t.ptw && t.pden && fast;
 #endif
 #ifdef CRLOT_OLD_CHUNKS  // A/B builds: fixed ~128-frame chunks
     const int target = 128;
@@ -1641,7 +1741,10 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     const bool pair = !use_pair && fused2_used(e, g.h / 128, fast);
     const int resident = use_pair ? fused_resident_waves() * pair_waves_per_cu() / 16
                          : pair && e == 8 ? fused_resident_waves() * 3 / 4 : fused_resident_waves();
-    choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
+    if (use_pair)
+        choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.n_chunks, a.M);
+    else
+        choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
     if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
         const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
         a.M = int((F + n - 1) / n);

@@ -23,7 +23,7 @@ if stats:
     shutil.copy(stats[0], f"profiles/{tag}_kernel_stats.csv")
 
 
-def counters(sub, pat="stft_ola_fused"):
+def counters(sub, pat="stft_ola"):
     agg = collections.defaultdict(list)
     for f in glob.glob(f"{src}/{sub}/run_counter_collection.csv"):
         per = collections.defaultdict(dict)
@@ -51,15 +51,15 @@ dur = None
 tr = glob.glob(f"{src}/trace/run_kernel_stats.csv")
 if tr:
     for r in csv.DictReader(open(tr[0])):
-        if "stft_ola_fused" in r["Name"]:
+        if "stft_ola" in r["Name"]:
             dur = float(r["AverageNs"])
 # per-dispatch durations of the fused kernel (the stats average includes warm-up launches)
-kname, med, mn = "k_stft_ola_fused", None, None
+kname, med, mn = "k_stft_ola", None, None
 kt = glob.glob(f"{src}/trace/run_kernel_trace.csv")
 if kt:
     ds = []
     for r in csv.DictReader(open(kt[0])):
-        if "stft_ola_fused" in r["Kernel_Name"]:
+        if "stft_ola" in r["Kernel_Name"]:
             kname = r["Kernel_Name"]
             ds.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     if ds:
