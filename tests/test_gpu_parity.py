@@ -169,6 +169,38 @@ def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkey
     monkeypatch.delenv("CRLOT_CHUNKS")
 
 
+@pytest.mark.parametrize("burst_hop", [82, 83])
+def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, burst_hop, monkeypatch):
+    """K_pair's unpaired regime: a hop of huge samples (1e25, beyond px_hi) makes
+    the pairs that contain it transform each frame alone, as the reference does,
+    so a neighbour sharing a pair with a burst frame keeps its own accuracy.  The
+    blocks no burst frame reaches match the oracle at the normal tolerance (a
+    shared transform would add ~1e25 * 2^-24 of rounding to them); the burst
+    region matches relative to its own scale; the bits do not depend on the
+    chunking."""
+    torch = torch_cuda
+    n, h, T = 1024, 256, 40_000
+    x = oracle.synth(T, 31).copy()
+    x[burst_hop * h:(burst_hop + 1) * h] *= np.float32(2e25)
+    x[5000:5100] = 0.0  # exact zeros keep the paired regime
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    xd = dev(torch, x[None])
+    y = host(plan.roundtrip(xd))[0]
+    ref = oracle.roundtrip(x, n, h)
+    assert y.shape == ref.shape and np.all(np.isfinite(y))
+    lo_blk, hi_blk = burst_hop - 3, burst_hop + 3  # frames burst_hop-3..burst_hop reach these blocks
+    clean = np.ones(y.size, bool)
+    clean[lo_blk * h:(hi_blk + 1) * h] = False
+    d = np.abs(y[clean].astype(np.float64) - ref[clean])
+    assert d.max() <= MAX_ABS * 0.5, d.max()
+    burst = ~clean
+    assert rel_l2(y[burst], ref[burst]) <= REL_L2
+    for chunks in ("1", "3", "16"):
+        monkeypatch.setenv("CRLOT_CHUNKS", chunks)
+        assert np.array_equal(bits(host(plan.roundtrip(xd))[0]), bits(y)), chunks
+    monkeypatch.delenv("CRLOT_CHUNKS")
+
+
 @pytest.mark.parametrize("scale", [1e-25, 1e25, 1.0])
 def test_fused_fast_division_and_fold_exact(pkg, oracle, torch_cuda, scale):
     """The fused kernel's exact rewrites (1/N folded into the window, Markstein
