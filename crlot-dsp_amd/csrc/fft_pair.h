@@ -35,38 +35,120 @@ __host__ __device__ constexpr int pair_bin_lane(int lane) {
 }
 __host__ __device__ constexpr int pair_bin(int lane, int d) { return pair_bin_lane(lane) + 64 * d; }
 
-// a * W for the fixed rotations of a 16-point DFT; INV conjugates W.
-// W16^j = (cos(pi j / 8), -sin(pi j / 8)) forward.
+// Packed complex: (re, im) in one 64-bit register pair, so every complex add is
+// ONE v_pk_add_f32 and every rotation two packed ops (v_pk_mul_f32 +
+// v_pk_fma_f32; swaps and sign flips ride on op_sel / neg modifiers).  On
+// gfx950 a packed op moves twice the data per issue of a scalar one at about
+// 1.2x its issue cost (tools/ubench/valu_issue.hip), and at 4 waves per SIMD
+// this kernel is issue-bound, not VALU-throughput-bound.
+typedef float pc __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ pc pc_mk(float r, float i) { return (pc){r, i}; }
+
+// Single packed instructions with the operand swaps / sign flips as VOP3P
+// modifiers (op_sel: half for the low lane, op_sel_hi: half for the high lane,
+// neg_lo / neg_hi: negate that lane's operand).  Written out because the
+// compiler materialises some of these shuffles with v_xor / v_mov.
+// (a.x + b.y, a.y - b.x)
+__device__ __forceinline__ pc pk_add_sw_nh(pc a, pc b) {
+    pc r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ pc pk_add_sw_nl(pc a, pc b) {
+    pc r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// (a.y - a.x, -a.x - a.y)
+__device__ __forceinline__ pc pk_w6f(pc a) {
+    pc r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(r) : "v"(a));
+    return r;
+}
+// (-a.y - a.x, a.x - a.y)
+__device__ __forceinline__ pc pk_w6i(pc a) {
+    pc r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(a));
+    return r;
+}
+// a * w = (a.x w.x - a.y w.y, a.x w.y + a.y w.x): one rounded product, one fma
+__device__ __forceinline__ pc pc_mul(pc a, pc w) {
+    pc p, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(p) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a), "v"(w), "v"(p));
+    return r;
+}
+// a * conj(w) = (a.x w.x + a.y w.y, a.y w.x - a.x w.y)
+__device__ __forceinline__ pc pc_mulc(pc a, pc w) {
+    pc p, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(p) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(w), "v"(p));
+    return r;
+}
 template <bool INV>
-__device__ __forceinline__ cf crot(cf a, float c, float s) {  // a * (c - i s) [fwd] / (c + i s) [inv]
-    return INV ? cf{__builtin_fmaf(a.r, c, -(a.i * s)), __builtin_fmaf(a.i, c, a.r * s)}
-               : cf{__builtin_fmaf(a.r, c, a.i * s), __builtin_fmaf(a.i, c, -(a.r * s))};
+__device__ __forceinline__ pc pc_tw(pc a, pc w) { return INV ? pc_mulc(a, w) : pc_mul(a, w); }
+// a + m(b) and a - m(b), m = multiply by -i (forward) / +i (inverse)
+template <bool INV>
+__device__ __forceinline__ pc pc_add_mi(pc a, pc b) { return INV ? pk_add_sw_nl(a, b) : pk_add_sw_nh(a, b); }
+template <bool INV>
+__device__ __forceinline__ pc pc_sub_mi(pc a, pc b) { return INV ? pk_add_sw_nh(a, b) : pk_add_sw_nl(a, b); }
+
+// DFT4; with MI2 the third input arrives as m^-1(x2) and is rotated on the fly
+template <bool INV, bool MI2 = false>
+__device__ __forceinline__ void pdft4(pc& x0, pc& x1, pc& x2, pc& x3) {
+    const pc s0 = MI2 ? pc_add_mi<INV>(x0, x2) : x0 + x2;
+    const pc s1 = MI2 ? pc_sub_mi<INV>(x0, x2) : x0 - x2;
+    const pc s2 = x1 + x3, d3 = x1 - x3;
+    x0 = s0 + s2;
+    x2 = s0 - s2;
+    x1 = pc_add_mi<INV>(s1, d3);
+    x3 = pc_sub_mi<INV>(s1, d3);
+}
+
+// a * W16^j (forward) / conj (inverse) for the fixed rotations of a 16-point DFT.
+// W8-type rotations (j = 2, 6) as h * (a + ...) : one add + one multiply.
+template <bool INV, int J>
+__device__ __forceinline__ pc rot16(pc a) {
+    constexpr float c1 = 0.92387953251128675613f;  // cos(pi/8)
+    constexpr float s1 = 0.38268343236508977173f;  // sin(pi/8)
+    constexpr float h = 0.70710678118654752440f;   // sqrt(1/2)
+    if constexpr (J == 1) return pc_tw<INV>(a, (pc){c1, -s1});
+    if constexpr (J == 3) return pc_tw<INV>(a, (pc){s1, -c1});
+    if constexpr (J == 9) return pc_tw<INV>(a, (pc){-c1, s1});
+    // W^2 = h (1 - i): fwd h (a.x + a.y, a.y - a.x), inv h (a.x - a.y, a.y + a.x)
+    if constexpr (J == 2) return (pc){h, h} * (INV ? pk_add_sw_nl(a, a) : pk_add_sw_nh(a, a));
+    // W^6 = h (-1 - i): fwd h (a.y - a.x, -a.x - a.y), inv h (-a.x - a.y, a.x - a.y)
+    if constexpr (J == 6) return (pc){h, h} * (INV ? pk_w6i(a) : pk_w6f(a));
+    static_assert(J == 1 || J == 2 || J == 3 || J == 6 || J == 9, "rotation");
+    return a;
 }
 
 // In-place 16-point DFT, natural order in and out: X[k] = sum_n x[n] W16^{+-nk}.
 // n = 4 n1 + n2, k = k1 + 4 k2: four DFT4 over n1, twiddles W16^{n2 k1}, four
 // DFT4 over n2 (outputs renamed in registers, no data movement).
 template <bool INV>
-__device__ __forceinline__ void dft16(cf (&x)[16]) {
-    constexpr float c1 = 0.92387953251128675613f;  // cos(pi/8)
-    constexpr float s1 = 0.38268343236508977173f;  // sin(pi/8)
-    constexpr float h = 0.70710678118654752440f;   // sqrt(1/2)
+__device__ __forceinline__ void pdft16(pc (&x)[16]) {
 #pragma unroll
-    for (int n2 = 0; n2 < 4; ++n2) dft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
+    for (int n2 = 0; n2 < 4; ++n2) pdft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
     // a[n2][k1] now at x[n2 + 4 k1]; multiply by W16^{n2 k1}
-    x[1 + 4 * 1] = crot<INV>(x[1 + 4 * 1], c1, s1);   // W^1
-    x[1 + 4 * 2] = crot<INV>(x[1 + 4 * 2], h, h);     // W^2
-    x[1 + 4 * 3] = crot<INV>(x[1 + 4 * 3], s1, c1);   // W^3
-    x[2 + 4 * 1] = crot<INV>(x[2 + 4 * 1], h, h);     // W^2
-    x[2 + 4 * 2] = mul_mi<INV>(x[2 + 4 * 2]);         // W^4 = -i
-    x[2 + 4 * 3] = crot<INV>(x[2 + 4 * 3], -h, h);    // W^6
-    x[3 + 4 * 1] = crot<INV>(x[3 + 4 * 1], s1, c1);   // W^3
-    x[3 + 4 * 2] = crot<INV>(x[3 + 4 * 2], -h, h);    // W^6
-    x[3 + 4 * 3] = crot<INV>(x[3 + 4 * 3], -c1, -s1); // W^9
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) dft4<INV>(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
+    x[1 + 4 * 1] = rot16<INV, 1>(x[1 + 4 * 1]);
+    x[1 + 4 * 2] = rot16<INV, 2>(x[1 + 4 * 2]);
+    x[1 + 4 * 3] = rot16<INV, 3>(x[1 + 4 * 3]);
+    x[2 + 4 * 1] = rot16<INV, 2>(x[2 + 4 * 1]);
+    // (W^4 = -i on x[2 + 4 * 2] is applied inside the k1 = 2 DFT4 below)
+    x[2 + 4 * 3] = rot16<INV, 6>(x[2 + 4 * 3]);
+    x[3 + 4 * 1] = rot16<INV, 3>(x[3 + 4 * 1]);
+    x[3 + 4 * 2] = rot16<INV, 6>(x[3 + 4 * 2]);
+    x[3 + 4 * 3] = rot16<INV, 9>(x[3 + 4 * 3]);
+    pdft4<INV>(x[0], x[1], x[2], x[3]);
+    pdft4<INV>(x[4], x[5], x[6], x[7]);
+    pdft4<INV, true>(x[8], x[9], x[10], x[11]);
+    pdft4<INV>(x[12], x[13], x[14], x[15]);
     // X[k1 + 4 k2] sits at x[4 k1 + k2]: transpose the 4x4 register grid
-    cf y[16];
+    pc y[16];
 #pragma unroll
     for (int k1 = 0; k1 < 4; ++k1)
 #pragma unroll
@@ -87,37 +169,43 @@ __device__ __forceinline__ void swap_f(float& a, float& b, bool b32) {
     a = __builtin_bit_cast(float, r0);
     b = __builtin_bit_cast(float, r1);
 }
-__device__ __forceinline__ void lane_reg_swap(cf (&v)[16]) {
+__device__ __forceinline__ void lane_reg_swap(pc (&v)[16]) {
 #ifdef CRLOT_ABL_NOPERM  // timing-only ablation: wrong results
     return;
 #endif
 #pragma unroll
     for (int r = 0; r < 16; ++r)
         if (!(r & 4)) {
-            swap_f(v[r].r, v[r | 4].r, false);
-            swap_f(v[r].i, v[r | 4].i, false);
+            float ar = v[r].x, ai = v[r].y, br = v[r | 4].x, bi = v[r | 4].y;
+            swap_f(ar, br, false);
+            swap_f(ai, bi, false);
+            v[r] = pc_mk(ar, ai);
+            v[r | 4] = pc_mk(br, bi);
         }
 #pragma unroll
     for (int r = 0; r < 16; ++r)
         if (!(r & 8)) {
-            swap_f(v[r].r, v[r | 8].r, true);
-            swap_f(v[r].i, v[r | 8].i, true);
+            float ar = v[r].x, ai = v[r].y, br = v[r | 8].x, bi = v[r | 8].y;
+            swap_f(ar, br, true);
+            swap_f(ai, bi, true);
+            v[r] = pc_mk(ar, ai);
+            v[r | 8] = pc_mk(br, bi);
         }
 }
 
 // 16x16 transpose inside each quarter wave through LDS: lane (x + 16 q),
 // register y  ->  lane (y + 16 q), register x.  Layout: q * 288 + 18 * row + col
-// (cf units): ds_write_b64 groups of 16 lanes hit 16 consecutive elements, and
-// each lane reads its 16 elements as 8 ds_read_b128 of 16-byte aligned pairs
+// (complex units): ds_write_b64 groups of 16 lanes hit 16 consecutive elements,
+// and each lane reads its 16 elements as 8 ds_read_b128 of 16-byte aligned pairs
 // whose starting banks 4 (9 x mod 16) are distinct in every b128 lane group --
 // conflict free; every address is one per-lane base plus an immediate.
-constexpr int kPairXbuf = 4 * 288;  // cf per wave
-__device__ __forceinline__ void transpose16(cf (&v)[16], cf* buf, int lane) {
+constexpr int kPairXbuf = 4 * 288;  // complex elements per wave
+__device__ __forceinline__ void transpose16(pc (&v)[16], pc* buf, int lane) {
 #ifdef CRLOT_ABL_NOXPOSE  // timing-only ablation: wrong results
     return;
 #endif
     const int q = lane >> 4, x = lane & 15;
-    cf* wb = buf + q * 288 + x;
+    pc* wb = buf + q * 288 + x;
     const float4* rb = reinterpret_cast<const float4*>(buf + q * 288 + 18 * x);
 #pragma unroll
     for (int y = 0; y < 16; ++y) wb[18 * y] = v[y];
@@ -125,61 +213,59 @@ __device__ __forceinline__ void transpose16(cf (&v)[16], cf* buf, int lane) {
 #pragma unroll
     for (int y = 0; y < 8; ++y) {
         const float4 t = rb[y];
-        v[2 * y] = cf{t.x, t.y};
-        v[2 * y + 1] = cf{t.z, t.w};
+        v[2 * y] = pc_mk(t.x, t.y);
+        v[2 * y + 1] = pc_mk(t.z, t.w);
     }
     wave_lds_fence();
 }
 
 // Twiddle table of the first pass, laid out for ds_read_b128: W1024^{l k1} for
 // k1 = 2j+1+e at t1[j * 128 + 2 l + e] (j < 7), k1 = 15 at t1[896 + l].
-constexpr int kPairT1 = 15 * 64;  // cf
+constexpr int kPairT1 = 15 * 64;  // complex elements
 __host__ __device__ constexpr int pair_t1_index(int k1, int l) {
     return k1 == 15 ? 896 + l : ((k1 - 1) >> 1) * 128 + 2 * l + ((k1 - 1) & 1);
 }
 template <bool INV>
-__device__ __forceinline__ void pair_t1_apply(cf (&v)[16], const cf* t1, int lane) {
+__device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const pc* t1, int lane) {
     const float4* t4 = reinterpret_cast<const float4*>(t1 + 2 * lane);
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
         const float4 t = t4[j * 64];
-        const cf w0{t.x, t.y}, w1{t.z, t.w};
-        v[2 * j + 1] = INV ? cmulc(v[2 * j + 1], w0) : cmul(v[2 * j + 1], w0);
-        v[2 * j + 2] = INV ? cmulc(v[2 * j + 2], w1) : cmul(v[2 * j + 2], w1);
+        v[2 * j + 1] = pc_tw<INV>(v[2 * j + 1], pc_mk(t.x, t.y));
+        v[2 * j + 2] = pc_tw<INV>(v[2 * j + 2], pc_mk(t.z, t.w));
     }
-    const cf w = t1[896 + lane];
-    v[15] = INV ? cmulc(v[15], w) : cmul(v[15], w);
+    v[15] = pc_tw<INV>(v[15], t1[896 + lane]);
 }
 
 // Forward: natural z[lane + 64 m] -> bin-scrambled X (pair_bin).
 //   t1: W1024^{l k1} (pair_t1_index), t2[16 (c - 1)] = W64^{(lane & 15) c} (LDS).
-__device__ __forceinline__ void pair_fft_fwd(cf (&v)[16], cf* buf, const cf* t1, const cf* t2, int lane) {
-    dft16<false>(v);
+__device__ __forceinline__ void pair_fft_fwd(pc (&v)[16], pc* buf, const pc* t1, const pc* t2, int lane) {
+    pdft16<false>(v);
     pair_t1_apply<false>(v, t1, lane);
     lane_reg_swap(v);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dft4<false>(v[j], v[j + 4], v[j + 8], v[j + 12]);
+    for (int j = 0; j < 4; ++j) pdft4<false>(v[j], v[j + 4], v[j + 8], v[j + 12]);
 #pragma unroll
     for (int c = 1; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = cmul(v[j + 4 * c], t2[16 * (c - 1)]);
+        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mul(v[j + 4 * c], t2[16 * (c - 1)]);
     transpose16(v, buf, lane);
-    dft16<false>(v);
+    pdft16<false>(v);
 }
 
 // Inverse (unnormalised): bin-scrambled Y -> natural y[lane + 64 m].
-__device__ __forceinline__ void pair_fft_inv(cf (&v)[16], cf* buf, const cf* t1, const cf* t2, int lane) {
-    dft16<true>(v);
+__device__ __forceinline__ void pair_fft_inv(pc (&v)[16], pc* buf, const pc* t1, const pc* t2, int lane) {
+    pdft16<true>(v);
     transpose16(v, buf, lane);
 #pragma unroll
     for (int c = 1; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = cmulc(v[j + 4 * c], t2[16 * (c - 1)]);
+        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mulc(v[j + 4 * c], t2[16 * (c - 1)]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
+    for (int j = 0; j < 4; ++j) pdft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
     lane_reg_swap(v);
     pair_t1_apply<true>(v, t1, lane);
-    dft16<true>(v);
+    pdft16<true>(v);
 }
 
 }  // namespace dev

@@ -532,6 +532,22 @@ struct PairLds {
     static constexpr size_t bytes = bufs + sizeof(cf) * dev::kPairXbuf * W;
 };
 
+#ifdef CRLOT_PAIR_TRACE
+__device__ uint32_t g_pair_trace[4 << 16];
+#endif
+#ifdef CRLOT_PAIR_PHASES  // debug builds: per-wave cycles by loop phase (s_memtime)
+__device__ uint32_t g_pair_phase[8 << 16];
+#define PHASE(i)                                              \
+    do {                                                      \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+        ph[i] += uint32_t(t_ - ph_last);                      \
+        ph_last = t_;                                         \
+    } while (0)
+#else
+#define PHASE(i) \
+    do {         \
+    } while (0)
+#endif
 #ifndef CRLOT_PAIR_MIN_WAVES
 #define CRLOT_PAIR_MIN_WAVES 4
 #endif
@@ -541,12 +557,12 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     static_assert(NB * SH == E, "N = NB * H");
     static_assert(SH >= 2, "den rows are read 16 bytes at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    cf* t1 = reinterpret_cast<cf*>(smem + PairLds<W>::t1);
-    cf* t2s = reinterpret_cast<cf*>(smem + PairLds<W>::t2);
+    dev::pc* t1 = reinterpret_cast<dev::pc*>(smem + PairLds<W>::t1);
+    dev::pc* t2s = reinterpret_cast<dev::pc*>(smem + PairLds<W>::t2);
     float* wa4 = reinterpret_cast<float*>(smem + PairLds<W>::wa);
     float* ws4 = reinterpret_cast<float*>(smem + PairLds<W>::ws);
     {
-        const cf* g1 = reinterpret_cast<const cf*>(a.t.ptw);
+        const dev::pc* g1 = reinterpret_cast<const dev::pc*>(a.t.ptw);
         for (int i = threadIdx.x; i < 15 * 64 + 3 * 16; i += 64 * W) t1[i] = g1[i];  // t1 | t2
         for (int i = threadIdx.x; i < N; i += 64 * W) {
             const int l = i & 63, m = i >> 6;  // tap n = l + 64 m
@@ -558,10 +574,13 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     }
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    cf* buf = reinterpret_cast<cf*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
-    const cf* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
+    const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
     const int gw = blockIdx.x * W + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
+#ifdef CRLOT_PAIR_TRACE  // debug builds: per-wave start/end (100 MHz clock) and hardware ids
+    const uint32_t trace_t0 = uint32_t(__builtin_amdgcn_s_memrealtime());
+#endif
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -570,6 +589,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const __amdgpu_buffer_rsrc_t ry =
         dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
@@ -589,7 +609,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
 
     // push_frame_AoS of one frame: (sanitized) inverse output, folded 1/N, window, gain
-    auto accumulate = [&](const cf (&v)[E], bool imag, bool paired) {
+    auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
 #pragma unroll
         for (int m4 = 0; m4 < E / 4; ++m4) {
             const float4 w = *reinterpret_cast<const float4*>(ws4 + m4 * 256 + lane * 4);
@@ -597,35 +617,44 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int m = 4 * m4 + u;
-                const float x = imag ? v[m].i : v[m].r;
+                const float x = imag ? v[m].y : v[m].x;
                 const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
                 float& r = acc[m / SH][m % SH];
                 r = __builtin_fmaf(__builtin_fmaf(o, wv[u], 0.0f), g, r);
             }
         }
     };
-    auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
-        if (k >= f0) {
-            float mx = 0.0f, mn = 0x1p127f;
+    // produce(H) of block k, then shift.  The divisions run for warm-up blocks
+    // too (only the stores are skipped), so the divisor loads are used
+    // unconditionally and stay where they are issued, ahead of the stores.
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {
+        float mx = 0.0f, mn = 0x1p127f;
 #pragma unroll
-            for (int q = 0; q < SH; ++q) {
-                const float t = __builtin_fabsf(acc[0][q]);
-                mx = __builtin_fmaxf(mx, t);
-                mn = __builtin_fminf(mn, t);
-            }
-            const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
-            const bool fast = __builtin_amdgcn_ballot_w64(!ok) == 0;
-#pragma unroll
-            for (int q = 0; q < SH; ++q) {
-#ifdef CRLOT_ABL_NODIV  // timing-only ablation
-                const float o = acc[0][q] * dr[SH + q];
-#else
-                const float o = fast ? mk_div(acc[0][q], dr[q], dr[SH + q]) : acc[0][q] / dr[q];
-#endif
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), ry, lane * 4,
-                                                      k * (4 * H) + q * 256, 0);
-            }
+        for (int q = 0; q < SH; ++q) {
+            const float t = __builtin_fabsf(acc[0][q]);
+            mx = __builtin_fmaxf(mx, t);
+            mn = __builtin_fminf(mn, t);
         }
+        const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(acc[0][q], dr[q], dr[SH + q]);
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {  // outside Markstein's exact range: IEEE
+#pragma unroll
+            for (int q = 0; q < SH; ++q) o[q] = acc[0][q] / dr[q];
+        }
+#ifdef CRLOT_ABL_NODIV  // timing-only ablation
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = acc[0][q] * dr[SH + q];
+#endif
+        // warm-up blocks (k < f0) store through a zero-size descriptor: every
+        // lane is out of range and the store is dropped.  No branch around the
+        // stores, so vmcnt bookkeeping stays exact at the next divisor wait.
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
+                                                  k * (4 * H) + q * 256, 0);
 #pragma unroll
         for (int j = 0; j < NB - 1; ++j)
 #pragma unroll
@@ -634,15 +663,23 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
     };
 
-    auto transform = [&](cf (&v)[E]) {  // forward, spectral gain, inverse (unnormalised)
+#ifdef CRLOT_PAIR_PHASES
+    uint32_t ph[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t ph_last = __builtin_amdgcn_s_memtime();
+#endif
+    auto transform = [&](dev::pc (&v)[E]) {  // forward, spectral gain, inverse (unnormalised)
+#ifdef CRLOT_ABL_NOFFT  // timing-only ablation: the memory stream alone
+        return;
+#endif
         dev::pair_fft_fwd(v, buf, t1, t2, lane);
+        PHASE(2);
         if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins
             const int gbase = dev::pair_bin_lane(lane);
 #pragma unroll
             for (int d = 0; d < E; ++d) {
                 const int kb = gbase + 64 * d;
                 const float gk = a.t.gain[kb <= N / 2 ? kb : N - kb];
-                v[d] = cf{v[d].r * gk, v[d].i * gk};
+                v[d] = v[d] * gk;
             }
         }
         dev::pair_fft_inv(v, buf, t1, t2, lane);
@@ -650,7 +687,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         {
             float d[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = v[i].r;
+            for (int i = 0; i < 8; ++i) d[i] = v[i].x;
 #pragma unroll
             for (int i = 0; i < CRLOT_ABL_DUMMY; ++i) {
 #if defined(CRLOT_ABL_DUMMY_PERM)
@@ -667,7 +704,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #endif
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) v[i].r = d[i];
+            for (int i = 0; i < 8; ++i) v[i].x = d[i];
         }
 #endif
     };
@@ -678,9 +715,10 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
         load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
         const bool paired = (hopok & kPairHops) == kPairHops;
+        PHASE(0);
         if (paired) {
             const bool partner = k + 1 < a.F;  // frame k+1 exists (even past this chunk)
-            cf v[E];
+            dev::pc v[E];
 #pragma unroll
             for (int m4 = 0; m4 < E / 4; ++m4) {
                 const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
@@ -688,35 +726,28 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int m = 4 * m4 + u;
-                    v[m].r = xin[m] * wv[u];
-                    v[m].i = partner ? xin[m + SH] * wv[u] : 0.0f;
+                    v[m] = dev::pc_mk(xin[m] * wv[u], partner ? xin[m + SH] * wv[u] : 0.0f);
                 }
             }
+            PHASE(1);
             transform(v);
-            float dr[2 * SH];
-#ifdef CRLOT_PAIR_DEN_LATE
+            PHASE(3);
+            // both blocks' divisors before this pair's stores: vmcnt retires in
+            // order, so a load issued after a store also waits for that store
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
+            load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
             accumulate(v, false, true);
-            load_den<SH>(dr, rp, lane, k % a.ring_blocks);
-            emit(k, dr);
+            emit(k, dr0);
             if (k + 1 < f1) {
                 accumulate(v, true, true);
-                load_den<SH>(dr, rp, lane, (k + 1) % a.ring_blocks);
-                emit(k + 1, dr);
+                emit(k + 1, dr1);
             }
-#else
-            load_den<SH>(dr, rp, lane, k % a.ring_blocks);
-            accumulate(v, false, true);
-            emit(k, dr);
-            if (k + 1 < f1) {
-                load_den<SH>(dr, rp, lane, (k + 1) % a.ring_blocks);
-                accumulate(v, true, true);
-                emit(k + 1, dr);
-            }
-#endif
+            PHASE(4);
         } else {  // unpaired: frames k and k+1 alone, full sanitize (never taken on finite audio)
             const int npass = min(2, f1 - k);
             for (int p = 0; p < npass; ++p) {
-                cf v[E];
+                dev::pc v[E];
 #pragma unroll
                 for (int m4 = 0; m4 < E / 4; ++m4) {
                     const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
@@ -724,8 +755,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int m = 4 * m4 + u;
-                        v[m].r = dev::sanit((p ? xin[m + SH] : xin[m]) * wv[u]);
-                        v[m].i = 0.0f;
+                        v[m] = dev::pc_mk(dev::sanit((p ? xin[m + SH] : xin[m]) * wv[u]), 0.0f);
                     }
                 }
                 transform(v);
@@ -741,6 +771,24 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
         for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
     }
+#ifdef CRLOT_PAIR_PHASES
+    PHASE(5);
+    if (lane == 0 && gw < (1 << 16)) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) g_pair_phase[8 * gw + i] = ph[i];
+        g_pair_phase[8 * gw + 6] = uint32_t((f1 - fs + 1) / 2);
+        g_pair_phase[8 * gw + 7] = 1;
+    }
+#endif
+#ifdef CRLOT_PAIR_TRACE
+    if (lane == 0 && gw < (1 << 16)) {
+        const uint32_t t1e = uint32_t(__builtin_amdgcn_s_memrealtime());
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20); // HW_REG_XCC_ID
+        uint4* tr = reinterpret_cast<uint4*>(g_pair_trace);
+        tr[gw] = make_uint4(trace_t0, t1e, hw, xcc);
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ fused, workgroup walker
@@ -2284,3 +2332,17 @@ hipError_t launch_irfft(const Geometry& g, const DevTables& t, const float* in, 
 }
 
 }  // namespace crlot
+
+#ifdef CRLOT_PAIR_TRACE
+extern "C" int crlot_debug_pair_trace(void* host, int64_t bytes) {
+    return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(crlot::g_pair_trace),
+                                   size_t(std::min<int64_t>(bytes, sizeof(crlot::g_pair_trace)))));
+}
+#endif
+
+#ifdef CRLOT_PAIR_PHASES
+extern "C" int crlot_debug_pair_phases(void* host, int64_t bytes) {
+    return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(crlot::g_pair_phase),
+                                   size_t(std::min<int64_t>(bytes, sizeof(crlot::g_pair_phase)))));
+}
+#endif

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Extra PMC passes on the headline kernel (one rocprofv3 run per pass).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc2
+mkdir -p $OUT
+i=0
+for set in "SQ_INSTS SQ_INSTS_SALU SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL" \
+           "SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_IFETCH SQ_ACTIVE_INST_SCA SQ_WAVE_CYCLES" \
+           "SQ_ACTIVE_INST_VALU2 SQ_INST_LEVEL_LDS SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_CYCLES"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --pmc $set --kernel-trace --stats -d $OUT/p$i -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3 > $OUT/p$i.log 2>&1 || { echo "pass $i rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
+done
+python3 - <<'PY'
+import csv, glob, collections
+agg = collections.defaultdict(list)
+for f in glob.glob("gpurun_out/pmc2/p*/run_counter_collection.csv"):
+    for r in csv.DictReader(open(f)):
+        if "stft_ola" in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, v in sorted(agg.items()):
+    print(f"{k:32s} {sum(v)/len(v):.4g}")
+PY
