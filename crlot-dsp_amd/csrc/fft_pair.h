@@ -193,6 +193,32 @@ __device__ __forceinline__ void lane_reg_swap(pc (&v)[16]) {
         }
 }
 
+// The same swap through LDS (one write and one read of every register, 16-lane
+// write groups and 32-lane read groups each on distinct banks):
+//   old (lane x + 16 q, reg a + 4 b) at x + 16 q + 64 a + 272 b (complex units),
+//   read back as (lane x + 16 b, reg a + 4 q).
+__device__ __forceinline__ void lane_reg_swap_lds(pc (&v)[16], pc* buf, int lane) {
+    const int x = lane & 15, q = lane >> 4;
+    pc* wb = buf + x + 16 * q;
+    const pc* rb = buf + x + 272 * q;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wb[64 * (r & 3) + 272 * (r >> 2)] = v[r];
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = rb[16 * (r >> 2) + 64 * (r & 3)];
+    wave_lds_fence();
+}
+template <int MODE>
+__device__ __forceinline__ void lane_reg_swap_any(pc (&v)[16], pc* buf, int lane) {
+    if constexpr (MODE == 1)
+        lane_reg_swap_lds(v, buf, lane);
+    else
+        lane_reg_swap(v);
+}
+#ifndef CRLOT_PAIR_SWAP_LDS
+#define CRLOT_PAIR_SWAP_LDS 0  // measured: the LDS swap costs as many cycles as the permlanes and more power
+#endif
+
 // 16x16 transpose inside each quarter wave through LDS: lane (x + 16 q),
 // register y  ->  lane (y + 16 q), register x.  Layout: q * 288 + 18 * row + col
 // (complex units): ds_write_b64 groups of 16 lanes hit 16 consecutive elements,
@@ -226,44 +252,71 @@ __host__ __device__ constexpr int pair_t1_index(int k1, int l) {
     return k1 == 15 ? 896 + l : ((k1 - 1) >> 1) * 128 + 2 * l + ((k1 - 1) & 1);
 }
 template <bool INV>
-__device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const pc* t1, int lane) {
+__device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const pc* const& t1, int lane) {
     const float4* t4 = reinterpret_cast<const float4*>(t1 + 2 * lane);
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
+#ifdef CRLOT_ABL_NOT1  // timing-only ablation: twiddles from registers, wrong results
+        const float4 t = make_float4(0.6f + j * 0.01f, 0.8f, 0.6f, -0.8f - j * 0.01f);
+#else
         const float4 t = t4[j * 64];
+#endif
         v[2 * j + 1] = pc_tw<INV>(v[2 * j + 1], pc_mk(t.x, t.y));
         v[2 * j + 2] = pc_tw<INV>(v[2 * j + 2], pc_mk(t.z, t.w));
     }
     v[15] = pc_tw<INV>(v[15], t1[896 + lane]);
 }
 
+// Register-resident twiddles (3 waves per SIMD builds): w1[k1 - 1] = W1024^{lane k1},
+// w2[c - 1] = W64^{(lane & 15) c}.
+struct PairTw {
+    pc w1[15];
+    pc w2[3];
+};
+__device__ __forceinline__ void pair_tw_load(PairTw& tw, const pc* t1, const pc* t2, int lane) {
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) tw.w1[k1 - 1] = t1[pair_t1_index(k1, lane)];
+#pragma unroll
+    for (int c = 1; c < 4; ++c) tw.w2[c - 1] = t2[16 * (c - 1)];
+}
+template <bool INV>
+__device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const PairTw& tw, int) {
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = pc_tw<INV>(v[k1], tw.w1[k1 - 1]);
+}
+__device__ __forceinline__ pc pair_t2(const pc* t2, int c) { return t2[16 * (c - 1)]; }
+__device__ __forceinline__ pc pair_t2(const PairTw& tw, int c) { return tw.w2[c - 1]; }
+
 // Forward: natural z[lane + 64 m] -> bin-scrambled X (pair_bin).
-//   t1: W1024^{l k1} (pair_t1_index), t2[16 (c - 1)] = W64^{(lane & 15) c} (LDS).
-__device__ __forceinline__ void pair_fft_fwd(pc (&v)[16], pc* buf, const pc* t1, const pc* t2, int lane) {
+//   t1: W1024^{l k1} (pair_t1_index), t2[16 (c - 1)] = W64^{(lane & 15) c} (LDS),
+//   or both from a PairTw (T1 = PairTw, t2 unused).
+template <typename T1, typename T2>
+__device__ __forceinline__ void pair_fft_fwd(pc (&v)[16], pc* buf, const T1& t1, const T2& t2, int lane) {
     pdft16<false>(v);
     pair_t1_apply<false>(v, t1, lane);
-    lane_reg_swap(v);
+    lane_reg_swap_any<CRLOT_PAIR_SWAP_LDS>(v, buf, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) pdft4<false>(v[j], v[j + 4], v[j + 8], v[j + 12]);
 #pragma unroll
     for (int c = 1; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mul(v[j + 4 * c], t2[16 * (c - 1)]);
+        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mul(v[j + 4 * c], pair_t2(t2, c));
     transpose16(v, buf, lane);
     pdft16<false>(v);
 }
 
 // Inverse (unnormalised): bin-scrambled Y -> natural y[lane + 64 m].
-__device__ __forceinline__ void pair_fft_inv(pc (&v)[16], pc* buf, const pc* t1, const pc* t2, int lane) {
+template <typename T1, typename T2>
+__device__ __forceinline__ void pair_fft_inv(pc (&v)[16], pc* buf, const T1& t1, const T2& t2, int lane) {
     pdft16<true>(v);
     transpose16(v, buf, lane);
 #pragma unroll
     for (int c = 1; c < 4; ++c)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mulc(v[j + 4 * c], t2[16 * (c - 1)]);
+        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mulc(v[j + 4 * c], pair_t2(t2, c));
 #pragma unroll
     for (int j = 0; j < 4; ++j) pdft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
-    lane_reg_swap(v);
+    lane_reg_swap_any<CRLOT_PAIR_SWAP_LDS>(v, buf, lane);
     pair_t1_apply<true>(v, t1, lane);
     pdft16<true>(v);
 }

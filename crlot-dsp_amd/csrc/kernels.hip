@@ -548,8 +548,11 @@ __device__ uint32_t g_pair_phase[8 << 16];
     do {         \
     } while (0)
 #endif
+#ifndef CRLOT_PAIR_REG_TW
+#define CRLOT_PAIR_REG_TW 0
+#endif
 #ifndef CRLOT_PAIR_MIN_WAVES
-#define CRLOT_PAIR_MIN_WAVES 4
+#define CRLOT_PAIR_MIN_WAVES (CRLOT_PAIR_REG_TW ? 3 : 4)
 #endif
 template <int SH, int NB, int W, bool HAS_GAIN>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
@@ -612,7 +615,11 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
 #pragma unroll
         for (int m4 = 0; m4 < E / 4; ++m4) {
+#ifdef CRLOT_ABL_NOWIN  // timing-only ablation: no window reads, wrong results
+            const float4 w = make_float4(1e-3f, 2e-3f, 1e-3f, 2e-3f);
+#else
             const float4 w = *reinterpret_cast<const float4*>(ws4 + m4 * 256 + lane * 4);
+#endif
             const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -650,7 +657,11 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         // warm-up blocks (k < f0) store through a zero-size descriptor: every
         // lane is out of range and the store is dropped.  No branch around the
         // stores, so vmcnt bookkeeping stays exact at the next divisor wait.
+#ifdef CRLOT_ABL_NOSTORE  // timing-only ablation: every store dropped
+        const __amdgpu_buffer_rsrc_t rk = ry_null;
+#else
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#endif
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
@@ -667,11 +678,20 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     uint32_t ph[6] = {0, 0, 0, 0, 0, 0};
     uint64_t ph_last = __builtin_amdgcn_s_memtime();
 #endif
+#if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
+    dev::PairTw tw;
+    dev::pair_tw_load(tw, t1, t2, lane);
+    const dev::PairTw& tw1 = tw;
+    const dev::PairTw& tw2 = tw;
+#else
+    const dev::pc* const tw1 = t1;
+    const dev::pc* const tw2 = t2;
+#endif
     auto transform = [&](dev::pc (&v)[E]) {  // forward, spectral gain, inverse (unnormalised)
 #ifdef CRLOT_ABL_NOFFT  // timing-only ablation: the memory stream alone
         return;
 #endif
-        dev::pair_fft_fwd(v, buf, t1, t2, lane);
+        dev::pair_fft_fwd(v, buf, tw1, tw2, lane);
         PHASE(2);
         if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins
             const int gbase = dev::pair_bin_lane(lane);
@@ -682,7 +702,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                 v[d] = v[d] * gk;
             }
         }
-        dev::pair_fft_inv(v, buf, t1, t2, lane);
+        dev::pair_fft_inv(v, buf, tw1, tw2, lane);
 #ifdef CRLOT_ABL_DUMMY  // timing-only: CRLOT_ABL_DUMMY extra independent VALU ops per transform
         {
             float d[8];
@@ -721,7 +741,11 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             dev::pc v[E];
 #pragma unroll
             for (int m4 = 0; m4 < E / 4; ++m4) {
+#ifdef CRLOT_ABL_NOWIN
+                const float4 w = make_float4(0.5f, 0.25f, 0.5f, 0.25f);
+#else
                 const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
+#endif
                 const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
@@ -1598,7 +1622,7 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
 // K_pair: N = 1024, H = 64 * SH.  W waves per workgroup (16: one workgroup of
 // 155 KB LDS per CU, 4 waves/SIMD at <= 128 VGPRs).
 #ifndef CRLOT_PAIR_WAVES
-#define CRLOT_PAIR_WAVES 16
+#define CRLOT_PAIR_WAVES (CRLOT_PAIR_REG_TW ? 12 : 16)
 #endif
 constexpr int kPairWaves = CRLOT_PAIR_WAVES;
 
