@@ -38,7 +38,7 @@ struct crlot_plan {
     float* d_wsn = nullptr;   // ws * (1/N)
     float* d_rden = nullptr;  // RN(1 / den)
     float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
-    float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024)
+    float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024: 64 lanes, N = 4096: 256)
     float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
@@ -95,8 +95,13 @@ crlot::DevTables tables(const crlot_plan* p) {
         t.rden = p->d_rden;
     }
     if (p->pairing) {
-        t.ptw = p->d_ptw;
-        t.pden = p->d_pden;
+        if (p->geo.n == 4096) {
+            t.ptw4 = p->d_ptw;
+            t.pden4 = p->d_pden;
+        } else {
+            t.ptw = p->d_ptw;
+            t.pden = p->d_pden;
+        }
         t.px_lo = p->px_lo;
         // no transform can overflow: |x w| <= 2^64 / max gain, so |X| < 2^75, |ifft| < 2^86
         t.px_hi = p->px_hi / std::max(1.0f, p->has_gain ? p->gain_max : 1.0f);
@@ -149,15 +154,16 @@ int upload_window_tables(crlot_plan* p) {
     }
     p->px_lo = wmin > 0.0 ? std::nextafter(float(double(1e-30f) / wmin * (1.0 + 0x1p-20)), INFINITY) : 0.0f;
     p->px_hi = float(0x1p64 / std::max(1.0, wmax));
-    if (p->d_pden) {  // [block][lane][den SH | rden SH]
-        const int h = p->geo.h, sh = h / 64, blocks = int(den.size()) / h;
+    if (p->d_pden) {  // [block][lane][den SH | rden SH], den at block offset lane + lanes q
+        const int h = p->geo.h, lanes = p->geo.n == 4096 ? 256 : 64, sh = h / lanes;
+        const int blocks = int(den.size()) / h;
         std::vector<float> pd(2 * den.size());
         for (int b = 0; b < blocks; ++b)
-            for (int l = 0; l < 64; ++l)
+            for (int l = 0; l < lanes; ++l)
                 for (int q = 0; q < sh; ++q) {
-                    const size_t at = (size_t(b) * 64 + l) * 2 * sh;
-                    pd[at + q] = den[size_t(b) * h + l + 64 * q];
-                    pd[at + sh + q] = rden[size_t(b) * h + l + 64 * q];
+                    const size_t at = (size_t(b) * lanes + l) * 2 * sh;
+                    pd[at + q] = den[size_t(b) * h + l + lanes * q];
+                    pd[at + sh + q] = rden[size_t(b) * h + l + lanes * q];
                 }
         hipError_t e = hipMemcpy(p->d_pden, pd.data(), sizeof(float) * pd.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pair den)");
@@ -300,8 +306,9 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }
-    if (n == 1024 && h % 128 == 0 && ring % h == 0) {  // K_pair tables
-        const std::vector<float> ptw = crlot::build_pair_twiddles();
+    if ((n == 1024 && h % 128 == 0 && ring % h == 0) ||
+        (n == 4096 && h % 512 == 0 && ring % h == 0)) {  // K_pair / K_pair4k tables
+        const std::vector<float> ptw = n == 1024 ? crlot::build_pair_twiddles() : crlot::build_pair4k_twiddles();
         if ((e = hipMalloc(&p->d_pden, sizeof(float) * 2 * ring)) ||
             (e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
             (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {

@@ -29,10 +29,16 @@ struct DevTables {
     // K_pair paired regime: samples x with x == 0 or px_lo <= |x| <= px_hi keep
     // sanitize(x * wa) == x * wa and the transforms finite (kernels.hip K_pair).
     float px_lo = 0.f, px_hi = 0.f;
+    // K_pair4k (N = 4096): twiddles (fft_pair4k.h kP4Tw float pairs) and divisors
+    // [ring_len/H][256 lanes][den SH | rden SH], SH = H/256.
+    const float* ptw4 = nullptr;
+    const float* pden4 = nullptr;
 };
 
 // Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.
 std::vector<float> build_pair_twiddles();
+// ... and of the 4096-point one (fft_pair4k.h).
+std::vector<float> build_pair4k_twiddles();
 
 // Per-pass Stockham twiddles for an N-point real frame (P = N/2 complex points),
 // laid out as the device reads them (fft_wave.h twiddle_table_size), computed in

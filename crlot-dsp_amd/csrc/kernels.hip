@@ -26,6 +26,7 @@
 
 #include "fft_any.h"
 #include "fft_pair.h"
+#include "fft_pair4k.h"
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -813,6 +814,191 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         tr[gw] = make_uint4(trace_t0, t1e, hw, xcc);
     }
 #endif
+}
+
+// ------------------------------------------------------------------ fused, frame pairs (N = 4096)
+// K_pair4k k_stft_ola_pair4k<SH,NB>: K_pair's walk for N = 4096 by a 256-lane
+// workgroup (fft_pair4k.h): frames 2j and 2j+1 of a stream in one 4096-point
+// complex transform, lane t holding samples t + 256 m; a hop is SH = H/256
+// floats per lane.  Same regimes, OLA order, divisions and store rules as
+// K_pair; the regime of a pair is agreed by the whole workgroup
+// (__syncthreads_or), since its transforms exchange data across the four waves.
+template <int SH>
+__device__ __forceinline__ void load_hop4k(float* dst, __amdgpu_buffer_rsrc_t rx, int t, int origin, int T,
+                                           int mode) {
+    constexpr int H = 256 * SH;
+    if (origin >= 0 && origin + H <= T) {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, t * 4, origin * 4 + q * 1024);
+    } else {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = fetch_x(rx, origin + t + 256 * q, T, mode);
+    }
+}
+template <int SH>
+__device__ __forceinline__ bool hop_bad(const float* h, float lo, float hi) {
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        const float a = __builtin_fabsf(h[q]);
+        bad |= !((a >= lo) & (a <= hi)) & (a != 0.0f);
+    }
+    return bad;
+}
+// den | rden of block b for workgroup lane t (DevTables::pden: [block][256][den SH | rden SH])
+template <int SH>
+__device__ __forceinline__ void load_den4k(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int t, int b) {
+#pragma unroll
+    for (int j = 0; j < 2 * SH / 4; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, t * (8 * SH), b * (2048 * SH) + 16 * j, 0);
+        const unsigned u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];  // (see bload2)
+        dr[4 * j] = __builtin_bit_cast(float, u0);
+        dr[4 * j + 1] = __builtin_bit_cast(float, u1);
+        dr[4 * j + 2] = __builtin_bit_cast(float, u2);
+        dr[4 * j + 3] = __builtin_bit_cast(float, u3);
+    }
+}
+
+constexpr size_t kPair4kLds = sizeof(cf) * (dev::kP4Xbuf + 4 * dev::kPairXbuf);
+
+template <int SH, int NB, bool HAS_GAIN>
+__global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
+    constexpr int E = 16, N = 4096, H = 256 * SH;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    dev::pc* xb = reinterpret_cast<dev::pc*>(smem);
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    dev::pc* qb = xb + dev::kP4Xbuf + wave * dev::kPairXbuf;
+
+    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
+    const float g = a.gain;
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
+
+    dev::Pair4kTw tw;
+    dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw4), t);
+    float wa[E], ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = a.t.wa[t + 256 * m];
+        ws[m] = a.t.wsn[t + 256 * m];
+    }
+
+    // xin[h*SH + q]: hop (k + h), h = 0..NB; bit h of hopok: hop k + h keeps the paired regime
+    float xin[E + SH];
+    uint32_t hopok = 0;
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop4k<SH>(xin + h * SH, rx, t, (fs + h) * H - a.pad, a.T, a.pad_mode);
+        hopok |= (__syncthreads_or(hop_bad<SH>(xin + h * SH, xlo, xhi)) ? 0u : 1u) << h;
+    }
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+
+    auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float x = imag ? v[m].y : v[m].x;
+            const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
+            float& r = acc[m / SH][m % SH];
+            r = __builtin_fmaf(__builtin_fmaf(o, ws[m], 0.0f), g, r);
+        }
+    };
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
+        float mx = 0.0f, mn = 0x1p127f;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const float u = __builtin_fabsf(acc[0][q]);
+            mx = __builtin_fmaxf(mx, u);
+            mn = __builtin_fminf(mn, u);
+        }
+        const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(acc[0][q], dr[q], dr[SH + q]);
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+#pragma unroll
+            for (int q = 0; q < SH; ++q) o[q] = acc[0][q] / dr[q];
+        }
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
+                                                  k * (4 * H) + q * 1024, 0);
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < SH; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
+    };
+    auto transform = [&](dev::pc (&v)[E]) {
+        dev::pair4k_fwd(v, xb, qb, tw, t);
+        if constexpr (HAS_GAIN) {
+#pragma unroll
+            for (int d = 0; d < E; ++d) {
+                const int kb = dev::pair4k_bin(t, d);
+                v[d] = v[d] * a.t.gain[kb <= N / 2 ? kb : N - kb];
+            }
+        }
+        dev::pair4k_inv(v, xb, qb, tw, t);
+    };
+
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
+    for (int k = fs; k < f1; k += 2) {
+        float nxt[2 * SH];
+        load_hop4k<SH>(nxt, rx, t, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
+        load_hop4k<SH>(nxt + SH, rx, t, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        const bool paired = (hopok & kPairHops) == kPairHops;
+        if (paired) {
+            const bool partner = k + 1 < a.F;
+            dev::pc v[E];
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(xin[m] * wa[m], partner ? xin[m + SH] * wa[m] : 0.0f);
+            transform(v);
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den4k<SH>(dr0, rp, t, k % a.ring_blocks);
+            load_den4k<SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
+            accumulate(v, false, true);
+            emit(k, dr0);
+            if (k + 1 < f1) {
+                accumulate(v, true, true);
+                emit(k + 1, dr1);
+            }
+        } else {  // unpaired: frames k and k+1 alone, full sanitize
+            const int npass = min(2, f1 - k);
+            for (int p = 0; p < npass; ++p) {
+                dev::pc v[E];
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    v[m] = dev::pc_mk(dev::sanit((p ? xin[m + SH] : xin[m]) * wa[m]), 0.0f);
+                transform(v);
+                float dr[2 * SH];
+                load_den4k<SH>(dr, rp, t, (k + p) % a.ring_blocks);
+                accumulate(v, false, false);
+                emit(k + p, dr);
+            }
+        }
+        const uint32_t ok1 = __syncthreads_or(hop_bad<SH>(nxt, xlo, xhi)) ? 0u : 1u;
+        const uint32_t ok2 = __syncthreads_or(hop_bad<SH>(nxt + SH, xlo, xhi)) ? 0u : 1u;
+        hopok = (hopok | ok1 << (NB + 1) | ok2 << (NB + 2)) >> 2;
+#pragma unroll
+        for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
+#pragma unroll
+        for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
+    }
 }
 
 // ------------------------------------------------------------------ fused, workgroup walker
@@ -1755,6 +1941,23 @@ std::vector<float> build_pair_twiddles() {
     return t;
 }
 
+std::vector<float> build_pair4k_twiddles() {
+    std::vector<float> t;
+    for (int k1 = 1; k1 < 16; ++k1)
+        for (int l = 0; l < 256; ++l) {
+            const double ph = -2.0 * M_PI * double(l * k1) / 4096.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    for (int k2 = 1; k2 < 16; ++k2)
+        for (int x = 0; x < 16; ++x) {
+            const double ph = -2.0 * M_PI * double(x * k2) / 256.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    return t;
+}
+
 std::vector<float> build_pass_twiddles(int n) {
     const int p = n / 2, e = p / 64;
     std::vector<float> t;
@@ -1841,6 +2044,17 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     }
 }
 
+// K_pair4k: N = 4096, H = 256 SH, one 256-lane workgroup per chunk, two per CU.
+template <int SH>
+static hipError_t pair4k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    constexpr int NB = 16 / SH;
+    auto k = a.t.gain ? k_stft_ola_pair4k<SH, NB, true> : k_stft_ola_pair4k<SH, NB, false>;
+    hipError_t e = set_lds(k, kPair4kLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(256), kPair4kLds, stream, a);
+    return hipGetLastError();
+}
+
 // Workgroup walker: N = 16 L (E = 8), H = 2 L S.
 template <int L, int S>
 static hipError_t fused_wg_ls(const FusedArgs& a, int64_t grid, hipStream_t stream) {
@@ -1901,6 +2115,22 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
     a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     a.gain = g.gain;
+    if (g.n == 4096 && t.ptw4 && t.pden4 && t.wsn && t.rden && (g.h == 512 || g.h == 1024 || g.h == 2048)) {
+        // K_pair4k: whole resident rounds of workgroups (two per CU)
+        choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 2, a.n_chunks, a.M);
+        if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
+            const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
+            a.M = int((F + n - 1) / n);
+            a.n_chunks = int((F + a.M - 1) / a.M);
+        }
+        const int64_t grid4 = int64_t(n_streams) * a.n_chunks;
+        switch (g.h / 256) {
+            case 2: return pair4k_sh<2>(a, grid4, stream);
+            case 4: return pair4k_sh<4>(a, grid4, stream);
+            case 8: return pair4k_sh<8>(a, grid4, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     const int64_t grid = int64_t(n_streams) * a.n_chunks;
     const int L = g.n / 16, s = g.h / (2 * L);
     switch (L) {

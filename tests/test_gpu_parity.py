@@ -131,13 +131,13 @@ def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
     assert np.array_equal(bits(y_unaligned), bits(y_fused))
 
 
-@pytest.mark.parametrize("h,mode", [(256, 0), (128, 0), (512, 1), (1024, 0), (256, 1)])
-def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, h, mode):
-    """K_pair (two frames per 1024-point complex transform) against the oracle's
-    per-frame kissfft chain and against the per-frame kernel, odd and even frame
-    counts, every hop the kernel takes."""
+@pytest.mark.parametrize("n,h,mode", [(1024, 256, 0), (1024, 128, 0), (1024, 512, 1), (1024, 1024, 0),
+                                      (1024, 256, 1), (4096, 1024, 0), (4096, 512, 1), (4096, 2048, 0)])
+def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
+    """K_pair / K_pair4k (two frames per 1024- / 4096-point complex transform)
+    against the oracle's per-frame kissfft chain and against the per-frame
+    kernel, odd and even frame counts, every hop the kernels take."""
     torch = torch_cuda
-    n = 1024
     for T in (100_002, 99_998 + h):  # even T: 8-byte aligned rows take the fused path
         x = oracle.synth_streams(3, T, config_id=h + mode + T % 7)
         xd = dev(torch, x)
@@ -152,11 +152,12 @@ def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, h, mode):
         assert not np.array_equal(bits(y), bits(yu))  # the pair kernel really ran
 
 
-def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch):
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024)])
+def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch, n, h):
     """Pairs are aligned to even frames, so a stream's output bits do not depend on
     how its frames are chunked over waves nor on the batch it is processed in."""
     torch = torch_cuda
-    n, h, T = 1024, 256, 60_000
+    T = 60_000
     x = oracle.synth_streams(5, T, config_id=12)
     xd = dev(torch, x)
     plan = pkg.Plan(frame_size=n, hop_size=h)
@@ -169,8 +170,8 @@ def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkey
     monkeypatch.delenv("CRLOT_CHUNKS")
 
 
-@pytest.mark.parametrize("burst_hop", [82, 83])
-def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, burst_hop, monkeypatch):
+@pytest.mark.parametrize("n,h,burst_hop", [(1024, 256, 82), (1024, 256, 83), (4096, 1024, 20), (4096, 1024, 21)])
+def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, n, h, burst_hop, monkeypatch):
     """K_pair's unpaired regime: a hop of huge samples (1e25, beyond px_hi) makes
     the pairs that contain it transform each frame alone, as the reference does,
     so a neighbour sharing a pair with a burst frame keeps its own accuracy.  The
@@ -179,7 +180,7 @@ def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, burst_hop, m
     region matches relative to its own scale; the bits do not depend on the
     chunking."""
     torch = torch_cuda
-    n, h, T = 1024, 256, 40_000
+    T = 40_000
     x = oracle.synth(T, 31).copy()
     x[burst_hop * h:(burst_hop + 1) * h] *= np.float32(2e25)
     x[5000:5100] = 0.0  # exact zeros keep the paired regime
