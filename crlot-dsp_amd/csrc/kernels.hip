@@ -1676,37 +1676,51 @@ __global__ __launch_bounds__(kBlock) void k_stream_hop(const StreamArgs a) {
     float* wa = reinterpret_cast<float*>(sth + P);
     float* ws = wa + N;
     cf* bufs = reinterpret_cast<cf*>(ws + N);
-    load_tables<E>(a.t, tw, st, sth, wa, ws, true);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    cf* buf = bufs + wave * xbuf_elems<P>();
     const int c = blockIdx.x * kWaves + wave;
-    if (c >= a.channels) return;
-    const float* in = a.in + c * a.in_ld;
-    float* hist = a.hist + int64_t(c) * N;
-    float* acc = a.acc + int64_t(c) * N;
+    const bool live = c < a.channels;
+    const int cc = live ? c : 0;
+    const float* in = a.in + cc * a.in_ld;
+    float* hist = a.hist + int64_t(cc) * N;
+    float* acc = a.acc + int64_t(cc) * N;
     const int64_t q = a.q;
-    // the new hop: frame pairs m in [E-S, E) when a frame completes this call
+    const bool frame = q >= NB - 1;
+    const int64_t f = q - (NB - 1);
+    // Everything a hop reads from global memory is requested before the table
+    // staging barrier, so the two latencies overlap (a hop is latency-bound).
     float2 hop[S];
 #pragma unroll
     for (int s2 = 0; s2 < S; ++s2) {
         const int i0 = 2 * (lane + 64 * s2);
         hop[s2] = make_float2(in[i0 * a.in_inc], in[(i0 + 1) * a.in_inc]);
     }
-    if (q >= NB - 1) {
-        const int64_t f = q - (NB - 1);
+    float2 xv[E];      // frame samples (older hops from their slots, the new hop last)
+    float2 cur[E];     // OLA blocks this frame adds to
+    float2 dd[S];      // divisors of the block that completes
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int i0 = 2 * (lane + 64 * m);
+        const int slot = int((f + m / S) % NB);
+        xv[m] = (frame && m < E - S) ? *reinterpret_cast<const float2*>(hist + slot * H + (i0 % H))
+                                     : make_float2(0.f, 0.f);
+        cur[m] = frame ? *reinterpret_cast<const float2*>(acc + slot * H + (i0 % H)) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int m = 0; m < S; ++m) {
+        const int64_t n = f * H + ((2 * (lane + 64 * m)) % H);
+        dd[m] = frame ? make_float2(a.t.den[n % a.ring_len], a.t.den[(n + 1) % a.ring_len]) : make_float2(1.f, 1.f);
+    }
+    load_tables<E>(a.t, tw, st, sth, wa, ws, true);
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    if (!live) return;
+    if (frame) {
         cf v[E];
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int i0 = 2 * (lane + 64 * m);
-            float2 xv;
-            if (m >= E - S) {
-                xv = hop[m - (E - S)];
-            } else {  // hop f + m/S sits in slot (f + m/S) mod NB
-                const int slot = int((f + m / S) % NB);
-                xv = *reinterpret_cast<const float2*>(hist + slot * H + (i0 % H));
-            }
-            v[m].r = dev::sanit(xv.x * wa[i0]);
-            v[m].i = dev::sanit(xv.y * wa[i0 + 1]);
+            const float2 x2 = m >= E - S ? hop[m - (E - S)] : xv[m];
+            v[m].r = dev::sanit(x2.x * wa[i0]);
+            v[m].i = dev::sanit(x2.y * wa[i0 + 1]);
         }
         dev::fft_wave<E, false>(v, buf, tw, lane);
         dev::real_split_hook_merge<E, HAS_GAIN, false>(v, buf, st, sth, a.t.gain, lane);
@@ -1718,19 +1732,17 @@ __global__ __launch_bounds__(kBlock) void k_stream_hop(const StreamArgs a) {
             const float o1 = dev::sanit(v[m].i * a.inv_n);
             const int slot = int((f + m / S) % NB);
             float2* r = reinterpret_cast<float2*>(acc + slot * H + (i0 % H));
-            float2 cur = *r;
-            cur.x = __builtin_fmaf(__builtin_fmaf(o0, ws[i0], 0.0f), a.gain, cur.x);
-            cur.y = __builtin_fmaf(__builtin_fmaf(o1, ws[i0 + 1], 0.0f), a.gain, cur.y);
+            float2 cu = cur[m];
+            cu.x = __builtin_fmaf(__builtin_fmaf(o0, ws[i0], 0.0f), a.gain, cu.x);
+            cu.y = __builtin_fmaf(__builtin_fmaf(o1, ws[i0 + 1], 0.0f), a.gain, cu.y);
             if (m < S) {  // block f is complete: produce(H) and clear its slot
                 const int pos = i0 % H;
-                const int64_t n = f * H + pos;
-                const float d0 = a.t.den[n % a.ring_len], d1 = a.t.den[(n + 1) % a.ring_len];
                 float* o = a.out + c * a.out_ld;
-                o[pos * a.out_inc] = cur.x / d0;
-                o[(pos + 1) * a.out_inc] = cur.y / d1;
-                cur = make_float2(0.f, 0.f);
+                o[pos * a.out_inc] = cu.x / dd[m].x;
+                o[(pos + 1) * a.out_inc] = cu.y / dd[m].y;
+                cu = make_float2(0.f, 0.f);
             }
-            *r = cur;
+            *r = cu;
         }
     }
     // store the new hop into its slot for later frames
