@@ -324,10 +324,12 @@ def test_windows_and_flags(pkg, oracle, torch_cuda):
                  host(plan.ola_gather(frames))[0], 0.5, "no-analysis y")
 
 
-def test_spectral_gain_hook(pkg, oracle, torch_cuda):
-    """Per-bin gain between rfft and irfft vs a float64 model of the same chain."""
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024)])
+def test_spectral_gain_hook(pkg, oracle, torch_cuda, n, h):
+    """Per-bin gain between rfft and irfft vs a float64 model of the same chain;
+    the frame-pair kernels (K_pair, K_pair4k) apply it per complex bin."""
     torch = torch_cuda
-    n, h, T = 1024, 256, 12000
+    T = 12000 if n == 1024 else 40000
     x = oracle.synth_streams(1, T, config_id=66)[0]
     g = np.linspace(1.0, 0.0, n // 2 + 1).astype(np.float32)
     plan = pkg.Plan(frame_size=n, hop_size=h)
