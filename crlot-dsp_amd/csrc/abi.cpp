@@ -306,9 +306,11 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }
-    if ((n == 1024 && h % 128 == 0 && ring % h == 0) ||
-        (n == 4096 && h % 512 == 0 && ring % h == 0)) {  // K_pair / K_pair4k tables
-        const std::vector<float> ptw = n == 1024 ? crlot::build_pair_twiddles() : crlot::build_pair4k_twiddles();
+    if ((n == 1024 && h % 128 == 0 && ring % h == 0) || (n == 512 && h % 128 == 0 && ring % h == 0) ||
+        (n == 4096 && h % 512 == 0 && ring % h == 0)) {  // K_pair / K_pair512 / K_pair4k tables
+        const std::vector<float> ptw = n == 1024  ? crlot::build_pair_twiddles()
+                                       : n == 512 ? crlot::build_pair512_twiddles()
+                                                  : crlot::build_pair4k_twiddles();
         if ((e = hipMalloc(&p->d_pden, sizeof(float) * 2 * ring)) ||
             (e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
             (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {

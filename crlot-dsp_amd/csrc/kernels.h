@@ -37,8 +37,9 @@ struct DevTables {
 
 // Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.
 std::vector<float> build_pair_twiddles();
-// ... and of the 4096-point one (fft_pair4k.h).
+// ... and of the 4096- and 512-point ones (fft_pair4k.h, fft_pair512.h).
 std::vector<float> build_pair4k_twiddles();
+std::vector<float> build_pair512_twiddles();
 
 // Per-pass Stockham twiddles for an N-point real frame (P = N/2 complex points),
 // laid out as the device reads them (fft_wave.h twiddle_table_size), computed in

@@ -27,6 +27,7 @@
 #include "fft_any.h"
 #include "fft_pair.h"
 #include "fft_pair4k.h"
+#include "fft_pair512.h"
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -814,6 +815,150 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         tr[gw] = make_uint4(trace_t0, t1e, hw, xcc);
     }
 #endif
+}
+
+// ------------------------------------------------------------------ fused, frame pairs (N = 512)
+// K_pair512 k_stft_ola_pair512<SH,NB>: K_pair's walk for N = 512 (fft_pair512.h):
+// frames 2j and 2j+1 of a stream in one 512-point complex transform per wave,
+// lane l holding samples l + 64 m (m < 8); a hop is SH = H/64 floats per lane.
+// Same regimes, OLA order, divisions and store rules as K_pair; twiddles and
+// both windows in registers; one 4.6 KB LDS buffer per wave.
+constexpr int kP512Waves = 4;
+template <int SH, int NB, bool HAS_GAIN>
+__global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const FusedArgs a) {
+    constexpr int E = 8, N = 512, H = 64 * SH;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kP512Buf;
+    const int gw = blockIdx.x * kP512Waves + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+    const float g = a.gain;
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
+
+    dev::Pair512Tw tw;
+    dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
+    float wa[E], ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = a.t.wa[lane + 64 * m];
+        ws[m] = a.t.wsn[lane + 64 * m];
+    }
+
+    float xin[E + SH];
+    uint32_t hopok = 0;
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop1<SH>(xin + h * SH, rx, lane, (fs + h) * H - a.pad, a.T, a.pad_mode);
+        hopok |= hop_ok<SH>(xin + h * SH, xlo, xhi) << h;
+    }
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+
+    auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float x = imag ? v[m].y : v[m].x;
+            const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
+            float& r = acc[m / SH][m % SH];
+            r = __builtin_fmaf(__builtin_fmaf(o, ws[m], 0.0f), g, r);
+        }
+    };
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
+        float mx = 0.0f, mn = 0x1p127f;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const float u = __builtin_fabsf(acc[0][q]);
+            mx = __builtin_fmaxf(mx, u);
+            mn = __builtin_fminf(mn, u);
+        }
+        const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(acc[0][q], dr[q], dr[SH + q]);
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+#pragma unroll
+            for (int q = 0; q < SH; ++q) o[q] = acc[0][q] / dr[q];
+        }
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
+                                                  k * (4 * H) + q * 256, 0);
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < SH; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
+    };
+    auto transform = [&](dev::pc (&v)[E]) {
+        dev::pair512_fwd(v, buf, tw, lane);
+        if constexpr (HAS_GAIN) {
+#pragma unroll
+            for (int d = 0; d < E; ++d) {
+                const int kb = dev::pair512_bin(lane, d);
+                v[d] = v[d] * a.t.gain[kb <= N / 2 ? kb : N - kb];
+            }
+        }
+        dev::pair512_inv(v, buf, tw, lane);
+    };
+
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
+    for (int k = fs; k < f1; k += 2) {
+        float nxt[2 * SH];
+        load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
+        load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        const bool paired = (hopok & kPairHops) == kPairHops;
+        if (paired) {
+            const bool partner = k + 1 < a.F;
+            dev::pc v[E];
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(xin[m] * wa[m], partner ? xin[m + SH] * wa[m] : 0.0f);
+            transform(v);
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
+            load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+            accumulate(v, false, true);
+            emit(k, dr0);
+            if (k + 1 < f1) {
+                accumulate(v, true, true);
+                emit(k + 1, dr1);
+            }
+        } else {  // unpaired: frames k and k+1 alone, full sanitize
+            const int npass = min(2, f1 - k);
+            for (int p = 0; p < npass; ++p) {
+                dev::pc v[E];
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    v[m] = dev::pc_mk(dev::sanit((p ? xin[m + SH] : xin[m]) * wa[m]), 0.0f);
+                transform(v);
+                float dr[2 * SH];
+                load_den<SH>(dr, rp, lane, (k + p) % a.ring_blocks);
+                accumulate(v, false, false);
+                emit(k + p, dr);
+            }
+        }
+        hopok = (hopok | hop_ok<SH>(nxt, xlo, xhi) << (NB + 1) | hop_ok<SH>(nxt + SH, xlo, xhi) << (NB + 2)) >> 2;
+#pragma unroll
+        for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
+#pragma unroll
+        for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
+    }
 }
 
 // ------------------------------------------------------------------ fused, frame pairs (N = 4096)
@@ -1852,6 +1997,27 @@ hipError_t launch_pair(int sh, const FusedArgs& a, int64_t waves, hipStream_t st
     }
 }
 
+// K_pair512: N = 512, H = 64 SH, 4 independent waves per workgroup.
+template <int SH>
+hipError_t pair512_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
+    constexpr int NB = 8 / SH;
+    auto k = a.t.gain ? k_stft_ola_pair512<SH, NB, true> : k_stft_ola_pair512<SH, NB, false>;
+    const size_t lds = sizeof(cf) * dev::kP512Buf * kP512Waves;
+    hipError_t e = set_lds(k, lds);
+    if (e != hipSuccess) return e;
+    const int64_t grid = (waves + kP512Waves - 1) / kP512Waves;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * kP512Waves), lds, stream, a);
+    return hipGetLastError();
+}
+hipError_t launch_pair512(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream) {
+    switch (sh) {
+        case 2: return pair512_sh<2>(a, waves, stream);
+        case 4: return pair512_sh<4>(a, waves, stream);
+        case 8: return pair512_sh<8>(a, waves, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 template <int E>
 hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) {
     if constexpr (E >= 1) {
@@ -1953,6 +2119,23 @@ std::vector<float> build_pair_twiddles() {
     return t;
 }
 
+std::vector<float> build_pair512_twiddles() {
+    std::vector<float> t;
+    for (int k1 = 1; k1 < 8; ++k1)
+        for (int l = 0; l < 64; ++l) {
+            const double ph = -2.0 * M_PI * double(l * k1) / 512.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    for (int k2 = 1; k2 < 8; ++k2)
+        for (int x = 0; x < 8; ++x) {
+            const double ph = -2.0 * M_PI * double(x * k2) / 64.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    return t;
+}
+
 std::vector<float> build_pair4k_twiddles() {
     std::vector<float> t;
     for (int k1 = 1; k1 < 16; ++k1)
@@ -2018,6 +2201,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
 #else
     const bool use_pair = g.n == 1024 && t.ptw && t.pden && fast;
 #endif
+    const bool use_pair512 = g.n == 512 && t.ptw && t.pden && fast && g.h >= 128;
 #ifdef CRLOT_OLD_CHUNKS  // A/B builds: fixed ~128-frame chunks
     const int target = 128;
     a.n_chunks = int((F + target - 1) / target);
@@ -2028,8 +2212,9 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     const bool pair = !use_pair && fused2_used(e, g.h / 128, fast);
     const int resident = use_pair ? fused_resident_waves() * pair_waves_per_cu() / 16
                          : pair && e == 8 ? fused_resident_waves() * 3 / 4 : fused_resident_waves();
-    if (use_pair)
-        choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.n_chunks, a.M);
+    if (use_pair || use_pair512)
+        choose_chunks_rounds(F, n_streams, g.n / g.h + 1, use_pair512 ? fused_resident_waves() : resident,
+                             a.n_chunks, a.M);
     else
         choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
     if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
@@ -2045,6 +2230,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     a.gain = g.gain;
     const int64_t waves = int64_t(n_streams) * a.n_chunks;
     if (use_pair) return launch_pair(g.h / 64, a, waves, stream);
+    if (use_pair512) return launch_pair512(g.h / 64, a, waves, stream);
     const int64_t grid = (waves + kWaves - 1) / kWaves;
     const int s = g.h / 128;
     switch (e) {

@@ -152,7 +152,7 @@ def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
         assert not np.array_equal(bits(y), bits(yu))  # the pair kernel really ran
 
 
-@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128)])
 def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch, n, h):
     """Pairs are aligned to even frames, so a stream's output bits do not depend on
     how its frames are chunked over waves nor on the batch it is processed in."""
@@ -170,7 +170,8 @@ def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkey
     monkeypatch.delenv("CRLOT_CHUNKS")
 
 
-@pytest.mark.parametrize("n,h,burst_hop", [(1024, 256, 82), (1024, 256, 83), (4096, 1024, 20), (4096, 1024, 21)])
+@pytest.mark.parametrize("n,h,burst_hop", [(1024, 256, 82), (1024, 256, 83), (4096, 1024, 20), (4096, 1024, 21),
+                                           (512, 128, 150), (512, 128, 151)])
 def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, n, h, burst_hop, monkeypatch):
     """K_pair's unpaired regime: a hop of huge samples (1e25, beyond px_hi) makes
     the pairs that contain it transform each frame alone, as the reference does,
@@ -324,12 +325,12 @@ def test_windows_and_flags(pkg, oracle, torch_cuda):
                  host(plan.ola_gather(frames))[0], 0.5, "no-analysis y")
 
 
-@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128)])
 def test_spectral_gain_hook(pkg, oracle, torch_cuda, n, h):
     """Per-bin gain between rfft and irfft vs a float64 model of the same chain;
     the frame-pair kernels (K_pair, K_pair4k) apply it per complex bin."""
     torch = torch_cuda
-    T = 12000 if n == 1024 else 40000
+    T = 40000 if n == 4096 else 12000
     x = oracle.synth_streams(1, T, config_id=66)[0]
     g = np.linspace(1.0, 0.0, n // 2 + 1).astype(np.float32)
     plan = pkg.Plan(frame_size=n, hop_size=h)
