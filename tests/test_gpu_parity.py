@@ -80,13 +80,13 @@ def test_golden_e2e(pkg, torch_cuda, e2e_gold):
 # ------------------------------------------------------------------ live oracle
 CASES = [
     # N, H, mode, S, T
-    (1024, 256, 0, 3, 48000),        # BASELINE config 2 shape (fused)
+    (1024, 256, 0, 3, 48000),        # BASELINE config 2 shape (K_pair)
     (1024, 256, 0, 2, 480000),       # full-length streams, 15 chunks per stream
-    (4096, 1024, 0, 2, 40000),       # config 3 shape (fused workgroup walker, L=256)
-    (4096, 512, 1, 2, 30000),        # workgroup walker S=1 NB=8, DROP
-    (4096, 2048, 0, 2, 30001),       # workgroup walker S=4, odd T
-    (512, 128, 1, 3, 24000),         # config 4 shape, DROP framing (fused)
-    (1024, 512, 0, 2, 30001),        # e2e harness hop, odd T (fused)
+    (4096, 1024, 0, 2, 40000),       # config 3 shape (K_pair4k)
+    (4096, 512, 1, 2, 30000),        # K_pair4k SH=2 NB=8, DROP
+    (4096, 2048, 0, 2, 30001),       # K_pair4k SH=8, odd T
+    (512, 128, 1, 3, 24000),         # config 4 shape, DROP framing (K_pair512)
+    (1024, 512, 0, 2, 30001),        # e2e harness hop, odd T (K_pair)
     (2048, 512, 0, 2, 20000),        # fused E=16
     (256, 128, 0, 2, 5000),          # fused E=2
     (1024, 300, 0, 2, 9000),         # hop not a multiple of 128 (staged)
@@ -132,9 +132,10 @@ def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
 
 
 @pytest.mark.parametrize("n,h,mode", [(1024, 256, 0), (1024, 128, 0), (1024, 512, 1), (1024, 1024, 0),
-                                      (1024, 256, 1), (4096, 1024, 0), (4096, 512, 1), (4096, 2048, 0)])
+                                      (1024, 256, 1), (4096, 1024, 0), (4096, 512, 1), (4096, 2048, 0),
+                                      (512, 128, 0), (512, 256, 1), (512, 128, 1)])
 def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
-    """K_pair / K_pair4k (two frames per 1024- / 4096-point complex transform)
+    """K_pair / K_pair4k / K_pair512 (two frames per 1024- / 4096- / 512-point complex transform)
     against the oracle's per-frame kissfft chain and against the per-frame
     kernel, odd and even frame counts, every hop the kernels take."""
     torch = torch_cuda
