@@ -2070,19 +2070,23 @@ void choose_chunks(int64_t F, int n_streams, int nb, int resident, int& n_chunks
     n_chunks = int((F + m - 1) / m);
 }
 
-// K_pair: whole resident rounds.  Its 16-wave workgroups only free a CU when
-// all 16 finish, so a grid that ends in a partial round idles the device for a
-// whole chunk's time (measured at the headline: 15 chunks = 3.75 rounds
-// 219k Msamples/s, 8 chunks = 2 rounds 232k).  At least two rounds, chunks of
-// 48..256 frames, and among those the fewest rounds x (frames + halo) per wave.
+// K_pair*: whole resident rounds.  A pair kernel's workgroup only frees its
+// slots when all of its waves finish, so a grid that ends in a partial round
+// idles the device for a whole chunk's time (headline, 16 waves/CU: 15 chunks
+// = 3.75 rounds 219k Msamples/s, 8 chunks = 2 rounds 232k).  Among chunk counts
+// with chunks of >= 48 frames, the fewest (rounds + 0.1) x (frames + halo + 10)
+// per wave: the 0.1 charges a single long round for its tail, the 10 a wave's
+// start-up (tables, first hops) (measured: headline 6 chunks = 2 rounds best,
+// 9-15 within 1-3 %; config-4 shape 64 chunks = one round best).
 void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m) {
     const int64_t S = std::max(1, n_streams), R = std::max(1, resident);
     const int64_t hi = std::max<int64_t>(1, F / 48);
-    const int64_t lo = std::min(hi, std::max((2 * R + S - 1) / S, (F + 255) / 256));
-    int64_t best_n = lo, best_cost = INT64_MAX;
-    for (int64_t n = lo; n <= std::min(hi, 2 * lo); ++n) {
+    const int64_t lo = std::min(hi, (F + 511) / 512);
+    int64_t best_n = lo;
+    double best_cost = 1e300;
+    for (int64_t n = lo; n <= hi; ++n) {
         const int64_t mm = (F + n - 1) / n, nc = (F + mm - 1) / mm;
-        const int64_t cost = ((S * nc + R - 1) / R) * (mm + halo);
+        const double cost = (double((S * nc + R - 1) / R) + 0.1) * double(mm + halo + 10);
         if (cost < best_cost) best_cost = cost, best_n = n;
     }
     m = int((F + best_n - 1) / best_n);
