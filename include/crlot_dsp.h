@@ -103,9 +103,12 @@ int crlot_plan_set_spectral_gain(crlot_plan* plan, const float* gain);
 /* Frame pairing on the fused round trip (default on): two consecutive frames
  * (2j, 2j+1) of a stream share one complex FFT, z = frame_2j + i frame_2j+1,
  * whose real and imaginary round-trip outputs are the two frames' (exact for
- * the real, bin-symmetric spectral gain).  Used where that kernel exists
- * (N = 1024); results equal the per-frame kissfft formulation within float32
- * rounding, not bit for bit.  0 selects the per-frame (kiss_fftr split)
+ * the real, bin-symmetric spectral gain).  Used where those kernels exist
+ * (N = 512, 1024, 4096 with the fused hop rules); a pair holding a NaN, Inf,
+ * huge or tiny sample is transformed frame by frame instead, so no frame's
+ * overflow reaches its neighbour.  Results equal the per-frame kissfft
+ * formulation within float32 rounding, not bit for bit, and do not depend on
+ * the batch or the chunking.  0 selects the per-frame (kiss_fftr split)
  * kernels, bit-identical to crlot_roundtrip_stages + crlot_ola_gather. */
 int crlot_plan_set_frame_pairing(crlot_plan* plan, int32_t enable);
 int crlot_plan_info(const crlot_plan* plan, int32_t* frame_size, int32_t* hop_size,

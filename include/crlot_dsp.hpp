@@ -129,6 +129,10 @@ class StftEngine {
     void set_spectral_gain(const float* gain_or_null) {
         check(crlot_plan_set_spectral_gain(plan_.get(), gain_or_null), "set_spectral_gain");
     }
+    // crlot_plan_set_frame_pairing: two frames per complex transform (default) or per frame
+    void set_frame_pairing(bool enable) {
+        check(crlot_plan_set_frame_pairing(plan_.get(), enable ? 1 : 0), "set_frame_pairing");
+    }
     crlot_plan* plan() const { return plan_.get(); }
 
    private:
