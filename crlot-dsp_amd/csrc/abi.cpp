@@ -95,7 +95,7 @@ crlot::DevTables tables(const crlot_plan* p) {
         t.rden = p->d_rden;
     }
     if (p->pairing) {
-        if (p->geo.n == 4096) {
+        if (p->geo.n == 4096 || p->geo.n == 2048) {
             t.ptw4 = p->d_ptw;
             t.pden4 = p->d_pden;
         } else {
@@ -155,7 +155,7 @@ int upload_window_tables(crlot_plan* p) {
     p->px_lo = wmin > 0.0 ? std::nextafter(float(double(1e-30f) / wmin * (1.0 + 0x1p-20)), INFINITY) : 0.0f;
     p->px_hi = float(0x1p64 / std::max(1.0, wmax));
     if (p->d_pden) {  // [block][lane][den SH | rden SH], den at block offset lane + lanes q
-        const int h = p->geo.h, lanes = p->geo.n == 4096 ? 256 : 64, sh = h / lanes;
+        const int h = p->geo.h, lanes = p->geo.n == 4096 ? 256 : p->geo.n == 2048 ? 128 : 64, sh = h / lanes;
         const int blocks = int(den.size()) / h;
         std::vector<float> pd(2 * den.size());
         for (int b = 0; b < blocks; ++b)
@@ -307,10 +307,12 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         return hip_fail(e, "hipMalloc(plan tables)");
     }
     if ((n == 1024 && h % 128 == 0 && ring % h == 0) || (n == 512 && h % 128 == 0 && ring % h == 0) ||
-        (n == 4096 && h % 512 == 0 && ring % h == 0)) {  // K_pair / K_pair512 / K_pair4k tables
-        const std::vector<float> ptw = n == 1024  ? crlot::build_pair_twiddles()
-                                       : n == 512 ? crlot::build_pair512_twiddles()
-                                                  : crlot::build_pair4k_twiddles();
+        (n == 2048 && h % 256 == 0 && ring % h == 0) ||
+        (n == 4096 && h % 512 == 0 && ring % h == 0)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k tables
+        const std::vector<float> ptw = n == 1024   ? crlot::build_pair_twiddles()
+                                       : n == 512  ? crlot::build_pair512_twiddles()
+                                       : n == 2048 ? crlot::build_pair2k_twiddles()
+                                                   : crlot::build_pair4k_twiddles();
         if ((e = hipMalloc(&p->d_pden, sizeof(float) * 2 * ring)) ||
             (e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
             (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {

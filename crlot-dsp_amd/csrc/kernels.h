@@ -29,8 +29,9 @@ struct DevTables {
     // K_pair paired regime: samples x with x == 0 or px_lo <= |x| <= px_hi keep
     // sanitize(x * wa) == x * wa and the transforms finite (kernels.hip K_pair).
     float px_lo = 0.f, px_hi = 0.f;
-    // K_pair4k (N = 4096): twiddles (fft_pair4k.h kP4Tw float pairs) and divisors
-    // [ring_len/H][256 lanes][den SH | rden SH], SH = H/256.
+    // K_pair4k (N = 4096) / K_pair2k (N = 2048): twiddles (fft_pair4k.h kP4Tw /
+    // fft_pair2k.h kP2Tw float pairs) and divisors [ring_len/H][L lanes][den SH | rden SH],
+    // L = 256 / 128, SH = H/L.
     const float* ptw4 = nullptr;
     const float* pden4 = nullptr;
 };
@@ -40,6 +41,7 @@ std::vector<float> build_pair_twiddles();
 // ... and of the 4096- and 512-point ones (fft_pair4k.h, fft_pair512.h).
 std::vector<float> build_pair4k_twiddles();
 std::vector<float> build_pair512_twiddles();
+std::vector<float> build_pair2k_twiddles();  // fft_pair2k.h (N = 2048; stored in DevTables::ptw4)
 
 // Per-pass Stockham twiddles for an N-point real frame (P = N/2 complex points),
 // laid out as the device reads them (fft_wave.h twiddle_table_size), computed in

@@ -28,6 +28,7 @@
 #include "fft_pair.h"
 #include "fft_pair4k.h"
 #include "fft_pair512.h"
+#include "fft_pair2k.h"
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -1146,6 +1147,177 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ fused, frame pairs (N = 2048)
+// K_pair2k k_stft_ola_pair2k<SH,NB>: K_pair4k's walk for N = 2048 by a 128-lane
+// workgroup (fft_pair2k.h), lane t holding samples t + 128 m; a hop is
+// SH = H/128 floats per lane; tables in DevTables::ptw4 / pden4 (128 lanes).
+template <int SH>
+__device__ __forceinline__ void load_hop2k(float* dst, __amdgpu_buffer_rsrc_t rx, int t, int origin, int T,
+                                           int mode) {
+    constexpr int H = 128 * SH;
+    if (origin >= 0 && origin + H <= T) {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, t * 4, origin * 4 + q * 512);
+    } else {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = fetch_x(rx, origin + t + 128 * q, T, mode);
+    }
+}
+template <int SH>
+__device__ __forceinline__ void load_den2k(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int t, int b) {
+#pragma unroll
+    for (int j = 0; j < 2 * SH / 4; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, t * (8 * SH), b * (1024 * SH) + 16 * j, 0);
+        const unsigned u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];  // (see bload2)
+        dr[4 * j] = __builtin_bit_cast(float, u0);
+        dr[4 * j + 1] = __builtin_bit_cast(float, u1);
+        dr[4 * j + 2] = __builtin_bit_cast(float, u2);
+        dr[4 * j + 3] = __builtin_bit_cast(float, u3);
+    }
+}
+
+constexpr size_t kPair2kLds = sizeof(cf) * (dev::kP2Xbuf + 2 * dev::kP2Tbuf);
+
+template <int SH, int NB, bool HAS_GAIN>
+__global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
+    constexpr int E = 16, N = 2048, H = 128 * SH;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    dev::pc* xb = reinterpret_cast<dev::pc*>(smem);
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+    dev::pc* qb = xb + dev::kP2Xbuf + wave * dev::kP2Tbuf;
+
+    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
+    const float g = a.gain;
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
+
+    dev::Pair2kTw tw;
+    dev::pair2k_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw4), t);
+    float wa[E], ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = a.t.wa[t + 128 * m];
+        ws[m] = a.t.wsn[t + 128 * m];
+    }
+
+    // xin[h*SH + q]: hop (k + h), h = 0..NB; bit h of hopok: hop k + h keeps the paired regime
+    float xin[E + SH];
+    uint32_t hopok = 0;
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop2k<SH>(xin + h * SH, rx, t, (fs + h) * H - a.pad, a.T, a.pad_mode);
+        hopok |= (__syncthreads_or(hop_bad<SH>(xin + h * SH, xlo, xhi)) ? 0u : 1u) << h;
+    }
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+
+    auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float x = imag ? v[m].y : v[m].x;
+            const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
+            float& r = acc[m / SH][m % SH];
+            r = __builtin_fmaf(__builtin_fmaf(o, ws[m], 0.0f), g, r);
+        }
+    };
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
+        float mx = 0.0f, mn = 0x1p127f;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const float u = __builtin_fabsf(acc[0][q]);
+            mx = __builtin_fmaxf(mx, u);
+            mn = __builtin_fminf(mn, u);
+        }
+        const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(acc[0][q], dr[q], dr[SH + q]);
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+#pragma unroll
+            for (int q = 0; q < SH; ++q) o[q] = acc[0][q] / dr[q];
+        }
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
+                                                  k * (4 * H) + q * 512, 0);
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < SH; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
+    };
+    auto transform = [&](dev::pc (&v)[E]) {
+        dev::pair2k_fwd(v, xb, qb, tw, t);
+        if constexpr (HAS_GAIN) {
+#pragma unroll
+            for (int d = 0; d < E; ++d) {
+                const int kb = dev::pair2k_bin(t, d);
+                v[d] = v[d] * a.t.gain[kb <= N / 2 ? kb : N - kb];
+            }
+        }
+        dev::pair2k_inv(v, xb, qb, tw, t);
+    };
+
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
+    for (int k = fs; k < f1; k += 2) {
+        float nxt[2 * SH];
+        load_hop2k<SH>(nxt, rx, t, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
+        load_hop2k<SH>(nxt + SH, rx, t, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        const bool paired = (hopok & kPairHops) == kPairHops;
+        if (paired) {
+            const bool partner = k + 1 < a.F;
+            dev::pc v[E];
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(xin[m] * wa[m], partner ? xin[m + SH] * wa[m] : 0.0f);
+            transform(v);
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den2k<SH>(dr0, rp, t, k % a.ring_blocks);
+            load_den2k<SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
+            accumulate(v, false, true);
+            emit(k, dr0);
+            if (k + 1 < f1) {
+                accumulate(v, true, true);
+                emit(k + 1, dr1);
+            }
+        } else {  // unpaired: frames k and k+1 alone, full sanitize
+            const int npass = min(2, f1 - k);
+            for (int p = 0; p < npass; ++p) {
+                dev::pc v[E];
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    v[m] = dev::pc_mk(dev::sanit((p ? xin[m + SH] : xin[m]) * wa[m]), 0.0f);
+                transform(v);
+                float dr[2 * SH];
+                load_den2k<SH>(dr, rp, t, (k + p) % a.ring_blocks);
+                accumulate(v, false, false);
+                emit(k + p, dr);
+            }
+        }
+        const uint32_t ok1 = __syncthreads_or(hop_bad<SH>(nxt, xlo, xhi)) ? 0u : 1u;
+        const uint32_t ok2 = __syncthreads_or(hop_bad<SH>(nxt + SH, xlo, xhi)) ? 0u : 1u;
+        hopok = (hopok | ok1 << (NB + 1) | ok2 << (NB + 2)) >> 2;
+#pragma unroll
+        for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
+#pragma unroll
+        for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
+    }
+}
+
 // ------------------------------------------------------------------ fused, workgroup walker
 // K_fused_wg k_stft_ola_wg<L,S,NB>: the fused walk of K_fused for frames too big
 // for one wave (N = 16 L, E = 8): a workgroup of L lanes owns a run of frames
@@ -2018,6 +2190,39 @@ hipError_t launch_pair512(int sh, const FusedArgs& a, int64_t waves, hipStream_t
     }
 }
 
+// K_pair2k: N = 2048, H = 128 SH, one 128-lane workgroup per chunk, four per CU.
+template <int SH>
+hipError_t pair2k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    constexpr int NB = 16 / SH;
+    auto k = a.t.gain ? k_stft_ola_pair2k<SH, NB, true> : k_stft_ola_pair2k<SH, NB, false>;
+    hipError_t e = set_lds(k, kPair2kLds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(128), kPair2kLds, stream, a);
+    return hipGetLastError();
+}
+void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m);
+int fused_resident_waves();
+hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_streams, hipStream_t stream) {
+    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 4, a.n_chunks, a.M);
+    if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
+        const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
+        a.M = int((F + n - 1) / n);
+        a.n_chunks = int((F + a.M - 1) / a.M);
+    }
+    a.ring_blocks = g.ring_len / g.h;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
+    a.inv_n = g.inv_n;
+    a.gain = g.gain;
+    const int64_t grid = int64_t(n_streams) * a.n_chunks;
+    switch (g.h / 128) {
+        case 2: return pair2k_sh<2>(a, grid, stream);
+        case 4: return pair2k_sh<4>(a, grid, stream);
+        case 8: return pair2k_sh<8>(a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 template <int E>
 hipError_t fused_e(int s, const FusedArgs& a, int64_t grid, hipStream_t stream) {
     if constexpr (E >= 1) {
@@ -2140,6 +2345,23 @@ std::vector<float> build_pair512_twiddles() {
     return t;
 }
 
+std::vector<float> build_pair2k_twiddles() {
+    std::vector<float> t;
+    for (int k1 = 1; k1 < 16; ++k1)
+        for (int l = 0; l < 128; ++l) {
+            const double ph = -2.0 * M_PI * double(l * k1) / 2048.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    for (int k2 = 1; k2 < 16; ++k2)
+        for (int x = 0; x < 8; ++x) {
+            const double ph = -2.0 * M_PI * double(x * k2) / 128.0;
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
+    return t;
+}
+
 std::vector<float> build_pair4k_twiddles() {
     std::vector<float> t;
     for (int k1 = 1; k1 < 16; ++k1)
@@ -2206,6 +2428,8 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     const bool use_pair = g.n == 1024 && t.ptw && t.pden && fast;
 #endif
     const bool use_pair512 = g.n == 512 && t.ptw && t.pden && fast && g.h >= 128;
+    if (g.n == 2048 && t.ptw4 && t.pden4 && fast && (g.h == 256 || g.h == 512 || g.h == 1024))
+        return launch_pair2k(g, a, F, n_streams, stream);
 #ifdef CRLOT_OLD_CHUNKS  // A/B builds: fixed ~128-frame chunks
     const int target = 128;
     a.n_chunks = int((F + target - 1) / target);

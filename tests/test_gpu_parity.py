@@ -133,9 +133,10 @@ def test_fused_equals_staged_bit_exact(pkg, oracle, torch_cuda, n, h):
 
 @pytest.mark.parametrize("n,h,mode", [(1024, 256, 0), (1024, 128, 0), (1024, 512, 1), (1024, 1024, 0),
                                       (1024, 256, 1), (4096, 1024, 0), (4096, 512, 1), (4096, 2048, 0),
-                                      (512, 128, 0), (512, 256, 1), (512, 128, 1)])
+                                      (512, 128, 0), (512, 256, 1), (512, 128, 1),
+                                      (2048, 512, 0), (2048, 256, 1), (2048, 1024, 0)])
 def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
-    """K_pair / K_pair4k / K_pair512 (two frames per 1024- / 4096- / 512-point complex transform)
+    """K_pair / K_pair4k / K_pair512 / K_pair2k (two frames per 1024- / 4096- / 512- / 2048-point transform)
     against the oracle's per-frame kissfft chain and against the per-frame
     kernel, odd and even frame counts, every hop the kernels take."""
     torch = torch_cuda
@@ -153,7 +154,7 @@ def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
         assert not np.array_equal(bits(y), bits(yu))  # the pair kernel really ran
 
 
-@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128), (2048, 512)])
 def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch, n, h):
     """Pairs are aligned to even frames, so a stream's output bits do not depend on
     how its frames are chunked over waves nor on the batch it is processed in."""
@@ -172,7 +173,7 @@ def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkey
 
 
 @pytest.mark.parametrize("n,h,burst_hop", [(1024, 256, 82), (1024, 256, 83), (4096, 1024, 20), (4096, 1024, 21),
-                                           (512, 128, 150), (512, 128, 151)])
+                                           (512, 128, 150), (512, 128, 151), (2048, 512, 40), (2048, 512, 41)])
 def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, n, h, burst_hop, monkeypatch):
     """K_pair's unpaired regime: a hop of huge samples (1e25, beyond px_hi) makes
     the pairs that contain it transform each frame alone, as the reference does,
@@ -326,7 +327,7 @@ def test_windows_and_flags(pkg, oracle, torch_cuda):
                  host(plan.ola_gather(frames))[0], 0.5, "no-analysis y")
 
 
-@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128), (2048, 512)])
 def test_spectral_gain_hook(pkg, oracle, torch_cuda, n, h):
     """Per-bin gain between rfft and irfft vs a float64 model of the same chain;
     the frame-pair kernels (K_pair, K_pair4k) apply it per complex bin."""
