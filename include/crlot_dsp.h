@@ -104,7 +104,7 @@ int crlot_plan_set_spectral_gain(crlot_plan* plan, const float* gain);
  * (2j, 2j+1) of a stream share one complex FFT, z = frame_2j + i frame_2j+1,
  * whose real and imaginary round-trip outputs are the two frames' (exact for
  * the real, bin-symmetric spectral gain).  Used where those kernels exist
- * (N = 512, 1024, 4096 with the fused hop rules); a pair holding a NaN, Inf,
+ * (N = 512, 1024, 2048, 4096 with the fused hop rules); a pair holding a NaN, Inf,
  * huge or tiny sample is transformed frame by frame instead, so no frame's
  * overflow reaches its neighbour.  Results equal the per-frame kissfft
  * formulation within float32 rounding, not bit for bit, and do not depend on
