@@ -2134,10 +2134,11 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// K_pair: N = 1024, H = 64 * SH.  W waves per workgroup (16: one workgroup of
-// 155 KB LDS per CU, 4 waves/SIMD at <= 128 VGPRs).
+// K_pair: N = 1024, H = 64 * SH.  W waves per workgroup: with register twiddles
+// (default) 4, three 53 KB workgroups per CU at <= 168 VGPRs (3 waves/SIMD);
+// with LDS twiddles 16, one 160 KB workgroup per CU at <= 128 VGPRs.
 #ifndef CRLOT_PAIR_WAVES
-#define CRLOT_PAIR_WAVES (CRLOT_PAIR_REG_TW ? 12 : 16)
+#define CRLOT_PAIR_WAVES (CRLOT_PAIR_REG_TW ? 4 : 16)  // 3 workgroups of 4 waves per CU: +0.5..3.5 % over one of 12 (8 of 8 A/B runs)
 #endif
 constexpr int kPairWaves = CRLOT_PAIR_WAVES;
 
