@@ -824,7 +824,10 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 // lane l holding samples l + 64 m (m < 8); a hop is SH = H/64 floats per lane.
 // Same regimes, OLA order, divisions and store rules as K_pair; twiddles and
 // both windows in registers; one 4.6 KB LDS buffer per wave.
-constexpr int kP512Waves = 4;
+#ifndef CRLOT_P512_WAVES
+#define CRLOT_P512_WAVES 4  // 2 waves: same time; 8 waves: -2 % (A/B at 1024 x 480000, 512/128)
+#endif
+constexpr int kP512Waves = CRLOT_P512_WAVES;
 template <int SH, int NB, bool HAS_GAIN>
 __global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const FusedArgs a) {
     constexpr int E = 8, N = 512, H = 64 * SH;
@@ -2138,7 +2141,7 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
 // (default) 4, three 53 KB workgroups per CU at <= 168 VGPRs (3 waves/SIMD);
 // with LDS twiddles 16, one 160 KB workgroup per CU at <= 128 VGPRs.
 #ifndef CRLOT_PAIR_WAVES
-#define CRLOT_PAIR_WAVES (CRLOT_PAIR_REG_TW ? 4 : 16)  // 3 workgroups of 4 waves per CU: +0.5..3.5 % over one of 12 (8 of 8 A/B runs)
+#define CRLOT_PAIR_WAVES (CRLOT_PAIR_REG_TW ? 4 : 16)  // 3 workgroups of 4 waves per CU; one of 12 is within +-1.5 % (slot-controlled A/B), 2 or 6 waves lose 7-25 %
 #endif
 constexpr int kPairWaves = CRLOT_PAIR_WAVES;
 
