@@ -1,5 +1,6 @@
 """A/B timing of library variants (crlot-dsp_amd/variants/*.so) in ONE process,
-interleaved rounds (cdna_hip_programming.md 5.4 rule 24).  Each variant is
+interleaved rounds (cdna_hip_programming.md 5.4 rule 24), the
+order rotated every round so that no library always holds the first slot.  Each variant is
 loaded through its own ctypes handle; the workload is the headline one."""
 import ctypes as C
 import glob
@@ -44,8 +45,9 @@ for path in libs:
 
 stream = torch.cuda.current_stream()
 times = {p: [] for p in libs}
-for rnd in range(5):
-    for p in libs:
+for rnd in range(len(libs) * 2):
+    # rotate the order each round: the first slot of a round can run 2-4 % slow
+    for p in libs[rnd % len(libs):] + libs[:rnd % len(libs)]:
         L, h, y = handles[p], plans[p], ys[p]
         for _ in range(2):
             L.crlot_roundtrip(h, x.data_ptr(), y.data_ptr(), S, T, T, F * H, stream.cuda_stream)
