@@ -6,23 +6,37 @@
 Metric: Msamples/s of the batched STFT -> iSTFT -> OLA round trip at
 frame=1024 hop=256 batch=1024 (1024 synthetic mono streams x 480 000 samples
 of 48 kHz audio = 10 s each, per GPU), inputs and outputs resident in HBM.
-A "step" is one crlot_roundtrip over the whole batch.  N GPUs = N ranks, each
-with its own 1024 streams (weak scaling, no data-path collective: the streams
-are independent).
+A "step" is one crlot_roundtrip over the whole batch.
+
+Multi-GPU: one process per GPU.  `--gpus N` without an external
+launcher starts the N ranks itself (dist.launch: fresh child processes, the
+parent never touches the GPU).  Streams are independent, so there is no
+data-path collective; the control plane (start/stop barrier, max-over-ranks
+time) runs over RCCL when every rank owns a GPU, over gloo when ranks share one.
+Two phases are timed:
+  weak    (the headline `value`)  every rank runs its own 1024 streams;
+  strong  (BASELINE config 5)     8192 streams in total, rank r takes
+                                  dist.stream_range(8192, N, r).
+`value` = samples all ranks processed / the slowest rank's wall time.
 
 Besides the contract fields the JSON line carries
-  roofline      the fused kernel's algorithmic HBM bytes (8 B per sample: 4 in,
-                4 out) per launch / its average launch time, measured with HIP
-                events on the launch stream inside the timed region; traffic =
-                PMC HBM bytes per launch from profiles/ (separate rocprofv3 run)
-  compute       the same launches priced in FP32 VALU flops
+  roofline      the round-trip kernel's algorithmic HBM bytes (8 B per sample:
+                4 in, 4 out) per launch / its average launch time, measured with
+                HIP events on the launch stream inside the timed region; the
+                same launches priced in FP32 VALU flops (what bounds the kernel,
+                DESIGN.md section 5); traffic = PMC HBM bytes per launch from
+                profiles/*pmc_summary.json when that profile was taken of the
+                same kernel sources (src_hash), else null and flagged stale
   cpu_baseline  the oracle's C restatement of the reference CPU path (kissfft
                 algorithm + scalar-FMA OLA, "kind": "port") timed on this host,
-                rank 0 at N=1 only, on a bounded sample of streams.
+                rank 0 at N=1 only, on a bounded sample of streams, at the
+                host's CPU share and single-threaded.
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
 import subprocess
@@ -34,6 +48,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/s STFT->OLA round-trip, frame=1024 hop=256 batch=1024; HBM roofline %"
 N_FFT, HOP, STREAMS, T_LEN = 1024, 256, 1024, 480_000
+STRONG_STREAMS = 8192          # BASELINE config 5
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector peak (spec)
 BYTES_PER_SAMPLE = 8           # 4 B read + 4 B written
@@ -45,9 +60,29 @@ def flop_per_sample(n: int, h: int) -> float:
     return 2 * 2.5 * n * math.log2(n) / h + 6
 
 
-def cpu_baseline(n_streams: int = 1024, threads: int = 16):
+def src_hash() -> str:
+    """Hash of the kernel sources; a PMC profile applies only to the same hash."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "crlot-dsp_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def cpu_share() -> int:
+    """Threads this process may use: the pool's per-GPU share (OMP_NUM_THREADS on
+    the GPU box) or the affinity mask, never the whole machine's os.cpu_count()."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
+
+
+def cpu_baseline(n_streams: int = 1024):
     """Oracle restatement of the reference CPU path on this host (kind "port")."""
-    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     native = False
@@ -57,7 +92,7 @@ def cpu_baseline(n_streams: int = 1024, threads: int = 16):
         native = True
     except Exception:
         pass
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = cpu_share()
     x = O.synth_streams(n_streams, T_LEN, config_id=2)
     O.roundtrip_batch(x[:threads], N_FFT, HOP, nthreads=threads, native=native)  # warm-up
     t0 = time.perf_counter()
@@ -67,6 +102,7 @@ def cpu_baseline(n_streams: int = 1024, threads: int = 16):
     t1 = time.perf_counter()
     O.roundtrip_batch(x1, N_FFT, HOP, nthreads=1, native=native)
     dt1 = time.perf_counter() - t1
+    single = 4 * T_LEN / dt1 / 1e6
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -75,33 +111,77 @@ def cpu_baseline(n_streams: int = 1024, threads: int = 16):
                 break
     except OSError:
         pass
+    ncpu = os.cpu_count() or 1
     return {
         "value": round(n_streams * T_LEN / dt / 1e6, 3),
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{n_streams} of the 1024 streams x {T_LEN} samples (the N=1 workload), {threads} pthreads, "
+        "sample": f"{n_streams} of the 1024 streams x {T_LEN} samples (the N=1 workload) on "
+                  f"{threads} pthreads (this host's CPU share: OMP_NUM_THREADS / affinity), "
                   f"oracle/crlot_oracle.c -O3{' -march=native' if native else ''} "
-                  f"(kissfft-algorithm + scalar-FMA OLA restatement), {dt:.2f} s",
-        "single_thread_value": round(4 * T_LEN / dt1 / 1e6, 3),
+                  f"(kissfft-algorithm + scalar-FMA OLA restatement), {dt:.2f} s; "
+                  f"single thread on 4 streams, {dt1:.2f} s",
+        "single_thread_value": round(single, 3),
+        "host_cpus": ncpu,
+        "all_cpus_linear_bound": round(single * ncpu, 1),
+        "all_cpus_note": "single_thread_value x host_cpus: an upper bound assuming perfect "
+                         "scaling over every CPU of the machine (not measured: the pool "
+                         "grants one GPU a share of the host)",
         "cpu_model": cpu_model,
     }
 
 
-def load_pmc_traffic():
-    """HBM bytes per launch from the newest profiles/*pmc*.json (rocprofv3 --pmc run)."""
+def load_pmc_traffic(workload_key: str):
+    """HBM bytes per launch from the newest profiles/*pmc_summary.json of this
+    workload; null (stale) unless it was taken of the same kernel sources."""
     pdir = os.path.join(ROOT, "profiles")
-    best = None
-    if os.path.isdir(pdir):
-        for f in sorted(os.listdir(pdir)):
-            if f.endswith(".json") and "pmc" in f and not f.startswith("_"):
-                try:
-                    d = json.load(open(os.path.join(pdir, f)))
-                except Exception:
-                    continue
-                if d.get("workload_key") == f"{STREAMS}x{T_LEN}_N{N_FFT}_H{HOP}":
-                    best = d
-    return None if best is None else best.get("hbm_bytes_per_launch")
+    best, best_f = None, None
+    for f in sorted(glob.glob(os.path.join(pdir, "*pmc_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload_key") == workload_key:
+            best, best_f = d, f
+    if best is None:
+        return None, {"file": None, "stale": True, "note": "no PMC profile of this workload"}
+    cur = src_hash()
+    stale = best.get("src_hash") != cur
+    meta = {"file": os.path.relpath(best_f, ROOT), "kernel": best.get("kernel"),
+            "profile_src_hash": best.get("src_hash"), "src_hash": cur, "stale": stale,
+            "hbm_over_algorithmic": best.get("hbm_over_algorithmic")}
+    return (None if stale else best.get("hbm_bytes_per_launch")), meta
+
+
+def timed_phase(plan, x, y, steps: int, warmup: int, D, dev, torch):
+    """Warm-up, then `steps` round trips bracketed by barrier + synchronize;
+    returns (wall seconds max over ranks, mean kernel ms on the launch stream)."""
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(warmup):
+        plan.roundtrip(x, y)
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    D.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record(stream)
+        plan.roundtrip(x, y)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    D.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    return D.max_over_ranks(elapsed, dev), kern_ms
+
+
+def synth_device(torch, S: int, T: int, dev, seed: int):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.empty((S, T), dtype=torch.float32, device=dev)
+    x.uniform_(-0.5, 0.5, generator=g)
+    return x
 
 
 def main():
@@ -110,53 +190,65 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=50)  # ~130 ms: lets the clocks ramp
     ap.add_argument("--streams", type=int, default=STREAMS)
+    ap.add_argument("--strong-streams", type=int, default=STRONG_STREAMS)
+    ap.add_argument("--strong-steps", type=int, default=10)
+    ap.add_argument("--no-strong", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    import torch
     from __graft_entry__ import load_pkg, load_dist
-
     D = load_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: start the N ranks here, before any GPU call
+        sys.exit(D.launch(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+
+    import torch
+
     _, world, local = D.env_rank_world()
-    dev = torch.device("cuda", local if world > 1 else 0)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    n_dev = torch.cuda.device_count()
+    dev = torch.device("cuda", D.device_for(local, n_dev))
     torch.cuda.set_device(dev)
-    rank, world = D.init("nccl", dev)
+    shared = local_world > n_dev
+    rank, world = D.init("gloo" if shared else "nccl", dev)
 
     pkg = load_pkg()
     plan = pkg.Plan(frame_size=N_FFT, hop_size=HOP, device=dev.index)
     S, T = args.streams, T_LEN
-    g = torch.Generator(device=dev).manual_seed(0xC0FFEE + rank)
-    x = (torch.rand((S, T), generator=g, device=dev) * 2.0 - 1.0) * 0.5
     L = plan.output_length(T)
+
+    # ---- weak phase (headline): S streams per rank
+    x = synth_device(torch, S, T, dev, 0xC0FFEE + rank)
     y = torch.empty((S, L), dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-
-    for _ in range(args.warmup):
-        plan.roundtrip(x, y)
-    torch.cuda.synchronize(dev)
-
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    D.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        plan.roundtrip(x, y)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize(dev)
-    D.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    elapsed_max = D.max_over_ranks(elapsed, dev)
+    elapsed_max, kern_ms = timed_phase(plan, x, y, args.steps, args.warmup, D, dev, torch)
+    del x, y
 
     samples_step_rank = S * T
-    total_samples = samples_step_rank * world * args.steps
-    value = total_samples / elapsed_max / 1e6
+    value = samples_step_rank * world * args.steps / elapsed_max / 1e6
     achieved_gbs = BYTES_PER_SAMPLE * samples_step_rank / (kern_ms * 1e-3) / 1e9
     fps = flop_per_sample(N_FFT, HOP)
     achieved_tf = fps * samples_step_rank / (kern_ms * 1e-3) / 1e12
-    traffic = load_pmc_traffic()
+    traffic, traffic_meta = load_pmc_traffic(f"{S}x{T}_N{N_FFT}_H{HOP}")
+
+    # ---- strong phase (config 5): a fixed 8192-stream job sharded over the ranks
+    strong = None
+    if not args.no_strong and args.strong_streams > 0:
+        lo, hi = D.stream_range(args.strong_streams, world, rank)
+        xs = synth_device(torch, hi - lo, T, dev, 0x5EED0000 + lo)
+        ys = torch.empty((hi - lo, L), dtype=torch.float32, device=dev)
+        el_s, km_s = timed_phase(plan, xs, ys, args.strong_steps, 3, D, dev, torch)
+        del xs, ys
+        strong = {
+            "workload": f"{args.strong_streams} streams x {T} samples in total (BASELINE config 5), "
+                        f"rank r takes dist.stream_range({args.strong_streams}, {world}, r)",
+            "scaling": "strong",
+            "value": round(args.strong_streams * T * args.strong_steps / el_s / 1e6, 3),
+            "unit": "Msamples/s",
+            "steps": args.strong_steps,
+            "ms_per_step": round(el_s / args.strong_steps * 1e3, 4),
+            "streams_per_rank": [D.stream_range(args.strong_streams, world, r) for r in range(world)],
+            "rank0_kernel_ms": round(km_s, 4),
+        }
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -172,6 +264,7 @@ def main():
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
+            "devices": min(world, n_dev),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
@@ -189,24 +282,31 @@ def main():
                 "frame": N_FFT,
                 "hop": HOP,
                 "global_batch": S * world,
-                "parallelism": f"streams sharded over {world} rank(s), no collective",
+                "parallelism": f"streams sharded over {world} rank(s) on {min(world, n_dev)} device(s), "
+                               f"no data-path collective (control plane over "
+                               f"{'gloo' if shared else 'RCCL'})",
             },
             "roofline": {
-                "bound": "hbm",
+                "bound": "valu",
                 "achieved": round(achieved_gbs, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_meta,
                 "kernel_ms": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": BYTES_PER_SAMPLE * samples_step_rank,
+                "valu": {
+                    "flop_per_sample": round(fps, 1),
+                    "achieved_tflops": round(achieved_tf, 2),
+                    "peak_tflops": VALU_PEAK_TFLOPS,
+                    "frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
+                },
+                "note": "frac is the metric's HBM-roofline fraction (8 B/sample); the kernel "
+                        "is bound on the VALU issue (DESIGN.md section 5), valu.frac prices "
+                        "the same launches in SURVEY 8d flops",
             },
-            "compute": {
-                "flop_per_sample": round(fps, 1),
-                "achieved_tflops": round(achieved_tf, 2),
-                "peak_tflops": VALU_PEAK_TFLOPS,
-                "frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
-            },
+            "strong_scaling": strong,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

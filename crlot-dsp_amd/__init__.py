@@ -87,6 +87,8 @@ def lib():
         "crlot_plan_destroy": ([vp], None),
         "crlot_plan_upload_tables": ([vp, vp, vp], C.c_int),
         "crlot_plan_set_spectral_gain": ([vp, vp], C.c_int),
+        "crlot_plan_upload_tables_async": ([vp, vp, vp, vp], C.c_int),
+        "crlot_plan_set_spectral_gain_async": ([vp, vp, vp], C.c_int),
         "crlot_plan_set_frame_pairing": ([vp, i32], C.c_int),
         "crlot_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "crlot_frame_count": ([vp, i64], i64),
@@ -263,11 +265,18 @@ class Plan:
     def reserve(self, nbytes: int):
         _check(lib().crlot_plan_reserve(self._h, nbytes))
 
+    def _cur_stream(self) -> int:
+        torch = _torch()
+        dev = self.cfg.device if self.cfg.device >= 0 else torch.cuda.current_device()
+        return int(torch.cuda.current_stream(dev).cuda_stream)
+
     def upload_tables(self, window=None, norm=None):
+        """Replace window / norm, ordered on the current torch stream."""
         w = None if window is None else np.ascontiguousarray(window, np.float32)
         nm = None if norm is None else np.ascontiguousarray(norm, np.float32)
-        _check(lib().crlot_plan_upload_tables(self._h, None if w is None else w.ctypes.data,
-                                              None if nm is None else nm.ctypes.data))
+        _check(lib().crlot_plan_upload_tables_async(self._h, None if w is None else w.ctypes.data,
+                                                    None if nm is None else nm.ctypes.data,
+                                                    self._cur_stream()))
 
     def set_frame_pairing(self, enable: bool = True):
         """Two frames per complex transform on the fused round trip (default);
@@ -278,7 +287,8 @@ class Plan:
         g = None if gain is None else np.ascontiguousarray(gain, np.float32)
         if g is not None and g.size != self.frame_size // 2 + 1:
             raise ValueError("gain needs N/2+1 bins")
-        _check(lib().crlot_plan_set_spectral_gain(self._h, None if g is None else g.ctypes.data))
+        _check(lib().crlot_plan_set_spectral_gain_async(self._h, None if g is None else g.ctypes.data,
+                                                        self._cur_stream()))
 
     # -- hot path
     def roundtrip(self, x, y=None, stream: int | None = None):

@@ -49,6 +49,12 @@ struct crlot_plan {
     // staged-path workspace
     float* d_work = nullptr;
     int64_t work_bytes = 0;
+    // pinned staging of table uploads (stream-ordered: hipMemcpyAsync on the
+    // caller's stream; the event guards the staging memory until the copies ran)
+    char* h_stage = nullptr;
+    size_t stage_bytes = 0;
+    hipEvent_t stage_ev = nullptr;
+    bool stage_pending = false;
 };
 
 namespace {
@@ -115,11 +121,62 @@ void free_plan(crlot_plan* p) {
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
                      p->d_rden, p->d_twany_own, p->d_ptw, p->d_pden})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
+    if (p->stage_pending) (void)hipEventSynchronize(p->stage_ev);
+    if (p->stage_ev) (void)hipEventDestroy(p->stage_ev);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
     delete p;
 }
 
-// Upload window-derived tables: analysis window, synthesis window, den.
-int upload_window_tables(crlot_plan* p) {
+// A batch of host -> device table copies, ordered on one stream.  The host
+// data is staged in the plan's pinned buffer so the copies are truly
+// asynchronous; a later batch first waits for the previous one's copies.
+class Upload {
+   public:
+    explicit Upload(crlot_plan* p) : p_(p) {}
+    void add(void* dst, const void* src, size_t bytes) {
+        items_.push_back({dst, data_.size(), bytes});
+        const char* c = static_cast<const char*>(src);
+        data_.insert(data_.end(), c, c + bytes);
+    }
+    hipError_t submit(hipStream_t s) {
+        hipError_t e;
+        if (p_->stage_pending) {
+            if ((e = hipEventSynchronize(p_->stage_ev)) != hipSuccess) return e;
+            p_->stage_pending = false;
+        }
+        if (!p_->stage_ev && (e = hipEventCreateWithFlags(&p_->stage_ev, hipEventDisableTiming)) != hipSuccess)
+            return e;
+        if (data_.size() > p_->stage_bytes) {
+            if (p_->h_stage) (void)hipHostFree(p_->h_stage);
+            p_->h_stage = nullptr;
+            p_->stage_bytes = 0;
+            if ((e = hipHostMalloc(reinterpret_cast<void**>(&p_->h_stage), data_.size())) != hipSuccess)
+                return e;
+            p_->stage_bytes = data_.size();
+        }
+        if (!data_.empty()) std::memcpy(p_->h_stage, data_.data(), data_.size());
+        for (const Item& it : items_)
+            if ((e = hipMemcpyAsync(it.dst, p_->h_stage + it.off, it.bytes, hipMemcpyHostToDevice, s)) !=
+                hipSuccess)
+                return e;
+        if ((e = hipEventRecord(p_->stage_ev, s)) != hipSuccess) return e;
+        p_->stage_pending = true;
+        return hipSuccess;
+    }
+
+   private:
+    struct Item {
+        void* dst;
+        size_t off, bytes;
+    };
+    crlot_plan* p_;
+    std::vector<Item> items_;
+    std::vector<char> data_;
+};
+
+// Upload window-derived tables: analysis window, synthesis window, den, ordered
+// on `s` (kernels enqueued on `s` before this call still read the old tables).
+int upload_window_tables(crlot_plan* p, hipStream_t s) {
     const int n = p->geo.n;
     std::vector<float> ones(n, 1.0f);
     const std::vector<float>& wa = p->desc.analysis_window ? p->window : ones;
@@ -154,6 +211,7 @@ int upload_window_tables(crlot_plan* p) {
     }
     p->px_lo = wmin > 0.0 ? std::nextafter(float(double(1e-30f) / wmin * (1.0 + 0x1p-20)), INFINITY) : 0.0f;
     p->px_hi = float(0x1p64 / std::max(1.0, wmax));
+    Upload up(p);
     if (p->d_pden) {  // [block][lane][den SH | rden SH], den at block offset lane + lanes q
         const int h = p->geo.h, lanes = p->geo.n == 4096 ? 256 : p->geo.n == 2048 ? 128 : 64, sh = h / lanes;
         const int blocks = int(den.size()) / h;
@@ -165,16 +223,15 @@ int upload_window_tables(crlot_plan* p) {
                     pd[at + q] = den[size_t(b) * h + l + lanes * q];
                     pd[at + sh + q] = rden[size_t(b) * h + l + lanes * q];
                 }
-        hipError_t e = hipMemcpy(p->d_pden, pd.data(), sizeof(float) * pd.size(), hipMemcpyHostToDevice);
-        if (e != hipSuccess) return hip_fail(e, "hipMemcpy(pair den)");
+        up.add(p->d_pden, pd.data(), sizeof(float) * pd.size());
     }
-    hipError_t e;
-    if ((e = hipMemcpy(p->d_wa, wa.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(p->d_ws, ws.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(p->d_den, den.data(), sizeof(float) * den.size(), hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(p->d_wsn, wsn.data(), sizeof(float) * n, hipMemcpyHostToDevice)) ||
-        (e = hipMemcpy(p->d_rden, rden.data(), sizeof(float) * den.size(), hipMemcpyHostToDevice)))
-        return hip_fail(e, "hipMemcpy(tables)");
+    up.add(p->d_wa, wa.data(), sizeof(float) * n);
+    up.add(p->d_ws, ws.data(), sizeof(float) * n);
+    up.add(p->d_den, den.data(), sizeof(float) * den.size());
+    up.add(p->d_wsn, wsn.data(), sizeof(float) * n);
+    up.add(p->d_rden, rden.data(), sizeof(float) * den.size());
+    hipError_t e = up.submit(s);
+    if (e != hipSuccess) return hip_fail(e, "table upload");
     p->fast_ok = ok;
     return CRLOT_OK;
 }
@@ -326,7 +383,9 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         free_plan(p);
         return hip_fail(e, "hipMemcpy(twiddles)");
     }
-    rc = upload_window_tables(p);
+    // no kernel reads this plan's tables yet: the null stream, then wait
+    rc = upload_window_tables(p, nullptr);
+    if (rc == CRLOT_OK && (e = hipStreamSynchronize(nullptr)) != hipSuccess) rc = hip_fail(e, "table upload");
     if (rc != CRLOT_OK) {
         free_plan(p);
         return rc;
@@ -337,7 +396,7 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
 
 void crlot_plan_destroy(crlot_plan* plan) { free_plan(plan); }
 
-int crlot_plan_upload_tables(crlot_plan* p, const float* window, const float* norm) {
+int crlot_plan_upload_tables_async(crlot_plan* p, const float* window, const float* norm, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     DeviceGuard g(p->device);
     if (window) std::memcpy(p->window.data(), window, sizeof(float) * p->window.size());
@@ -348,10 +407,26 @@ int crlot_plan_upload_tables(crlot_plan* p, const float* window, const float* no
         crlot_norm_table(p->window.data(), p->geo.n, p->geo.h, p->geo.ring_len,
                          p->desc.apply_window_inside, p->desc.eps, p->norm.data());
     }
-    return upload_window_tables(p);
+    return upload_window_tables(p, static_cast<hipStream_t>(stream));
 }
 
-int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
+// The stream-less entries cannot know which stream still reads the tables:
+// drain the device first, copy, and wait for the copies.
+static int sync_upload(crlot_plan* p, int rc_of_async) {
+    if (rc_of_async != CRLOT_OK) return rc_of_async;
+    hipError_t e = hipStreamSynchronize(nullptr);
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "table upload");
+}
+
+int crlot_plan_upload_tables(crlot_plan* p, const float* window, const float* norm) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    DeviceGuard g(p->device);
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+    return sync_upload(p, crlot_plan_upload_tables_async(p, window, norm, nullptr));
+}
+
+int crlot_plan_set_spectral_gain_async(crlot_plan* p, const float* gain, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     DeviceGuard g(p->device);
     if (!gain) {
@@ -359,13 +434,23 @@ int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
         return CRLOT_OK;
     }
     const int bins = p->geo.n / 2 + 1;
-    hipError_t e = hipMemcpy(p->d_gain, gain, sizeof(float) * bins, hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpy(gain)");
+    Upload up(p);
+    up.add(p->d_gain, gain, sizeof(float) * bins);
+    hipError_t e = up.submit(static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "gain upload");
     p->has_gain = true;
     float gm = 0.0f;
     for (int i = 0; i < bins; ++i) gm = std::isnan(gain[i]) ? INFINITY : std::max(gm, std::fabs(gain[i]));
     p->gain_max = gm;
     return CRLOT_OK;
+}
+
+int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    DeviceGuard g(p->device);
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+    return sync_upload(p, crlot_plan_set_spectral_gain_async(p, gain, nullptr));
 }
 
 int crlot_plan_set_frame_pairing(crlot_plan* p, int32_t enable) {
@@ -700,7 +785,8 @@ void crlot_stream_destroy(crlot_stream* st) {
 int crlot_stream_reset(crlot_stream* st) {
     if (!st) return fail(CRLOT_EINVAL, "null stream");
     DeviceGuard g(st->plan->device);
-    hipError_t e;
+    hipError_t e = hipDeviceSynchronize();  // a hop still in flight reads the state
+    if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
     if ((e = hipMemset(st->d_hist, 0, sizeof(float) * st->hist_floats)) ||
         (e = hipMemset(st->d_acc, 0, sizeof(float) * st->acc_floats)))
         return hip_fail(e, "hipMemset(stream state)");

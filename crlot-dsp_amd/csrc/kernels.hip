@@ -2205,14 +2205,26 @@ hipError_t pair2k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     return hipGetLastError();
 }
 void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m);
+// CRLOT_CHUNKS (tuning override: chunks per stream), read once per process so
+// the launch path does no environment lookups.
+int chunks_env() {
+    static const int v = [] {
+        const char* e = std::getenv("CRLOT_CHUNKS");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+void chunk_override(int64_t F, FusedArgs& a) {
+    const int c = chunks_env();
+    if (c <= 0) return;
+    const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, c));
+    a.M = int((F + n - 1) / n);
+    a.n_chunks = int((F + a.M - 1) / a.M);
+}
 int fused_resident_waves();
 hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_streams, hipStream_t stream) {
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 4, a.n_chunks, a.M);
-    if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
-        const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
-        a.M = int((F + n - 1) / n);
-        a.n_chunks = int((F + a.M - 1) / a.M);
-    }
+    chunk_override(F, a);
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
     a.pad_mode = g.pad_mode;
@@ -2449,11 +2461,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
                              a.n_chunks, a.M);
     else
         choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
-    if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
-        const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
-        a.M = int((F + n - 1) / n);
-        a.n_chunks = int((F + a.M - 1) / a.M);
-    }
+    chunk_override(F, a);
 #endif
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
@@ -2548,11 +2556,7 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
     if (g.n == 4096 && t.ptw4 && t.pden4 && t.wsn && t.rden && (g.h == 512 || g.h == 1024 || g.h == 2048)) {
         // K_pair4k: whole resident rounds of workgroups (two per CU)
         choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 2, a.n_chunks, a.M);
-        if (const char* ev = std::getenv("CRLOT_CHUNKS")) {  // tuning override: chunks per stream
-            const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, std::atoi(ev)));
-            a.M = int((F + n - 1) / n);
-            a.n_chunks = int((F + a.M - 1) / a.M);
-        }
+        chunk_override(F, a);
         const int64_t grid4 = int64_t(n_streams) * a.n_chunks;
         switch (g.h / 256) {
             case 2: return pair4k_sh<2>(a, grid4, stream);

@@ -2,11 +2,23 @@
 
 The round trip has no exchange step (streams are independent), so
 the only collectives are the start/stop barrier and the max-over-ranks timing
-reduction.  Backend "nccl" (= RCCL on ROCm) on GPUs, "gloo" for CPU tests.
+reduction -- control plane, never data.  Backend "nccl" (= RCCL on ROCm) when
+every rank owns its own GPU; "gloo" for CPU tests and for several ranks that
+share one device (RCCL rejects two ranks on one GPU).
+
+launch(n, argv) starts n ranks of a script as fresh child processes (the
+torch.distributed.run environment contract: RANK, LOCAL_RANK, WORLD_SIZE,
+MASTER_ADDR=127.0.0.1, MASTER_PORT), so `bench.py --gpus N` works without an
+external launcher.  The parent never touches the GPU.
 """
 from __future__ import annotations
 
 import os
+import socket
+import subprocess
+import sys
+
+_backend = None
 
 
 def env_rank_world():
@@ -14,12 +26,20 @@ def env_rank_world():
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def device_for(local_rank: int, n_devices: int) -> int:
+    """Device ordinal of a local rank: one rank per GPU, round-robin when there
+    are more ranks than GPUs (rehearsal of the N-rank path on a 1-GPU box)."""
+    return local_rank % max(1, n_devices)
+
+
 def init(backend: str, device=None):
+    global _backend
     import torch.distributed as dist
     rank, world, _ = env_rank_world()
     if world > 1 and not dist.is_initialized():
         kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
         dist.init_process_group(backend, **kw)
+    _backend = backend
     return rank, world
 
 
@@ -41,7 +61,8 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return float(value)
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    on_dev = _backend == "nccl" and device is not None
+    t = torch.tensor([value], dtype=torch.float64, device=device if on_dev else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -50,3 +71,36 @@ def finalize():
     import torch.distributed as dist
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(n: int, argv: list[str], timeout: float | None = None) -> int:
+    """Run `python argv...` as n ranks on this node; returns the worst exit code.
+
+    Children are fresh processes started before anything in this process has
+    touched the GPU (no exec from a GPU-initialised process)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
+               WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable] + argv, env=e))
+    rc = 0
+    try:
+        for p in procs:
+            code = p.wait(timeout=timeout)
+            if code != 0 and rc == 0:
+                rc = code
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc

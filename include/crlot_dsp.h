@@ -100,6 +100,15 @@ int crlot_plan_upload_tables(crlot_plan* plan, const float* window, const float*
 /* Spectral hook between rfft and irfft: real per-bin gain, N/2+1 host floats;
  * NULL restores the identity step of the reference (e2e_benchmark.cc:161-162). */
 int crlot_plan_set_spectral_gain(crlot_plan* plan, const float* gain);
+/* Stream-ordered forms of the two table updates: the host data is staged in
+ * pinned memory and copied with hipMemcpyAsync on `stream`, so work enqueued on
+ * `stream` before the call sees the old tables and work after it the new ones
+ * (the host arrays may be reused as soon as the call returns).  The stream-less
+ * entries above first drain the device (hipDeviceSynchronize), so a round trip
+ * in flight on any stream never reads a half-updated table. */
+int crlot_plan_upload_tables_async(crlot_plan* plan, const float* window, const float* norm,
+                                   void* stream);
+int crlot_plan_set_spectral_gain_async(crlot_plan* plan, const float* gain, void* stream);
 /* Frame pairing on the fused round trip (default on): two consecutive frames
  * (2j, 2j+1) of a stream share one complex FFT, z = frame_2j + i frame_2j+1,
  * whose real and imaginary round-trip outputs are the two frames' (exact for

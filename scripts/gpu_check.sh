@@ -27,13 +27,16 @@ if [[ $MODE == sel ]]; then  # sel "<pytest -k expr>": selected GPU tests, then 
   step bench 600 python bench.py --no-cpu-baseline
 fi
 if [[ $MODE == all || $MODE == test ]]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread
 fi
 if [[ $MODE == all || $MODE == smoke ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
   step bench 600 python bench.py
+fi
+if [[ $MODE == all || $MODE == bench2 ]]; then  # the N-rank path through bench.py's own launcher
+  step bench2 600 python bench.py --gpus 2 --no-cpu-baseline
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline

@@ -15,6 +15,9 @@ import os
 import shutil
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import src_hash  # noqa: E402
+
 tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 src = f"gpurun_out/prof_{tag}"
 os.makedirs("profiles", exist_ok=True)
@@ -76,6 +79,7 @@ out = {
     "tag": tag,
     "workload_key": f"{S}x{T}_N{N}_H{H}",
     "kernel": kname,
+    "src_hash": src_hash(),
     "median_duration_ns_trace": med,
     "min_duration_ns_trace": mn,
     "avg_duration_ns_trace": dur,
