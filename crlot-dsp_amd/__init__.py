@@ -55,6 +55,20 @@ class PlanDesc(C.Structure):
     ]
 
 
+class OlaConfigC(C.Structure):
+    """crlot_ola_config (include/crlot_dsp.h) = dsp::OLAConfig + device."""
+    _fields_ = [
+        ("sample_rate", C.c_int32),
+        ("frame_size", C.c_int64),
+        ("hop_size", C.c_int64),
+        ("channels", C.c_int64),
+        ("eps", C.c_float),
+        ("apply_window_inside", C.c_int32),
+        ("shadow_ring", C.c_int32),
+        ("device", C.c_int32),
+    ]
+
+
 class FftDesc(C.Structure):
     """crlot_fft_desc (include/crlot_dsp.h)."""
     _fields_ = [("domain", C.c_int32), ("nfft", C.c_int32), ("device", C.c_int32)]
@@ -122,6 +136,31 @@ def lib():
                                    C.POINTER(vp)], C.c_int),
         "crlot_wav_writer_write": ([vp, fp, C.c_uint64, C.POINTER(C.c_uint64)], C.c_int),
         "crlot_wav_writer_close": ([vp], C.c_int),
+        "crlot_framer_create": ([C.POINTER(vp)], C.c_int),
+        "crlot_framer_destroy": ([vp], None),
+        "crlot_framer_set_params": ([vp, i64, i64, i64, i32], C.c_int),
+        "crlot_framer_push": ([vp, vp, i64], C.c_int),
+        "crlot_framer_pop": ([vp, vp], C.c_int),
+        "crlot_framer_available": ([vp], i64),
+        "crlot_framer_reset": ([vp], C.c_int),
+        "crlot_framer_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i32),
+                               C.POINTER(i64)], C.c_int),
+        "crlot_ola_create": ([C.POINTER(OlaConfigC), C.POINTER(vp)], C.c_int),
+        "crlot_ola_destroy": ([vp], None),
+        "crlot_ola_set_window": ([vp, vp, i32], C.c_int),
+        "crlot_ola_add_frame_soa": ([vp, vp, vp, i64, i64, i64, f32], C.c_int),
+        "crlot_ola_push_frame_aos": ([vp, vp, vp, i64, i64, i64, f32], C.c_int),
+        "crlot_ola_produce": ([vp, vp, i64, C.POINTER(i64)], C.c_int),
+        "crlot_ola_add_frame_soa_device": ([vp, vp, i64, vp, i64, i64, i64, f32, vp], C.c_int),
+        "crlot_ola_push_frame_aos_device": ([vp, vp, vp, i64, i64, i64, f32, vp], C.c_int),
+        "crlot_ola_produce_device": ([vp, vp, i64, i64, C.POINTER(i64), vp], C.c_int),
+        "crlot_ola_flush": ([vp], C.c_int),
+        "crlot_ola_reset": ([vp], C.c_int),
+        "crlot_ola_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i32)],
+                           C.c_int),
+        "crlot_ola_meter_peak": ([vp, C.POINTER(f32)], C.c_int),
+        "crlot_ola_norm_table": ([vp, fp], C.c_int),
+        "crlot_ola_synchronize": ([vp], C.c_int),
         "crlot_window_table": ([i32, i64, i32, i32, fp], C.c_int),
         "crlot_ring_len": ([i64, i64], i64),
         "crlot_norm_table": ([fp, i64, i64, i64, i32, f32, fp], C.c_int),
@@ -473,6 +512,236 @@ class Stream:
         _check(lib().crlot_stream_push_hop(self._h, hop.data_ptr(), out.data_ptr(), C.byref(em), s),
                "crlot_stream_push_hop")
         return out, em.value
+
+
+# ----------------------------------------------------------------- Framer / OLAAccumulator
+class Framer:
+    """dsp::Framer (framer.h:26-127): host object, interleaved PCM in, frames out.
+    set_params raises ValueError (std::invalid_argument) on zero sizes; push/pop
+    return the reference's bools."""
+
+    def __init__(self):
+        h = C.c_void_p()
+        _check(lib().crlot_framer_create(C.byref(h)), "crlot_framer_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().crlot_framer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def set_params(self, frame_size: int, hop_size: int, channels: int = 1,
+                   boundary_mode: int = ZERO_PAD):
+        _check(lib().crlot_framer_set_params(self._h, frame_size, hop_size, channels,
+                                             boundary_mode), "set_params")
+
+    def push(self, interleaved, frames: int | None = None) -> bool:
+        if interleaved is None:
+            return bool(_check(lib().crlot_framer_push(self._h, None, frames or 0)))
+        a = np.ascontiguousarray(interleaved, np.float32).reshape(-1)
+        ch = self.channels()
+        frames = a.size // ch if frames is None else frames
+        if frames * ch > a.size:
+            raise ValueError("push: fewer samples than frames * channels")
+        return bool(_check(lib().crlot_framer_push(self._h, a.ctypes.data if a.size else None,
+                                                   frames)))
+
+    def pop(self, out: np.ndarray | None = None):
+        """Next frame (frame_size*channels floats) or None when none is available."""
+        n, ch = self.frame_size(), self.channels()
+        buf = np.empty(max(1, n * ch), np.float32) if out is None else out
+        ok = _check(lib().crlot_framer_pop(self._h, buf.ctypes.data))
+        return buf[:n * ch] if ok else None
+
+    def available_frames(self) -> int:
+        return _check(int(lib().crlot_framer_available(self._h)))
+
+    def reset(self):
+        _check(lib().crlot_framer_reset(self._h))
+
+    def _info(self):
+        n, h, c, b = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        m = C.c_int32()
+        _check(lib().crlot_framer_info(self._h, C.byref(n), C.byref(h), C.byref(c), C.byref(m),
+                                       C.byref(b)))
+        return n.value, h.value, c.value, m.value, b.value
+
+    def frame_size(self) -> int:
+        return self._info()[0]
+
+    def hop_size(self) -> int:
+        return self._info()[1]
+
+    def channels(self) -> int:
+        return self._info()[2]
+
+    def boundary_mode(self) -> int:
+        return self._info()[3]
+
+    def buffer_size(self) -> int:
+        return self._info()[4]
+
+
+@dataclass
+class OLAConfig:
+    """dsp::OLAConfig (OLAAccumulator.h:15-29)."""
+    sample_rate: int = 48000
+    frame_size: int = 1024
+    hop_size: int = 256
+    channels: int = 1
+    eps: float = 1e-8
+    apply_window_inside: bool = True
+    shadow_ring: bool = False
+    device: int = -1
+
+    def isValid(self) -> bool:  # noqa: N802 (reference name)
+        return (self.sample_rate > 0 and self.frame_size > 0 and self.hop_size > 0
+                and self.channels > 0 and self.eps > 0.0)
+
+
+class OLAAccumulator:
+    """dsp::OLAAccumulator (OLAAccumulator.h:63-217) with its rings on the device.
+
+    Host forms take numpy arrays (the reference's pointers); *_device forms take
+    float32 CUDA tensors and run on the current torch stream."""
+
+    def __init__(self, cfg: OLAConfig):
+        self.cfg = cfg
+        self._h = None
+        c = OlaConfigC(cfg.sample_rate, cfg.frame_size, cfg.hop_size, cfg.channels, cfg.eps,
+                       int(cfg.apply_window_inside), int(cfg.shadow_ring), cfg.device)
+        h = C.c_void_p()
+        _check(lib().crlot_ola_create(C.byref(c), C.byref(h)), "OLAAccumulator")
+        self._h = h
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().crlot_ola_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def config(self) -> OLAConfig:
+        return self.cfg
+
+    def set_window(self, w, wlen: int | None = None):
+        if w is None:
+            _check(lib().crlot_ola_set_window(self._h, None, wlen or 0), "set_window")
+            return
+        a = np.ascontiguousarray(w, np.float32)
+        _check(lib().crlot_ola_set_window(self._h, a.ctypes.data, a.size if wlen is None else wlen),
+               "set_window")
+
+    @staticmethod
+    def _win(window):
+        if window is None:
+            return None, None
+        a = np.ascontiguousarray(window, np.float32)
+        return a, a.ctypes.data
+
+    def add_frame_SoA(self, ch_frames, window, start_sample: int, start_off: int, size: int,  # noqa: N802
+                      gain: float = 1.0):
+        """ch_frames: sequence of per-channel arrays (None entries allowed, as null pointers)."""
+        if ch_frames is None:
+            _check(lib().crlot_ola_add_frame_soa(self._h, None, None, start_sample, start_off,
+                                                 size, gain), "add_frame_SoA")
+            return
+        arrs = [None if f is None else np.ascontiguousarray(f, np.float32) for f in ch_frames]
+        ptrs = (C.c_void_p * max(1, len(arrs)))(*[None if a is None else a.ctypes.data for a in arrs])
+        wa, wp = self._win(window)
+        _check(lib().crlot_ola_add_frame_soa(self._h, ptrs, wp, start_sample, start_off, size, gain),
+               "add_frame_SoA")
+
+    def push_frame_AoS(self, interleaved, window, start_sample: int, start_off: int, size: int,  # noqa: N802
+                       gain: float = 1.0):
+        a = None if interleaved is None else np.ascontiguousarray(interleaved, np.float32)
+        wa, wp = self._win(window)
+        _check(lib().crlot_ola_push_frame_aos(self._h, None if a is None else a.ctypes.data, wp,
+                                              start_sample, start_off, size, gain),
+               "push_frame_AoS")
+
+    def produce(self, n: int, out=None):
+        """Returns (count, [per-channel arrays of n floats]); out may be given
+        as a list of float32 arrays (their tails beyond count stay untouched)."""
+        ch = self.cfg.channels
+        if out is None:
+            out = [np.zeros(max(n, 1), np.float32) for _ in range(ch)]
+        ptrs = (C.c_void_p * max(1, ch))(*[None if o is None else o.ctypes.data for o in out])
+        got = C.c_int64()
+        _check(lib().crlot_ola_produce(self._h, ptrs, n, C.byref(got)), "produce")
+        return got.value, out
+
+    # -- device forms (float32 CUDA tensors, current torch stream)
+    def add_frame_SoA_device(self, frames, window, start_sample: int, start_off: int, size: int,  # noqa: N802
+                             gain: float = 1.0):
+        """frames: (channels, >= frame_size) tensor, rows contiguous."""
+        ld = _ld(frames, 0, frames.shape[-1]) if frames.dim() == 2 else frames.shape[-1]
+        _check(lib().crlot_ola_add_frame_soa_device(
+            self._h, frames.data_ptr(), ld, None if window is None else window.data_ptr(),
+            start_sample, start_off, size, gain, _stream_handle(frames)), "add_frame_SoA_device")
+
+    def push_frame_AoS_device(self, interleaved, window, start_sample: int, start_off: int,  # noqa: N802
+                              size: int, gain: float = 1.0):
+        _check(lib().crlot_ola_push_frame_aos_device(
+            self._h, interleaved.data_ptr(), None if window is None else window.data_ptr(),
+            start_sample, start_off, size, gain, _stream_handle(interleaved)),
+            "push_frame_AoS_device")
+
+    def produce_device(self, out, n: int) -> int:
+        """out: (channels, >= n) tensor; returns the samples provided."""
+        got = C.c_int64()
+        ld = _ld(out, 0, out.shape[-1]) if out.dim() == 2 else out.shape[-1]
+        _check(lib().crlot_ola_produce_device(self._h, out.data_ptr(), ld, n, C.byref(got),
+                                              _stream_handle(out)), "produce_device")
+        return got.value
+
+    def flush(self):
+        _check(lib().crlot_ola_flush(self._h))
+
+    def reset(self):
+        _check(lib().crlot_ola_reset(self._h))
+
+    def synchronize(self):
+        _check(lib().crlot_ola_synchronize(self._h))
+
+    def _info(self):
+        p, r, rs = C.c_int64(), C.c_int64(), C.c_int64()
+        hw = C.c_int32()
+        _check(lib().crlot_ola_info(self._h, C.byref(p), C.byref(r), C.byref(rs), C.byref(hw)))
+        return p.value, r.value, rs.value, bool(hw.value)
+
+    def produced_samples(self) -> int:
+        return self._info()[0]
+
+    def read_pos(self) -> int:
+        return self._info()[1]
+
+    def ring_size(self) -> int:
+        return self._info()[2]
+
+    def has_window(self) -> bool:
+        return self._info()[3]
+
+    def meter_peak(self) -> float:
+        v = C.c_float()
+        _check(lib().crlot_ola_meter_peak(self._h, C.byref(v)))
+        return v.value
+
+    def norm(self) -> np.ndarray:
+        out = np.zeros(self.ring_size(), np.float32)
+        _check(lib().crlot_ola_norm_table(self._h, _fptr(out)))
+        return out
 
 
 # ----------------------------------------------------------------- WAV I/O

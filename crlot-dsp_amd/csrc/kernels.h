@@ -127,4 +127,16 @@ hipError_t launch_cfft(const Geometry& g, const DevTables& t, const float* in, f
                        int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, bool inverse,
                        hipStream_t stream);
 
+// OLAAccumulator object (ola.hip): ring [C][R], den [R].  add: source element
+// (c, j) at src[c*cs + j*js], window win[j] or nullptr, ring position
+// (start + j) mod R for j < len <= R.  produce: out[c*ldo + j] = ring / den at
+// (rp + j) mod R, j < len, ring cleared; peak (nullable) = running max |out|
+// over channel 0's first n_total samples, as float bits.
+hipError_t launch_ola_add(float* ring, int channels, int64_t R, const float* src, int64_t cs,
+                          int64_t js, const float* win, int64_t start, int64_t len, float gain,
+                          hipStream_t s);
+hipError_t launch_ola_produce(float* ring, int channels, int64_t R, const float* den, float* out,
+                              int64_t ldo, int64_t rp, int64_t len, int64_t n_total, unsigned* peak,
+                              hipStream_t s);
+
 }  // namespace crlot

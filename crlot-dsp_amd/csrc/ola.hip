@@ -1,0 +1,106 @@
+// ola.hip -- device arithmetic of the OLAAccumulator object (crlot_ola_*, objects.cpp).
+//
+// The object keeps the reference's ring per channel in HBM, [C][R] floats
+// (R = ring_len), plus den[R] = (norm > eps ? norm : eps).  The host side runs
+// the reference's state machine (read_pos_, produced_, flush, reset:
+// OLAAccumulator.cc:54-247); these kernels do the per-sample work of one call:
+//
+//   k_ola_add      add_frame_SoA / push_frame_AoS after clamping
+//                  (OLAAccumulator.cc:54-160): ring[c][(start + j) mod R] =
+//                  fma(fma(src, w, 0), g, ring) with a window, fma(src, g, ring)
+//                  without (kernels.cc:18-28, the scalar forms Highway matches);
+//                  source element (c, j) at src[c*cs + j*js], so the same
+//                  kernel reads SoA frames (cs = ld, js = 1) and interleaved
+//                  AoS frames (cs = 1, js = C: aos_to_soa.cc:7-18 fused away).
+//   k_ola_produce  produce (OLAAccumulator.cc:162-221) -> normalize_and_clear
+//                  (kernels.cc:30-36): out = ring / den (IEEE division), ring = 0,
+//                  and the channel-0 peak meter (:289-295) as a running maximum
+//                  of |out| kept in device memory (NaN never raises it, as with
+//                  std::max(peak, NaN)).
+//
+// A call touches each ring position at most once (len <= R), so threads never
+// race; calls are ordered by the stream.  One thread per (sample, channel):
+// these are tiny HBM/L2-resident launches whose cost is the launch itself.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace crlot {
+namespace {
+
+__global__ void __launch_bounds__(256) k_ola_add(float* __restrict__ ring, int64_t R,
+                                                 const float* __restrict__ src, int64_t cs,
+                                                 int64_t js, const float* __restrict__ win,
+                                                 int64_t start, int64_t len, float gain) {
+    const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t c = blockIdx.y;
+    if (j >= len) return;
+    int64_t p = start + j;
+    if (p >= R) p -= R;  // second span of RingBuffer::split (ring_buffer.cc:44-85)
+    float* r = ring + c * R + p;
+    const float s = src[c * cs + j * js];
+    if (win)
+        *r = __builtin_fmaf(__builtin_fmaf(s, win[j], 0.0f), gain, *r);
+    else
+        *r = __builtin_fmaf(s, gain, *r);
+}
+
+__device__ inline float wave_max(float v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_ola_produce(float* __restrict__ ring, int64_t R,
+                                                     const float* __restrict__ den,
+                                                     float* __restrict__ out, int64_t ldo,
+                                                     int64_t rp, int64_t len, int64_t n_total,
+                                                     unsigned* __restrict__ peak) {
+    const int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t c = blockIdx.y;
+    float v = 0.0f;
+    bool have = false;
+    if (j < len) {
+        int64_t p = rp + j;
+        if (p >= R) p -= R;
+        float* r = ring + c * R + p;
+        v = *r / den[p];
+        out[c * ldo + j] = v;
+        *r = 0.0f;
+        have = true;
+    } else if (c == 0 && peak && j < n_total) {
+        // produce(n) with n > R: split() clamps the work to R samples but the
+        // meter still reads n (OLAAccumulator.cc:217 over the caller's buffer)
+        v = out[j];
+        have = true;
+    }
+    if (c != 0 || !peak) return;
+    float a = (have && !(v != v)) ? fabsf(v) : 0.0f;
+    a = wave_max(a);
+    if ((threadIdx.x & 63) == 0 && a > 0.0f) atomicMax(peak, __float_as_uint(a));
+}
+
+}  // namespace
+
+hipError_t launch_ola_add(float* ring, int channels, int64_t R, const float* src, int64_t cs,
+                          int64_t js, const float* win, int64_t start, int64_t len, float gain,
+                          hipStream_t s) {
+    if (len <= 0 || channels <= 0) return hipSuccess;
+    const dim3 grid(unsigned((len + 255) / 256), unsigned(channels));
+    hipLaunchKernelGGL(k_ola_add, grid, dim3(256), 0, s, ring, R, src, cs, js, win, start, len, gain);
+    return hipGetLastError();
+}
+
+hipError_t launch_ola_produce(float* ring, int channels, int64_t R, const float* den, float* out,
+                              int64_t ldo, int64_t rp, int64_t len, int64_t n_total, unsigned* peak,
+                              hipStream_t s) {
+    const int64_t span = peak && n_total > len ? n_total : len;
+    if (span <= 0 || channels <= 0) return hipSuccess;
+    const dim3 grid(unsigned((span + 255) / 256), unsigned(channels));
+    hipLaunchKernelGGL(k_ola_produce, grid, dim3(256), 0, s, ring, R, den, out, ldo, rp, len, n_total,
+                       peak);
+    return hipGetLastError();
+}
+
+}  // namespace crlot

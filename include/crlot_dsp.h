@@ -223,6 +223,85 @@ int crlot_stream_set_layout(crlot_stream* st, int32_t interleaved);
 int crlot_stream_push_hop(crlot_stream* st, const float* d_hop_in, float* d_hop_out,
                           int32_t* emitted, void* stream);
 
+/* ---------------------------------------------------------------- Framer (host)
+ * dsp::Framer (framer.h:26-127, framer.cc:15-181): interleaved PCM of
+ * `channels` channels in, frames of frame_size*channels interleaved samples out
+ * every hop_size samples per channel; ZERO_PAD pads the last partial frame with
+ * zeros, DROP never emits one.  A host object (bookkeeping and copies); the
+ * batched crlot_roundtrip frames on the device instead.
+ * push / pop return 1 (true) or 0 (false) as the reference's bool, negative on
+ * a bad handle; set_params fails with CRLOT_EINVAL and the reference's message
+ * (std::invalid_argument) on a zero size. */
+typedef struct crlot_framer crlot_framer;
+int crlot_framer_create(crlot_framer** out);
+void crlot_framer_destroy(crlot_framer* f);
+int crlot_framer_set_params(crlot_framer* f, int64_t frame_size, int64_t hop_size, int64_t channels,
+                            int32_t boundary_mode);
+int crlot_framer_push(crlot_framer* f, const float* interleaved, int64_t frames);
+int crlot_framer_pop(crlot_framer* f, float* out_frame);
+int64_t crlot_framer_available(const crlot_framer* f);
+int crlot_framer_reset(crlot_framer* f);
+int crlot_framer_info(const crlot_framer* f, int64_t* frame_size, int64_t* hop_size,
+                      int64_t* channels, int32_t* boundary_mode, int64_t* buffer_size);
+
+/* ---------------------------------------------------------------- OLAAccumulator
+ * dsp::OLAAccumulator (OLAAccumulator.h:15-217, OLAAccumulator.cc:13-295) with
+ * its state on the device: per-channel rings [channels][ring_len] and the COLA
+ * divisors in HBM, every add / produce a kernel; the host keeps the reference's
+ * counters (produced_samples, read_pos, flush, reset) so any call sequence
+ * behaves as the reference's.  Per-sample arithmetic is the reference's scalar
+ * kernels (kernels.cc:18-36): fma(fma(x, w, 0), gain, acc) or fma(x, gain, acc);
+ * out = acc / (norm > eps ? norm : eps), acc = 0.
+ * Two call forms: host pointers (the reference's signatures; staged through
+ * pinned memory on the object's own stream, produce() returns when the samples
+ * are in the caller's buffers) and _device forms on caller-owned HBM with a
+ * stream (NULL = the object's stream); calls on different streams are ordered
+ * by the object.  Null pointers fail with CRLOT_EINVAL and the reference's
+ * messages.  Not thread-safe (as the reference). */
+typedef struct crlot_ola crlot_ola;
+typedef struct crlot_ola_config { /* dsp::OLAConfig (OLAAccumulator.h:15-29) */
+    int32_t sample_rate;
+    int64_t frame_size;
+    int64_t hop_size;
+    int64_t channels;
+    float eps;                   /* reference default 1e-8f */
+    int32_t apply_window_inside;
+    int32_t shadow_ring;         /* accepted; value-neutral (ola_accumulator_test.cc:1079-1120) */
+    int32_t device;              /* HIP device ordinal, -1 = current */
+} crlot_ola_config;
+int crlot_ola_create(const crlot_ola_config* cfg, crlot_ola** out);
+void crlot_ola_destroy(crlot_ola* o);
+int crlot_ola_set_window(crlot_ola* o, const float* window, int32_t wlen);
+/* ch_frames[c] (host), c < channels */
+int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const float* window,
+                            int64_t start_sample, int64_t start_off, int64_t size, float gain);
+/* interleaved [frame_size][channels] (host) */
+int crlot_ola_push_frame_aos(crlot_ola* o, const float* interleaved, const float* window,
+                             int64_t start_sample, int64_t start_off, int64_t size, float gain);
+/* ch_out[c] (host) receives up to n samples; *n_out = samples provided */
+int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_out);
+/* device forms: channel c of a frame at d_frames + c*ld_frames; window (when the
+ * object does not apply its own) a device array of frame_size floats */
+int crlot_ola_add_frame_soa_device(crlot_ola* o, const float* d_frames, int64_t ld_frames,
+                                   const float* d_window, int64_t start_sample, int64_t start_off,
+                                   int64_t size, float gain, void* stream);
+int crlot_ola_push_frame_aos_device(crlot_ola* o, const float* d_interleaved, const float* d_window,
+                                    int64_t start_sample, int64_t start_off, int64_t size, float gain,
+                                    void* stream);
+/* channel c written to d_out + c*ld_out (n floats per channel must be valid) */
+int crlot_ola_produce_device(crlot_ola* o, float* d_out, int64_t ld_out, int64_t n, int64_t* n_out,
+                             void* stream);
+int crlot_ola_flush(crlot_ola* o);
+int crlot_ola_reset(crlot_ola* o);
+int crlot_ola_info(const crlot_ola* o, int64_t* produced_samples, int64_t* read_pos,
+                   int64_t* ring_size, int32_t* has_window);
+/* channel-0 peak of every sample produced so far (waits for device produces) */
+int crlot_ola_meter_peak(crlot_ola* o, float* peak);
+/* the object's COLA norm table (ring_size floats, before the eps guard) */
+int crlot_ola_norm_table(const crlot_ola* o, float* out);
+/* wait for everything issued on the object */
+int crlot_ola_synchronize(crlot_ola* o);
+
 /* ---------------------------------------------------------------- WAV I/O
  * io/wav.{h,cc} (WavReader / WavWriter over dr_wav): RIFF WAVE, 1 or 2
  * channels, 16/24/32-bit PCM or 32-bit IEEE float (wav.cc:26-55 guards; a

@@ -1,7 +1,11 @@
 // crlot_dsp.hpp -- C++ host surface over the C ABI (header-only).
 //
 // Mirrors the reference's C++ API for the hot path so C++ callers drop in:
-//   crlot::dsp::WindowLUT          <- dsp::WindowLUT        (WindowLUT.h:80-199)
+//   crlot::dsp::Framer             <- dsp::Framer           (framer.h:26-127)
+//   crlot::dsp::OLAConfig          <- dsp::OLAConfig        (OLAAccumulator.h:15-29)
+//   crlot::dsp::OLAAccumulator     <- dsp::OLAAccumulator   (OLAAccumulator.h:63-217), device rings
+//   crlot::dsp::WindowLUT          <- dsp::WindowLUT        (WindowLUT.h:80-287), incl. the
+//                                     GetWindowSafe / GetWindow / getInstance cache
 //   crlot::dsp::fft::FftPlanDesc   <- dsp::fft::FftPlanDesc (fft_api.h:16-23)
 //   crlot::dsp::fft::IFftPlan      <- dsp::fft::IFftPlan    (fft_api.h:26-48)
 //   crlot::dsp::fft::HipFftPlan    <- KissFftPlan (kissfft_adapter.cc:11-264), Real + Complex
@@ -17,12 +21,16 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
+#include <cmath>
 #include <complex>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "crlot_dsp.h"
@@ -239,23 +247,308 @@ namespace dsp {
 enum class WindowType { HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS };
 enum class NormalizationType { NONE, SUM_TO_ONE, L2_NORM, OLA_UNITY_GAIN, OLA_SUM_WSQ };
 
-// WindowLUT(nfft, type, periodic, norm).data(): the reference's tables, bit-exact.
+// dsp::WindowLUT (WindowLUT.h:80-287): an instance owns one table
+// (WindowLUT(nfft, type, periodic, norm).data()), and the process-wide cache
+// hands out tables by (type, N, periodic, norm) -- GetWindowSafe as an aliasing
+// shared_ptr that outlives clearCache(), the deprecated GetWindow as a raw
+// pointer valid until clearCache().  Tables are the reference's, bit-exact
+// (crlot_window_table, host code).
+struct WindowData {
+    std::vector<float> values;
+    size_t size = 0;
+    WindowType type = WindowType::HANN;
+    bool periodic = false;
+    NormalizationType norm = NormalizationType::NONE;
+};
+
 class WindowLUT {
    public:
     WindowLUT(size_t nfft, WindowType type, bool periodic = false,
-              NormalizationType norm = NormalizationType::NONE)
-        : data_(nfft) {
+              NormalizationType norm = NormalizationType::NONE) {
         if (nfft == 0) throw std::invalid_argument("Window size must be greater than 0");
-        if (type == WindowType::BLACKMAN_HARRIS)
-            throw std::invalid_argument("Blackman-Harris window not yet implemented");
-        check(crlot_window_table(int32_t(type), int64_t(nfft), periodic, int32_t(norm), data_.data()),
-              "crlot_window_table");
+        data_ = create(type, nfft, periodic, norm);
     }
-    const float* data() const { return data_.data(); }
-    size_t size() const { return data_.size(); }
+    WindowLUT() = default;  // cache-only instance (getInstance)
+    WindowLUT(const WindowLUT&) = delete;
+    WindowLUT& operator=(const WindowLUT&) = delete;
+
+    const float* data() const {
+        if (!data_) throw std::runtime_error("Window data not initialized");
+        return data_->values.data();
+    }
+    size_t size() const { return data_ ? data_->size : 0; }
+    WindowType type() const { return data_ ? data_->type : WindowType::HANN; }
+    bool periodic() const { return data_ ? data_->periodic : false; }
+    NormalizationType normalization() const { return data_ ? data_->norm : NormalizationType::NONE; }
+
+    // WindowLUT.cc:75-105: a hit must be of the current generation
+    std::shared_ptr<const float> GetWindowSafe(WindowType type, size_t N, bool periodic = false,
+                                               NormalizationType norm = NormalizationType::NONE) {
+        if (N == 0) throw std::invalid_argument("Window size must be greater than 0");
+        const uint64_t key = cache_key(type, N, periodic, norm);
+        const uint64_t gen = generation().load();
+        std::lock_guard<std::mutex> lock(mutex());
+        auto it = safe_cache().find(key);
+        if (it != safe_cache().end() && it->second.generation == gen)
+            return std::shared_ptr<const float>(it->second.data, it->second.data->values.data());
+        std::shared_ptr<WindowData> d(create(type, N, periodic, norm).release());
+        safe_cache()[key] = Entry{d, gen};
+        return std::shared_ptr<const float>(d, d->values.data());
+    }
+
+    // WindowLUT.cc:107-131 (deprecated in the reference: valid until clearCache)
+    [[deprecated("Use GetWindowSafe() for thread safety")]]
+    const float* GetWindow(WindowType type, size_t N, bool periodic = false,
+                           NormalizationType norm = NormalizationType::NONE) {
+        if (N == 0) throw std::invalid_argument("Window size must be greater than 0");
+        const uint64_t key = cache_key(type, N, periodic, norm);
+        std::lock_guard<std::mutex> lock(mutex());
+        auto it = legacy_cache().find(key);
+        if (it != legacy_cache().end()) return it->second->values.data();
+        auto d = create(type, N, periodic, norm);
+        const float* p = d->values.data();
+        legacy_cache()[key] = std::move(d);
+        return p;
+    }
+
+    static WindowLUT& getInstance() {
+        static WindowLUT instance;
+        return instance;
+    }
+    size_t getCacheSize() const {
+        std::lock_guard<std::mutex> lock(mutex());
+        return safe_cache().size() + legacy_cache().size();
+    }
+    // WindowLUT.cc:138-162: bump the generation (older handles stay valid),
+    // drop entries two generations old; force_immediate empties both caches
+    void clearCache(bool force_immediate = false) {
+        std::lock_guard<std::mutex> lock(mutex());
+        if (force_immediate) {
+            safe_cache().clear();
+            legacy_cache().clear();
+            return;
+        }
+        generation().fetch_add(1);
+        const uint64_t cur = generation().load();
+        for (auto it = safe_cache().begin(); it != safe_cache().end();)
+            it = (it->second.generation < cur - 1) ? safe_cache().erase(it) : std::next(it);
+        legacy_cache().clear();
+    }
+    uint64_t getCurrentGeneration() const { return generation().load(); }
+
+    static double calculateSum(const float* w, size_t N) {
+        double s = 0.0;
+        for (size_t i = 0; w && i < N; ++i) s += double(w[i]);
+        return s;
+    }
+    static double calculateSumOfSquares(const float* w, size_t N) {
+        double s = 0.0;
+        for (size_t i = 0; w && i < N; ++i) s += double(w[i]) * double(w[i]);
+        return s;
+    }
+    static double calculateRMSError(const float* a, const float* b, size_t N) {
+        if (!a || !b || N == 0) return 0.0;
+        double s = 0.0;
+        for (size_t i = 0; i < N; ++i) {
+            const double d = double(a[i]) - double(b[i]);
+            s += d * d;
+        }
+        return std::sqrt(s / double(N));
+    }
 
    private:
-    std::vector<float> data_;
+    struct Entry {
+        std::shared_ptr<WindowData> data;
+        uint64_t generation = 0;
+    };
+    // [type:8][periodic:1][norm:3][size:52] (WindowLUT.cc:448-457)
+    static uint64_t cache_key(WindowType t, size_t N, bool periodic, NormalizationType norm) {
+        return (uint64_t(t) << 56) | (uint64_t(periodic ? 1 : 0) << 55) | (uint64_t(norm) << 52) |
+               (uint64_t(N) & 0xFFFFFFFFFFFFFULL);
+    }
+    static std::unique_ptr<WindowData> create(WindowType type, size_t N, bool periodic,
+                                              NormalizationType norm) {
+        if (type == WindowType::BLACKMAN_HARRIS)
+            throw std::invalid_argument("Blackman-Harris window not yet implemented");
+        auto d = std::make_unique<WindowData>();
+        d->values.resize(N);
+        d->size = N;
+        d->type = type;
+        d->periodic = periodic;
+        d->norm = norm;
+        check(crlot_window_table(int32_t(type), int64_t(N), periodic, int32_t(norm), d->values.data()),
+              "crlot_window_table");
+        return d;
+    }
+    static std::mutex& mutex() {
+        static std::mutex m;
+        return m;
+    }
+    static std::unordered_map<uint64_t, Entry>& safe_cache() {
+        static std::unordered_map<uint64_t, Entry> c;
+        return c;
+    }
+    static std::unordered_map<uint64_t, std::unique_ptr<WindowData>>& legacy_cache() {
+        static std::unordered_map<uint64_t, std::unique_ptr<WindowData>> c;
+        return c;
+    }
+    static std::atomic<uint64_t>& generation() {
+        static std::atomic<uint64_t> g{1};
+        return g;
+    }
+    std::unique_ptr<WindowData> data_;
+};
+
+// dsp::BoundaryMode (framer.h:11-14)
+enum class BoundaryMode { ZERO_PAD, DROP };
+
+// dsp::Framer (framer.h:26-127), host object over crlot_framer_*.
+class Framer {
+   public:
+    Framer() { check(crlot_framer_create(&f_), "crlot_framer_create"); }
+    ~Framer() { crlot_framer_destroy(f_); }
+    Framer(const Framer&) = delete;
+    Framer& operator=(const Framer&) = delete;
+    void set_params(size_t frame_size, size_t hop_size, size_t channels = 1,
+                    BoundaryMode boundary_mode = BoundaryMode::ZERO_PAD) {
+        check(crlot_framer_set_params(f_, int64_t(frame_size), int64_t(hop_size), int64_t(channels),
+                                      boundary_mode == BoundaryMode::DROP ? CRLOT_DROP : CRLOT_ZERO_PAD),
+              "Framer::set_params");
+    }
+    bool push(const float* interleaved, size_t frames) {
+        return check_bool(crlot_framer_push(f_, interleaved, int64_t(frames)));
+    }
+    bool pop(float* out_frame) { return check_bool(crlot_framer_pop(f_, out_frame)); }
+    size_t available_frames() const { return size_t(crlot_framer_available(f_)); }
+    void reset() { check(crlot_framer_reset(f_), "Framer::reset"); }
+    size_t frame_size() const { return size_t(info().n); }
+    size_t hop_size() const { return size_t(info().h); }
+    size_t channels() const { return size_t(info().c); }
+    BoundaryMode boundary_mode() const {
+        return info().mode == CRLOT_DROP ? BoundaryMode::DROP : BoundaryMode::ZERO_PAD;
+    }
+    size_t buffer_size() const { return size_t(info().buf); }
+
+   private:
+    struct Info {
+        int64_t n = 0, h = 0, c = 0, buf = 0;
+        int32_t mode = 0;
+    };
+    Info info() const {
+        Info i;
+        check(crlot_framer_info(f_, &i.n, &i.h, &i.c, &i.mode, &i.buf), "Framer");
+        return i;
+    }
+    static bool check_bool(int rc) {
+        check(rc, "Framer");
+        return rc == 1;
+    }
+    crlot_framer* f_ = nullptr;
+};
+
+// dsp::OLAConfig (OLAAccumulator.h:15-29); `device` selects the HIP device (-1: current).
+struct OLAConfig {
+    int sample_rate = 0;
+    size_t frame_size = 0;
+    size_t hop_size = 0;
+    size_t channels = 0;
+    float eps = 1e-8f;
+    bool apply_window_inside = false;
+    bool shadow_ring = false;
+    int device = -1;
+    bool isValid() const {
+        return sample_rate > 0 && frame_size > 0 && hop_size > 0 && channels > 0 && eps > 0.0f;
+    }
+};
+
+// dsp::OLAAccumulator (OLAAccumulator.h:63-217): the rings live on the device
+// (crlot_ola_*); the reference's signatures take host pointers, the *_device
+// forms take HBM pointers and a stream.  Non-copyable, non-movable, like the
+// reference.
+class OLAAccumulator {
+   public:
+    explicit OLAAccumulator(const OLAConfig& cfg) : cfg_(cfg) {
+        if (!cfg.isValid()) throw std::invalid_argument("Invalid OLA configuration");
+        crlot_ola_config c{};
+        c.sample_rate = cfg.sample_rate;
+        c.frame_size = int64_t(cfg.frame_size);
+        c.hop_size = int64_t(cfg.hop_size);
+        c.channels = int64_t(cfg.channels);
+        c.eps = cfg.eps;
+        c.apply_window_inside = cfg.apply_window_inside;
+        c.shadow_ring = cfg.shadow_ring;
+        c.device = cfg.device;
+        check(crlot_ola_create(&c, &o_), "OLAAccumulator");
+    }
+    ~OLAAccumulator() { crlot_ola_destroy(o_); }
+    OLAAccumulator(const OLAAccumulator&) = delete;
+    OLAAccumulator& operator=(const OLAAccumulator&) = delete;
+    OLAAccumulator(OLAAccumulator&&) = delete;
+    OLAAccumulator& operator=(OLAAccumulator&&) = delete;
+
+    void set_window(const float* w, int wlen) { check(crlot_ola_set_window(o_, w, wlen), "set_window"); }
+    void add_frame_SoA(const float* const* ch_frames, const float* window, size_t start_sample,
+                       size_t start_off, size_t size, float gain) {
+        check(crlot_ola_add_frame_soa(o_, ch_frames, window, int64_t(start_sample), int64_t(start_off),
+                                      int64_t(size), gain),
+              "add_frame_SoA");
+    }
+    void push_frame_AoS(const float* interleaved, const float* window, size_t start_sample,
+                        size_t start_off, size_t size, float gain) {
+        check(crlot_ola_push_frame_aos(o_, interleaved, window, int64_t(start_sample), int64_t(start_off),
+                                       int64_t(size), gain),
+              "push_frame_AoS");
+    }
+    size_t produce(float* const* ch_out, size_t n) {
+        int64_t got = 0;
+        check(crlot_ola_produce(o_, ch_out, int64_t(n), &got), "produce");
+        return size_t(got);
+    }
+    // device forms: frames / outputs in HBM, channel c at +c*ld
+    void add_frame_SoA_device(const float* d_frames, size_t ld_frames, const float* d_window,
+                              size_t start_sample, size_t start_off, size_t size, float gain,
+                              hipStream_t s = nullptr) {
+        check(crlot_ola_add_frame_soa_device(o_, d_frames, int64_t(ld_frames), d_window, int64_t(start_sample),
+                                             int64_t(start_off), int64_t(size), gain, s),
+              "add_frame_SoA_device");
+    }
+    void push_frame_AoS_device(const float* d_interleaved, const float* d_window, size_t start_sample,
+                               size_t start_off, size_t size, float gain, hipStream_t s = nullptr) {
+        check(crlot_ola_push_frame_aos_device(o_, d_interleaved, d_window, int64_t(start_sample),
+                                              int64_t(start_off), int64_t(size), gain, s),
+              "push_frame_AoS_device");
+    }
+    size_t produce_device(float* d_out, size_t ld_out, size_t n, hipStream_t s = nullptr) {
+        int64_t got = 0;
+        check(crlot_ola_produce_device(o_, d_out, int64_t(ld_out), int64_t(n), &got, s), "produce_device");
+        return size_t(got);
+    }
+    void flush() { check(crlot_ola_flush(o_), "flush"); }
+    void reset() { check(crlot_ola_reset(o_), "reset"); }
+    void synchronize() { check(crlot_ola_synchronize(o_), "synchronize"); }
+    size_t produced_samples() const { return size_t(state().produced); }
+    size_t read_pos() const { return size_t(state().read_pos); }
+    float meter_peak() const {
+        float p = 0.0f;
+        check(crlot_ola_meter_peak(o_, &p), "meter_peak");
+        return p;
+    }
+    const OLAConfig& config() const { return cfg_; }
+    bool has_window() const { return state().has_window != 0; }
+    size_t ring_size() const { return size_t(state().ring); }
+
+   private:
+    struct State {
+        int64_t produced = 0, read_pos = 0, ring = 0;
+        int32_t has_window = 0;
+    };
+    State state() const {
+        State s;
+        check(crlot_ola_info(o_, &s.produced, &s.read_pos, &s.ring, &s.has_window), "OLAAccumulator");
+        return s;
+    }
+    OLAConfig cfg_;
+    crlot_ola* o_ = nullptr;
 };
 
 namespace fft {
@@ -311,7 +604,7 @@ class HipFftPlan final : public IFftPlan {
             throw std::runtime_error("Real FFT not supported for Complex domain plan");
         check_batch(batch);
         const int64_t n = d_.nfft, bins = n / 2 + 1;
-        run(in, 1, batch * d_.stride_in * n, reinterpret_cast<float*>(out), 2, batch * d_.stride_out * bins,
+        run(in, 1, span(batch, d_.stride_in, n), reinterpret_cast<float*>(out), 2, span(batch, d_.stride_out, bins),
             [&](const float* i, float* o) {
                 return crlot_fft_forward(p_, i, o, batch, d_.stride_in * n, d_.stride_in,
                                          2 * d_.stride_out * bins, d_.stride_out, nullptr);
@@ -322,8 +615,8 @@ class HipFftPlan final : public IFftPlan {
             throw std::runtime_error("Real FFT not supported for Complex domain plan");
         check_batch(batch);
         const int64_t n = d_.nfft, bins = n / 2 + 1;
-        run(reinterpret_cast<const float*>(in), 2, batch * d_.stride_in * bins, out, 1,
-            batch * d_.stride_out * n, [&](const float* i, float* o) {
+        run(reinterpret_cast<const float*>(in), 2, span(batch, d_.stride_in, bins), out, 1,
+            span(batch, d_.stride_out, n), [&](const float* i, float* o) {
                 return crlot_fft_inverse(p_, i, o, batch, 2 * d_.stride_in * bins, d_.stride_in,
                                          d_.stride_out * n, d_.stride_out, nullptr);
             });
@@ -349,6 +642,11 @@ class HipFftPlan final : public IFftPlan {
             throw std::runtime_error("FFT size must be even for real FFT");
         return d;
     }
+    // elements a strided batch addresses: the last batch's last element + 1
+    // (the reference touches only i*stride, i < len: kissfft_adapter.cc:97-98, 139-140)
+    static int64_t span(int batch, int stride, int64_t len) {
+        return (int64_t(batch) - 1) * stride * len + (len - 1) * stride + 1;
+    }
     void check_batch(int batch) const {
         if (batch < 1 || batch > d_.batch) throw std::runtime_error("Invalid batch size");
     }
@@ -357,8 +655,8 @@ class HipFftPlan final : public IFftPlan {
             throw std::runtime_error("Complex FFT not supported for Real domain plan");
         check_batch(batch);
         const int64_t n = d_.nfft;
-        run(reinterpret_cast<const float*>(in), 2, batch * d_.stride_in * n,
-            reinterpret_cast<float*>(out), 2, batch * d_.stride_out * n, [&](const float* i, float* o) {
+        run(reinterpret_cast<const float*>(in), 2, span(batch, d_.stride_in, n),
+            reinterpret_cast<float*>(out), 2, span(batch, d_.stride_out, n), [&](const float* i, float* o) {
                 return (inv ? crlot_fft_inverse_complex : crlot_fft_forward_complex)(
                     p_, i, o, batch, 2 * d_.stride_in * n, d_.stride_in, 2 * d_.stride_out * n,
                     d_.stride_out, nullptr);

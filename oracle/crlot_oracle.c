@@ -771,6 +771,22 @@ size_t or_ola_produce(or_ola* o, float* const* out, size_t n) {
     return n;
 }
 
+/* OLAAccumulator::flush (OLAAccumulator.cc:223-228): counters only */
+void or_ola_flush(or_ola* o) {
+    if (o->read_pos + o->n > o->produced) o->produced = o->read_pos + o->n;
+}
+
+/* OLAAccumulator::reset (OLAAccumulator.cc:230-247): rings zeroed, window dropped */
+void or_ola_reset(or_ola* o) {
+    memset(o->ring, 0, sizeof(float) * o->c * o->ring_len);
+    o->read_pos = 0;
+    o->produced = 0;
+    o->meter_peak = 0.0f;
+    free(o->window);
+    o->window = NULL;
+    or_init_normalization(o->norm, NULL, o->ring_len, o->n, o->h, o->inside, o->eps);
+}
+
 size_t or_ola_ring_size(const or_ola* o) { return o->ring_len; }
 const float* or_ola_norm(const or_ola* o) { return o->norm; }
 size_t or_ola_produced(const or_ola* o) { return o->produced; }

@@ -94,6 +94,8 @@ void or_ola_add_frame_soa(or_ola*, const float* const* ch_frames, const float* w
 void or_ola_push_frame_aos(or_ola*, const float* interleaved, const float* window,
                            size_t start_sample, size_t start_off, size_t size, float gain);
 size_t or_ola_produce(or_ola*, float* const* ch_out, size_t n);
+void or_ola_flush(or_ola*);
+void or_ola_reset(or_ola*);
 size_t or_ola_ring_size(const or_ola*);
 const float* or_ola_norm(const or_ola*);
 size_t or_ola_produced(const or_ola*);

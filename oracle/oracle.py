@@ -72,6 +72,14 @@ def lib(native: bool = False):
     L.or_ola_add_frame_soa.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, sz, sz, sz, C.c_float]
     L.or_ola_produce.argtypes = [C.c_void_p, C.c_void_p, sz]
     L.or_ola_produce.restype = sz
+    L.or_ola_flush.argtypes = [C.c_void_p]
+    L.or_ola_reset.argtypes = [C.c_void_p]
+    L.or_ola_produced.argtypes = [C.c_void_p]
+    L.or_ola_produced.restype = sz
+    L.or_ola_read_pos.argtypes = [C.c_void_p]
+    L.or_ola_read_pos.restype = sz
+    L.or_ola_meter_peak.argtypes = [C.c_void_p]
+    L.or_ola_meter_peak.restype = C.c_float
     L.or_ola_ring_size.argtypes = [C.c_void_p]
     L.or_ola_ring_size.restype = sz
     L.or_ola_norm.argtypes = [C.c_void_p]
@@ -247,6 +255,37 @@ class Ola:
         ptrs = (C.c_void_p * self.c)(*[o.ctypes.data for o in outs])
         got = lib().or_ola_produce(self.p, ptrs, n)
         return [o[:got] for o in outs]
+
+    def produce_into(self, n, outs):
+        """produce(ch_out, n) into caller buffers (tails beyond the count untouched)."""
+        ptrs = (C.c_void_p * self.c)(*[o.ctypes.data for o in outs])
+        return int(lib().or_ola_produce(self.p, ptrs, n))
+
+    def add_frame_soa(self, frames, start, off=0, size=None, gain=1.0, window=None):
+        size = self.n if size is None else size
+        arrs = [np.ascontiguousarray(f, np.float32) for f in frames]
+        ptrs = (C.c_void_p * self.c)(*[a.ctypes.data for a in arrs])
+        wp = None if window is None else np.ascontiguousarray(window, np.float32)
+        lib().or_ola_add_frame_soa(self.p, ptrs, None if wp is None else wp.ctypes.data, start, off,
+                                   size, gain)
+
+    def flush(self):
+        lib().or_ola_flush(self.p)
+
+    def reset(self):
+        lib().or_ola_reset(self.p)
+
+    @property
+    def produced(self):
+        return int(lib().or_ola_produced(self.p))
+
+    @property
+    def read_pos(self):
+        return int(lib().or_ola_read_pos(self.p))
+
+    @property
+    def meter_peak(self):
+        return float(lib().or_ola_meter_peak(self.p))
 
     @property
     def ring_size(self):

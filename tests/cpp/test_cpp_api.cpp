@@ -161,6 +161,75 @@ int main() {
         or_window(OR_HANN, 1024, 0, OR_NORM_NONE, ref.data());
         for (int i = 0; i < 1024; ++i) EXPECT(lut.data()[i] == ref[i], "window %d", i);
     }
+    // WindowLUT cache (window_lut_test.cc): GetWindowSafe hits within a generation,
+    // handles outlive clearCache(), the deprecated GetWindow stays bit-identical
+    {
+        WindowLUT& lut = WindowLUT::getInstance();
+        EXPECT(&lut == &WindowLUT::getInstance(), "singleton");
+        lut.clearCache(true);
+        auto a = lut.GetWindowSafe(WindowType::HANN, 1024);
+        auto b = lut.GetWindowSafe(WindowType::HANN, 1024);
+        EXPECT(a.get() == b.get() && lut.getCacheSize() == 1, "cache hit");
+        auto p = lut.GetWindowSafe(WindowType::HANN, 1024, true);
+        EXPECT(p.get() != a.get() && lut.getCacheSize() == 2, "periodic is its own key");
+        const uint64_t g0 = lut.getCurrentGeneration();
+        lut.clearCache();
+        EXPECT(lut.getCurrentGeneration() == g0 + 1, "generation");
+        auto c = lut.GetWindowSafe(WindowType::HANN, 1024);
+        EXPECT(c.get() != a.get() && a.get()[512] == c.get()[512], "old handle survives, new table equal");
+        std::vector<float> ref(1024);
+        or_window(OR_HANN, 1024, 0, OR_NORM_NONE, ref.data());
+        for (int i = 0; i < 1024; ++i) EXPECT(c.get()[i] == ref[i], "cached window %d", i);
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wdeprecated-declarations"
+        const float* raw = lut.GetWindow(WindowType::HAMMING, 512);
+        EXPECT(raw == lut.GetWindow(WindowType::HAMMING, 512), "legacy cache hit");
+#pragma GCC diagnostic pop
+        WindowLUT inst(512, WindowType::HAMMING);
+        for (int i = 0; i < 512; ++i) EXPECT(raw[i] == inst.data()[i], "legacy %d", i);
+        EXPECT(inst.size() == 512 && inst.type() == WindowType::HAMMING && !inst.periodic(), "getters");
+        int threw = 0;
+        try { lut.GetWindowSafe(WindowType::HANN, 0); } catch (const std::invalid_argument&) { ++threw; }
+        try { WindowLUT bad(0, WindowType::HANN); } catch (const std::invalid_argument&) { ++threw; }
+        try { WindowLUT bh(64, WindowType::BLACKMAN_HARRIS); } catch (const std::invalid_argument&) { ++threw; }
+        try { WindowLUT empty; (void)empty.data(); } catch (const std::runtime_error&) { ++threw; }
+        EXPECT(threw == 4, "WindowLUT exceptions %d", threw);
+        EXPECT(std::fabs(WindowLUT::calculateSum(inst.data(), 512) - 0.54 * 511 - 0.54) < 1.0, "sum");
+    }
+    // Framer / OLAAccumulator exception types (framer.cc:15-35, OLAAccumulator.cc:17-19, 38-45)
+    {
+        int threw = 0;
+        Framer f;
+        try { f.set_params(0, 1); } catch (const std::invalid_argument&) { ++threw; }
+        EXPECT(!f.pop(nullptr) && !f.push(nullptr, 4), "framer guards");
+        OLAConfig bad;
+        bad.sample_rate = 48000;
+        bad.frame_size = 256;
+        bad.hop_size = 64;
+        bad.channels = 0;
+        try { OLAAccumulator o(bad); } catch (const std::invalid_argument&) { ++threw; }
+        OLAConfig ok = bad;
+        ok.channels = 2;
+        ok.apply_window_inside = true;
+        OLAAccumulator o(ok);
+        try { o.set_window(nullptr, 256); } catch (const std::invalid_argument&) { ++threw; }
+        std::vector<float> w(256, 1.0f);
+        try { o.set_window(w.data(), 255); } catch (const std::invalid_argument&) { ++threw; }
+        try { o.push_frame_AoS(nullptr, nullptr, 0, 0, 256, 1.0f); } catch (const std::invalid_argument&) { ++threw; }
+        float* outs[2] = {nullptr, nullptr};
+        try { o.produce(outs, 1); } catch (const std::invalid_argument&) { ++threw; }
+        EXPECT(threw == 6, "exceptions %d", threw);
+        o.set_window(w.data(), 256);
+        std::vector<float> aos(512);
+        for (int i = 0; i < 512; ++i) aos[i] = (i % 2) ? -0.25f : 0.5f;
+        o.push_frame_AoS(aos.data(), nullptr, 0, 0, 256, 1.0f);
+        std::vector<float> c0(64), c1(64);
+        float* co[2] = {c0.data(), c1.data()};
+        EXPECT(o.produce(co, 64) == 64 && o.read_pos() == 64 && o.produced_samples() == 256, "counters");
+        EXPECT(o.meter_peak() > 0.0f && o.has_window() && o.ring_size() == 24 * 64, "state");
+        o.reset();
+        EXPECT(!o.has_window() && o.produced_samples() == 0 && o.meter_peak() == 0.0f, "reset");
+    }
     // e2e round trip: StftEngine vs the oracle restatement of e2e_benchmark.cc
     {
         crlot::StftEngine::Config c;
