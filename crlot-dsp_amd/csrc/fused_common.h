@@ -1,0 +1,120 @@
+// fused_common.h -- device and host pieces shared by the fused walker kernels
+// (kernels.hip: K_fused*, K_pair512/2k/4k, K_fused_wg; pair1k.hip: K_pair).
+#pragma once
+
+#include <cstdint>
+
+#include "fft_wave.h"
+#include "kernels.h"
+
+namespace crlot {
+namespace fk {
+
+struct FusedArgs {
+    DevTables t;
+    const float* x;
+    float* y;
+    int64_t ld_x, ld_y;
+    int T, out_len;  // per stream, T * 4 and out_len * 4 < 2^31 (checked on the host)
+    int n_streams, F, n_chunks, M, ring_blocks;
+    int pad, pad_mode;  // framing (Geometry)
+    float inv_n, gain;
+};
+
+// FrameQueue padding (Indexing.h:18-37): left side i -> -i-1, right side
+// i -> 2n-2-i, repeated until inside.
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n <= 1) return 0;
+    while (i < 0 || i >= n) i = i < 0 ? -i - 1 : 2 * n - 2 - i;
+    return i;
+}
+
+// x[j] of a T-sample stream with the plan's padding outside [0, T)
+// (getPaddingValueSafe, Indexing.h:48-68): 0 zeros, 1 reflect101, 2 edge.
+__device__ __forceinline__ float fetch_x(__amdgpu_buffer_rsrc_t rx, int j, int T, int mode) {
+    if (mode == 1) j = reflect101(j, T);
+    else if (mode == 2) j = j < 0 ? 0 : (j >= T ? T - 1 : j);
+    const bool ok = j >= 0 && j < T;
+    const float v = dev::bload1(rx, (ok ? j : 0) * 4, 0);
+    return ok ? v : 0.0f;
+}
+
+
+// Division acc / den by Markstein's correction with r = RN(1/den): exact (equal
+// to the IEEE quotient) for den in [2^-40, 2^40] (host-checked) and acc = 0 or
+// |acc| in [2^-64, 2^64]; any other value sends the whole wave to the IEEE
+// division.  Verified exhaustively over den significands.
+__device__ __forceinline__ bool mk_ok(float a) {
+    const float t = __builtin_fabsf(a);
+    return t <= 0x1p64f && (t >= 0x1p-64f || t == 0.0f);
+}
+__device__ __forceinline__ float mk_div(float a, float d, float r) {
+    const float q = a * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, d, a), r, q);
+}
+
+// ------------------------------------------------------------------ pair-walker hop helpers
+template <int SH>
+__device__ __forceinline__ void load_hop1(float* dst, __amdgpu_buffer_rsrc_t rx, int lane, int origin,
+                                          int T, int mode) {
+    constexpr int H = 64 * SH;
+#ifdef CRLOT_ABL_NOLOAD  // timing-only ablation: wrong results
+#pragma unroll
+    for (int q = 0; q < SH; ++q) dst[q] = float(lane + q + origin) * 1e-3f;
+    return;
+#endif
+    if (origin >= 0 && origin + H <= T) {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, lane * 4, origin * 4 + q * 256);
+    } else {
+#pragma unroll
+        for (int q = 0; q < SH; ++q) dst[q] = fetch_x(rx, origin + lane + 64 * q, T, mode);
+    }
+}
+
+// 1 when every sample of the hop (SH per lane, whole wave) keeps the paired regime.
+template <int SH>
+__device__ __forceinline__ uint32_t hop_ok(const float* h, float lo, float hi) {
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        const float t = __builtin_fabsf(h[q]);
+        bad |= !((t >= lo) & (t <= hi)) & (t != 0.0f);
+    }
+    return __builtin_amdgcn_ballot_w64(bad) == 0 ? 1u : 0u;
+}
+
+// den / rden of OLA block b for this lane (DevTables::pden: [block][lane][den SH | rden SH]).
+template <int SH>
+__device__ __forceinline__ void load_den(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int lane, int b) {
+#ifdef CRLOT_ABL_NODEN  // timing-only ablation: wrong results
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        dr[q] = 1.5f;
+        dr[SH + q] = 0.6666667f;
+    }
+    return;
+#endif
+#pragma unroll
+    for (int j = 0; j < 2 * SH / 4; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, lane * (8 * SH), b * (512 * SH) + 16 * j, 0);
+        const unsigned u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];  // (see bload2)
+        dr[4 * j] = __builtin_bit_cast(float, u0);
+        dr[4 * j + 1] = __builtin_bit_cast(float, u1);
+        dr[4 * j + 2] = __builtin_bit_cast(float, u2);
+        dr[4 * j + 3] = __builtin_bit_cast(float, u3);
+    }
+}
+
+template <typename K>
+hipError_t set_lds(K kernel, size_t lds) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+}
+
+// K_pair (pair1k.hip): waves a CU holds, and the launch for H = 64 * sh.
+int pair_waves_per_cu();
+hipError_t launch_pair(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream);
+
+}  // namespace fk
+}  // namespace crlot
