@@ -39,6 +39,8 @@ struct crlot_plan {
     float* d_rden = nullptr;  // RN(1 / den)
     float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
     float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024: 64 lanes, N = 4096: 256)
+    uint32_t* d_pflags = nullptr;  // K_pair per-walker regime flags (DevTables::pflags)
+    int64_t pflags_len = 0;
     float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
@@ -108,6 +110,8 @@ crlot::DevTables tables(const crlot_plan* p) {
             t.ptw = p->d_ptw;
             t.pden = p->d_pden;
         }
+        t.pflags = p->d_pflags;
+        t.pflags_len = p->pflags_len;
         t.px_lo = p->px_lo;
         // no transform can overflow: |x w| <= 2^64 / max gain, so |X| < 2^75, |ifft| < 2^86
         t.px_hi = p->px_hi / std::max(1.0f, p->has_gain ? p->gain_max : 1.0f);
@@ -121,6 +125,7 @@ void free_plan(crlot_plan* p) {
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
                      p->d_rden, p->d_twany_own, p->d_ptw, p->d_pden})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
+    if (p->d_pflags) (void)hipFree(p->d_pflags);
     if (p->stage_pending) (void)hipEventSynchronize(p->stage_ev);
     if (p->stage_ev) (void)hipEventDestroy(p->stage_ev);
     if (p->h_stage) (void)hipHostFree(p->h_stage);
@@ -244,6 +249,21 @@ int ensure_workspace(crlot_plan* p, int64_t bytes) {
     hipError_t e = hipMalloc(&p->d_work, size_t(bytes));
     if (e != hipSuccess) return fail(CRLOT_ENOMEM, "workspace hipMalloc failed");
     p->work_bytes = bytes;
+    return CRLOT_OK;
+}
+
+// K_pair's per-walker flags: at most one walker per frame and stream.  Grown
+// (never shrunk) on the calling thread before the launch that needs them.
+int ensure_pair_flags(crlot_plan* p, int32_t n_streams, int64_t F) {
+    if (!p->pairing || p->geo.n != 1024) return CRLOT_OK;
+    const int64_t need = int64_t(n_streams) * F;
+    if (need <= p->pflags_len) return CRLOT_OK;
+    if (p->d_pflags) (void)hipFree(p->d_pflags);
+    p->d_pflags = nullptr;
+    p->pflags_len = 0;
+    hipError_t e = hipMalloc(&p->d_pflags, sizeof(uint32_t) * size_t(need));
+    if (e != hipSuccess) return fail(CRLOT_ENOMEM, "pair flag hipMalloc failed");
+    p->pflags_len = need;
     return CRLOT_OK;
 }
 
@@ -512,8 +532,12 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
     if (ld_x < T || ld_y < out_len) return fail(CRLOT_EINVAL, "leading dimension too small");
     DeviceGuard g(p->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const crlot::DevTables t = tables(p);
     hipError_t e;
+    if (use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len)) {
+        const int rcf = ensure_pair_flags(p, n_streams, F);
+        if (rcf != CRLOT_OK) return rcf;
+    }
+    const crlot::DevTables t = tables(p);
     if (use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len)) {
         e = !crlot::fused_wg_supported(p->geo.n, p->geo.h)
                 ? crlot::launch_fused(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s)

@@ -19,6 +19,7 @@ struct FusedArgs {
     int n_streams, F, n_chunks, M, ring_blocks;
     int pad, pad_mode;  // framing (Geometry)
     float inv_n, gain;
+    int fix_all = 0;  // K_pair: the fix-up walker redoes every chunk (padding rules it alone handles)
 };
 
 // FrameQueue padding (Indexing.h:18-37): left side i -> -i-1, right side
@@ -63,13 +64,29 @@ __device__ __forceinline__ void load_hop1(float* dst, __amdgpu_buffer_rsrc_t rx,
     for (int q = 0; q < SH; ++q) dst[q] = float(lane + q + origin) * 1e-3f;
     return;
 #endif
+#ifdef CRLOT_ABL_HOTONLY  // ISA-count builds: interior hops only (wrong at stream edges)
+    if (true) {
+#else
     if (origin >= 0 && origin + H <= T) {
+#endif
 #pragma unroll
         for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, lane * 4, origin * 4 + q * 256);
     } else {
 #pragma unroll
         for (int q = 0; q < SH; ++q) dst[q] = fetch_x(rx, origin + lane + 64 * q, T, mode);
     }
+}
+
+// The same for framing whose padding is zeros (Framer ZERO_PAD / DROP, FrameQueue
+// CONSTANT): the whole offset rides in voffset + the immediate, which the raw
+// buffer's range check covers per lane, so every sample outside [0, T) -- past
+// the end, or before 0 through the unsigned wrap of a negative offset (T * 4 <
+// 2^31, host-checked) -- reads 0 and edge hops need no branch.
+template <int SH>
+__device__ __forceinline__ void load_hop0(float* dst, __amdgpu_buffer_rsrc_t rx, int lane, int origin) {
+    const int v = (origin + lane) * 4;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, v + q * 256, 0);
 }
 
 // 1 when every sample of the hop (SH per lane, whole wave) keeps the paired regime.

@@ -34,6 +34,11 @@ struct DevTables {
     // L = 256 / 128, SH = H/L.
     const float* ptw4 = nullptr;
     const float* pden4 = nullptr;
+    // K_pair (N = 1024): one flag per walker wave, written by the paired-only
+    // walker (1 = a pair of its chunk left the paired regime) and read by the
+    // fix-up walker that redoes those chunks; pflags_len flags of capacity.
+    uint32_t* pflags = nullptr;
+    int64_t pflags_len = 0;
 };
 
 // Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.

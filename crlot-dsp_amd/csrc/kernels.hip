@@ -1973,7 +1973,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
 #ifdef CRLOT_NO_PAIR  // A/B builds: per-frame kernels only
     const bool use_pair = false;
 #else
-    const bool use_pair = g.n == 1024 && t.ptw && t.pden && fast;
+    const bool use_pair = g.n == 1024 && t.ptw && t.pden && t.pflags && fast;
 #endif
     const bool use_pair512 = g.n == 512 && t.ptw && t.pden && fast && g.h >= 128;
     if (g.n == 2048 && t.ptw4 && t.pden4 && fast && (g.h == 256 || g.h == 512 || g.h == 1024))

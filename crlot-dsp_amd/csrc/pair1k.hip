@@ -2,6 +2,8 @@
 // Numerics as kernels.hip (header comment there); the transform is fft_pair.h.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <type_traits>
 
 #include "fft_pair.h"
 #include "fused_common.h"
@@ -49,31 +51,31 @@ struct PairLds {
     static constexpr size_t bytes = bufs + sizeof(cf) * dev::kPairXbuf * W;
 };
 
-#ifdef CRLOT_PAIR_TRACE
-__device__ uint32_t g_pair_trace[4 << 16];
-#endif
-#ifdef CRLOT_PAIR_PHASES  // debug builds: per-wave cycles by loop phase (s_memtime)
-__device__ uint32_t g_pair_phase[8 << 16];
-#define PHASE(i)                                              \
-    do {                                                      \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
-        ph[i] += uint32_t(t_ - ph_last);                      \
-        ph_last = t_;                                         \
-    } while (0)
-#else
-#define PHASE(i) \
-    do {         \
-    } while (0)
-#endif
 #ifndef CRLOT_PAIR_REG_TW
-#define CRLOT_PAIR_REG_TW 1  // measured: same cycles as LDS twiddles at 4 waves/SIMD, +0.2..5.6 % on the clock
+#define CRLOT_PAIR_REG_TW 1  // measured: LDS twiddles at 4 waves/SIMD take 5 % more cycles
 #endif
 #ifndef CRLOT_PAIR_MIN_WAVES
 #define CRLOT_PAIR_MIN_WAVES (CRLOT_PAIR_REG_TW ? 3 : 4)
 #endif
-template <int SH, int NB, int W, bool HAS_GAIN>
+
+// Register rotation of the walk.  Hop h of the chunk (counted from fs) lives in
+// slot h % R of a ring of R hop slots (the pair at k reads hops k .. k+NB and
+// prefetches k+NB+1, k+NB+2, so R >= NB + 3), OLA block b in acc[b % NB].  The
+// loop body is unrolled U = R/2 pairs so every slot and block index is a
+// compile-time constant: no register shifting, and the block a frame opens (its
+// last, k+NB-1 for frame k) starts from a literal zero instead of a cleared
+// register (the register held a block already produced).
+template <int NB>
+struct PairRot {
+    static constexpr int R = NB == 1 ? 4 : NB == 2 ? 8 : NB == 4 ? 8 : 16;
+    static constexpr int U = R / 2;
+    static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
+};
+
+template <int SH, int NB, int W>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
     constexpr int E = 16, N = 1024, H = 64 * SH;
+    constexpr int R = PairRot<NB>::R, U = PairRot<NB>::U;
     static_assert(NB * SH == E, "N = NB * H");
     static_assert(SH >= 2, "den rows are read 16 bytes at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -98,9 +100,220 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
     const int gw = blockIdx.x * W + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
-#ifdef CRLOT_PAIR_TRACE  // debug builds: per-wave start/end (100 MHz clock) and hardware ids
-    const uint32_t trace_t0 = uint32_t(__builtin_amdgcn_s_memrealtime());
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry =
+        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const float g = a.gain;
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
+
+    // xr[slot][q]: sample lane + 64 q of the hop in that slot; bit j of hopok:
+    // hop k + j (k = the current pair) keeps the paired regime
+    float xr[R][SH];
+    uint32_t hopok = 0;
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop0<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
+        hopok |= hop_ok<SH>(xr[h], xlo, xhi) << h;
+    }
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+
+    bool bad = false;  // this walk needs k_stft_ola_pair_fix: a pair left the paired regime or a division its exact range
+    // produce(H) of block k (values av): IEEE av / den by Markstein's correction.
+    // The divisions run for warm-up blocks too, only their stores are dropped
+    // (zero-size descriptor), so the divisor loads are used unconditionally and
+    // vmcnt bookkeeping stays exact at the next wait.
+    auto emit = [&](const float (&av)[SH], int k, const float (&dr)[2 * SH]) {
+        // Markstein is exact for acc = 0 and |acc| in [2^-64, 2^64] (finite sums
+        // here): frexp exponents in [-63, 65], zero's being 0; any lane outside
+        // flags the walk for the IEEE division of the fix-up walker
+        int ex_lo = 0, ex_hi = 0;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const int e = __builtin_amdgcn_frexp_expf(av[q]);
+            ex_lo = min(ex_lo, e);
+            ex_hi = max(ex_hi, e);
+        }
+        const bool ok = (ex_lo >= -63) & (ex_hi <= 65);
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
+        // outside Markstein's exact range the fix-up walker redoes the chunk with
+        // the IEEE division (a block of sums below 2^-64 or above 2^64)
+        bad |= !ok;
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
+                                                  k * (4 * H) + q * 256, 0);
+    };
+
+#if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
+    dev::PairTw tw;
+    dev::pair_tw_load(tw, t1, t2, lane);
+    const dev::PairTw& tw1 = tw;
+    const dev::PairTw& tw2 = tw;
+#else
+    const dev::pc* const tw1 = t1;
+    const dev::pc* const tw2 = t2;
 #endif
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
+
+    // One pair (frames k, k+1) at unroll position PH: hop k in slot S0, frame
+    // k's first block in acc[B0].
+    auto step = [&](auto phc, int k) {
+        constexpr int PH = decltype(phc)::value;
+        constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
+        // prefetch hops k+NB+1, k+NB+2 for the next pairs (their slots are free)
+        load_hop0<SH>(xr[(S0 + NB + 1) % R], rx, lane, (k + NB + 1) * H - a.pad);
+        load_hop0<SH>(xr[(S0 + NB + 2) % R], rx, lane, (k + NB + 2) * H - a.pad);
+        const bool paired = (hopok & kPairHops) == kPairHops;
+        bad |= !paired;
+        {
+            // z = frame k * w + i frame k+1 * w
+            dev::pc v[E];
+#pragma unroll
+            for (int m4 = 0; m4 < E / 4; ++m4) {
+                const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
+                const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int m = 4 * m4 + u;
+                    v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wv[u],
+                                      xr[(S0 + 1 + m / SH) % R][m % SH] * wv[u]);
+                }
+            }
+            // (frame k+1 = F past the last frame of an odd count still transforms
+            // the framed samples there -- zeros for ZERO_PAD, the padding rule's
+            // values otherwise: deterministic per stream, and never produced)
+            dev::pair_fft_fwd(v, buf, tw1, tw2, lane);
+            // both blocks' divisors (L2-resident table) during the inverse, before
+            // this pair's stores: vmcnt retires in order, so a load issued after
+            // a store would also wait for that store
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
+            load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+            dev::pair_fft_inv(v, buf, tw1, tw2, lane);
+            // output sanitize (kissfft_adapter.cc:156-163): finite here, the threshold alone
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                v[m] = dev::pc_mk(dev::sanit_scaled_finite<N>(v[m].x), dev::sanit_scaled_finite<N>(v[m].y));
+            // push_frame_AoS of both frames: fma(fma(o, w, 0), g, acc), the window
+            // product of both parts in one packed multiply (v * (w, w) gives -0
+            // only where fma(o, w, 0) gives +0, and fma(-0, g, acc) == fma(+0, g, acc))
+#pragma unroll
+            for (int m4 = 0; m4 < E / 4; ++m4) {
+                const dev::pc* w2 = reinterpret_cast<const dev::pc*>(ws4 + m4 * 256 + lane * 4);
+                const dev::pc wl = w2[0], wh = w2[1];
+                v[4 * m4 + 0] = v[4 * m4 + 0] * dev::pc{wl.x, wl.x};
+                v[4 * m4 + 1] = v[4 * m4 + 1] * dev::pc{wl.y, wl.y};
+                v[4 * m4 + 2] = v[4 * m4 + 2] * dev::pc{wh.x, wh.x};
+                v[4 * m4 + 3] = v[4 * m4 + 3] * dev::pc{wh.y, wh.y};
+            }
+            // frame k -> blocks k .. k+NB-1 (the last opens), produce block k
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                float& r = acc[(B0 + m / SH) % NB][m % SH];
+                r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
+            }
+            emit(acc[B0], k, dr0);
+            // frame k+1 -> blocks k+1 .. k+NB (k+NB opens in acc[B0]), produce block k+1
+            // (past the chunk when k+1 == f1: dropped like a warm-up store)
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
+                r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
+            }
+            emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
+        }
+        hopok = (hopok | hop_ok<SH>(xr[(S0 + NB + 1) % R], xlo, xhi) << (NB + 1) |
+                 hop_ok<SH>(xr[(S0 + NB + 2) % R], xlo, xhi) << (NB + 2)) >> 2;
+    };
+    for (int k = fs; k < f1; k += 2 * U) {
+        step(std::integral_constant<int, 0>(), k);
+        if constexpr (U > 1) {
+            if (k + 2 >= f1) break;
+            step(std::integral_constant<int, 1>(), k + 2);
+        }
+        if constexpr (U > 2) {
+            if (k + 4 >= f1) break;
+            step(std::integral_constant<int, 2>(), k + 4);
+            if (k + 6 >= f1) break;
+            step(std::integral_constant<int, 3>(), k + 6);
+        }
+        if constexpr (U > 4) {
+            if (k + 8 >= f1) break;
+            step(std::integral_constant<int, 4>(), k + 8);
+            if (k + 10 >= f1) break;
+            step(std::integral_constant<int, 5>(), k + 10);
+            if (k + 12 >= f1) break;
+            step(std::integral_constant<int, 6>(), k + 12);
+            if (k + 14 >= f1) break;
+            step(std::integral_constant<int, 7>(), k + 14);
+        }
+    }
+    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if (lane == 0) a.t.pflags[gw] = any_bad ? 1u : 0u;
+}
+
+
+// K_pair fix-up walker k_stft_ola_pair_fix: the walk with both regimes, run
+// after k_stft_ola_pair over the chunks it flagged (never on finite audio; the
+// launch exits at once otherwise).  Its paired pairs compute exactly what the
+// paired-only walker computes, so a redone chunk has the same bits wherever
+// both regimes would have agreed.
+//  * paired: every sample is 0 or px_lo <= |x| <= px_hi (DevTables, set on the
+//    host from the window and the spectral gain).  Then sanitize(x*w) == x*w up
+//    to the sign of a zero, which no output bit can see (a nonzero value plus a
+//    zero of either sign is exact, and the output sanitize maps both zeros to
+//    +0); no transform can overflow; and the output sanitize reduces to its
+//    threshold test.
+//  * unpaired (a NaN, Inf, huge or tiny sample): each frame gets a transform of
+//    its own (imaginary part zero) with the full sanitize on both sides, so a
+//    frame whose spectrum overflows cannot leak into its neighbour -- the
+//    reference transforms every frame alone (kissfft_adapter.cc:83-168).
+template <int SH, int NB, int W, bool HAS_GAIN>
+__global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_fix(const FusedArgs a) {
+    constexpr int E = 16, N = 1024, H = 64 * SH;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    {  // only walkers the paired-only pass flagged; whole workgroups leave together
+        const int64_t w0 = int64_t(blockIdx.x) * W;
+        const int t = threadIdx.x;
+        const bool mine = t < W && w0 + t < int64_t(a.n_streams) * a.n_chunks && (a.fix_all || a.t.pflags[w0 + t] != 0u);
+        if (!__syncthreads_or(mine)) return;
+    }
+    dev::pc* t1 = reinterpret_cast<dev::pc*>(smem + PairLds<W>::t1);
+    dev::pc* t2s = reinterpret_cast<dev::pc*>(smem + PairLds<W>::t2);
+    float* wa4 = reinterpret_cast<float*>(smem + PairLds<W>::wa);
+    float* ws4 = reinterpret_cast<float*>(smem + PairLds<W>::ws);
+    {
+        const dev::pc* g1 = reinterpret_cast<const dev::pc*>(a.t.ptw);
+        for (int i = threadIdx.x; i < 15 * 64 + 3 * 16; i += 64 * W) t1[i] = g1[i];  // t1 | t2
+        for (int i = threadIdx.x; i < N; i += 64 * W) {
+            const int l = i & 63, m = i >> 6;  // tap n = l + 64 m
+            const int d = (m >> 2) * 256 + l * 4 + (m & 3);
+            wa4[d] = a.t.wa[i];
+            ws4[d] = a.t.wsn[i];
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
+    const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
+    const int gw = blockIdx.x * W + wave;
+    if (gw >= a.n_streams * a.n_chunks || (!a.fix_all && a.t.pflags[gw] == 0u)) return;
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -132,11 +345,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
 #pragma unroll
         for (int m4 = 0; m4 < E / 4; ++m4) {
-#ifdef CRLOT_ABL_NOWIN  // timing-only ablation: no window reads, wrong results
-            const float4 w = make_float4(1e-3f, 2e-3f, 1e-3f, 2e-3f);
-#else
             const float4 w = *reinterpret_cast<const float4*>(ws4 + m4 * 256 + lane * 4);
-#endif
             const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -167,18 +376,10 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
             for (int q = 0; q < SH; ++q) o[q] = acc[0][q] / dr[q];
         }
-#ifdef CRLOT_ABL_NODIV  // timing-only ablation
-#pragma unroll
-        for (int q = 0; q < SH; ++q) o[q] = acc[0][q] * dr[SH + q];
-#endif
         // warm-up blocks (k < f0) store through a zero-size descriptor: every
         // lane is out of range and the store is dropped.  No branch around the
         // stores, so vmcnt bookkeeping stays exact at the next divisor wait.
-#ifdef CRLOT_ABL_NOSTORE  // timing-only ablation: every store dropped
-        const __amdgpu_buffer_rsrc_t rk = ry_null;
-#else
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-#endif
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
@@ -191,10 +392,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         for (int q = 0; q < SH; ++q) acc[NB - 1][q] = 0.f;
     };
 
-#ifdef CRLOT_PAIR_PHASES
-    uint32_t ph[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t ph_last = __builtin_amdgcn_s_memtime();
-#endif
 #if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
     dev::PairTw tw;
     dev::pair_tw_load(tw, t1, t2, lane);
@@ -205,11 +402,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const dev::pc* const tw2 = t2;
 #endif
     auto transform = [&](dev::pc (&v)[E]) {  // forward, spectral gain, inverse (unnormalised)
-#ifdef CRLOT_ABL_NOFFT  // timing-only ablation: the memory stream alone
-        return;
-#endif
         dev::pair_fft_fwd(v, buf, tw1, tw2, lane);
-        PHASE(2);
         if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins
             const int gbase = dev::pair_bin_lane(lane);
 #pragma unroll
@@ -220,30 +413,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             }
         }
         dev::pair_fft_inv(v, buf, tw1, tw2, lane);
-#ifdef CRLOT_ABL_DUMMY  // timing-only: CRLOT_ABL_DUMMY extra independent VALU ops per transform
-        {
-            float d[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = v[i].x;
-#pragma unroll
-            for (int i = 0; i < CRLOT_ABL_DUMMY; ++i) {
-#if defined(CRLOT_ABL_DUMMY_PERM)
-                if ((i & 1) == 0) {
-                    const unsigned a0 = __builtin_bit_cast(unsigned, d[i & 7]);
-                    const unsigned b0 = __builtin_bit_cast(unsigned, d[(i + 1) & 7]);
-                    const auto r = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
-                    const unsigned r0 = r[0], r1 = r[1];
-                    d[i & 7] = __builtin_bit_cast(float, r0);
-                    d[(i + 1) & 7] = __builtin_bit_cast(float, r1);
-                }
-#else
-                asm volatile("v_add_f32 %0, %0, %0" : "+v"(d[i & 7]));
-#endif
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v[i].x = d[i];
-        }
-#endif
     };
     constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
     for (int k = fs; k < f1; k += 2) {
@@ -252,27 +421,19 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
         load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
         const bool paired = (hopok & kPairHops) == kPairHops;
-        PHASE(0);
         if (paired) {
-            const bool partner = k + 1 < a.F;  // frame k+1 exists (even past this chunk)
             dev::pc v[E];
 #pragma unroll
             for (int m4 = 0; m4 < E / 4; ++m4) {
-#ifdef CRLOT_ABL_NOWIN
-                const float4 w = make_float4(0.5f, 0.25f, 0.5f, 0.25f);
-#else
                 const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
-#endif
                 const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int m = 4 * m4 + u;
-                    v[m] = dev::pc_mk(xin[m] * wv[u], partner ? xin[m + SH] * wv[u] : 0.0f);
+                    v[m] = dev::pc_mk(xin[m] * wv[u], xin[m + SH] * wv[u]);
                 }
             }
-            PHASE(1);
             transform(v);
-            PHASE(3);
             // both blocks' divisors before this pair's stores: vmcnt retires in
             // order, so a load issued after a store also waits for that store
             float dr0[2 * SH], dr1[2 * SH];
@@ -284,7 +445,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                 accumulate(v, true, true);
                 emit(k + 1, dr1);
             }
-            PHASE(4);
         } else {  // unpaired: frames k and k+1 alone, full sanitize (never taken on finite audio)
             const int npass = min(2, f1 - k);
             for (int p = 0; p < npass; ++p) {
@@ -312,24 +472,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
         for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
     }
-#ifdef CRLOT_PAIR_PHASES
-    PHASE(5);
-    if (lane == 0 && gw < (1 << 16)) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) g_pair_phase[8 * gw + i] = ph[i];
-        g_pair_phase[8 * gw + 6] = uint32_t((f1 - fs + 1) / 2);
-        g_pair_phase[8 * gw + 7] = 1;
-    }
-#endif
-#ifdef CRLOT_PAIR_TRACE
-    if (lane == 0 && gw < (1 << 16)) {
-        const uint32_t t1e = uint32_t(__builtin_amdgcn_s_memrealtime());
-        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20); // HW_REG_XCC_ID
-        uint4* tr = reinterpret_cast<uint4*>(g_pair_trace);
-        tr[gw] = make_uint4(trace_t0, t1e, hw, xcc);
-    }
-#endif
 }
 
 
@@ -347,15 +489,46 @@ int pair_waves_per_cu() {
     return std::min(int(163840 / PairLds<kPairWaves>::bytes) * kPairWaves, 4 * CRLOT_PAIR_MIN_WAVES);
 }
 
+// CRLOT_PAIR_NOFIX=1 (diagnostics: how much the fix-up walker redoes) skips it.
+bool pair_nofix() {
+    static const bool v = [] {
+        const char* e = std::getenv("CRLOT_PAIR_NOFIX");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+// The paired-only walker where it holds its registers without spilling: hops
+// of 256 (SH = 4; SH = 8 spills 9 VGPRs) without a spectral gain.  Other hops, a gain, and
+// reflect / edge padding run the two-regime walker over every chunk.
+template <int SH>
+constexpr bool pair_hot(bool gain) {
+    return SH == 4 && !gain;
+}
+
 template <int SH>
 hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     constexpr int NB = 16 / SH, W = kPairWaves;
-    auto k = a.t.gain ? k_stft_ola_pair<SH, NB, W, true> : k_stft_ola_pair<SH, NB, W, false>;
     const size_t lds = PairLds<W>::bytes;
-    hipError_t e = set_lds(k, lds);
-    if (e != hipSuccess) return e;
     const int64_t grid = (waves + W - 1) / W;
-    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
+    hipError_t e;
+    auto kf = a.t.gain ? k_stft_ola_pair_fix<SH, NB, W, true> : k_stft_ola_pair_fix<SH, NB, W, false>;
+    if ((e = set_lds(kf, lds)) != hipSuccess) return e;
+    if (!a.t.pflags || a.t.pflags_len < waves) return hipErrorInvalidValue;
+    if constexpr (pair_hot<SH>(false)) {
+        if (a.pad_mode == 0 && !a.t.gain) {
+            auto k = k_stft_ola_pair<SH, NB, W>;
+            if ((e = set_lds(k, lds)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if (pair_nofix()) return hipSuccess;  // diagnostics only: flagged chunks stay wrong
+            hipLaunchKernelGGL(kf, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
+            return hipGetLastError();
+        }
+    }
+    FusedArgs b = a;
+    b.fix_all = 1;
+    hipLaunchKernelGGL(kf, dim3(unsigned(grid)), dim3(64 * W), lds, stream, b);
     return hipGetLastError();
 }
 
@@ -393,16 +566,3 @@ std::vector<float> build_pair_twiddles() {
 
 }  // namespace crlot
 
-#ifdef CRLOT_PAIR_TRACE
-extern "C" int crlot_debug_pair_trace(void* host, int64_t bytes) {
-    return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(crlot::fk::g_pair_trace),
-                                   size_t(std::min<int64_t>(bytes, sizeof(crlot::fk::g_pair_trace)))));
-}
-#endif
-
-#ifdef CRLOT_PAIR_PHASES
-extern "C" int crlot_debug_pair_phases(void* host, int64_t bytes) {
-    return int(hipMemcpyFromSymbol(host, HIP_SYMBOL(crlot::fk::g_pair_phase),
-                                   size_t(std::min<int64_t>(bytes, sizeof(crlot::fk::g_pair_phase)))));
-}
-#endif
