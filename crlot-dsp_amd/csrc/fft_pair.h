@@ -90,6 +90,41 @@ __device__ __forceinline__ pc pc_mulc(pc a, pc w) {
 }
 template <bool INV>
 __device__ __forceinline__ pc pc_tw(pc a, pc w) { return INV ? pc_mulc(a, w) : pc_mul(a, w); }
+
+// The same two instructions issued apart: a VOP3P result read by the next VOP3P
+// right away costs a wait state (s_nop 0) on gfx950, so a run of rotations is
+// issued skewed -- product i+1 before the fma of i (pc_tw_run).
+template <bool INV>
+__device__ __forceinline__ pc pc_tw_p(pc a, pc w) {
+    pc p;
+    if constexpr (INV)
+        asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(p) : "v"(a), "v"(w));
+    else
+        asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(p) : "v"(a), "v"(w));
+    return p;
+}
+template <bool INV>
+__device__ __forceinline__ pc pc_tw_f(pc a, pc w, pc p) {
+    pc r;
+    if constexpr (INV)
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(w), "v"(p));
+    else
+        asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+            : "=v"(r) : "v"(a), "v"(w), "v"(p));
+    return r;
+}
+// v[idx[i]] *= w[i] (conj for INV), i < K, skewed by one.
+template <bool INV, int K, typename WF>
+__device__ __forceinline__ void pc_tw_run(pc* v, const int (&idx)[K], WF w) {
+    pc pp = pc_tw_p<INV>(v[idx[0]], w(0));
+#pragma unroll
+    for (int i = 1; i < K; ++i) {
+        const pc pn = pc_tw_p<INV>(v[idx[i]], w(i));
+        v[idx[i - 1]] = pc_tw_f<INV>(v[idx[i - 1]], w(i - 1), pp);
+        pp = pn;
+    }
+    v[idx[K - 1]] = pc_tw_f<INV>(v[idx[K - 1]], w(K - 1), pp);
+}
 // a + m(b) and a - m(b), m = multiply by -i (forward) / +i (inverse)
 template <bool INV>
 __device__ __forceinline__ pc pc_add_mi(pc a, pc b) { return INV ? pk_add_sw_nl(a, b) : pk_add_sw_nh(a, b); }
@@ -126,6 +161,28 @@ __device__ __forceinline__ pc rot16(pc a) {
     return a;
 }
 
+// rot16 in two halves: _a (the product, or the W8-type add) and _b (the fma, or
+// the scale by sqrt(1/2)).
+template <bool INV, int J>
+__device__ __forceinline__ pc rot16_a(pc a) {
+    constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+    if constexpr (J == 1) return pc_tw_p<INV>(a, (pc){c1, -s1});
+    if constexpr (J == 3) return pc_tw_p<INV>(a, (pc){s1, -c1});
+    if constexpr (J == 9) return pc_tw_p<INV>(a, (pc){-c1, s1});
+    if constexpr (J == 2) return INV ? pk_add_sw_nl(a, a) : pk_add_sw_nh(a, a);
+    if constexpr (J == 6) return INV ? pk_w6i(a) : pk_w6f(a);
+    return a;
+}
+template <bool INV, int J>
+__device__ __forceinline__ pc rot16_b(pc a, pc m) {
+    constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+    constexpr float h = 0.70710678118654752440f;
+    if constexpr (J == 1) return pc_tw_f<INV>(a, (pc){c1, -s1}, m);
+    if constexpr (J == 3) return pc_tw_f<INV>(a, (pc){s1, -c1}, m);
+    if constexpr (J == 9) return pc_tw_f<INV>(a, (pc){-c1, s1}, m);
+    return (pc){h, h} * m;  // J = 2, 6
+}
+
 // In-place 16-point DFT, natural order in and out: X[k] = sum_n x[n] W16^{+-nk}.
 // n = 4 n1 + n2, k = k1 + 4 k2: four DFT4 over n1, twiddles W16^{n2 k1}, four
 // DFT4 over n2 (outputs renamed in registers, no data movement).
@@ -133,16 +190,27 @@ template <bool INV>
 __device__ __forceinline__ void pdft16(pc (&x)[16]) {
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) pdft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
-    // a[n2][k1] now at x[n2 + 4 k1]; multiply by W16^{n2 k1}
-    x[1 + 4 * 1] = rot16<INV, 1>(x[1 + 4 * 1]);
-    x[1 + 4 * 2] = rot16<INV, 2>(x[1 + 4 * 2]);
-    x[1 + 4 * 3] = rot16<INV, 3>(x[1 + 4 * 3]);
-    x[2 + 4 * 1] = rot16<INV, 2>(x[2 + 4 * 1]);
+    // a[n2][k1] now at x[n2 + 4 k1]; multiply by W16^{n2 k1} (first halves of the
+    // two-instruction rotations issued one ahead of their second halves)
     // (W^4 = -i on x[2 + 4 * 2] is applied inside the k1 = 2 DFT4 below)
-    x[2 + 4 * 3] = rot16<INV, 6>(x[2 + 4 * 3]);
-    x[3 + 4 * 1] = rot16<INV, 3>(x[3 + 4 * 1]);
-    x[3 + 4 * 2] = rot16<INV, 6>(x[3 + 4 * 2]);
-    x[3 + 4 * 3] = rot16<INV, 9>(x[3 + 4 * 3]);
+    {
+        pc m5 = rot16_a<INV, 1>(x[5]);
+        const pc m9 = rot16_a<INV, 2>(x[9]);
+        x[5] = rot16_b<INV, 1>(x[5], m5);
+        const pc m13 = rot16_a<INV, 3>(x[13]);
+        x[9] = rot16_b<INV, 2>(x[9], m9);
+        const pc m6 = rot16_a<INV, 2>(x[6]);
+        x[13] = rot16_b<INV, 3>(x[13], m13);
+        const pc m14 = rot16_a<INV, 6>(x[14]);
+        x[6] = rot16_b<INV, 2>(x[6], m6);
+        const pc m7 = rot16_a<INV, 3>(x[7]);
+        x[14] = rot16_b<INV, 6>(x[14], m14);
+        const pc m11 = rot16_a<INV, 6>(x[11]);
+        x[7] = rot16_b<INV, 3>(x[7], m7);
+        m5 = rot16_a<INV, 9>(x[15]);
+        x[11] = rot16_b<INV, 6>(x[11], m11);
+        x[15] = rot16_b<INV, 9>(x[15], m5);
+    }
     pdft4<INV>(x[0], x[1], x[2], x[3]);
     pdft4<INV>(x[4], x[5], x[6], x[7]);
     pdft4<INV, true>(x[8], x[9], x[10], x[11]);
@@ -281,8 +349,8 @@ __device__ __forceinline__ void pair_tw_load(PairTw& tw, const pc* t1, const pc*
 }
 template <bool INV>
 __device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const PairTw& tw, int) {
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) v[k1] = pc_tw<INV>(v[k1], tw.w1[k1 - 1]);
+    constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+    pc_tw_run<INV>(v, idx, [&](int i) { return tw.w1[i]; });
 }
 __device__ __forceinline__ pc pair_t2(const pc* t2, int c) { return t2[16 * (c - 1)]; }
 __device__ __forceinline__ pc pair_t2(const PairTw& tw, int c) { return tw.w2[c - 1]; }
@@ -297,10 +365,10 @@ __device__ __forceinline__ void pair_fft_fwd(pc (&v)[16], pc* buf, const T1& t1,
     lane_reg_swap_any<CRLOT_PAIR_SWAP_LDS>(v, buf, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) pdft4<false>(v[j], v[j + 4], v[j + 8], v[j + 12]);
-#pragma unroll
-    for (int c = 1; c < 4; ++c)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mul(v[j + 4 * c], pair_t2(t2, c));
+    {
+        constexpr int idx[12] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+        pc_tw_run<false>(v, idx, [&](int i) { return pair_t2(t2, 1 + i / 4); });
+    }
     transpose16(v, buf, lane);
     pdft16<false>(v);
 }
@@ -310,10 +378,10 @@ template <typename T1, typename T2>
 __device__ __forceinline__ void pair_fft_inv(pc (&v)[16], pc* buf, const T1& t1, const T2& t2, int lane) {
     pdft16<true>(v);
     transpose16(v, buf, lane);
-#pragma unroll
-    for (int c = 1; c < 4; ++c)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j + 4 * c] = pc_mulc(v[j + 4 * c], pair_t2(t2, c));
+    {
+        constexpr int idx[12] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+        pc_tw_run<true>(v, idx, [&](int i) { return pair_t2(t2, 1 + i / 4); });
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) pdft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
     lane_reg_swap_any<CRLOT_PAIR_SWAP_LDS>(v, buf, lane);

@@ -101,6 +101,23 @@ __device__ __forceinline__ uint32_t hop_ok(const float* h, float lo, float hi) {
     return __builtin_amdgcn_ballot_w64(bad) == 0 ? 1u : 0u;
 }
 
+// hop_ok on the bit patterns: with u = |x| as bits (float order == unsigned
+// order for |x|, NaN above every finite bit pattern), a sample keeps the regime
+// iff u == 0 or lo_bits <= u <= hi_bits, i.e. u <= hi_bits and u - 1 >= lo_bits - 1
+// (unsigned, 0 wrapping to the top): per sample an and, a subtract and half a
+// max3 / min3, one compare pair per hop.
+template <int SH>
+__device__ __forceinline__ uint32_t hop_ok_bits(const float* h, uint32_t lo_bits, uint32_t hi_bits) {
+    uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) {
+        const uint32_t u = __builtin_bit_cast(uint32_t, h[q]) & 0x7fffffffu;
+        mx = max(mx, u);
+        mn = min(mn, u - 1u);
+    }
+    return __builtin_amdgcn_ballot_w64((mx > hi_bits) | (mn < lo_bits - 1u)) == 0 ? 1u : 0u;
+}
+
 // den / rden of OLA block b for this lane (DevTables::pden: [block][lane][den SH | rden SH]).
 template <int SH>
 __device__ __forceinline__ void load_den(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int lane, int b) {

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const float g = a.gain;
-    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
+    const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
     // xr[slot][q]: sample lane + 64 q of the hop in that slot; bit j of hopok:
     // hop k + j (k = the current pair) keeps the paired regime
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
     for (int h = 0; h <= NB; ++h) {
         load_hop0<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
-        hopok |= hop_ok<SH>(xr[h], xlo, xhi) << h;
+        hopok |= hop_ok_bits<SH>(xr[h], xlo_b, xhi_b) << h;
     }
     float acc[NB][SH];
 #pragma unroll
@@ -203,10 +203,19 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
             load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
             dev::pair_fft_inv(v, buf, tw1, tw2, lane);
-            // output sanitize (kissfft_adapter.cc:156-163): finite here, the threshold alone
+            // output sanitize (kissfft_adapter.cc:156-163): finite here, so only its
+            // threshold |v| < 1e-30 N (= 2^-89.66 N / 1024) can act, and only on a
+            // nonzero v.  frexp exponents find every 0 < |v| < 2^-89 (zero's is 0):
+            // one such value sends the walk to k_stft_ola_pair_fix (a value in
+            // [1e-30 N, 2^-89) too, harmlessly), otherwise the sanitize is the identity.
+            static_assert(N == 1024, "threshold exponent");
+            {
+                int e[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int m = 0; m < E; ++m)
-                v[m] = dev::pc_mk(dev::sanit_scaled_finite<N>(v[m].x), dev::sanit_scaled_finite<N>(v[m].y));
+                for (int m = 0; m < E; ++m)
+                    e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
+                bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -89;
+            }
             // push_frame_AoS of both frames: fma(fma(o, w, 0), g, acc), the window
             // product of both parts in one packed multiply (v * (w, w) gives -0
             // only where fma(o, w, 0) gives +0, and fma(-0, g, acc) == fma(+0, g, acc))
@@ -235,8 +244,12 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             }
             emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
         }
-        hopok = (hopok | hop_ok<SH>(xr[(S0 + NB + 1) % R], xlo, xhi) << (NB + 1) |
-                 hop_ok<SH>(xr[(S0 + NB + 2) % R], xlo, xhi) << (NB + 2)) >> 2;
+#ifdef CRLOT_ABL_NOHOPCHK  // timing-only ablation
+        hopok = ~0u;
+#else
+        hopok = (hopok | hop_ok_bits<SH>(xr[(S0 + NB + 1) % R], xlo_b, xhi_b) << (NB + 1) |
+                 hop_ok_bits<SH>(xr[(S0 + NB + 2) % R], xlo_b, xhi_b) << (NB + 2)) >> 2;
+#endif
     };
     for (int k = fs; k < f1; k += 2 * U) {
         step(std::integral_constant<int, 0>(), k);

@@ -15,7 +15,7 @@ for d in sorted(glob.glob("gpurun_out/cyc_*/")):
     cc = glob.glob(d + "run_counter_collection.csv"); kt = glob.glob(d + "run_kernel_trace.csv")
     if not cc or not kt: continue
     tr = {r["Dispatch_Id"]: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(kt[0]))}
-    g = {r["Dispatch_Id"]: float(r["Counter_Value"]) / 8 for r in csv.DictReader(open(cc[0])) if "stft_ola" in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE"}
+    g = {r["Dispatch_Id"]: float(r["Counter_Value"]) / 8 for r in csv.DictReader(open(cc[0])) if "stft_ola" in r["Kernel_Name"] and "_fix" not in r["Kernel_Name"] and r["Counter_Name"] == "GRBM_GUI_ACTIVE"}
     ids = sorted(g, key=int)[4:]
     cyc = sum(g[i] for i in ids) / len(ids); us = sum(tr[i] for i in ids) / len(ids) / 1e3
     print(f"{os.path.basename(d[:-1])[4:]:24s} cycles {cyc/1e6:6.3f}M  kernel {us:7.1f} us  clock {cyc/us/1e3:5.3f} GHz")
