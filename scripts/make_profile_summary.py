@@ -26,48 +26,63 @@ if stats:
     shutil.copy(stats[0], f"profiles/{tag}_kernel_stats.csv")
 
 
-def counters(sub, pat="stft_ola"):
+def trace_rows():
+    kt = glob.glob(f"{src}/trace/run_kernel_trace.csv")
+    return list(csv.DictReader(open(kt[0]))) if kt else []
+
+
+# The dominant kernel: the stft_ola kernel with the largest total time in the
+# trace; its headline dispatches are the most common grid size among them (the
+# bench also times the 8192-stream strong-scaling phase with a larger grid).
+rows = [r for r in trace_rows() if "stft_ola" in r["Kernel_Name"]]
+tot = collections.Counter()
+for r in rows:
+    tot[r["Kernel_Name"]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+kname = tot.most_common(1)[0][0] if tot else "k_stft_ola"
+grids = collections.Counter(r["Grid_Size_X"] for r in rows if r["Kernel_Name"] == kname)
+grid = grids.most_common(1)[0][0] if grids else None
+ds = sorted(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
+            if r["Kernel_Name"] == kname and r["Grid_Size_X"] == grid)
+med = ds[len(ds) // 2] if ds else None
+mn = ds[0] if ds else None
+dur = sum(ds) / len(ds) if ds else None
+others = sorted({r["Kernel_Name"] for r in rows} - {kname})
+
+
+def counters(sub, name):
+    """Mean per-dispatch counter values of kernel `name` (prof_driver runs only
+    the headline workload, so every dispatch of it is a headline launch)."""
     agg = collections.defaultdict(list)
     for f in glob.glob(f"{src}/{sub}/run_counter_collection.csv"):
         per = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
-            if pat in r["Kernel_Name"]:
+            if r["Kernel_Name"] == name:
                 per[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
-                kname = r["Kernel_Name"]
-                vg = r.get("VGPR_Count")
         for c in per.values():
             for k, v in c.items():
                 agg[k].append(v)
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def hbm_of(p):
+    if "FETCH_SIZE" in p and "WRITE_SIZE" in p:
+        return (2 * p["FETCH_SIZE"] + p["WRITE_SIZE"]) * 1024
+    return None
+
+
 pmc = {}
 for sub in ("fetch", "write", "sq", "lds"):
-    pmc.update(counters(sub))
+    pmc.update(counters(sub, kname))
 S, T, N, H = 1024, 480000, 1024, 256
 alg_read = S * T * 4
 alg_write = S * T * 4
-hbm = None
-if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-    hbm = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
-dur = None
-tr = glob.glob(f"{src}/trace/run_kernel_stats.csv")
-if tr:
-    for r in csv.DictReader(open(tr[0])):
-        if "stft_ola" in r["Name"]:
-            dur = float(r["AverageNs"])
-# per-dispatch durations of the fused kernel (the stats average includes warm-up launches)
-kname, med, mn = "k_stft_ola", None, None
-kt = glob.glob(f"{src}/trace/run_kernel_trace.csv")
-if kt:
-    ds = []
-    for r in csv.DictReader(open(kt[0])):
-        if "stft_ola" in r["Kernel_Name"]:
-            kname = r["Kernel_Name"]
-            ds.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    if ds:
-        ds.sort()
-        med, mn = ds[len(ds) // 2], ds[0]
+hbm = hbm_of(pmc)
+aux = {}
+for o in others:
+    po = {}
+    for sub in ("fetch", "write"):
+        po.update(counters(sub, o))
+    aux[o] = {"hbm_bytes_per_launch": hbm_of(po), "pmc_per_launch": po}
 # bench.py's own HIP-event kernel time from the same profiled run (trace.log)
 bench_ms = None
 for lf in (f"{src}/trace.log",):
@@ -90,6 +105,8 @@ out = {
     "hbm_over_algorithmic": None if hbm is None else hbm / (alg_read + alg_write),
     "fetch_bytes_corrected": None if "FETCH_SIZE" not in pmc else 2 * pmc["FETCH_SIZE"] * 1024,
     "write_bytes": None if "WRITE_SIZE" not in pmc else pmc["WRITE_SIZE"] * 1024,
+    "headline_grid": grid,
+    "aux_kernels": aux,
     "note": __doc__.strip(),
 }
 json.dump(out, open(f"profiles/{tag}_pmc_summary.json", "w"), indent=1)
