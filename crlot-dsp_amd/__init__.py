@@ -126,6 +126,15 @@ def lib():
         "crlot_stream_reset": ([vp], C.c_int),
         "crlot_stream_push_hop": ([vp, vp, vp, C.POINTER(i32), vp], C.c_int),
         "crlot_stream_set_layout": ([vp, i32], C.c_int),
+        "crlot_stream_rt_create": ([vp, i32, i32, i32, C.POINTER(vp)], C.c_int),
+        "crlot_stream_rt_destroy": ([vp], None),
+        "crlot_stream_rt_reset": ([vp], C.c_int),
+        "crlot_stream_rt_push_hop": ([vp, vp, vp, C.POINTER(i32)], C.c_int),
+        "crlot_stream_rt_input_slot": ([vp], vp),
+        "crlot_stream_rt_submit": ([vp, C.POINTER(i64)], C.c_int),
+        "crlot_stream_rt_wait": ([vp, i64, C.POINTER(vp), C.POINTER(i32)], C.c_int),
+        "crlot_stream_rt_info": ([vp, C.POINTER(i64), C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
+        "crlot_stream_rt_set_idle_timeout": ([vp, C.c_double, C.c_double], C.c_int),
         "crlot_wav_reader_open": ([C.c_char_p, C.POINTER(vp)], C.c_int),
         "crlot_wav_reader_close": ([vp], None),
         "crlot_wav_reader_info": ([vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -512,6 +521,55 @@ class Stream:
         _check(lib().crlot_stream_push_hop(self._h, hop.data_ptr(), out.data_ptr(), C.byref(em), s),
                "crlot_stream_push_hop")
         return out, em.value
+
+
+class StreamRT:
+    """Resident low-latency per-hop path (config 4) for hops in host memory: the
+    crlot_stream_rt_* entries.  Same contract and bits as Stream; hops are numpy
+    float32 arrays (channels, H), or (H, channels) if interleaved."""
+
+    def __init__(self, plan: Plan, channels: int, interleaved: bool = False, depth: int = 4):
+        self.plan = plan
+        self.channels = channels
+        self.interleaved = interleaved
+        self.depth = depth
+        h = C.c_void_p()
+        _check(lib().crlot_stream_rt_create(plan._h, channels, int(interleaved), depth, C.byref(h)),
+               "crlot_stream_rt_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().crlot_stream_rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def reset(self):
+        _check(lib().crlot_stream_rt_reset(self._h))
+
+    def set_idle_timeout(self, idle_seconds: float, hop_timeout_seconds: float = 2.0):
+        _check(lib().crlot_stream_rt_set_idle_timeout(self._h, idle_seconds, hop_timeout_seconds))
+
+    def push_hop(self, hop, out=None) -> tuple:
+        """Returns (out, emitted) where emitted is 0 or H (out untouched when 0)."""
+        import numpy as np
+        hop = np.ascontiguousarray(hop, dtype=np.float32)
+        if out is None:
+            out = np.zeros_like(hop)
+        em = C.c_int32()
+        _check(lib().crlot_stream_rt_push_hop(self._h, hop.ctypes.data, out.ctypes.data, C.byref(em)),
+               "crlot_stream_rt_push_hop")
+        return out, em.value
+
+    def info(self) -> dict:
+        hops, ns, run = C.c_int64(), C.c_double(), C.c_int32()
+        _check(lib().crlot_stream_rt_info(self._h, C.byref(hops), C.byref(ns), C.byref(run)))
+        return {"hops": hops.value, "last_device_ns": ns.value, "running": bool(run.value)}
 
 
 # ----------------------------------------------------------------- Framer / OLAAccumulator

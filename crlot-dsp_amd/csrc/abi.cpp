@@ -8,7 +8,10 @@
 // handles any hop and N up to 4096 through a plan-owned frame workspace.
 // There is no CPU fallback: an unsupported shape is CRLOT_EUNSUPPORTED.
 #include <hip/hip_runtime.h>
+#include <xmmintrin.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -28,6 +31,7 @@ struct crlot_plan {
     // host copies
     std::vector<float> window, norm;
     bool has_gain = false;
+    uint64_t table_gen = 0;   // bumped by every table / gain update (resident kernels re-stage)
     // device tables
     float* d_wa = nullptr;
     float* d_ws = nullptr;
@@ -216,6 +220,7 @@ int upload_window_tables(crlot_plan* p, hipStream_t s) {
     }
     p->px_lo = wmin > 0.0 ? std::nextafter(float(double(1e-30f) / wmin * (1.0 + 0x1p-20)), INFINITY) : 0.0f;
     p->px_hi = float(0x1p64 / std::max(1.0, wmax));
+    p->table_gen += 1;
     Upload up(p);
     if (p->d_pden) {  // [block][lane][den SH | rden SH], den at block offset lane + lanes q
         const int h = p->geo.h, lanes = p->geo.n == 4096 ? 256 : p->geo.n == 2048 ? 128 : 64, sh = h / lanes;
@@ -449,6 +454,7 @@ int crlot_plan_upload_tables(crlot_plan* p, const float* window, const float* no
 int crlot_plan_set_spectral_gain_async(crlot_plan* p, const float* gain, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     DeviceGuard g(p->device);
+    p->table_gen += 1;
     if (!gain) {
         p->has_gain = false;
         return CRLOT_OK;
@@ -853,6 +859,306 @@ int crlot_stream_push_hop(crlot_stream* st, const float* d_in, float* d_out, int
     if (emitted) *emitted = (st->q >= nb - 1) ? int32_t(H) : 0;
     st->q += 1;
     return CRLOT_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ resident streaming
+// K_stream_rt (stream_rt.hip): one resident kernel per object, hops through
+// pinned host memory.  The host side here: the rings, the doorbell, the wait,
+// (re)launching the kernel when it is not running (first hop, after an idle
+// exit, after a table update), and stopping it for reset / destroy.
+struct crlot_stream_rt {
+    crlot_plan* plan = nullptr;
+    int channels = 0, interleaved = 0, depth = 0, wgs = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;   // recorded after each launch: complete = kernel gone
+    bool launched = false;
+    uint64_t gen = 0;          // plan->table_gen the running kernel staged
+    crlot::RtCtl* ctl = nullptr;
+    float* in_ring = nullptr;
+    float* out_ring = nullptr;
+    crlot::RtCtl* d_ctl = nullptr;  // device views of the pinned blocks
+    float* d_in_ring = nullptr;
+    float* d_out_ring = nullptr;
+    float* d_state = nullptr;
+    size_t state_floats = 0;
+    uint64_t q = 0;            // hops submitted
+    uint64_t idle_ticks = 0;
+    double tick_ns = 10.0;
+    int64_t timeout_us = 2000000;
+};
+
+namespace {
+
+// dst[c * rows + r] = src[r * cols + c]: 4x4 SSE blocks (x86-64 baseline) where
+// the shape allows, scalar otherwise.
+void transpose_f32(const float* src, float* dst, size_t rows, size_t cols) {
+    if (rows % 4 == 0 && cols % 4 == 0) {
+        for (size_t r = 0; r < rows; r += 4)
+            for (size_t c = 0; c < cols; c += 4) {
+                __m128 a = _mm_loadu_ps(src + (r + 0) * cols + c), b = _mm_loadu_ps(src + (r + 1) * cols + c);
+                __m128 x = _mm_loadu_ps(src + (r + 2) * cols + c), y = _mm_loadu_ps(src + (r + 3) * cols + c);
+                _MM_TRANSPOSE4_PS(a, b, x, y);
+                _mm_storeu_ps(dst + (c + 0) * rows + r, a);
+                _mm_storeu_ps(dst + (c + 1) * rows + r, b);
+                _mm_storeu_ps(dst + (c + 2) * rows + r, x);
+                _mm_storeu_ps(dst + (c + 3) * rows + r, y);
+            }
+        return;
+    }
+    for (size_t r = 0; r < rows; ++r)
+        for (size_t c = 0; c < cols; ++c) dst[c * rows + r] = src[r * cols + c];
+}
+
+inline uint64_t rt_done_min(const crlot_stream_rt* st) {
+    uint64_t m = UINT64_MAX;
+    for (int w = 0; w < st->wgs; ++w) {
+        const uint64_t d = __atomic_load_n(&st->ctl->done[w], __ATOMIC_ACQUIRE);
+        m = d < m ? d : m;
+    }
+    return m;
+}
+
+int rt_launch(crlot_stream_rt* st) {
+    crlot_plan* p = st->plan;
+    crlot::RtArgs a;
+    a.t = tables(p);
+    a.ctl = st->d_ctl;
+    a.in_ring = st->d_in_ring;
+    a.out_ring = st->d_out_ring;
+    a.state = st->d_state;
+    a.channels = st->channels;
+    a.interleaved = st->interleaved;
+    a.depth = st->depth;
+    a.ring_len = p->geo.ring_len;
+    a.inv_n = p->geo.inv_n;
+    a.gain = p->geo.gain;
+    a.idle_ticks = st->idle_ticks;
+    __atomic_store_n(&st->ctl->stop, 0, __ATOMIC_RELEASE);
+    hipError_t e = crlot::launch_stream_rt(p->geo, a, st->s);
+    if (e == hipSuccess) e = hipEventRecord(st->ev, st->s);
+    if (e != hipSuccess) return hip_fail(e, "resident stream kernel launch");
+    st->launched = true;
+    st->gen = p->table_gen;
+    return CRLOT_OK;
+}
+
+bool rt_running(crlot_stream_rt* st) { return st->launched && hipEventQuery(st->ev) == hipErrorNotReady; }
+
+int rt_stop(crlot_stream_rt* st) {
+    if (!st->launched) return CRLOT_OK;
+    __atomic_store_n(&st->ctl->stop, 1, __ATOMIC_RELEASE);
+    hipError_t e = hipStreamSynchronize(st->s);
+    __atomic_store_n(&st->ctl->stop, 0, __ATOMIC_RELEASE);
+    st->launched = false;
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "resident stream kernel");
+}
+
+// Wait until every workgroup completed `hops` hops, relaunching the kernel if it
+// exited (idle) before seeing the last doorbell.
+int rt_wait_done(crlot_stream_rt* st, uint64_t hops) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if (rt_done_min(st) >= hops) return CRLOT_OK;
+        if ((spin & 1023) == 1023) {
+            if (!rt_running(st)) {
+                if (st->launched) {  // gone: surface a fault, else relaunch
+                    hipError_t e = hipEventSynchronize(st->ev);
+                    if (e != hipSuccess) return hip_fail(e, "resident stream kernel");
+                    st->launched = false;
+                }
+                if (rt_done_min(st) >= hops) return CRLOT_OK;
+                int rc = rt_launch(st);
+                if (rc != CRLOT_OK) return rc;
+            }
+            const auto us = std::chrono::duration_cast<std::chrono::microseconds>(
+                                std::chrono::steady_clock::now() - t0).count();
+            if (us > st->timeout_us) return fail(CRLOT_EHIP, "resident stream kernel: hop timed out");
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int crlot_stream_rt_create(crlot_plan* p, int32_t channels, int32_t interleaved, int32_t depth,
+                           crlot_stream_rt** out) {
+    if (!p || !out) return fail(CRLOT_EINVAL, "bad argument");
+    *out = nullptr;
+    if (channels <= 0 || channels > crlot::kRtMaxChannels)
+        return fail(CRLOT_EINVAL, "channels must be 1..1024 on the resident streaming path");
+    if (depth <= 0) depth = 4;
+    if (depth > 64) return fail(CRLOT_EINVAL, "depth must be 1..64");
+    if (p->boundary == CRLOT_FRAMEQUEUE)
+        return fail(CRLOT_EINVAL, "FrameQueue framing is whole-signal; stream with ZERO_PAD/DROP");
+    if (!crlot::fused_supported(p->geo.n, p->geo.h) || p->geo.n > 2048)
+        return fail(CRLOT_EUNSUPPORTED, "resident streaming needs N in 256..2048, H % 128 == 0, N % H == 0");
+    DeviceGuard g(p->device);
+    crlot_stream_rt* st = new crlot_stream_rt();
+    st->plan = p;
+    st->channels = channels;
+    st->interleaved = interleaved ? 1 : 0;
+    st->depth = depth;
+    st->wgs = crlot::stream_rt_workgroups(channels);
+    int khz = 100000;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, p->device) != hipSuccess || khz <= 0)
+        khz = 100000;
+    st->tick_ns = 1e6 / double(khz);
+    st->idle_ticks = uint64_t(20.0e6 / st->tick_ns);  // 20 ms without a hop
+    const size_t ring = sizeof(float) * size_t(depth) * size_t(channels) * size_t(p->geo.h);
+    st->state_floats = size_t(channels) * 2 * size_t(p->geo.n);
+    hipError_t e;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    if ((e = hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking)) ||
+        (e = hipEventCreateWithFlags(&st->ev, hipEventDisableTiming)) ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&st->ctl), sizeof(crlot::RtCtl), fl)) ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&st->in_ring), ring, fl)) ||
+        (e = hipHostMalloc(reinterpret_cast<void**>(&st->out_ring), ring, fl)) ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->d_ctl), st->ctl, 0)) ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->d_in_ring), st->in_ring, 0)) ||
+        (e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->d_out_ring), st->out_ring, 0)) ||
+        (e = hipMalloc(&st->d_state, sizeof(float) * st->state_floats)) ||
+        (e = hipMemset(st->d_state, 0, sizeof(float) * st->state_floats))) {
+        crlot_stream_rt_destroy(st);
+        return hip_fail(e, "resident stream allocation");
+    }
+    std::memset(static_cast<void*>(st->ctl), 0, sizeof(crlot::RtCtl));
+    std::memset(st->in_ring, 0, ring);
+    std::memset(st->out_ring, 0, ring);
+    *out = st;
+    return CRLOT_OK;
+}
+
+void crlot_stream_rt_destroy(crlot_stream_rt* st) {
+    if (!st) return;
+    DeviceGuard g(st->plan->device);
+    if (st->ctl) (void)rt_stop(st);
+    if (st->d_state) (void)hipFree(st->d_state);
+    if (st->in_ring) (void)hipHostFree(st->in_ring);
+    if (st->out_ring) (void)hipHostFree(st->out_ring);
+    if (st->ctl) (void)hipHostFree(st->ctl);
+    if (st->ev) (void)hipEventDestroy(st->ev);
+    if (st->s) (void)hipStreamDestroy(st->s);
+    delete st;
+}
+
+int crlot_stream_rt_reset(crlot_stream_rt* st) {
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    DeviceGuard g(st->plan->device);
+    int rc = rt_stop(st);
+    if (rc != CRLOT_OK) return rc;
+    hipError_t e = hipMemsetAsync(st->d_state, 0, sizeof(float) * st->state_floats, st->s);
+    if (e == hipSuccess) e = hipStreamSynchronize(st->s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemset(stream state)");
+    std::memset(static_cast<void*>(st->ctl), 0, sizeof(crlot::RtCtl));
+    st->q = 0;
+    return CRLOT_OK;
+}
+
+float* crlot_stream_rt_input_slot(crlot_stream_rt* st) {
+    if (!st) return nullptr;
+    // the slot of hop q is free once hop q - depth has completed
+    if (st->q >= uint64_t(st->depth) && rt_wait_done(st, st->q - st->depth + 1) != CRLOT_OK) return nullptr;
+    const size_t hop = size_t(st->channels) * size_t(st->plan->geo.h);
+    return st->in_ring + size_t(st->q % st->depth) * hop;
+}
+
+int crlot_stream_rt_submit(crlot_stream_rt* st, int64_t* hop_index) {
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    DeviceGuard g(st->plan->device);
+    if (st->q >= uint64_t(st->depth)) {
+        int rc = rt_wait_done(st, st->q - st->depth + 1);
+        if (rc != CRLOT_OK) return rc;
+    }
+    if (st->launched && st->gen != st->plan->table_gen) {  // tables changed: re-stage them
+        int rc = rt_stop(st);
+        if (rc != CRLOT_OK) return rc;
+        hipError_t e = hipDeviceSynchronize();  // the table copies, on whatever stream
+        if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+    }
+    __atomic_store_n(&st->ctl->seq, st->q + 1, __ATOMIC_RELEASE);
+    if (hop_index) *hop_index = int64_t(st->q);
+    st->q += 1;
+    if (!rt_running(st)) {
+        if (st->launched) {
+            hipError_t e = hipEventSynchronize(st->ev);
+            if (e != hipSuccess) return hip_fail(e, "resident stream kernel");
+            st->launched = false;
+        }
+        return rt_launch(st);
+    }
+    return CRLOT_OK;
+}
+
+int crlot_stream_rt_wait(crlot_stream_rt* st, int64_t hop_index, const float** out, int32_t* emitted) {
+    if (out) *out = nullptr;
+    if (emitted) *emitted = 0;
+    if (!st || hop_index < 0 || uint64_t(hop_index) >= st->q) return fail(CRLOT_EINVAL, "bad hop index");
+    if (uint64_t(hop_index) + st->depth < st->q) return fail(CRLOT_EINVAL, "hop slot already reused");
+    DeviceGuard g(st->plan->device);
+    int rc = rt_wait_done(st, uint64_t(hop_index) + 1);
+    if (rc != CRLOT_OK) return rc;
+    const int64_t nb = st->plan->geo.n / st->plan->geo.h;
+    const bool em = hop_index >= nb - 1;
+    if (emitted) *emitted = em ? st->plan->geo.h : 0;
+    if (out && em)
+        *out = st->out_ring + size_t(hop_index % st->depth) * size_t(st->channels) * size_t(st->plan->geo.h);
+    return CRLOT_OK;
+}
+
+int crlot_stream_rt_push_hop(crlot_stream_rt* st, const float* h_in, float* h_out, int32_t* emitted) {
+    if (emitted) *emitted = 0;
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    if (!h_in || !h_out) return fail(CRLOT_EINVAL, "null buffer");
+    const size_t C = size_t(st->channels), H = size_t(st->plan->geo.h), hop = C * H;
+    float* slot = crlot_stream_rt_input_slot(st);
+    if (!slot) return fail(CRLOT_EHIP, "resident stream kernel: input slot unavailable");
+    if (st->interleaved) {  // [H][C] -> the slot's [C][H]
+        transpose_f32(h_in, slot, H, C);
+    } else {
+        std::memcpy(slot, h_in, sizeof(float) * hop);
+    }
+    int64_t qi = 0;
+    int rc = crlot_stream_rt_submit(st, &qi);
+    if (rc != CRLOT_OK) return rc;
+    const float* o = nullptr;
+    int32_t em = 0;
+    if ((rc = crlot_stream_rt_wait(st, qi, &o, &em)) != CRLOT_OK) return rc;
+    if (o && st->interleaved) {
+        transpose_f32(o, h_out, C, H);
+    } else if (o) {
+        std::memcpy(h_out, o, sizeof(float) * hop);
+    }
+    if (emitted) *emitted = em;
+    return CRLOT_OK;
+}
+
+int crlot_stream_rt_info(const crlot_stream_rt* st, int64_t* hops, double* last_device_ns, int32_t* running) {
+    if (!st) return fail(CRLOT_EINVAL, "null stream");
+    if (hops) *hops = int64_t(st->q);
+    if (last_device_ns) {
+        uint64_t mx = 0;
+        for (int w = 0; w < st->wgs; ++w) mx = std::max(mx, __atomic_load_n(&st->ctl->ticks[w], __ATOMIC_ACQUIRE));
+        *last_device_ns = double(mx) * st->tick_ns;
+    }
+    if (running) *running = rt_running(const_cast<crlot_stream_rt*>(st)) ? 1 : 0;
+    return CRLOT_OK;
+}
+
+int crlot_stream_rt_phases(const crlot_stream_rt* st, double* ns8) {
+    if (!st || !ns8) return fail(CRLOT_EINVAL, "bad argument");
+    for (int i = 0; i < 8; ++i) ns8[i] = double(__atomic_load_n(&st->ctl->phase[i], __ATOMIC_ACQUIRE)) * st->tick_ns;
+    return CRLOT_OK;
+}
+
+int crlot_stream_rt_set_idle_timeout(crlot_stream_rt* st, double seconds, double hop_timeout_seconds) {
+    if (!st || !(seconds > 0.0) || !(hop_timeout_seconds > 0.0)) return fail(CRLOT_EINVAL, "bad argument");
+    st->idle_ticks = uint64_t(seconds * 1e9 / st->tick_ns);
+    st->timeout_us = int64_t(hop_timeout_seconds * 1e6);
+    return rt_stop(st);  // the next hop relaunches with the new timeout
 }
 
 }  // extern "C"

@@ -120,6 +120,33 @@ hipError_t launch_stream_hop(const Geometry& g, const DevTables& t, const float*
                              int64_t in_inc, float* out, int64_t out_ld, int64_t out_inc,
                              float* hist, float* acc, int channels, int64_t q, hipStream_t stream);
 
+// Resident streaming kernel (stream_rt.hip, BASELINE config 4).  The control
+// block and the hop rings live in pinned host memory; the host writes hop q
+// into in_ring slot q % depth, then seq = q + 1; workgroup w publishes
+// done[w] = q + 1 once its channels' output block is in out_ring slot q % depth.
+constexpr int kRtMaxChannels = 1024;
+constexpr int kRtMaxWg = kRtMaxChannels / 4;
+struct alignas(64) RtCtl {
+    uint64_t seq;             // hops submitted (host, release)
+    uint64_t stop;            // nonzero: every workgroup exits at its next poll
+    uint64_t pad0[6];
+    uint64_t done[kRtMaxWg];  // hops completed per workgroup (device, release)
+    uint64_t ticks[kRtMaxWg]; // s_memrealtime ticks (100 MHz) of the last hop per workgroup
+    uint64_t phase[8];        // CRLOT_RT_PHASES diagnostic builds: workgroup 0's phase stamps
+};
+struct RtArgs {
+    DevTables t;
+    RtCtl* ctl;
+    const float* in_ring;     // [depth][C * H] host-pinned
+    float* out_ring;          // [depth][C * H] host-pinned
+    float* state;             // [C][2N] device: hist | acc, saved at exit, restored at launch
+    int channels = 0, interleaved = 0, depth = 0, ring_len = 0;
+    float inv_n = 0.f, gain = 1.f;
+    uint64_t idle_ticks = 0;  // exit after this long without a hop
+};
+int stream_rt_workgroups(int channels);
+hipError_t launch_stream_rt(const Geometry& g, const RtArgs& a, hipStream_t stream);
+
 // Batched adapter-semantics real FFTs.
 hipError_t launch_rfft(const Geometry& g, const DevTables& t, const float* in, float* out,
                        int batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,

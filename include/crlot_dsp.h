@@ -223,6 +223,50 @@ int crlot_stream_set_layout(crlot_stream* st, int32_t interleaved);
 int crlot_stream_push_hop(crlot_stream* st, const float* d_hop_in, float* d_hop_out,
                           int32_t* emitted, void* stream);
 
+/* ---------------------------------------------------------------- resident streaming
+ * The same per-hop contract as crlot_stream_* (DROP Framer fed H samples per
+ * channel per hop, push_frame_AoS + produce(H); framer.cc:37-117,
+ * OLAAccumulator.cc:124-221; bit-identical outputs) for real-time callers whose
+ * hops live in HOST memory (BASELINE config 4, the ring-buffer low-latency path).
+ * One kernel stays resident on the device with the tables in LDS and each
+ * channel's state in registers; hops travel through pinned host rings of
+ * `depth` slots (0 -> 4) with a doorbell, so a hop costs no kernel launch and no
+ * copy-engine transfer.  The kernel exits after 20 ms without a hop (or on
+ * reset / destroy / a plan table update) and is relaunched by the next hop; a
+ * hipDeviceSynchronize elsewhere in the process therefore waits at most that
+ * idle time.  N in 256..2048, H % 128 == 0, N % H == 0, channels 1..1024.
+ *   push_hop      copy h_in into the next slot, submit, wait, copy the H output
+ *                 samples per channel into h_out (*emitted = 0 or H); h_in /
+ *                 h_out are [H][C] interleaved PCM if `interleaved`, else [C][H]
+ *   input_slot    zero-copy form: the host slot for the next hop (C*H floats,
+ *                 always channel-major [C][H]), then submit -> hop index,
+ *                 wait -> pointer to that hop's [C][H] output slot (valid until hop
+ *                 index + depth is submitted); up to `depth` hops in flight
+ *   info          hops submitted, the device time of the last hop (ns, from the
+ *                 kernel's own clock: doorbell seen -> output published), running */
+typedef struct crlot_stream_rt crlot_stream_rt;
+int crlot_stream_rt_create(crlot_plan* plan, int32_t channels, int32_t interleaved, int32_t depth,
+                           crlot_stream_rt** out);
+void crlot_stream_rt_destroy(crlot_stream_rt* st);
+int crlot_stream_rt_reset(crlot_stream_rt* st);
+int crlot_stream_rt_push_hop(crlot_stream_rt* st, const float* h_hop_in, float* h_hop_out,
+                             int32_t* emitted);
+float* crlot_stream_rt_input_slot(crlot_stream_rt* st);
+int crlot_stream_rt_submit(crlot_stream_rt* st, int64_t* hop_index);
+int crlot_stream_rt_wait(crlot_stream_rt* st, int64_t hop_index, const float** h_hop_out,
+                         int32_t* emitted);
+int crlot_stream_rt_info(const crlot_stream_rt* st, int64_t* hops, double* last_device_ns,
+                         int32_t* running);
+/* diagnostic: workgroup 0's phase times of the last hop (ns after the doorbell
+ * was seen: hop read issued, hop staged, transform done, output barrier, output
+ * issued, release fence, publish barrier); zeros unless the library was built
+ * with -DCRLOT_RT_PHASES */
+int crlot_stream_rt_phases(const crlot_stream_rt* st, double* ns8);
+/* idle exit after `idle_seconds` without a hop; a wait fails (CRLOT_EHIP) after
+ * `hop_timeout_seconds` (defaults 0.02 and 2) */
+int crlot_stream_rt_set_idle_timeout(crlot_stream_rt* st, double idle_seconds,
+                                     double hop_timeout_seconds);
+
 /* ---------------------------------------------------------------- Framer (host)
  * dsp::Framer (framer.h:26-127, framer.cc:15-181): interleaved PCM of
  * `channels` channels in, frames of frame_size*channels interleaved samples out

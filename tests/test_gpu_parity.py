@@ -762,3 +762,117 @@ def test_stream_per_hop_equals_batched_drop(pkg, oracle, torch_cuda, n, h, inter
     st.reset()
     out, em = st.push_hop(xd[:, :h].t().contiguous() if interleaved else xd[:, :h].contiguous())
     assert em == (h if nb == 1 else 0)
+
+
+# ------------------------------------------------------------------ resident streaming (config 4)
+@pytest.mark.parametrize("n,h,C_,interleaved,gain", [(512, 128, 64, True, False), (512, 128, 64, False, False),
+                                                      (512, 128, 7, True, True), (1024, 256, 12, False, True),
+                                                      (256, 128, 5, False, False), (2048, 512, 4, True, False),
+                                                      (1024, 1024, 8, True, False)])
+def test_stream_rt_equals_batched_drop(pkg, oracle, torch_cuda, n, h, C_, interleaved, gain):
+    """The resident kernel (hops through pinned host memory, state in registers)
+    reproduces the batched DROP round trip (pairing off) bit for bit, for channel
+    counts that do and do not fill its 4-channel workgroups, both PCM layouts."""
+    torch = torch_cuda
+    hops = 40
+    x = oracle.synth_streams(C_, hops * h, config_id=46)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP, frame_pairing=False)
+    if gain:
+        plan.set_spectral_gain(np.linspace(1.0, 0.25, n // 2 + 1).astype(np.float32))
+    y_batch = host(plan.roundtrip(dev(torch, x)))
+    st = pkg.StreamRT(plan, C_, interleaved=interleaved)
+    nb = n // h
+    outs = []
+    for q in range(hops):
+        hop = x[:, q * h:(q + 1) * h]
+        hop = np.ascontiguousarray(hop.T if interleaved else hop)
+        out, em = st.push_hop(hop)
+        assert em == (h if q >= nb - 1 else 0), q
+        if em:
+            outs.append(out.T if interleaved else out)
+    y_rt = np.concatenate(outs, axis=1)
+    assert y_rt.shape == y_batch.shape
+    assert np.array_equal(bits(y_rt), bits(y_batch))
+    inf = st.info()
+    assert inf["hops"] == hops and inf["last_device_ns"] > 0
+    st.close()
+
+
+def test_stream_rt_idle_exit_reset_and_table_update(pkg, oracle, torch_cuda):
+    """Exit/relaunch paths keep the bits: an idle exit mid-stream (state saved to
+    HBM and restored), reset(), and a spectral-gain update mid-stream (the kernel
+    re-stages its tables) all equal the per-launch Stream fed the same hops."""
+    import time
+    torch = torch_cuda
+    n, h, C_, hops = 512, 128, 16, 30
+    x = oracle.synth_streams(C_, hops * h, config_id=47)
+    xd = dev(torch, x)
+    g2 = np.linspace(1.5, 0.5, n // 2 + 1).astype(np.float32)
+
+    def run(kind):
+        plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP, frame_pairing=False)
+        st = pkg.StreamRT(plan, C_) if kind == "rt" else pkg.Stream(plan, C_)
+        if kind == "rt":
+            st.set_idle_timeout(0.002)
+        ys = []
+        for q in range(hops):
+            if q == 12:
+                plan.set_spectral_gain(g2)
+            if q == 20:
+                st.reset()
+            if kind == "rt":
+                if q in (5, 15):
+                    time.sleep(0.05)  # > idle timeout: the kernel exits and is relaunched
+                    assert not st.info()["running"]
+                out, em = st.push_hop(x[:, q * h:(q + 1) * h])
+            else:
+                out, em = st.push_hop(xd[:, q * h:(q + 1) * h].contiguous())
+                out = host(out)
+            ys.append(out.copy() if em else None)
+        st.close()
+        return ys
+
+    a, b = run("rt"), run("ref")
+    for q, (ya, yb) in enumerate(zip(a, b)):
+        assert (ya is None) == (yb is None), q
+        if ya is not None:
+            assert np.array_equal(bits(ya), bits(yb)), q
+
+
+def test_stream_rt_pipelined_depth(pkg, oracle, torch_cuda):
+    """Zero-copy form with hops in flight (submit several, then wait): same bits as
+    the synchronous form."""
+    import ctypes
+    n, h, C_, hops, depth = 512, 128, 64, 48, 4
+    x = oracle.synth_streams(C_, hops * h, config_id=48)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP, frame_pairing=False)
+    ref = pkg.StreamRT(plan, C_, interleaved=True)
+    want = []
+    for q in range(hops):
+        o, em = ref.push_hop(np.ascontiguousarray(x[:, q * h:(q + 1) * h].T))
+        want.append(o.copy() if em else None)
+    ref.close()
+    st = pkg.StreamRT(plan, C_, interleaved=True, depth=depth)
+    L = pkg.lib()
+    got = []
+    pending = []
+    for q in range(hops):
+        slot = L.crlot_stream_rt_input_slot(st._h)
+        assert slot
+        buf = np.ctypeslib.as_array(ctypes.cast(slot, ctypes.POINTER(ctypes.c_float)), shape=(C_, h))
+        buf[:] = x[:, q * h:(q + 1) * h]  # slots are channel-major
+        qi = ctypes.c_int64()
+        assert L.crlot_stream_rt_submit(st._h, ctypes.byref(qi)) == 0
+        pending.append(qi.value)
+        if len(pending) == depth or q == hops - 1:
+            for hq in pending:
+                op, em = ctypes.c_void_p(), ctypes.c_int32()
+                assert L.crlot_stream_rt_wait(st._h, hq, ctypes.byref(op), ctypes.byref(em)) == 0
+                got.append(np.ctypeslib.as_array(ctypes.cast(op, ctypes.POINTER(ctypes.c_float)),
+                                                 shape=(C_, h)).T.copy() if em.value else None)
+            pending = []
+    st.close()
+    for q in range(hops):
+        assert (got[q] is None) == (want[q] is None), q
+        if got[q] is not None:
+            assert np.array_equal(bits(got[q]), bits(want[q])), q
