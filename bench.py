@@ -43,6 +43,8 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -184,6 +186,222 @@ def synth_device(torch, S: int, T: int, dev, seed: int):
     return x
 
 
+
+# --------------------------------------------------------------------------- suites
+# `bench.py --suite NAME` runs one of the reference's other bench/ programs
+# against the product (one JSON line each, never the headline contract line);
+# their CPU legs are this file's cpu_baseline legs (the oracle's C restatement
+# timed on this host, single thread, as the reference's benchmarks run).
+def _oracle(native_try=True):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    native = False
+    if native_try:
+        try:
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"], check=True,
+                           capture_output=True, timeout=120)
+            native = True
+        except Exception:
+            pass
+    return O, native
+
+
+def _ev_time(torch, fn, reps, stream=None):
+    """Mean ms per call of fn() by HIP events on the current stream (after one warm-up)."""
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _sync_latency_us(torch, fn, reps):
+    """p50 wall us of fn() + synchronize (the per-call latency a host caller sees)."""
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e6)
+    ts.sort()
+    return round(ts[len(ts) // 2], 2)
+
+
+def suite_ola(pkg, torch, dev):
+    """bench/ola_benchmark.cc counterparts.  GPU-native form: the OLA-only stage
+    batched (crlot_ola_gather: frames already in HBM -> produced samples), over the
+    reference's parameter grid N x H (ParamAddFrameSoA/ParamProduce, :465-485),
+    priced against HBM (4 B read per frame sample + 4 B written per output
+    sample).  Per-call form: the device-backed dsp::OLAAccumulator object driven
+    call by call as the fixture does (AddFrameSoA / Produce / AddFrameAoS /
+    Multichannel / FullPipeline, :120-240), launch-bound by construction."""
+    O, native = _oracle()
+    res = {"suite": "ola", "reference": "bench/ola_benchmark.cc", "grid": [], "per_call": {}}
+    g = torch.Generator(device=dev).manual_seed(11)
+    for n in (1024, 2048, 4096):
+        for h in (n // 4, n // 2):
+            S, F = 256, (480_000 // h)
+            plan = pkg.Plan(frame_size=n, hop_size=h, device=dev.index)
+            frames = torch.rand((S, F, n), generator=g, device=dev) - 0.5
+            y = torch.empty((S, F * h), device=dev)
+            ms = _ev_time(torch, lambda: plan.ola_gather(frames, y), 10)
+            gbs = (S * F * n * 4 + S * F * h * 4) / (ms * 1e-3) / 1e9
+            # CPU: the reference's streaming add_frame_SoA + produce(H), one stream, one thread
+            Fc = min(F, 600)
+            fr = frames[0, :Fc].cpu().numpy()[:, None, :]
+            w = O.window(O.HANN, n)
+            O.bench_ola_stream(fr[:8], n, h, w, native=native)
+            t0 = time.perf_counter()
+            O.bench_ola_stream(fr, n, h, w, native=native)
+            cpu_s = time.perf_counter() - t0
+            res["grid"].append({
+                "frame": n, "hop": h, "streams": S, "frames_per_stream": F,
+                "gpu_ms": round(ms, 4), "gpu_msamples_s": round(S * F * h / (ms * 1e-3) / 1e6, 1),
+                "gpu_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+                "cpu_msamples_s_1thread": round(Fc * h / cpu_s / 1e6, 2),
+                "cpu_us_per_frame": round(cpu_s / Fc * 1e6, 3)})
+            del frames, y
+    # per-call object API, N=1024 H=256 (the fixture's OLAConfig)
+    n, h = 1024, 256
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                        apply_window_inside=False)
+    w = pkg.window_table(pkg.HANN, n)
+    wd = torch.from_numpy(w).to(dev)
+    fr = (torch.rand((2, n), generator=g, device=dev) - 0.5).contiguous()
+    out = torch.empty((2, h), device=dev)
+    ola = pkg.OLAAccumulator(cfg)
+    ola.set_window(w)
+    k = [0]
+
+    def add():
+        ola.add_frame_SoA_device(fr[:1], wd, k[0] * h, 0, n, 1.0)
+
+    def add_produce():
+        ola.add_frame_SoA_device(fr[:1], wd, k[0] * h, 0, n, 1.0)
+        ola.produce_device(out[:1], h)
+        k[0] += 1
+
+    res["per_call"]["AddFrameSoA_us_p50_synced"] = _sync_latency_us(torch, add, 200)
+    res["per_call"]["AddFrameSoA_produce_us_p50_synced"] = _sync_latency_us(torch, add_produce, 200)
+    t0 = time.perf_counter()
+    for _ in range(2000):
+        add_produce()
+    torch.cuda.synchronize()
+    res["per_call"]["AddFrameSoA_produce_us_async_issue"] = round((time.perf_counter() - t0) / 2000 * 1e6, 2)
+    frames_cpu = np.random.default_rng(3).standard_normal((4000, 1, n)).astype(np.float32)
+    t0 = time.perf_counter()
+    O.bench_ola_stream(frames_cpu, n, h, w, inside=False, native=native)
+    res["per_call"]["cpu_AddFrameSoA_produce_us"] = round((time.perf_counter() - t0) / 4000 * 1e6, 3)
+    res["note"] = ("GPU per-call numbers are one kernel launch (+ sync) each: the object API is "
+                   "latency-bound on any GPU; the batched grid is the GPU-native OLA-only form")
+    res["cpu_native_build"] = native
+    return res
+
+
+def suite_fft(pkg, torch, dev):
+    """bench/micro_fft_benchmark.cc counterparts: IFftPlan::forward at 512/1024/2048,
+    batch 1 and batch 4 (:117-214) per call, plus the batched GPU-native form
+    (2^18 frames per launch) priced against HBM (4 N B in, 8 (N/2+1) B out)."""
+    O, native = _oracle()
+    res = {"suite": "fft", "reference": "bench/micro_fft_benchmark.cc", "sizes": []}
+    g = torch.Generator(device=dev).manual_seed(12)
+    for n in (512, 1024, 2048):
+        plan = pkg.FftPlan(n, device=dev.index)
+        t = torch.arange(n, device=dev, dtype=torch.float64) / 48000.0
+        sig = (0.3 * torch.sin(2 * np.pi * 440 * t) + 0.2 * torch.sin(2 * np.pi * 880 * t)
+               + 0.1 * torch.sin(2 * np.pi * 1760 * t)).float()
+        one, four = sig[None].contiguous(), sig[None].repeat(4, 1).contiguous()
+        B = 1 << 18
+        big = torch.rand((B, n), generator=g, device=dev) - 0.5
+        ms = _ev_time(torch, lambda: plan.forward(big), 10)
+        gbs = B * (4 * n + 8 * (n // 2 + 1)) / (ms * 1e-3) / 1e9
+        xc = big[:20000].cpu().numpy()
+        O.bench_rfft(xc[:100], n, native=native)
+        t0 = time.perf_counter()
+        O.bench_rfft(xc, n, native=native)
+        cpu_us = (time.perf_counter() - t0) / xc.shape[0] * 1e6
+        res["sizes"].append({
+            "nfft": n,
+            "single_us_p50_synced": _sync_latency_us(torch, lambda: plan.forward(one), 300),
+            "batch4_us_p50_synced": _sync_latency_us(torch, lambda: plan.forward(four), 300),
+            "batched_frames": B, "batched_ms": round(ms, 4),
+            "batched_ns_per_frame": round(ms * 1e6 / B, 3),
+            "batched_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+            "cpu_us_per_frame_1thread": round(cpu_us, 3)})
+        del big
+    res["cpu_native_build"] = native
+    return res
+
+
+def suite_streaming(pkg, torch, dev):
+    """BASELINE config 4 (64 ch, N=512 H=128, DROP, per hop): the C++ latency
+    harness (harness/stream_latency: per-launch crlot_stream_push_hop and the
+    resident crlot_stream_rt path) next to the oracle's per-hop CPU cost."""
+    exe = os.path.join(ROOT, "harness", "stream_latency")
+    r = subprocess.run([exe, "3750"], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError(f"stream_latency failed: {r.stdout} {r.stderr}")
+    res = {"suite": "streaming", **json.loads(r.stdout.strip().splitlines()[-1])}
+    O, native = _oracle()
+    hops = 2000
+    xs = O.synth(hops * 128, 9)
+    O.roundtrip(xs[:4096], 512, 128, mode=O.DROP)
+    t0 = time.perf_counter()
+    O.roundtrip(xs, 512, 128, mode=O.DROP)
+    per_hop_1ch = (time.perf_counter() - t0) / hops
+    res["hop_budget_us_realtime"] = round(128 / 48000 * 1e6, 1)
+    res["cpu_oracle_1core_us_per_hop_64ch"] = round(per_hop_1ch * 64 * 1e6, 1)
+    return res
+
+
+def suite_config1(pkg, torch, dev):
+    """BASELINE config 1: assets/oboe.wav (tests/golden/oboe.wav) -> WavReader ->
+    mono mixdown (main/main.cc:155-160) -> N=1024/H=256 Hann round trip on the GPU,
+    the oracle beside it; writes gpurun_out/oboe_roundtrip.wav through WavWriter."""
+    O, _ = _oracle(native_try=False)
+    x, sr = pkg.load_wav_mono(os.path.join(ROOT, "tests", "golden", "oboe.wav"))
+    n, h = 1024, 256
+    t0 = time.perf_counter()
+    ref = O.roundtrip(x, n, h)
+    cpu_s = time.perf_counter() - t0
+    plan = pkg.Plan(frame_size=n, hop_size=h, device=dev.index)
+    xd = torch.from_numpy(x[None]).to(dev)
+    out = plan.roundtrip(xd)
+    ms = _ev_time(torch, lambda: plan.roundtrip(xd, out), 20)
+    y = out[0].cpu().numpy()
+    d = y.astype(np.float64) - ref
+    path = os.path.join(ROOT, "gpurun_out", "oboe_roundtrip.wav")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    w = pkg.WavWriter()
+    assert w.open(path, 1, sr, 16)
+    w.write(np.clip(y[:x.size], -1, 1))
+    w.close()
+    return {"suite": "config1", "config": "oboe.wav mono, N=1024 H=256 Hann", "samples": int(x.size),
+            "sample_rate": sr, "gpu_ms": round(ms, 4), "gpu_msamples_s": round(x.size / ms / 1e3, 1),
+            "cpu_oracle_ms_1thread": round(cpu_s * 1e3, 3),
+            "rel_l2_vs_oracle": float(np.linalg.norm(d) / np.linalg.norm(ref)),
+            "max_abs_vs_oracle": float(np.max(np.abs(d))), "wrote": os.path.relpath(path, ROOT)}
+
+
+SUITES = {"ola": suite_ola, "fft": suite_fft, "streaming": suite_streaming, "config1": suite_config1}
+
+
+def run_suite(name):
+    import numpy as _np  # noqa: F401
+    import torch
+    from __graft_entry__ import load_pkg
+    pkg = load_pkg()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    print(json.dumps(SUITES[name](pkg, torch, dev)), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -194,7 +412,10 @@ def main():
     ap.add_argument("--strong-steps", type=int, default=10)
     ap.add_argument("--no-strong", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--suite", choices=sorted(SUITES), help="run one reference bench/ counterpart instead")
     args = ap.parse_args()
+    if args.suite:
+        return run_suite(args.suite)
 
     from __graft_entry__ import load_pkg, load_dist
     D = load_dist()

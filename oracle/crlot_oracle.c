@@ -1021,3 +1021,34 @@ void or_synth_fill(float* x, size_t n, unsigned long long seed) {
         x[i] = (u * 2.0f - 1.0f) * 0.5f;
     }
 }
+
+/* ---- bench.py cpu_baseline helpers: the reference harnesses' per-frame call
+ * sequences run in C (no Python per call).  Test/measurement infrastructure. */
+
+/* ola_benchmark.cc ParamAddFrameSoA + ParamProduce in streaming order over F
+ * frames of c channels: add_frame_SoA(frame k, window, k*h, 0, n, gain) then
+ * produce(h).  frames: [F][c][n]; out: [c][F*h]. */
+void or_bench_ola_stream(size_t n, size_t h, size_t c, int inside, const float* window,
+                         const float* frames, int64_t F, float gain, float* out) {
+    or_ola* o = or_ola_new(n, h, c, 1e-8f, inside);
+    if (!o) return;
+    or_ola_set_window(o, window);
+    const float* ch[64];
+    float* och[64];
+    for (int64_t k = 0; k < F; ++k) {
+        for (size_t j = 0; j < c && j < 64; ++j) {
+            ch[j] = frames + ((size_t)k * c + j) * n;
+            och[j] = out + j * (size_t)F * h + (size_t)k * h;
+        }
+        or_ola_add_frame_soa(o, ch, window, (size_t)k * h, 0, n, gain);
+        or_ola_produce(o, och, h);
+    }
+    or_ola_free(o);
+}
+
+/* micro_fft_benchmark.cc: IFftPlan::forward over B frames of nfft samples. */
+void or_bench_rfft(int nfft, const float* x, int64_t B, float* out) {
+    or_kfftr_cfg* f = or_kfftr_alloc(nfft, 0);
+    for (int64_t b = 0; b < B; ++b) or_adapter_forward(f, nfft, x + (size_t)b * nfft, out + (size_t)b * (nfft + 2));
+    or_kfftr_free(f);
+}

@@ -39,6 +39,10 @@ def lib(native: bool = False):
         build(native)
     L = C.CDLL(path)
     sz = C.c_size_t
+    L.or_bench_ola_stream.argtypes = [sz, sz, sz, C.c_int, _f32p, _f32p, C.c_int64, C.c_float, _f32p]
+    L.or_bench_ola_stream.restype = None
+    L.or_bench_rfft.argtypes = [C.c_int, _f32p, C.c_int64, _f32p]
+    L.or_bench_rfft.restype = None
     L.or_window.argtypes = [C.c_int, sz, C.c_int, C.c_int, _f32p]
     L.or_window.restype = C.c_int
     L.or_ring_len.argtypes = [sz, sz]
@@ -294,6 +298,24 @@ class Ola:
     def norm(self):
         r = self.ring_size
         return np.ctypeslib.as_array(lib().or_ola_norm(self.p), shape=(r,)).copy()
+
+
+def bench_ola_stream(frames, n, h, window, inside=True, gain=1.0, native=False):
+    """frames [F][c][n] -> out [c][F*h]: the C loop of or_bench_ola_stream."""
+    frames = np.ascontiguousarray(frames, np.float32)
+    F, c, _ = frames.shape
+    out = np.zeros((c, F * h), np.float32)
+    lib(native).or_bench_ola_stream(n, h, c, int(inside), np.ascontiguousarray(window, np.float32), frames,
+                                    F, gain, out)
+    return out
+
+
+def bench_rfft(x, nfft, native=False):
+    """x [B][nfft] -> [B][nfft/2+1] complex64 through or_bench_rfft."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros((x.shape[0], nfft + 2), np.float32)
+    lib(native).or_bench_rfft(nfft, x, x.shape[0], out)
+    return out.view(np.complex64)
 
 
 def roundtrip(x, n, h, wtype=HANN, periodic=False, mode=ZERO_PAD, want_frames=False,
