@@ -389,7 +389,31 @@ def suite_config1(pkg, torch, dev):
             "max_abs_vs_oracle": float(np.max(np.abs(d))), "wrote": os.path.relpath(path, ROOT)}
 
 
-SUITES = {"ola": suite_ola, "fft": suite_fft, "streaming": suite_streaming, "config1": suite_config1}
+def suite_multichannel(pkg, torch, dev):
+    """Interleaved multi-channel batches (Framer(N, H, C) PCM): 1024 streams as
+    1024/C groups of C channels through crlot_roundtrip_interleaved, vs the same
+    streams as mono rows (the headline shape), N=1024 H=256."""
+    res = {"suite": "multichannel", "frame": N_FFT, "hop": HOP, "samples_per_channel": T_LEN, "runs": []}
+    plan = pkg.Plan(frame_size=N_FFT, hop_size=HOP, device=dev.index)
+    g = torch.Generator(device=dev).manual_seed(21)
+    x = torch.rand((STREAMS, T_LEN), generator=g, device=dev) - 0.5
+    y = torch.empty((STREAMS, plan.output_length(T_LEN)), device=dev)
+    ms = _ev_time(torch, lambda: plan.roundtrip(x, y), 20)
+    res["runs"].append({"layout": "mono rows", "channels": 1, "ms": round(ms, 4),
+                        "msamples_s": round(STREAMS * T_LEN / ms / 1e3, 1)})
+    del x, y
+    for c in (2, 8):
+        G = STREAMS // c
+        xi = torch.rand((G, T_LEN, c), generator=g, device=dev) - 0.5
+        yi = torch.empty((G, plan.output_length(T_LEN), c), device=dev)
+        ms = _ev_time(torch, lambda: plan.roundtrip_interleaved(xi, yi), 20)
+        res["runs"].append({"layout": "interleaved", "channels": c, "groups": G, "ms": round(ms, 4),
+                            "msamples_s": round(G * c * T_LEN / ms / 1e3, 1)})
+        del xi, yi
+    return res
+
+
+SUITES = {"ola": suite_ola, "multichannel": suite_multichannel, "fft": suite_fft, "streaming": suite_streaming, "config1": suite_config1}
 
 
 def run_suite(name):

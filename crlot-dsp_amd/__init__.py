@@ -121,6 +121,7 @@ def lib():
         "crlot_fft_inverse": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
         "crlot_fft_forward_complex": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
         "crlot_fft_inverse_complex": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_roundtrip_interleaved": ([vp, vp, vp, i32, i32, i64, i64, i64, vp], C.c_int),
         "crlot_stream_create": ([vp, i32, C.POINTER(vp)], C.c_int),
         "crlot_stream_destroy": ([vp], None),
         "crlot_stream_reset": ([vp], C.c_int),
@@ -357,6 +358,23 @@ class Plan:
         s = _stream_handle(x) if stream is None else stream
         _check(lib().crlot_roundtrip(self._h, x.data_ptr(), y.data_ptr(), S, T, _ld(x, 0, T),
                                      _ld(y, 0, L), s), "crlot_roundtrip")
+        return y
+
+    def roundtrip_interleaved(self, x, y=None, stream: int | None = None):
+        """x: (G, T, C) float32 CUDA tensor of G groups of C interleaved channels ->
+        y: (G, F*H, C), each channel an independent stream (crlot_roundtrip_interleaved)."""
+        torch = _torch()
+        G, T, Cc = x.shape
+        if x.stride(2) != 1 or x.stride(1) != Cc:
+            raise ValueError("x must be (G, T, C) with contiguous rows of C samples")
+        L = self.output_length(T)
+        if y is None:
+            y = torch.empty((G, L, Cc), dtype=torch.float32, device=x.device)
+        s = _stream_handle(x) if stream is None else stream
+        ldx = x.stride(0) if G > 1 else T * Cc
+        ldy = y.stride(0) if G > 1 else L * Cc
+        _check(lib().crlot_roundtrip_interleaved(self._h, x.data_ptr(), y.data_ptr(), G, Cc, T, ldx, ldy, s),
+               "crlot_roundtrip_interleaved")
         return y
 
     def stages(self, x, want_spec=True):

@@ -55,6 +55,9 @@ struct crlot_plan {
     // staged-path workspace
     float* d_work = nullptr;
     int64_t work_bytes = 0;
+    // channel planes of crlot_roundtrip_interleaved (input planes, then output planes)
+    float* d_planes = nullptr;
+    int64_t planes_bytes = 0;
     // pinned staging of table uploads (stream-ordered: hipMemcpyAsync on the
     // caller's stream; the event guards the staging memory until the copies ran)
     char* h_stage = nullptr;
@@ -126,7 +129,7 @@ crlot::DevTables tables(const crlot_plan* p) {
 void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
-    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_wsn,
+    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_planes, p->d_wsn,
                      p->d_rden, p->d_twany_own, p->d_ptw, p->d_pden})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
     if (p->d_pflags) (void)hipFree(p->d_pflags);
@@ -567,6 +570,38 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
     e = crlot::launch_ola_gather(p->geo, t, p->d_work, p->geo.n, d_y, n_streams, F, ld_y,
                                  out_len, s);
     if (e != hipSuccess) return hip_fail(e, "gather kernel launch");
+    return CRLOT_OK;
+}
+
+int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int32_t n_groups,
+                                int32_t channels, int64_t T, int64_t ld_x, int64_t ld_y, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_groups < 0 || T < 0 || channels <= 0 || channels > 64) return fail(CRLOT_EINVAL, "bad size");
+    const int64_t F = frames_for(p, T);
+    if (n_groups == 0 || F == 0) return CRLOT_OK;
+    if ((!d_x && T > 0) || !d_y) return fail(CRLOT_EINVAL, "null buffer");
+    const int64_t L = F * p->geo.h, C = channels;
+    if (ld_x < T * C || ld_y < L * C) return fail(CRLOT_EINVAL, "leading dimension too small");
+    if (int64_t(n_groups) * C > INT32_MAX) return fail(CRLOT_EINVAL, "too many streams");
+    DeviceGuard g(p->device);
+    const int64_t need = int64_t(n_groups) * C * (T + L) * int64_t(sizeof(float));
+    if (need > p->planes_bytes) {
+        if (p->d_planes) (void)hipFree(p->d_planes);
+        p->d_planes = nullptr;
+        p->planes_bytes = 0;
+        if (hipMalloc(&p->d_planes, size_t(need)) != hipSuccess)
+            return fail(CRLOT_ENOMEM, "channel-plane workspace hipMalloc failed");
+        p->planes_bytes = need;
+    }
+    float* xin = p->d_planes;
+    float* yout = p->d_planes + int64_t(n_groups) * C * T;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e = crlot::launch_deinterleave(d_x, ld_x, xin, n_groups, T, channels, s);
+    if (e != hipSuccess) return hip_fail(e, "deinterleave kernel launch");
+    const int rc = crlot_roundtrip(p, xin, yout, int32_t(n_groups * C), T, T, L, stream);
+    if (rc != CRLOT_OK) return rc;
+    e = crlot::launch_interleave(yout, L, d_y, ld_y, n_groups, channels, s);
+    if (e != hipSuccess) return hip_fail(e, "interleave kernel launch");
     return CRLOT_OK;
 }
 

@@ -164,6 +164,11 @@ hipError_t launch_cfft(const Geometry& g, const DevTables& t, const float* in, f
 // (start + j) mod R for j < len <= R.  produce: out[c*ldo + j] = ring / den at
 // (rp + j) mod R, j < len, ring cleared; peak (nullable) = running max |out|
 // over channel 0's first n_total samples, as float bits.
+// PCM layout: groups of T rows x C interleaved samples <-> channel planes [g][c][T].
+hipError_t launch_deinterleave(const float* x, int64_t ld_x, float* planes, int groups, int64_t T, int C,
+                               hipStream_t s);
+hipError_t launch_interleave(const float* planes, int64_t L, float* y, int64_t ld_y, int groups, int C,
+                             hipStream_t s);
 hipError_t launch_ola_add(float* ring, int channels, int64_t R, const float* src, int64_t cs,
                           int64_t js, const float* win, int64_t start, int64_t len, float gain,
                           hipStream_t s);

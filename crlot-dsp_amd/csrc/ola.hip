@@ -81,7 +81,48 @@ __global__ void __launch_bounds__(256) k_ola_produce(float* __restrict__ ring, i
     if ((threadIdx.x & 63) == 0 && a > 0.0f) atomicMax(peak, __float_as_uint(a));
 }
 
+// PCM layout for the batched multi-channel round trip (crlot_roundtrip_interleaved):
+// group g holds T rows of C interleaved samples (the reference's PCM,
+// framer.cc:15-35).  k_deinterleave writes channel planes [g][c][t]; one thread
+// per row reads its C contiguous floats and writes C coalesced planes, so both
+// sides stream at HBM rate with no LDS.  k_interleave is the inverse.
+__global__ void __launch_bounds__(256) k_deinterleave(const float* __restrict__ x, int64_t ld_x,
+                                                      float* __restrict__ planes, int64_t T, int C) {
+    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t g = blockIdx.y;
+    if (t >= T) return;
+    const float* row = x + g * ld_x + t * C;
+    float* o = planes + g * C * T + t;
+    for (int c = 0; c < C; ++c) o[int64_t(c) * T] = row[c];
+}
+
+__global__ void __launch_bounds__(256) k_interleave(const float* __restrict__ planes, int64_t L,
+                                                    float* __restrict__ y, int64_t ld_y, int C) {
+    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t g = blockIdx.y;
+    if (t >= L) return;
+    const float* in = planes + g * C * L + t;
+    float* row = y + g * ld_y + t * C;
+    for (int c = 0; c < C; ++c) row[c] = in[int64_t(c) * L];
+}
+
 }  // namespace
+
+hipError_t launch_deinterleave(const float* x, int64_t ld_x, float* planes, int groups, int64_t T, int C,
+                               hipStream_t s) {
+    if (groups <= 0 || T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_deinterleave, dim3(unsigned((T + 255) / 256), unsigned(groups)), dim3(256), 0, s,
+                       x, ld_x, planes, T, C);
+    return hipGetLastError();
+}
+
+hipError_t launch_interleave(const float* planes, int64_t L, float* y, int64_t ld_y, int groups, int C,
+                             hipStream_t s) {
+    if (groups <= 0 || L <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_interleave, dim3(unsigned((L + 255) / 256), unsigned(groups)), dim3(256), 0, s,
+                       planes, L, y, ld_y, C);
+    return hipGetLastError();
+}
 
 hipError_t launch_ola_add(float* ring, int channels, int64_t R, const float* src, int64_t cs,
                           int64_t js, const float* win, int64_t start, int64_t len, float gain,

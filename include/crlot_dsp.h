@@ -144,6 +144,17 @@ int crlot_plan_reserve(crlot_plan* plan, int64_t bytes);
 int crlot_roundtrip(crlot_plan* plan, const float* d_x, float* d_y, int32_t n_streams, int64_t T,
                     int64_t ld_x, int64_t ld_y, void* stream);
 
+/* The same round trip for n_groups groups of `channels` interleaved channels
+ * (the reference's multi-channel PCM: Framer::set_params(N, H, C) frames N*C
+ * interleaved samples, push_frame_AoS deinterleaves them; framer.cc:15-35,
+ * aos_to_soa.cc:7-18): group g's input is T rows of C samples at d_x + g*ld_x
+ * (ld_x >= T*C), its output F*H rows of C samples at d_y + g*ld_y.  Every
+ * channel is an independent stream, bit-identical to crlot_roundtrip on that
+ * channel's plane.  Runs deinterleave -> the mono kernels -> interleave through
+ * a plan-owned workspace of n_groups*C*(T + F*H) floats (two extra HBM passes). */
+int crlot_roundtrip_interleaved(crlot_plan* plan, const float* d_x, float* d_y, int32_t n_groups,
+                                int32_t channels, int64_t T, int64_t ld_x, int64_t ld_y, void* stream);
+
 /* Per-stage outputs of the same path (parity/debug): d_frames gets, per
  * stream and frame, the N-sample push_frame_AoS input (sanitized inverse
  * output, before the synthesis window), [s][k][N]; d_spec (optional) the
