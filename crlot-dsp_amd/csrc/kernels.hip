@@ -612,6 +612,9 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     dev::pc* qb = xb + dev::kP4Xbuf + wave * dev::kPairXbuf;
 
+    // as the fix-up walker after k_stft_ola_pair4k_hot (pair4k.hip): only the
+    // chunks it flagged (uniform per workgroup, before any barrier)
+    if (!a.fix_all && a.t.pflags[blockIdx.x] == 0u) return;
     const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -2014,6 +2017,15 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     }
 }
 
+// CRLOT_PAIR4K_NOHOT=1 (A/B): the two-regime walker alone over every chunk.
+static bool pair4k_hot_disabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("CRLOT_PAIR4K_NOHOT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 // K_pair4k: N = 4096, H = 256 SH, one 256-lane workgroup per chunk, two per CU.
 template <int SH>
 static hipError_t pair4k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
@@ -2090,6 +2102,15 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
         choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 2, a.n_chunks, a.M);
         chunk_override(F, a);
         const int64_t grid4 = int64_t(n_streams) * a.n_chunks;
+        if (!t.pflags || t.pflags_len < grid4) return hipErrorInvalidValue;
+        // the paired-only hot walker, then the two-regime walker over the chunks it
+        // flagged; a spectral gain or reflect/edge padding: the two-regime walker alone
+        if (!t.gain && a.pad_mode == 0 && !pair4k_hot_disabled()) {
+            hipError_t e = launch_pair4k_hot(g.h / 256, a, grid4, stream);
+            if (e != hipSuccess) return e;
+        } else {
+            a.fix_all = 1;
+        }
         switch (g.h / 256) {
             case 2: return pair4k_sh<2>(a, grid4, stream);
             case 4: return pair4k_sh<4>(a, grid4, stream);

@@ -1,0 +1,279 @@
+// pair4k.hip -- K_pair4k's hot walker k_stft_ola_pair4k_hot (N = 4096, config 3).
+//
+// The same walk, transform and arithmetic as k_stft_ola_pair4k (kernels.hip),
+// restructured the way K_pair's hot walker is (pair1k.hip):
+//   * paired regime only: a hop outside the paired range, an output below the
+//     sanitize threshold or a block outside Markstein's exact range flags the
+//     workgroup's chunk, and k_stft_ola_pair4k (the two-regime walker, run after
+//     it with the flags) redoes exactly those chunks -- so the per-pair
+//     __syncthreads_or regime votes and the per-sample sanitize selects leave the
+//     loop;
+//   * the two workgroup exchanges of a pair use two buffers (A forward, B
+//     inverse), so each costs one barrier instead of two: between a buffer's
+//     reads and its next writes every wave passes the other buffer's barrier;
+//   * each wave's quarter-wave transposes run in the exchange rows it alone
+//     reads (forward, A) or writes (inverse, B), so the double buffer costs no
+//     extra LDS: two 78 KB workgroups per CU as before;
+//   * hops and OLA blocks rotate through registers (compile-time slots), no
+//     shifting.
+// Outputs are bit-identical to k_stft_ola_pair4k: every paired pair runs the
+// same operations in the same order.
+#include <type_traits>
+
+#include "fft_pair4k.h"
+#include "fused_common.h"
+
+namespace crlot {
+namespace fk {
+
+namespace {
+
+// Exchange rows of 304 complex: a wave's four rows (1216) hold a 1152-element
+// transpose buffer; 2432 B = 128 B mod 256 B keeps the 16-lane groups of a
+// 32-lane b64 access on distinct banks, as kP4Stride does.
+constexpr int kS = 304;
+constexpr int kBuf = 16 * kS;
+
+// (lane t, reg k1) -> (lane 16 k1 + x, reg r), t = x + 16 r, through buffer A
+__device__ __forceinline__ void xchg_fwd(dev::pc (&v)[16], dev::pc* A, int t) {
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) A[kS * k1 + t] = v[k1];
+    __syncthreads();
+    const dev::pc* rb = A + kS * (t >> 4) + (t & 15);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = rb[16 * r];
+}
+// the inverse mapping through buffer B
+__device__ __forceinline__ void xchg_inv(dev::pc (&v)[16], dev::pc* B, int t) {
+    dev::pc* wb = B + kS * (t >> 4) + (t & 15);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) wb[16 * r] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) v[k1] = B[kS * k1 + t];
+}
+
+__device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const dev::Pair4kTw& tw, int t, int wave) {
+    dev::pdft16<false>(v);
+    {
+        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+        dev::pc_tw_run<false>(v, idx, [&](int i) { return tw.w1[i]; });
+    }
+    xchg_fwd(v, A, t);
+    dev::pdft16<false>(v);
+    {
+        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+        dev::pc_tw_run<false>(v, idx, [&](int i) { return tw.w2[i]; });
+    }
+    dev::transpose16(v, A + kS * 4 * wave, t & 63);  // this wave's own rows of A
+    dev::pdft16<false>(v);
+}
+
+__device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const dev::Pair4kTw& tw, int t, int wave) {
+    dev::pdft16<true>(v);
+    dev::transpose16(v, B + kS * 4 * wave, t & 63);  // this wave's own rows of B
+    {
+        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+        dev::pc_tw_run<true>(v, idx, [&](int i) { return tw.w2[i]; });
+    }
+    dev::pdft16<true>(v);
+    xchg_inv(v, B, t);
+    {
+        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+        dev::pc_tw_run<true>(v, idx, [&](int i) { return tw.w1[i]; });
+    }
+    dev::pdft16<true>(v);
+}
+
+template <int NB>
+struct Rot4k {
+    static constexpr int R = NB == 2 ? 8 : NB == 4 ? 8 : 16;
+    static constexpr int U = R / 2;
+    static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
+};
+
+template <int SH>
+__device__ __forceinline__ void load_hop4k0(float* dst, __amdgpu_buffer_rsrc_t rx, int t, int origin) {
+    const int v = (origin + t) * 4;  // out-of-range lanes (either side) read 0: see load_hop0
+#pragma unroll
+    for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, v + q * 1024, 0);
+}
+
+template <int SH>
+__device__ __forceinline__ void load_den4kh(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int t, int b) {
+#pragma unroll
+    for (int j = 0; j < 2 * SH / 4; ++j) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, t * (8 * SH), b * (2048 * SH) + 16 * j, 0);
+        const unsigned u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];  // (see bload2)
+        dr[4 * j] = __builtin_bit_cast(float, u0);
+        dr[4 * j + 1] = __builtin_bit_cast(float, u1);
+        dr[4 * j + 2] = __builtin_bit_cast(float, u2);
+        dr[4 * j + 3] = __builtin_bit_cast(float, u3);
+    }
+}
+
+}  // namespace
+
+constexpr size_t kPair4kHotLds = sizeof(dev::pc) * 2 * kBuf;
+
+template <int SH, int NB>
+__global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k_hot(const FusedArgs a) {
+    constexpr int E = 16, N = 4096, H = 256 * SH;
+    constexpr int R = Rot4k<NB>::R, U = Rot4k<NB>::U;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    dev::pc* A = reinterpret_cast<dev::pc*>(smem);
+    dev::pc* B = A + kBuf;
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+
+    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
+    const float g = a.gain;
+    const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
+
+    dev::Pair4kTw tw;
+    dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw4), t);
+    float wa[E], ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = a.t.wa[t + 256 * m];
+        ws[m] = a.t.wsn[t + 256 * m];
+    }
+
+    // a hop keeps the paired regime iff every sample is 0 or in [px_lo, px_hi]
+    // (hop_ok_bits on this lane's samples; the workgroup's verdict is the OR at the end)
+    bool bad = false;
+    auto hop_check = [&](const float (&h)[SH]) {
+        uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const uint32_t u = __builtin_bit_cast(uint32_t, h[q]) & 0x7fffffffu;
+            mx = max(mx, u);
+            mn = min(mn, u - 1u);
+        }
+        bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
+    };
+    float xr[R][SH];
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop4k0<SH>(xr[h], rx, t, (fs + h) * H - a.pad);
+        hop_check(xr[h]);
+    }
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+
+    // produce(H) of block k: Markstein division, exact for sums 0 or |acc| in
+    // [2^-64, 2^64]; anything else flags the chunk for the IEEE division
+    auto emit = [&](const float (&av)[SH], int k, const float (&dr)[2 * SH]) {
+        int ex_lo = 0, ex_hi = 0;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const int e = __builtin_amdgcn_frexp_expf(av[q]);
+            ex_lo = min(ex_lo, e);
+            ex_hi = max(ex_hi, e);
+        }
+        bad |= !((ex_lo >= -63) & (ex_hi <= 65));
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
+                                                  k * (4 * H) + q * 1024, 0);
+    };
+
+    auto step = [&](auto phc, int k) {
+        constexpr int PH = decltype(phc)::value;
+        constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
+        load_hop4k0<SH>(xr[(S0 + NB + 1) % R], rx, t, (k + NB + 1) * H - a.pad);
+        load_hop4k0<SH>(xr[(S0 + NB + 2) % R], rx, t, (k + NB + 2) * H - a.pad);
+        const bool partner = k + 1 < a.F;  // frame k+1 past the last: imaginary part 0 (as k_stft_ola_pair4k)
+        dev::pc v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m)
+            v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wa[m],
+                              partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wa[m] : 0.0f);
+        fwd(v, A, tw, t, wave);
+        float dr0[2 * SH], dr1[2 * SH];
+        load_den4kh<SH>(dr0, rp, t, k % a.ring_blocks);
+        load_den4kh<SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
+        inv(v, B, tw, t, wave);
+        // output sanitize: finite here, so only its threshold |v| < 1e-30 N
+        // (= 2^-87.66 at N = 4096) can act; frexp exponents <= -87 flag the chunk
+        {
+            int e[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
+            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -87;
+        }
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            float& r = acc[(B0 + m / SH) % NB][m % SH];
+            r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
+        }
+        emit(acc[B0], k, dr0);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
+            r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
+        }
+        emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
+        hop_check(xr[(S0 + NB + 1) % R]);
+        hop_check(xr[(S0 + NB + 2) % R]);
+    };
+    for (int k = fs; k < f1; k += 2 * U) {
+        step(std::integral_constant<int, 0>(), k);
+        if (k + 2 >= f1) break;
+        step(std::integral_constant<int, 1>(), k + 2);
+        if (k + 4 >= f1) break;
+        step(std::integral_constant<int, 2>(), k + 4);
+        if (k + 6 >= f1) break;
+        step(std::integral_constant<int, 3>(), k + 6);
+        if constexpr (U > 4) {
+            if (k + 8 >= f1) break;
+            step(std::integral_constant<int, 4>(), k + 8);
+            if (k + 10 >= f1) break;
+            step(std::integral_constant<int, 5>(), k + 10);
+            if (k + 12 >= f1) break;
+            step(std::integral_constant<int, 6>(), k + 12);
+            if (k + 14 >= f1) break;
+            step(std::integral_constant<int, 7>(), k + 14);
+        }
+    }
+    // every wave leaves the loop at the same k (f1 is per workgroup): one vote
+    if (__syncthreads_or(bad) && t == 0) a.t.pflags[blockIdx.x] = 1u;
+    else if (t == 0) a.t.pflags[blockIdx.x] = 0u;
+}
+
+hipError_t launch_pair4k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    auto go = [&](auto k) {
+        hipError_t e = set_lds(k, kPair4kHotLds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(256), kPair4kHotLds, stream, a);
+        return hipGetLastError();
+    };
+    switch (sh) {
+        case 2: return go(k_stft_ola_pair4k_hot<2, 8>);
+        case 4: return go(k_stft_ola_pair4k_hot<4, 4>);
+        case 8: return go(k_stft_ola_pair4k_hot<8, 2>);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace fk
+}  // namespace crlot

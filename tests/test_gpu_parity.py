@@ -898,3 +898,23 @@ def test_roundtrip_interleaved_equals_per_channel(pkg, oracle, torch_cuda, n, h,
     ref = oracle.roundtrip_batch(x[0], n, h, mode=oracle.DROP if mode == "drop" else oracle.ZERO_PAD)
     for c in range(C_):
         assert_close(y[0, :, c], ref[c], 0.5, f"group 0 ch {c}")
+
+
+@pytest.mark.parametrize("n,h,T", [(4096, 1024, 123_457), (4096, 512, 60_000), (4096, 2048, 70_001),
+                                   (1024, 256, 50_000)])
+def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h, T):
+    """The paired-only hot walkers (K_pair, K_pair4k) and the two-regime walkers
+    they fall back to agree bit for bit: a spectral gain of exactly 1 sends the
+    plan through the two-regime walker over every chunk (x * 1 is exact), no gain
+    through the hot walker; a burst of out-of-range samples exercises the flagged
+    chunks' fix-up inside the hot run."""
+    torch = torch_cuda
+    x = oracle.synth_streams(6, T, config_id=71)
+    x[2, T // 3:T // 3 + 5] = 1e25   # unpaired regime: that chunk is redone
+    x[4, T // 2] = 1e-33              # tiny sample: also outside the paired range
+    xd = dev(torch, x)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    y_hot = host(plan.roundtrip(xd))
+    plan.set_spectral_gain(np.ones(n // 2 + 1, np.float32))
+    y_fix = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(y_hot), bits(y_fix))
