@@ -151,6 +151,8 @@ int pair_waves_per_cu();
 hipError_t launch_pair(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream);
 // K_pair4k's paired-only hot walker (pair4k.hip), H = 256 * sh; writes pflags per workgroup.
 hipError_t launch_pair4k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
+// ... and K_pair2k's (H = 128 * sh)
+hipError_t launch_pair2k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
 
 }  // namespace fk
 }  // namespace crlot

@@ -786,6 +786,9 @@ __global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     dev::pc* qb = xb + dev::kP2Xbuf + wave * dev::kP2Tbuf;
 
+    // as the fix-up walker after the hot walker (pair4k.hip): only the chunks it
+    // flagged (uniform per workgroup, before any barrier)
+    if (!a.fix_all && a.t.pflags[blockIdx.x] == 0u) return;
     const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -1757,6 +1760,15 @@ hipError_t pair2k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(128), kPair2kLds, stream, a);
     return hipGetLastError();
 }
+// CRLOT_PAIR4K_NOHOT=1 (A/B, N = 4096 and 2048): the two-regime walker alone over every chunk.
+static bool pair4k_hot_disabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("CRLOT_PAIR4K_NOHOT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m);
 // CRLOT_CHUNKS (tuning override: chunks per stream), read once per process so
 // the launch path does no environment lookups.
@@ -1784,6 +1796,15 @@ hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_stream
     a.inv_n = g.inv_n;
     a.gain = g.gain;
     const int64_t grid = int64_t(n_streams) * a.n_chunks;
+    if (!a.t.pflags || a.t.pflags_len < grid) return hipErrorInvalidValue;
+    // the paired-only hot walker where it holds its registers (H = 512), then the
+    // two-regime walker over the chunks it flagged; otherwise the latter alone
+    if (g.h == 512 && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled()) {
+        hipError_t e = launch_pair2k_hot(4, a, grid, stream);
+        if (e != hipSuccess) return e;
+    } else {
+        a.fix_all = 1;
+    }
     switch (g.h / 128) {
         case 2: return pair2k_sh<2>(a, grid, stream);
         case 4: return pair2k_sh<4>(a, grid, stream);
@@ -2015,15 +2036,6 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
         case 16: return fused_e<16>(s, a, grid, stream);
         default: return hipErrorInvalidValue;
     }
-}
-
-// CRLOT_PAIR4K_NOHOT=1 (A/B): the two-regime walker alone over every chunk.
-static bool pair4k_hot_disabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PAIR4K_NOHOT");
-        return e && e[0] == '1';
-    }();
-    return v;
 }
 
 // K_pair4k: N = 4096, H = 256 SH, one 256-lane workgroup per chunk, two per CU.

@@ -1,6 +1,7 @@
-// pair4k.hip -- K_pair4k's hot walker k_stft_ola_pair4k_hot (N = 4096, config 3).
+// pair4k.hip -- the hot walkers of the workgroup frame-pair kernels:
+// k_pair_wg_hot<Geo4k> (N = 4096, config 3) and <Geo2k> (N = 2048).
 //
-// The same walk, transform and arithmetic as k_stft_ola_pair4k (kernels.hip),
+// The same walk, transform and arithmetic as k_stft_ola_pair4k / _pair2k (kernels.hip),
 // restructured the way K_pair's hot walker is (pair1k.hip):
 //   * paired regime only: a hop outside the paired range, an output below the
 //     sanitize threshold or a block outside Markstein's exact range flags the
@@ -13,13 +14,14 @@
 //     reads and its next writes every wave passes the other buffer's barrier;
 //   * each wave's quarter-wave transposes run in the exchange rows it alone
 //     reads (forward, A) or writes (inverse, B), so the double buffer costs no
-//     extra LDS: two 78 KB workgroups per CU as before;
+//     extra LDS: two 78 KB workgroups per CU at N = 4096, four 39 KB ones at 2048;
 //   * hops and OLA blocks rotate through registers (compile-time slots), no
 //     shifting.
-// Outputs are bit-identical to k_stft_ola_pair4k: every paired pair runs the
-// same operations in the same order.
+// Outputs are bit-identical to the two-regime walkers: every paired pair runs
+// the same operations in the same order.
 #include <type_traits>
 
+#include "fft_pair2k.h"
 #include "fft_pair4k.h"
 #include "fused_common.h"
 
@@ -28,82 +30,118 @@ namespace fk {
 
 namespace {
 
-// Exchange rows of 304 complex: a wave's four rows (1216) hold a 1152-element
-// transpose buffer; 2432 B = 128 B mod 256 B keeps the 16-lane groups of a
-// 32-lane b64 access on distinct banks, as kP4Stride does.
-constexpr int kS = 304;
-constexpr int kBuf = 16 * kS;
-
-// (lane t, reg k1) -> (lane 16 k1 + x, reg r), t = x + 16 r, through buffer A
-__device__ __forceinline__ void xchg_fwd(dev::pc (&v)[16], dev::pc* A, int t) {
+// Exchange rows: a wave's own rows hold its 1152-element transpose buffer, and
+// the row stride keeps the lane groups of a 32-lane b64 access on distinct
+// banks (4k: 16-lane groups 2432 B = 128 B mod 256 B apart, as kP4Stride;
+// 2k: 8-lane groups 1216 B = 192 B mod 256 B apart, as kP2Stride).
+template <int SIDE>  // lanes t = x + SIDE r
+struct XchgRows {
+    // (lane t, reg k1) -> (lane SIDE k1 + x, reg r) through buffer A
+    template <int KS>
+    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, int t) {
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) A[kS * k1 + t] = v[k1];
-    __syncthreads();
-    const dev::pc* rb = A + kS * (t >> 4) + (t & 15);
+        for (int k1 = 0; k1 < 16; ++k1) A[KS * k1 + t] = v[k1];
+        __syncthreads();
+        const dev::pc* rb = A + KS * (t / SIDE) + (t % SIDE);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = rb[16 * r];
-}
-// the inverse mapping through buffer B
-__device__ __forceinline__ void xchg_inv(dev::pc (&v)[16], dev::pc* B, int t) {
-    dev::pc* wb = B + kS * (t >> 4) + (t & 15);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) wb[16 * r] = v[r];
-    __syncthreads();
-#pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) v[k1] = B[kS * k1 + t];
-}
-
-__device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const dev::Pair4kTw& tw, int t, int wave) {
-    dev::pdft16<false>(v);
-    {
-        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-        dev::pc_tw_run<false>(v, idx, [&](int i) { return tw.w1[i]; });
+        for (int r = 0; r < 16; ++r) v[r] = rb[SIDE * r];
     }
-    xchg_fwd(v, A, t);
-    dev::pdft16<false>(v);
-    {
-        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-        dev::pc_tw_run<false>(v, idx, [&](int i) { return tw.w2[i]; });
+    // the inverse mapping through buffer B
+    template <int KS>
+    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, int t) {
+        dev::pc* wb = B + KS * (t / SIDE) + (t % SIDE);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) wb[SIDE * r] = v[r];
+        __syncthreads();
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) v[k1] = B[KS * k1 + t];
     }
-    dev::transpose16(v, A + kS * 4 * wave, t & 63);  // this wave's own rows of A
-    dev::pdft16<false>(v);
+};
+
+template <bool INV, typename TW>
+__device__ __forceinline__ void tw_all(dev::pc (&v)[16], const TW& w) {
+    constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+    dev::pc_tw_run<INV>(v, idx, [&](int i) { return w[i]; });
 }
 
-__device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const dev::Pair4kTw& tw, int t, int wave) {
-    dev::pdft16<true>(v);
-    dev::transpose16(v, B + kS * 4 * wave, t & 63);  // this wave's own rows of B
-    {
-        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-        dev::pc_tw_run<true>(v, idx, [&](int i) { return tw.w2[i]; });
+// N = 4096: 256 lanes (fft_pair4k.h), rows of 304, a wave's own rows 4w .. 4w+3
+struct Geo4k {
+    static constexpr int N = 4096, L = 256, KS = 304, ROWS_PER_WAVE = 4, MIN_EXP = -87;  // 1e-30 N = 2^-87.66
+    using Tw = dev::Pair4kTw;
+    using X = XchgRows<16>;
+    static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
+        dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
     }
-    dev::pdft16<true>(v);
-    xchg_inv(v, B, t);
-    {
-        constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-        dev::pc_tw_run<true>(v, idx, [&](int i) { return tw.w1[i]; });
+    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const Tw& tw, int t, int wave) {
+        dev::pdft16<false>(v);
+        tw_all<false>(v, tw.w1);
+        X::fwd<KS>(v, A, t);
+        dev::pdft16<false>(v);
+        tw_all<false>(v, tw.w2);
+        dev::transpose16(v, A + KS * ROWS_PER_WAVE * wave, t & 63);
+        dev::pdft16<false>(v);
     }
-    dev::pdft16<true>(v);
-}
+    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const Tw& tw, int t, int wave) {
+        dev::pdft16<true>(v);
+        dev::transpose16(v, B + KS * ROWS_PER_WAVE * wave, t & 63);
+        tw_all<true>(v, tw.w2);
+        dev::pdft16<true>(v);
+        X::inv<KS>(v, B, t);
+        tw_all<true>(v, tw.w1);
+        dev::pdft16<true>(v);
+    }
+};
+
+// N = 2048: 128 lanes (fft_pair2k.h), rows of 152, a wave's own rows 8w .. 8w+7
+struct Geo2k {
+    static constexpr int N = 2048, L = 128, KS = 152, ROWS_PER_WAVE = 8, MIN_EXP = -88;  // 1e-30 N = 2^-88.66
+    using Tw = dev::Pair2kTw;
+    using X = XchgRows<8>;
+    static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
+        dev::pair2k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
+    }
+    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const Tw& tw, int t, int wave) {
+        dev::pdft16<false>(v);
+        tw_all<false>(v, tw.w1);
+        X::fwd<KS>(v, A, t);
+        dev::pdft16<false>(v);
+        tw_all<false>(v, tw.w2);
+        dev::pair2k_t8(v, A + KS * ROWS_PER_WAVE * wave, t & 63);
+        dev::pdft8_halves<false>(v);
+    }
+    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const Tw& tw, int t, int wave) {
+        dev::pdft8_halves<true>(v);
+        dev::pair2k_t8(v, B + KS * ROWS_PER_WAVE * wave, t & 63);
+        tw_all<true>(v, tw.w2);
+        dev::pdft16<true>(v);
+        X::inv<KS>(v, B, t);
+        tw_all<true>(v, tw.w1);
+        dev::pdft16<true>(v);
+    }
+};
+static_assert(Geo4k::KS * Geo4k::ROWS_PER_WAVE >= dev::kPairXbuf, "4k transpose in own rows");
+static_assert(Geo2k::KS * Geo2k::ROWS_PER_WAVE >= dev::kP2Tbuf, "2k transpose in own rows");
 
 template <int NB>
-struct Rot4k {
+struct RotWg {
     static constexpr int R = NB == 2 ? 8 : NB == 4 ? 8 : 16;
     static constexpr int U = R / 2;
     static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
 };
 
-template <int SH>
-__device__ __forceinline__ void load_hop4k0(float* dst, __amdgpu_buffer_rsrc_t rx, int t, int origin) {
+template <int L, int SH>
+__device__ __forceinline__ void load_hop_wg0(float* dst, __amdgpu_buffer_rsrc_t rx, int t, int origin) {
     const int v = (origin + t) * 4;  // out-of-range lanes (either side) read 0: see load_hop0
 #pragma unroll
-    for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, v + q * 1024, 0);
+    for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, v + q * (4 * L), 0);
 }
 
-template <int SH>
-__device__ __forceinline__ void load_den4kh(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int t, int b) {
+// den | rden of block b (DevTables::pden4: [block][L][den SH | rden SH])
+template <int L, int SH>
+__device__ __forceinline__ void load_den_wg(float (&dr)[2 * SH], __amdgpu_buffer_rsrc_t rp, int t, int b) {
 #pragma unroll
     for (int j = 0; j < 2 * SH / 4; ++j) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, t * (8 * SH), b * (2048 * SH) + 16 * j, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rp, t * (8 * SH), b * (8 * L * SH) + 16 * j, 0);
         const unsigned u0 = v[0], u1 = v[1], u2 = v[2], u3 = v[3];  // (see bload2)
         dr[4 * j] = __builtin_bit_cast(float, u0);
         dr[4 * j + 1] = __builtin_bit_cast(float, u1);
@@ -114,17 +152,22 @@ __device__ __forceinline__ void load_den4kh(float (&dr)[2 * SH], __amdgpu_buffer
 
 }  // namespace
 
-constexpr size_t kPair4kHotLds = sizeof(dev::pc) * 2 * kBuf;
+// Both geometries: two waves per SIMD (<= 256 VGPRs), two 4k / four 2k workgroups per CU.
+template <typename G>
+constexpr size_t hot_lds() {
+    return sizeof(dev::pc) * 2 * 16 * G::KS;  // exchange buffers A | B
+}
 
-template <int SH, int NB>
-__global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k_hot(const FusedArgs a) {
-    constexpr int E = 16, N = 4096, H = 256 * SH;
-    constexpr int R = Rot4k<NB>::R, U = Rot4k<NB>::U;
+// One workgroup (G::L lanes) walks one chunk; lane t holds samples t + L m.
+template <typename G, int SH, int NB>
+__global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pair_wg_hot(const FusedArgs a) {
+    constexpr int E = 16, N = G::N, L = G::L, H = L * SH;
+    constexpr int R = RotWg<NB>::R, U = RotWg<NB>::U;
     static_assert(NB * SH == E, "N = NB * H");
     static_assert(SH >= 2, "den rows are read 16 bytes at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     dev::pc* A = reinterpret_cast<dev::pc*>(smem);
-    dev::pc* B = A + kBuf;
+    dev::pc* B = A + 16 * G::KS;
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
 
@@ -139,13 +182,13 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k_hot(const FusedArgs 
     const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
-    dev::Pair4kTw tw;
-    dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw4), t);
+    typename G::Tw tw;
+    G::tw_load(tw, a.t.ptw4, t);
     float wa[E], ws[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        wa[m] = a.t.wa[t + 256 * m];
-        ws[m] = a.t.wsn[t + 256 * m];
+        wa[m] = a.t.wa[t + L * m];
+        ws[m] = a.t.wsn[t + L * m];
     }
 
     // a hop keeps the paired regime iff every sample is 0 or in [px_lo, px_hi]
@@ -164,7 +207,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k_hot(const FusedArgs 
     float xr[R][SH];
 #pragma unroll
     for (int h = 0; h <= NB; ++h) {
-        load_hop4k0<SH>(xr[h], rx, t, (fs + h) * H - a.pad);
+        load_hop_wg0<L, SH>(xr[h], rx, t, (fs + h) * H - a.pad);
         hop_check(xr[h]);
     }
     float acc[NB][SH];
@@ -191,33 +234,33 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k_hot(const FusedArgs 
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
-                                                  k * (4 * H) + q * 1024, 0);
+                                                  k * (4 * H) + q * (4 * L), 0);
     };
 
     auto step = [&](auto phc, int k) {
         constexpr int PH = decltype(phc)::value;
         constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
-        load_hop4k0<SH>(xr[(S0 + NB + 1) % R], rx, t, (k + NB + 1) * H - a.pad);
-        load_hop4k0<SH>(xr[(S0 + NB + 2) % R], rx, t, (k + NB + 2) * H - a.pad);
-        const bool partner = k + 1 < a.F;  // frame k+1 past the last: imaginary part 0 (as k_stft_ola_pair4k)
+        load_hop_wg0<L, SH>(xr[(S0 + NB + 1) % R], rx, t, (k + NB + 1) * H - a.pad);
+        load_hop_wg0<L, SH>(xr[(S0 + NB + 2) % R], rx, t, (k + NB + 2) * H - a.pad);
+        const bool partner = k + 1 < a.F;  // frame k+1 past the last: imaginary part 0 (as the two-regime walker)
         dev::pc v[E];
 #pragma unroll
         for (int m = 0; m < E; ++m)
             v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wa[m],
                               partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wa[m] : 0.0f);
-        fwd(v, A, tw, t, wave);
+        G::fwd(v, A, tw, t, wave);
         float dr0[2 * SH], dr1[2 * SH];
-        load_den4kh<SH>(dr0, rp, t, k % a.ring_blocks);
-        load_den4kh<SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
-        inv(v, B, tw, t, wave);
-        // output sanitize: finite here, so only its threshold |v| < 1e-30 N
-        // (= 2^-87.66 at N = 4096) can act; frexp exponents <= -87 flag the chunk
+        load_den_wg<L, SH>(dr0, rp, t, k % a.ring_blocks);
+        load_den_wg<L, SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
+        G::inv(v, B, tw, t, wave);
+        // output sanitize: finite here, so only its threshold |v| < 1e-30 N can
+        // act; frexp exponents <= G::MIN_EXP flag the chunk
         {
             int e[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int m = 0; m < E; ++m)
                 e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
-            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -87;
+            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= G::MIN_EXP;
         }
 #pragma unroll
         for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
@@ -256,23 +299,32 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k_hot(const FusedArgs 
         }
     }
     // every wave leaves the loop at the same k (f1 is per workgroup): one vote
-    if (__syncthreads_or(bad) && t == 0) a.t.pflags[blockIdx.x] = 1u;
-    else if (t == 0) a.t.pflags[blockIdx.x] = 0u;
+    const bool any_bad = __syncthreads_or(bad);
+    if (t == 0) a.t.pflags[blockIdx.x] = any_bad ? 1u : 0u;
 }
 
-hipError_t launch_pair4k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+template <typename G>
+hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    constexpr size_t lds = hot_lds<G>();
     auto go = [&](auto k) {
-        hipError_t e = set_lds(k, kPair4kHotLds);
+        hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(256), kPair4kHotLds, stream, a);
+        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(G::L), lds, stream, a);
         return hipGetLastError();
     };
     switch (sh) {
-        case 2: return go(k_stft_ola_pair4k_hot<2, 8>);
-        case 4: return go(k_stft_ola_pair4k_hot<4, 4>);
-        case 8: return go(k_stft_ola_pair4k_hot<8, 2>);
+        case 2: return go(k_pair_wg_hot<G, 2, 8>);
+        case 4: return go(k_pair_wg_hot<G, 4, 4>);
+        case 8: return go(k_pair_wg_hot<G, 8, 2>);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t launch_pair4k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    return launch_wg_hot<Geo4k>(sh, a, grid, stream);
+}
+hipError_t launch_pair2k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
+    return launch_wg_hot<Geo2k>(sh, a, grid, stream);
 }
 
 }  // namespace fk
