@@ -263,7 +263,7 @@ int ensure_workspace(crlot_plan* p, int64_t bytes) {
 // K_pair's per-walker flags: at most one walker per frame and stream.  Grown
 // (never shrunk) on the calling thread before the launch that needs them.
 int ensure_pair_flags(crlot_plan* p, int32_t n_streams, int64_t F) {
-    if (!p->pairing || (p->geo.n != 1024 && p->geo.n != 2048 && p->geo.n != 4096)) return CRLOT_OK;
+    if (!p->pairing || (p->geo.n != 512 && p->geo.n != 1024 && p->geo.n != 2048 && p->geo.n != 4096)) return CRLOT_OK;
     const int64_t need = int64_t(n_streams) * F;
     if (need <= p->pflags_len) return CRLOT_OK;
     if (p->d_pflags) (void)hipFree(p->d_pflags);

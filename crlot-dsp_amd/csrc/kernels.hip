@@ -430,6 +430,7 @@ __global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const Fuse
     dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kP512Buf;
     const int gw = blockIdx.x * kP512Waves + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
+    if (!a.fix_all && a.t.pflags[gw] == 0u) return;  // fix-up walker: flagged chunks only
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -612,7 +613,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     dev::pc* qb = xb + dev::kP4Xbuf + wave * dev::kPairXbuf;
 
-    // as the fix-up walker after k_stft_ola_pair4k_hot (pair4k.hip): only the
+    // as the fix-up walker after k_stft_ola_pair4k_hot (pair_hot.hip): only the
     // chunks it flagged (uniform per workgroup, before any barrier)
     if (!a.fix_all && a.t.pflags[blockIdx.x] == 0u) return;
     const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
@@ -786,7 +787,7 @@ __global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
     dev::pc* qb = xb + dev::kP2Xbuf + wave * dev::kP2Tbuf;
 
-    // as the fix-up walker after the hot walker (pair4k.hip): only the chunks it
+    // as the fix-up walker after the hot walker (pair_hot.hip): only the chunks it
     // flagged (uniform per workgroup, before any barrier)
     if (!a.fix_all && a.t.pflags[blockIdx.x] == 0u) return;
     const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
@@ -1729,6 +1730,15 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// CRLOT_PAIR4K_NOHOT=1 (A/B, N = 4096, 2048 and 512): the two-regime walker alone over every chunk.
+static bool pair4k_hot_disabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("CRLOT_PAIR4K_NOHOT");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 // K_pair512: N = 512, H = 64 SH, 4 independent waves per workgroup.
 template <int SH>
 hipError_t pair512_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
@@ -1738,7 +1748,16 @@ hipError_t pair512_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
     const int64_t grid = (waves + kP512Waves - 1) / kP512Waves;
-    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * kP512Waves), lds, stream, a);
+    if (!a.t.pflags || a.t.pflags_len < waves) return hipErrorInvalidValue;
+    FusedArgs b = a;
+    // the paired-only hot walker (H = 128, 256), then this two-regime walker over
+    // the chunks it flagged; a gain or reflect/edge padding: the latter alone
+    if ((SH == 2 || SH == 4) && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled()) {
+        if ((e = launch_pair512_hot(SH, a, waves, kP512Waves, stream)) != hipSuccess) return e;
+    } else {
+        b.fix_all = 1;
+    }
+    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * kP512Waves), lds, stream, b);
     return hipGetLastError();
 }
 hipError_t launch_pair512(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream) {
@@ -1760,15 +1779,6 @@ hipError_t pair2k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(128), kPair2kLds, stream, a);
     return hipGetLastError();
 }
-// CRLOT_PAIR4K_NOHOT=1 (A/B, N = 4096 and 2048): the two-regime walker alone over every chunk.
-static bool pair4k_hot_disabled() {
-    static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PAIR4K_NOHOT");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
 void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m);
 // CRLOT_CHUNKS (tuning override: chunks per stream), read once per process so
 // the launch path does no environment lookups.

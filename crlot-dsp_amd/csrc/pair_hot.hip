@@ -1,7 +1,10 @@
-// pair4k.hip -- the hot walkers of the workgroup frame-pair kernels:
-// k_pair_wg_hot<Geo4k> (N = 4096, config 3) and <Geo2k> (N = 2048).
+// pair_hot.hip -- paired-only hot walkers of the frame-pair kernels other than
+// K_pair (pair1k.hip): k_pair_wg_hot<Geo4k> (N = 4096, config 3) and <Geo2k>
+// (N = 2048), one workgroup per chunk; k_pair512_hot (N = 512, the config-4
+// shape batched), one wave per chunk.
 //
-// The same walk, transform and arithmetic as k_stft_ola_pair4k / _pair2k (kernels.hip),
+// The same walk, transform and arithmetic as k_stft_ola_pair4k / _pair2k /
+// _pair512 (kernels.hip),
 // restructured the way K_pair's hot walker is (pair1k.hip):
 //   * paired regime only: a hop outside the paired range, an output below the
 //     sanitize threshold or a block outside Markstein's exact range flags the
@@ -23,6 +26,7 @@
 
 #include "fft_pair2k.h"
 #include "fft_pair4k.h"
+#include "fft_pair512.h"
 #include "fused_common.h"
 
 namespace crlot {
@@ -161,7 +165,7 @@ constexpr size_t hot_lds() {
 // One workgroup (G::L lanes) walks one chunk; lane t holds samples t + L m.
 template <typename G, int SH, int NB>
 __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pair_wg_hot(const FusedArgs a) {
-    constexpr int E = 16, N = G::N, L = G::L, H = L * SH;
+    constexpr int E = 16, L = G::L, H = L * SH;
     constexpr int R = RotWg<NB>::R, U = RotWg<NB>::U;
     static_assert(NB * SH == E, "N = NB * H");
     static_assert(SH >= 2, "den rows are read 16 bytes at a time");
@@ -312,10 +316,169 @@ hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t s
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(G::L), lds, stream, a);
         return hipGetLastError();
     };
+    if constexpr (G::N == 2048) {  // H = 256 / 1024 spill at N = 2048: the two-regime walker runs those
+        return sh == 4 ? go(k_pair_wg_hot<G, 4, 4>) : hipErrorInvalidValue;
+    } else {
+        switch (sh) {
+            case 2: return go(k_pair_wg_hot<G, 2, 8>);
+            case 4: return go(k_pair_wg_hot<G, 4, 4>);
+            case 8: return go(k_pair_wg_hot<G, 8, 2>);
+            default: return hipErrorInvalidValue;
+        }
+    }
+}
+
+// ---- N = 512: one wave per chunk (W per workgroup, independent), lane l holds
+// samples l + 64 m (m < 8); flags per wave.
+template <int SH, int NB, int W>
+__global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
+    constexpr int E = 8, N = 512, H = 64 * SH;
+    constexpr int R = RotWg<NB>::R, U = RotWg<NB>::U;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    static_assert(N == 512, "threshold exponent");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kP512Buf;
+    const int gw = blockIdx.x * W + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+    const float g = a.gain;
+    const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
+
+    dev::Pair512Tw tw;
+    dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
+    float wa[E], ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = a.t.wa[lane + 64 * m];
+        ws[m] = a.t.wsn[lane + 64 * m];
+    }
+    bool bad = false;
+    auto hop_check = [&](const float (&h)[SH]) {
+        uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const uint32_t u = __builtin_bit_cast(uint32_t, h[q]) & 0x7fffffffu;
+            mx = max(mx, u);
+            mn = min(mn, u - 1u);
+        }
+        bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
+    };
+    float xr[R][SH];
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop0<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
+        hop_check(xr[h]);
+    }
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+    auto emit = [&](const float (&av)[SH], int k, const float (&dr)[2 * SH]) {
+        int ex_lo = 0, ex_hi = 0;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {
+            const int e = __builtin_amdgcn_frexp_expf(av[q]);
+            ex_lo = min(ex_lo, e);
+            ex_hi = max(ex_hi, e);
+        }
+        bad |= !((ex_lo >= -63) & (ex_hi <= 65));
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
+                                                  k * (4 * H) + q * 256, 0);
+    };
+    auto step = [&](auto phc, int k) {
+        constexpr int PH = decltype(phc)::value;
+        constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
+        load_hop0<SH>(xr[(S0 + NB + 1) % R], rx, lane, (k + NB + 1) * H - a.pad);
+        load_hop0<SH>(xr[(S0 + NB + 2) % R], rx, lane, (k + NB + 2) * H - a.pad);
+        const bool partner = k + 1 < a.F;  // as the two-regime walker
+        dev::pc v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m)
+            v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wa[m],
+                              partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wa[m] : 0.0f);
+        dev::pair512_fwd(v, buf, tw, lane);
+        float dr0[2 * SH], dr1[2 * SH];
+        load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
+        load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+        dev::pair512_inv(v, buf, tw, lane);
+        {  // output sanitize threshold 1e-30 N = 2^-90.66: frexp exponents <= -90 flag the chunk
+            int e[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
+            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -90;
+        }
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            float& r = acc[(B0 + m / SH) % NB][m % SH];
+            r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
+        }
+        emit(acc[B0], k, dr0);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
+            r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
+        }
+        emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
+        hop_check(xr[(S0 + NB + 1) % R]);
+        hop_check(xr[(S0 + NB + 2) % R]);
+    };
+    for (int k = fs; k < f1; k += 2 * U) {
+        step(std::integral_constant<int, 0>(), k);
+        if (k + 2 >= f1) break;
+        step(std::integral_constant<int, 1>(), k + 2);
+        if (k + 4 >= f1) break;
+        step(std::integral_constant<int, 2>(), k + 4);
+        if (k + 6 >= f1) break;
+        step(std::integral_constant<int, 3>(), k + 6);
+        if constexpr (U > 4) {
+            if (k + 8 >= f1) break;
+            step(std::integral_constant<int, 4>(), k + 8);
+            if (k + 10 >= f1) break;
+            step(std::integral_constant<int, 5>(), k + 10);
+            if (k + 12 >= f1) break;
+            step(std::integral_constant<int, 6>(), k + 12);
+            if (k + 14 >= f1) break;
+            step(std::integral_constant<int, 7>(), k + 14);
+        }
+    }
+    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if (lane == 0) a.t.pflags[gw] = any_bad ? 1u : 0u;
+}
+
+hipError_t launch_pair512_hot(int sh, const FusedArgs& a, int64_t waves, int w, hipStream_t stream) {
+    constexpr int W = 4;
+    if (w != W) return hipErrorInvalidValue;
+    const size_t lds = sizeof(dev::pc) * dev::kP512Buf * W;
+    const int64_t grid = (waves + W - 1) / W;
+    auto go = [&](auto k) {
+        hipError_t e = set_lds(k, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
+        return hipGetLastError();
+    };
     switch (sh) {
-        case 2: return go(k_pair_wg_hot<G, 2, 8>);
-        case 4: return go(k_pair_wg_hot<G, 4, 4>);
-        case 8: return go(k_pair_wg_hot<G, 8, 2>);
+        case 2: return go(k_pair512_hot<2, 4, W>);
+        case 4: return go(k_pair512_hot<4, 2, W>);
         default: return hipErrorInvalidValue;
     }
 }

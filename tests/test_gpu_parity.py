@@ -901,9 +901,10 @@ def test_roundtrip_interleaved_equals_per_channel(pkg, oracle, torch_cuda, n, h,
 
 
 @pytest.mark.parametrize("n,h,T", [(4096, 1024, 123_457), (4096, 512, 60_000), (4096, 2048, 70_001),
-                                   (2048, 512, 80_003), (2048, 512, 33_000), (1024, 256, 50_000)])
+                                   (2048, 512, 80_003), (2048, 512, 33_000), (1024, 256, 50_000),
+                                   (512, 128, 40_001), (512, 256, 25_000)])
 def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h, T):
-    """The paired-only hot walkers (K_pair, K_pair4k, K_pair2k) and the two-regime walkers
+    """The paired-only hot walkers (K_pair, K_pair4k, K_pair2k, K_pair512) and the two-regime walkers
     they fall back to agree bit for bit: a spectral gain of exactly 1 sends the
     plan through the two-regime walker over every chunk (x * 1 is exact), no gain
     through the hot walker; a burst of out-of-range samples exercises the flagged
