@@ -134,6 +134,13 @@ class StftEngine {
                   "hipMemcpy");
         return y;
     }
+    // groups of `channels` interleaved channels (Framer(N, H, C) PCM): d_x group g
+    // at +g*ld_x (T rows of C), d_y group g at +g*ld_y (output_length(T) rows of C)
+    void roundtrip_interleaved_device(const float* d_x, float* d_y, int n_groups, int channels, int64_t T,
+                                      int64_t ld_x, int64_t ld_y, hipStream_t s = nullptr) {
+        check(crlot_roundtrip_interleaved(plan_.get(), d_x, d_y, n_groups, channels, T, ld_x, ld_y, s),
+              "crlot_roundtrip_interleaved");
+    }
     void set_spectral_gain(const float* gain_or_null) {
         check(crlot_plan_set_spectral_gain(plan_.get(), gain_or_null), "set_spectral_gain");
     }
@@ -162,6 +169,37 @@ class StftEngine {
     }
     Plan plan_;
     DeviceBuffer<float> dx_, dy_;
+};
+
+// Real-time per-hop streaming with hops in host memory (BASELINE config 4):
+// the resident kernel behind crlot_stream_rt_*.  push_hop copies one hop of
+// channels x H samples in ([H][C] interleaved PCM or [C][H]), returns the H
+// output samples per channel in the same layout once the frame completes
+// (DROP Framer + push_frame_AoS + produce(H); 0 before N samples arrived).
+class RealtimeStream {
+   public:
+    RealtimeStream(const StftEngine& eng, int channels, bool interleaved, int depth = 4) {
+        check(crlot_stream_rt_create(eng.plan(), channels, interleaved ? 1 : 0, depth, &st_),
+              "crlot_stream_rt_create");
+    }
+    ~RealtimeStream() { crlot_stream_rt_destroy(st_); }
+    RealtimeStream(const RealtimeStream&) = delete;
+    RealtimeStream& operator=(const RealtimeStream&) = delete;
+    size_t push_hop(const float* hop_in, float* hop_out) {
+        int32_t em = 0;
+        check(crlot_stream_rt_push_hop(st_, hop_in, hop_out, &em), "crlot_stream_rt_push_hop");
+        return size_t(em);
+    }
+    void reset() { check(crlot_stream_rt_reset(st_), "crlot_stream_rt_reset"); }
+    double last_device_ns() const {
+        double ns = 0;
+        check(crlot_stream_rt_info(st_, nullptr, &ns, nullptr), "crlot_stream_rt_info");
+        return ns;
+    }
+    crlot_stream_rt* handle() const { return st_; }
+
+   private:
+    crlot_stream_rt* st_ = nullptr;
 };
 
 // io/wav.h WavReader / WavWriter (same methods; open() returns false on a
