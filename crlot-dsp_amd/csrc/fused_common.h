@@ -20,6 +20,7 @@ struct FusedArgs {
     int pad, pad_mode;  // framing (Geometry)
     float inv_n, gain;
     int fix_all = 0;  // K_pair: the fix-up walker redoes every chunk (padding rules it alone handles)
+    int hop = 0;      // K_pair960 (runtime hop; the power-of-two walkers take it as a template constant)
 };
 
 // FrameQueue padding (Indexing.h:18-37): left side i -> -i-1, right side

@@ -1348,6 +1348,8 @@ struct AnyFusedArgs {
     int out_len_i, n_chunks, M, F, rl;  // rl = ring floats per wave
     int ring_len;
     float gain;
+    const uint32_t* mask;  // K_pair960 flags [stream][mask_chunks], or nullptr: every stream
+    int mask_chunks;
 };
 
 template <bool HAS_GAIN>
@@ -1367,6 +1369,11 @@ __global__ __launch_bounds__(1024) void k_stft_ola_any(const AnyFusedArgs f) {
     const int64_t gw = int64_t(blockIdx.x) * a.waves_per_block + wave;
     if (gw >= int64_t(a.n_streams) * f.n_chunks) return;
     const int64_t s = gw / f.n_chunks, c = gw - s * f.n_chunks;
+    if (f.mask) {  // redo only the streams the pair walker flagged
+        bool any = false;
+        for (int j = 0; j < f.mask_chunks; ++j) any |= f.mask[s * f.mask_chunks + j] != 0u;
+        if (!any) return;
+    }
     const int nbr = f.rl / H;
     const int f0 = int(c) * f.M;
     const int f1 = min(f.F, f0 + f.M);
@@ -2278,7 +2285,8 @@ hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* 
 
 hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,
                             const float* x, float* y, int n_streams, int64_t T, int64_t ld_x,
-                            int64_t ld_y, int64_t F, hipStream_t stream) {
+                            int64_t ld_y, int64_t F, hipStream_t stream, const uint32_t* mask,
+                            int mask_chunks) {
     const int p = g.n / 2;
     if (F <= 0 || n_streams <= 0 || !any_supported(p)) return hipErrorInvalidValue;
     AnyFusedArgs f{};
@@ -2301,6 +2309,8 @@ hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* 
     f.rl = g.h * ((g.n + g.h - 1) / g.h);
     f.ring_len = g.ring_len;
     f.gain = g.gain;
+    f.mask = mask;
+    f.mask_chunks = mask_chunks;
     const size_t tables = sizeof(cf) * (size_t(a.tw_len) + p) + sizeof(float) * 4 * p;  // + ws
     const size_t per_wave = sizeof(cf) * 2 * p + sizeof(float) * f.rl;
     // two workgroups per CU when each still holds >= 3 walkers (their tails overlap),

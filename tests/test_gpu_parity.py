@@ -527,7 +527,8 @@ def test_roundtrip_any_size_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
     for s in range(2):
         assert_close(y[s], ref[s], float(np.max(np.abs(x))), f"N={n} H={h} stream {s}")
     frames, spec = plan.stages(xd)
-    assert np.array_equal(bits(y), bits(host(plan.ola_gather(frames))))
+    plan.set_frame_pairing(False)  # the per-frame walker (N = 960 pairs frames by default)
+    assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(host(plan.ola_gather(frames))))
     _, fr_ref, sp_ref = oracle.roundtrip(x[0], n, h, mode=mode, want_frames=True, want_spec=True)
     assert rel_l2(host(spec)[0], sp_ref) <= REL_L2
 
@@ -722,7 +723,8 @@ def test_stream_any_shape(pkg, oracle, torch_cuda, n, h, interleaved):
     assert y_stream.shape == ref.shape
     for s in range(C_):
         assert_close(y_stream[s], ref[s], 0.5, f"stream ch {s}")
-    if n & (n - 1):  # batched path is the any-size walker too
+    if n & (n - 1):  # batched path is the any-size walker too (per frame: pairing off)
+        plan.set_frame_pairing(False)
         assert np.array_equal(bits(y_stream), bits(host(plan.roundtrip(xd))))
 
 
@@ -919,3 +921,48 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     plan.set_spectral_gain(np.ones(n // 2 + 1, np.float32))
     y_fix = host(plan.roundtrip(xd))
     assert np.array_equal(bits(y_hot), bits(y_fix))
+
+
+# ------------------------------------------------------------------ K_pair960 (N = 960 frame pairs)
+@pytest.mark.parametrize("h,mode,T", [(240, 0, 48_000), (240, 1, 48_001), (480, 0, 30_011), (320, 1, 25_000),
+                                      (256, 0, 40_123), (100, 0, 9_999), (960, 0, 20_000), (240, 0, 700)])
+def test_pair960_vs_oracle_and_chunking(pkg, oracle, torch_cuda, h, mode, T):
+    """N = 960 frames in pairs through one 960-point complex transform (Good-Thomas
+    15 x the 64-lane stage): the oracle within the float32 tolerance, frame
+    counts as the Framer's, and bits independent of the batch (so of the chunking)."""
+    torch = torch_cuda
+    n = 960
+    x = oracle.synth_streams(5, T, config_id=97 + h)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode)
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    assert y.shape == (5, oracle.frame_count(T, n, h, mode) * h)
+    ref = oracle.roundtrip_batch(x, n, h, mode=mode, nthreads=4)
+    for s_ in range(5):
+        assert_close(y[s_], ref[s_], float(np.max(np.abs(x))), f"N=960 H={h} stream {s_}")
+    y1 = host(plan.roundtrip(xd[3:4].contiguous()))  # alone: other chunk counts
+    assert np.array_equal(bits(y1[0]), bits(y[3]))
+
+
+def test_pair960_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda):
+    """A stream with a sample outside the paired range (NaN, 1e30, 1e-35) is
+    recomputed whole by the per-frame walker -- equal bit for bit to the plan with
+    pairing off -- while its neighbours keep the paired bits."""
+    torch = torch_cuda
+    n, h, T = 960, 240, 60_000
+    x = oracle.synth_streams(4, T, config_id=131)
+    x[1, 31_000] = np.nan
+    x[2, 5_000] = 1e30
+    x[3, 44_444] = 1e-35
+    xd = dev(torch, x)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    y = host(plan.roundtrip(xd))
+    y_clean = host(plan.roundtrip(xd[0:1].contiguous()))
+    plan.set_frame_pairing(False)
+    y_pf = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(y[0]), bits(y_clean[0]))
+    for s_ in (1, 2, 3):
+        assert np.array_equal(bits(y[s_]), bits(y_pf[s_])), s_
+    ref = oracle.roundtrip_batch(x[[0, 3]], n, h, nthreads=2)
+    assert_close(y[0], ref[0], float(np.max(np.abs(x[0]))), "clean stream")
+    assert_close(y[3], ref[1], float(np.max(np.abs(x[0]))), "tiny sample stream")
