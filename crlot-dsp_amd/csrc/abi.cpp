@@ -263,8 +263,8 @@ int ensure_workspace(crlot_plan* p, int64_t bytes) {
 // K_pair's per-walker flags: at most one walker per frame and stream.  Grown
 // (never shrunk) on the calling thread before the launch that needs them.
 int ensure_pair_flags(crlot_plan* p, int32_t n_streams, int64_t F) {
-    if (!p->pairing || (p->geo.n != 512 && p->geo.n != 960 && p->geo.n != 1024 && p->geo.n != 2048 &&
-                        p->geo.n != 4096)) return CRLOT_OK;
+    if (!p->pairing || (p->geo.n != 480 && p->geo.n != 512 && p->geo.n != 960 && p->geo.n != 1024 &&
+                        p->geo.n != 2048 && p->geo.n != 4096)) return CRLOT_OK;
     const int64_t need = int64_t(n_streams) * F;
     if (need <= p->pflags_len) return CRLOT_OK;
     if (p->d_pflags) (void)hipFree(p->d_pflags);
@@ -395,8 +395,8 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     if ((n == 1024 && h % 128 == 0 && ring % h == 0) || (n == 512 && h % 128 == 0 && ring % h == 0) ||
         (n == 2048 && h % 256 == 0 && ring % h == 0) ||
         (n == 4096 && h % 512 == 0 && ring % h == 0) ||
-        crlot::pair960_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair960 tables
-        const std::vector<float> ptw = n == 960    ? crlot::build_pair15_twiddles()
+        crlot::pair15_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair15 tables
+        const std::vector<float> ptw = (n == 960 || n == 480) ? crlot::build_pair15_twiddles(n)
                                        : n == 1024 ? crlot::build_pair_twiddles()
                                        : n == 512  ? crlot::build_pair512_twiddles()
                                        : n == 2048 ? crlot::build_pair2k_twiddles()
@@ -558,18 +558,19 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
         return CRLOT_OK;
     }
     if (p->generic && crlot::fused_any_fits(p->geo.n, p->geo.h) && ld_x < (int64_t(1) << 40)) {
-        // N = 960 frame pairs (K_pair960), then the per-frame walker over the streams it flagged
+        // N = 960 / 480 frame pairs (K_pair15), then the per-frame walker over the streams it flagged
+        const int64_t lim = int64_t(1) << 27;
         if (p->pairing && t.ptw && !p->has_gain && p->geo.pad_mode == 0 &&
-            crlot::pair960_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < (int64_t(1) << 29) &&
-            out_len < (int64_t(1) << 29) && ld_x < (int64_t(1) << 40)) {
+            crlot::pair15_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < lim && out_len < lim &&
+            ld_x < lim && ld_y < lim) {
             const int rcf = ensure_pair_flags(p, n_streams, F);
             if (rcf != CRLOT_OK) return rcf;
             const crlot::DevTables tp = tables(p);
-            int nch = 0;
-            e = crlot::launch_pair960(p->geo, tp, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, &nch, s);
-            if (e != hipSuccess) return hip_fail(e, "pair (N = 960) kernel launch");
+            int nch = 0, per = 1;
+            e = crlot::launch_pair15(p->geo, tp, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, &nch, &per, s);
+            if (e != hipSuccess) return hip_fail(e, "pair (N = 15 L) kernel launch");
             e = crlot::launch_fused_any(p->geo, tp, p->d_twany, d_x, d_y, n_streams, T, ld_x, ld_y, F, s,
-                                        tp.pflags, nch);
+                                        tp.pflags, nch, per);
             if (e != hipSuccess) return hip_fail(e, "fused (any size) kernel launch");
             return CRLOT_OK;
         }

@@ -127,5 +127,77 @@ __device__ __forceinline__ void pair15_inv(pc (&v)[16], pc* buf, const Pair15Tw&
     pdft15<true>(v);
 }
 
+// ---- N = 480 = 15 x 32: one transform per 32-lane half (two walks per wave).
+// Half-lane h (0..31) holds z[h + 32 m], m < 15.  After the 15-point DFT over
+// the registers and W480^{h k1}, a batch of 32-point DFTs over the half's lanes,
+// h = b + 16 a: lane bit 4 (a) swapped with register bit 3 (v_permlane16_swap
+// stays inside each 32-lane half), DFT2, W32^{b c}, the quarter-wave 16 x 16
+// transpose, DFT16.  k = k1 + 15 (c + 2 d).
+__device__ __forceinline__ void lane_reg_swap_b4r3(pc (&v)[16]) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        float ar = v[r].x, ai = v[r].y, br = v[r + 8].x, bi = v[r + 8].y;
+        swap_f(ar, br, false);
+        swap_f(ai, bi, false);
+        v[r] = pc_mk(ar, ai);
+        v[r + 8] = pc_mk(br, bi);
+    }
+}
+
+// w1[k1 - 1] = W480^{h k1} (k1 = 1..14), w32 = W32^{h & 15}
+struct Pair15hTw {
+    pc w1[14];
+    pc w32;
+};
+// Device table (float pairs): [14][32] of W480^{h k1}, then [16] of W32^{b}.
+constexpr int kP15hTw = 14 * 32 + 16;
+__device__ __forceinline__ void pair15h_tw_load(Pair15hTw& tw, const pc* g, int hl) {
+#pragma unroll
+    for (int k = 1; k < 15; ++k) tw.w1[k - 1] = g[(k - 1) * 32 + hl];
+    tw.w32 = g[14 * 32 + (hl & 15)];
+}
+
+__device__ __forceinline__ void pair15h_fwd(pc (&v)[16], pc* buf, const Pair15hTw& tw, int lane) {
+    pdft15<false>(v);
+    {
+        constexpr int idx[14] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14};
+        pc_tw_run<false>(v, idx, [&](int i) { return tw.w1[i]; });
+    }
+    lane_reg_swap_b4r3(v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const pc a = v[j], b = v[j + 8];
+        v[j] = a + b;
+        v[j + 8] = a - b;
+    }
+    {
+        constexpr int idx[8] = {8, 9, 10, 11, 12, 13, 14, 15};
+        pc_tw_run<false>(v, idx, [&](int) { return tw.w32; });
+    }
+    transpose16(v, buf, lane);
+    pdft16<false>(v);
+}
+
+__device__ __forceinline__ void pair15h_inv(pc (&v)[16], pc* buf, const Pair15hTw& tw, int lane) {
+    pdft16<true>(v);
+    transpose16(v, buf, lane);
+    {
+        constexpr int idx[8] = {8, 9, 10, 11, 12, 13, 14, 15};
+        pc_tw_run<true>(v, idx, [&](int) { return tw.w32; });
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const pc a = v[j], b = v[j + 8];
+        v[j] = a + b;
+        v[j + 8] = a - b;
+    }
+    lane_reg_swap_b4r3(v);
+    {
+        constexpr int idx[14] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14};
+        pc_tw_run<true>(v, idx, [&](int i) { return tw.w1[i]; });
+    }
+    pdft15<true>(v);
+}
+
 }  // namespace dev
 }  // namespace crlot

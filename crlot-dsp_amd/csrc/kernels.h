@@ -107,21 +107,22 @@ hipError_t launch_stream_any(const Geometry& g, const DevTables& t, const float*
                              int64_t q, int64_t k, hipStream_t stream);
 
 // Fused any-size walker (OLA ring in LDS): bit-identical to synth_any + ola_gather.
-// mask (optional): per-chunk flags of a K_pair960 launch with mask_chunks chunks
-// per stream; only streams with a flagged chunk are walked.
+// mask (optional): per-walker flags of a K_pair15 launch, [stream / mask_div][mask_chunks],
+// bit (stream % mask_div) for the stream; only streams with a flagged walker are walked.
 bool fused_any_fits(int n, int h);
 hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,
                             const float* x, float* y, int n_streams, int64_t T, int64_t ld_x,
                             int64_t ld_y, int64_t F, hipStream_t stream,
-                            const uint32_t* mask = nullptr, int mask_chunks = 0);
+                            const uint32_t* mask = nullptr, int mask_chunks = 0, int mask_div = 1);
 
-// K_pair960 (pair_any.hip): N = 960 frame pairs, paired regime only, flags per
-// walker in t.pflags (n_streams x *n_chunks); table t.ptw = build_pair15_twiddles().
-bool pair960_supported(int n, int h, int ring_len);
-hipError_t launch_pair960(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams,
-                          int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks,
-                          hipStream_t stream);
-std::vector<float> build_pair15_twiddles();
+// K_pair15 (pair_any.hip): N = 960 / 480 frame pairs, paired regime only; flags
+// per walker in t.pflags ([stream / *streams_per_walk][*n_chunks]); table t.ptw =
+// build_pair15_twiddles(N).
+bool pair15_supported(int n, int h, int ring_len);
+hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams,
+                         int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks,
+                         int* streams_per_walk, hipStream_t stream);
+std::vector<float> build_pair15_twiddles(int n);
 hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
                           const float* in, float* out, int batch, int64_t ld_in, int64_t inc_in,
                           int64_t ld_out, int64_t inc_out, hipStream_t stream);

@@ -1411,8 +1411,8 @@ struct AnyFusedArgs {
     int out_len_i, n_chunks, M, F, rl;  // rl = ring floats per wave
     int ring_len;
     float gain;
-    const uint32_t* mask;  // K_pair960 flags [stream][mask_chunks], or nullptr: every stream
-    int mask_chunks;
+    const uint32_t* mask;  // K_pair15 flags [stream / mask_div][mask_chunks], or nullptr: every stream
+    int mask_chunks, mask_div;
 };
 
 template <bool HAS_GAIN>
@@ -1434,7 +1434,8 @@ __global__ __launch_bounds__(1024) void k_stft_ola_any(const AnyFusedArgs f) {
     const int64_t s = gw / f.n_chunks, c = gw - s * f.n_chunks;
     if (f.mask) {  // redo only the streams the pair walker flagged
         bool any = false;
-        for (int j = 0; j < f.mask_chunks; ++j) any |= f.mask[s * f.mask_chunks + j] != 0u;
+        for (int j = 0; j < f.mask_chunks; ++j)
+            any |= ((f.mask[(s / f.mask_div) * f.mask_chunks + j] >> (s % f.mask_div)) & 1u) != 0u;
         if (!any) return;
     }
     const int nbr = f.rl / H;
@@ -2349,7 +2350,7 @@ hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* 
 hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,
                             const float* x, float* y, int n_streams, int64_t T, int64_t ld_x,
                             int64_t ld_y, int64_t F, hipStream_t stream, const uint32_t* mask,
-                            int mask_chunks) {
+                            int mask_chunks, int mask_div) {
     const int p = g.n / 2;
     if (F <= 0 || n_streams <= 0 || !any_supported(p)) return hipErrorInvalidValue;
     AnyFusedArgs f{};
@@ -2374,6 +2375,7 @@ hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* 
     f.gain = g.gain;
     f.mask = mask;
     f.mask_chunks = mask_chunks;
+    f.mask_div = mask_div > 0 ? mask_div : 1;
     const size_t tables = sizeof(cf) * (size_t(a.tw_len) + p) + sizeof(float) * 4 * p;  // + ws
     const size_t per_wave = sizeof(cf) * 2 * p + sizeof(float) * f.rl;
     // two workgroups per CU when each still holds >= 3 walkers (their tails overlap),

@@ -1,16 +1,22 @@
-// pair_any.hip -- K_pair960: the frame-pair round trip at N = 960 (20 ms at
-// 48 kHz), any hop H whose ring the plan allows.
+// pair_any.hip -- K_pair15: the frame-pair round trip at N = 960 (20 ms at
+// 48 kHz, one transform per wave) and N = 480 (10 ms, one per 32-lane half),
+// any hop H whose ring the plan allows.
 //
-// Frames 2j and 2j+1 of a stream travel as one 960-point complex transform per
-// wave (fft_pair15.h), z = x_2j w + i x_2j+1 w, as the power-of-two pair kernels
-// do.  H is in general not a multiple of the 64 lanes, so a sample does not stay
-// in its lane from frame to frame: every pair loads its two frames whole (15
-// dwords per lane each, mostly L2 hits -- each sample is read N/H times) and
-// the overlap-add runs in a per-wave LDS ring of H (ceil(N/H) + 1) floats:
-// push frame k (fma(o * ws, g, ring) in ascending k), produce block k (ring /
-// den, IEEE division, then clear), push frame k+1, produce block k+1 -- the
+// Frames 2j and 2j+1 of a stream travel as one N-point complex transform,
+// z = x_2j w + i x_2j+1 w, as the power-of-two pair kernels do (fft_pair15.h:
+// a Good-Thomas 15-point DFT over 15 registers, then a batch of 64- or 32-point
+// DFTs over the lanes).  H is in general not a multiple of the lanes, so a
+// sample does not stay in its lane from frame to frame: every pair loads its two
+// frames whole (15 dwords per lane each, mostly L2 hits -- each sample is read
+// N/H times) and the overlap-add runs in an LDS ring of H ceil(N/H) floats per
+// walk: push frame k (fma(o * ws, g, ring) in ascending k), produce block k (ring
+// / den, IEEE division, then clear), push frame k+1, produce block k+1 -- the
 // reference's streaming-interleaved order.  o = v * (1/N) after the inverse, as
 // kissfft_adapter.cc:154 scales.
+//
+// At N = 480 the two halves of a wave walk two streams (2p, 2p+1) over the same
+// chunk, so every branch is uniform; addresses carry the half's stream offset
+// and edge frames select zero padding per sample.
 //
 // Paired regime only (like the hot walkers of pair_hot.hip): a sample outside
 // [px_lo, px_hi] (or NaN / Inf), or an output below the sanitize threshold,
@@ -19,6 +25,8 @@
 // full sanitize), so a stream's bits depend only on its own samples.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "fft_pair15.h"
@@ -29,66 +37,153 @@ namespace fk {
 
 namespace {
 
-// frame k of the walk: 15 samples per lane, x[origin + lane + 64 m]; out-of-range
-// lanes (either side, zero padding) read 0 (see load_hop0)
-__device__ __forceinline__ void load_frame15(float (&f)[15], __amdgpu_buffer_rsrc_t rx, int lane, int origin) {
-    const int v = (origin + lane) * 4;
-#pragma unroll
-    for (int m = 0; m < 15; ++m) f[m] = dev::bload1(rx, v + m * 256, 0);
+constexpr int kE = 15;  // registers per lane
+
+template <int L>
+struct P15 {
+    static constexpr int N = 15 * L;
+    using Tw = std::conditional_t<L == 64, dev::Pair15Tw, dev::Pair15hTw>;
+    static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int hl) {
+        if constexpr (L == 64)
+            dev::pair15_tw_load(tw, reinterpret_cast<const dev::pc*>(g), hl);
+        else
+            dev::pair15h_tw_load(tw, reinterpret_cast<const dev::pc*>(g), hl);
+    }
+    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* buf, const Tw& tw, int lane) {
+        if constexpr (L == 64)
+            dev::pair15_fwd(v, buf, tw, lane);
+        else
+            dev::pair15h_fwd(v, buf, tw, lane);
+    }
+    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* buf, const Tw& tw, int lane) {
+        if constexpr (L == 64)
+            dev::pair15_inv(v, buf, tw, lane);
+        else
+            dev::pair15h_inv(v, buf, tw, lane);
+    }
+};
+
+// LDS: per wave [transpose 1152 cf][ring(s) 64 / L x RL f], then the windows
+// [2][4][L][4] f shared by the workgroup.
+template <int L>
+size_t p15_lds(int h, int w) {
+    const int nb = (15 * L + h - 1) / h, rl = h * nb;
+    return size_t(w) * (sizeof(dev::pc) * dev::kPairXbuf + sizeof(float) * (64 / L) * rl) +
+           sizeof(float) * 2 * 16 * L;
 }
+
+// Launch shapes (CRLOT_P15_VARIANT overrides, A/B): 0 = 5 walks per workgroup,
+// windows in LDS, 3 waves/SIMD budget; 1 = 2 walks, windows in registers,
+// 2 waves/SIMD; 2 = 4 walks, LDS windows; 3 = 2 walks, LDS windows.
+struct P15Shape {
+    int w;
+    bool wreg;
+};
+constexpr P15Shape kP15Shapes[4] = {{5, false}, {2, true}, {4, false}, {2, false}};
+constexpr int kP15Waves = 5;  // the widest shape (support check)
 
 }  // namespace
 
-template <int W>
-__global__ __launch_bounds__(64 * W) void k_pair960_hot(const FusedArgs a) {
-    constexpr int E = 15, N = 960;
+template <int L, int W, bool WREG, int WPE>  // WREG: windows in registers (else LDS)
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_pair15_hot(const FusedArgs a) {
+    constexpr int E = kE, N = P15<L>::N, HALVES = 64 / L;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, hl = lane % L, half = lane / L;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = a.hop;
-    const int NB = (N + H - 1) / H, RL = H * (NB + 1);
+    const int NB = (N + H - 1) / H, RL = H * NB;  // a frame spans at most RL: ring of NB blocks
     dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kPairXbuf;
-    float* ring = reinterpret_cast<float*>(reinterpret_cast<dev::pc*>(smem) + W * dev::kPairXbuf) + wave * RL;
+    float* rings = reinterpret_cast<float*>(reinterpret_cast<dev::pc*>(smem) + W * dev::kPairXbuf);
+    float* wa4 = rings + W * HALVES * RL;  // tap n = hl + L m at (m / 4) 4 L + 4 hl + m % 4
+    float* ws4 = wa4 + 16 * L;
+    for (int i = threadIdx.x; i < (WREG ? 0 : 16 * L); i += 64 * W) {
+        const int l = i % L, m = i / L;
+        const int d = (m >> 2) * (4 * L) + l * 4 + (m & 3);
+        wa4[d] = m < E ? a.t.wa[i] : 0.0f;
+        ws4[d] = m < E ? a.t.ws[i] : 0.0f;
+    }
+    __syncthreads();
+    float* ring = rings + (wave * HALVES + half) * RL;
     const int gw = blockIdx.x * W + wave;
-    if (gw >= a.n_streams * a.n_chunks) return;
-    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int n_units = (a.n_streams + HALVES - 1) / HALVES;  // streams (960) or stream pairs (480)
+    if (gw >= n_units * a.n_chunks) return;
+    const int u = gw / a.n_chunks, c = gw - u * a.n_chunks;
+    const int s0 = u * HALVES;  // this wave's first stream
+    const bool pair_full = s0 + HALVES <= a.n_streams;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
     const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
-    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
-    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    // one descriptor over the wave's streams: the half's stream is an offset (a
+    // missing second stream falls outside the range: reads 0, stores dropped)
+    const uint32_t span_x = uint32_t((HALVES == 2 && pair_full ? a.ld_x + a.T : a.T) * 4);
+    const uint32_t span_y = uint32_t((HALVES == 2 && pair_full ? a.ld_y + a.out_len : a.out_len) * 4);
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s0) * a.ld_x, span_x);
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s0) * a.ld_y, span_y);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const int xo = half * int(a.ld_x), yo = half * int(a.ld_y);  // < 2^27 (host-checked)
     const float g = a.gain, inv_n = a.inv_n;
     const int ring_blocks = a.ring_blocks;  // ring_len / H (the den table's blocks)
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
-    dev::Pair15Tw tw;
-    dev::pair15_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
-    float wa[E], ws[E];
+    typename P15<L>::Tw tw;
+    P15<L>::tw_load(tw, a.t.ptw, hl);
+    float war[WREG ? E : 1], wsr[WREG ? E : 1];
+    if constexpr (WREG) {
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        wa[m] = a.t.wa[lane + 64 * m];
-        ws[m] = a.t.ws[lane + 64 * m];
+        for (int m = 0; m < E; ++m) {
+            war[m] = a.t.wa[hl + L * m];
+            wsr[m] = a.t.ws[hl + L * m];
+        }
     }
-    for (int i = lane; i < RL; i += 64) ring[i] = 0.0f;
+    auto win4 = [&](const float* w4, const float* wr, int m4, float (&wv)[4]) {
+        if constexpr (WREG) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) wv[q] = 4 * m4 + q < E ? wr[4 * m4 + q] : 0.0f;
+        } else {
+            const float4 w = *reinterpret_cast<const float4*>(w4 + m4 * (4 * L) + hl * 4);
+            wv[0] = w.x;
+            wv[1] = w.y;
+            wv[2] = w.z;
+            wv[3] = w.w;
+        }
+    };
+    for (int i = hl; i < RL; i += L) ring[i] = 0.0f;
+    dev::wave_lds_fence();
 
+    // frame k: 15 samples per lane, x[origin + hl + L m] of the half's stream;
+    // samples outside [0, T) read 0 (zero padding)
+    auto load_frame = [&](float (&f)[E], int origin) {
+        if (HALVES == 1 || (origin >= 0 && origin + N <= a.T)) {  // uniform: both halves share k and T
+            const int v = (xo + origin + hl) * 4;  // at N = 960 the range check does the padding
+#pragma unroll
+            for (int m = 0; m < E; ++m) f[m] = dev::bload1(rx, v + m * (4 * L), 0);
+        } else {
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const int t = origin + hl + L * m;
+                const int v = (t >= 0 && t < a.T) ? (xo + t) * 4 : 0x7ffffff0;
+                f[m] = dev::bload1(rx, v, 0);
+            }
+        }
+    };
     bool bad = false;
     auto check = [&](const float (&f)[E]) {
         uint32_t mx = 0u, mn = ~0u;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const uint32_t u = __builtin_bit_cast(uint32_t, f[m]) & 0x7fffffffu;
-            mx = max(mx, u);
-            mn = min(mn, u - 1u);
+            const uint32_t w = __builtin_bit_cast(uint32_t, f[m]) & 0x7fffffffu;
+            mx = max(mx, w);
+            mn = min(mn, w - 1u);
         }
         bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
     };
     // push one frame's window-weighted output into the ring at block k's position
     auto push = [&](const float (&p)[E], int k) {
-        int base = (k % (NB + 1)) * H;  // k H mod RL
+        const int base = (k % NB) * H;  // k H mod RL
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            int pos = base + lane + 64 * m;
+            int pos = base + hl + L * m;
             pos = pos >= RL ? pos - RL : pos;
             ring[pos] = __builtin_fmaf(p[m], g, ring[pos]);
         }
@@ -96,36 +191,44 @@ __global__ __launch_bounds__(64 * W) void k_pair960_hot(const FusedArgs a) {
     };
     // produce(H) of block k: ring / den (IEEE), clear; stored when k >= f0
     auto produce = [&](int k) {
-        const int base = (k % (NB + 1)) * H;
+        const int base = (k % NB) * H;
         const int dbase = (k % ring_blocks) * H;
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-        for (int j = lane; j < H; j += 64) {
+        for (int j = hl; j < H; j += L) {
             int pos = base + j;
             pos = pos >= RL ? pos - RL : pos;
             const float v = ring[pos];
             ring[pos] = 0.0f;
             const float o = v / a.t.den[dbase + j];
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (k * H + j) * 4, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (yo + k * H + j) * 4, 0, 0);
         }
         dev::wave_lds_fence();
     };
 
     float fa[E], fb[E];
-    load_frame15(fa, rx, lane, fs * H - a.pad);
-    load_frame15(fb, rx, lane, (fs + 1) * H - a.pad);
+    load_frame(fa, fs * H - a.pad);
+    load_frame(fb, (fs + 1) * H - a.pad);
     for (int k = fs; k < f1; k += 2) {
         check(fa);
         check(fb);
         const bool partner = k + 1 < a.F;  // frame k+1 past the last: imaginary part 0
         dev::pc v[16];
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(fa[m] * wa[m], partner ? fb[m] * wa[m] : 0.0f);
+        for (int m4 = 0; m4 < 4; ++m4) {
+            float wv[4];
+            win4(wa4, war, m4, wv);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = 4 * m4 + q;
+                if (m < E) v[m] = dev::pc_mk(fa[m] * wv[q], partner ? fb[m] * wv[q] : 0.0f);
+            }
+        }
         v[15] = dev::pc_mk(0.0f, 0.0f);
         // the next pair's frames, in flight during this pair's transforms
-        load_frame15(fa, rx, lane, (k + 2) * H - a.pad);
-        load_frame15(fb, rx, lane, (k + 3) * H - a.pad);
-        dev::pair15_fwd(v, buf, tw, lane);
-        dev::pair15_inv(v, buf, tw, lane);
+        load_frame(fa, (k + 2) * H - a.pad);
+        load_frame(fb, (k + 3) * H - a.pad);
+        P15<L>::fwd(v, buf, tw, lane);
+        P15<L>::inv(v, buf, tw, lane);
         // o = v / N; its sanitize threshold 1e-30 = 2^-99.66: frexp exponents <= -99 flag the walk
         {
             int e[4] = {0, 0, 0, 0};
@@ -138,9 +241,17 @@ __global__ __launch_bounds__(64 * W) void k_pair960_hot(const FusedArgs a) {
         }
         float p[E];
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            v[m] = v[m] * dev::pc{ws[m], ws[m]};
-            p[m] = v[m].x;
+        for (int m4 = 0; m4 < 4; ++m4) {
+            float wv[4];
+            win4(ws4, wsr, m4, wv);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int m = 4 * m4 + q;
+                if (m < E) {
+                    v[m] = v[m] * dev::pc{wv[q], wv[q]};
+                    p[m] = v[m].x;
+                }
+            }
         }
         push(p, k);
         produce(k);
@@ -149,30 +260,39 @@ __global__ __launch_bounds__(64 * W) void k_pair960_hot(const FusedArgs a) {
         push(p, k + 1);
         if (k + 1 < f1) produce(k + 1);
     }
-    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-    if (lane == 0) a.t.pflags[gw] = any_bad ? 1u : 0u;
-}
-
-constexpr int kP960Waves = 2;  // per workgroup; LDS (transpose + ring per wave) sets the CU's share
-
-size_t pair960_lds(int h) {
-    const int nb = (960 + h - 1) / h, rl = h * (nb + 1);
-    return size_t(kP960Waves) * (sizeof(dev::pc) * dev::kPairXbuf + sizeof(float) * rl);
+    // flag bit h: the stream of half h redoes (a stream's bits depend on its samples only)
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(bad);
+    const uint32_t fl = HALVES == 1 ? (bal != 0 ? 1u : 0u)
+                                    : ((bal & 0xffffffffull) != 0 ? 1u : 0u) | ((bal >> 32) != 0 ? 2u : 0u);
+    if (lane == 0) a.t.pflags[gw] = fl;
 }
 
 }  // namespace fk
 
-bool pair960_supported(int n, int h, int ring_len) {
-    return n == 960 && h >= 64 && h <= 960 && ring_len % h == 0 && fk::pair960_lds(h) <= 64 * 1024;
+bool pair15_supported(int n, int h, int ring_len) {
+    if (n != 960 && n != 480) return false;
+    if (h < 32 || h > n || ring_len % h != 0) return false;
+    const size_t lds = n == 960 ? fk::p15_lds<64>(h, fk::kP15Waves) : fk::p15_lds<32>(h, fk::kP15Waves);
+    return lds <= 80 * 1024;
 }
 
-hipError_t launch_pair960(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams,
-                          int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks,
-                          hipStream_t stream) {
+hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams,
+                         int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks,
+                         int* streams_per_walk, hipStream_t stream) {
     using namespace fk;
-    if (!pair960_supported(g.n, g.h, g.ring_len) || !t.ptw || !t.pflags || F <= 0 || n_streams <= 0 ||
-        T >= (int64_t(1) << 29) || out_len >= (int64_t(1) << 29))
+    static const int venv = [] {
+        const char* e = std::getenv("CRLOT_P15_VARIANT");
+        return e ? std::atoi(e) & 3 : -1;
+    }();
+    // measured (960/240, 480/120 x 1024 streams): 4 walks with LDS windows at N = 960
+    // (149.6k vs 115.5k / 122.0k / 123.2k Msamples/s), 2 at N = 480 (145.1k vs 106.1k / 140.5k / 140.6k)
+    const int v = venv >= 0 ? venv : (g.n == 960 ? 2 : 3);
+    const int W = kP15Shapes[v].w;
+    if (!pair15_supported(g.n, g.h, g.ring_len) || !t.ptw || !t.pflags || F <= 0 || n_streams <= 0 ||
+        T >= (int64_t(1) << 27) || out_len >= (int64_t(1) << 27) || ld_x >= (int64_t(1) << 27) ||
+        ld_y >= (int64_t(1) << 27))
         return hipErrorInvalidValue;
+    const int halves = g.n == 480 ? 2 : 1;
     FusedArgs a;
     a.t = t;
     a.x = x;
@@ -191,38 +311,53 @@ hipError_t launch_pair960(const Geometry& g, const DevTables& t, const float* x,
     a.gain = g.gain;
     // chunks: about two resident rounds of walkers, each >= 48 frames
     int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const size_t lds = pair960_lds(g.h);
-    const int64_t resident = int64_t(cus) * kP960Waves * int64_t(std::max<size_t>(1, 160 * 1024 / lds));
-    int64_t n = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + n_streams - 1) / n_streams));
+    const size_t lds = g.n == 960 ? p15_lds<64>(g.h, W) : p15_lds<32>(g.h, W);
+    const int64_t wpc = std::min<int64_t>(W * int64_t(160 * 1024 / lds), kP15Shapes[v].wreg ? 8 : 12);  // waves per CU
+    const int64_t resident = int64_t(cus) * std::max<int64_t>(W, wpc);
+    const int64_t units = (n_streams + halves - 1) / halves;
+    const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + units - 1) / units));
     a.M = int((F + n - 1) / n);
     a.n_chunks = int((F + a.M - 1) / a.M);
-    const int64_t waves = int64_t(n_streams) * a.n_chunks;
+    const int64_t waves = units * a.n_chunks;
     if (t.pflags_len < waves) return hipErrorInvalidValue;
     *n_chunks = a.n_chunks;
-    auto k = k_pair960_hot<kP960Waves>;
-    hipError_t e = set_lds(k, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k, dim3(unsigned((waves + kP960Waves - 1) / kP960Waves)), dim3(64 * kP960Waves), lds,
-                       stream, a);
+    *streams_per_walk = halves;
+    hipError_t e = hipSuccess;
+    auto go = [&](auto k, int w) {
+        if ((e = set_lds(k, lds)) != hipSuccess) return;
+        hipLaunchKernelGGL(k, dim3(unsigned((waves + w - 1) / w)), dim3(64 * w), lds, stream, a);
+        e = hipGetLastError();
+    };
+    switch (v) {
+        case 1: g.n == 960 ? go(k_pair15_hot<64, 2, true, 2>, 2) : go(k_pair15_hot<32, 2, true, 2>, 2); break;
+        case 2: g.n == 960 ? go(k_pair15_hot<64, 4, false, 3>, 4) : go(k_pair15_hot<32, 4, false, 3>, 4); break;
+        case 3: g.n == 960 ? go(k_pair15_hot<64, 2, false, 3>, 2) : go(k_pair15_hot<32, 2, false, 3>, 2); break;
+        default: g.n == 960 ? go(k_pair15_hot<64, 5, false, 3>, 5) : go(k_pair15_hot<32, 5, false, 3>, 5); break;
+    }
+    return e;
     return hipGetLastError();
 }
 
-std::vector<float> build_pair15_twiddles() {
+// [14][L] of W_N^{l k1} (N = 15 L), then at L = 64 [3][16] of W64^{b c}, at
+// L = 32 [16] of W32^{b}
+std::vector<float> build_pair15_twiddles(int n) {
+    const int L = n / 15;
     std::vector<float> t;
+    auto put = [&](double ph) {
+        t.push_back(float(std::cos(ph)));
+        t.push_back(float(std::sin(ph)));
+    };
     for (int k1 = 1; k1 < 15; ++k1)
-        for (int l = 0; l < 64; ++l) {
-            const double ph = -2.0 * M_PI * double(l * k1) / 960.0;
-            t.push_back(float(std::cos(ph)));
-            t.push_back(float(std::sin(ph)));
-        }
-    for (int c = 1; c < 4; ++c)
-        for (int b = 0; b < 16; ++b) {
-            const double ph = -2.0 * M_PI * double(b * c) / 64.0;
-            t.push_back(float(std::cos(ph)));
-            t.push_back(float(std::sin(ph)));
-        }
+        for (int l = 0; l < L; ++l) put(-2.0 * M_PI * double(l * k1) / double(n));
+    if (L == 64) {
+        for (int c = 1; c < 4; ++c)
+            for (int b = 0; b < 16; ++b) put(-2.0 * M_PI * double(b * c) / 64.0);
+    } else {
+        for (int b = 0; b < 16; ++b) put(-2.0 * M_PI * double(b) / 32.0);
+    }
     return t;
 }
 

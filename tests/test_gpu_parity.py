@@ -924,14 +924,17 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
 
 
 # ------------------------------------------------------------------ K_pair960 (N = 960 frame pairs)
-@pytest.mark.parametrize("h,mode,T", [(240, 0, 48_000), (240, 1, 48_001), (480, 0, 30_011), (320, 1, 25_000),
-                                      (256, 0, 40_123), (100, 0, 9_999), (960, 0, 20_000), (240, 0, 700)])
-def test_pair960_vs_oracle_and_chunking(pkg, oracle, torch_cuda, h, mode, T):
-    """N = 960 frames in pairs through one 960-point complex transform (Good-Thomas
-    15 x the 64-lane stage): the oracle within the float32 tolerance, frame
-    counts as the Framer's, and bits independent of the batch (so of the chunking)."""
+@pytest.mark.parametrize("n,h,mode,T", [(960, 240, 0, 48_000), (960, 240, 1, 48_001), (960, 480, 0, 30_011),
+                                        (960, 320, 1, 25_000), (960, 256, 0, 40_123), (960, 100, 0, 9_999),
+                                        (960, 960, 0, 20_000), (960, 240, 0, 700), (480, 120, 0, 48_000),
+                                        (480, 120, 1, 24_001), (480, 160, 0, 20_011), (480, 96, 0, 9_999),
+                                        (480, 480, 0, 5_000), (480, 120, 0, 400)])
+def test_pair15_vs_oracle_and_chunking(pkg, oracle, torch_cuda, n, h, mode, T):
+    """N = 960 (480) frames in pairs through one 960-point complex transform per
+    wave (480-point per 32-lane half; Good-Thomas 15 x the lane stage): the oracle
+    within the float32 tolerance, frame counts as the Framer's, and bits
+    independent of the batch (so of the chunking, and of the half a stream walks in)."""
     torch = torch_cuda
-    n = 960
     x = oracle.synth_streams(5, T, config_id=97 + h)
     plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode)
     xd = dev(torch, x)
@@ -944,12 +947,14 @@ def test_pair960_vs_oracle_and_chunking(pkg, oracle, torch_cuda, h, mode, T):
     assert np.array_equal(bits(y1[0]), bits(y[3]))
 
 
-def test_pair960_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda):
+@pytest.mark.parametrize("n,h", [(960, 240), (480, 120)])
+def test_pair15_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda, n, h):
     """A stream with a sample outside the paired range (NaN, 1e30, 1e-35) is
     recomputed whole by the per-frame walker -- equal bit for bit to the plan with
-    pairing off -- while its neighbours keep the paired bits."""
+    pairing off -- while its neighbours (at N = 480 also the stream sharing its
+    wave) keep the paired bits."""
     torch = torch_cuda
-    n, h, T = 960, 240, 60_000
+    T = 60_000
     x = oracle.synth_streams(4, T, config_id=131)
     x[1, 31_000] = np.nan
     x[2, 5_000] = 1e30
