@@ -402,7 +402,8 @@ def suite_multichannel(pkg, torch, dev):
     res["runs"].append({"layout": "mono rows", "channels": 1, "ms": round(ms, 4),
                         "msamples_s": round(STREAMS * T_LEN / ms / 1e3, 1)})
     del x, y
-    for c in (2, 8):
+    chans = [int(v) for v in os.environ.get("CRLOT_MC_CHANNELS", "2,4,5,8,16").split(",")]
+    for c in chans:
         G = STREAMS // c
         xi = torch.rand((G, T_LEN, c), generator=g, device=dev) - 0.5
         yi = torch.empty((G, plan.output_length(T_LEN), c), device=dev)

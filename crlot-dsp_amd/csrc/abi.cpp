@@ -291,6 +291,7 @@ int64_t frames_for(const crlot_plan* p, int64_t T) {
 }
 
 bool aligned8(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 7u) == 0; }
+bool aligned4(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 3u) == 0; }
 
 }  // namespace
 
@@ -514,10 +515,16 @@ int64_t crlot_output_length(const crlot_plan* p, int64_t T) {
 static bool use_fused(const crlot_plan* p, const float* x, const float* y, int64_t ld_x,
                       int64_t ld_y, int32_t n_streams, int64_t T, int64_t out_len) {
     const int64_t lim = int64_t(1) << 29;
+    // K_pair (N = 1024 frame pairs) moves single floats: any 4-byte-aligned rows
+    // take it, so a stream's bits do not depend on the parity of its row stride;
+    // the other fused walkers move float2
+    const crlot::DevTables t = tables(p);
+    const bool pair1k = p->geo.n == 1024 && t.ptw && t.pden && t.wsn && t.rden;
+    const bool layout_ok = pair1k ? aligned4(x) && aligned4(y)
+                                  : aligned8(x) && aligned8(y) && ld_x % 2 == 0 && ld_y % 2 == 0;
     return (crlot::fused_supported(p->geo.n, p->geo.h) ||
             crlot::fused_wg_supported(p->geo.n, p->geo.h)) &&
-           p->geo.ring_len % p->geo.h == 0 &&
-           aligned8(x) && aligned8(y) && ld_x % 2 == 0 && ld_y % 2 == 0 && T < lim &&
+           p->geo.ring_len % p->geo.h == 0 && layout_ok && T < lim &&
            out_len + 2 * p->geo.n < lim && int64_t(n_streams) * (T / p->geo.h + 1) < lim;
 }
 
@@ -603,6 +610,27 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
     if (ld_x < T * C || ld_y < L * C) return fail(CRLOT_EINVAL, "leading dimension too small");
     if (int64_t(n_groups) * C > INT32_MAX) return fail(CRLOT_EINVAL, "too many streams");
     DeviceGuard g(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipError_t e;
+    // K_pair plans (N = 1024, zero padding) walk the interleaved rows of up to 5
+    // channels directly: one pass over HBM, bit-identical to the per-channel
+    // planes.  Wider rows spread a wave's hop over 2C cache lines per load and
+    // partial lines per store; there the LDS-tiled transposes around the mono
+    // walk win (1024 streams x 480 000, 1024/256: direct 258k / 248k / 168k / 142k
+    // / 113k Msamples/s at C = 2 / 4 / 5 / 6 / 8, three passes 153k / 157k / 153k /
+    // 150k / 144k)
+    static const bool three_pass = [] {
+        const char* v = std::getenv("CRLOT_ILV_3PASS");  // A/B: always deinterleave -> planes -> interleave
+        return v && v[0] == '1';
+    }();
+    if (!three_pass && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0 && aligned4(d_x) &&
+        aligned4(d_y)) {
+        const int rcf = ensure_pair_flags(p, int32_t(n_groups * C), F);
+        if (rcf != CRLOT_OK) return rcf;
+        e = crlot::launch_pair_interleaved(p->geo, tables(p), d_x, d_y, n_groups, channels, T, ld_x, ld_y, F, L, s);
+        if (e == hipSuccess) return CRLOT_OK;
+        if (e != hipErrorNotSupported && e != hipErrorInvalidValue) return hip_fail(e, "interleaved pair kernel launch");
+    }
     const int64_t need = int64_t(n_groups) * C * (T + L) * int64_t(sizeof(float));
     if (need > p->planes_bytes) {
         if (p->d_planes) (void)hipFree(p->d_planes);
@@ -614,8 +642,7 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
     }
     float* xin = p->d_planes;
     float* yout = p->d_planes + int64_t(n_groups) * C * T;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    hipError_t e = crlot::launch_deinterleave(d_x, ld_x, xin, n_groups, T, channels, s);
+    e = crlot::launch_deinterleave(d_x, ld_x, xin, n_groups, T, channels, s);
     if (e != hipSuccess) return hip_fail(e, "deinterleave kernel launch");
     const int rc = crlot_roundtrip(p, xin, yout, int32_t(n_groups * C), T, T, L, stream);
     if (rc != CRLOT_OK) return rc;

@@ -21,7 +21,37 @@ struct FusedArgs {
     float inv_n, gain;
     int fix_all = 0;  // K_pair: the fix-up walker redoes every chunk (padding rules it alone handles)
     int hop = 0;      // K_pair960 (runtime hop; the power-of-two walkers take it as a template constant)
+    int cs = 1;       // K_pair interleaved groups: channels per group (stream g*cs + c is sample i at
+                      // x[g*ld_x + i*cs + c]); 1 = planar rows
 };
+
+// Wave gw of a chunked walk -> stream s, chunk c and the element offsets of the
+// stream's first input / output sample.  Planar rows: stream-major.  Interleaved
+// groups (ILV, a.cs channels): the channels of one group and chunk on
+// consecutive waves, so the waves of a workgroup read and write whole sample
+// rows together (lines shared in their XCD's L2 instead of refetched).
+struct WalkId {
+    int s, c;
+    int64_t xo, yo;
+};
+template <bool ILV>
+__device__ __forceinline__ WalkId walk_id(const FusedArgs& a, int gw) {
+    WalkId w;
+    if constexpr (!ILV) {
+        w.s = gw / a.n_chunks;
+        w.c = gw - w.s * a.n_chunks;
+        w.xo = int64_t(w.s) * a.ld_x;
+        w.yo = int64_t(w.s) * a.ld_y;
+    } else {
+        const int r = gw / a.cs, ch = gw - r * a.cs;
+        const int g = r / a.n_chunks;
+        w.c = r - g * a.n_chunks;
+        w.s = g * a.cs + ch;
+        w.xo = int64_t(g) * a.ld_x + ch;
+        w.yo = int64_t(g) * a.ld_y + ch;
+    }
+    return w;
+}
 
 // FrameQueue padding (Indexing.h:18-37): left side i -> -i-1, right side
 // i -> 2n-2-i, repeated until inside.
@@ -88,6 +118,31 @@ __device__ __forceinline__ void load_hop0(float* dst, __amdgpu_buffer_rsrc_t rx,
     const int v = (origin + lane) * 4;
 #pragma unroll
     for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, v + q * 256, 0);
+}
+// bytes a stream's descriptor spans: n samples cs floats apart
+__device__ __forceinline__ uint32_t span_bytes(int n, int cs) {
+    return n > 0 ? uint32_t((n - 1) * cs + 1) * 4u : 0u;
+}
+// Hop loads with samples cs floats apart (interleaved channels; (T + 2N) * cs
+// * 4 < 2^31, host-checked): one descriptor per q starting at sample 64 q and
+// ending after sample T-1, so the one per-lane offset (origin + lane) * 4 cs
+// is range-checked for every q (zeros outside [0, T)) without a VGPR per q.
+template <int SH>
+struct HopRsrc {
+    __amdgpu_buffer_rsrc_t r[SH];
+};
+template <int SH>
+__device__ __forceinline__ HopRsrc<SH> hop_rsrc(const float* base, int T, int cs) {
+    HopRsrc<SH> h;
+#pragma unroll
+    for (int q = 0; q < SH; ++q) h.r[q] = dev::make_rsrc(base + int64_t(64 * q) * cs, span_bytes(T - 64 * q, cs));
+    return h;
+}
+template <int SH>
+__device__ __forceinline__ void load_hop0s(float* dst, const HopRsrc<SH>& rx, int lane, int origin, int cs) {
+    const int v = (origin + lane) * (4 * cs);
+#pragma unroll
+    for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx.r[q], v, 0);
 }
 
 // 1 when every sample of the hop (SH per lane, whole wave) keeps the paired regime.

@@ -72,6 +72,11 @@ bool fused_supported(int n, int h);
 hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, float* y,
                         int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
                         int64_t out_len, hipStream_t stream);
+// K_pair on interleaved groups (crlot_roundtrip_interleaved's direct path);
+// hipErrorNotSupported when the plan's kernel is not K_pair (N = 1024, zero padding)
+hipError_t launch_pair_interleaved(const Geometry& g, const DevTables& t, const float* x, float* y, int n_groups,
+                                   int channels, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                                   int64_t out_len, hipStream_t stream);
 
 // Fused workgroup-walker path for frames too large for one wave: N = 4096
 // (256 lanes per frame), H % 512 == 0, N % H == 0; same preconditions otherwise.

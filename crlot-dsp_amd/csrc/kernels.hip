@@ -2119,6 +2119,43 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
     }
 }
 
+// K_pair straight on interleaved groups (N = 1024, zero padding): n_groups x
+// channels streams, sample i of channel c of group g at x[g*ld_x + i*channels + c]
+// (outputs likewise), chunked exactly as launch_fused chunks the same number of
+// planar streams.  hipErrorNotSupported when the plan is not on K_pair.
+hipError_t launch_pair_interleaved(const Geometry& g, const DevTables& t, const float* x, float* y, int n_groups,
+                                   int channels, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                                   int64_t out_len, hipStream_t stream) {
+    const bool fast = t.wsn && t.rden;
+    if (!(g.n == 1024 && t.ptw && t.pden && t.pflags && fast && g.pad_mode == 0 && fused_supported(g.n, g.h) &&
+          g.h <= 512))
+        return hipErrorNotSupported;
+    const int64_t S = int64_t(n_groups) * channels;
+    if (F <= 0 || n_groups <= 0 || channels < 1 || S > INT32_MAX || (T + 2 * g.n) * channels >= (int64_t(1) << 29) ||
+        (out_len + 2 * g.n) * channels >= (int64_t(1) << 29))
+        return hipErrorInvalidValue;
+    FusedArgs a;
+    a.t = t;
+    a.x = x;
+    a.y = y;
+    a.ld_x = ld_x;
+    a.ld_y = ld_y;
+    a.T = int(T);
+    a.out_len = int(out_len);
+    a.n_streams = int(S);
+    a.F = int(F);
+    a.cs = channels;
+    choose_chunks_rounds(F, a.n_streams, g.n / g.h + 1, fused_resident_waves() * pair_waves_per_cu() / 16,
+                         a.n_chunks, a.M);
+    chunk_override(F, a);
+    a.ring_blocks = g.ring_len / g.h;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
+    a.inv_n = g.inv_n;
+    a.gain = g.gain;
+    return launch_pair(g.h / 64, a, S * a.n_chunks, stream);
+}
+
 // K_pair4k: N = 4096, H = 256 SH, one 256-lane workgroup per chunk, two per CU.
 template <int SH>
 static hipError_t pair4k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {

@@ -81,29 +81,49 @@ __global__ void __launch_bounds__(256) k_ola_produce(float* __restrict__ ring, i
     if ((threadIdx.x & 63) == 0 && a > 0.0f) atomicMax(peak, __float_as_uint(a));
 }
 
-// PCM layout for the batched multi-channel round trip (crlot_roundtrip_interleaved):
-// group g holds T rows of C interleaved samples (the reference's PCM,
-// framer.cc:15-35).  k_deinterleave writes channel planes [g][c][t]; one thread
-// per row reads its C contiguous floats and writes C coalesced planes, so both
-// sides stream at HBM rate with no LDS.  k_interleave is the inverse.
+// Interleaved PCM <-> channel planes (crlot_roundtrip_interleaved for plans
+// off the direct K_pair path; Framer(N, H, C) frames N*C interleaved samples,
+// framer.cc:15-35).  A workgroup moves a tile of TR rows x C channels: the
+// tile's TR*C interleaved floats are one contiguous run (coalesced loads or
+// stores), each plane's TR floats another; the transpose runs through LDS with
+// rows padded to C+1 words, so the column walks are bank-conflict-free.
+constexpr int kIlvTileFloats = 8192;  // 32 KB of LDS (+ padding) per workgroup
+__host__ __device__ constexpr int ilv_rows(int C) {
+    const int r = kIlvTileFloats / C;
+    return r >= 1024 ? 1024 : r < 64 ? 64 : r & ~63;
+}
 __global__ void __launch_bounds__(256) k_deinterleave(const float* __restrict__ x, int64_t ld_x,
                                                       float* __restrict__ planes, int64_t T, int C) {
-    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int64_t g = blockIdx.y;
-    if (t >= T) return;
-    const float* row = x + g * ld_x + t * C;
-    float* o = planes + g * C * T + t;
-    for (int c = 0; c < C; ++c) o[int64_t(c) * T] = row[c];
+    extern __shared__ float tile[];
+    const int TR = ilv_rows(C);
+    const int64_t g = blockIdx.y, r0 = int64_t(blockIdx.x) * TR;
+    const int rows = int(T - r0 < TR ? T - r0 : TR);
+    const float* src = x + g * ld_x + r0 * C;
+    for (int e = threadIdx.x; e < rows * C; e += 256) {
+        const int r = e / C;
+        tile[e + r] = src[e];  // [r][c] at r * (C + 1) + c
+    }
+    __syncthreads();
+    float* dst = planes + g * C * T + r0;
+    for (int c = 0; c < C; ++c)
+        for (int r = threadIdx.x; r < rows; r += 256) dst[int64_t(c) * T + r] = tile[r * (C + 1) + c];
 }
 
 __global__ void __launch_bounds__(256) k_interleave(const float* __restrict__ planes, int64_t L,
                                                     float* __restrict__ y, int64_t ld_y, int C) {
-    const int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int64_t g = blockIdx.y;
-    if (t >= L) return;
-    const float* in = planes + g * C * L + t;
-    float* row = y + g * ld_y + t * C;
-    for (int c = 0; c < C; ++c) row[c] = in[int64_t(c) * L];
+    extern __shared__ float tile[];
+    const int TR = ilv_rows(C);
+    const int64_t g = blockIdx.y, r0 = int64_t(blockIdx.x) * TR;
+    const int rows = int(L - r0 < TR ? L - r0 : TR);
+    const float* src = planes + g * C * L + r0;
+    for (int c = 0; c < C; ++c)
+        for (int r = threadIdx.x; r < rows; r += 256) tile[r * (C + 1) + c] = src[int64_t(c) * L + r];
+    __syncthreads();
+    float* dst = y + g * ld_y + r0 * C;
+    for (int e = threadIdx.x; e < rows * C; e += 256) {
+        const int r = e / C;
+        dst[e] = tile[e + r];
+    }
 }
 
 }  // namespace
@@ -111,7 +131,9 @@ __global__ void __launch_bounds__(256) k_interleave(const float* __restrict__ pl
 hipError_t launch_deinterleave(const float* x, int64_t ld_x, float* planes, int groups, int64_t T, int C,
                                hipStream_t s) {
     if (groups <= 0 || T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_deinterleave, dim3(unsigned((T + 255) / 256), unsigned(groups)), dim3(256), 0, s,
+    const int tr = ilv_rows(C);
+    const size_t lds = sizeof(float) * size_t(tr) * (C + 1);
+    hipLaunchKernelGGL(k_deinterleave, dim3(unsigned((T + tr - 1) / tr), unsigned(groups)), dim3(256), lds, s,
                        x, ld_x, planes, T, C);
     return hipGetLastError();
 }
@@ -119,7 +141,9 @@ hipError_t launch_deinterleave(const float* x, int64_t ld_x, float* planes, int 
 hipError_t launch_interleave(const float* planes, int64_t L, float* y, int64_t ld_y, int groups, int C,
                              hipStream_t s) {
     if (groups <= 0 || L <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_interleave, dim3(unsigned((L + 255) / 256), unsigned(groups)), dim3(256), 0, s,
+    const int tr = ilv_rows(C);
+    const size_t lds = sizeof(float) * size_t(tr) * (C + 1);
+    hipLaunchKernelGGL(k_interleave, dim3(unsigned((L + tr - 1) / tr), unsigned(groups)), dim3(256), lds, s,
                        planes, L, y, ld_y, C);
     return hipGetLastError();
 }

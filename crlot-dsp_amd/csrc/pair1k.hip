@@ -72,7 +72,7 @@ struct PairRot {
     static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
 };
 
-template <int SH, int NB, int W>
+template <int SH, int NB, int W, bool ILV>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
     constexpr int E = 16, N = 1024, H = 64 * SH;
     constexpr int R = PairRot<NB>::R, U = PairRot<NB>::U;
@@ -100,13 +100,21 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
     const int gw = blockIdx.x * W + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
-    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const WalkId wid = walk_id<ILV>(a, gw);
+    const int c = wid.c;
+    const int cs = ILV ? a.cs : 1;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
     const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
-    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
-    const __amdgpu_buffer_rsrc_t ry =
-        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + wid.xo, span_bytes(a.T, cs));
+    const HopRsrc<ILV ? SH : 1> rxq = hop_rsrc<ILV ? SH : 1>(a.x + wid.xo, ILV ? a.T : 0, cs);
+    auto load_hop = [&](float* dst, int origin) {
+        if constexpr (ILV)
+            load_hop0s<SH>(dst, rxq, lane, origin, cs);
+        else
+            load_hop0<SH>(dst, rx, lane, origin);
+    };
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + wid.yo, span_bytes(a.out_len, cs));
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const float g = a.gain;
@@ -118,7 +126,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     uint32_t hopok = 0;
 #pragma unroll
     for (int h = 0; h <= NB; ++h) {
-        load_hop0<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
+        load_hop(xr[h], (fs + h) * H - a.pad);
         hopok |= hop_ok_bits<SH>(xr[h], xlo_b, xhi_b) << h;
     }
     float acc[NB][SH];
@@ -153,8 +161,8 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
 #pragma unroll
         for (int q = 0; q < SH; ++q)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
-                                                  k * (4 * H) + q * 256, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * (4 * cs),
+                                                  (k * (4 * H) + q * 256) * cs, 0);
     };
 
 #if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
@@ -174,8 +182,8 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         constexpr int PH = decltype(phc)::value;
         constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
         // prefetch hops k+NB+1, k+NB+2 for the next pairs (their slots are free)
-        load_hop0<SH>(xr[(S0 + NB + 1) % R], rx, lane, (k + NB + 1) * H - a.pad);
-        load_hop0<SH>(xr[(S0 + NB + 2) % R], rx, lane, (k + NB + 2) * H - a.pad);
+        load_hop(xr[(S0 + NB + 1) % R], (k + NB + 1) * H - a.pad);
+        load_hop(xr[(S0 + NB + 2) % R], (k + NB + 2) * H - a.pad);
         const bool paired = (hopok & kPairHops) == kPairHops;
         bad |= !paired;
         {
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 //    its own (imaginary part zero) with the full sanitize on both sides, so a
 //    frame whose spectrum overflows cannot leak into its neighbour -- the
 //    reference transforms every frame alone (kissfft_adapter.cc:83-168).
-template <int SH, int NB, int W, bool HAS_GAIN>
+template <int SH, int NB, int W, bool HAS_GAIN, bool ILV>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_fix(const FusedArgs a) {
     constexpr int E = 16, N = 1024, H = 64 * SH;
     static_assert(NB * SH == E, "N = NB * H");
@@ -327,13 +335,21 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
     const int gw = blockIdx.x * W + wave;
     if (gw >= a.n_streams * a.n_chunks || (!a.fix_all && a.t.pflags[gw] == 0u)) return;
-    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const WalkId wid = walk_id<ILV>(a, gw);
+    const int c = wid.c;
+    const int cs = ILV ? a.cs : 1;  // interleaved groups: zero padding only (host-checked)
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
     const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
-    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
-    const __amdgpu_buffer_rsrc_t ry =
-        dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + wid.xo, span_bytes(a.T, cs));
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + wid.yo, span_bytes(a.out_len, cs));
+    const HopRsrc<ILV ? SH : 1> rxq = hop_rsrc<ILV ? SH : 1>(a.x + wid.xo, ILV ? a.T : 0, cs);
+    auto load_hop = [&](float* dst, int origin) {
+        if constexpr (ILV)
+            load_hop0s<SH>(dst, rxq, lane, origin, cs);
+        else
+            load_hop1<SH>(dst, rx, lane, origin, a.T, a.pad_mode);
+    };
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const float g = a.gain;
@@ -345,7 +361,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     uint32_t hopok = 0;
 #pragma unroll
     for (int h = 0; h <= NB; ++h) {
-        load_hop1<SH>(xin + h * SH, rx, lane, (fs + h) * H - a.pad, a.T, a.pad_mode);
+        load_hop(xin + h * SH, (fs + h) * H - a.pad);
         hopok |= hop_ok<SH>(xin + h * SH, xlo, xhi) << h;
     }
     float acc[NB][SH];
@@ -395,8 +411,8 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
 #pragma unroll
         for (int q = 0; q < SH; ++q)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
-                                                  k * (4 * H) + q * 256, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * (4 * cs),
+                                                  (k * (4 * H) + q * 256) * cs, 0);
 #pragma unroll
         for (int j = 0; j < NB - 1; ++j)
 #pragma unroll
@@ -431,8 +447,8 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     for (int k = fs; k < f1; k += 2) {
         // prefetch hops k+NB+1, k+NB+2 for the next pair
         float nxt[2 * SH];
-        load_hop1<SH>(nxt, rx, lane, (k + NB + 1) * H - a.pad, a.T, a.pad_mode);
-        load_hop1<SH>(nxt + SH, rx, lane, (k + NB + 2) * H - a.pad, a.T, a.pad_mode);
+        load_hop(nxt, (k + NB + 1) * H - a.pad);
+        load_hop(nxt + SH, (k + NB + 2) * H - a.pad);
         const bool paired = (hopok & kPairHops) == kPairHops;
         if (paired) {
             dev::pc v[E];
@@ -519,18 +535,19 @@ constexpr bool pair_hot(bool gain) {
     return SH == 4 && !gain;
 }
 
-template <int SH>
+template <int SH, bool ILV>
 hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     constexpr int NB = 16 / SH, W = kPairWaves;
     const size_t lds = PairLds<W>::bytes;
     const int64_t grid = (waves + W - 1) / W;
     hipError_t e;
-    auto kf = a.t.gain ? k_stft_ola_pair_fix<SH, NB, W, true> : k_stft_ola_pair_fix<SH, NB, W, false>;
+    if (ILV && (a.cs < 1 || a.pad_mode != 0)) return hipErrorInvalidValue;
+    auto kf = a.t.gain ? k_stft_ola_pair_fix<SH, NB, W, true, ILV> : k_stft_ola_pair_fix<SH, NB, W, false, ILV>;
     if ((e = set_lds(kf, lds)) != hipSuccess) return e;
     if (!a.t.pflags || a.t.pflags_len < waves) return hipErrorInvalidValue;
     if constexpr (pair_hot<SH>(false)) {
         if (a.pad_mode == 0 && !a.t.gain) {
-            auto k = k_stft_ola_pair<SH, NB, W>;
+            auto k = k_stft_ola_pair<SH, NB, W, ILV>;
             if ((e = set_lds(k, lds)) != hipSuccess) return e;
             hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -546,11 +563,19 @@ hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
 }
 
 hipError_t launch_pair(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream) {
+    if (a.cs != 1) {
+        switch (sh) {
+            case 2: return pair_sh<2, true>(a, waves, stream);
+            case 4: return pair_sh<4, true>(a, waves, stream);
+            case 8: return pair_sh<8, true>(a, waves, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (sh) {
-        case 2: return pair_sh<2>(a, waves, stream);
-        case 4: return pair_sh<4>(a, waves, stream);
-        case 8: return pair_sh<8>(a, waves, stream);
-        case 16: return pair_sh<16>(a, waves, stream);
+        case 2: return pair_sh<2, false>(a, waves, stream);
+        case 4: return pair_sh<4, false>(a, waves, stream);
+        case 8: return pair_sh<8, false>(a, waves, stream);
+        case 16: return pair_sh<16, false>(a, waves, stream);
         default: return hipErrorInvalidValue;
     }
 }

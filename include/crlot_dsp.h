@@ -150,8 +150,11 @@ int crlot_roundtrip(crlot_plan* plan, const float* d_x, float* d_y, int32_t n_st
  * aos_to_soa.cc:7-18): group g's input is T rows of C samples at d_x + g*ld_x
  * (ld_x >= T*C), its output F*H rows of C samples at d_y + g*ld_y.  Every
  * channel is an independent stream, bit-identical to crlot_roundtrip on that
- * channel's plane.  Runs deinterleave -> the mono kernels -> interleave through
- * a plan-owned workspace of n_groups*C*(T + F*H) floats (two extra HBM passes). */
+ * channel's plane.  N = 1024 plans with zero padding walk the interleaved rows
+ * of up to 5 channels directly (K_pair with strided hop loads and stores: one
+ * pass over HBM); other plans and wider rows run LDS-tiled deinterleave -> the
+ * mono kernels -> interleave through a plan-owned workspace of
+ * n_groups*C*(T + F*H) floats (two extra HBM passes). */
 int crlot_roundtrip_interleaved(crlot_plan* plan, const float* d_x, float* d_y, int32_t n_groups,
                                 int32_t channels, int64_t T, int64_t ld_x, int64_t ld_y, void* stream);
 

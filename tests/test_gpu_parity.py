@@ -902,6 +902,42 @@ def test_roundtrip_interleaved_equals_per_channel(pkg, oracle, torch_cuda, n, h,
         assert_close(y[0, :, c], ref[c], 0.5, f"group 0 ch {c}")
 
 
+@pytest.mark.parametrize("h,C_,T,mode,gain,burst", [
+    (256, 2, 50_000, "zpad", False, True), (256, 8, 20_011, "drop", False, True), (256, 3, 1_000, "zpad", False, False),
+    (256, 64, 6_000, "zpad", False, False), (128, 4, 30_001, "zpad", False, True), (256, 5, 9_000, "drop", False, True), (512, 2, 41_000, "drop", False, False),
+    (256, 2, 33_333, "zpad", True, True), (256, 1, 12_345, "zpad", False, True), (256, 5, 700, "zpad", False, False)])
+def test_roundtrip_interleaved_direct_pair_walker(pkg, oracle, torch_cuda, h, C_, T, mode, gain, burst):
+    """N = 1024 plans walk the interleaved rows directly (K_pair with strided hop
+    loads and stores, the channels of a group and chunk on neighbouring waves): bit-
+    identical to each channel's plane through crlot_roundtrip, including chunks the
+    fix-up walker redoes (a burst of huge samples, a tiny one), the two-regime walker
+    (H = 128 / 512, a spectral gain), short streams (T < N) and group rows with slack
+    (ld_x > T*C)."""
+    torch = torch_cuda
+    G = 3
+    bm = pkg.DROP if mode == "drop" else pkg.ZERO_PAD
+    x = oracle.synth_streams(G * C_, T, config_id=67).reshape(G, C_, T)
+    if burst and T > 4000:
+        x[1, C_ - 1, T // 3:T // 3 + 5] = 1e25
+        x[2, 0, T // 2] = 1e-33
+    plan = pkg.Plan(frame_size=1024, hop_size=h, boundary_mode=bm)
+    if gain:
+        g = np.linspace(0.25, 1.5, 513).astype(np.float32)
+        plan.set_spectral_gain(g)
+    slack = 37
+    xi = torch.zeros((G, T * C_ + slack), dtype=torch.float32, device="cuda")
+    xi[:, :T * C_] = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 2, 1)).reshape(G, T * C_)).cuda()
+    xv = xi[:, :T * C_].view(G, T, C_)  # (G, T, C) with row stride T*C + slack
+    y = host(plan.roundtrip_interleaved(xv))                                   # (G, L, C)
+    y_mono = host(plan.roundtrip(dev(torch, x.reshape(G * C_, T)))).reshape(G, C_, -1)
+    assert y.shape == (G, y_mono.shape[2], C_)
+    assert np.array_equal(bits(y.transpose(0, 2, 1)), bits(y_mono))
+    if not gain:
+        ref = oracle.roundtrip_batch(x[0], 1024, h, mode=oracle.DROP if mode == "drop" else oracle.ZERO_PAD)
+        for c in range(C_):
+            assert_close(y[0, :, c], ref[c], 0.5, f"group 0 ch {c}")
+
+
 @pytest.mark.parametrize("n,h,T", [(4096, 1024, 123_457), (4096, 512, 60_000), (4096, 2048, 70_001),
                                    (2048, 512, 80_003), (2048, 512, 33_000), (1024, 256, 50_000),
                                    (512, 128, 40_001), (512, 256, 25_000)])
