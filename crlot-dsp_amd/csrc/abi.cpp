@@ -40,7 +40,7 @@ struct crlot_plan {
     float* d_st = nullptr;
     float* d_gain = nullptr;
     float* d_wsn = nullptr;   // ws * (1/N)
-    float* d_rden = nullptr;  // RN(1 / den)
+    float* d_rden = nullptr;  // RN(1 / den) [ring], then {den, RN(1 / den)} pairs [ring][2]
     float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
     float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024: 64 lanes, N = 4096: 256)
     uint32_t* d_pflags = nullptr;  // K_pair per-walker regime flags (DevTables::pflags)
@@ -49,6 +49,7 @@ struct crlot_plan {
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
     bool fast_ok = false;     // both exact rewrites valid for the current tables
+    bool den_mk_ok = false;   // every den in [2^-40, 2^40]: Markstein division exact
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
     float* d_twany = nullptr; // per-pass twiddles of the mixed-radix path (aliases d_tw when generic)
     float* d_twany_own = nullptr;  // ... or its own table (power-of-two plans, any-shape streams)
@@ -109,6 +110,7 @@ crlot::DevTables tables(const crlot_plan* p) {
         t.wsn = p->d_wsn;
         t.rden = p->d_rden;
     }
+    if (p->den_mk_ok && !exact_div) t.den_rden = p->d_rden + p->geo.ring_len;
     if (p->pairing) {
         if (p->geo.n == 4096 || p->geo.n == 2048) {
             t.ptw4 = p->d_ptw;
@@ -208,8 +210,9 @@ int upload_window_tables(crlot_plan* p, hipStream_t s) {
         wsn[i] = ws[i] * p->geo.inv_n;
         if (ws[i] != 0.0f && !(std::fabs(wsn[i]) >= 0x1p-126f)) ok = false;
     }
+    bool dok = true;
     for (size_t i = 0; i < den.size(); ++i) {
-        if (!(den[i] >= 0x1p-40f && den[i] <= 0x1p40f)) ok = false;
+        if (!(den[i] >= 0x1p-40f && den[i] <= 0x1p40f)) ok = dok = false;
         rden[i] = 1.0f / den[i];
     }
     // K_pair: the paired regime needs sanitize(x * wa) == x * wa (up to the sign of
@@ -242,10 +245,17 @@ int upload_window_tables(crlot_plan* p, hipStream_t s) {
     up.add(p->d_ws, ws.data(), sizeof(float) * n);
     up.add(p->d_den, den.data(), sizeof(float) * den.size());
     up.add(p->d_wsn, wsn.data(), sizeof(float) * n);
+    std::vector<float> dr2(2 * den.size());
+    for (size_t i = 0; i < den.size(); ++i) {
+        dr2[2 * i] = den[i];
+        dr2[2 * i + 1] = rden[i];
+    }
     up.add(p->d_rden, rden.data(), sizeof(float) * den.size());
+    up.add(p->d_rden + den.size(), dr2.data(), sizeof(float) * dr2.size());
     hipError_t e = up.submit(s);
     if (e != hipSuccess) return hip_fail(e, "table upload");
     p->fast_ok = ok;
+    p->den_mk_ok = dok;
     return CRLOT_OK;
 }
 
@@ -389,7 +399,7 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         (e = hipMalloc(&p->d_st, sizeof(float) * 2 * P)) ||
         (e = hipMalloc(&p->d_gain, sizeof(float) * (P + 1))) ||
         (e = hipMalloc(&p->d_wsn, sizeof(float) * n)) ||
-        (e = hipMalloc(&p->d_rden, sizeof(float) * ring))) {
+        (e = hipMalloc(&p->d_rden, sizeof(float) * 3 * ring))) {
         free_plan(p);
         return hip_fail(e, "hipMalloc(plan tables)");
     }

@@ -20,6 +20,10 @@ struct DevTables {
     // fall outside the ranges where the rewrites are bit-identical):
     const float* wsn = nullptr;  // ws * (1/N): folds the inverse's 1/N into the window
     const float* rden = nullptr; // RN(1 / den): Markstein division
+    // {den, RN(1 / den)} pairs [ring_len] whenever every den lies in [2^-40, 2^40]
+    // (Markstein's exact range), whatever the window rewrite says (K_pair15 keeps
+    // the window and 1/N apart)
+    const float* den_rden = nullptr;
     // Frame-pair transform tables (N = 1024 plans with pairing on, else nullptr):
     // W1024^{l k1} (15 x 64, fft_pair.h pair_t1_index) then W64^{b c} [c-1][b] (3 x 16), float pairs.
     const float* ptw = nullptr;

@@ -63,12 +63,19 @@ struct P15 {
     }
 };
 
+// OLA ring of a walk: the live span is at most H ceil(N/H) floats; the ring is
+// the next power of two, so a position wraps with one AND.
+__host__ __device__ inline int p15_ring(int n, int h) {
+    const int span = h * ((n + h - 1) / h);
+    int r = 1;
+    while (r < span) r <<= 1;
+    return r;
+}
 // LDS: per wave [transpose 1152 cf][ring(s) 64 / L x RL f], then the windows
 // [2][4][L][4] f shared by the workgroup.
 template <int L>
 size_t p15_lds(int h, int w) {
-    const int nb = (15 * L + h - 1) / h, rl = h * nb;
-    return size_t(w) * (sizeof(dev::pc) * dev::kPairXbuf + sizeof(float) * (64 / L) * rl) +
+    return size_t(w) * (sizeof(dev::pc) * dev::kPairXbuf + sizeof(float) * (64 / L) * p15_ring(15 * L, h)) +
            sizeof(float) * 2 * 16 * L;
 }
 
@@ -92,7 +99,8 @@ void k_pair15_hot(const FusedArgs a) {
     const int lane = threadIdx.x & 63, hl = lane % L, half = lane / L;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int H = a.hop;
-    const int NB = (N + H - 1) / H, RL = H * NB;  // a frame spans at most RL: ring of NB blocks
+    const int RL = p15_ring(N, H), RM = RL - 1;  // ring >= H ceil(N/H): no live position aliases
+    const int NB = (N + H - 1) / H;
     dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kPairXbuf;
     float* rings = reinterpret_cast<float*>(reinterpret_cast<dev::pc*>(smem) + W * dev::kPairXbuf);
     float* wa4 = rings + W * HALVES * RL;  // tap n = hl + L m at (m / 4) 4 L + 4 hl + m % 4
@@ -180,26 +188,36 @@ void k_pair15_hot(const FusedArgs a) {
     };
     // push one frame's window-weighted output into the ring at block k's position
     auto push = [&](const float (&p)[E], int k) {
-        const int base = (k % NB) * H;  // k H mod RL
+        const int base = k * H + hl;  // k H < 2^27 (host-checked)
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            int pos = base + hl + L * m;
-            pos = pos >= RL ? pos - RL : pos;
+            const int pos = (base + L * m) & RM;
             ring[pos] = __builtin_fmaf(p[m], g, ring[pos]);
         }
         dev::wave_lds_fence();
     };
-    // produce(H) of block k: ring / den (IEEE), clear; stored when k >= f0
+    // produce(H) of block k: ring / den, clear; stored when k >= f0.  The quotient
+    // is IEEE's: Markstein's correction with RN(1/den) when the plan's divisors
+    // allow it (den in [2^-40, 2^40]) and the sums are 0 or in [2^-64, 2^64]
+    // (frexp exponents in [-63, 65]; a walk with any other sum is flagged and its
+    // stream redone by the per-frame walker), else the division itself.
+    const float2* const dr2 = reinterpret_cast<const float2*>(a.t.den_rden);
     auto produce = [&](int k) {
-        const int base = (k % NB) * H;
+        const int base = k * H;
         const int dbase = (k % ring_blocks) * H;
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
         for (int j = hl; j < H; j += L) {
-            int pos = base + j;
-            pos = pos >= RL ? pos - RL : pos;
+            const int pos = (base + j) & RM;
             const float v = ring[pos];
             ring[pos] = 0.0f;
-            const float o = v / a.t.den[dbase + j];
+            float o;
+            if (dr2) {
+                const float2 dr = dr2[dbase + j];
+                o = mk_div(v, dr.x, dr.y);
+                bad |= uint32_t(__builtin_amdgcn_frexp_expf(v) + 63) > 128u;  // exponent outside [-63, 65]
+            } else {
+                o = v / a.t.den[dbase + j];
+            }
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (yo + k * H + j) * 4, 0, 0);
         }
         dev::wave_lds_fence();
