@@ -74,19 +74,21 @@ __host__ __device__ inline int p15_ring(int n, int h) {
 // LDS: per wave [transpose 1152 cf][ring(s) 64 / L x RL f], then the windows
 // [2][4][L][4] f shared by the workgroup.
 template <int L>
-size_t p15_lds(int h, int w) {
+size_t p15_lds(int h, int w, bool wreg = false) {
     return size_t(w) * (sizeof(dev::pc) * dev::kPairXbuf + sizeof(float) * (64 / L) * p15_ring(15 * L, h)) +
-           sizeof(float) * 2 * 16 * L;
+           (wreg ? 0 : sizeof(float) * 2 * 16 * L);
 }
 
 // Launch shapes (CRLOT_P15_VARIANT overrides, A/B): 0 = 5 walks per workgroup,
 // windows in LDS, 3 waves/SIMD budget; 1 = 2 walks, windows in registers,
-// 2 waves/SIMD; 2 = 4 walks, LDS windows; 3 = 2 walks, LDS windows.
+// 2 waves/SIMD; 2 = 4 walks, LDS windows; 3 = 2 walks, LDS windows; 4 = 4 walks,
+// windows in registers, 3 waves/SIMD (13 KB of LDS per walk: 12 waves per CU).
 struct P15Shape {
     int w;
     bool wreg;
+    int wpe;  // register budget: waves per SIMD
 };
-constexpr P15Shape kP15Shapes[4] = {{5, false}, {2, true}, {4, false}, {2, false}};
+constexpr P15Shape kP15Shapes[5] = {{5, false, 3}, {2, true, 2}, {4, false, 3}, {2, false, 3}, {4, true, 3}};
 constexpr int kP15Waves = 5;  // the widest shape (support check)
 
 }  // namespace
@@ -300,11 +302,13 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
     using namespace fk;
     static const int venv = [] {
         const char* e = std::getenv("CRLOT_P15_VARIANT");
-        return e ? std::atoi(e) & 3 : -1;
+        const int v = e ? std::atoi(e) : -1;
+        return v >= 0 && v < 5 ? v : -1;
     }();
-    // measured (960/240, 480/120 x 1024 streams): 4 walks with LDS windows at N = 960
-    // (149.6k vs 115.5k / 122.0k / 123.2k Msamples/s), 2 at N = 480 (145.1k vs 106.1k / 140.5k / 140.6k)
-    const int v = venv >= 0 ? venv : (g.n == 960 ? 2 : 3);
+    // measured (960/240, 480/120 x 1024 streams): 4 walks with the windows in
+    // registers, 12 waves per CU (174k / 173.5k Msamples/s) vs 4 walks with LDS
+    // windows, 8 waves per CU (148k / 140.5k) and 2 walks (117k / 148.5k)
+    const int v = venv >= 0 ? venv : 4;
     const int W = kP15Shapes[v].w;
     if (!pair15_supported(g.n, g.h, g.ring_len) || !t.ptw || !t.pflags || F <= 0 || n_streams <= 0 ||
         T >= (int64_t(1) << 27) || out_len >= (int64_t(1) << 27) || ld_x >= (int64_t(1) << 27) ||
@@ -332,8 +336,9 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const size_t lds = g.n == 960 ? p15_lds<64>(g.h, W) : p15_lds<32>(g.h, W);
-    const int64_t wpc = std::min<int64_t>(W * int64_t(160 * 1024 / lds), kP15Shapes[v].wreg ? 8 : 12);  // waves per CU
+    const bool wreg = kP15Shapes[v].wreg;
+    const size_t lds = g.n == 960 ? p15_lds<64>(g.h, W, wreg) : p15_lds<32>(g.h, W, wreg);
+    const int64_t wpc = std::min<int64_t>(W * int64_t(160 * 1024 / lds), 4 * kP15Shapes[v].wpe);  // waves per CU
     const int64_t resident = int64_t(cus) * std::max<int64_t>(W, wpc);
     const int64_t units = (n_streams + halves - 1) / halves;
     const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + units - 1) / units));
@@ -353,6 +358,7 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         case 1: g.n == 960 ? go(k_pair15_hot<64, 2, true, 2>, 2) : go(k_pair15_hot<32, 2, true, 2>, 2); break;
         case 2: g.n == 960 ? go(k_pair15_hot<64, 4, false, 3>, 4) : go(k_pair15_hot<32, 4, false, 3>, 4); break;
         case 3: g.n == 960 ? go(k_pair15_hot<64, 2, false, 3>, 2) : go(k_pair15_hot<32, 2, false, 3>, 2); break;
+        case 4: g.n == 960 ? go(k_pair15_hot<64, 4, true, 3>, 4) : go(k_pair15_hot<32, 4, true, 3>, 4); break;
         default: g.n == 960 ? go(k_pair15_hot<64, 5, false, 3>, 5) : go(k_pair15_hot<32, 5, false, 3>, 5); break;
     }
     return e;
