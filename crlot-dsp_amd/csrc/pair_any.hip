@@ -362,7 +362,6 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         default: g.n == 960 ? go(k_pair15_hot<64, 5, false, 3>, 5) : go(k_pair15_hot<32, 5, false, 3>, 5); break;
     }
     return e;
-    return hipGetLastError();
 }
 
 // [14][L] of W_N^{l k1} (N = 15 L), then at L = 64 [3][16] of W64^{b c}, at
