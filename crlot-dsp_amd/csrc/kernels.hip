@@ -1163,6 +1163,53 @@ __global__ __launch_bounds__(256) void k_ola_gather2(const GatherArgs a) {
     }
 }
 
+// One workgroup per (output block b of H samples, stream): the block's
+// frames are k = b-nb+1 .. b (nb = ceil(N/H)), frame k's samples for it a
+// contiguous run at (b-k) H, so a thread's offsets need no division.  Every
+// frame sample, window tap and the divisor are requested before the sum, which
+// runs in ascending k exactly as k_ola_gather's.
+template <int MAXNB>
+__global__ __launch_bounds__(256) void k_ola_gather_blk(const GatherArgs a, int bpb) {
+    const int64_t s = blockIdx.y;
+    const int h = a.h, N = a.n;
+    const int nb = (N + h - 1) / h;
+    const float* fr = a.frames + s * a.F * a.ld_frames;
+    const int b1 = int(min<int64_t>(a.F, int64_t(blockIdx.x + 1) * bpb));
+    for (int b = int(blockIdx.x) * bpb; b < b1; ++b) {  // bpb blocks per workgroup (short hops)
+    const int kmin = max(0, b - nb + 1), kmax = min(b, int(a.F) - 1);
+    const int dbase = int(int64_t(b) * h % a.ring_len);
+    float* yo = a.y + s * a.ld_y + int64_t(b) * h;
+    for (int j = int(threadIdx.x); j < h; j += int(blockDim.x)) {
+        if (int64_t(b) * h + j >= a.out_len) break;
+        int d = dbase + j;
+        d = d >= a.ring_len ? d - a.ring_len : d;
+        const float dv = a.den[d];
+        float acc = 0.0f;
+        if (kmax - kmin + 1 <= MAXNB) {
+            float src[MAXNB], w[MAXNB];
+#pragma unroll
+            for (int i = 0; i < MAXNB; ++i) {
+                const int k = kmin + i, off = (b - k) * h + j;
+                const bool in = k <= kmax && off < N;
+                src[i] = in ? fr[int64_t(k) * a.ld_frames + off] : 0.0f;
+                w[i] = in ? a.ws[off] : 0.0f;
+            }
+#pragma unroll
+            for (int i = 0; i < MAXNB; ++i) {
+                const int k = kmin + i, off = (b - k) * h + j;
+                if (k <= kmax && off < N) acc = __builtin_fmaf(__builtin_fmaf(src[i], w[i], 0.0f), a.gain, acc);
+            }
+        } else {
+            for (int k = kmin; k <= kmax; ++k) {
+                const int off = (b - k) * h + j;
+                if (off < N) acc = __builtin_fmaf(__builtin_fmaf(fr[int64_t(k) * a.ld_frames + off], a.ws[off], 0.0f), a.gain, acc);
+            }
+        }
+        yo[j] = acc / dv;
+    }
+    }
+}
+
 // ------------------------------------------------------------------ rfft / irfft
 struct FftArgs {
     DevTables t;
@@ -2584,6 +2631,24 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
     a.ring_len = g.ring_len;
     a.n_streams = n_streams;
     a.gain = g.gain;
+    static const int gv = [] {  // A/B: CRLOT_GATHER=2 the per-sample-grid kernel
+        const char* e = std::getenv("CRLOT_GATHER");
+        return e ? std::atoi(e) : 3;
+    }();
+    if (gv == 3 && n_streams <= 65535 && F < (int64_t(1) << 31) && out_len <= F * g.h &&
+        out_len < (int64_t(1) << 31) - int64_t(g.h)) {
+        const int nb = (g.n + g.h - 1) / g.h;
+        auto kg = nb <= 4 ? k_ola_gather_blk<4> : k_ola_gather_blk<8>;
+        const int threads = g.h >= 256 ? 256 : (g.h + 63) / 64 * 64;
+        static const int bpb_env = [] {
+            const char* e = std::getenv("CRLOT_GATHER_BPB");
+            return e ? std::atoi(e) : 0;
+        }();
+        const int bpb = bpb_env > 0 ? bpb_env : std::max(1, 1024 / g.h);  // >= 1024 outputs per workgroup
+        hipLaunchKernelGGL(kg, dim3(unsigned((F + bpb - 1) / bpb), unsigned(n_streams)), dim3(threads), 0, stream,
+                           a, bpb);
+        return hipGetLastError();
+    }
     if (n_streams <= 65535 && out_len < (int64_t(1) << 31) - 256 && int64_t(g.h) + 256 < (1 << 24)) {
         // one sample per thread (two per thread measured 5-15 % slower: occupancy)
         auto kg = (g.n + g.h - 1) / g.h <= 4 ? k_ola_gather2<1, 4> : k_ola_gather2<1, 8>;
