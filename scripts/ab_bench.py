@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 S, T, N, H = int(os.environ.get("AB_S", 1024)), 480000, int(os.environ.get("AB_N", 1024)), int(os.environ.get("AB_H", 256))
-libs = sorted(glob.glob(os.path.join(ROOT, "crlot-dsp_amd", "variants", "*.so")))
+libs = sorted(glob.glob(os.environ.get("AB_GLOB") or os.path.join(ROOT, "crlot-dsp_amd", "variants", "*.so")))
 base = os.path.join(ROOT, "crlot-dsp_amd", "libcrlot_dsp.so")
 libs = [base] + libs
 
@@ -63,6 +63,6 @@ for p in libs:
     t = sorted(times[p])
     same = bool(torch.equal(ys[p], ref))
     maxd = float((ys[p] - ref).abs().max())
-    print(json.dumps({"lib": os.path.basename(p), "ms_median": round(t[len(t) // 2], 4),
+    print(json.dumps({"lib": os.path.relpath(p, ROOT), "ms_median": round(t[len(t) // 2], 4),
                       "ms_min": round(t[0], 4), "Msamples_s": round(S * T / t[len(t) // 2] / 1e3, 1),
                       "bitexact_vs_base": same, "maxdiff": maxd}))
