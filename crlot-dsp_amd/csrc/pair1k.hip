@@ -54,6 +54,15 @@ struct PairLds {
 #ifndef CRLOT_PAIR_REG_TW
 #define CRLOT_PAIR_REG_TW 1  // measured: LDS twiddles at 4 waves/SIMD take 5 % more cycles
 #endif
+// Cache policy of the hot walker's hop loads and output stores: nt (streaming;
+// each sample is read by one walk and written once).  Measured +0.1-1.6 % over
+// the default policy in four interleaved A/B runs (scripts/ab_bench.py).
+#ifndef CRLOT_PAIR_LD_AUX
+#define CRLOT_PAIR_LD_AUX 2
+#endif
+#ifndef CRLOT_PAIR_ST_AUX
+#define CRLOT_PAIR_ST_AUX 2
+#endif
 #ifndef CRLOT_PAIR_MIN_WAVES
 #define CRLOT_PAIR_MIN_WAVES (CRLOT_PAIR_REG_TW ? 3 : 4)
 #endif
@@ -109,10 +118,15 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + wid.xo, span_bytes(a.T, cs));
     const HopRsrc<ILV ? SH : 1> rxq = hop_rsrc<ILV ? SH : 1>(a.x + wid.xo, ILV ? a.T : 0, cs);
     auto load_hop = [&](float* dst, int origin) {
-        if constexpr (ILV)
+        if constexpr (ILV) {
             load_hop0s<SH>(dst, rxq, lane, origin, cs);
-        else
-            load_hop0<SH>(dst, rx, lane, origin);
+        } else {
+            const int v = (origin + lane) * 4;
+#pragma unroll
+            for (int q = 0; q < SH; ++q)
+                dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, v + q * 256, 0,
+                                                                                        CRLOT_PAIR_LD_AUX));
+        }
     };
     const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + wid.yo, span_bytes(a.out_len, cs));
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
@@ -162,7 +176,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * (4 * cs),
-                                                  (k * (4 * H) + q * 256) * cs, 0);
+                                                  (k * (4 * H) + q * 256) * cs, CRLOT_PAIR_ST_AUX);
     };
 
 #if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
