@@ -34,6 +34,13 @@ namespace fk {
 
 namespace {
 
+// Cache policy of the hot walkers' hop loads and output stores (2 = nt, streaming).
+// Default policy kept: nt measured 4096/1024 +1.6 / -2.5 %, 512/128 -1.6 / -1.8 %,
+// 2048/512 +2.0 / +0.9 % in interleaved A/Bs (scripts/ab_bench.py).
+#ifndef CRLOT_HOT_AUX
+#define CRLOT_HOT_AUX 0
+#endif
+
 // Exchange rows: a wave's own rows hold its 1152-element transpose buffer, and
 // the row stride keeps the lane groups of a 32-lane b64 access on distinct
 // banks (4k: 16-lane groups 2432 B = 128 B mod 256 B apart, as kP4Stride;
@@ -137,7 +144,13 @@ template <int L, int SH>
 __device__ __forceinline__ void load_hop_wg0(float* dst, __amdgpu_buffer_rsrc_t rx, int t, int origin) {
     const int v = (origin + t) * 4;  // out-of-range lanes (either side) read 0: see load_hop0
 #pragma unroll
-    for (int q = 0; q < SH; ++q) dst[q] = dev::bload1(rx, v + q * (4 * L), 0);
+    for (int q = 0; q < SH; ++q)
+        dst[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, v + q * (4 * L), 0, CRLOT_HOT_AUX));
+}
+// ... for one wave (lane l holds samples l + 64 q)
+template <int SH>
+__device__ __forceinline__ void load_hop_w(float* dst, __amdgpu_buffer_rsrc_t rx, int lane, int origin) {
+    load_hop_wg0<64, SH>(dst, rx, lane, origin);
 }
 
 // den | rden of block b (DevTables::pden4: [block][L][den SH | rden SH])
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
-                                                  k * (4 * H) + q * (4 * L), 0);
+                                                  k * (4 * H) + q * (4 * L), CRLOT_HOT_AUX);
     };
 
     auto step = [&](auto phc, int k) {
@@ -376,7 +389,7 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
     float xr[R][SH];
 #pragma unroll
     for (int h = 0; h <= NB; ++h) {
-        load_hop0<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
+        load_hop_w<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
         hop_check(xr[h]);
     }
     float acc[NB][SH];
@@ -400,13 +413,13 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
-                                                  k * (4 * H) + q * 256, 0);
+                                                  k * (4 * H) + q * 256, CRLOT_HOT_AUX);
     };
     auto step = [&](auto phc, int k) {
         constexpr int PH = decltype(phc)::value;
         constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
-        load_hop0<SH>(xr[(S0 + NB + 1) % R], rx, lane, (k + NB + 1) * H - a.pad);
-        load_hop0<SH>(xr[(S0 + NB + 2) % R], rx, lane, (k + NB + 2) * H - a.pad);
+        load_hop_w<SH>(xr[(S0 + NB + 1) % R], rx, lane, (k + NB + 1) * H - a.pad);
+        load_hop_w<SH>(xr[(S0 + NB + 2) % R], rx, lane, (k + NB + 2) * H - a.pad);
         const bool partner = k + 1 < a.F;  // as the two-regime walker
         dev::pc v[E];
 #pragma unroll
