@@ -63,10 +63,12 @@ def flop_per_sample(n: int, h: int) -> float:
 
 
 def src_hash() -> str:
-    """Hash of the kernel sources; a PMC profile applies only to the same hash."""
+    """Hash of the kernel sources and their build flags (Makefile); a PMC profile
+    applies only to the same hash."""
     h = hashlib.sha256()
     csrc = os.path.join(ROOT, "crlot-dsp_amd", "csrc")
-    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h"))):
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")) +
+                    [os.path.join(csrc, "Makefile")]):
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
