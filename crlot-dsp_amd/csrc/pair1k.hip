@@ -56,7 +56,10 @@ struct PairLds {
 #endif
 // Cache policy of the hot walker's hop loads and output stores: nt (streaming;
 // each sample is read by one walk and written once).  Measured +0.1-1.6 % over
-// the default policy in four interleaved A/B runs (scripts/ab_bench.py).
+// the default policy in four interleaved A/B runs (scripts/ab_bench.py).  The
+// interleaved-group walk keeps the default policy for its stores: its rows are
+// written a word per lane by several waves, which L2 must merge (nt stores
+// there: C = 4 251k -> 142k Msamples/s).
 #ifndef CRLOT_PAIR_LD_AUX
 #define CRLOT_PAIR_LD_AUX 2
 #endif
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * (4 * cs),
-                                                  (k * (4 * H) + q * 256) * cs, CRLOT_PAIR_ST_AUX);
+                                                  (k * (4 * H) + q * 256) * cs, ILV ? 0 : CRLOT_PAIR_ST_AUX);
     };
 
 #if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
