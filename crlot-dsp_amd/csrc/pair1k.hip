@@ -325,11 +325,20 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     static_assert(NB * SH == E, "N = NB * H");
     static_assert(SH >= 2, "den rows are read 16 bytes at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    {  // only walkers the paired-only pass flagged; whole workgroups leave together
+    {  // only walkers the paired-only pass flagged; whole workgroups leave together.
+       // The vote goes through the (still unused) transpose buffers rather than
+       // __syncthreads_or, whose 256 B of static LDS would not fit beside a
+       // 16-wave workgroup's 160 KB.
         const int64_t w0 = int64_t(blockIdx.x) * W;
         const int t = threadIdx.x;
-        const bool mine = t < W && w0 + t < int64_t(a.n_streams) * a.n_chunks && (a.fix_all || a.t.pflags[w0 + t] != 0u);
-        if (!__syncthreads_or(mine)) return;
+        uint32_t* vote = reinterpret_cast<uint32_t*>(smem + PairLds<W>::bufs);
+        if (t < W)
+            vote[t] = (w0 + t < int64_t(a.n_streams) * a.n_chunks && (a.fix_all || a.t.pflags[w0 + t] != 0u)) ? 1u : 0u;
+        __syncthreads();
+        uint32_t any = 0;
+#pragma unroll
+        for (int i = 0; i < W; ++i) any |= vote[i];
+        if (!any) return;
     }
     dev::pc* t1 = reinterpret_cast<dev::pc*>(smem + PairLds<W>::t1);
     dev::pc* t2s = reinterpret_cast<dev::pc*>(smem + PairLds<W>::t2);
