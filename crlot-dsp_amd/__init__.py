@@ -329,8 +329,9 @@ class Plan:
 
     def set_frame_pairing(self, enable: bool = True):
         """Two frames per complex transform on the fused round trip (default);
-        False selects the per-frame kernels, bit-identical to stages + ola_gather."""
-        _check(lib().crlot_plan_set_frame_pairing(self._h, int(bool(enable))))
+        False selects the per-frame kernels, bit-identical to stages + ola_gather;
+        2 pairs through the two-regime walkers only (hot walkers off, same bits)."""
+        _check(lib().crlot_plan_set_frame_pairing(self._h, 2 if enable == 2 else int(bool(enable))))
 
     def set_spectral_gain(self, gain=None):
         g = None if gain is None else np.ascontiguousarray(gain, np.float32)

@@ -48,6 +48,7 @@ struct crlot_plan {
     float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
+    bool hot = true;          // ... 2: pairing with the two-regime walkers only
     bool fast_ok = false;     // both exact rewrites valid for the current tables
     bool den_mk_ok = false;   // every den in [2^-40, 2^40]: Markstein division exact
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
@@ -121,6 +122,7 @@ crlot::DevTables tables(const crlot_plan* p) {
         }
         t.pflags = p->d_pflags;
         t.pflags_len = p->pflags_len;
+        t.hot = p->hot ? 1 : 0;
         t.px_lo = p->px_lo;
         // no transform can overflow: |x w| <= 2^64 / max gain, so |X| < 2^75, |ifft| < 2^86
         t.px_hi = p->px_hi / std::max(1.0f, p->has_gain ? p->gain_max : 1.0f);
@@ -498,7 +500,9 @@ int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
 
 int crlot_plan_set_frame_pairing(crlot_plan* p, int32_t enable) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (enable < 0 || enable > 2) return fail(CRLOT_EINVAL, "frame pairing mode is 0, 1 or 2");
     p->pairing = enable != 0;
+    p->hot = enable != 2;
     return CRLOT_OK;
 }
 

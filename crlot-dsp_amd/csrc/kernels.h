@@ -43,6 +43,9 @@ struct DevTables {
     // fix-up walker that redoes those chunks; pflags_len flags of capacity.
     uint32_t* pflags = nullptr;
     int64_t pflags_len = 0;
+    // 0: the paired-only hot walkers stay off and the two-regime walkers run every
+    // chunk (crlot_plan_set_frame_pairing(plan, 2): parity diagnostics)
+    int hot = 1;
 };
 
 // Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.

@@ -1870,7 +1870,7 @@ hipError_t pair512_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     FusedArgs b = a;
     // the paired-only hot walker (H = 128, 256), then this two-regime walker over
     // the chunks it flagged; a gain or reflect/edge padding: the latter alone
-    if ((SH == 2 || SH == 4) && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled()) {
+    if ((SH == 2 || SH == 4) && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
         if ((e = launch_pair512_hot(SH, a, waves, kP512Waves, stream)) != hipSuccess) return e;
     } else {
         b.fix_all = 1;
@@ -1927,7 +1927,7 @@ hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_stream
     if (!a.t.pflags || a.t.pflags_len < grid) return hipErrorInvalidValue;
     // the paired-only hot walker where it holds its registers (H = 512), then the
     // two-regime walker over the chunks it flagged; otherwise the latter alone
-    if (g.h == 512 && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled()) {
+    if (g.h == 512 && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
         hipError_t e = launch_pair2k_hot(4, a, grid, stream);
         if (e != hipSuccess) return e;
     } else {
@@ -2282,7 +2282,7 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
         if (!t.pflags || t.pflags_len < grid4) return hipErrorInvalidValue;
         // the paired-only hot walker, then the two-regime walker over the chunks it
         // flagged; a spectral gain or reflect/edge padding: the two-regime walker alone
-        if (!t.gain && a.pad_mode == 0 && !pair4k_hot_disabled()) {
+        if (!t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
             hipError_t e = launch_pair4k_hot(g.h / 256, a, grid4, stream);
             if (e != hipSuccess) return e;
         } else {

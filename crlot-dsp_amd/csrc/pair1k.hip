@@ -84,7 +84,7 @@ struct PairRot {
     static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
 };
 
-template <int SH, int NB, int W, bool ILV>
+template <int SH, int NB, int W, bool ILV, bool HAS_GAIN>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
     constexpr int E = 16, N = 1024, H = 64 * SH;
     constexpr int R = PairRot<NB>::R, U = PairRot<NB>::U;
@@ -110,6 +110,26 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     dev::pc* buf = reinterpret_cast<dev::pc*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
     const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
+#if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
+    dev::PairTw tw;
+    dev::pair_tw_load(tw, t1, t2, lane);
+    const dev::PairTw& tw1 = tw;
+    const dev::PairTw& tw2 = tw;
+#else
+    const dev::pc* const tw1 = t1;
+    const dev::pc* const tw2 = t2;
+#endif
+    // spectral gain (the spectral hook, the two-regime walker's operation): once
+    // every wave holds its twiddles in registers, the per-bin gain [N] replaces
+    // the twiddle table in LDS (no room for both beside three workgroups per CU)
+    const float* const gl = reinterpret_cast<const float*>(smem + PairLds<W>::t1) + dev::pair_bin_lane(lane);
+    if constexpr (HAS_GAIN) {
+        static_assert(CRLOT_PAIR_REG_TW, "the gain table overlays the twiddle table");
+        __syncthreads();
+        float* gw_ = reinterpret_cast<float*>(smem + PairLds<W>::t1);
+        for (int i = threadIdx.x; i < N; i += 64 * W) gw_[i] = a.t.gain[i <= N / 2 ? i : N - i];
+        __syncthreads();
+    }
     const int gw = blockIdx.x * W + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
     const WalkId wid = walk_id<ILV>(a, gw);
@@ -182,15 +202,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                                                   (k * (4 * H) + q * 256) * cs, ILV ? 0 : CRLOT_PAIR_ST_AUX);
     };
 
-#if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
-    dev::PairTw tw;
-    dev::pair_tw_load(tw, t1, t2, lane);
-    const dev::PairTw& tw1 = tw;
-    const dev::PairTw& tw2 = tw;
-#else
-    const dev::pc* const tw1 = t1;
-    const dev::pc* const tw2 = t2;
-#endif
     constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
 
     // One pair (frames k, k+1) at unroll position PH: hop k in slot S0, frame
@@ -221,6 +232,10 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             // the framed samples there -- zeros for ZERO_PAD, the padding rule's
             // values otherwise: deterministic per stream, and never produced)
             dev::pair_fft_fwd(v, buf, tw1, tw2, lane);
+            if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins (as the two-regime walker)
+#pragma unroll
+                for (int d = 0; d < E; ++d) v[d] = v[d] * gl[64 * d];
+            }
             // both blocks' divisors (L2-resident table) during the inverse, before
             // this pair's stores: vmcnt retires in order, so a load issued after
             // a store would also wait for that store
@@ -554,11 +569,12 @@ bool pair_nofix() {
 }
 
 // The paired-only walker where it holds its registers without spilling: hops
-// of 256 (SH = 4; SH = 8 spills 9 VGPRs) without a spectral gain.  Other hops, a gain, and
-// reflect / edge padding run the two-regime walker over every chunk.
+// of 256 (SH = 4; SH = 8 spills 9 VGPRs), with or without a spectral gain (the
+// gain table overlays the twiddle table, so only with register twiddles).
+// Other hops and reflect / edge padding run the two-regime walker over every chunk.
 template <int SH>
-constexpr bool pair_hot(bool gain) {
-    return SH == 4 && !gain;
+constexpr bool pair_hot() {
+    return SH == 4;
 }
 
 template <int SH, bool ILV>
@@ -571,9 +587,9 @@ hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     auto kf = a.t.gain ? k_stft_ola_pair_fix<SH, NB, W, true, ILV> : k_stft_ola_pair_fix<SH, NB, W, false, ILV>;
     if ((e = set_lds(kf, lds)) != hipSuccess) return e;
     if (!a.t.pflags || a.t.pflags_len < waves) return hipErrorInvalidValue;
-    if constexpr (pair_hot<SH>(false)) {
-        if (a.pad_mode == 0 && !a.t.gain) {
-            auto k = k_stft_ola_pair<SH, NB, W, ILV>;
+    if constexpr (pair_hot<SH>()) {
+        if (a.pad_mode == 0 && a.t.hot && (!a.t.gain || CRLOT_PAIR_REG_TW)) {
+            auto k = a.t.gain ? k_stft_ola_pair<SH, NB, W, ILV, CRLOT_PAIR_REG_TW != 0> : k_stft_ola_pair<SH, NB, W, ILV, false>;
             if ((e = set_lds(k, lds)) != hipSuccess) return e;
             hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -118,7 +118,10 @@ int crlot_plan_set_spectral_gain_async(crlot_plan* plan, const float* gain, void
  * overflow reaches its neighbour.  Results equal the per-frame kissfft
  * formulation within float32 rounding, not bit for bit, and do not depend on
  * the batch or the chunking.  0 selects the per-frame (kiss_fftr split)
- * kernels, bit-identical to crlot_roundtrip_stages + crlot_ola_gather. */
+ * kernels, bit-identical to crlot_roundtrip_stages + crlot_ola_gather.  2 keeps
+ * pairing but runs the power-of-two pair kernels' two-regime walkers on every
+ * chunk (their paired-only hot walkers off): bit-identical to 1, for parity
+ * diagnostics.  Other values: CRLOT_EINVAL. */
 int crlot_plan_set_frame_pairing(crlot_plan* plan, int32_t enable);
 int crlot_plan_info(const crlot_plan* plan, int32_t* frame_size, int32_t* hop_size,
                     int32_t* ring_len);

@@ -943,10 +943,11 @@ def test_roundtrip_interleaved_direct_pair_walker(pkg, oracle, torch_cuda, h, C_
                                    (512, 128, 40_001), (512, 256, 25_000)])
 def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h, T):
     """The paired-only hot walkers (K_pair, K_pair4k, K_pair2k, K_pair512) and the two-regime walkers
-    they fall back to agree bit for bit: a spectral gain of exactly 1 sends the
-    plan through the two-regime walker over every chunk (x * 1 is exact), no gain
-    through the hot walker; a burst of out-of-range samples exercises the flagged
-    chunks' fix-up inside the hot run."""
+    they fall back to agree bit for bit: pairing mode 2 sends the plan through the
+    two-regime walker over every chunk, mode 1 through the hot walker; a burst of
+    out-of-range samples exercises the flagged chunks' fix-up inside the hot run.
+    A spectral gain of exactly 1 (x * 1 is exact) gives the same bits again, through
+    K_pair's gain-carrying hot walker or the others' two-regime walkers."""
     torch = torch_cuda
     x = oracle.synth_streams(6, T, config_id=71)
     x[2, T // 3:T // 3 + 5] = 1e25   # unpaired regime: that chunk is redone
@@ -954,9 +955,44 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     xd = dev(torch, x)
     plan = pkg.Plan(frame_size=n, hop_size=h)
     y_hot = host(plan.roundtrip(xd))
-    plan.set_spectral_gain(np.ones(n // 2 + 1, np.float32))
+    plan.set_frame_pairing(2)
     y_fix = host(plan.roundtrip(xd))
     assert np.array_equal(bits(y_hot), bits(y_fix))
+    plan.set_frame_pairing(1)
+    plan.set_spectral_gain(np.ones(n // 2 + 1, np.float32))
+    y_gain1 = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(y_hot), bits(y_gain1))
+
+
+@pytest.mark.parametrize("h,T,ilv", [(256, 50_000, 1), (256, 33_001, 3), (256, 2_000, 1)])
+def test_pair_hot_walker_spectral_gain_equals_two_regime(pkg, oracle, torch_cuda, h, T, ilv):
+    """K_pair's hot walker applies a spectral gain (the spectral hook) with the
+    two-regime walker's operation: bit-identical to pairing mode 2 on mono rows and
+    on interleaved groups, with flagged chunks redone inside the hot run."""
+    torch = torch_cuda
+    n = 1024
+    x = oracle.synth_streams(6, T, config_id=73)
+    if T > 10_000:
+        x[1, T // 3:T // 3 + 5] = 1e25
+        x[3, T // 2] = 1e-33
+    gain = (0.25 + np.abs(np.sin(np.arange(n // 2 + 1) * 0.013))).astype(np.float32)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_spectral_gain(gain)
+
+    def run():
+        if ilv == 1:
+            return host(plan.roundtrip(dev(torch, x)))
+        xi = torch.from_numpy(np.ascontiguousarray(x.reshape(6 // ilv, ilv, T).transpose(0, 2, 1))).cuda()
+        return host(plan.roundtrip_interleaved(xi))
+    y_hot = run()
+    plan.set_frame_pairing(2)
+    y_fix = run()
+    assert np.array_equal(bits(y_hot), bits(y_fix))
+    plan.set_frame_pairing(False)  # per-frame kernels: the same chain within float32 rounding
+    y_pf = run()
+    if ilv == 1:
+        for s_ in (0, 2, 4, 5):
+            assert_close(y_hot[s_], y_pf[s_], 0.5, f"stream {s_} paired vs per-frame")
 
 
 # ------------------------------------------------------------------ K_pair960 (N = 960 frame pairs)
