@@ -2281,8 +2281,9 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
         const int64_t grid4 = int64_t(n_streams) * a.n_chunks;
         if (!t.pflags || t.pflags_len < grid4) return hipErrorInvalidValue;
         // the paired-only hot walker, then the two-regime walker over the chunks it
-        // flagged; a spectral gain or reflect/edge padding: the two-regime walker alone
-        if (!t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
+        // flagged; reflect/edge padding, or a spectral gain at H != 1024: the
+        // two-regime walker alone
+        if ((!t.gain || g.h == 1024) && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
             hipError_t e = launch_pair4k_hot(g.h / 256, a, grid4, stream);
             if (e != hipSuccess) return e;
         } else {

@@ -83,6 +83,7 @@ struct Geo4k {
     static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
         dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
     }
+    static constexpr __device__ int bin(int t, int d) { return dev::pair4k_bin(t, d); }
     static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const Tw& tw, int t, int wave) {
         dev::pdft16<false>(v);
         tw_all<false>(v, tw.w1);
@@ -176,7 +177,7 @@ constexpr size_t hot_lds() {
 }
 
 // One workgroup (G::L lanes) walks one chunk; lane t holds samples t + L m.
-template <typename G, int SH, int NB>
+template <typename G, int SH, int NB, bool HAS_GAIN = false>
 __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_pair_wg_hot(const FusedArgs a) {
     constexpr int E = 16, L = G::L, H = L * SH;
     constexpr int R = RotWg<NB>::R, U = RotWg<NB>::U;
@@ -206,6 +207,15 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     for (int m = 0; m < E; ++m) {
         wa[m] = a.t.wa[t + L * m];
         ws[m] = a.t.wsn[t + L * m];
+    }
+    // spectral gain of this lane's bins (the two-regime walker's operation), in registers
+    float gr[HAS_GAIN ? E : 1];
+    if constexpr (HAS_GAIN) {
+#pragma unroll
+        for (int d = 0; d < E; ++d) {
+            const int kb = G::bin(t, d);
+            gr[d] = a.t.gain[kb <= G::N / 2 ? kb : G::N - kb];
+        }
     }
 
     // a hop keeps the paired regime iff every sample is 0 or in [px_lo, px_hi]
@@ -266,6 +276,10 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
             v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wa[m],
                               partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wa[m] : 0.0f);
         G::fwd(v, A, tw, t, wave);
+        if constexpr (HAS_GAIN) {
+#pragma unroll
+            for (int d = 0; d < E; ++d) v[d] = v[d] * gr[d];
+        }
         float dr0[2 * SH], dr1[2 * SH];
         load_den_wg<L, SH>(dr0, rp, t, k % a.ring_blocks);
         load_den_wg<L, SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
@@ -330,8 +344,12 @@ hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t s
         return hipGetLastError();
     };
     if constexpr (G::N == 2048) {  // H = 256 / 1024 spill at N = 2048: the two-regime walker runs those
-        return sh == 4 ? go(k_pair_wg_hot<G, 4, 4>) : hipErrorInvalidValue;
+        return sh == 4 && !a.t.gain ? go(k_pair_wg_hot<G, 4, 4>) : hipErrorInvalidValue;
     } else {
+        if (a.t.gain) {  // the gain's 16 registers fit beside H = 1024's walk only
+            auto kg = k_pair_wg_hot<G, 4, 4, true>;
+            return sh == 4 ? go(kg) : hipErrorInvalidValue;
+        }
         switch (sh) {
             case 2: return go(k_pair_wg_hot<G, 2, 8>);
             case 4: return go(k_pair_wg_hot<G, 4, 4>);

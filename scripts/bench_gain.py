@@ -14,7 +14,8 @@ def main():
     import torch
     from __graft_entry__ import load_pkg
     pkg = load_pkg()
-    S, T, N, H = 1024, 480000, 1024, 256
+    S, T = 1024, 480000
+    N, H = int(os.environ.get("BG_N", 1024)), int(os.environ.get("BG_H", 256))
     g = torch.Generator(device="cuda").manual_seed(5)
     x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
     for label, gain in (("no gain", None), ("spectral gain", np.linspace(0.5, 1.5, N // 2 + 1).astype(np.float32))):

@@ -964,13 +964,14 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     assert np.array_equal(bits(y_hot), bits(y_gain1))
 
 
-@pytest.mark.parametrize("h,T,ilv", [(256, 50_000, 1), (256, 33_001, 3), (256, 2_000, 1)])
-def test_pair_hot_walker_spectral_gain_equals_two_regime(pkg, oracle, torch_cuda, h, T, ilv):
-    """K_pair's hot walker applies a spectral gain (the spectral hook) with the
-    two-regime walker's operation: bit-identical to pairing mode 2 on mono rows and
-    on interleaved groups, with flagged chunks redone inside the hot run."""
+@pytest.mark.parametrize("n,h,T,ilv", [(1024, 256, 50_000, 1), (1024, 256, 33_001, 3), (1024, 256, 2_000, 1),
+                                       (4096, 1024, 123_457, 1), (4096, 1024, 9_000, 1)])
+def test_pair_hot_walker_spectral_gain_equals_two_regime(pkg, oracle, torch_cuda, n, h, T, ilv):
+    """The hot walkers of K_pair (and K_pair4k at H = 1024) apply a spectral gain
+    (the spectral hook) with the two-regime walker's operation: bit-identical to
+    pairing mode 2 on mono rows and on interleaved groups, with flagged chunks
+    redone inside the hot run."""
     torch = torch_cuda
-    n = 1024
     x = oracle.synth_streams(6, T, config_id=73)
     if T > 10_000:
         x[1, T // 3:T // 3 + 5] = 1e25
