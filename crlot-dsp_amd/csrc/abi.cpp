@@ -581,7 +581,7 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
     if (p->generic && crlot::fused_any_fits(p->geo.n, p->geo.h) && ld_x < (int64_t(1) << 40)) {
         // N = 960 / 480 frame pairs (K_pair15), then the per-frame walker over the streams it flagged
         const int64_t lim = int64_t(1) << 27;
-        if (p->pairing && t.ptw && !p->has_gain && p->geo.pad_mode == 0 &&
+        if (p->pairing && t.ptw && p->geo.pad_mode == 0 &&
             crlot::pair15_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < lim && out_len < lim &&
             ld_x < lim && ld_y < lim) {
             const int rcf = ensure_pair_flags(p, n_streams, F);

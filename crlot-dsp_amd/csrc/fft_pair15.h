@@ -22,6 +22,12 @@ namespace dev {
 __host__ __device__ constexpr int pair15_bin(int lane, int d) {
     return ((lane & 3) + 4 * (lane >> 4)) + 15 * (((lane >> 2) & 3) + 4 * d);  // k1 = 15: no bin
 }
+// N = 480 (pair15h_fwd): half-lane h = lane & 31 holds k1 = (h & 7) + 8 (h >> 4),
+// c = (h >> 3) & 1 and, in register e, bin k1 + 15 (c + 2 e) (k1 = 15: the zero row)
+__host__ __device__ constexpr int pair15h_bin(int lane, int e) {
+    const int h = lane & 31;
+    return ((h & 7) + 8 * (h >> 4)) + 15 * (((h >> 3) & 1) + 2 * e);
+}
 
 __device__ __forceinline__ pc pc_fma(pc a, pc b, pc c) { return __builtin_elementwise_fma(a, b, c); }
 

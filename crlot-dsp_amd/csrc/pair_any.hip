@@ -93,7 +93,7 @@ constexpr int kP15Waves = 5;  // the widest shape (support check)
 
 }  // namespace
 
-template <int L, int W, bool WREG, int WPE>  // WREG: windows in registers (else LDS)
+template <int L, int W, bool WREG, int WPE, bool HAS_GAIN = false>  // WREG: windows in registers (else LDS)
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_pair15_hot(const FusedArgs a) {
     constexpr int E = kE, N = P15<L>::N, HALVES = 64 / L;
@@ -248,6 +248,13 @@ void k_pair15_hot(const FusedArgs a) {
         load_frame(fa, (k + 2) * H - a.pad);
         load_frame(fb, (k + 3) * H - a.pad);
         P15<L>::fwd(v, buf, tw, lane);
+        if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins (L2-resident table)
+#pragma unroll
+            for (int d = 0; d < 16; ++d) {
+                const int kb = L == 64 ? dev::pair15_bin(lane, d) : dev::pair15h_bin(lane, d);  // <= N
+                v[d] = v[d] * a.t.gain[kb <= N / 2 ? kb : N - kb];
+            }
+        }
         P15<L>::inv(v, buf, tw, lane);
         // o = v / N; its sanitize threshold 1e-30 = 2^-99.66: frexp exponents <= -99 flag the walk
         {
@@ -308,7 +315,8 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
     // measured (960/240, 480/120 x 1024 streams): 4 walks with the windows in
     // registers, 12 waves per CU (174k / 173.5k Msamples/s) vs 4 walks with LDS
     // windows, 8 waves per CU (148k / 140.5k) and 2 walks (117k / 148.5k)
-    const int v = venv >= 0 ? venv : 4;
+    const int v = venv >= 0 && !t.gain ? venv : 4;
+    const bool wreg = kP15Shapes[v].wreg && !t.gain;  // the gain walker keeps the windows in LDS
     const int W = kP15Shapes[v].w;
     if (!pair15_supported(g.n, g.h, g.ring_len) || !t.ptw || !t.pflags || F <= 0 || n_streams <= 0 ||
         T >= (int64_t(1) << 27) || out_len >= (int64_t(1) << 27) || ld_x >= (int64_t(1) << 27) ||
@@ -336,7 +344,6 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const bool wreg = kP15Shapes[v].wreg;
     const size_t lds = g.n == 960 ? p15_lds<64>(g.h, W, wreg) : p15_lds<32>(g.h, W, wreg);
     const int64_t wpc = std::min<int64_t>(W * int64_t(160 * 1024 / lds), 4 * kP15Shapes[v].wpe);  // waves per CU
     const int64_t resident = int64_t(cus) * std::max<int64_t>(W, wpc);
@@ -358,7 +365,12 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         case 1: g.n == 960 ? go(k_pair15_hot<64, 2, true, 2>, 2) : go(k_pair15_hot<32, 2, true, 2>, 2); break;
         case 2: g.n == 960 ? go(k_pair15_hot<64, 4, false, 3>, 4) : go(k_pair15_hot<32, 4, false, 3>, 4); break;
         case 3: g.n == 960 ? go(k_pair15_hot<64, 2, false, 3>, 2) : go(k_pair15_hot<32, 2, false, 3>, 2); break;
-        case 4: g.n == 960 ? go(k_pair15_hot<64, 4, true, 3>, 4) : go(k_pair15_hot<32, 4, true, 3>, 4); break;
+        case 4:
+            if (t.gain)  // the spectral hook: 4 walks, the windows in LDS (the gain loads need the registers)
+                g.n == 960 ? go(k_pair15_hot<64, 4, false, 3, true>, 4) : go(k_pair15_hot<32, 4, false, 3, true>, 4);
+            else
+                g.n == 960 ? go(k_pair15_hot<64, 4, true, 3>, 4) : go(k_pair15_hot<32, 4, true, 3>, 4);
+            break;
         default: g.n == 960 ? go(k_pair15_hot<64, 5, false, 3>, 5) : go(k_pair15_hot<32, 5, false, 3>, 5); break;
     }
     return e;

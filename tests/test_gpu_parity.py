@@ -1021,6 +1021,30 @@ def test_pair15_vs_oracle_and_chunking(pkg, oracle, torch_cuda, n, h, mode, T):
 
 
 @pytest.mark.parametrize("n,h", [(960, 240), (480, 120)])
+def test_pair15_spectral_gain(pkg, oracle, torch_cuda, n, h):
+    """K_pair15 applies a spectral gain per complex bin (the spectral hook): the
+    paired result equals the per-frame kernels' within float32 rounding on clean
+    streams, a flagged stream is recomputed whole per frame (bit-identical to
+    pairing off), and the result does not depend on the batch around a stream."""
+    torch = torch_cuda
+    T = 50_000
+    x = oracle.synth_streams(4, T, config_id=137)
+    x[2, 7_000] = 1e30
+    xd = dev(torch, x)
+    gain = (0.2 + np.abs(np.cos(np.arange(n // 2 + 1) * 0.021))).astype(np.float32)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_spectral_gain(gain)
+    y = host(plan.roundtrip(xd))
+    y_one = host(plan.roundtrip(xd[1:2].contiguous()))
+    plan.set_frame_pairing(False)
+    y_pf = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(y[1]), bits(y_one[0]))
+    assert np.array_equal(bits(y[2]), bits(y_pf[2]))
+    for s_ in (0, 1, 3):
+        assert_close(y[s_], y_pf[s_], float(np.max(np.abs(x[s_]))), f"stream {s_} paired vs per-frame")
+
+
+@pytest.mark.parametrize("n,h", [(960, 240), (480, 120)])
 def test_pair15_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda, n, h):
     """A stream with a sample outside the paired range (NaN, 1e30, 1e-35) is
     recomputed whole by the per-frame walker -- equal bit for bit to the plan with
