@@ -93,7 +93,9 @@ constexpr int kP15Waves = 5;  // the widest shape (support check)
 
 }  // namespace
 
-template <int L, int W, bool WREG, int WPE, bool HAS_GAIN = false>  // WREG: windows in registers (else LDS)
+// WREG: windows in registers (else LDS); DPRE: H <= 4 L and the plan has the
+// {den, 1/den} table (host-checked), divisors fetched ahead of the pushes
+template <int L, int W, bool WREG, int WPE, bool HAS_GAIN = false, bool DPRE = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE)))
 void k_pair15_hot(const FusedArgs a) {
     constexpr int E = kE, N = P15<L>::N, HALVES = 64 / L;
@@ -224,6 +226,36 @@ void k_pair15_hot(const FusedArgs a) {
         }
         dev::wave_lds_fence();
     };
+    // H <= 4 L (960/240, 480/120, every hop up to N/4): a block is at most 4 rows
+    // of the walk, so both blocks' {den, 1/den} pairs are fetched before the pushes.
+    // In the loop above every row's divisor load waits on vmcnt(0), which on gfx950
+    // also drains the previous rows' output stores: one store round trip per row.
+    constexpr int JD = 4;
+    auto den_fetch = [&](int k, float2 (&d)[JD]) {
+        const int dbase = (k % ring_blocks) * H;
+#pragma unroll
+        for (int i = 0; i < JD; ++i) {
+            const int j = hl + L * i;
+            d[i] = dr2[dbase + (j < H ? j : hl)];  // rows past H read a valid entry, unused
+        }
+    };
+    auto produce_pre = [&](int k, const float2 (&d)[JD]) {
+        const int base = k * H;
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int i = 0; i < JD; ++i) {
+            const int j = hl + L * i;
+            if (j < H) {
+                const int pos = (base + j) & RM;
+                const float v = ring[pos];
+                ring[pos] = 0.0f;
+                const float o = mk_div(v, d[i].x, d[i].y);
+                bad |= uint32_t(__builtin_amdgcn_frexp_expf(v) + 63) > 128u;  // exponent outside [-63, 65]
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (yo + base + j) * 4, 0, 0);
+            }
+        }
+        dev::wave_lds_fence();
+    };
 
     float fa[E], fb[E];
     load_frame(fa, fs * H - a.pad);
@@ -280,12 +312,30 @@ void k_pair15_hot(const FusedArgs a) {
                 }
             }
         }
-        push(p, k);
-        produce(k);
+        if constexpr (DPRE) {
+            // block k's divisors in flight during its push, block k+1's issued before
+            // block k's stores (waiting for them does not drain the stores); the sched
+            // barrier keeps d1's loads below the push (register pressure: 166-168
+            // VGPRs, no spill; at L = 32 every placement tried spilled 12-15)
+            static_assert(L == 64, "divisor prefetch: N = 960 walks only");
+            float2 d0[JD], d1[JD];
+            den_fetch(k, d0);
+            push(p, k);
+            __builtin_amdgcn_sched_barrier(0);
+            den_fetch(k + 1, d1);
+            produce_pre(k, d0);
 #pragma unroll
-        for (int m = 0; m < E; ++m) p[m] = v[m].y;
-        push(p, k + 1);
-        if (k + 1 < f1) produce(k + 1);
+            for (int m = 0; m < E; ++m) p[m] = v[m].y;
+            push(p, k + 1);
+            if (k + 1 < f1) produce_pre(k + 1, d1);
+        } else {
+            push(p, k);
+            produce(k);
+#pragma unroll
+            for (int m = 0; m < E; ++m) p[m] = v[m].y;
+            push(p, k + 1);
+            if (k + 1 < f1) produce(k + 1);
+        }
     }
     // flag bit h: the stream of half h redoes (a stream's bits depend on its samples only)
     const uint64_t bal = __builtin_amdgcn_ballot_w64(bad);
@@ -323,6 +373,13 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         ld_y >= (int64_t(1) << 27))
         return hipErrorInvalidValue;
     const int halves = g.n == 480 ? 2 : 1;
+    // N = 960, H <= 256: a block is at most 4 rows of the walk, its divisors are
+    // fetched ahead (CRLOT_P15_DPRE=0 keeps the row loop, A/B)
+    static const bool dpre_env = [] {
+        const char* e = std::getenv("CRLOT_P15_DPRE");
+        return !(e && e[0] == '0');
+    }();
+    const bool dpre = dpre_env && g.n == 960 && t.den_rden != nullptr && g.h <= 4 * 64;
     FusedArgs a;
     a.t = t;
     a.x = x;
@@ -366,8 +423,12 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         case 2: g.n == 960 ? go(k_pair15_hot<64, 4, false, 3>, 4) : go(k_pair15_hot<32, 4, false, 3>, 4); break;
         case 3: g.n == 960 ? go(k_pair15_hot<64, 2, false, 3>, 2) : go(k_pair15_hot<32, 2, false, 3>, 2); break;
         case 4:
-            if (t.gain)  // the spectral hook: 4 walks, the windows in LDS (the gain loads need the registers)
+            if (t.gain && dpre)  // the spectral hook: 4 walks, the windows in LDS (the gain loads need the registers)
+                go(k_pair15_hot<64, 4, false, 3, true, true>, 4);
+            else if (t.gain)
                 g.n == 960 ? go(k_pair15_hot<64, 4, false, 3, true>, 4) : go(k_pair15_hot<32, 4, false, 3, true>, 4);
+            else if (dpre)
+                go(k_pair15_hot<64, 4, true, 3, false, true>, 4);
             else
                 g.n == 960 ? go(k_pair15_hot<64, 4, true, 3>, 4) : go(k_pair15_hot<32, 4, true, 3>, 4);
             break;
