@@ -230,18 +230,35 @@ void k_pair15_hot(const FusedArgs a) {
     // of the walk, so both blocks' {den, 1/den} pairs are fetched before the pushes.
     // In the loop above every row's divisor load waits on vmcnt(0), which on gfx950
     // also drains the previous rows' output stores: one store round trip per row.
-    constexpr int JD = 4;
-    auto den_fetch = [&](int k, float2 (&d)[JD]) {
+    // At L = 32 the halves need the same divisors: half h fetches rows h and 2 + h
+    // (JF = 2 pairs per block), a permlane32 swap hands each half the other's rows.
+    constexpr int JD = 4, JF = L == 64 ? 4 : 2;
+    // buffer loads: the block's base in the scalar offset, rows as immediate
+    // offsets (no per-row 64-bit addresses); rows past the table read 0, unused
+    const __amdgpu_buffer_rsrc_t rden = dev::make_rsrc(dr2, uint32_t(ring_blocks * H) * 8u);
+    auto den_fetch = [&](int k, float2 (&d)[JF]) {
         const int dbase = (k % ring_blocks) * H;
 #pragma unroll
-        for (int i = 0; i < JD; ++i) {
-            const int j = hl + L * i;
-            d[i] = dr2[dbase + (j < H ? j : hl)];  // rows past H read a valid entry, unused
-        }
+        for (int q = 0; q < JF; ++q)
+            d[q] = dev::bload2(rden, (hl + L * (L == 64 ? q : 2 * q + half)) * 8, dbase * 8);
     };
-    auto produce_pre = [&](int k, const float2 (&d)[JD]) {
+    auto produce_pre = [&](int k, const float2 (&d)[JF]) {
         const int base = k * H;
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+        float2 dd[JD];
+        if constexpr (L == 64) {
+#pragma unroll
+            for (int i = 0; i < JD; ++i) dd[i] = d[i];
+        } else {
+#pragma unroll
+            for (int q = 0; q < JF; ++q) {  // lower half: row 2q -> a, upper half: row 2q+1 -> b
+                float ax = d[q].x, bx = d[q].x, ay = d[q].y, by = d[q].y;
+                dev::swap_f(ax, bx, true);
+                dev::swap_f(ay, by, true);
+                dd[2 * q] = float2{ax, ay};
+                dd[2 * q + 1] = float2{bx, by};
+            }
+        }
 #pragma unroll
         for (int i = 0; i < JD; ++i) {
             const int j = hl + L * i;
@@ -249,7 +266,7 @@ void k_pair15_hot(const FusedArgs a) {
                 const int pos = (base + j) & RM;
                 const float v = ring[pos];
                 ring[pos] = 0.0f;
-                const float o = mk_div(v, d[i].x, d[i].y);
+                const float o = mk_div(v, dd[i].x, dd[i].y);
                 bad |= uint32_t(__builtin_amdgcn_frexp_expf(v) + 63) > 128u;  // exponent outside [-63, 65]
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (yo + base + j) * 4, 0, 0);
             }
@@ -316,12 +333,12 @@ void k_pair15_hot(const FusedArgs a) {
             // block k's divisors in flight during its push, block k+1's issued before
             // block k's stores (waiting for them does not drain the stores); the sched
             // barrier keeps d1's loads below the push (register pressure: 166-168
-            // VGPRs, no spill; at L = 32 every placement tried spilled 12-15)
-            static_assert(L == 64, "divisor prefetch: N = 960 walks only");
-            float2 d0[JD], d1[JD];
-            den_fetch(k, d0);
+            // VGPRs at L = 64, no spill)
+            float2 d0[JF], d1[JF];
+            if constexpr (L == 64) den_fetch(k, d0);
             push(p, k);
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (L != 64) den_fetch(k, d0);  // L = 32: after the push (167 VGPRs before)
             den_fetch(k + 1, d1);
             produce_pre(k, d0);
 #pragma unroll
@@ -373,13 +390,13 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         ld_y >= (int64_t(1) << 27))
         return hipErrorInvalidValue;
     const int halves = g.n == 480 ? 2 : 1;
-    // N = 960, H <= 256: a block is at most 4 rows of the walk, its divisors are
-    // fetched ahead (CRLOT_P15_DPRE=0 keeps the row loop, A/B)
+    // H <= 4 L: a block is at most 4 rows of the walk, its divisors are fetched
+    // ahead (CRLOT_P15_DPRE=0 keeps the row loop, A/B)
     static const bool dpre_env = [] {
         const char* e = std::getenv("CRLOT_P15_DPRE");
         return !(e && e[0] == '0');
     }();
-    const bool dpre = dpre_env && g.n == 960 && t.den_rden != nullptr && g.h <= 4 * 64;
+    const bool dpre = dpre_env && t.den_rden != nullptr && g.h <= 4 * (g.n / 15);
     FusedArgs a;
     a.t = t;
     a.x = x;
@@ -424,11 +441,13 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
         case 3: g.n == 960 ? go(k_pair15_hot<64, 2, false, 3>, 2) : go(k_pair15_hot<32, 2, false, 3>, 2); break;
         case 4:
             if (t.gain && dpre)  // the spectral hook: 4 walks, the windows in LDS (the gain loads need the registers)
-                go(k_pair15_hot<64, 4, false, 3, true, true>, 4);
+                g.n == 960 ? go(k_pair15_hot<64, 4, false, 3, true, true>, 4)
+                           : go(k_pair15_hot<32, 4, false, 3, true, true>, 4);
             else if (t.gain)
                 g.n == 960 ? go(k_pair15_hot<64, 4, false, 3, true>, 4) : go(k_pair15_hot<32, 4, false, 3, true>, 4);
             else if (dpre)
-                go(k_pair15_hot<64, 4, true, 3, false, true>, 4);
+                g.n == 960 ? go(k_pair15_hot<64, 4, true, 3, false, true>, 4)
+                           : go(k_pair15_hot<32, 4, true, 3, false, true>, 4);
             else
                 g.n == 960 ? go(k_pair15_hot<64, 4, true, 3>, 4) : go(k_pair15_hot<32, 4, true, 3>, 4);
             break;
