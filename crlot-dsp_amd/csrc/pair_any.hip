@@ -206,36 +206,55 @@ void k_pair15_hot(const FusedArgs a) {
     // (frexp exponents in [-63, 65]; a walk with any other sum is flagged and its
     // stream redone by the per-frame walker), else the division itself.
     const float2* const dr2 = reinterpret_cast<const float2*>(a.t.den_rden);
+    // buffer loads of the {den, 1/den} pairs: the block's base in the scalar
+    // offset, rows as immediate offsets (no per-row 64-bit addresses); rows past
+    // the table read 0, unused
+    const __amdgpu_buffer_rsrc_t rden = dev::make_rsrc(dr2, uint32_t(ring_blocks * H) * 8u);
     auto produce = [&](int k) {
         const int base = k * H;
         const int dbase = (k % ring_blocks) * H;
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-        for (int j = hl; j < H; j += L) {
-            const int pos = (base + j) & RM;
-            const float v = ring[pos];
-            ring[pos] = 0.0f;
-            float o;
-            if (dr2) {
-                const float2 dr = dr2[dbase + j];
-                o = mk_div(v, dr.x, dr.y);
-                bad |= uint32_t(__builtin_amdgcn_frexp_expf(v) + 63) > 128u;  // exponent outside [-63, 65]
-            } else {
-                o = v / a.t.den[dbase + j];
+        if (dr2) {
+            // groups of 4 rows whose divisor loads issue together: a divisor load
+            // waits on every earlier store too (one vmcnt counter), so a block pays
+            // ceil(H / 4L) such waits instead of one per row
+            for (int j0 = hl; j0 < H; j0 += 4 * L) {
+                float2 d[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) d[i] = dev::bload2(rden, (j0 + L * i) * 8, dbase * 8);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int j = j0 + L * i;
+                    if (j < H) {
+                        const int pos = (base + j) & RM;
+                        const float v = ring[pos];
+                        ring[pos] = 0.0f;
+                        const float o = mk_div(v, d[i].x, d[i].y);
+                        bad |= uint32_t(__builtin_amdgcn_frexp_expf(v) + 63) > 128u;  // exponent outside [-63, 65]
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk,
+                                                              (yo + base + j) * 4, 0, 0);
+                    }
+                }
             }
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (yo + k * H + j) * 4, 0, 0);
+        } else {
+            for (int j = hl; j < H; j += L) {
+                const int pos = (base + j) & RM;
+                const float v = ring[pos];
+                ring[pos] = 0.0f;
+                const float o = v / a.t.den[dbase + j];
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (yo + base + j) * 4, 0, 0);
+            }
         }
         dev::wave_lds_fence();
     };
     // H <= 4 L (960/240, 480/120, every hop up to N/4): a block is at most 4 rows
     // of the walk, so both blocks' {den, 1/den} pairs are fetched before the pushes.
-    // In the loop above every row's divisor load waits on vmcnt(0), which on gfx950
-    // also drains the previous rows' output stores: one store round trip per row.
+    // The row loop this replaces waited on vmcnt(0) at every row's divisor load,
+    // which on gfx950 also drains the earlier rows' stores: one store round trip
+    // per row (produce above still pays one per group of 4 rows).
     // At L = 32 the halves need the same divisors: half h fetches rows h and 2 + h
     // (JF = 2 pairs per block), a permlane32 swap hands each half the other's rows.
     constexpr int JD = 4, JF = L == 64 ? 4 : 2;
-    // buffer loads: the block's base in the scalar offset, rows as immediate
-    // offsets (no per-row 64-bit addresses); rows past the table read 0, unused
-    const __amdgpu_buffer_rsrc_t rden = dev::make_rsrc(dr2, uint32_t(ring_blocks * H) * 8u);
     auto den_fetch = [&](int k, float2 (&d)[JF]) {
         const int dbase = (k % ring_blocks) * H;
 #pragma unroll
