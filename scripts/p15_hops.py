@@ -1,4 +1,5 @@
-"""K_pair15 round-trip throughput at several hops (1024 streams x 480 000)."""
+"""Round-trip throughput at several frame/hop shapes (1024 streams x 480 000;
+P15_SHAPES="N/H,..." overrides the K_pair15 default list)."""
 import json
 import os
 import sys
@@ -7,7 +8,8 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SHAPES = [(960, 240), (960, 480), (960, 320), (480, 120), (480, 240)]
+SHAPES = [tuple(int(v) for v in sh.split("/")) for sh in os.environ.get("P15_SHAPES", "").split(",") if sh] or \
+    [(960, 240), (960, 480), (960, 320), (480, 120), (480, 240)]
 
 
 def main():

@@ -8,7 +8,7 @@ rc=$?; tail -3 gpurun_out/p15_tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for lib in libcrlot_dsp_head.so crlot-dsp_amd/libcrlot_dsp.so; do
     echo "LIB=$lib" >> gpurun_out/p15_hops.log
-    CRLOT_LIB=$PWD/$lib timeout -k 10 120 python scripts/p15_hops.py >> gpurun_out/p15_hops.log 2>&1 || exit $?
+    P15_SHAPES=${P15_SHAPES:-} CRLOT_LIB=$PWD/$lib timeout -k 10 120 python scripts/p15_hops.py >> gpurun_out/p15_hops.log 2>&1 || exit $?
   done
 done
 cat gpurun_out/p15_hops.log
