@@ -511,8 +511,8 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world,
-            "devices": min(world, n_dev),
+            "n_gpus": min(world, n_dev),   # distinct devices (ranks may share one on a 1-GPU box)
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),

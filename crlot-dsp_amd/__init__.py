@@ -109,6 +109,7 @@ def lib():
         "crlot_output_length": ([vp, i64], i64),
         "crlot_workspace_bytes": ([vp, i32, i64], i64),
         "crlot_plan_reserve": ([vp, i64], C.c_int),
+        "crlot_plan_reserve_stream": ([vp, i32, i64, i32, vp], C.c_int),
         "crlot_roundtrip": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
         "crlot_roundtrip_stages": ([vp, vp, i32, i64, i64, vp, vp, vp], C.c_int),
         "crlot_ola_gather": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
@@ -313,6 +314,12 @@ class Plan:
 
     def reserve(self, nbytes: int):
         _check(lib().crlot_plan_reserve(self._h, nbytes))
+
+    def reserve_stream(self, n_streams: int, T: int, channels: int = 1, stream: int | None = None):
+        """Grow `stream`'s scratch slot (default: the current torch stream) for
+        round trips of this shape, so those launches never allocate."""
+        s = self._cur_stream() if stream is None else stream
+        _check(lib().crlot_plan_reserve_stream(self._h, n_streams, T, channels, s), "reserve_stream")
 
     def _cur_stream(self) -> int:
         torch = _torch()

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <xmmintrin.h>
 
+#include <mutex>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -22,6 +24,24 @@
 
 #include "crlot_dsp.h"
 #include "kernels.h"
+
+namespace crlot {
+// One stream's launch scratch.  Growth is stream-ordered (hipFreeAsync /
+// hipMallocAsync on the slot's stream): work already queued on that stream
+// keeps the old buffer, nothing waits for the device, and no other stream's
+// launches can see the buffer.
+struct Scratch {
+    hipStream_t s = nullptr;
+    uint64_t last_use = 0;
+    uint32_t* pflags = nullptr;  // K_pair per-walker regime flags (DevTables::pflags)
+    int64_t pflags_len = 0;
+    float* work = nullptr;       // staged path: [s][k][N] push_frame_AoS frames
+    int64_t work_bytes = 0;
+    float* planes = nullptr;     // crlot_roundtrip_interleaved: input planes, then output planes
+    int64_t planes_bytes = 0;
+};
+constexpr size_t kMaxScratchSlots = 16;
+}  // namespace crlot
 
 struct crlot_plan {
     crlot_plan_desc desc{};
@@ -43,8 +63,6 @@ struct crlot_plan {
     float* d_rden = nullptr;  // RN(1 / den) [ring], then {den, RN(1 / den)} pairs [ring][2]
     float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
     float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024: 64 lanes, N = 4096: 256)
-    uint32_t* d_pflags = nullptr;  // K_pair per-walker regime flags (DevTables::pflags)
-    int64_t pflags_len = 0;
     float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
@@ -54,12 +72,15 @@ struct crlot_plan {
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
     float* d_twany = nullptr; // per-pass twiddles of the mixed-radix path (aliases d_tw when generic)
     float* d_twany_own = nullptr;  // ... or its own table (power-of-two plans, any-shape streams)
-    // staged-path workspace
-    float* d_work = nullptr;
-    int64_t work_bytes = 0;
-    // channel planes of crlot_roundtrip_interleaved (input planes, then output planes)
-    float* d_planes = nullptr;
-    int64_t planes_bytes = 0;
+    // Launch scratch, one slot per HIP stream (crlot::Scratch): K_pair's regime
+    // flags, the staged path's frames and the interleaved path's channel planes.
+    // Calls on one stream are ordered by the stream; calls on different streams
+    // never share a slot, so one plan serves several streams at once.
+    std::mutex mu;  // guards the slots and the table state against concurrent host threads
+    std::vector<crlot::Scratch*> scratch;
+    uint64_t scratch_clock = 0;
+    // resident streaming objects on this plan: stopped before a table update
+    std::vector<crlot_stream_rt*> residents;
     // pinned staging of table uploads (stream-ordered: hipMemcpyAsync on the
     // caller's stream; the event guards the staging memory until the copies ran)
     char* h_stage = nullptr;
@@ -95,7 +116,7 @@ struct DeviceGuard {
     }
 };
 
-crlot::DevTables tables(const crlot_plan* p) {
+crlot::DevTables tables(const crlot_plan* p, const crlot::Scratch* sc = nullptr) {
     crlot::DevTables t;
     t.wa = p->d_wa;
     t.ws = p->d_ws;
@@ -120,8 +141,10 @@ crlot::DevTables tables(const crlot_plan* p) {
             t.ptw = p->d_ptw;
             t.pden = p->d_pden;
         }
-        t.pflags = p->d_pflags;
-        t.pflags_len = p->pflags_len;
+        if (sc) {
+            t.pflags = sc->pflags;
+            t.pflags_len = sc->pflags_len;
+        }
         t.hot = p->hot ? 1 : 0;
         t.px_lo = p->px_lo;
         // no transform can overflow: |x w| <= 2^64 / max gain, so |X| < 2^75, |ifft| < 2^86
@@ -130,13 +153,27 @@ crlot::DevTables tables(const crlot_plan* p) {
     return t;
 }
 
+// Release one slot's buffers.  The caller has drained the device (the slot's
+// stream may already be destroyed), so the frees are ordered on the null stream.
+void free_scratch(crlot::Scratch* sc) {
+    if (sc->pflags) (void)hipFreeAsync(sc->pflags, nullptr);
+    if (sc->work) (void)hipFreeAsync(sc->work, nullptr);
+    if (sc->planes) (void)hipFreeAsync(sc->planes, nullptr);
+    delete sc;
+}
+
 void free_plan(crlot_plan* p) {
     if (!p) return;
     DeviceGuard g(p->device);
-    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_work, p->d_planes, p->d_wsn,
+    if (!p->scratch.empty()) {
+        (void)hipDeviceSynchronize();
+        for (crlot::Scratch* sc : p->scratch) free_scratch(sc);
+        p->scratch.clear();
+        (void)hipStreamSynchronize(nullptr);
+    }
+    for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_wsn,
                      p->d_rden, p->d_twany_own, p->d_ptw, p->d_pden})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
-    if (p->d_pflags) (void)hipFree(p->d_pflags);
     if (p->stage_pending) (void)hipEventSynchronize(p->stage_ev);
     if (p->stage_ev) (void)hipEventDestroy(p->stage_ev);
     if (p->h_stage) (void)hipHostFree(p->h_stage);
@@ -190,6 +227,12 @@ class Upload {
     std::vector<char> data_;
 };
 
+// Defined with the resident streaming objects below: finish the hops every
+// resident kernel on the plan has been handed and stop it, so a table update
+// never lands under a running kernel (the next hop relaunches it behind the
+// update's copies).
+int stop_residents(crlot_plan* p);
+
 // Upload window-derived tables: analysis window, synthesis window, den, ordered
 // on `s` (kernels enqueued on `s` before this call still read the old tables).
 int upload_window_tables(crlot_plan* p, hipStream_t s) {
@@ -228,6 +271,8 @@ int upload_window_tables(crlot_plan* p, hipStream_t s) {
     }
     p->px_lo = wmin > 0.0 ? std::nextafter(float(double(1e-30f) / wmin * (1.0 + 0x1p-20)), INFINITY) : 0.0f;
     p->px_hi = float(0x1p64 / std::max(1.0, wmax));
+    const int rs = stop_residents(p);
+    if (rs != CRLOT_OK) return rs;
     p->table_gen += 1;
     Upload up(p);
     if (p->d_pden) {  // [block][lane][den SH | rden SH], den at block offset lane + lanes q
@@ -261,31 +306,65 @@ int upload_window_tables(crlot_plan* p, hipStream_t s) {
     return CRLOT_OK;
 }
 
-int ensure_workspace(crlot_plan* p, int64_t bytes) {
-    if (bytes <= p->work_bytes) return CRLOT_OK;
-    if (p->d_work) (void)hipFree(p->d_work);
-    p->d_work = nullptr;
-    p->work_bytes = 0;
-    hipError_t e = hipMalloc(&p->d_work, size_t(bytes));
-    if (e != hipSuccess) return fail(CRLOT_ENOMEM, "workspace hipMalloc failed");
-    p->work_bytes = bytes;
+// The scratch slot of stream `s` (caller holds p->mu).  A new stream takes a
+// fresh slot; past kMaxScratchSlots streams the least recently used slot is
+// recycled after draining the device (its stream may have work in flight).
+crlot::Scratch* scratch_slot(crlot_plan* p, hipStream_t s) {
+    const uint64_t now = ++p->scratch_clock;
+    for (crlot::Scratch* sc : p->scratch)
+        if (sc->s == s) {
+            sc->last_use = now;
+            return sc;
+        }
+    if (p->scratch.size() >= crlot::kMaxScratchSlots) {
+        size_t lru = 0;
+        for (size_t i = 1; i < p->scratch.size(); ++i)
+            if (p->scratch[i]->last_use < p->scratch[lru]->last_use) lru = i;
+        if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+        free_scratch(p->scratch[lru]);
+        p->scratch.erase(p->scratch.begin() + lru);
+    }
+    crlot::Scratch* sc = new crlot::Scratch();
+    sc->s = s;
+    sc->last_use = now;
+    p->scratch.push_back(sc);
+    return sc;
+}
+
+// Grow *buf to `bytes` in the order of stream s: the old buffer is released
+// behind the work already queued on s, the new one is valid for work queued
+// after this call.  No device-wide synchronisation.
+template <class T>
+int grow_on_stream(T** buf, int64_t* have, int64_t bytes, hipStream_t s, const char* what) {
+    if (bytes <= *have) return CRLOT_OK;
+    if (*buf) (void)hipFreeAsync(*buf, s);
+    *buf = nullptr;
+    *have = 0;
+    void* q = nullptr;
+    if (hipMallocAsync(&q, size_t(bytes), s) != hipSuccess)
+        return fail(CRLOT_ENOMEM, std::string(what) + " hipMallocAsync failed");
+    *buf = static_cast<T*>(q);
+    *have = bytes;
     return CRLOT_OK;
 }
 
-// K_pair's per-walker flags: at most one walker per frame and stream.  Grown
-// (never shrunk) on the calling thread before the launch that needs them.
-int ensure_pair_flags(crlot_plan* p, int32_t n_streams, int64_t F) {
-    if (!p->pairing || (p->geo.n != 480 && p->geo.n != 512 && p->geo.n != 960 && p->geo.n != 1024 &&
-                        p->geo.n != 2048 && p->geo.n != 4096)) return CRLOT_OK;
-    const int64_t need = int64_t(n_streams) * F;
-    if (need <= p->pflags_len) return CRLOT_OK;
-    if (p->d_pflags) (void)hipFree(p->d_pflags);
-    p->d_pflags = nullptr;
-    p->pflags_len = 0;
-    hipError_t e = hipMalloc(&p->d_pflags, sizeof(uint32_t) * size_t(need));
-    if (e != hipSuccess) return fail(CRLOT_ENOMEM, "pair flag hipMalloc failed");
-    p->pflags_len = need;
-    return CRLOT_OK;
+int ensure_workspace(crlot::Scratch* sc, int64_t bytes) {
+    return grow_on_stream(&sc->work, &sc->work_bytes, bytes, sc->s, "workspace");
+}
+
+bool pair_plan(const crlot_plan* p) {
+    return p->pairing && (p->geo.n == 480 || p->geo.n == 512 || p->geo.n == 960 || p->geo.n == 1024 ||
+                          p->geo.n == 2048 || p->geo.n == 4096);
+}
+
+// K_pair's per-walker flags: at most one walker per frame and stream.
+int ensure_pair_flags(const crlot_plan* p, crlot::Scratch* sc, int32_t n_streams, int64_t F) {
+    if (!pair_plan(p)) return CRLOT_OK;
+    int64_t have = sc->pflags_len * int64_t(sizeof(uint32_t));
+    const int rc = grow_on_stream(&sc->pflags, &have, int64_t(n_streams) * F * int64_t(sizeof(uint32_t)), sc->s,
+                                  "pair flag");
+    sc->pflags_len = have / int64_t(sizeof(uint32_t));
+    return rc;
 }
 
 int64_t frames_for(const crlot_plan* p, int64_t T) {
@@ -443,6 +522,7 @@ void crlot_plan_destroy(crlot_plan* plan) { free_plan(plan); }
 int crlot_plan_upload_tables_async(crlot_plan* p, const float* window, const float* norm, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     DeviceGuard g(p->device);
+    std::lock_guard<std::mutex> lk(p->mu);
     if (window) std::memcpy(p->window.data(), window, sizeof(float) * p->window.size());
     if (norm) {
         std::memcpy(p->norm.data(), norm, sizeof(float) * p->norm.size());
@@ -473,6 +553,9 @@ int crlot_plan_upload_tables(crlot_plan* p, const float* window, const float* no
 int crlot_plan_set_spectral_gain_async(crlot_plan* p, const float* gain, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     DeviceGuard g(p->device);
+    std::lock_guard<std::mutex> lk(p->mu);
+    const int rs = stop_residents(p);
+    if (rs != CRLOT_OK) return rs;
     p->table_gen += 1;
     if (!gain) {
         p->has_gain = false;
@@ -501,6 +584,7 @@ int crlot_plan_set_spectral_gain(crlot_plan* p, const float* gain) {
 int crlot_plan_set_frame_pairing(crlot_plan* p, int32_t enable) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (enable < 0 || enable > 2) return fail(CRLOT_EINVAL, "frame pairing mode is 0, 1 or 2");
+    std::lock_guard<std::mutex> lk(p->mu);
     p->pairing = enable != 0;
     p->hot = enable != 2;
     return CRLOT_OK;
@@ -550,28 +634,59 @@ int64_t crlot_workspace_bytes(const crlot_plan* p, int32_t n_streams, int64_t T)
 int crlot_plan_reserve(crlot_plan* p, int64_t bytes) {
     if (!p || bytes < 0) return fail(CRLOT_EINVAL, "bad argument");
     DeviceGuard g(p->device);
-    return ensure_workspace(p, bytes);
+    std::lock_guard<std::mutex> lk(p->mu);
+    crlot::Scratch* sc = scratch_slot(p, nullptr);
+    if (!sc) return fail(CRLOT_EHIP, "scratch slot");
+    const int rc = ensure_workspace(sc, bytes);
+    if (rc != CRLOT_OK) return rc;
+    const hipError_t e = hipStreamSynchronize(nullptr);
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "workspace reserve");
 }
 
-int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_streams, int64_t T,
-                    int64_t ld_x, int64_t ld_y, void* stream) {
-    if (!p) return fail(CRLOT_EINVAL, "null plan");
-    if (n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "negative size");
-    const int64_t F = frames_for(p, T);
-    // nothing to emit (n_streams == 0, T == 0, or DROP with T < N: the Framer never yields)
-    if (n_streams == 0 || F == 0) return CRLOT_OK;
-    if ((!d_x && T > 0) || !d_y) return fail(CRLOT_EINVAL, "null buffer");
-    const int64_t out_len = F * p->geo.h;
-    if (ld_x < T || ld_y < out_len) return fail(CRLOT_EINVAL, "leading dimension too small");
+// The scratch a round trip of this shape takes (aligned rows, ld = T / F*H).
+static void scratch_need(const crlot_plan* p, int32_t n_streams, int64_t T, int32_t channels, int64_t* flags,
+                         int64_t* work, int64_t* planes) {
+    const int64_t F = frames_for(p, T), S = int64_t(n_streams) * channels, L = F * p->geo.h;
+    *flags = pair_plan(p) ? S * F : 0;
+    const bool direct_ilv = channels > 1 && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0;
+    *planes = (channels > 1 && !direct_ilv) ? S * (T + L) * int64_t(sizeof(float)) : 0;
+    static const float probe[2] = {0.f, 0.f};
+    const bool fused = use_fused(p, probe, const_cast<float*>(probe), T + (T & 1), L + (L & 1), int32_t(S), T, L);
+    const bool any = p->generic && crlot::fused_any_fits(p->geo.n, p->geo.h);
+    *work = (fused || any) ? 0 : S * F * p->geo.n * int64_t(sizeof(float));
+}
+
+int crlot_plan_reserve_stream(crlot_plan* p, int32_t n_streams, int64_t T, int32_t channels, void* stream) {
+    if (!p || n_streams < 0 || T < 0 || channels <= 0 || channels > 64) return fail(CRLOT_EINVAL, "bad argument");
     DeviceGuard g(p->device);
+    std::lock_guard<std::mutex> lk(p->mu);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    crlot::Scratch* sc = scratch_slot(p, s);
+    if (!sc) return fail(CRLOT_EHIP, "scratch slot");
+    int64_t flags = 0, work = 0, planes = 0;
+    scratch_need(p, n_streams, T, channels, &flags, &work, &planes);
+    int rc = CRLOT_OK;
+    if (flags > sc->pflags_len) {
+        int64_t have = sc->pflags_len * int64_t(sizeof(uint32_t));
+        rc = grow_on_stream(&sc->pflags, &have, flags * int64_t(sizeof(uint32_t)), s, "pair flag");
+        sc->pflags_len = have / int64_t(sizeof(uint32_t));
+    }
+    if (rc == CRLOT_OK) rc = ensure_workspace(sc, work);
+    if (rc == CRLOT_OK) rc = grow_on_stream(&sc->planes, &sc->planes_bytes, planes, s, "channel-plane workspace");
+    return rc;
+}
+
+static int roundtrip_impl(crlot_plan* p, crlot::Scratch* sc, const float* d_x, float* d_y, int32_t n_streams,
+                          int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, hipStream_t s) {
+    const int64_t out_len = F * p->geo.h;
     hipError_t e;
-    if (use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len)) {
-        const int rcf = ensure_pair_flags(p, n_streams, F);
+    const bool fused = use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len);
+    if (fused) {
+        const int rcf = ensure_pair_flags(p, sc, n_streams, F);
         if (rcf != CRLOT_OK) return rcf;
     }
-    const crlot::DevTables t = tables(p);
-    if (use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len)) {
+    const crlot::DevTables t = tables(p, sc);
+    if (fused) {
         e = !crlot::fused_wg_supported(p->geo.n, p->geo.h)
                 ? crlot::launch_fused(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s)
                 : crlot::launch_fused_wg(p->geo, t, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, s);
@@ -584,9 +699,9 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
         if (p->pairing && t.ptw && p->geo.pad_mode == 0 &&
             crlot::pair15_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < lim && out_len < lim &&
             ld_x < lim && ld_y < lim) {
-            const int rcf = ensure_pair_flags(p, n_streams, F);
+            const int rcf = ensure_pair_flags(p, sc, n_streams, F);
             if (rcf != CRLOT_OK) return rcf;
-            const crlot::DevTables tp = tables(p);
+            const crlot::DevTables tp = tables(p, sc);
             int nch = 0, per = 1;
             e = crlot::launch_pair15(p->geo, tp, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, &nch, &per, s);
             if (e != hipSuccess) return hip_fail(e, "pair (N = 15 L) kernel launch");
@@ -600,17 +715,34 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
         return CRLOT_OK;
     }
     const int64_t need = int64_t(n_streams) * F * p->geo.n * int64_t(sizeof(float));
-    int rc = ensure_workspace(p, need);
+    int rc = ensure_workspace(sc, need);
     if (rc != CRLOT_OK) return rc;
     e = p->generic ? crlot::launch_synth_any(p->geo, t, p->d_twany, d_x, n_streams, T, ld_x, F,
-                                             p->d_work, nullptr, s)
-                   : crlot::launch_synth_frames(p->geo, t, d_x, n_streams, T, ld_x, F, p->d_work,
+                                             sc->work, nullptr, s)
+                   : crlot::launch_synth_frames(p->geo, t, d_x, n_streams, T, ld_x, F, sc->work,
                                                 nullptr, s);
     if (e != hipSuccess) return hip_fail(e, "synth kernel launch");
-    e = crlot::launch_ola_gather(p->geo, t, p->d_work, p->geo.n, d_y, n_streams, F, ld_y,
+    e = crlot::launch_ola_gather(p->geo, t, sc->work, p->geo.n, d_y, n_streams, F, ld_y,
                                  out_len, s);
     if (e != hipSuccess) return hip_fail(e, "gather kernel launch");
     return CRLOT_OK;
+}
+
+int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_streams, int64_t T,
+                    int64_t ld_x, int64_t ld_y, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "negative size");
+    const int64_t F = frames_for(p, T);
+    // nothing to emit (n_streams == 0, T == 0, or DROP with T < N: the Framer never yields)
+    if (n_streams == 0 || F == 0) return CRLOT_OK;
+    if ((!d_x && T > 0) || !d_y) return fail(CRLOT_EINVAL, "null buffer");
+    if (ld_x < T || ld_y < F * p->geo.h) return fail(CRLOT_EINVAL, "leading dimension too small");
+    DeviceGuard g(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(p->mu);
+    crlot::Scratch* sc = scratch_slot(p, s);
+    if (!sc) return fail(CRLOT_EHIP, "scratch slot");
+    return roundtrip_impl(p, sc, d_x, d_y, n_streams, T, ld_x, ld_y, F, s);
 }
 
 int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int32_t n_groups,
@@ -625,6 +757,9 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
     if (int64_t(n_groups) * C > INT32_MAX) return fail(CRLOT_EINVAL, "too many streams");
     DeviceGuard g(p->device);
     hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(p->mu);
+    crlot::Scratch* sc = scratch_slot(p, s);
+    if (!sc) return fail(CRLOT_EHIP, "scratch slot");
     hipError_t e;
     // K_pair plans (N = 1024, zero padding) walk the interleaved rows of up to 5
     // channels directly: one pass over HBM, bit-identical to the per-channel
@@ -639,26 +774,21 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
     }();
     if (!three_pass && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0 && aligned4(d_x) &&
         aligned4(d_y)) {
-        const int rcf = ensure_pair_flags(p, int32_t(n_groups * C), F);
+        const int rcf = ensure_pair_flags(p, sc, int32_t(n_groups * C), F);
         if (rcf != CRLOT_OK) return rcf;
-        e = crlot::launch_pair_interleaved(p->geo, tables(p), d_x, d_y, n_groups, channels, T, ld_x, ld_y, F, L, s);
+        e = crlot::launch_pair_interleaved(p->geo, tables(p, sc), d_x, d_y, n_groups, channels, T, ld_x, ld_y, F,
+                                           L, s);
         if (e == hipSuccess) return CRLOT_OK;
         if (e != hipErrorNotSupported && e != hipErrorInvalidValue) return hip_fail(e, "interleaved pair kernel launch");
     }
     const int64_t need = int64_t(n_groups) * C * (T + L) * int64_t(sizeof(float));
-    if (need > p->planes_bytes) {
-        if (p->d_planes) (void)hipFree(p->d_planes);
-        p->d_planes = nullptr;
-        p->planes_bytes = 0;
-        if (hipMalloc(&p->d_planes, size_t(need)) != hipSuccess)
-            return fail(CRLOT_ENOMEM, "channel-plane workspace hipMalloc failed");
-        p->planes_bytes = need;
-    }
-    float* xin = p->d_planes;
-    float* yout = p->d_planes + int64_t(n_groups) * C * T;
+    int rc = grow_on_stream(&sc->planes, &sc->planes_bytes, need, s, "channel-plane workspace");
+    if (rc != CRLOT_OK) return rc;
+    float* xin = sc->planes;
+    float* yout = sc->planes + int64_t(n_groups) * C * T;
     e = crlot::launch_deinterleave(d_x, ld_x, xin, n_groups, T, channels, s);
     if (e != hipSuccess) return hip_fail(e, "deinterleave kernel launch");
-    const int rc = crlot_roundtrip(p, xin, yout, int32_t(n_groups * C), T, T, L, stream);
+    rc = roundtrip_impl(p, sc, xin, yout, int32_t(n_groups * C), T, T, L, F, s);
     if (rc != CRLOT_OK) return rc;
     e = crlot::launch_interleave(yout, L, d_y, ld_y, n_groups, channels, s);
     if (e != hipSuccess) return hip_fail(e, "interleave kernel launch");
@@ -1031,7 +1161,11 @@ int rt_launch(crlot_stream_rt* st) {
     a.gain = p->geo.gain;
     a.idle_ticks = st->idle_ticks;
     __atomic_store_n(&st->ctl->stop, 0, __ATOMIC_RELEASE);
-    hipError_t e = crlot::launch_stream_rt(p->geo, a, st->s);
+    hipError_t e = hipSuccess;
+    // the kernel stages the tables at launch: order it behind a pending table copy
+    // (an _async update queued on another stream)
+    if (p->stage_pending) e = hipStreamWaitEvent(st->s, p->stage_ev, 0);
+    if (e == hipSuccess) e = crlot::launch_stream_rt(p->geo, a, st->s);
     if (e == hipSuccess) e = hipEventRecord(st->ev, st->s);
     if (e != hipSuccess) return hip_fail(e, "resident stream kernel launch");
     st->launched = true;
@@ -1073,6 +1207,16 @@ int rt_wait_done(crlot_stream_rt* st, uint64_t hops) {
         }
         __builtin_ia32_pause();
     }
+}
+
+int stop_residents(crlot_plan* p) {
+    for (crlot_stream_rt* st : p->residents) {
+        if (!st->launched && st->q == 0) continue;
+        int rc = st->q ? rt_wait_done(st, st->q) : CRLOT_OK;  // hops already handed over see the old tables
+        if (rc == CRLOT_OK) rc = rt_stop(st);
+        if (rc != CRLOT_OK) return rc;
+    }
+    return CRLOT_OK;
 }
 
 }  // namespace
@@ -1123,6 +1267,10 @@ int crlot_stream_rt_create(crlot_plan* p, int32_t channels, int32_t interleaved,
     std::memset(static_cast<void*>(st->ctl), 0, sizeof(crlot::RtCtl));
     std::memset(st->in_ring, 0, ring);
     std::memset(st->out_ring, 0, ring);
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        p->residents.push_back(st);
+    }
     *out = st;
     return CRLOT_OK;
 }
@@ -1130,6 +1278,11 @@ int crlot_stream_rt_create(crlot_plan* p, int32_t channels, int32_t interleaved,
 void crlot_stream_rt_destroy(crlot_stream_rt* st) {
     if (!st) return;
     DeviceGuard g(st->plan->device);
+    {
+        std::lock_guard<std::mutex> lk(st->plan->mu);
+        auto& v = st->plan->residents;
+        v.erase(std::remove(v.begin(), v.end(), st), v.end());
+    }
     if (st->ctl) (void)rt_stop(st);
     if (st->d_state) (void)hipFree(st->d_state);
     if (st->in_ring) (void)hipHostFree(st->in_ring);
@@ -1155,6 +1308,7 @@ int crlot_stream_rt_reset(crlot_stream_rt* st) {
 
 float* crlot_stream_rt_input_slot(crlot_stream_rt* st) {
     if (!st) return nullptr;
+    DeviceGuard g(st->plan->device);
     // the slot of hop q is free once hop q - depth has completed
     if (st->q >= uint64_t(st->depth) && rt_wait_done(st, st->q - st->depth + 1) != CRLOT_OK) return nullptr;
     const size_t hop = size_t(st->channels) * size_t(st->plan->geo.h);
@@ -1169,10 +1323,8 @@ int crlot_stream_rt_submit(crlot_stream_rt* st, int64_t* hop_index) {
         if (rc != CRLOT_OK) return rc;
     }
     if (st->launched && st->gen != st->plan->table_gen) {  // tables changed: re-stage them
-        int rc = rt_stop(st);
+        int rc = rt_stop(st);  // (the update stopped it already; rt_launch orders the relaunch behind the copies)
         if (rc != CRLOT_OK) return rc;
-        hipError_t e = hipDeviceSynchronize();  // the table copies, on whatever stream
-        if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
     }
     __atomic_store_n(&st->ctl->seq, st->q + 1, __ATOMIC_RELEASE);
     if (hop_index) *hop_index = int64_t(st->q);

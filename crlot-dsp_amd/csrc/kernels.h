@@ -152,7 +152,8 @@ constexpr int kRtMaxChannels = 1024;
 constexpr int kRtMaxWg = kRtMaxChannels / 4;
 struct alignas(64) RtCtl {
     uint64_t seq;             // hops submitted (host, release)
-    uint64_t stop;            // nonzero: every workgroup exits at its next poll
+    uint64_t stop;            // nonzero: every workgroup exits at its next poll (host: 1 =
+                              // stop; device: 2 = a workgroup's idle timer expired)
     uint64_t pad0[6];
     uint64_t done[kRtMaxWg];  // hops completed per workgroup (device, release)
     uint64_t ticks[kRtMaxWg]; // s_memrealtime ticks (100 MHz) of the last hop per workgroup

@@ -143,7 +143,14 @@ __global__ __launch_bounds__(kRtBlock) void k_stream_rt(const RtArgs a) {
                     break;
                 }
                 if (ld_sys64(&ctl->stop) != 0) break;
-                if (wall_clock64() - t_last > a.idle_ticks) break;
+                if (wall_clock64() - t_last > a.idle_ticks) {
+                    // idle exit, decided once for the whole grid: stop = 2 makes every
+                    // other workgroup leave at its next poll too, so the kernel is gone
+                    // (and the host relaunches it for the next doorbell) instead of
+                    // some workgroups serving hops while others wait out their own timers
+                    __hip_atomic_store(&ctl->stop, uint64_t(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
             cmd[my & 1] = k;

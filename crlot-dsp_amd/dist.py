@@ -32,12 +32,20 @@ def device_for(local_rank: int, n_devices: int) -> int:
     return local_rank % max(1, n_devices)
 
 
+def init_kwargs(backend: str, device=None) -> dict:
+    """init_process_group keywords: RCCL binds the rank's device eagerly
+    (device_id), gloo takes none."""
+    if backend not in ("nccl", "gloo"):
+        raise ValueError(f"backend must be 'nccl' (RCCL) or 'gloo', got {backend!r}")
+    return {"device_id": device} if (backend == "nccl" and device is not None) else {}
+
+
 def init(backend: str, device=None):
     global _backend
     import torch.distributed as dist
     rank, world, _ = env_rank_world()
+    kw = init_kwargs(backend, device)
     if world > 1 and not dist.is_initialized():
-        kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
         dist.init_process_group(backend, **kw)
     _backend = backend
     return rank, world
@@ -56,13 +64,18 @@ def barrier():
         dist.barrier()
 
 
+def reduce_device(device=None):
+    """Where the timing reduction's tensor lives: on the rank's GPU under RCCL
+    (which reduces device memory only), on the host under gloo."""
+    return device if (_backend == "nccl" and device is not None) else "cpu"
+
+
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
     if not (dist.is_initialized() and dist.get_world_size() > 1):
         return float(value)
-    on_dev = _backend == "nccl" and device is not None
-    t = torch.tensor([value], dtype=torch.float64, device=device if on_dev else "cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=reduce_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

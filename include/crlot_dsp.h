@@ -19,8 +19,15 @@
  * passed as void* (NULL = default stream).  Every entry returns 0 on success or
  * a negative CRLOT_E* code; crlot_last_error() gives the message of the last
  * failure on the calling thread.  Nothing throws across this boundary.
- * A plan is not thread-safe (like KissFftPlan, whose scratch makes it
- * non-reentrant: kissfft_adapter.cc:256-263); use one plan per host thread.
+ * Streams and threads: a plan may serve several HIP streams at once.  Its
+ * launch scratch (K_pair's regime flags, the staged path's frame workspace, the
+ * interleaved path's channel planes) is kept per stream handle, so round trips
+ * issued on different streams never share device scratch, and growth is
+ * stream-ordered (hipMallocAsync / hipFreeAsync on the calling stream: no
+ * device-wide synchronisation).  Host-side entry points take the plan's lock,
+ * so several host threads may also share a plan (the reference's KissFftPlan
+ * is non-reentrant: kissfft_adapter.cc:256-263).  Streaming objects
+ * (crlot_stream*, crlot_stream_rt*, crlot_ola*) are single-owner objects.
  */
 #ifndef CRLOT_DSP_H_
 #define CRLOT_DSP_H_
@@ -131,9 +138,15 @@ int64_t crlot_frame_count(const crlot_plan* plan, int64_t T);
 /* Samples the streaming-interleaved round trip emits: F*H */
 int64_t crlot_output_length(const crlot_plan* plan, int64_t T);
 /* Device workspace a non-fast-path crlot_roundtrip needs (bytes); reserve it
- * up front so the launch itself never allocates (graph capture). */
+ * up front so the launch itself never allocates (graph capture).
+ * crlot_plan_reserve grows the default (NULL) stream's slot and waits for it;
+ * crlot_plan_reserve_stream grows `stream`'s slot (regime flags, frame
+ * workspace, channel planes) for round trips of n_streams groups of `channels`
+ * channels (1 = crlot_roundtrip) of T samples, stream-ordered. */
 int64_t crlot_workspace_bytes(const crlot_plan* plan, int32_t n_streams, int64_t T);
 int crlot_plan_reserve(crlot_plan* plan, int64_t bytes);
+int crlot_plan_reserve_stream(crlot_plan* plan, int32_t n_streams, int64_t T, int32_t channels,
+                              void* stream);
 
 /* ---------------------------------------------------------------- hot path */
 /* The round trip for n_streams independent mono streams: stream s reads

@@ -74,3 +74,50 @@ def test_stream_range_partitions():
             ranges = [D.stream_range(total, world, r) for r in range(world)]
             assert ranges[0][0] == 0 and ranges[-1][1] == total
             assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+
+
+def _load_dist():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("crlot_dist_t", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+    D = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(D)
+    return D
+
+
+def test_nccl_init_arguments_and_reduce_device(monkeypatch):
+    """The RCCL control-plane path without RCCL: init("nccl", dev) hands the rank's
+    device to init_process_group (device_id), gloo hands nothing; the max-over-ranks
+    reduction runs on the device under nccl and on the host under gloo; a
+    single-rank job never initialises a process group."""
+    import torch
+    import torch.distributed as dist
+    D = _load_dist()
+    calls = []
+    monkeypatch.setattr(dist, "is_initialized", lambda: bool(calls))
+    monkeypatch.setattr(dist, "init_process_group", lambda backend, **kw: calls.append((backend, kw)))
+    dev = torch.device("cuda", 3)
+    assert D.init_kwargs("nccl", dev) == {"device_id": dev}
+    assert D.init_kwargs("nccl", None) == {}
+    assert D.init_kwargs("gloo", dev) == {}
+    try:
+        D.init_kwargs("mpi", dev)
+        raise AssertionError("unknown backend accepted")
+    except ValueError:
+        pass
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+    assert D.init("nccl", dev) == (0, 1) and calls == []
+    assert D.reduce_device(dev) == dev  # backend recorded even for one rank
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("RANK", "5")
+    assert D.init("nccl", dev) == (5, 8)
+    assert calls == [("nccl", {"device_id": dev})]
+    assert D.reduce_device(dev) == dev and D.reduce_device(None) == "cpu"
+    D.init("gloo", dev)  # already initialised: no second group
+    assert len(calls) == 1 and D.reduce_device(dev) == "cpu"
+    # max_over_ranks: the all_reduce sees a tensor on the chosen device
+    seen = []
+    monkeypatch.setattr(dist, "get_world_size", lambda: 8)
+    monkeypatch.setattr(dist, "all_reduce", lambda t, op=None: seen.append((t.device.type, op)))
+    assert D.max_over_ranks(1.5, None) == 1.5
+    assert seen == [("cpu", dist.ReduceOp.MAX)]
