@@ -32,7 +32,7 @@ PAD_CONSTANT, PAD_REFLECT, PAD_EDGE = 0, 1, 2
 # dsp::fft::FftDomain
 FFT_REAL, FFT_COMPLEX = 0, 1
 
-OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ERUNTIME = 0, -1, -2, -3, -4, -5
+OK, EINVAL, EUNSUPPORTED, EHIP, ENOMEM, ERUNTIME, ERANGE = 0, -1, -2, -3, -4, -5, -6
 
 
 class PlanDesc(C.Structure):
@@ -109,7 +109,6 @@ def lib():
         "crlot_output_length": ([vp, i64], i64),
         "crlot_workspace_bytes": ([vp, i32, i64], i64),
         "crlot_plan_reserve": ([vp, i64], C.c_int),
-        "crlot_plan_reserve_stream": ([vp, i32, i64, i32, vp], C.c_int),
         "crlot_roundtrip": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
         "crlot_roundtrip_stages": ([vp, vp, i32, i64, i64, vp, vp, vp], C.c_int),
         "crlot_ola_gather": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
@@ -172,6 +171,26 @@ def lib():
         "crlot_ola_meter_peak": ([vp, C.POINTER(f32)], C.c_int),
         "crlot_ola_norm_table": ([vp, fp], C.c_int),
         "crlot_ola_synchronize": ([vp], C.c_int),
+        "crlot_fft_forward_host": ([vp, vp, vp, i32, i64, i64, i64, i64], C.c_int),
+        "crlot_fft_inverse_host": ([vp, vp, vp, i32, i64, i64, i64, i64], C.c_int),
+        "crlot_fft_forward_complex_host": ([vp, vp, vp, i32, i64, i64, i64, i64], C.c_int),
+        "crlot_fft_inverse_complex_host": ([vp, vp, vp, i32, i64, i64, i64, i64], C.c_int),
+        "crlot_axpy": ([vp, vp, f32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_axpy_windowed": ([vp, vp, vp, f32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_normalize_and_clear": ([vp, vp, vp, f32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_call_axpy": ([vp, vp, f32, i64], C.c_int),
+        "crlot_call_axpy_windowed": ([vp, vp, vp, f32, i64], C.c_int),
+        "crlot_call_normalize_and_clear": ([vp, vp, vp, f32, i64], C.c_int),
+        "crlot_framequeue_count": ([i64, i64, i64, i32], i64),
+        "crlot_framequeue_frames": ([vp, i32, i64, i64, i64, i64, i32, i32, vp, vp], C.c_int),
+        "crlot_framequeue_create": ([vp, i64, i64, i64, i32, i32, i32, C.POINTER(vp)], C.c_int),
+        "crlot_framequeue_destroy": ([vp], None),
+        "crlot_framequeue_info": ([vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
+        "crlot_framequeue_frame": ([vp, i64], vp),
+        "crlot_framequeue_copy_frame": ([vp, i64, vp], C.c_int),
+        "crlot_framequeue_all_frames": ([vp], vp),
+        "crlot_framequeue_device_frames": ([vp], vp),
+        "crlot_plan_reserve_stream": ([vp, i32, i64, i32, vp], C.c_int),
         "crlot_window_table": ([i32, i64, i32, i32, fp], C.c_int),
         "crlot_ring_len": ([i64, i64], i64),
         "crlot_norm_table": ([fp, i64, i64, i64, i32, f32, fp], C.c_int),
@@ -195,6 +214,8 @@ def _check(rc: int, what: str = "") -> int:
         raise NotImplementedError(msg)
     if rc == ENOMEM:
         raise MemoryError(msg)
+    if rc == ERANGE:
+        raise IndexError(msg)
     raise RuntimeError(msg)
 
 
@@ -505,6 +526,172 @@ class FftPlan:
     def inverse_complex(self, Z):
         """(B, nfft) complex64 -> (B, nfft) complex64, *1/nfft, sanitize."""
         return self._cplx(lib().crlot_fft_inverse_complex, "inverse_complex", Z)
+
+    # -- host-pointer forms (numpy in/out; the reference's calling convention,
+    #    served by the plan's resident call kernel)
+    def forward_host(self, x, out=None, inc_in: int = 1, inc_out: int = 1):
+        """x: (B, nfft*inc_in) float32 numpy -> (B, (nfft/2+1)*inc_out) complex64."""
+        x = np.ascontiguousarray(x, np.float32)
+        x2 = x.reshape(-1, x.shape[-1])
+        B = x2.shape[0]
+        bins = self.nfft // 2 + 1
+        if out is None:
+            out = np.zeros((B, bins * inc_out), np.complex64)
+        _check(lib().crlot_fft_forward_host(self._h, x2.ctypes.data, out.ctypes.data, B, x2.shape[1], inc_in,
+                                            2 * out.shape[1], inc_out), "forward_host")
+        return out
+
+    def inverse_host(self, X, out=None, inc_in: int = 1, inc_out: int = 1):
+        """X: (B, (nfft/2+1)*inc_in) complex64 numpy -> (B, nfft*inc_out) float32."""
+        X = np.ascontiguousarray(X, np.complex64)
+        X2 = X.reshape(-1, X.shape[-1])
+        B = X2.shape[0]
+        if out is None:
+            out = np.zeros((B, self.nfft * inc_out), np.float32)
+        _check(lib().crlot_fft_inverse_host(self._h, X2.ctypes.data, out.ctypes.data, B, 2 * X2.shape[1], inc_in,
+                                            out.shape[1], inc_out), "inverse_host")
+        return out
+
+    def _cplx_host(self, fn, name, Z):
+        Z = np.ascontiguousarray(Z, np.complex64)
+        Z2 = Z.reshape(-1, Z.shape[-1])
+        out = np.zeros_like(Z2)
+        _check(fn(self._h, Z2.ctypes.data, out.ctypes.data, Z2.shape[0], 2 * Z2.shape[1], 1, 2 * Z2.shape[1], 1),
+               name)
+        return out
+
+    def forward_complex_host(self, Z):
+        return self._cplx_host(lib().crlot_fft_forward_complex_host, "forward_complex_host", Z)
+
+    def inverse_complex_host(self, Z):
+        return self._cplx_host(lib().crlot_fft_inverse_complex_host, "inverse_complex_host", Z)
+
+
+# ----------------------------------------------------------------- OLA kernels (free functions)
+def axpy(dst, src, g: float, win=None, stream: int | None = None):
+    """dsp::axpy / axpy_windowed on device tensors: dst (B, n) += (src (B, n) [* win (n)]) * g,
+    per element fma(src, g, dst) / fma(fma(src, win, 0), g, dst) (kernels.cc:18-28)."""
+    d2 = dst if dst.dim() == 2 else dst[None]
+    s2 = src if src.dim() == 2 else src[None]
+    B, n = d2.shape
+    if d2.stride(1) != 1 or s2.stride(1) != 1 or s2.shape != d2.shape:
+        raise ValueError("dst / src must be (B, n) with contiguous rows")
+    s = _stream_handle(dst) if stream is None else stream
+    if win is None:
+        _check(lib().crlot_axpy(d2.data_ptr(), s2.data_ptr(), g, n, B, _ld(d2, 0, n), _ld(s2, 0, n), s), "axpy")
+    else:
+        _check(lib().crlot_axpy_windowed(d2.data_ptr(), s2.data_ptr(), win.data_ptr(), g, n, B, _ld(d2, 0, n),
+                                         _ld(s2, 0, n), s), "axpy_windowed")
+    return dst
+
+
+def normalize_and_clear(out, acc, norm, eps: float, stream: int | None = None):
+    """dsp::normalize_and_clear on device tensors: out (B, n) = acc / max(norm, eps), acc = 0."""
+    o2 = out if out.dim() == 2 else out[None]
+    a2 = acc if acc.dim() == 2 else acc[None]
+    B, n = a2.shape
+    s = _stream_handle(acc) if stream is None else stream
+    _check(lib().crlot_normalize_and_clear(o2.data_ptr(), a2.data_ptr(), norm.data_ptr(), eps, n, B,
+                                           _ld(o2, 0, n), _ld(a2, 0, n), s), "normalize_and_clear")
+    return out
+
+
+def axpy_host(dst: np.ndarray, src: np.ndarray, g: float, win: np.ndarray | None = None):
+    """The reference's host-pointer dsp::axpy / axpy_windowed (in place on dst, numpy float32)."""
+    assert dst.dtype == np.float32 and dst.flags.c_contiguous
+    src = np.ascontiguousarray(src, np.float32)
+    if win is None:
+        _check(lib().crlot_call_axpy(dst.ctypes.data, src.ctypes.data, g, dst.size), "axpy")
+    else:
+        win = np.ascontiguousarray(win, np.float32)
+        _check(lib().crlot_call_axpy_windowed(dst.ctypes.data, src.ctypes.data, win.ctypes.data, g, dst.size),
+               "axpy_windowed")
+    return dst
+
+
+def normalize_and_clear_host(out: np.ndarray, acc: np.ndarray, norm: np.ndarray, eps: float):
+    """The reference's host-pointer dsp::normalize_and_clear (numpy float32, acc zeroed)."""
+    assert out.dtype == np.float32 and acc.dtype == np.float32 and acc.flags.c_contiguous
+    norm = np.ascontiguousarray(norm, np.float32)
+    _check(lib().crlot_call_normalize_and_clear(out.ctypes.data, acc.ctypes.data, norm.ctypes.data, eps, acc.size),
+           "normalize_and_clear")
+    return out
+
+
+# ----------------------------------------------------------------- FrameQueue
+def framequeue_count(T: int, frame_size: int, hop_size: int, center: bool = True) -> int:
+    return _check(int(lib().crlot_framequeue_count(T, frame_size, hop_size, int(center))), "framequeue_count")
+
+
+def framequeue_frames(x, frame_size: int, hop_size: int, center: bool = True, pad_mode: int = PAD_CONSTANT,
+                      stream: int | None = None):
+    """Batched device form: x (S, T) CUDA tensor -> frames (S, F, N) (crlot_framequeue_frames)."""
+    torch = _torch()
+    x2 = x if x.dim() == 2 else x[None]
+    S, T = x2.shape
+    F = framequeue_count(T, frame_size, hop_size, center)
+    fr = torch.empty((S, F, frame_size), dtype=torch.float32, device=x.device)
+    s = _stream_handle(x) if stream is None else stream
+    _check(lib().crlot_framequeue_frames(x2.data_ptr() if T else None, S, T, _ld(x2, 0, T), frame_size, hop_size,
+                                         int(center), pad_mode, fr.data_ptr(), s), "framequeue_frames")
+    return fr if x.dim() == 2 else fr[0]
+
+
+class FrameQueue:
+    """dsp::FrameQueue (FrameQueue.h:35-59): frames built on the device at construction."""
+
+    def __init__(self, x, frame_size: int, hop_size: int, center: bool = True, pad_mode: int = PAD_CONSTANT,
+                 device: int = -1):
+        self._h = None
+        a = None if x is None else np.ascontiguousarray(x, np.float32).reshape(-1)
+        n = 0 if a is None else a.size
+        h = C.c_void_p()
+        _check(lib().crlot_framequeue_create(None if a is None or n == 0 else a.ctypes.data, n, frame_size,
+                                             hop_size, int(center), pad_mode, device, C.byref(h)), "FrameQueue")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().crlot_framequeue_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _info(self):
+        f, n, h = C.c_int64(), C.c_int64(), C.c_int64()
+        _check(lib().crlot_framequeue_info(self._h, C.byref(f), C.byref(n), C.byref(h)))
+        return f.value, n.value, h.value
+
+    def getNumFrames(self) -> int:
+        return self._info()[0]
+
+    def getFrameSize(self) -> int:
+        return self._info()[1]
+
+    def getHopSize(self) -> int:
+        return self._info()[2]
+
+    def getFrame(self, idx: int) -> np.ndarray:
+        p = lib().crlot_framequeue_frame(self._h, idx)
+        if not p:
+            _check(ERANGE if idx < 0 or idx >= self.getNumFrames() else EINVAL, "getFrame")
+        n = self.getFrameSize()
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (n,)).copy()
+
+    def copyFrame(self, idx: int, out: np.ndarray):
+        _check(lib().crlot_framequeue_copy_frame(self._h, idx, None if out is None else out.ctypes.data),
+               "copyFrame")
+
+    def getAllFrames(self) -> np.ndarray:
+        f, n, _ = self._info()
+        if f == 0:
+            return np.zeros(0, np.float32)
+        p = lib().crlot_framequeue_all_frames(self._h)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), (f * n,)).copy()
 
 
 class Stream:

@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "call.h"
 #include "crlot_dsp.h"
 #include "kernels.h"
 
@@ -874,7 +875,76 @@ struct crlot_fft_plan {
     int domain = CRLOT_FFT_REAL;
     int nfft = 0;
     crlot_plan* inner = nullptr;
+    // host-pointer calls (crlot_fft_*_host): the call server shared by every
+    // plan of this size on the device, or staged launches for sizes it has no
+    // instantiation for
+    std::mutex mu;
+    int e = 0;                          // K_call instantiation (0: staged launches)
+    std::vector<float> pack;            // strided <-> dense staging
+    float* d_stage = nullptr;           // staged-launch buffers (device)
+    size_t stage_floats = 0;
 };
+
+namespace {
+// One resident K_call<E> per (device, size), shared by the size's plans (so a
+// forward on one plan object and the inverse on another -- the reference's
+// e2e_benchmark uses one plan, multi-channel callers two -- share the
+// speculation), with its own copy of the size's FFT tables.
+struct FftCallShared {
+    std::mutex mu;
+    crlot::CallServer* srv = nullptr;
+    float* d_tw = nullptr;  // pass twiddles, super twiddles (device, owned)
+    float* d_st = nullptr;
+    struct Spec {           // the inverse speculated after the last forward
+        bool valid = false;
+        uint64_t index = 0;
+        int batch = 0;
+        crlot::CallSlot slot;
+    } spec;
+};
+std::mutex g_fft_shared_mu;
+FftCallShared* g_fft_shared[64][6] = {};  // [device][log2(E)]
+
+void stop_shared_servers() {
+    for (auto& row : g_fft_shared)
+        for (FftCallShared* s : row)
+            if (s && s->srv) (void)s->srv->stop();
+    crlot::stop_free_function_servers();
+}
+
+FftCallShared* fft_shared(const crlot_fft_plan* p, int* rc) {
+    const int dev = p->inner->device;
+    int lg = 0;
+    while ((2 << lg) < p->e) ++lg;  // e = 2, 4, ..., 32 -> 0..4
+    if (dev < 0 || dev >= 64 || lg > 5) {
+        *rc = fail(CRLOT_EUNSUPPORTED, "call server slot");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_fft_shared_mu);
+    FftCallShared*& s = g_fft_shared[dev][lg];
+    if (!s) {
+        static const bool hooked = [] { return std::atexit(stop_shared_servers) == 0; }();
+        (void)hooked;
+        FftCallShared* n = new FftCallShared();
+        const int P = 64 * p->e;
+        const std::vector<float> tw = crlot::build_pass_twiddles(2 * P);
+        hipError_t e;
+        if ((e = hipMalloc(&n->d_tw, sizeof(float) * tw.size())) ||
+            (e = hipMalloc(&n->d_st, sizeof(float) * 2 * P)) ||
+            (e = hipMemcpy(n->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
+            (e = hipMemcpy(n->d_st, p->inner->d_st, sizeof(float) * 2 * P, hipMemcpyDeviceToDevice))) {
+            *rc = hip_fail(e, "call server tables");
+            return nullptr;
+        }
+        const size_t row = size_t(2 * P + 2) * 2;
+        *rc = crlot::CallServer::create(dev, p->e, 4, 4 * row, 4 * row, 4 * row, &n->srv);
+        if (*rc != CRLOT_OK) return nullptr;
+        s = n;
+    }
+    *rc = CRLOT_OK;
+    return s;
+}
+}  // namespace
 
 int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
     if (!d || !out) return fail(CRLOT_EINVAL, "null argument");
@@ -902,12 +972,19 @@ int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
     p->domain = d->domain;
     p->nfft = d->nfft;
     p->inner = inner;
+    p->e = (!inner->generic && is_pow2(pd.frame_size) && pd.frame_size >= 256 && pd.frame_size <= 4096)
+               ? pd.frame_size / 128  // K_call<E>, E = P / 64
+               : 0;
     *out = p;
     return CRLOT_OK;
 }
 
 void crlot_fft_plan_destroy(crlot_fft_plan* p) {
     if (!p) return;
+    {
+        DeviceGuard g(p->inner->device);
+        if (p->d_stage) (void)hipFree(p->d_stage);
+    }
     crlot_plan_destroy(p->inner);
     delete p;
 }
@@ -973,6 +1050,160 @@ int crlot_fft_inverse_complex(crlot_fft_plan* p, const float* d_in, float* d_out
                               void* stream) {
     return cfft_common(p, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, true, stream);
 }
+
+// ------------------------------------------------------------------ FFT plans, host pointers
+// IFftPlan::forward / inverse / _complex with the reference's host-pointer
+// signature (kissfft_adapter.cc:83-246): synchronous, one call at a time.
+// Power-of-two plans run on the plan's resident call server (call_rt.hip: no
+// launch, no copy engine); after a real forward the server also runs the
+// inverse of the spectrum it returned, and an inverse called with exactly those
+// bits is served from that result.  Other sizes stage through device buffers
+// and a launch.  Element i of batch b at [b*ld + i*inc] as the device forms.
+}  // extern "C"
+
+namespace {
+
+// gather / scatter between strided caller memory and dense [batch][len] rows
+// (w = 1 for real samples, 2 for complex pairs)
+void gather(const float* src, float* dst, int batch, int64_t len, int w, int64_t ld, int64_t inc) {
+    for (int b = 0; b < batch; ++b) {
+        const float* s = src + int64_t(b) * ld;
+        float* d = dst + int64_t(b) * len * w;
+        if (inc == 1) {
+            std::memcpy(d, s, sizeof(float) * size_t(len * w));
+        } else {
+            for (int64_t i = 0; i < len; ++i)
+                for (int c = 0; c < w; ++c) d[i * w + c] = s[i * inc * w + c];
+        }
+    }
+}
+void scatter(const float* src, float* dst, int batch, int64_t len, int w, int64_t ld, int64_t inc) {
+    for (int b = 0; b < batch; ++b) {
+        const float* s = src + int64_t(b) * len * w;
+        float* d = dst + int64_t(b) * ld;
+        if (inc == 1) {
+            std::memcpy(d, s, sizeof(float) * size_t(len * w));
+        } else {
+            for (int64_t i = 0; i < len; ++i)
+                for (int c = 0; c < w; ++c) d[i * inc * w + c] = s[i * w + c];
+        }
+    }
+}
+
+// staged fallback: host -> device, the device form, device -> host
+int fft_host_staged(crlot_fft_plan* p, int kind, const float* in, float* out, int batch, int64_t in_len,
+                    int in_w, int64_t ld_in, int64_t inc_in, int64_t out_len, int out_w, int64_t ld_out,
+                    int64_t inc_out) {
+    const size_t nin = size_t(batch) * size_t(in_len * in_w), nout = size_t(batch) * size_t(out_len * out_w);
+    if (nin + nout > p->stage_floats) {
+        if (p->d_stage) (void)hipFree(p->d_stage);
+        p->d_stage = nullptr;
+        p->stage_floats = 0;
+        if (hipMalloc(&p->d_stage, sizeof(float) * (nin + nout)) != hipSuccess)
+            return fail(CRLOT_ENOMEM, "FFT staging hipMalloc failed");
+        p->stage_floats = nin + nout;
+    }
+    p->pack.resize(std::max(nin, nout));
+    gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
+    hipError_t e = hipMemcpy(p->d_stage, p->pack.data(), sizeof(float) * nin, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+    float* dout = p->d_stage + nin;
+    const int64_t ldi = in_len * in_w, ldo = out_len * out_w;
+    int rc = kind == 0   ? crlot_fft_forward(p, p->d_stage, dout, batch, ldi, 1, ldo, 1, nullptr)
+             : kind == 1 ? crlot_fft_inverse(p, p->d_stage, dout, batch, ldi, 1, ldo, 1, nullptr)
+             : kind == 2 ? crlot_fft_forward_complex(p, p->d_stage, dout, batch, ldi, 1, ldo, 1, nullptr)
+                         : crlot_fft_inverse_complex(p, p->d_stage, dout, batch, ldi, 1, ldo, 1, nullptr);
+    if (rc != CRLOT_OK) return rc;
+    if ((e = hipMemcpy(p->pack.data(), dout, sizeof(float) * nout, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy");
+    scatter(p->pack.data(), out, batch, out_len, out_w, ld_out, inc_out);
+    return CRLOT_OK;
+}
+
+// kind: 0 forward, 1 inverse (real), 2 forward_complex, 3 inverse_complex
+int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t batch, int64_t ld_in,
+             int64_t inc_in, int64_t ld_out, int64_t inc_out) {
+    const int want = kind < 2 ? CRLOT_FFT_REAL : CRLOT_FFT_COMPLEX;
+    int rc = fft_domain_check(p, want);
+    if (rc != CRLOT_OK) return rc;
+    if (batch < 0 || inc_in < 1 || inc_out < 1) return fail(CRLOT_EINVAL, "bad batch/stride");
+    if (batch == 0) return CRLOT_OK;
+    if (!in || !out) return fail(CRLOT_EINVAL, "null buffer");
+    std::lock_guard<std::mutex> lk(p->mu);
+    DeviceGuard g(p->inner->device);
+    const int64_t n = p->nfft, bins = n / 2 + 1;
+    // element counts and widths of the input / output rows
+    const int64_t in_len = kind == 0 ? n : kind == 1 ? bins : n, out_len = kind == 0 ? bins : kind == 1 ? n : n;
+    const int in_w = kind == 0 ? 1 : 2, out_w = kind == 1 ? 1 : 2;
+    if (p->e == 0) {
+        return fft_host_staged(p, kind, in, out, batch, in_len, in_w, ld_in, inc_in, out_len, out_w, ld_out,
+                               inc_out);
+    }
+    const size_t nin = size_t(batch) * size_t(in_len * in_w), nout = size_t(batch) * size_t(out_len * out_w);
+    p->pack.resize(std::max(nin, nout));
+    gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
+    FftCallShared* sh = fft_shared(p, &rc);
+    if (!sh) return rc;
+    std::lock_guard<std::mutex> slk(sh->mu);
+    crlot::CallServer* sv = sh->srv;
+    if (kind == 1 && sh->spec.valid && sh->spec.index == sv->submitted() && sh->spec.batch == batch &&
+        std::memcmp(p->pack.data(), sh->spec.slot.out, sizeof(float) * nin) == 0) {
+        // the spectrum the last forward returned, unchanged: its inverse is in the speculation slot
+        sh->spec.valid = false;
+        if ((rc = sv->wait_spec(sh->spec.index)) != CRLOT_OK) return rc;
+        scatter(sh->spec.slot.spec, out, batch, out_len, out_w, ld_out, inc_out);
+        return CRLOT_OK;
+    }
+    sh->spec.valid = false;
+    const bool spec = kind == 0 && batch <= 4 && p->e <= 16;
+    if ((rc = sv->grow(nin, nout, spec ? size_t(batch) * size_t(n) : 0)) != CRLOT_OK) return rc;
+    crlot::CallSlot sl;
+    if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
+    sv->put(sl.in, p->pack.data(), nin);
+    crlot::CallReq r{};
+    r.op = kind == 0 ? crlot::kCallRfft : kind == 1 ? crlot::kCallIrfft : kind == 2 ? crlot::kCallCfft : crlot::kCallIcfft;
+    r.batch = batch;
+    r.win_off = -1;
+    r.p0 = sh->d_tw;
+    r.p1 = sh->d_st;
+    r.f0 = kind < 2 ? p->inner->geo.inv_n : 1.0f / float(p->nfft);
+    if (spec) r.flags = crlot::kCallSpec;
+    if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+    if ((rc = sv->wait(sl.index)) != CRLOT_OK) return rc;
+    scatter(sl.out, out, batch, out_len, out_w, ld_out, inc_out);
+    if (spec) {
+        sh->spec.valid = true;
+        sh->spec.index = sl.index;
+        sh->spec.batch = batch;
+        sh->spec.slot = sl;
+    }
+    return CRLOT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crlot_fft_forward_host(crlot_fft_plan* p, const float* in, float* out_complex, int32_t batch, int64_t ld_in,
+                           int64_t inc_in, int64_t ld_out, int64_t inc_out) {
+    return fft_host(p, 0, in, out_complex, batch, ld_in, inc_in, ld_out, inc_out);
+}
+int crlot_fft_inverse_host(crlot_fft_plan* p, const float* in_complex, float* out, int32_t batch, int64_t ld_in,
+                           int64_t inc_in, int64_t ld_out, int64_t inc_out) {
+    return fft_host(p, 1, in_complex, out, batch, ld_in, inc_in, ld_out, inc_out);
+}
+int crlot_fft_forward_complex_host(crlot_fft_plan* p, const float* in, float* out, int32_t batch, int64_t ld_in,
+                                   int64_t inc_in, int64_t ld_out, int64_t inc_out) {
+    return fft_host(p, 2, in, out, batch, ld_in, inc_in, ld_out, inc_out);
+}
+int crlot_fft_inverse_complex_host(crlot_fft_plan* p, const float* in, float* out, int32_t batch, int64_t ld_in,
+                                   int64_t inc_in, int64_t ld_out, int64_t inc_out) {
+    return fft_host(p, 3, in, out, batch, ld_in, inc_in, ld_out, inc_out);
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // ------------------------------------------------------------------ streaming
 struct crlot_stream {

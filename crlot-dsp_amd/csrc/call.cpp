@@ -1,0 +1,384 @@
+// call.cpp -- host side of K_call (call_rt.hip): the resident server that runs
+// the reference's host-pointer calls one at a time (IFftPlan::forward /
+// inverse, OLAAccumulator add / push / produce, dsp::axpy / axpy_windowed /
+// normalize_and_clear) without a kernel launch or a copy-engine transfer per
+// call.
+//
+// Memory: a fine-grained DEVICE block [CallCtl][depth descriptors][input
+// arena] that the host writes through the BAR (write-combined stores, then an
+// sfence before and after the doorbell), and a pinned HOST block
+// [CallHostCtl][output arena][speculation arena] that the kernel writes.  Request q uses
+// slot q % depth of each arena; a slot is reused only after request q - depth
+// (and its speculation) completed.  If the device block cannot be allocated
+// host-visible, the input side falls back to pinned host memory (the kernel's
+// system-scope loads read either).
+#include "call.h"
+
+#include <immintrin.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <string>
+
+namespace crlot {
+int set_error(int code, const std::string& msg);  // abi.cpp
+
+namespace {
+int fail(int code, const std::string& msg) { return set_error(code, msg); }
+int hip_fail(hipError_t e, const char* what) { return fail(CRLOT_EHIP, std::string(what) + ": " + hipGetErrorString(e)); }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// write-combined copy into BAR-mapped device memory: 16-byte streaming stores
+// (dst 16-byte aligned), scalar tail
+void copy_wc(float* dst, const float* src, size_t n) {
+    size_t i = 0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+        for (; i + 4 <= n; i += 4)
+            _mm_stream_ps(dst + i, _mm_loadu_ps(src + i));
+    }
+    for (; i < n; ++i) dst[i] = src[i];
+}
+
+inline uint64_t load_acq(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+
+constexpr size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+}  // namespace
+
+CallServer::~CallServer() { release(); }
+
+void CallServer::release() {
+    DeviceGuard g(device_);
+    (void)stop();
+    if (dblk_) (void)hipFree(dblk_);
+    if (dhost_) (void)hipHostFree(dhost_);
+    if (hblk_) (void)hipHostFree(hblk_);
+    dblk_ = nullptr;
+    dhost_ = nullptr;
+    hblk_ = nullptr;
+    if (ev_) (void)hipEventDestroy(ev_);
+    if (s_) (void)hipStreamDestroy(s_);
+    ev_ = nullptr;
+    s_ = nullptr;
+}
+
+int CallServer::create(int device, int e, int depth, size_t in_cap, size_t out_cap, size_t spec_cap,
+                       CallServer** out) {
+    *out = nullptr;
+    if (call_lds_bytes(e) == 0) return fail(CRLOT_EUNSUPPORTED, "call server: no instantiation for this size");
+    CallServer* sv = new CallServer();
+    sv->device_ = device;
+    sv->e_ = e;
+    sv->depth_ = depth;
+    DeviceGuard g(device);
+    hipError_t err;
+    if ((err = hipStreamCreateWithFlags(&sv->s_, hipStreamNonBlocking)) ||
+        (err = hipEventCreateWithFlags(&sv->ev_, hipEventDisableTiming))) {
+        delete sv;
+        return hip_fail(err, "call server stream");
+    }
+    int khz = 100000;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+    sv->tick_ns_ = 1e6 / double(khz);
+    sv->idle_ticks_ = uint64_t(20.0e6 / sv->tick_ns_);  // 20 ms without a call
+    const int rc = sv->alloc(in_cap, out_cap, spec_cap);
+    if (rc != CRLOT_OK) {
+        delete sv;
+        return rc;
+    }
+    *out = sv;
+    return CRLOT_OK;
+}
+
+int CallServer::alloc(size_t in_cap, size_t out_cap, size_t spec_cap) {
+    in_cap_ = align_up(std::max<size_t>(in_cap, 64), 32);
+    out_cap_ = align_up(std::max<size_t>(out_cap, 64), 32);
+    spec_cap_ = align_up(spec_cap, 32);
+    const size_t dbytes = sizeof(CallCtl) + sizeof(CallReq) * size_t(depth_) + sizeof(float) * in_cap_ * depth_;
+    const size_t hbytes =
+        sizeof(CallHostCtl) + sizeof(float) * (out_cap_ + spec_cap_) * size_t(depth_);
+    hipError_t err;
+    const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+    static const bool host_inputs = [] {
+        const char* v = std::getenv("CRLOT_CALL_HOST_INPUTS");  // A/B: inputs in pinned host memory
+        return v && v[0] == '1';
+    }();
+    void* d = nullptr;
+    if (!host_inputs && hipExtMallocWithFlags(&d, dbytes, hipDeviceMallocFinegrained) == hipSuccess) {
+        dblk_ = static_cast<char*>(d);
+        wc_inputs_ = true;
+        ddev_ = dblk_;
+    } else {
+        if ((err = hipHostMalloc(reinterpret_cast<void**>(&dhost_), dbytes, fl)) != hipSuccess)
+            return hip_fail(err, "call server input block");
+        void* dp = nullptr;
+        if ((err = hipHostGetDevicePointer(&dp, dhost_, 0)) != hipSuccess) return hip_fail(err, "call server map");
+        ddev_ = static_cast<char*>(dp);
+        wc_inputs_ = false;
+    }
+    char* hin = dblk_ ? dblk_ : dhost_;  // host view of the input block
+    if ((err = hipHostMalloc(reinterpret_cast<void**>(&hblk_), hbytes, fl)) != hipSuccess)
+        return hip_fail(err, "call server output block");
+    void* hdp = nullptr;
+    if ((err = hipHostGetDevicePointer(&hdp, hblk_, 0)) != hipSuccess) return hip_fail(err, "call server map");
+    hctl_dev_ = static_cast<char*>(hdp);
+    ctl_ = reinterpret_cast<CallCtl*>(hin);
+    reqs_ = reinterpret_cast<CallReq*>(hin + sizeof(CallCtl));
+    in_ = reinterpret_cast<float*>(hin + sizeof(CallCtl) + sizeof(CallReq) * size_t(depth_));
+    hctl_ = reinterpret_cast<CallHostCtl*>(hblk_);
+    out_ = reinterpret_cast<float*>(hblk_ + sizeof(CallHostCtl));
+    std::memset(hblk_, 0, sizeof(CallHostCtl));
+    CallCtl zero{};
+    copy_wc(reinterpret_cast<float*>(ctl_), reinterpret_cast<const float*>(&zero), sizeof(CallCtl) / 4);
+    _mm_sfence();
+    q_ = 0;
+    spec_req_.assign(size_t(depth_), 0);
+    return CRLOT_OK;
+}
+
+int CallServer::grow(size_t in_cap, size_t out_cap, size_t spec_cap) {
+    if (in_cap <= in_cap_ && out_cap <= out_cap_ && spec_cap <= spec_cap_) return CRLOT_OK;
+    DeviceGuard g(device_);
+    int rc = drain();
+    if (rc == CRLOT_OK) rc = stop();
+    if (rc != CRLOT_OK) return rc;
+    if (dblk_) (void)hipFree(dblk_);
+    if (dhost_) (void)hipHostFree(dhost_);
+    if (hblk_) (void)hipHostFree(hblk_);
+    dblk_ = dhost_ = hblk_ = nullptr;
+    // request numbers stay monotonic across the reallocation (a speculation
+    // recorded before it can never match a later request)
+    const uint64_t q = q_;
+    rc = alloc(std::max(in_cap, in_cap_), std::max(out_cap, out_cap_), std::max(spec_cap, spec_cap_));
+    if (rc != CRLOT_OK) return rc;
+    q_ = q;
+    hctl_->done = hctl_->spec_done = q;
+    store_ctl(&ctl_->seq, q);
+    return CRLOT_OK;
+}
+
+bool CallServer::running() { return launched_ && hipEventQuery(ev_) == hipErrorNotReady; }
+
+int CallServer::launch() {
+    CallArgs a;
+    a.ctl = reinterpret_cast<CallCtl*>(ddev_);
+    a.hctl = reinterpret_cast<CallHostCtl*>(hctl_dev_);
+    a.reqs = reinterpret_cast<const CallReq*>(ddev_ + sizeof(CallCtl));
+    a.in_arena = reinterpret_cast<const float*>(ddev_ + sizeof(CallCtl) + sizeof(CallReq) * size_t(depth_));
+    a.out_arena = reinterpret_cast<float*>(hctl_dev_ + sizeof(CallHostCtl));
+    a.depth = depth_;
+    a.first = load_acq(&hctl_->done);
+    a.idle_ticks = idle_ticks_;
+    store_ctl(&ctl_->stop, 0);
+    hipError_t e = launch_call(e_, a, s_);
+    if (e == hipSuccess) e = hipEventRecord(ev_, s_);
+    if (e != hipSuccess) return hip_fail(e, "call server launch");
+    launched_ = true;
+    return CRLOT_OK;
+}
+
+void CallServer::store_ctl(uint64_t* p, uint64_t v) {
+    if (wc_inputs_) {
+        _mm_sfence();
+        *reinterpret_cast<volatile uint64_t*>(p) = v;
+        _mm_sfence();  // out of the write-combining buffer now
+    } else {
+        __atomic_store_n(p, v, __ATOMIC_RELEASE);
+    }
+}
+
+int CallServer::stop() {
+    if (!launched_) return CRLOT_OK;
+    store_ctl(&ctl_->stop, 1);
+    hipError_t e = hipStreamSynchronize(s_);
+    launched_ = false;
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "call server");
+}
+
+int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+        if (load_acq(ctr) >= target) return CRLOT_OK;
+        if ((spin & 1023) == 1023) {
+            if (!running()) {
+                if (launched_) {
+                    hipError_t e = hipEventSynchronize(ev_);
+                    if (e != hipSuccess) return hip_fail(e, "call server");
+                    launched_ = false;
+                }
+                if (load_acq(ctr) >= target) return CRLOT_OK;
+                // exited idle just as the request arrived: relaunch (it resumes at done)
+                int rc = launch();
+                if (rc != CRLOT_OK) return rc;
+            }
+            const auto us =
+                std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+            if (us > 5000000) return fail(CRLOT_EHIP, "call server: request timed out");
+        }
+        _mm_pause();
+    }
+}
+
+int CallServer::drain() {
+    if (q_ == 0) return CRLOT_OK;
+    int rc = wait_counter(&hctl_->done, q_);
+    if (rc != CRLOT_OK) return rc;
+    for (int i = 0; i < depth_; ++i)
+        if (spec_req_[size_t(i)]) {
+            rc = wait_counter(&hctl_->spec_done, spec_req_[size_t(i)]);
+            if (rc != CRLOT_OK) return rc;
+        }
+    return CRLOT_OK;
+}
+
+int CallServer::next_slot(CallSlot* sl) {
+    // slot q % depth was last used by request q - depth + 1 (1-based): wait for it
+    const int k = int(q_ % uint64_t(depth_));
+    if (q_ >= uint64_t(depth_)) {
+        int rc = wait_counter(&hctl_->done, q_ - uint64_t(depth_) + 1);
+        if (rc != CRLOT_OK) return rc;
+    }
+    if (spec_req_[size_t(k)]) {
+        int rc = wait_counter(&hctl_->spec_done, spec_req_[size_t(k)]);
+        if (rc != CRLOT_OK) return rc;
+        spec_req_[size_t(k)] = 0;
+    }
+    sl->index = q_ + 1;
+    sl->in = in_ + size_t(k) * in_cap_;
+    sl->out = out_ + size_t(k) * out_cap_;
+    sl->spec = out_ + size_t(depth_) * out_cap_ + size_t(k) * spec_cap_;
+    sl->in_off = int64_t(size_t(k) * in_cap_);
+    sl->out_off = int64_t(size_t(k) * out_cap_);
+    sl->spec_off = int64_t(size_t(depth_) * out_cap_ + size_t(k) * spec_cap_);
+    return CRLOT_OK;
+}
+
+void CallServer::put(float* dst, const float* src, size_t n) {
+    if (wc_inputs_)
+        copy_wc(dst, src, n);
+    else
+        std::memcpy(dst, src, sizeof(float) * n);
+}
+
+int CallServer::submit(CallReq& r, const CallSlot& sl) {
+    r.in_off = sl.in_off;
+    r.out_off = sl.out_off;
+    r.spec_off = sl.spec_off;
+    if (acquire_next_) {
+        r.flags |= kCallAcquire;
+        acquire_next_ = false;
+    }
+    const int k = int(q_ % uint64_t(depth_));
+    if (wc_inputs_)
+        copy_wc(reinterpret_cast<float*>(reqs_ + k), reinterpret_cast<const float*>(&r), sizeof(CallReq) / 4);
+    else
+        std::memcpy(reqs_ + k, &r, sizeof(CallReq));
+    spec_req_[size_t(k)] = (r.flags & kCallSpec) ? q_ + 1 : 0;
+    q_ += 1;
+    store_ctl(&ctl_->seq, q_);  // sfence: payload and descriptor land before the doorbell
+    if (!running()) {
+        if (launched_) {
+            hipError_t e = hipEventSynchronize(ev_);
+            if (e != hipSuccess) return hip_fail(e, "call server");
+            launched_ = false;
+        }
+        return launch();
+    }
+    return CRLOT_OK;
+}
+
+int CallServer::wait(uint64_t index) { return wait_counter(&hctl_->done, index); }
+int CallServer::wait_spec(uint64_t index) { return wait_counter(&hctl_->spec_done, index); }
+
+// ------------------------------------------------------------------ shared servers
+// One E = 0 server per device for the free functions (dsp::axpy & co).
+namespace {
+std::mutex g_free_mu;
+CallServer* g_free[64] = {};
+}  // namespace
+
+CallServer* free_function_server(int device, int* rc) {
+    if (device < 0 || device >= 64) {
+        *rc = fail(CRLOT_EINVAL, "device ordinal");
+        return nullptr;
+    }
+    if (!g_free[device]) {
+        CallServer* s = nullptr;
+        *rc = CallServer::create(device, 0, 4, 3 * 4096, 2 * 4096, 0, &s);
+        if (*rc != CRLOT_OK) return nullptr;
+        static const bool hooked = [] { return std::atexit(stop_free_function_servers) == 0; }();
+        (void)hooked;
+        g_free[device] = s;
+    }
+    *rc = CRLOT_OK;
+    return g_free[device];
+}
+std::mutex& free_function_mutex() { return g_free_mu; }
+
+void stop_free_function_servers() {
+    for (CallServer* s : g_free)
+        if (s) (void)s->stop();
+}
+
+}  // namespace crlot
+
+// ------------------------------------------------------------------ free functions (host pointers)
+extern "C" {
+
+static int free_call(uint32_t op, float* dst, float* dst2, const float* a, const float* b, const float* c, float f,
+                     int64_t n) {
+    using namespace crlot;
+    if (n < 0) return fail(CRLOT_EINVAL, "negative size");
+    if (n == 0) return CRLOT_OK;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return fail(CRLOT_EHIP, "no HIP device");
+    std::lock_guard<std::mutex> lk(free_function_mutex());
+    int rc = CRLOT_OK;
+    CallServer* sv = free_function_server(dev, &rc);
+    if (!sv) return rc;
+    const int nin = c ? 3 : 2, nout = dst2 ? 2 : 1;
+    if ((rc = sv->grow(size_t(nin) * size_t(n), size_t(nout) * size_t(n), 0)) != CRLOT_OK) return rc;
+    CallSlot sl;
+    if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
+    sv->put(sl.in, a, size_t(n));
+    sv->put(sl.in + n, b, size_t(n));
+    if (c) sv->put(sl.in + 2 * n, c, size_t(n));
+    CallReq r{};
+    r.op = op;
+    r.win_off = -1;
+    r.i[0] = n;
+    r.f0 = f;
+    if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+    if ((rc = sv->wait(sl.index)) != CRLOT_OK) return rc;
+    std::memcpy(dst, sl.out, sizeof(float) * size_t(n));
+    if (dst2) std::memcpy(dst2, sl.out + n, sizeof(float) * size_t(n));
+    return CRLOT_OK;
+}
+
+int crlot_call_axpy(float* dst, const float* src, float g, int64_t n) {
+    if (n > 0 && (!dst || !src)) return crlot::fail(CRLOT_EINVAL, "null buffer");
+    return free_call(crlot::kCallAxpy, dst, nullptr, dst, src, nullptr, g, n);
+}
+
+int crlot_call_axpy_windowed(float* dst, const float* src, const float* win, float g, int64_t n) {
+    if (n > 0 && (!dst || !src || !win)) return crlot::fail(CRLOT_EINVAL, "null buffer");
+    return free_call(crlot::kCallAxpyWin, dst, nullptr, dst, src, win, g, n);
+}
+
+int crlot_call_normalize_and_clear(float* out, float* acc, const float* norm, float eps, int64_t n) {
+    if (n > 0 && (!out || !acc || !norm)) return crlot::fail(CRLOT_EINVAL, "null buffer");
+    return free_call(crlot::kCallNormalize, out, acc, acc, norm, nullptr, eps, n);
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// call.h -- host side of the resident call server (call.cpp, call_rt.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <vector>
+
+#include "crlot_dsp.h"
+#include "kernels.h"
+
+namespace crlot {
+
+// The arena slots of one request: host views (in: write-combined device
+// memory or pinned host memory; out / spec: pinned host memory) and offsets.
+struct CallSlot {
+    uint64_t index = 0;  // 1-based request number: done >= index once it completed
+    float* in = nullptr;
+    float* out = nullptr;
+    float* spec = nullptr;
+    int64_t in_off = 0, out_off = 0, spec_off = 0;
+};
+
+// One resident K_call<e> kernel and its request ring.  Single-owner: callers
+// serialise access (the objects are single-threaded like the reference's).
+class CallServer {
+   public:
+    static int create(int device, int e, int depth, size_t in_cap, size_t out_cap, size_t spec_cap,
+                      CallServer** out);
+    ~CallServer();
+    CallServer(const CallServer&) = delete;
+    CallServer& operator=(const CallServer&) = delete;
+
+    // make every slot hold at least these many floats (drains and reallocates)
+    int grow(size_t in_cap, size_t out_cap, size_t spec_cap);
+    // the slots of the next request (waits until their previous user finished)
+    int next_slot(CallSlot* sl);
+    // copy n input floats into an input slot (write-combined when in device memory)
+    void put(float* dst, const float* src, size_t n);
+    // fill the slot offsets of r, post it, ring the doorbell, (re)launch if needed
+    int submit(CallReq& r, const CallSlot& sl);
+    int wait(uint64_t index);       // request `index` completed (its out slot is readable)
+    int wait_spec(uint64_t index);  // ... and its speculation slot
+    int drain();                    // every submitted request (and speculation) completed
+    int stop();                     // kernel gone (requests already completed stay so)
+    // the next request runs an agent-scope acquire first (the object's device
+    // state was written by kernels on other streams since the last request)
+    void acquire_next() { acquire_next_ = true; }
+    uint64_t submitted() const { return q_; }
+    uint64_t done() const { return __atomic_load_n(&hctl_->done, __ATOMIC_ACQUIRE); }
+    int device() const { return device_; }
+
+   private:
+    CallServer() = default;
+    int alloc(size_t in_cap, size_t out_cap, size_t spec_cap);
+    void release();
+    int launch();
+    bool running();
+    int wait_counter(const uint64_t* ctr, uint64_t target);
+    void store_ctl(uint64_t* p, uint64_t v);
+
+    int device_ = 0, e_ = 0, depth_ = 4;
+    hipStream_t s_ = nullptr;
+    hipEvent_t ev_ = nullptr;  // recorded after each launch: complete = kernel gone
+    bool launched_ = false;
+    bool wc_inputs_ = false;   // input block in fine-grained device memory (BAR writes)
+    bool acquire_next_ = false;
+    char* dblk_ = nullptr;     // fine-grained device block (host-mapped)
+    char* dhost_ = nullptr;    // ... or pinned host block (fallback)
+    char* ddev_ = nullptr;     // device view of the input block
+    char* hblk_ = nullptr;     // pinned host block
+    char* hctl_dev_ = nullptr; // device view of hblk_
+    CallCtl* ctl_ = nullptr;
+    CallReq* reqs_ = nullptr;
+    float* in_ = nullptr;
+    CallHostCtl* hctl_ = nullptr;
+    float* out_ = nullptr;
+    size_t in_cap_ = 0, out_cap_ = 0, spec_cap_ = 0;
+    uint64_t q_ = 0;                   // requests submitted
+    std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
+    uint64_t idle_ticks_ = 0;
+    double tick_ns_ = 10.0;
+};
+
+// atexit: stop the per-device free-function servers (their kernels would
+// otherwise idle out after the process began tearing the runtime down)
+void stop_free_function_servers();
+
+}  // namespace crlot

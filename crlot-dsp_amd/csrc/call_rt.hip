@@ -1,0 +1,400 @@
+// call_rt.hip -- K_call: the resident server behind the reference's
+// host-pointer, one-call-at-a-time API (the drop-in per-frame loop of
+// bench/e2e_benchmark.cc:152-170: Framer::pop -> IFftPlan::forward ->
+// IFftPlan::inverse -> OLAAccumulator::push_frame_AoS -> produce).
+//
+// A launch + synchronize costs ~15 us of host wall time even for an empty kernel
+// (DESIGN.md section 5), several times the reference's whole per-frame CPU cost.
+// K_call is launched once per object and stays resident (one 256-thread
+// workgroup); a call is a request descriptor:
+//   * the host copies the call's input (a frame, a spectrum, OLA samples) and the
+//     128-byte descriptor into fine-grained DEVICE memory through the BAR with
+//     write-combined stores, then bumps `seq` there (posted PCIe writes land in
+//     order), so the kernel polls and reads its own HBM, not host memory;
+//   * the kernel runs the call (the same device arithmetic as the launched
+//     kernels: fft_wave + kiss_fftr split / merge, the OLA ring ops, the scalar
+//     OLA kernels), writes the result straight into pinned HOST memory, fences
+//     at system scope and publishes done = seq;
+//   * speculation (bit-identical, validated by the host): after a forward real
+//     FFT the kernel also runs the inverse of the spectrum it just produced
+//     (IFftPlan::inverse is almost always called next on exactly those bits),
+//     and after an OLA add it computes the produce(n) block the host predicts,
+//     without clearing; each lands in a host slot with its own counter.  The
+//     host serves the next call from a slot only when the call's inputs match
+//     the speculated ones bit for bit (memcmp of the spectrum; equal read
+//     position and count with no call in between), else it submits the call.
+//     A served produce is committed by a clear-only request.
+// Exit conditions every thread reaches: `stop` (host 1, or 2 written by the
+// kernel itself on idle), or no request for `idle_ticks` of the 100 MHz clock;
+// the host relaunches on the next call (call.cpp).
+#include "fft_wave.h"
+#include "kernels.h"
+
+namespace crlot {
+
+using dev::cf;
+
+namespace {
+
+constexpr int kCallBlock = 256;
+constexpr int kCallWaves = kCallBlock / 64;
+
+// fine-grained device memory written by the host (relaxed system-scope loads:
+// straight from memory, nothing kept in L2) and host memory written by us
+__device__ __forceinline__ uint64_t ld_sys64(const void* p) {
+    return __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys32(const float* p) {
+    return __uint_as_float(
+        __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+}
+__device__ __forceinline__ float2 ld_sys2(const float* p) {
+    const uint64_t v = ld_sys64(p);
+    return make_float2(__uint_as_float(uint32_t(v)), __uint_as_float(uint32_t(v >> 32)));
+}
+__device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// LDS: [tw TW cf][st P cf][sth P cf][bufs kCallWaves x P cf][spec kCallWaves x (P+1) cf][req 128 B][cmd]
+// (the speculation buffers hold each wave's spectrum for the speculative
+// inverse; N = 4096 plans go without speculation to stay within 160 KB)
+template <int E>
+struct CallLds {
+    static constexpr int P = E > 0 ? 64 * E : 1;
+    static constexpr int TW = E > 0 ? dev::twiddle_table_size(E) : 1;
+    static constexpr bool SPEC = E > 0 && E <= 16;
+    static constexpr int SP = SPEC ? P + 1 : 0;
+    static constexpr size_t bytes =
+        sizeof(cf) * (size_t(TW) + 2 * P + size_t(kCallWaves) * (P + SP)) + sizeof(CallReq) + 16;
+};
+
+// ---- FFTs, one wave per transform (k_rfft / k_irfft / k_cfft's arithmetic)
+template <int E>
+__device__ __forceinline__ void rfft_core(cf (&v)[E], cf* buf, const cf* tw, int lane) {
+    dev::fft_wave<E, false>(v, buf, tw, lane);
+}
+
+// forward real FFT of in[0..N) (dense, fine-grained device memory) into the
+// spectrum sp[0..P] (cf, host memory); the spectrum also stays in `buf`+regs
+// for the speculative inverse: xs[m] = X[lane + 64 m], xp0 = X[P] (lane 0)
+template <int E>
+__device__ __forceinline__ void call_rfft(const float* in, float* sp, cf* buf, const cf* tw, const cf* sth,
+                                          int lane, cf (&xs)[E], cf& xpp) {
+    constexpr int P = 64 * E;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const float2 x2 = ld_sys2(in + 2 * (lane + 64 * m));
+        v[m].r = dev::sanit(x2.x);
+        v[m].i = dev::sanit(x2.y);
+    }
+    rfft_core<E>(v, buf, tw, lane);
+#pragma unroll
+    for (int m = 0; m < E; ++m) buf[lane + 64 * m] = v[m];
+    dev::wave_lds_fence();
+    xpp = cf{0.0f, 0.0f};
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + 64 * m;
+        const cf zk = v[m];
+        const cf fpnk = dev::conj(buf[(P - k) & (P - 1)]);
+        const cf f1 = dev::cadd(zk, fpnk);
+        const cf f2 = dev::csub(zk, fpnk);
+        const cf t = dev::cmul(f2, sth[k]);
+        cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)}, xp;
+        if (k == 0) {
+            dev::dc_split(zk, xk, xp);
+            xpp = xp;
+            *reinterpret_cast<float2*>(sp + 2 * P) = make_float2(xp.r, xp.i);
+        }
+        *reinterpret_cast<float2*>(sp + 2 * k) = make_float2(xk.r, xk.i);
+        xs[m] = xk;
+    }
+    dev::wave_lds_fence();
+}
+
+// inverse real FFT: spectrum X (bins 0..P) given by get(k) -> out[0..N) (host memory)
+template <int E, typename G>
+__device__ __forceinline__ void call_irfft(G get, float* out, cf* buf, const cf* tw, const cf* st, float inv_n,
+                                           int lane) {
+    constexpr int P = 64 * E;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int k = lane + 64 * m;
+        const cf xk = get(k);
+        const cf xpk = get(P - k);
+        const cf w = st[k];
+        const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+        const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+        v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
+        v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
+        if (k == 0) v[m] = dev::dc_merge(xk, xpk);
+    }
+    dev::fft_wave<E, true>(v, buf, tw, lane);
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int i0 = 2 * (lane + 64 * m);
+        *reinterpret_cast<float2*>(out + i0) =
+            make_float2(dev::sanit(v[m].r * inv_n), dev::sanit(v[m].i * inv_n));
+    }
+}
+
+template <int E, bool INV>
+__device__ __forceinline__ void call_cfft(const float* in, float* out, cf* buf, const cf* tw, float inv_p,
+                                          int lane) {
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const float2 x2 = ld_sys2(in + 2 * (lane + 64 * m));
+        v[m] = {x2.x, x2.y};
+    }
+    dev::fft_wave<E, INV>(v, buf, tw, lane);
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int i = lane + 64 * m;
+        if constexpr (INV)
+            *reinterpret_cast<float2*>(out + 2 * i) =
+                make_float2(dev::sanit(v[m].r * inv_p), dev::sanit(v[m].i * inv_p));
+        else
+            *reinterpret_cast<float2*>(out + 2 * i) = make_float2(v[m].r, v[m].i);
+    }
+}
+
+template <int E>
+__global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
+    constexpr int P = CallLds<E>::P, TW = CallLds<E>::TW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + TW;
+    cf* sth = st + P;
+    cf* bufs = sth + P;
+    cf* specs = bufs + kCallWaves * P;
+    CallReq* rq = reinterpret_cast<CallReq*>(specs + kCallWaves * CallLds<E>::SP);
+    uint32_t* cmd = reinterpret_cast<uint32_t*>(rq + 1);
+
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    cf* buf = bufs + wave * P;
+    cf* spb = specs + wave * CallLds<E>::SP;  // this wave's last spectrum (speculation)
+    CallCtl* ctl = a.ctl;
+    const float* staged_tw = nullptr;  // tables now in LDS (uniform)
+
+    uint64_t my = a.first;
+    uint64_t t_last = wall_clock64();
+    for (;;) {
+        // ---- wait for request `my` (thread 0 polls device memory, the workgroup follows)
+        if (t == 0) {
+            uint32_t k = 0;
+            for (;;) {
+                if (ld_sys64(&ctl->seq) > my) {
+                    k = 1;
+                    break;
+                }
+                if (ld_sys64(&ctl->stop) != 0) break;
+                if (wall_clock64() - t_last > a.idle_ticks) {
+                    __hip_atomic_store(&ctl->stop, uint64_t(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            cmd[0] = k;
+        }
+        __syncthreads();
+        if (cmd[0] == 0) break;
+        // the descriptor: 16 lanes x 8 bytes into LDS
+        const CallReq* src = a.reqs + (my % uint64_t(a.depth));
+        if (t < 16)
+            reinterpret_cast<uint64_t*>(rq)[t] = ld_sys64(reinterpret_cast<const uint64_t*>(src) + t);
+        __syncthreads();
+        const CallReq r = *rq;
+        if (r.flags & kCallAcquire)  // device-form calls ran on streams since the last request
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const float* in = a.in_arena + r.in_off;
+        float* out = a.out_arena + r.out_off;
+        bool spec = false;
+
+        if constexpr (E > 0) {
+            if (r.op >= kCallRfft && r.op <= kCallIcfft && r.p0 != staged_tw) {
+                // stage the plan's tables (k_rfft's load_tables)
+                const cf* gtw = reinterpret_cast<const cf*>(r.p0);
+                const cf* gst = reinterpret_cast<const cf*>(r.p1);
+                for (int i = t; i < TW; i += kCallBlock) tw[i] = gtw[i];
+                for (int i = t; i < P; i += kCallBlock) {
+                    const cf w = gst[i];
+                    st[i] = w;
+                    sth[i] = cf{w.r * 0.5f, w.i * 0.5f};  // exact
+                }
+                staged_tw = r.p0;
+                __syncthreads();
+            }
+            if (r.op == kCallRfft) {
+                // speculation keeps each wave's spectrum in LDS: one transform per wave
+                spec = CallLds<E>::SPEC && (r.flags & kCallSpec) != 0 && r.batch <= kCallWaves;
+                for (int b = wave; b < r.batch; b += kCallWaves) {
+                    cf xs[E > 0 ? E : 1];
+                    cf xpp;
+                    float* sp = out + int64_t(b) * (2 * P + 2);
+                    call_rfft<E>(in + int64_t(b) * 2 * P, sp, buf, tw, sth, lane, xs, xpp);
+                    if (CallLds<E>::SPEC && spec) {
+#pragma unroll
+                        for (int m = 0; m < E; ++m) spb[lane + 64 * m] = xs[m];
+                        if (lane == 0) spb[P] = xpp;
+                    }
+                }
+            } else if (r.op == kCallIrfft) {
+                for (int b = wave; b < r.batch; b += kCallWaves) {
+                    const float* x = in + int64_t(b) * (2 * P + 2);
+                    call_irfft<E>([&](int k) {
+                        const float2 v = ld_sys2(x + 2 * k);
+                        return cf{v.x, v.y};
+                    }, out + int64_t(b) * 2 * P, buf, tw, st, r.f0, lane);
+                }
+            } else if (r.op == kCallCfft || r.op == kCallIcfft) {
+                for (int b = wave; b < r.batch; b += kCallWaves) {
+                    if (r.op == kCallCfft)
+                        call_cfft<E, false>(in + int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
+                    else
+                        call_cfft<E, true>(in + int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
+                }
+            }
+        }
+        if (r.op == kCallOlaAdd) {
+            // add_frame_SoA / push_frame_AoS (ola.hip k_ola_add): channel c element j
+            // at in[c*cs + j*js]; window from the request (caller's) or the object
+            float* ring = r.p2;
+            const int64_t R = r.i[0], start = r.i[1], len = r.i[2], C = r.channels;
+            const bool aos = r.i[3] != 0;
+            const float* wreq = r.win_off >= 0 ? a.in_arena + r.win_off : nullptr;
+            const float* wobj = r.p0;
+            for (int64_t e = t; e < len * C; e += kCallBlock) {
+                const int64_t c = e / len, j = e - c * len;
+                int64_t p = start + j;
+                if (p >= R) p -= R;
+                float* rr = ring + c * R + p;
+                const float s = ld_sys32(in + (aos ? j * C + c : c * len + j));
+                if (wreq || wobj) {
+                    const float w = wreq ? ld_sys32(wreq + j) : wobj[j];
+                    *rr = __builtin_fmaf(__builtin_fmaf(s, w, 0.0f), r.f0, *rr);
+                } else {
+                    *rr = __builtin_fmaf(s, r.f0, *rr);
+                }
+            }
+            spec = (r.flags & kCallSpec) != 0;
+        } else if (r.op == kCallOlaProduce) {
+            // produce -> normalize_and_clear (ola.hip k_ola_produce), or the clear
+            // alone for a produce already served from the speculation slot
+            float* ring = r.p2;
+            const float* den = r.p1;
+            const int64_t R = r.i[0], rp = r.i[1], len = r.i[2], C = r.channels;
+            const bool clear_only = (r.flags & kCallClearOnly) != 0;
+            for (int64_t e = t; e < len * C; e += kCallBlock) {
+                const int64_t c = e / len, j = e - c * len;
+                int64_t p = rp + j;
+                if (p >= R) p -= R;
+                float* rr = ring + c * R + p;
+                if (!clear_only) out[c * len + j] = *rr / den[p];
+                *rr = 0.0f;
+            }
+        } else if (r.op == kCallAxpy || r.op == kCallAxpyWin) {
+            // dsp::axpy / axpy_windowed (kernels.cc:18-28): in = dst | src [| win]
+            const int64_t n = r.i[0];
+            for (int64_t j = t; j < n; j += kCallBlock) {
+                const float d = ld_sys32(in + j), s = ld_sys32(in + n + j);
+                const float x = r.op == kCallAxpyWin ? __builtin_fmaf(s, ld_sys32(in + 2 * n + j), 0.0f) : s;
+                out[j] = __builtin_fmaf(x, r.f0, d);
+            }
+        } else if (r.op == kCallNormalize) {
+            // dsp::normalize_and_clear (kernels.cc:30-36): in = acc | norm; out = out | acc
+            const int64_t n = r.i[0];
+            for (int64_t j = t; j < n; j += kCallBlock) {
+                const float ac = ld_sys32(in + j), nv = ld_sys32(in + n + j);
+                out[j] = ac / ((nv > r.f0) ? nv : r.f0);
+                out[n + j] = 0.0f;
+            }
+        }
+
+        // ---- publish: results visible system-wide, then done.  An add's only
+        // reader is its speculated produce: it publishes once, with the speculation.
+        my += 1;
+        const bool merged = spec && r.op == kCallOlaAdd;
+        if (!merged) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __syncthreads();
+            if (t == 0) st_sys64(&a.hctl->done, my);
+        }
+
+        // ---- speculation after the publish (the host is already running)
+        if (spec) {
+            float* so = a.out_arena + r.spec_off;
+            if constexpr (E > 0) {
+                if (CallLds<E>::SPEC && r.op == kCallRfft) {
+                    // inverse of the spectrum just written (the same bits, from LDS;
+                    // call_irfft is the inverse call's code)
+                    dev::wave_lds_fence();
+                    for (int b = wave; b < r.batch; b += kCallWaves)
+                        call_irfft<E>([&](int k) { return spb[k]; }, so + int64_t(b) * 2 * P, buf, tw, st, r.f0,
+                                      lane);
+                }
+            }
+            if (r.op == kCallOlaAdd) {
+                // the produce(n) the host predicts, without the clear
+                float* ring = r.p2;
+                const float* den = r.p1;
+                const int64_t R = r.i[0], rp = r.i[4], len = r.i[5], C = r.channels;
+                __syncthreads();  // every add of this request is in the ring
+                for (int64_t e = t; e < len * C; e += kCallBlock) {
+                    const int64_t c = e / len, j = e - c * len;
+                    int64_t p = rp + j;
+                    if (p >= R) p -= R;
+                    so[c * len + j] = ring[c * R + p] / den[p];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __syncthreads();
+            if (t == 0) {
+                if (merged) st_sys64(&a.hctl->done, my);
+                st_sys64(&a.hctl->spec_done, my);
+            }
+        }
+        t_last = wall_clock64();
+    }
+}
+
+}  // namespace
+
+size_t call_lds_bytes(int e) {
+    switch (e) {
+        case 0: return CallLds<0>::bytes;
+        case 2: return CallLds<2>::bytes;
+        case 4: return CallLds<4>::bytes;
+        case 8: return CallLds<8>::bytes;
+        case 16: return CallLds<16>::bytes;
+        case 32: return CallLds<32>::bytes;
+        default: return 0;
+    }
+}
+
+hipError_t launch_call(int e, const CallArgs& a, hipStream_t s) {
+    const size_t lds = call_lds_bytes(e);
+    if (!lds) return hipErrorInvalidValue;
+    void (*k)(const CallArgs) = nullptr;
+    switch (e) {
+        case 0: k = k_call<0>; break;
+        case 2: k = k_call<2>; break;
+        case 4: k = k_call<4>; break;
+        case 8: k = k_call<8>; break;
+        case 16: k = k_call<16>; break;
+        case 32: k = k_call<32>; break;
+        default: return hipErrorInvalidValue;
+    }
+    if (lds > 65536) {
+        hipError_t err = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+        if (err != hipSuccess) return err;
+    }
+    hipLaunchKernelGGL(k, dim3(1), dim3(kCallBlock), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace crlot

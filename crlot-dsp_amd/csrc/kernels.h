@@ -201,4 +201,59 @@ hipError_t launch_ola_produce(float* ring, int channels, int64_t R, const float*
                               int64_t ldo, int64_t rp, int64_t len, int64_t n_total, unsigned* peak,
                               hipStream_t s);
 
+// Resident call server (call_rt.hip, host side call.cpp): the reference's
+// host-pointer calls as request descriptors.  Ops and flags:
+enum : uint32_t {
+    kCallRfft = 1, kCallIrfft, kCallCfft, kCallIcfft,  // IFftPlan forward / inverse / _complex
+    kCallOlaAdd, kCallOlaProduce,                      // OLAAccumulator add_frame_SoA|push_frame_AoS / produce
+    kCallAxpy, kCallAxpyWin, kCallNormalize            // dsp::axpy / axpy_windowed / normalize_and_clear
+};
+enum : uint32_t { kCallSpec = 1, kCallClearOnly = 2, kCallAcquire = 4 };
+struct alignas(128) CallReq {
+    uint32_t op, flags;
+    int32_t batch, channels;
+    int64_t in_off, out_off, spec_off, win_off;  // floats into in_arena (device) / out_arena (host); win_off < 0: none
+    const float* p0;  // FFT: pass twiddles   | OLA add: the object's window (nullable)
+    const float* p1;  // FFT: super twiddles  | OLA: den = max(norm, eps)
+    float* p2;        // OLA: ring [C][R]
+    int64_t i[6];     // OLA: R, ring start / read pos, len, AoS?, speculated read pos, speculated count
+    float f0, f1;     // FFT: 1/N (1/P complex) | OLA add: gain | axpy: g | normalize: eps
+};
+static_assert(sizeof(CallReq) == 128, "one descriptor = one 128-byte line");
+struct alignas(64) CallCtl {  // fine-grained device memory, written by the host (BAR)
+    uint64_t seq;             // requests submitted
+    uint64_t pad0[7];
+    uint64_t stop;            // host: 1 = stop; kernel: 2 = idle exit
+    uint64_t pad1[7];
+};
+struct alignas(64) CallHostCtl {  // pinned host memory, written by the kernel
+    uint64_t done;                // requests completed
+    uint64_t pad0[7];
+    uint64_t spec_done;           // requests whose speculation slot is written
+    uint64_t pad1[7];
+};
+struct CallArgs {
+    CallCtl* ctl = nullptr;
+    CallHostCtl* hctl = nullptr;
+    const CallReq* reqs = nullptr;  // [depth], fine-grained device memory
+    const float* in_arena = nullptr;
+    float* out_arena = nullptr;     // pinned host memory
+    int depth = 0;
+    uint64_t first = 0;             // requests completed before this launch
+    uint64_t idle_ticks = 0;
+};
+// e = 0 (OLA / kernel ops only) or the FFT's E = P / 64 in {2, 4, 8, 16, 32}
+size_t call_lds_bytes(int e);
+hipError_t launch_call(int e, const CallArgs& a, hipStream_t s);
+
+// dsp::axpy / axpy_windowed (win != nullptr) / normalize_and_clear over `batch`
+// rows of n elements (ola.hip); the window / norm row is shared by every row.
+hipError_t launch_axpy(float* dst, int64_t ld_dst, const float* src, int64_t ld_src, const float* win, float g,
+                       int64_t n, int64_t batch, hipStream_t s);
+hipError_t launch_normalize_and_clear(float* out, int64_t ld_out, float* acc, int64_t ld_acc, const float* norm,
+                                      float eps, int64_t n, int64_t batch, hipStream_t s);
+// dsp::FrameQueue frames on the device: [stream][F][N] from x [stream][ld_x]
+hipError_t launch_fq_frames(const float* x, int64_t T, int64_t ld_x, int n_streams, float* frames, int64_t F,
+                            int64_t N, int64_t H, int64_t pad, int pad_mode, hipStream_t s);
+
 }  // namespace crlot

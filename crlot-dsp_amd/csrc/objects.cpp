@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "call.h"
 #include "crlot_dsp.h"
 #include "kernels.h"
 
@@ -179,8 +180,6 @@ struct crlot_ola {
     float* d_ring = nullptr;          // [C][R]
     float* d_den = nullptr;           // [R]
     float* d_win = nullptr;           // [N]
-    float* d_in = nullptr;            // staged frame: C*N samples + N window values
-    float* d_out = nullptr;           // produce staging [C][R]
     unsigned* d_peak = nullptr;       // running max |out| of device produce() calls (float bits)
     hipStream_t own = nullptr;        // stream of the host-pointer calls
     hipStream_t last = nullptr;       // stream of the previous call (cross-stream ordering)
@@ -193,7 +192,17 @@ struct crlot_ola {
         bool pending = false;
     } slot[kSlots];
     int next_slot = 0;
-    float* h_out = nullptr;           // pinned produce landing [C][R]
+    // host-pointer calls run on a resident call server (call_rt.hip); device-form
+    // calls on streams.  Switching between the two drains the other side first.
+    crlot::CallServer* srv = nullptr;
+    int mode = 0;                     // 0 none yet, 1 streams, 2 call server
+    int64_t last_req_n = 0;           // n of the last produce(): the next one's prediction
+    struct Spec {                     // produce block speculated after the last add
+        bool valid = false;
+        uint64_t index = 0;
+        int64_t rp = 0, n = 0;
+        crlot::CallSlot slot;
+    } spec;
 
     int64_t N() const { return cfg.frame_size; }
     int64_t H() const { return cfg.hop_size; }
@@ -205,23 +214,29 @@ namespace {
 void ola_free(crlot_ola* o) {
     if (!o) return;
     DeviceGuard g(o->device);
+    delete o->srv;  // waits for its requests, stops the kernel
     if (o->own) (void)hipStreamSynchronize(o->own);
     if (o->last_set && o->last) (void)hipStreamSynchronize(o->last);
     for (auto& s : o->slot) {
         if (s.ev) (void)hipEventDestroy(s.ev);
         if (s.h) (void)hipHostFree(s.h);
     }
-    for (float* p : {o->d_ring, o->d_den, o->d_win, o->d_in, o->d_out})
+    for (float* p : {o->d_ring, o->d_den, o->d_win})
         if (p) (void)hipFree(p);
     if (o->d_peak) (void)hipFree(o->d_peak);
-    if (o->h_out) (void)hipHostFree(o->h_out);
     if (o->order) (void)hipEventDestroy(o->order);
     if (o->own) (void)hipStreamDestroy(o->own);
     delete o;
 }
 
-// Make `s` the object's stream, ordered after everything issued on the previous one.
+// Make `s` the object's stream, ordered after everything issued on the previous
+// one and after every request of the call server.
 hipError_t use_stream(crlot_ola* o, hipStream_t s) {
+    if (o->mode == 2) {
+        if (o->srv->drain() != CRLOT_OK) return hipErrorLaunchFailure;
+        o->spec.valid = false;
+    }
+    o->mode = 1;
     if (o->last_set && o->last != s) {
         hipError_t e;
         if ((e = hipEventRecord(o->order, o->last)) != hipSuccess) return e;
@@ -301,25 +316,81 @@ int add_common(crlot_ola* o, const float* d_src, int64_t cs, int64_t js, const f
     return CRLOT_OK;
 }
 
-// stage `floats` host values (frames, then optionally a window slice) and copy
-// them to d_in on the object's own stream
-int stage_in(crlot_ola* o, const std::vector<std::pair<const float*, int64_t>>& parts) {
-    size_t total = 0;
-    for (auto& p : parts) total += size_t(p.second);
-    crlot_ola::Slot* sl = nullptr;
-    hipError_t e = take_slot(o, total, &sl);
-    if (e != hipSuccess) return hip_fail(e, "staging");
-    size_t at = 0;
-    for (auto& p : parts) {
-        std::memcpy(sl->h + at, p.first, sizeof(float) * size_t(p.second));
-        at += size_t(p.second);
+// Host-pointer calls run on the object's call server: first wait for the
+// stream-ordered work issued since the last request (and make the next request
+// re-read device memory).
+int to_server(crlot_ola* o) {
+    if (!o->srv) {
+        const size_t C = size_t(o->C()), N = size_t(o->N()), R = size_t(o->R);
+        const size_t blk = std::min(R, std::max<size_t>(N, 1024));
+        int rc = crlot::CallServer::create(o->device, 0, 8, C * N + N, C * blk, C * blk, &o->srv);
+        if (rc != CRLOT_OK) return rc;
     }
-    if ((e = hipMemcpyAsync(o->d_in, sl->h, sizeof(float) * total, hipMemcpyHostToDevice, o->own)) ||
-        (e = hipEventRecord(sl->ev, o->own)))
-        return hip_fail(e, "frame upload");
-    sl->pending = true;
+    if (o->mode == 1) {
+        hipError_t e = o->last_set ? hipStreamSynchronize(o->last) : hipSuccess;
+        if (e != hipSuccess) return hip_fail(e, "stream order");
+        o->srv->acquire_next();
+    }
+    o->mode = 2;
     return CRLOT_OK;
 }
+
+// add_frame_SoA (rows = ch channel pointers) / push_frame_AoS (rows[0] = the
+// interleaved frame at start_off): eff samples per channel; caller_win: a window
+// slice the host copies in; obj_win: the object's device window (or null)
+int server_add(crlot_ola* o, const float* const* rows, int64_t ch, bool aos, const float* caller_win,
+               const float* obj_win, int64_t start_sample, int64_t eff, float gain) {
+    int rc = to_server(o);
+    if (rc != CRLOT_OK) return rc;
+    crlot::CallServer* sv = o->srv;
+    const int64_t C = o->C();
+    const int64_t len = std::min(eff, o->R);  // RingBuffer::split clamps to capacity
+    // speculate the produce the host will ask for next: its last count (H before the first)
+    const int64_t produced_after = ch == C ? std::max(o->produced, start_sample + eff) : o->produced;
+    const int64_t avail = produced_after > o->read_pos ? produced_after - o->read_pos : 0;
+    const int64_t pn = std::min({o->last_req_n > 0 ? o->last_req_n : o->H(), avail, o->R});
+    if ((rc = sv->grow(size_t(C * eff + eff), size_t(C * std::max<int64_t>(pn, 1)),
+                       size_t(C * std::max<int64_t>(pn, 1)))) != CRLOT_OK)
+        return rc;
+    crlot::CallSlot sl;
+    if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
+    if (aos) {
+        sv->put(sl.in, rows[0], size_t(eff * C));
+    } else {
+        for (int64_t c = 0; c < ch; ++c) sv->put(sl.in + c * eff, rows[c], size_t(eff));
+    }
+    crlot::CallReq r{};
+    r.op = crlot::kCallOlaAdd;
+    r.channels = int32_t(ch);
+    r.win_off = -1;
+    if (caller_win) {
+        sv->put(sl.in + ch * eff, caller_win, size_t(eff));
+        r.win_off = sl.in_off + ch * eff;
+    }
+    r.p0 = obj_win;
+    r.p1 = o->d_den;
+    r.p2 = o->d_ring;
+    r.i[0] = o->R;
+    r.i[1] = start_sample % o->R;
+    r.i[2] = len;
+    r.i[3] = aos ? 1 : 0;
+    r.f0 = gain;
+    const bool spec = ch == C && pn > 0;
+    if (spec) {
+        r.flags = crlot::kCallSpec;
+        r.i[4] = o->read_pos % o->R;
+        r.i[5] = pn;
+    }
+    if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+    o->spec.valid = spec;
+    o->spec.index = sl.index;
+    o->spec.rp = o->read_pos;
+    o->spec.n = pn;
+    o->spec.slot = sl;
+    if (ch == C) o->produced = std::max(o->produced, start_sample + eff);  // :114
+    return CRLOT_OK;
+}
+
 
 }  // namespace
 
@@ -352,9 +423,7 @@ int crlot_ola_create(const crlot_ola_config* cfg, crlot_ola** out) {
     if ((e = hipStreamCreateWithFlags(&o->own, hipStreamNonBlocking)) ||
         (e = hipEventCreateWithFlags(&o->order, hipEventDisableTiming)) ||
         (e = hipMalloc(&o->d_ring, sizeof(float) * C * R)) || (e = hipMalloc(&o->d_den, sizeof(float) * R)) ||
-        (e = hipMalloc(&o->d_win, sizeof(float) * N)) || (e = hipMalloc(&o->d_in, sizeof(float) * (C + 1) * N)) ||
-        (e = hipMalloc(&o->d_out, sizeof(float) * C * R)) || (e = hipMalloc(&o->d_peak, sizeof(unsigned))) ||
-        (e = hipHostMalloc(reinterpret_cast<void**>(&o->h_out), sizeof(float) * C * R))) {
+        (e = hipMalloc(&o->d_win, sizeof(float) * N)) || (e = hipMalloc(&o->d_peak, sizeof(unsigned)))) {
         ola_free(o);
         return e == hipErrorOutOfMemory ? fail(CRLOT_ENOMEM, "OLA object allocation")
                                         : hip_fail(e, "OLA object allocation");
@@ -400,17 +469,12 @@ int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const f
     int64_t ok = 0;
     while (ok < o->C() && ch_frames[ok]) ++ok;
     DeviceGuard g(o->device);
-    hipError_t e = use_stream(o, o->own);
-    if (e != hipSuccess) return hip_fail(e, "stream order");
     const bool uw = use_window(o, window != nullptr);
     const bool caller_win = uw && !o->cfg.apply_window_inside;
-    std::vector<std::pair<const float*, int64_t>> parts;
-    for (int64_t c = 0; c < ok; ++c) parts.push_back({ch_frames[c] + start_off, eff});
-    if (caller_win) parts.push_back({window + start_off, eff});
-    int rc = stage_in(o, parts);
-    if (rc != CRLOT_OK) return rc;
-    const float* dw = !uw ? nullptr : caller_win ? o->d_in + ok * eff : o->d_win + start_off;
-    rc = add_common(o, o->d_in, eff, 1, dw, start_sample, eff, gain, o->own, ok);
+    std::vector<const float*> rows;
+    for (int64_t c = 0; c < ok; ++c) rows.push_back(ch_frames[c] + start_off);
+    int rc = server_add(o, rows.data(), ok, false, caller_win ? window + start_off : nullptr,
+                        (uw && !caller_win) ? o->d_win + start_off : nullptr, start_sample, eff, gain);
     if (rc != CRLOT_OK) return rc;
     return ok < o->C() ? fail(CRLOT_EINVAL, "Channel frame pointer cannot be null") : CRLOT_OK;
 }
@@ -423,19 +487,14 @@ int crlot_ola_push_frame_aos(crlot_ola* o, const float* interleaved, const float
     int64_t eff = 0;
     if (!clamp(o, start_off, size, &eff)) return CRLOT_OK;
     DeviceGuard g(o->device);
-    hipError_t e = use_stream(o, o->own);
-    if (e != hipSuccess) return hip_fail(e, "stream order");
     // push_frame_AoS deinterleaves [start_off, start_off + eff) and calls
     // add_frame_SoA with start_off = 0, so the window is read from index 0
     // (OLAAccumulator.cc:146-159)
     const bool uw = use_window(o, window != nullptr);
     const bool caller_win = uw && !o->cfg.apply_window_inside;
-    std::vector<std::pair<const float*, int64_t>> parts{{interleaved + start_off * o->C(), eff * o->C()}};
-    if (caller_win) parts.push_back({window, eff});
-    int rc = stage_in(o, parts);
-    if (rc != CRLOT_OK) return rc;
-    const float* dw = !uw ? nullptr : caller_win ? o->d_in + o->C() * eff : o->d_win;
-    return add_common(o, o->d_in, 1, o->C(), dw, start_sample, eff, gain, o->own);
+    const float* src = interleaved + start_off * o->C();
+    return server_add(o, &src, o->C(), true, caller_win ? window : nullptr, (uw && !caller_win) ? o->d_win : nullptr,
+                      start_sample, eff, gain);
 }
 
 int crlot_ola_add_frame_soa_device(crlot_ola* o, const float* d_frames, int64_t ld_frames,
@@ -482,21 +541,47 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
     if (n == 0) return CRLOT_OK;
     for (int64_t c = 0; c < o->C(); ++c)
         if (!ch_out[c]) return fail(CRLOT_EINVAL, "Output channel buffer cannot be null");
+    o->last_req_n = n;
     const int64_t avail = o->produced > o->read_pos ? o->produced - o->read_pos : 0;
     if (avail == 0) return CRLOT_OK;
     n = std::min(n, avail);
     const int64_t len = std::min(n, o->R);  // split() clamps to capacity
     DeviceGuard g(o->device);
-    hipError_t e = use_stream(o, o->own);
-    if (e != hipSuccess) return hip_fail(e, "stream order");
-    if ((e = crlot::launch_ola_produce(o->d_ring, int(o->C()), o->R, o->d_den, o->d_out, len,
-                                       o->read_pos % o->R, len, len, nullptr, o->own)) ||
-        (e = hipMemcpyAsync(o->h_out, o->d_out, sizeof(float) * size_t(len * o->C()), hipMemcpyDeviceToHost,
-                            o->own)) ||
-        (e = hipStreamSynchronize(o->own)))
-        return hip_fail(e, "OLA produce");
-    for (int64_t c = 0; c < o->C(); ++c)
-        std::memcpy(ch_out[c], o->h_out + c * len, sizeof(float) * size_t(len));
+    int rc = to_server(o);
+    if (rc != CRLOT_OK) return rc;
+    crlot::CallServer* sv = o->srv;
+    const int64_t C = o->C();
+    const bool hit = o->spec.valid && o->spec.index == sv->submitted() && o->spec.rp == o->read_pos &&
+                     o->spec.n == len;
+    o->spec.valid = false;
+    if (!hit && (rc = sv->grow(size_t(C * o->N() + o->N()), size_t(C * len), size_t(C * len))) != CRLOT_OK)
+        return rc;
+    crlot::CallReq r{};
+    r.op = crlot::kCallOlaProduce;
+    r.win_off = -1;
+    r.channels = int32_t(C);
+    r.p1 = o->d_den;
+    r.p2 = o->d_ring;
+    r.i[0] = o->R;
+    r.i[1] = o->read_pos % o->R;
+    r.i[2] = len;
+    if (hit) {
+        // served from the block speculated after the last add (the same bits); the
+        // ring is cleared by a request behind it
+        if ((rc = sv->wait_spec(o->spec.index)) != CRLOT_OK) return rc;
+        for (int64_t c = 0; c < C; ++c)
+            std::memcpy(ch_out[c], o->spec.slot.spec + c * len, sizeof(float) * size_t(len));
+        crlot::CallSlot sl;
+        if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
+        r.flags = crlot::kCallClearOnly;
+        if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+    } else {
+        crlot::CallSlot sl;
+        if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
+        if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+        if ((rc = sv->wait(sl.index)) != CRLOT_OK) return rc;
+        for (int64_t c = 0; c < C; ++c) std::memcpy(ch_out[c], sl.out + c * len, sizeof(float) * size_t(len));
+    }
     o->read_pos = (o->read_pos + n) % o->R;  // :213
     for (int64_t i = 0; i < n; ++i) {        // update_peak_meter (:289-295), channel 0
         const float a = std::fabs(ch_out[0][i]);
@@ -587,8 +672,191 @@ int crlot_ola_norm_table(const crlot_ola* o, float* out) {
 int crlot_ola_synchronize(crlot_ola* o) {
     if (!o) return fail(CRLOT_EINVAL, "null OLA object");
     DeviceGuard g(o->device);
+    if (o->mode == 2) return o->srv->drain();
     hipError_t e = o->last_set ? hipStreamSynchronize(o->last) : hipSuccess;
     return e == hipSuccess ? CRLOT_OK : hip_fail(e, "sync");
 }
+
+}  // extern "C"
+
+// =================================================================== OLA kernels (free functions)
+// dsp::axpy / axpy_windowed / normalize_and_clear (kernels.h:28-53): batched
+// device forms over rows of n elements (ola.hip).  The reference's host-pointer
+// signatures are served by the resident call path (call_rt.hip).
+extern "C" {
+
+int crlot_axpy(float* d_dst, const float* d_src, float g, int64_t n, int64_t batch, int64_t ld_dst,
+               int64_t ld_src, void* stream) {
+    if (n < 0 || batch < 0) return fail(CRLOT_EINVAL, "negative size");
+    if (n == 0 || batch == 0) return CRLOT_OK;
+    if (!d_dst || !d_src) return fail(CRLOT_EINVAL, "null buffer");
+    if (batch > 1 && (ld_dst < n || ld_src < n)) return fail(CRLOT_EINVAL, "leading dimension too small");
+    if (batch > 65535) return fail(CRLOT_EUNSUPPORTED, "batch above 65535 rows");
+    hipError_t e = crlot::launch_axpy(d_dst, ld_dst, d_src, ld_src, nullptr, g, n, batch,
+                                      static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "axpy kernel launch");
+}
+
+int crlot_axpy_windowed(float* d_dst, const float* d_src, const float* d_win, float g, int64_t n, int64_t batch,
+                        int64_t ld_dst, int64_t ld_src, void* stream) {
+    if (n < 0 || batch < 0) return fail(CRLOT_EINVAL, "negative size");
+    if (n == 0 || batch == 0) return CRLOT_OK;
+    if (!d_dst || !d_src || !d_win) return fail(CRLOT_EINVAL, "null buffer");
+    if (batch > 1 && (ld_dst < n || ld_src < n)) return fail(CRLOT_EINVAL, "leading dimension too small");
+    if (batch > 65535) return fail(CRLOT_EUNSUPPORTED, "batch above 65535 rows");
+    hipError_t e = crlot::launch_axpy(d_dst, ld_dst, d_src, ld_src, d_win, g, n, batch,
+                                      static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "axpy_windowed kernel launch");
+}
+
+int crlot_normalize_and_clear(float* d_out, float* d_acc, const float* d_norm, float eps, int64_t n, int64_t batch,
+                              int64_t ld_out, int64_t ld_acc, void* stream) {
+    if (n < 0 || batch < 0) return fail(CRLOT_EINVAL, "negative size");
+    if (n == 0 || batch == 0) return CRLOT_OK;
+    if (!d_out || !d_acc || !d_norm) return fail(CRLOT_EINVAL, "null buffer");
+    if (batch > 1 && (ld_out < n || ld_acc < n)) return fail(CRLOT_EINVAL, "leading dimension too small");
+    if (batch > 65535) return fail(CRLOT_EUNSUPPORTED, "batch above 65535 rows");
+    hipError_t e = crlot::launch_normalize_and_clear(d_out, ld_out, d_acc, ld_acc, d_norm, eps, n, batch,
+                                                     static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "normalize_and_clear kernel launch");
+}
+
+}  // extern "C"
+
+// =================================================================== FrameQueue
+// dsp::FrameQueue (FrameQueue.h:35-59, FrameQueue.cc:9-115): every frame of a
+// whole signal materialised at construction, AoS [frame][N].  Frames are built
+// on the device (k_fq_frames, ola.hip) and kept there (device_frames: the
+// GPU-native input of batched transforms); the reference's host-pointer
+// accessors read a host copy taken at construction.
+struct crlot_framequeue {
+    int device = 0;
+    int64_t n = 0, h = 0, f = 0;
+    float* d_frames = nullptr;
+    std::vector<float> frames;  // host copy (getFrame / getAllFrames)
+};
+
+namespace {
+// FrameQueue::calculateNumFrames on the padded length (FrameQueue.cc:98-115)
+int64_t fq_count(int64_t T, int64_t n, int64_t h, bool center) {
+    const int64_t padded = T + (center ? 2 * (n / 2) : 0);
+    if (padded < n) return 0;
+    const int64_t tail = n > h ? n - h : 0;
+    return (padded - tail) / h;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t crlot_framequeue_count(int64_t T, int64_t frame_size, int64_t hop_size, int32_t center) {
+    if (T < 0 || frame_size <= 0 || hop_size <= 0) return fail(CRLOT_EINVAL, "bad argument");
+    return fq_count(T, frame_size, hop_size, center != 0);
+}
+
+int crlot_framequeue_frames(const float* d_x, int32_t n_streams, int64_t T, int64_t ld_x, int64_t frame_size,
+                            int64_t hop_size, int32_t center, int32_t pad_mode, float* d_frames, void* stream) {
+    if (frame_size <= 0) return fail(CRLOT_EINVAL, "Frame size must be greater than 0");
+    if (hop_size <= 0) return fail(CRLOT_EINVAL, "Hop size must be greater than 0");
+    if (n_streams < 0 || T < 0 || (n_streams > 1 && ld_x < T)) return fail(CRLOT_EINVAL, "bad size");
+    if (pad_mode < CRLOT_PAD_CONSTANT || pad_mode > CRLOT_PAD_EDGE) return fail(CRLOT_EINVAL, "Unknown pad mode");
+    if (!d_x && T > 0) return fail(CRLOT_EINVAL, "Input pointer cannot be null when length > 0");
+    const int64_t F = fq_count(T, frame_size, hop_size, center != 0);
+    if (F == 0 || n_streams == 0) return CRLOT_OK;
+    if (!d_frames) return fail(CRLOT_EINVAL, "null buffer");
+    hipError_t e = crlot::launch_fq_frames(d_x, T, ld_x, n_streams, d_frames, F, frame_size, hop_size,
+                                           center ? frame_size / 2 : 0, pad_mode, static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "FrameQueue kernel launch");
+}
+
+int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, int64_t hop_size, int32_t center,
+                            int32_t pad_mode, int32_t device, crlot_framequeue** out) {
+    if (!out) return fail(CRLOT_EINVAL, "null argument");
+    *out = nullptr;
+    // FrameQueue.cc:13-22
+    if (frame_size <= 0) return fail(CRLOT_EINVAL, "Frame size must be greater than 0");
+    if (hop_size <= 0) return fail(CRLOT_EINVAL, "Hop size must be greater than 0");
+    if (!in && len > 0) return fail(CRLOT_EINVAL, "Input pointer cannot be null when length > 0");
+    if (len < 0) return fail(CRLOT_EINVAL, "negative length");
+    if (pad_mode < CRLOT_PAD_CONSTANT || pad_mode > CRLOT_PAD_EDGE) return fail(CRLOT_EINVAL, "Unknown pad mode");
+    crlot_framequeue* q = new crlot_framequeue();
+    if (device < 0) {
+        if (hipGetDevice(&q->device) != hipSuccess) {
+            delete q;
+            return fail(CRLOT_EHIP, "no HIP device");
+        }
+    } else {
+        q->device = device;
+    }
+    DeviceGuard g(q->device);
+    q->n = frame_size;
+    q->h = hop_size;
+    q->f = fq_count(len, frame_size, hop_size, center != 0);
+    const size_t nf = size_t(q->f) * size_t(q->n);
+    q->frames.resize(nf);
+    if (nf == 0) {
+        *out = q;
+        return CRLOT_OK;
+    }
+    float* d_x = nullptr;
+    hipStream_t s = nullptr;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) ||
+        (e = hipMalloc(&q->d_frames, sizeof(float) * nf)) ||
+        (len > 0 && (e = hipMalloc(&d_x, sizeof(float) * size_t(len)))) ||
+        (len > 0 && (e = hipMemcpyAsync(d_x, in, sizeof(float) * size_t(len), hipMemcpyHostToDevice, s))) ||
+        (e = crlot::launch_fq_frames(d_x, len, len, 1, q->d_frames, q->f, q->n, q->h,
+                                     center ? frame_size / 2 : 0, pad_mode, s)) ||
+        (e = hipMemcpyAsync(q->frames.data(), q->d_frames, sizeof(float) * nf, hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s))) {
+        if (d_x) (void)hipFree(d_x);
+        if (s) (void)hipStreamDestroy(s);
+        if (q->d_frames) (void)hipFree(q->d_frames);
+        delete q;
+        return e == hipErrorOutOfMemory ? fail(CRLOT_ENOMEM, "FrameQueue allocation") : hip_fail(e, "FrameQueue");
+    }
+    if (d_x) (void)hipFree(d_x);
+    (void)hipStreamDestroy(s);
+    *out = q;
+    return CRLOT_OK;
+}
+
+void crlot_framequeue_destroy(crlot_framequeue* q) {
+    if (!q) return;
+    DeviceGuard g(q->device);
+    if (q->d_frames) (void)hipFree(q->d_frames);
+    delete q;
+}
+
+int crlot_framequeue_info(const crlot_framequeue* q, int64_t* num_frames, int64_t* frame_size, int64_t* hop_size) {
+    if (!q) return fail(CRLOT_EINVAL, "null FrameQueue");
+    if (num_frames) *num_frames = q->f;
+    if (frame_size) *frame_size = q->n;
+    if (hop_size) *hop_size = q->h;
+    return CRLOT_OK;
+}
+
+const float* crlot_framequeue_frame(const crlot_framequeue* q, int64_t frame_idx) {
+    if (!q) {
+        fail(CRLOT_EINVAL, "null FrameQueue");
+        return nullptr;
+    }
+    if (frame_idx < 0 || frame_idx >= q->f) {  // FrameQueue.cc:49-54
+        fail(CRLOT_ERANGE, "Frame index out of range");
+        return nullptr;
+    }
+    return q->frames.data() + size_t(frame_idx) * size_t(q->n);
+}
+
+int crlot_framequeue_copy_frame(const crlot_framequeue* q, int64_t frame_idx, float* out) {
+    if (!q) return fail(CRLOT_EINVAL, "null FrameQueue");
+    if (frame_idx < 0 || frame_idx >= q->f) return fail(CRLOT_ERANGE, "Frame index out of range");
+    if (!out) return fail(CRLOT_EINVAL, "Output buffer cannot be null");  // FrameQueue.cc:56-67
+    std::memcpy(out, q->frames.data() + size_t(frame_idx) * size_t(q->n), sizeof(float) * size_t(q->n));
+    return CRLOT_OK;
+}
+
+const float* crlot_framequeue_all_frames(const crlot_framequeue* q) { return q ? q->frames.data() : nullptr; }
+
+const float* crlot_framequeue_device_frames(const crlot_framequeue* q) { return q ? q->d_frames : nullptr; }
 
 }  // extern "C"

@@ -126,7 +126,137 @@ __global__ void __launch_bounds__(256) k_interleave(const float* __restrict__ pl
     }
 }
 
+// dsp::axpy / axpy_windowed / normalize_and_clear (kernels.h:28-53) over a batch
+// of rows: row b of dst at dst + b*ld_dst, of src at src + b*ld_src; the window
+// and the norm row are shared by every row (the OLA's use).  Per element the
+// reference's scalar forms (kernels.cc:18-36), which its Highway versions match:
+//   axpy           dst = fma(src, g, dst)
+//   axpy_windowed  dst = fma(fma(src, win, 0), g, dst)
+//   normalize      out = acc / (norm > eps ? norm : eps)   (IEEE division), acc = 0
+// HBM-bound elementwise work (12 B per element, the shared row cache-resident):
+// VEC moves 4 elements per thread with 16-byte accesses when every row is
+// 16-byte aligned; otherwise one element per thread.
+template <bool VEC, bool WIN>
+__global__ void __launch_bounds__(256) k_axpy(float* __restrict__ dst, int64_t ld_dst,
+                                              const float* __restrict__ src, int64_t ld_src,
+                                              const float* __restrict__ win, float g, int64_t n) {
+    const int64_t b = blockIdx.y;
+    const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * (VEC ? 4 : 1);
+    if (i >= n) return;
+    float* d = dst + b * ld_dst + i;
+    const float* s = src + b * ld_src + i;
+    if constexpr (VEC) {
+        const float4 sv = *reinterpret_cast<const float4*>(s);
+        float4 dv = *reinterpret_cast<const float4*>(d);
+        float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (WIN) wv = *reinterpret_cast<const float4*>(win + i);
+        dv.x = __builtin_fmaf(WIN ? __builtin_fmaf(sv.x, wv.x, 0.0f) : sv.x, g, dv.x);
+        dv.y = __builtin_fmaf(WIN ? __builtin_fmaf(sv.y, wv.y, 0.0f) : sv.y, g, dv.y);
+        dv.z = __builtin_fmaf(WIN ? __builtin_fmaf(sv.z, wv.z, 0.0f) : sv.z, g, dv.z);
+        dv.w = __builtin_fmaf(WIN ? __builtin_fmaf(sv.w, wv.w, 0.0f) : sv.w, g, dv.w);
+        *reinterpret_cast<float4*>(d) = dv;
+    } else {
+        const float x = WIN ? __builtin_fmaf(*s, win[i], 0.0f) : *s;
+        *d = __builtin_fmaf(x, g, *d);
+    }
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) k_normalize_and_clear(float* __restrict__ out, int64_t ld_out,
+                                                             float* __restrict__ acc, int64_t ld_acc,
+                                                             const float* __restrict__ norm, float eps,
+                                                             int64_t n) {
+    const int64_t b = blockIdx.y;
+    const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * (VEC ? 4 : 1);
+    if (i >= n) return;
+    float* o = out + b * ld_out + i;
+    float* a = acc + b * ld_acc + i;
+    if constexpr (VEC) {
+        const float4 av = *reinterpret_cast<const float4*>(a);
+        const float4 nv = *reinterpret_cast<const float4*>(norm + i);
+        float4 r;
+        r.x = av.x / ((nv.x > eps) ? nv.x : eps);
+        r.y = av.y / ((nv.y > eps) ? nv.y : eps);
+        r.z = av.z / ((nv.z > eps) ? nv.z : eps);
+        r.w = av.w / ((nv.w > eps) ? nv.w : eps);
+        *reinterpret_cast<float4*>(o) = r;
+        *reinterpret_cast<float4*>(a) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        const float nv = norm[i];
+        *o = *a / ((nv > eps) ? nv : eps);
+        *a = 0.0f;
+    }
+}
+
+// dsp::FrameQueue (FrameQueue.cc:9-115, Indexing.h:18-70) materialised on the
+// device: frame k of stream s is padded positions [k*H, k*H + N) of the stream
+// padded by `pad` (N/2 with center, else 0) on both sides; original index
+// idx = k*H + j - pad, taken from x where 0 <= idx < T, else from the pad rule
+// (CONSTANT 0, REFLECT reflect-101 about the ends, EDGE the end sample; any
+// rule gives 0 for an empty stream).  One thread per frame sample.
+__device__ __forceinline__ int64_t fq_reflect101(int64_t i, int64_t n) {
+    if (n <= 1) return 0;
+    while (i < 0 || i >= n) i = i < 0 ? -i - 1 : 2 * n - 2 - i;  // Indexing.h:18-33
+    return i;
+}
+__global__ void __launch_bounds__(256) k_fq_frames(const float* __restrict__ x, int64_t T, int64_t ld_x,
+                                                   float* __restrict__ frames, int64_t F, int64_t N, int64_t H,
+                                                   int64_t pad, int pad_mode) {
+    const int64_t s = blockIdx.y;
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (e >= F * N) return;
+    const int64_t k = e / N, j = e - k * N;
+    const int64_t idx = k * H + j - pad;
+    const float* xs = x + s * ld_x;
+    float v = 0.0f;
+    if (idx >= 0 && idx < T)
+        v = xs[idx];
+    else if (T > 0 && pad_mode == 1)
+        v = xs[fq_reflect101(idx, T)];
+    else if (T > 0 && pad_mode == 2)
+        v = xs[idx < 0 ? 0 : T - 1];
+    frames[s * F * N + e] = v;
+}
+
 }  // namespace
+
+hipError_t launch_axpy(float* dst, int64_t ld_dst, const float* src, int64_t ld_src, const float* win, float g,
+                       int64_t n, int64_t batch, hipStream_t s) {
+    if (n <= 0 || batch <= 0) return hipSuccess;
+    if (batch > 65535) return hipErrorInvalidValue;
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+    const bool vec = n % 4 == 0 && al16(dst) && al16(src) && (!win || al16(win)) &&
+                     (batch == 1 || (ld_dst % 4 == 0 && ld_src % 4 == 0));
+    const int64_t per = vec ? 1024 : 256;
+    const dim3 grid(unsigned((n + per - 1) / per), unsigned(batch));
+    auto k = vec ? (win ? k_axpy<true, true> : k_axpy<true, false>)
+                 : (win ? k_axpy<false, true> : k_axpy<false, false>);
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, dst, ld_dst, src, ld_src, win, g, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_normalize_and_clear(float* out, int64_t ld_out, float* acc, int64_t ld_acc, const float* norm,
+                                      float eps, int64_t n, int64_t batch, hipStream_t s) {
+    if (n <= 0 || batch <= 0) return hipSuccess;
+    if (batch > 65535) return hipErrorInvalidValue;
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; };
+    const bool vec = n % 4 == 0 && al16(out) && al16(acc) && al16(norm) &&
+                     (batch == 1 || (ld_out % 4 == 0 && ld_acc % 4 == 0));
+    const int64_t per = vec ? 1024 : 256;
+    const dim3 grid(unsigned((n + per - 1) / per), unsigned(batch));
+    auto k = vec ? k_normalize_and_clear<true> : k_normalize_and_clear<false>;
+    hipLaunchKernelGGL(k, grid, dim3(256), 0, s, out, ld_out, acc, ld_acc, norm, eps, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_frames(const float* x, int64_t T, int64_t ld_x, int n_streams, float* frames, int64_t F,
+                            int64_t N, int64_t H, int64_t pad, int pad_mode, hipStream_t s) {
+    if (F <= 0 || n_streams <= 0) return hipSuccess;
+    if (n_streams > 65535 || F * N > (int64_t(1) << 40)) return hipErrorInvalidValue;
+    const dim3 grid(unsigned((F * N + 255) / 256), unsigned(n_streams));
+    hipLaunchKernelGGL(k_fq_frames, grid, dim3(256), 0, s, x, T, ld_x, frames, F, N, H, pad, pad_mode);
+    return hipGetLastError();
+}
 
 hipError_t launch_deinterleave(const float* x, int64_t ld_x, float* planes, int groups, int64_t T, int C,
                                hipStream_t s) {

@@ -47,6 +47,7 @@ extern "C" {
 #define CRLOT_EHIP (-3)         /* HIP runtime error */
 #define CRLOT_ENOMEM (-4)       /* allocation failed (reference: std::bad_alloc) */
 #define CRLOT_ERUNTIME (-5)     /* reference: std::runtime_error */
+#define CRLOT_ERANGE (-6)       /* reference: std::out_of_range */
 
 /* dsp::WindowType (WindowLUT.h:14-20) */
 #define CRLOT_WIN_HANN 0
@@ -234,6 +235,29 @@ int crlot_fft_inverse_complex(crlot_fft_plan* plan, const float* d_in_complex, f
                               int32_t batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
                               int64_t inc_out, void* stream);
 
+/* Host-pointer forms of the four transforms: the reference's own calling
+ * convention (IFftPlan::forward(const float*, complex<float>*, batch) etc.),
+ * synchronous, data in host memory, same semantics and layout parameters as
+ * the device forms.  Power-of-two plans (real nfft 256..4096, complex
+ * 128..2048) run on a resident server kernel owned by the plan (call_rt.hip):
+ * no kernel launch and no copy-engine transfer per call, the input written into
+ * fine-grained device memory through the BAR, the result written by the kernel
+ * into pinned host memory.  After a real forward of batch <= 4 the server also
+ * runs the inverse of the spectrum it returned; an inverse called next with
+ * exactly those bits (memcmp) is served from that result (bit-identical to
+ * running it).  The server exits after 20 ms without a call.  Other sizes stage
+ * through device buffers and a launch. */
+int crlot_fft_forward_host(crlot_fft_plan* plan, const float* in, float* out_complex, int32_t batch,
+                           int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out);
+int crlot_fft_inverse_host(crlot_fft_plan* plan, const float* in_complex, float* out, int32_t batch,
+                           int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out);
+int crlot_fft_forward_complex_host(crlot_fft_plan* plan, const float* in_complex, float* out_complex,
+                                   int32_t batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                                   int64_t inc_out);
+int crlot_fft_inverse_complex_host(crlot_fft_plan* plan, const float* in_complex, float* out_complex,
+                                   int32_t batch, int64_t ld_in, int64_t inc_in, int64_t ld_out,
+                                   int64_t inc_out);
+
 /* ---------------------------------------------------------------- streaming
  * Low-latency per-hop path (BASELINE config 4): `channels` independent
  * channels, Framer in DROP mode fed H samples per channel per call
@@ -326,11 +350,15 @@ int crlot_framer_info(const crlot_framer* f, int64_t* frame_size, int64_t* hop_s
  * behaves as the reference's.  Per-sample arithmetic is the reference's scalar
  * kernels (kernels.cc:18-36): fma(fma(x, w, 0), gain, acc) or fma(x, gain, acc);
  * out = acc / (norm > eps ? norm : eps), acc = 0.
- * Two call forms: host pointers (the reference's signatures; staged through
- * pinned memory on the object's own stream, produce() returns when the samples
- * are in the caller's buffers) and _device forms on caller-owned HBM with a
- * stream (NULL = the object's stream); calls on different streams are ordered
- * by the object.  Null pointers fail with CRLOT_EINVAL and the reference's
+ * Two call forms: host pointers (the reference's signatures) run on a resident
+ * server kernel owned by the object (call_rt.hip): an add is posted without
+ * waiting, produce() returns when the samples are in the caller's buffers; after
+ * each add the server also computes the produce(n) block the object predicts
+ * (n of the previous produce, H before the first), without clearing, and a
+ * produce asking for exactly that block is served from it (the ring is cleared
+ * by a request behind it).  _device forms run on caller-owned HBM with a stream
+ * (NULL = the object's stream); calls on different streams, and switches between
+ * the two forms, are ordered by the object.  Null pointers fail with CRLOT_EINVAL and the reference's
  * messages.  Not thread-safe (as the reference). */
 typedef struct crlot_ola crlot_ola;
 typedef struct crlot_ola_config { /* dsp::OLAConfig (OLAAccumulator.h:15-29) */
@@ -375,6 +403,55 @@ int crlot_ola_meter_peak(crlot_ola* o, float* peak);
 int crlot_ola_norm_table(const crlot_ola* o, float* out);
 /* wait for everything issued on the object */
 int crlot_ola_synchronize(crlot_ola* o);
+
+/* ---------------------------------------------------------------- OLA kernels
+ * dsp::axpy / axpy_windowed / normalize_and_clear (ola/kernels.h:28-53; scalar
+ * forms kernels.cc:18-36, which the Highway forms match) as batched device
+ * entries: `batch` rows of n elements, row b of dst / src / out / acc at
+ * + b*ld; the window (axpy_windowed) and the norm row (normalize_and_clear) are
+ * one row of n shared by every row.  Per element, bit-exact with the reference:
+ *   axpy               dst = fma(src, g, dst)
+ *   axpy_windowed      dst = fma(fma(src, win, 0), g, dst)
+ *   normalize_and_clear out = acc / (norm > eps ? norm : eps), acc = 0
+ * batch <= 65535.
+ * crlot_call_*: the reference's host-pointer signatures (n elements in host
+ * memory, synchronous), run on a per-device resident server kernel
+ * (call_rt.hip); normalize_and_clear also zeroes acc, as the reference. */
+int crlot_axpy(float* d_dst, const float* d_src, float g, int64_t n, int64_t batch, int64_t ld_dst,
+               int64_t ld_src, void* stream);
+int crlot_axpy_windowed(float* d_dst, const float* d_src, const float* d_win, float g, int64_t n,
+                        int64_t batch, int64_t ld_dst, int64_t ld_src, void* stream);
+int crlot_normalize_and_clear(float* d_out, float* d_acc, const float* d_norm, float eps, int64_t n,
+                              int64_t batch, int64_t ld_out, int64_t ld_acc, void* stream);
+int crlot_call_axpy(float* dst, const float* src, float g, int64_t n);
+int crlot_call_axpy_windowed(float* dst, const float* src, const float* win, float g, int64_t n);
+int crlot_call_normalize_and_clear(float* out, float* acc, const float* norm, float eps, int64_t n);
+
+/* ---------------------------------------------------------------- FrameQueue
+ * dsp::FrameQueue (FrameQueue.h:35-59, FrameQueue.cc:9-115, Indexing.h:18-70):
+ * all frames of a whole signal, padded by N/2 on both sides when `center`
+ * (CRLOT_PAD_CONSTANT zeros / REFLECT reflect-101 / EDGE), frame k = padded
+ * samples [k*H, k*H + N), count floor((len + pad - max(N - H, 0)) / H) on the
+ * padded length.  The object builds the frames on the device at construction
+ * (device_frames: [num_frames][N] in HBM) and keeps the reference's AoS host
+ * copy for frame / copy_frame / all_frames.  Errors: CRLOT_EINVAL with the
+ * reference's std::invalid_argument messages, CRLOT_ERANGE for a frame index
+ * out of range (std::out_of_range; crlot_framequeue_frame returns NULL).
+ * crlot_framequeue_frames is the batched device form: n_streams streams of T
+ * samples at d_x + s*ld_x -> d_frames [s][count][frame_size]. */
+typedef struct crlot_framequeue crlot_framequeue;
+int64_t crlot_framequeue_count(int64_t T, int64_t frame_size, int64_t hop_size, int32_t center);
+int crlot_framequeue_frames(const float* d_x, int32_t n_streams, int64_t T, int64_t ld_x, int64_t frame_size,
+                            int64_t hop_size, int32_t center, int32_t pad_mode, float* d_frames, void* stream);
+int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, int64_t hop_size, int32_t center,
+                            int32_t pad_mode, int32_t device, crlot_framequeue** out);
+void crlot_framequeue_destroy(crlot_framequeue* q);
+int crlot_framequeue_info(const crlot_framequeue* q, int64_t* num_frames, int64_t* frame_size,
+                          int64_t* hop_size);
+const float* crlot_framequeue_frame(const crlot_framequeue* q, int64_t frame_idx);
+int crlot_framequeue_copy_frame(const crlot_framequeue* q, int64_t frame_idx, float* out);
+const float* crlot_framequeue_all_frames(const crlot_framequeue* q);
+const float* crlot_framequeue_device_frames(const crlot_framequeue* q);
 
 /* ---------------------------------------------------------------- WAV I/O
  * io/wav.{h,cc} (WavReader / WavWriter over dr_wav): RIFF WAVE, 1 or 2

@@ -2,6 +2,9 @@
 //
 // Mirrors the reference's C++ API for the hot path so C++ callers drop in:
 //   crlot::dsp::Framer             <- dsp::Framer           (framer.h:26-127)
+//   crlot::dsp::FrameQueue         <- dsp::FrameQueue       (FrameQueue.h:35-59), device-built frames
+//   crlot::dsp::axpy / axpy_windowed / normalize_and_clear
+//                                  <- dsp/ola/kernels.h:28-53 (+ batched _device forms)
 //   crlot::dsp::OLAConfig          <- dsp::OLAConfig        (OLAAccumulator.h:15-29)
 //   crlot::dsp::OLAAccumulator     <- dsp::OLAAccumulator   (OLAAccumulator.h:63-217), device rings
 //   crlot::dsp::WindowLUT          <- dsp::WindowLUT        (WindowLUT.h:80-287), incl. the
@@ -21,8 +24,11 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
+#include <exception>
 #include <complex>
 #include <cstdint>
 #include <memory>
@@ -42,6 +48,7 @@ inline void check(int rc, const char* what) {
     std::string msg = std::string(what) + ": " + crlot_last_error();
     if (rc == CRLOT_EINVAL) throw std::invalid_argument(msg);
     if (rc == CRLOT_ENOMEM) throw std::bad_alloc();
+    if (rc == CRLOT_ERANGE) throw std::out_of_range(msg);
     throw std::runtime_error(msg);
 }
 
@@ -589,6 +596,92 @@ class OLAAccumulator {
     crlot_ola* o_ = nullptr;
 };
 
+// dsp::PadMode (FrameQueue.h:8-12)
+enum class PadMode { CONSTANT, REFLECT, EDGE };
+
+// dsp::FrameQueue (FrameQueue.h:35-59): every frame of a whole signal, built on
+// the device at construction (crlot_framequeue_*).  getFrame / copyFrame /
+// getAllFrames read the reference's AoS host copy; device_frames() is the same
+// [num_frames][frame_size] block in HBM.  Throws as the reference:
+// std::invalid_argument on zero sizes or a null input with len > 0,
+// std::out_of_range on a frame index past the end.
+class FrameQueue {
+   public:
+    FrameQueue(const float* in, size_t len, size_t frame_size, size_t hop_size, bool center = true,
+               PadMode pad_mode = PadMode::CONSTANT, int device = -1) {
+        const int rc = crlot_framequeue_create(in, int64_t(len), int64_t(frame_size), int64_t(hop_size),
+                                               center ? 1 : 0, int32_t(pad_mode), device, &q_);
+        if (rc != CRLOT_OK) check(rc, "FrameQueue");
+        check(crlot_framequeue_info(q_, &f_, &n_, &h_), "FrameQueue");
+        const float* a = crlot_framequeue_all_frames(q_);
+        frames_.assign(a, a + size_t(f_ * n_));
+    }
+    ~FrameQueue() { crlot_framequeue_destroy(q_); }
+    FrameQueue(const FrameQueue&) = delete;
+    FrameQueue& operator=(const FrameQueue&) = delete;
+    size_t getNumFrames() const { return size_t(f_); }
+    size_t getFrameSize() const { return size_t(n_); }
+    size_t getHopSize() const { return size_t(h_); }
+    const float* getFrame(size_t frame_idx) const {
+        if (frame_idx >= size_t(f_)) throw std::out_of_range("Frame index out of range");
+        return frames_.data() + frame_idx * size_t(n_);
+    }
+    void copyFrame(size_t frame_idx, float* output) const {
+        if (frame_idx >= size_t(f_)) throw std::out_of_range("Frame index out of range");
+        if (output == nullptr) throw std::invalid_argument("Output buffer cannot be null");
+        const float* f = frames_.data() + frame_idx * size_t(n_);
+        std::copy(f, f + n_, output);
+    }
+    const std::vector<float>& getAllFrames() const { return frames_; }
+    const float* device_frames() const { return crlot_framequeue_device_frames(q_); }
+
+   private:
+    crlot_framequeue* q_ = nullptr;
+    int64_t f_ = 0, n_ = 0, h_ = 0;
+    std::vector<float> frames_;
+};
+
+// dsp::axpy / axpy_windowed / normalize_and_clear (kernels.h:28-53): the
+// reference's noexcept host-pointer signatures, run on the device (a resident
+// call kernel, crlot_call_*).  A device failure cannot be reported through a
+// noexcept signature: it terminates, as an exception escaping one would.
+namespace detail {
+[[noreturn]] inline void kernel_failed(const char* what) noexcept {
+    std::fprintf(stderr, "crlot::dsp::%s failed: %s\n", what, crlot_last_error());
+    std::terminate();
+}
+}  // namespace detail
+inline void axpy(float* dst, const float* src, float g, size_t n) noexcept {
+    if (crlot_call_axpy(dst, src, g, int64_t(n)) != CRLOT_OK) detail::kernel_failed("axpy");
+}
+inline void axpy_windowed(float* dst, const float* src, const float* win, float g, size_t n) noexcept {
+    if (crlot_call_axpy_windowed(dst, src, win, g, int64_t(n)) != CRLOT_OK) detail::kernel_failed("axpy_windowed");
+}
+inline void normalize_and_clear(float* out, float* acc, const float* norm, float eps, size_t n) noexcept {
+    if (crlot_call_normalize_and_clear(out, acc, norm, eps, int64_t(n)) != CRLOT_OK)
+        detail::kernel_failed("normalize_and_clear");
+}
+// batched device forms: `batch` rows of n at + b*ld, the window / norm row shared
+inline void axpy_device(float* d_dst, const float* d_src, float g, size_t n, size_t batch = 1, size_t ld_dst = 0,
+                        size_t ld_src = 0, hipStream_t s = nullptr) {
+    check(crlot_axpy(d_dst, d_src, g, int64_t(n), int64_t(batch), int64_t(ld_dst ? ld_dst : n),
+                     int64_t(ld_src ? ld_src : n), s),
+          "axpy_device");
+}
+inline void axpy_windowed_device(float* d_dst, const float* d_src, const float* d_win, float g, size_t n,
+                                 size_t batch = 1, size_t ld_dst = 0, size_t ld_src = 0, hipStream_t s = nullptr) {
+    check(crlot_axpy_windowed(d_dst, d_src, d_win, g, int64_t(n), int64_t(batch), int64_t(ld_dst ? ld_dst : n),
+                              int64_t(ld_src ? ld_src : n), s),
+          "axpy_windowed_device");
+}
+inline void normalize_and_clear_device(float* d_out, float* d_acc, const float* d_norm, float eps, size_t n,
+                                       size_t batch = 1, size_t ld_out = 0, size_t ld_acc = 0,
+                                       hipStream_t s = nullptr) {
+    check(crlot_normalize_and_clear(d_out, d_acc, d_norm, eps, int64_t(n), int64_t(batch),
+                                    int64_t(ld_out ? ld_out : n), int64_t(ld_acc ? ld_acc : n), s),
+          "normalize_and_clear_device");
+}
+
 namespace fft {
 
 enum class FftDomain { Real, Complex };
@@ -624,9 +717,10 @@ class IFftPlan {
 // Batch b starts at b*stride*len, element i sits at i*stride (len = nfft, or
 // nfft/2+1 for the real spectrum).  Validation mirrors KissFftPlan
 // (kissfft_adapter.cc:13-63) except the batch ceiling, which the device path
-// does not need (MakeFftPlan below applies it).  Host pointers are staged
-// through device buffers owned by the plan, so calls are not reentrant (as in
-// the reference, whose plan owns scratch).
+// does not need (MakeFftPlan below applies it).  Host pointers go to the plan's
+// resident call kernel (crlot_fft_*_host: no launch or copy-engine transfer per
+// call); calls on one plan are serialised, as the reference's plan owns scratch.
+// forward_device / inverse_device take HBM pointers and a stream.
 class HipFftPlan final : public IFftPlan {
    public:
     explicit HipFftPlan(const FftPlanDesc& d) : d_(validate(d)) {
@@ -644,8 +738,8 @@ class HipFftPlan final : public IFftPlan {
         const int64_t n = d_.nfft, bins = n / 2 + 1;
         run(in, 1, span(batch, d_.stride_in, n), reinterpret_cast<float*>(out), 2, span(batch, d_.stride_out, bins),
             [&](const float* i, float* o) {
-                return crlot_fft_forward(p_, i, o, batch, d_.stride_in * n, d_.stride_in,
-                                         2 * d_.stride_out * bins, d_.stride_out, nullptr);
+                return crlot_fft_forward_host(p_, i, o, batch, d_.stride_in * n, d_.stride_in,
+                                              2 * d_.stride_out * bins, d_.stride_out);
             });
     }
     void inverse(const std::complex<float>* in, float* out, int batch = 1) override {
@@ -655,8 +749,8 @@ class HipFftPlan final : public IFftPlan {
         const int64_t n = d_.nfft, bins = n / 2 + 1;
         run(reinterpret_cast<const float*>(in), 2, span(batch, d_.stride_in, bins), out, 1,
             span(batch, d_.stride_out, n), [&](const float* i, float* o) {
-                return crlot_fft_inverse(p_, i, o, batch, 2 * d_.stride_in * bins, d_.stride_in,
-                                         d_.stride_out * n, d_.stride_out, nullptr);
+                return crlot_fft_inverse_host(p_, i, o, batch, 2 * d_.stride_in * bins, d_.stride_in,
+                                              d_.stride_out * n, d_.stride_out);
             });
     }
     void forward_complex(const std::complex<float>* in, std::complex<float>* out, int batch = 1) override {
@@ -668,6 +762,17 @@ class HipFftPlan final : public IFftPlan {
     FftDomain domain() const override { return d_.domain; }
     int size() const override { return d_.nfft; }
     crlot_fft_plan* handle() const { return p_; }
+    // device forms: any batch, dense rows (ld = nfft floats in, nfft/2+1 pairs out)
+    void forward_device(const float* d_in, std::complex<float>* d_out, int batch, hipStream_t s = nullptr) {
+        const int64_t n = d_.nfft, bins = n / 2 + 1;
+        check(crlot_fft_forward(p_, d_in, reinterpret_cast<float*>(d_out), batch, n, 1, 2 * bins, 1, s),
+              "forward_device");
+    }
+    void inverse_device(const std::complex<float>* d_in, float* d_out, int batch, hipStream_t s = nullptr) {
+        const int64_t n = d_.nfft, bins = n / 2 + 1;
+        check(crlot_fft_inverse(p_, reinterpret_cast<const float*>(d_in), d_out, batch, 2 * bins, 1, n, 1, s),
+              "inverse_device");
+    }
 
    private:
     static FftPlanDesc validate(const FftPlanDesc& d) {
@@ -695,27 +800,20 @@ class HipFftPlan final : public IFftPlan {
         const int64_t n = d_.nfft;
         run(reinterpret_cast<const float*>(in), 2, span(batch, d_.stride_in, n),
             reinterpret_cast<float*>(out), 2, span(batch, d_.stride_out, n), [&](const float* i, float* o) {
-                return (inv ? crlot_fft_inverse_complex : crlot_fft_forward_complex)(
+                return (inv ? crlot_fft_inverse_complex_host : crlot_fft_forward_complex_host)(
                     p_, i, o, batch, 2 * d_.stride_in * n, d_.stride_in, 2 * d_.stride_out * n,
-                    d_.stride_out, nullptr);
+                    d_.stride_out);
             });
     }
-    // stage host -> device, launch, device -> host.  The reference writes only
-    // the strided output elements, so the device output starts as a copy of the
-    // caller's buffer.
+    // host pointers straight to the plan's host-call path (crlot_fft_*_host:
+    // the resident call kernel; the reference writes only the strided output
+    // elements, and so do these)
     template <typename F>
-    void run(const float* in, int in_w, int64_t in_elems, float* out, int out_w, int64_t out_elems, F launch) {
-        const size_t in_f = size_t(in_w) * in_elems, out_f = size_t(out_w) * out_elems;
-        din_.resize(in_f);
-        dout_.resize(out_f);
-        hip_check(hipMemcpy(din_.get(), in, sizeof(float) * in_f, hipMemcpyHostToDevice), "hipMemcpy");
-        hip_check(hipMemcpy(dout_.get(), out, sizeof(float) * out_f, hipMemcpyHostToDevice), "hipMemcpy");
-        check(launch(din_.get(), dout_.get()), "fft");
-        hip_check(hipMemcpy(out, dout_.get(), sizeof(float) * out_f, hipMemcpyDeviceToHost), "hipMemcpy");
+    void run(const float* in, int, int64_t, float* out, int, int64_t, F launch) {
+        check(launch(in, out), "fft");
     }
     FftPlanDesc d_;
     crlot_fft_plan* p_ = nullptr;
-    DeviceBuffer<float> din_, dout_;
 };
 using HipRealFftPlan = HipFftPlan;  // earlier name
 

@@ -49,6 +49,12 @@ def lib(native: bool = False):
     L.or_ring_len.restype = sz
     L.or_build_norm_linear.argtypes = [_f32p, _f32p, sz, sz, sz]
     L.or_init_normalization.argtypes = [_f32p, C.c_void_p, sz, sz, sz, C.c_int, C.c_float]
+    L.or_axpy.argtypes = [_f32p, _f32p, C.c_float, sz]
+    L.or_axpy.restype = None
+    L.or_axpy_windowed.argtypes = [_f32p, _f32p, _f32p, C.c_float, sz]
+    L.or_axpy_windowed.restype = None
+    L.or_normalize_and_clear.argtypes = [_f32p, _f32p, _f32p, C.c_float, sz]
+    L.or_normalize_and_clear.restype = None
     L.or_framer_new.argtypes = [sz, sz, sz, C.c_int]
     L.or_framer_new.restype = C.c_void_p
     L.or_framer_free.argtypes = [C.c_void_p]
@@ -358,6 +364,25 @@ def roundtrip_batch(x2d, n, h, wtype=HANN, periodic=False, mode=ZERO_PAD, nthrea
 
 def fq_count(T, n, h, center=True):
     return int(lib().or_fq_count(T, n, h, int(center)))
+
+
+def axpy(dst, src, g, win=None):
+    """dsp::axpy_scalar / axpy_windowed_scalar (kernels.cc:18-28) on copies; returns dst'."""
+    d = np.array(dst, np.float32, copy=True)
+    s = np.ascontiguousarray(src, np.float32)
+    if win is None:
+        lib().or_axpy(d, s, g, d.size)
+    else:
+        lib().or_axpy_windowed(d, s, np.ascontiguousarray(win, np.float32), g, d.size)
+    return d
+
+
+def normalize_and_clear(acc, norm, eps):
+    """dsp::normalize_and_clear_scalar (kernels.cc:30-36): returns (out, acc')."""
+    a = np.array(acc, np.float32, copy=True)
+    out = np.zeros_like(a)
+    lib().or_normalize_and_clear(out, a, np.ascontiguousarray(norm, np.float32), eps, a.size)
+    return out, a
 
 
 def fq_frames(x, n, h, center=True, pad_mode=PAD_CONSTANT):

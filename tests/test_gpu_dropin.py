@@ -1,0 +1,278 @@
+"""The reference's remaining drop-in surfaces on the device, against the oracle:
+
+* dsp::axpy / axpy_windowed / normalize_and_clear (ola/kernels.h:28-53): the
+  batched device forms and the host-pointer forms (resident call kernel),
+  BIT-EXACT with the scalar kernels (kernels.cc:18-36) -- the reference's own
+  bar is +-1 ULP between its Highway and scalar forms (tests/kernels_test.cc:
+  214-429) -- at the reference test's sizes {0, 1, 7, ..., 4096} and at a
+  batched size, plus kernels_test.cc's known values;
+* dsp::FrameQueue (FrameQueue.h:35-59): the object and the batched device form,
+  BIT-EXACT against the 48 fixtures dumped from the reference's own compiled
+  FrameQueue.cc (tests/golden/ref_tables.npz fq_*), its exceptions;
+* IFftPlan host-pointer calls on the resident call kernel: bit-identical to the
+  launched device kernels (the same arithmetic), speculation hits and misses,
+  strides, both domains, the staged fallback for other sizes; within the parity
+  tolerance of the kissfft restatement.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [0, 1, 7, 8, 15, 16, 31, 32, 63, 64, 127, 128, 255, 256, 511, 512, 1023, 1024, 4096]
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------------ OLA kernels
+def test_kernels_known_values(pkg, torch_cuda):
+    """kernels_test.cc:67-207 values through the host-pointer forms."""
+    dst = np.ones(10, np.float32)
+    pkg.axpy_host(dst, np.full(10, 2, np.float32), 0.5)
+    assert np.all(dst == 2.0)
+    dst = np.ones(10, np.float32)
+    pkg.axpy_host(dst, np.full(10, 2, np.float32), 0.0)
+    assert np.all(dst == 1.0)
+    dst = np.ones(1000, np.float32)
+    pkg.axpy_host(dst, np.full(1000, 2, np.float32), 0.5)
+    assert np.all(dst == 2.0)
+    dst = np.ones(10, np.float32)
+    pkg.axpy_host(dst, np.full(10, 2, np.float32), 1.0, win=np.full(10, 0.5, np.float32))
+    assert np.all(dst == 2.0)
+    acc = np.full(10, 4, np.float32)
+    out = np.zeros(10, np.float32)
+    pkg.normalize_and_clear_host(out, acc, np.full(10, 2, np.float32), 1e-8)
+    assert np.all(out == 2.0) and np.all(acc == 0.0)
+    acc = np.full(10, 1, np.float32)
+    pkg.normalize_and_clear_host(out, acc, np.zeros(10, np.float32), 1e-3)  # eps guard
+    assert np.all(out == np.float32(1.0) / np.float32(1e-3))
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_kernels_bit_exact_vs_scalar(pkg, oracle, torch_cuda, n):
+    torch = torch_cuda
+    rng = np.random.default_rng(42 + n)  # kernels_test.cc:219 mt19937(42), U(-10, 10)
+    d, s, w = (rng.uniform(-10, 10, n).astype(np.float32) for _ in range(3))
+    nrm = rng.uniform(-1, 3, n).astype(np.float32)  # some below eps
+    nrm[::5] = 0.0
+    for g in (1.0, 0.5, -1.75):
+        want = oracle.axpy(d, s, g)
+        want_w = oracle.axpy(d, s, g, win=w)
+        # host-pointer forms (resident call kernel)
+        a = d.copy()
+        pkg.axpy_host(a, s, g)
+        assert np.array_equal(bits(a), bits(want)), (n, g)
+        a = d.copy()
+        pkg.axpy_host(a, s, g, win=w)
+        assert np.array_equal(bits(a), bits(want_w)), (n, g)
+        if n == 0:
+            continue
+        # device forms, one row
+        dd = dev(torch, d)
+        pkg.axpy(dd, dev(torch, s), g)
+        assert np.array_equal(bits(host(dd)), bits(want)), (n, g)
+        dd = dev(torch, d)
+        pkg.axpy(dd, dev(torch, s), g, win=dev(torch, w))
+        assert np.array_equal(bits(host(dd)), bits(want_w)), (n, g)
+    out_w, acc_w = oracle.normalize_and_clear(d, nrm, 0.25)
+    out, acc = np.zeros(n, np.float32), d.copy()
+    pkg.normalize_and_clear_host(out, acc, nrm, 0.25)
+    assert np.array_equal(bits(out), bits(out_w)) and np.array_equal(acc, acc_w)
+    if n:
+        do, da = dev(torch, np.zeros(n, np.float32)), dev(torch, d)
+        pkg.normalize_and_clear(do, da, dev(torch, nrm), 0.25)
+        assert np.array_equal(bits(host(do)), bits(out_w)) and np.all(host(da) == 0)
+
+
+def test_kernels_batched_rows_and_leading_dims(pkg, oracle, torch_cuda):
+    """Batched device forms: B rows with padded leading dimensions (scalar and
+    16-byte paths), the shared window / norm row, against the scalar kernels."""
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    for B, n, ld in ((64, 1024, 1024), (33, 1000, 1003), (5, 4096, 4100)):
+        d = rng.uniform(-10, 10, (B, ld)).astype(np.float32)
+        s = rng.uniform(-10, 10, (B, ld)).astype(np.float32)
+        w = rng.uniform(0, 1, n).astype(np.float32)
+        nrm = rng.uniform(0, 4, n).astype(np.float32)
+        dd = dev(torch, d)
+        pkg.axpy(dd[:, :n], dev(torch, s)[:, :n], 0.5, win=dev(torch, w))
+        got = host(dd)
+        for b in range(B):
+            assert np.array_equal(bits(got[b, :n]), bits(oracle.axpy(d[b, :n], s[b, :n], 0.5, win=w))), (B, n, b)
+        assert np.array_equal(got[:, n:], d[:, n:])  # padding untouched
+        da = dev(torch, d)
+        do = torch.zeros((B, ld), dtype=torch.float32, device="cuda")
+        pkg.normalize_and_clear(do[:, :n], da[:, :n], dev(torch, nrm), 1e-8)
+        go, ga = host(do), host(da)
+        for b in range(B):
+            ow, aw = oracle.normalize_and_clear(d[b, :n], nrm, 1e-8)
+            assert np.array_equal(bits(go[b, :n]), bits(ow)) and np.array_equal(ga[b, :n], aw)
+        assert np.array_equal(ga[:, n:], d[:, n:])
+
+
+# ------------------------------------------------------------------ FrameQueue
+def _fq_cases(ref_tables):
+    for key in sorted(ref_tables.files):
+        if key.startswith("fq_") and key.endswith("_meta"):
+            base = key[:-5]
+            T, N, H, c, m, F = (int(v) for v in ref_tables[key])
+            yield base, T, N, H, c, m, F
+
+
+def test_framequeue_object_bit_exact_vs_reference(pkg, torch_cuda, ref_tables):
+    """All 48 fixtures of the reference's compiled FrameQueue (3 pad modes, centre
+    on / off, signals shorter than the pad, T = 0): counts and every frame."""
+    torch = torch_cuda
+    cases = 0
+    for base, T, N, H, c, m, F in _fq_cases(ref_tables):
+        x = ref_tables[base + "_x"]
+        want = ref_tables[base + "_frames"]
+        q = pkg.FrameQueue(x, N, H, center=bool(c), pad_mode=m)
+        assert q.getNumFrames() == F and q.getFrameSize() == N and q.getHopSize() == H, base
+        assert np.array_equal(bits(q.getAllFrames()), bits(want)), base
+        for k in {0, F // 2, F - 1} if F else ():
+            assert np.array_equal(bits(q.getFrame(k)), bits(want[k * N:(k + 1) * N])), (base, k)
+            buf = np.zeros(N, np.float32)
+            q.copyFrame(k, buf)
+            assert np.array_equal(bits(buf), bits(want[k * N:(k + 1) * N]))
+        with pytest.raises(IndexError):
+            q.getFrame(F)
+        # the batched device form, two copies of the stream, padded rows
+        if T:
+            xd = torch.zeros((2, T + 3), dtype=torch.float32, device="cuda")
+            xd[:, :T] = dev(torch, x)
+            fr = host(pkg.framequeue_frames(xd[:, :T], N, H, center=bool(c), pad_mode=m))
+            assert fr.shape == (2, F, N)
+            for s in range(2):
+                assert np.array_equal(bits(fr[s].reshape(-1)), bits(want)), base
+        cases += 1
+    assert cases == 48
+
+
+def test_framequeue_errors(pkg, torch_cuda):
+    """FrameQueue.cc:13-22, 49-67: the reference's exceptions."""
+    x = np.arange(100, dtype=np.float32)
+    with pytest.raises(ValueError):
+        pkg.FrameQueue(x, 0, 4)
+    with pytest.raises(ValueError):
+        pkg.FrameQueue(x, 8, 0)
+    with pytest.raises(ValueError):  # null input with len > 0
+        pkg._check(pkg.lib().crlot_framequeue_create(None, 5, 8, 4, 1, 0, -1, pkg.C.byref(pkg.C.c_void_p())))
+    q = pkg.FrameQueue(x, 16, 4, center=True)
+    with pytest.raises(IndexError):
+        q.copyFrame(q.getNumFrames(), np.zeros(16, np.float32))
+    with pytest.raises(ValueError):
+        q.copyFrame(0, None)
+    e = pkg.FrameQueue(np.zeros(0, np.float32), 16, 4, center=False)
+    assert e.getNumFrames() == 0 and e.getAllFrames().size == 0
+
+
+# ------------------------------------------------------------------ IFftPlan host calls
+@pytest.mark.parametrize("nfft", [256, 512, 1024, 2048, 4096])
+def test_fft_host_calls_equal_device_kernels(pkg, oracle, torch_cuda, nfft):
+    """forward_host / inverse_host (resident call kernel) give the launched device
+    kernels' bits; an unchanged spectrum takes the speculated inverse, a changed
+    one a real call -- both the device inverse's bits; the kissfft restatement
+    agrees within the parity tolerance."""
+    torch = torch_cuda
+    rng = np.random.default_rng(nfft)
+    plan = pkg.FftPlan(nfft)
+    for B in (1, 3, 4, 16):
+        x = rng.standard_normal((B, nfft)).astype(np.float32)
+        X = plan.forward_host(x)
+        Xd = host(plan.forward(dev(torch, x)))
+        assert np.array_equal(X.view(np.uint32), Xd.view(np.uint32)), (nfft, B)
+        ref = oracle.bench_rfft(x, nfft)
+        assert np.linalg.norm(X - ref) <= 1e-6 * np.linalg.norm(ref)
+        y_dev = host(plan.inverse(dev(torch, X)))
+        y = plan.inverse_host(X)  # speculation hit (batch <= 4, nfft <= 2048) or a real call
+        assert np.array_equal(bits(y), bits(y_dev)), (nfft, B)
+        X2 = X.copy()
+        X2[:, 3] *= 2.0  # a processed spectrum: the speculation must not serve it
+        plan.forward_host(x)
+        y2 = plan.inverse_host(X2)
+        assert np.array_equal(bits(y2), bits(host(plan.inverse(dev(torch, X2))))), (nfft, B)
+        # another call between forward and inverse also voids the speculation
+        plan.forward_host(x)
+        plan.forward_host(x[::-1].copy())
+        y3 = plan.inverse_host(X)
+        assert np.array_equal(bits(y3), bits(y_dev)), (nfft, B)
+
+
+def test_fft_host_strides_complex_and_fallback(pkg, oracle, torch_cuda):
+    """The reference's stride semantics (kissfft_adapter.cc:97-98, 139-140): batch b
+    at b*stride*len, element i at i*stride, untouched elements kept; the complex
+    domain; a size without a call-kernel instantiation (staged launches)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(9)
+    n, B, st = 1024, 4, 2
+    plan = pkg.FftPlan(n)
+    x = rng.standard_normal((B, n * st)).astype(np.float32)
+    out = np.full((B, (n // 2 + 1) * st), 7 + 7j, np.complex64)
+    plan.forward_host(x, out=out, inc_in=st, inc_out=st)
+    dense = plan.forward_host(np.ascontiguousarray(x[:, ::st]))
+    assert np.array_equal(np.ascontiguousarray(out[:, ::st]).view(np.uint32), dense.view(np.uint32))
+    assert np.all(out[:, 1::st] == 7 + 7j)
+    yo = np.full((B, n * st), -3, np.float32)
+    plan.inverse_host(np.ascontiguousarray(out[:, ::st]), out=yo, inc_out=st)
+    assert np.array_equal(bits(yo[:, ::st]), bits(host(plan.inverse(dev(torch, dense)))))
+    assert np.all(yo[:, 1::st] == -3)
+    for nc in (128, 512, 2048, 100):
+        cp = pkg.FftPlan(nc, domain=pkg.FFT_COMPLEX)
+        z = (rng.standard_normal((3, nc)) + 1j * rng.standard_normal((3, nc))).astype(np.complex64)
+        Z = cp.forward_complex_host(z)
+        assert np.array_equal(Z.view(np.uint32), host(cp.forward_complex(dev(torch, z))).view(np.uint32)), nc
+        zi = cp.inverse_complex_host(Z)
+        assert np.array_equal(zi.view(np.uint32), host(cp.inverse_complex(dev(torch, Z))).view(np.uint32)), nc
+        assert np.linalg.norm(zi - z) <= 1e-5 * np.linalg.norm(z), nc
+    p960 = pkg.FftPlan(960)  # mixed radix: staged launches
+    x = rng.standard_normal((2, 960)).astype(np.float32)
+    X = p960.forward_host(x)
+    assert np.array_equal(X.view(np.uint32), host(p960.forward(dev(torch, x))).view(np.uint32))
+    assert np.array_equal(bits(p960.inverse_host(X)), bits(host(p960.inverse(dev(torch, X)))))
+    with pytest.raises(RuntimeError):
+        plan.forward_complex_host(np.zeros((1, n), np.complex64))
+
+
+def test_ola_host_calls_speculated_produce(pkg, oracle, torch_cuda):
+    """OLAAccumulator host calls on the call kernel: produce(H) after every push
+    (served from the block speculated after the push), produce with other counts
+    (real calls), host / device-form calls interleaved on one object -- all
+    bit-identical to the oracle's OLAAccumulator restatement."""
+    torch = torch_cuda
+    n, h, C = 1024, 256, 2
+    rng = np.random.default_rng(21)
+    w = oracle.window(oracle.HANN, n)
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=C, eps=1e-8,
+                        apply_window_inside=True)
+    ola = pkg.OLAAccumulator(cfg)
+    ola.set_window(w)
+    ref = oracle.Ola(n, h, C, eps=1e-8, inside=True)
+    ref.set_window(w)
+    outs, refs = [], []
+    for k in range(60):
+        fr = rng.standard_normal((n, C)).astype(np.float32)
+        if k % 7 == 3:  # a device-form push in between
+            ola.push_frame_AoS_device(dev(torch, fr), None, k * h, 0, n, 1.0)
+        else:
+            ola.push_frame_AoS(fr, None, k * h, 0, n, 1.0)
+        ref.push_frame_aos(fr, k * h, 0, n, 1.0)
+        m = h if k % 5 else (h // 2 if k % 10 else 3 * h)
+        got, chans = ola.produce(m)
+        outs.append([c[:got] for c in chans])
+        refs.append(ref.produce(m))
+    for a, b in zip(outs, refs):
+        assert len(a) == len(b)
+        for ca, cb in zip(a, b):
+            assert ca.shape == cb.shape and np.array_equal(bits(ca), bits(cb))
+    assert ola.produced_samples() == ref.produced and ola.read_pos() == ref.read_pos
