@@ -416,7 +416,108 @@ def suite_multichannel(pkg, torch, dev):
     return res
 
 
-SUITES = {"ola": suite_ola, "multichannel": suite_multichannel, "fft": suite_fft, "streaming": suite_streaming, "config1": suite_config1}
+def _harness(name, *args, timeout=300):
+    exe = os.path.join(ROOT, "harness", name)
+    r = subprocess.run([exe, *[str(a) for a in args]], capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"{name} failed ({r.returncode}): {r.stdout[-500:]} {r.stderr[-1500:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _cpu_loop_us(O, native, x, n, h, reps=5, **ex):
+    """Median seconds of the oracle's per-stream C loop (the reference's Framer /
+    window / forward / inverse / push / produce chain, one thread) on x."""
+    L = O.lib(native)
+    T = x.size
+    mode = ex.get("mode", O.ZERO_PAD)
+    F = O.frames_for(T, n, h, mode, ex.get("center", True))
+    y = np.zeros(max(F * h, 1), np.float32)
+    ts = []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        if ex:
+            L.or_roundtrip_ex(x, T, n, h, O.HANN, 0, mode, int(ex.get("center", True)), O.PAD_CONSTANT,
+                              int(ex.get("analysis_window", True)), y, F * h, None, None)
+        else:
+            L.or_roundtrip(x, T, n, h, O.HANN, 0, O.ZERO_PAD, y, F * h, None, None)
+        ts.append(time.perf_counter() - t0)
+    ts = sorted(ts[1:])
+    return ts[len(ts) // 2] * 1e6, F
+
+
+def suite_e2e(pkg, torch, dev):
+    """bench/e2e_benchmark.cc counterpart: the per-frame drop-in loop through the
+    C++ classes (harness/e2e_bench: Framer -> window -> IFftPlan::forward ->
+    inverse -> push_frame_AoS -> produce, on the resident call kernels) at the
+    harness's hop 512 and at 256, with the oracle's single-thread C loop of the
+    same chain on the same 1 s, 3-tone input beside it."""
+    O, native = _oracle()
+    res = {"suite": "e2e", "reference": "bench/e2e_benchmark.cc", "runs": []}
+    t = np.arange(48000) / 48000.0
+    x = (0.5 * np.sin(2 * np.pi * 440 * t) + 0.3 * np.sin(2 * np.pi * 880 * t)
+         + 0.2 * np.sin(2 * np.pi * 1320 * t)).astype(np.float32)
+    for h in (256, 512):
+        g = _harness("e2e_bench", h, 200)
+        cpu_us, F = _cpu_loop_us(O, native, x, 1024, h)
+        g["cpu_oracle_1thread"] = {"ms_per_iteration": round(cpu_us / 1e3, 4), "us_per_frame": round(cpu_us / F, 3),
+                                   "x_realtime": round(1e6 / cpu_us, 1)}
+        res["runs"].append(g)
+    res["cpu_native_build"] = native
+    return res
+
+
+def suite_kernels(pkg, torch, dev):
+    """bench/micro_kernels_benchmark.cc + bench/kernels_benchmark.cc counterparts
+    (harness/kernels_bench: host-pointer calls on the call kernel per size, the
+    OLA push / pull calls, the batched device forms against HBM), with the
+    oracle's scalar kernels timed per call in C beside them."""
+    O, native = _oracle()
+    res = {"suite": "kernels", **_harness("kernels_bench", 2000)}
+    cpu = []
+    for n in (16, 32, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768):
+        reps = max(2000, int(2e7 / n))
+        cpu.append({"n": n, **{k: round(O.bench_kernel(op, n, reps, native=native) * 1e6, 4)
+                               for op, k in enumerate(("axpy", "axpy_windowed", "normalize_and_clear"))}})
+    res["cpu_oracle_us_per_call_1thread"] = cpu
+    res["cpu_native_build"] = native
+    return res
+
+
+def suite_pipeline(pkg, torch, dev):
+    """bench/performance_benchmark.cc:174-246 (IntegratedPipelinePerformance)
+    counterparts: the per-frame loop through the drop-in classes
+    (harness/pipeline_bench: FrameQueue(x, 16384, 1024, 512, centre) ->
+    forward -> inverse -> add_frame_SoA(window) -> produce(hop)), and the
+    GPU-native batched form of the same pipeline (crlot_roundtrip with
+    FrameQueue framing, no analysis window) on 1024 streams x 480 000 samples,
+    the oracle's single-thread C loop beside both."""
+    O, native = _oracle()
+    res = {"suite": "pipeline", "reference": "bench/performance_benchmark.cc:174-246",
+           "per_frame": _harness("pipeline_bench", 200)}
+    x16 = np.random.default_rng(42).standard_normal(16384).astype(np.float32)
+    cpu_us, F = _cpu_loop_us(O, native, x16, 1024, 512, mode=O.FRAMEQUEUE, center=True, analysis_window=False)
+    res["per_frame"]["cpu_oracle_1thread"] = {"us_per_iteration": round(cpu_us, 2), "frames": F,
+                                              "us_per_frame": round(cpu_us / F, 3)}
+    plan = pkg.Plan(frame_size=1024, hop_size=512, boundary_mode=pkg.FRAMEQUEUE, analysis_window=False,
+                    device=dev.index)
+    S, T = STREAMS, T_LEN
+    g = torch.Generator(device=dev).manual_seed(31)
+    xb = torch.rand((S, T), generator=g, device=dev) - 0.5
+    yb = torch.empty((S, plan.output_length(T)), device=dev)
+    ms = _ev_time(torch, lambda: plan.roundtrip(xb, yb), 20)
+    xs = O.synth(T, 7)
+    cpu1, _ = _cpu_loop_us(O, native, xs, 1024, 512, reps=3, mode=O.FRAMEQUEUE, center=True, analysis_window=False)
+    res["batched"] = {"streams": S, "samples_per_stream": T, "frame": 1024, "hop": 512,
+                      "framing": "FrameQueue centre, constant pad, no analysis window",
+                      "gpu_ms": round(ms, 4), "gpu_msamples_s": round(S * T / ms / 1e3, 1),
+                      "hbm_frac": round(8 * S * T / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "cpu_oracle_msamples_s_1thread": round(T / cpu1, 3)}
+    res["cpu_native_build"] = native
+    return res
+
+
+SUITES = {"ola": suite_ola, "multichannel": suite_multichannel, "fft": suite_fft, "streaming": suite_streaming,
+          "config1": suite_config1, "e2e": suite_e2e, "kernels": suite_kernels, "pipeline": suite_pipeline}
 
 
 def run_suite(name):

@@ -102,7 +102,8 @@ int CallServer::create(int device, int e, int depth, size_t in_cap, size_t out_c
 }
 
 int CallServer::alloc(size_t in_cap, size_t out_cap, size_t spec_cap) {
-    in_cap_ = align_up(std::max<size_t>(in_cap, 64), 32);
+    // >= 1024 floats: the kernel fetches the first 4 KB of a slot with its descriptor
+    in_cap_ = align_up(std::max<size_t>(in_cap, 1024), 32);
     out_cap_ = align_up(std::max<size_t>(out_cap, 64), 32);
     spec_cap_ = align_up(spec_cap, 32);
     const size_t dbytes = sizeof(CallCtl) + sizeof(CallReq) * size_t(depth_) + sizeof(float) * in_cap_ * depth_;
@@ -178,6 +179,7 @@ int CallServer::launch() {
     a.in_arena = reinterpret_cast<const float*>(ddev_ + sizeof(CallCtl) + sizeof(CallReq) * size_t(depth_));
     a.out_arena = reinterpret_cast<float*>(hctl_dev_ + sizeof(CallHostCtl));
     a.depth = depth_;
+    a.in_cap = int64_t(in_cap_);
     a.first = load_acq(&hctl_->done);
     a.idle_ticks = idle_ticks_;
     store_ctl(&ctl_->stop, 0);

@@ -50,6 +50,7 @@ class CallServer {
     uint64_t submitted() const { return q_; }
     uint64_t done() const { return __atomic_load_n(&hctl_->done, __ATOMIC_ACQUIRE); }
     int device() const { return device_; }
+    const CallHostCtl* host_ctl() const { return hctl_; }  // diagnostics (phase stamps)
 
    private:
     CallServer() = default;

@@ -38,6 +38,29 @@ namespace {
 
 constexpr int kCallBlock = 256;
 constexpr int kCallWaves = kCallBlock / 64;
+// the first kCallPre floats of a request's input slot are fetched together with
+// its descriptor (the slot's place is known before the descriptor is read), so a
+// call of up to 4 KB of input pays one memory latency, not two
+constexpr int kCallPre = 4 * kCallBlock;
+
+// input float i (and i + 1) of the request: from the prefetched copy in LDS
+// when the whole input fits it (PRE, decided once per request), else memory
+template <bool PRE>
+struct CallIn {
+    const float* mem;
+    const float* pre;
+    __device__ __forceinline__ float at(int64_t i) const { return PRE ? pre[i] : ld_sys32_(mem + i); }
+    __device__ __forceinline__ float2 at2(int64_t i) const {
+        if constexpr (PRE) return *reinterpret_cast<const float2*>(pre + i);
+        const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(mem + i), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+        return make_float2(__uint_as_float(uint32_t(v)), __uint_as_float(uint32_t(v >> 32)));
+    }
+    __device__ static __forceinline__ float ld_sys32_(const float* p) {
+        return __uint_as_float(
+            __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+};
 
 // fine-grained device memory written by the host (relaxed system-scope loads:
 // straight from memory, nothing kept in L2) and host memory written by us
@@ -65,8 +88,8 @@ struct CallLds {
     static constexpr int TW = E > 0 ? dev::twiddle_table_size(E) : 1;
     static constexpr bool SPEC = E > 0 && E <= 16;
     static constexpr int SP = SPEC ? P + 1 : 0;
-    static constexpr size_t bytes =
-        sizeof(cf) * (size_t(TW) + 2 * P + size_t(kCallWaves) * (P + SP)) + sizeof(CallReq) + 16;
+    static constexpr size_t bytes = sizeof(cf) * (size_t(TW) + 2 * P + size_t(kCallWaves) * (P + SP)) +
+                                    sizeof(float) * kCallPre + sizeof(CallReq) + 16;
 };
 
 // ---- FFTs, one wave per transform (k_rfft / k_irfft / k_cfft's arithmetic)
@@ -78,14 +101,14 @@ __device__ __forceinline__ void rfft_core(cf (&v)[E], cf* buf, const cf* tw, int
 // forward real FFT of in[0..N) (dense, fine-grained device memory) into the
 // spectrum sp[0..P] (cf, host memory); the spectrum also stays in `buf`+regs
 // for the speculative inverse: xs[m] = X[lane + 64 m], xp0 = X[P] (lane 0)
-template <int E>
-__device__ __forceinline__ void call_rfft(const float* in, float* sp, cf* buf, const cf* tw, const cf* sth,
-                                          int lane, cf (&xs)[E], cf& xpp) {
+template <int E, bool PRE>
+__device__ __forceinline__ void call_rfft(const CallIn<PRE>& in, int64_t off, float* sp, cf* buf, const cf* tw,
+                                          const cf* sth, int lane, cf (&xs)[E], cf& xpp) {
     constexpr int P = 64 * E;
     cf v[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        const float2 x2 = ld_sys2(in + 2 * (lane + 64 * m));
+        const float2 x2 = in.at2(off + 2 * (lane + 64 * m));
         v[m].r = dev::sanit(x2.x);
         v[m].i = dev::sanit(x2.y);
     }
@@ -141,13 +164,13 @@ __device__ __forceinline__ void call_irfft(G get, float* out, cf* buf, const cf*
     }
 }
 
-template <int E, bool INV>
-__device__ __forceinline__ void call_cfft(const float* in, float* out, cf* buf, const cf* tw, float inv_p,
-                                          int lane) {
+template <int E, bool INV, bool PRE>
+__device__ __forceinline__ void call_cfft(const CallIn<PRE>& in, int64_t off, float* out, cf* buf, const cf* tw,
+                                          float inv_p, int lane) {
     cf v[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        const float2 x2 = ld_sys2(in + 2 * (lane + 64 * m));
+        const float2 x2 = in.at2(off + 2 * (lane + 64 * m));
         v[m] = {x2.x, x2.y};
     }
     dev::fft_wave<E, INV>(v, buf, tw, lane);
@@ -171,7 +194,8 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     cf* sth = st + P;
     cf* bufs = sth + P;
     cf* specs = bufs + kCallWaves * P;
-    CallReq* rq = reinterpret_cast<CallReq*>(specs + kCallWaves * CallLds<E>::SP);
+    float* pre = reinterpret_cast<float*>(specs + kCallWaves * CallLds<E>::SP);
+    CallReq* rq = reinterpret_cast<CallReq*>(pre + kCallPre);
     uint32_t* cmd = reinterpret_cast<uint32_t*>(rq + 1);
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -196,23 +220,59 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                     __hip_atomic_store(&ctl->stop, uint64_t(2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
             }
             cmd[0] = k;
         }
         __syncthreads();
         if (cmd[0] == 0) break;
-        // the descriptor: 16 lanes x 8 bytes into LDS
-        const CallReq* src = a.reqs + (my % uint64_t(a.depth));
-        if (t < 16)
-            reinterpret_cast<uint64_t*>(rq)[t] = ld_sys64(reinterpret_cast<const uint64_t*>(src) + t);
+        // the descriptor (16 lanes x 8 bytes) and the first 4 KB of the slot's input,
+        // requested together
+        const int slot = int(my % uint64_t(a.depth));
+        const CallReq* src = a.reqs + slot;
+        {
+            const uint64_t* pin = reinterpret_cast<const uint64_t*>(a.in_arena + int64_t(slot) * a.in_cap);
+            const uint64_t v0 = ld_sys64(pin + t), v1 = ld_sys64(pin + kCallBlock + t);
+            if (t < 16)
+                reinterpret_cast<uint64_t*>(rq)[t] = ld_sys64(reinterpret_cast<const uint64_t*>(src) + t);
+            reinterpret_cast<uint64_t*>(pre)[t] = v0;
+            reinterpret_cast<uint64_t*>(pre)[kCallBlock + t] = v1;
+        }
         __syncthreads();
-        const CallReq r = *rq;
+#ifdef CRLOT_CALL_PHASES
+        const uint64_t ph0 = wall_clock64();
+#define CALL_PH(i) if (t == 0) a.hctl->ph[i] = wall_clock64() - ph0
+#else
+#define CALL_PH(i)
+#endif
+        // the descriptor into scalar registers: every branch on it is uniform
+        CallReq r;
+        {
+            const uint32_t* s = reinterpret_cast<const uint32_t*>(rq);
+            uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+            for (int i = 0; i < int(sizeof(CallReq) / 4); ++i) d[i] = __builtin_amdgcn_readfirstlane(s[i]);
+        }
         if (r.flags & kCallAcquire)  // device-form calls ran on streams since the last request
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const float* in = a.in_arena + r.in_off;
+        const float* in = a.in_arena + r.in_off;  // r.in_off is the slot's start
+        // the input floats this request reads: when they fit the prefetched 4 KB,
+        // every read comes from LDS
+        const int64_t need = r.op == kCallOlaAdd ? r.i[2] * r.channels + (r.win_off >= 0 ? r.i[2] : 0)
+                             : r.op == kCallRfft ? int64_t(r.batch) * 2 * P
+                             : r.op == kCallIrfft ? int64_t(r.batch) * (2 * P + 2)
+                             : (r.op == kCallCfft || r.op == kCallIcfft) ? int64_t(r.batch) * 2 * P
+                             : (r.op == kCallAxpy || r.op == kCallNormalize) ? 2 * r.i[0]
+                             : r.op == kCallAxpyWin ? 3 * r.i[0] : 0;
+        const bool pre_all = need <= kCallPre;
         float* out = a.out_arena + r.out_off;
         bool spec = false;
+        // body(cin) with the input reader of this request
+        auto with_in = [&](auto body) {
+            if (pre_all)
+                body(CallIn<true>{in, pre});
+            else
+                body(CallIn<false>{in, pre});
+        };
 
         if constexpr (E > 0) {
             if (r.op >= kCallRfft && r.op <= kCallIcfft && r.p0 != staged_tw) {
@@ -231,56 +291,110 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             if (r.op == kCallRfft) {
                 // speculation keeps each wave's spectrum in LDS: one transform per wave
                 spec = CallLds<E>::SPEC && (r.flags & kCallSpec) != 0 && r.batch <= kCallWaves;
+                with_in([&](const auto& cin) {
                 for (int b = wave; b < r.batch; b += kCallWaves) {
                     cf xs[E > 0 ? E : 1];
                     cf xpp;
                     float* sp = out + int64_t(b) * (2 * P + 2);
-                    call_rfft<E>(in + int64_t(b) * 2 * P, sp, buf, tw, sth, lane, xs, xpp);
+                    call_rfft<E>(cin, int64_t(b) * 2 * P, sp, buf, tw, sth, lane, xs, xpp);
                     if (CallLds<E>::SPEC && spec) {
 #pragma unroll
                         for (int m = 0; m < E; ++m) spb[lane + 64 * m] = xs[m];
                         if (lane == 0) spb[P] = xpp;
                     }
                 }
+                });
             } else if (r.op == kCallIrfft) {
+                with_in([&](const auto& cin) {
                 for (int b = wave; b < r.batch; b += kCallWaves) {
-                    const float* x = in + int64_t(b) * (2 * P + 2);
+                    const int64_t x = int64_t(b) * (2 * P + 2);
                     call_irfft<E>([&](int k) {
-                        const float2 v = ld_sys2(x + 2 * k);
+                        const float2 v = cin.at2(x + 2 * k);
                         return cf{v.x, v.y};
                     }, out + int64_t(b) * 2 * P, buf, tw, st, r.f0, lane);
                 }
+                });
             } else if (r.op == kCallCfft || r.op == kCallIcfft) {
+                with_in([&](const auto& cin) {
                 for (int b = wave; b < r.batch; b += kCallWaves) {
                     if (r.op == kCallCfft)
-                        call_cfft<E, false>(in + int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
+                        call_cfft<E, false>(cin, int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
                     else
-                        call_cfft<E, true>(in + int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
+                        call_cfft<E, true>(cin, int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
                 }
+                });
             }
         }
         if (r.op == kCallOlaAdd) {
-            // add_frame_SoA / push_frame_AoS (ola.hip k_ola_add): channel c element j
-            // at in[c*cs + j*js]; window from the request (caller's) or the object
+            // add_frame_SoA / push_frame_AoS (ola.hip k_ola_add): element e = channel-major
+            // for SoA frames, interleaved for AoS; window from the request (caller's) or
+            // the object.  K elements per thread per pass, every load of a pass issued
+            // before its first store.  With speculation, an element that lands in the
+            // predicted produce block [srp, srp + sn) also writes its quotient to the
+            // speculation slot (the sum it just formed / den), and the block's positions
+            // the add does not touch are read afterwards.
+            constexpr int K = 8;
             float* ring = r.p2;
+            const float* den = r.p1;
             const int64_t R = r.i[0], start = r.i[1], len = r.i[2], C = r.channels;
             const bool aos = r.i[3] != 0;
-            const float* wreq = r.win_off >= 0 ? a.in_arena + r.win_off : nullptr;
+            const int64_t woff = r.win_off >= 0 ? r.win_off - r.in_off : -1;  // the window slice, in the slot
             const float* wobj = r.p0;
-            for (int64_t e = t; e < len * C; e += kCallBlock) {
-                const int64_t c = e / len, j = e - c * len;
-                int64_t p = start + j;
-                if (p >= R) p -= R;
-                float* rr = ring + c * R + p;
-                const float s = ld_sys32(in + (aos ? j * C + c : c * len + j));
-                if (wreq || wobj) {
-                    const float w = wreq ? ld_sys32(wreq + j) : wobj[j];
-                    *rr = __builtin_fmaf(__builtin_fmaf(s, w, 0.0f), r.f0, *rr);
-                } else {
-                    *rr = __builtin_fmaf(s, r.f0, *rr);
+            const bool win = woff >= 0 || wobj;
+            spec = (r.flags & kCallSpec) != 0;
+            const int64_t srp = r.i[4], sn = spec ? r.i[5] : 0;
+            float* so = a.out_arena + r.spec_off;
+            // channels outer, samples inner: no division per element; inactive lanes load
+            // a clamped (valid) element and store nothing
+            with_in([&](const auto& cin) {
+            for (int64_t c = 0; c < C; ++c) {
+                for (int64_t jb = 0; jb < len; jb += int64_t(kCallBlock) * K) {
+                    float s[K], w[K], acc[K], dv[K];
+                    int64_t at[K], sj[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int64_t jr = jb + int64_t(k) * kCallBlock + t;
+                        const bool ok = jr < len;
+                        const int64_t j = ok ? jr : len - 1;
+                        int64_t p = start + j;
+                        if (p >= R) p -= R;
+                        at[k] = c * R + p;
+                        int64_t q = p - srp;  // offset in the speculated block
+                        if (q < 0) q += R;
+                        sj[k] = (ok && q < sn) ? c * sn + q : -1;
+                        s[k] = cin.at(aos ? j * C + c : c * len + j);
+                        w[k] = woff >= 0 ? cin.at(woff + j) : wobj ? wobj[j] : 1.0f;
+                        acc[k] = ring[at[k]];
+                        dv[k] = den[p];
+                        if (!ok) at[k] = -1;
+                    }
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        if (at[k] < 0) continue;
+                        const float v = win ? __builtin_fmaf(__builtin_fmaf(s[k], w[k], 0.0f), r.f0, acc[k])
+                                            : __builtin_fmaf(s[k], r.f0, acc[k]);
+#ifdef CRLOT_CALL_NT_RING
+                        __builtin_nontemporal_store(v, ring + at[k]);
+#else
+                        ring[at[k]] = v;
+#endif
+                        if (sj[k] >= 0) so[sj[k]] = v / dv[k];
+                    }
                 }
             }
-            spec = (r.flags & kCallSpec) != 0;
+            });
+            if (spec) {
+                // block positions outside this add: the ring as it stands
+                for (int64_t c = 0; c < C; ++c)
+                    for (int64_t q = t; q < sn; q += kCallBlock) {
+                        int64_t p = srp + q;
+                        if (p >= R) p -= R;
+                        int64_t d = p - start;  // inside [start, start + len) was written above
+                        if (d < 0) d += R;
+                        if (d < len) continue;
+                        so[c * sn + q] = ring[c * R + p] / den[p];
+                    }
+            }
         } else if (r.op == kCallOlaProduce) {
             // produce -> normalize_and_clear (ola.hip k_ola_produce), or the clear
             // alone for a produce already served from the speculation slot
@@ -288,38 +402,70 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             const float* den = r.p1;
             const int64_t R = r.i[0], rp = r.i[1], len = r.i[2], C = r.channels;
             const bool clear_only = (r.flags & kCallClearOnly) != 0;
-            for (int64_t e = t; e < len * C; e += kCallBlock) {
-                const int64_t c = e / len, j = e - c * len;
-                int64_t p = rp + j;
-                if (p >= R) p -= R;
-                float* rr = ring + c * R + p;
-                if (!clear_only) out[c * len + j] = *rr / den[p];
-                *rr = 0.0f;
-            }
+            for (int64_t c = 0; c < C; ++c)
+                for (int64_t j = t; j < len; j += kCallBlock) {
+                    int64_t p = rp + j;
+                    if (p >= R) p -= R;
+                    float* rr = ring + c * R + p;
+                    if (!clear_only) out[c * len + j] = *rr / den[p];
+                    *rr = 0.0f;
+                }
         } else if (r.op == kCallAxpy || r.op == kCallAxpyWin) {
             // dsp::axpy / axpy_windowed (kernels.cc:18-28): in = dst | src [| win]
+            constexpr int K = 8;
             const int64_t n = r.i[0];
-            for (int64_t j = t; j < n; j += kCallBlock) {
-                const float d = ld_sys32(in + j), s = ld_sys32(in + n + j);
-                const float x = r.op == kCallAxpyWin ? __builtin_fmaf(s, ld_sys32(in + 2 * n + j), 0.0f) : s;
-                out[j] = __builtin_fmaf(x, r.f0, d);
+            with_in([&](const auto& cin) {
+            for (int64_t base = 0; base < n; base += int64_t(kCallBlock) * K) {
+                float d[K], s[K], w[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int64_t j = base + int64_t(k) * kCallBlock + t;
+                    const bool ok = j < n;
+                    d[k] = ok ? cin.at(j) : 0.0f;
+                    s[k] = ok ? cin.at(n + j) : 0.0f;
+                    w[k] = ok && r.op == kCallAxpyWin ? cin.at(2 * n + j) : 0.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int64_t j = base + int64_t(k) * kCallBlock + t;
+                    if (j >= n) continue;
+                    const float x = r.op == kCallAxpyWin ? __builtin_fmaf(s[k], w[k], 0.0f) : s[k];
+                    out[j] = __builtin_fmaf(x, r.f0, d[k]);
+                }
             }
+            });
         } else if (r.op == kCallNormalize) {
             // dsp::normalize_and_clear (kernels.cc:30-36): in = acc | norm; out = out | acc
+            constexpr int K = 8;
             const int64_t n = r.i[0];
-            for (int64_t j = t; j < n; j += kCallBlock) {
-                const float ac = ld_sys32(in + j), nv = ld_sys32(in + n + j);
-                out[j] = ac / ((nv > r.f0) ? nv : r.f0);
-                out[n + j] = 0.0f;
+            with_in([&](const auto& cin) {
+            for (int64_t base = 0; base < n; base += int64_t(kCallBlock) * K) {
+                float ac[K], nv[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int64_t j = base + int64_t(k) * kCallBlock + t;
+                    ac[k] = j < n ? cin.at(j) : 0.0f;
+                    nv[k] = j < n ? cin.at(n + j) : 1.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int64_t j = base + int64_t(k) * kCallBlock + t;
+                    if (j >= n) continue;
+                    out[j] = ac[k] / ((nv[k] > r.f0) ? nv[k] : r.f0);
+                    out[n + j] = 0.0f;
+                }
             }
+            });
         }
 
         // ---- publish: results visible system-wide, then done.  An add's only
         // reader is its speculated produce: it publishes once, with the speculation.
+        CALL_PH(0);
         my += 1;
         const bool merged = spec && r.op == kCallOlaAdd;
         if (!merged) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            CALL_PH(1);
             __syncthreads();
             if (t == 0) st_sys64(&a.hctl->done, my);
         }
@@ -337,20 +483,9 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                                       lane);
                 }
             }
-            if (r.op == kCallOlaAdd) {
-                // the produce(n) the host predicts, without the clear
-                float* ring = r.p2;
-                const float* den = r.p1;
-                const int64_t R = r.i[0], rp = r.i[4], len = r.i[5], C = r.channels;
-                __syncthreads();  // every add of this request is in the ring
-                for (int64_t e = t; e < len * C; e += kCallBlock) {
-                    const int64_t c = e / len, j = e - c * len;
-                    int64_t p = rp + j;
-                    if (p >= R) p -= R;
-                    so[c * len + j] = ring[c * R + p] / den[p];
-                }
-            }
+            CALL_PH(2);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            CALL_PH(3);
             __syncthreads();
             if (t == 0) {
                 if (merged) st_sys64(&a.hctl->done, my);

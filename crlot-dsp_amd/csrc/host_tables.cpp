@@ -8,7 +8,8 @@
 //            + dsp::ola::build_norm_linear (norm_builder.cc:8-52)
 //
 // Bit-exactness against the reference's compiled sources is checked by
-// tests/test_host_tables.py on the fixtures in tests/golden/.  This file is built
+// tests/test_host_abi.py (test_window_tables_bit_exact_vs_reference,
+// test_norm_tables_bit_exact_vs_reference) on tests/golden/ref_tables.npz.  This file is built
 // with -ffp-contract=off: the reference builds these translation units as ISO
 // C++17 where GCC 11 keeps each double operation separately rounded.
 #include <cmath>

@@ -231,6 +231,7 @@ struct alignas(64) CallHostCtl {  // pinned host memory, written by the kernel
     uint64_t pad0[7];
     uint64_t spec_done;           // requests whose speculation slot is written
     uint64_t pad1[7];
+    uint64_t ph[8];               // -DCRLOT_CALL_PHASES builds: the last request's phase stamps
 };
 struct CallArgs {
     CallCtl* ctl = nullptr;
@@ -239,6 +240,7 @@ struct CallArgs {
     const float* in_arena = nullptr;
     float* out_arena = nullptr;     // pinned host memory
     int depth = 0;
+    int64_t in_cap = 0;             // floats per input slot (slot q % depth at q * in_cap)
     uint64_t first = 0;             // requests completed before this launch
     uint64_t idle_ticks = 0;
 };

@@ -559,13 +559,19 @@ int pair_waves_per_cu() {
     return std::min(int(163840 / PairLds<kPairWaves>::bytes) * kPairWaves, 4 * CRLOT_PAIR_MIN_WAVES);
 }
 
-// CRLOT_PAIR_NOFIX=1 (diagnostics: how much the fix-up walker redoes) skips it.
+// Diagnostic builds only (-DCRLOT_PAIR_NOFIX_DIAG, e.g. `make variant`):
+// CRLOT_PAIR_NOFIX=1 then skips the fix-up walker to time how much it redoes,
+// leaving flagged chunks wrong.  The release library always runs it.
 bool pair_nofix() {
+#ifdef CRLOT_PAIR_NOFIX_DIAG
     static const bool v = [] {
         const char* e = std::getenv("CRLOT_PAIR_NOFIX");
         return e && e[0] == '1';
     }();
     return v;
+#else
+    return false;
+#endif
 }
 
 // The paired-only walker where it holds its registers without spilling: hops

@@ -1,0 +1,112 @@
+// pipeline_bench: counterpart of the reference's integrated pipeline,
+// bench/performance_benchmark.cc:174-246 (IntegratedPipelinePerformance),
+// written against the drop-in classes of include/crlot_dsp.hpp as the
+// reference writes it against dsp::*: per iteration
+//   FrameQueue(x, 16384, 1024, 512, center = true)        (:181)
+//   WindowLUT::GetWindowSafe(HANN, 1024); OLAAccumulator(apply_window_inside)
+//   MakeFftPlan(Real, 1024)
+//   per frame: copy -> forward -> inverse -> add_frame_SoA(window, i*hop)  (:213-229)
+//   produce(hop) until 16384 samples                                       (:232-240)
+// The reference pushes every frame before producing, which aliases its ring
+// once 16384 + 512 > ring; this counterpart times that literal
+// order ("literal") and the streaming-interleaved one ("interleaved": produce
+// after each add, the semantics the batched engine implements).
+// Usage: pipeline_bench [iterations=200]
+#include <algorithm>
+#include <chrono>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../include/crlot_dsp.hpp"
+
+using namespace crlot::dsp;
+using namespace crlot::dsp::fft;
+using clk = std::chrono::steady_clock;
+
+static double p50(std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v.empty() ? 0.0 : v[v.size() / 2];
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 200;
+    const size_t L = 16384, N = 1024, H = 512;
+    std::vector<float> x(L);
+    std::mt19937 gen(42);
+    std::normal_distribution<float> dist(0.0f, 1.0f);
+    for (auto& v : x) v = dist(gen);
+    struct Times {
+        double total_us, loop_us;
+        size_t frames;
+    };
+    try {
+        auto run = [&](bool interleaved) -> Times {
+            const auto t0 = clk::now();
+            FrameQueue frames(x.data(), L, N, H, true);
+            auto window = WindowLUT::getInstance().GetWindowSafe(WindowType::HANN, N);
+            OLAConfig config;
+            config.sample_rate = 48000;
+            config.frame_size = N;
+            config.hop_size = H;
+            config.channels = 1;
+            config.eps = 1e-8f;
+            config.apply_window_inside = true;
+            OLAAccumulator ola(config);
+            ola.set_window(window.get(), int(N));
+            FftPlanDesc desc{FftDomain::Real, int(N), false, 1, 1, 1};
+            auto fft_plan = MakeFftPlan(desc);
+            std::vector<std::complex<float>> spectrum(N / 2 + 1);
+            std::vector<float> processed(N), output(L + N);
+            const auto t_loop = clk::now();
+            size_t total = 0;
+            float* ch_out[1] = {output.data()};
+            for (size_t i = 0; i < frames.getNumFrames(); ++i) {
+                const float* frame = frames.getFrame(i);
+                std::copy(frame, frame + N, processed.begin());
+                fft_plan->forward(processed.data(), spectrum.data());
+                fft_plan->inverse(spectrum.data(), processed.data());
+                const float* ch_frames[1] = {processed.data()};
+                ola.add_frame_SoA(ch_frames, window.get(), i * H, 0, N, 1.0f);
+                if (interleaved && total < L) {
+                    ch_out[0] = output.data() + total;
+                    total += ola.produce(ch_out, H);
+                }
+            }
+            while (total < L) {
+                ch_out[0] = output.data() + total;
+                const size_t s = ola.produce(ch_out, H);
+                if (s == 0) break;
+                total += s;
+            }
+            const auto t1 = clk::now();
+            return Times{std::chrono::duration<double, std::micro>(t1 - t0).count(),
+                         std::chrono::duration<double, std::micro>(t1 - t_loop).count(), frames.getNumFrames()};
+        };
+        for (int w = 0; w < 5; ++w) run(true);
+        std::vector<double> lit, ilv, lit_loop, ilv_loop;
+        size_t F = 0;
+        for (int i = 0; i < iters; ++i) {
+            const Times a = run(false), b = run(true);
+            lit.push_back(a.total_us);
+            ilv.push_back(b.total_us);
+            lit_loop.push_back(a.loop_us);
+            ilv_loop.push_back(b.loop_us);
+            F = a.frames;
+        }
+        // total: the reference's iteration (object construction included, :181-210);
+        // loop: the per-frame calls and the produce loop only
+        std::printf("{\"harness\": \"pipeline_bench\", \"reference\": \"bench/performance_benchmark.cc:174-246\", "
+                    "\"input_length\": %zu, \"frame\": %zu, \"hop\": %zu, \"frames\": %zu, \"iterations\": %d, "
+                    "\"literal\": {\"total_us_p50\": %.2f, \"loop_us_p50\": %.2f, \"loop_us_per_frame\": %.3f}, "
+                    "\"interleaved\": {\"total_us_p50\": %.2f, \"loop_us_p50\": %.2f, \"loop_us_per_frame\": %.3f}}\n",
+                    L, N, H, F, iters, p50(lit), p50(lit_loop), p50(lit_loop) / double(F), p50(ilv), p50(ilv_loop),
+                    p50(ilv_loop) / double(F));
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "exception: %s\n", e.what());
+        return 4;
+    }
+    return 0;
+}

@@ -1052,3 +1052,18 @@ void or_bench_rfft(int nfft, const float* x, int64_t B, float* out) {
     for (int64_t b = 0; b < B; ++b) or_adapter_forward(f, nfft, x + (size_t)b * nfft, out + (size_t)b * (nfft + 2));
     or_kfftr_free(f);
 }
+
+/* kernels_benchmark.cc / micro_kernels_benchmark.cc: `reps` calls of one scalar
+ * kernel (kernels.cc:18-36) on n elements (op 0 axpy, 1 axpy_windowed,
+ * 2 normalize_and_clear); the caller times the call. */
+void or_bench_kernel(int op, size_t n, int64_t reps, float* dst, const float* src, const float* win,
+                     float* out) {
+    for (int64_t r = 0; r < reps; ++r) {
+        if (op == 0)
+            or_axpy(dst, src, 0.5f, n);
+        else if (op == 1)
+            or_axpy_windowed(dst, src, win, 0.5f, n);
+        else
+            or_normalize_and_clear(out, dst, win, 1e-8f, n);
+    }
+}

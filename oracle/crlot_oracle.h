@@ -23,6 +23,7 @@
 #define CRLOT_ORACLE_H_
 
 #include <stddef.h>
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -82,6 +83,8 @@ void or_adapter_inverse_complex(or_kfft_cfg* inv, int nfft, const float* in, flo
 void or_axpy(float* dst, const float* src, float g, size_t n);
 void or_axpy_windowed(float* dst, const float* src, const float* win, float g, size_t n);
 void or_normalize_and_clear(float* out, float* acc, const float* norm, float eps, size_t n);
+void or_bench_kernel(int op, size_t n, int64_t reps, float* dst, const float* src, const float* win,
+                     float* out);
 
 /* ---- OLAAccumulator (OLAAccumulator.cc:13-295), channels SoA ---- */
 typedef struct or_ola or_ola;

@@ -49,6 +49,8 @@ def lib(native: bool = False):
     L.or_ring_len.restype = sz
     L.or_build_norm_linear.argtypes = [_f32p, _f32p, sz, sz, sz]
     L.or_init_normalization.argtypes = [_f32p, C.c_void_p, sz, sz, sz, C.c_int, C.c_float]
+    L.or_bench_kernel.argtypes = [C.c_int, sz, C.c_int64, _f32p, _f32p, _f32p, _f32p]
+    L.or_bench_kernel.restype = None
     L.or_axpy.argtypes = [_f32p, _f32p, C.c_float, sz]
     L.or_axpy.restype = None
     L.or_axpy_windowed.argtypes = [_f32p, _f32p, _f32p, C.c_float, sz]
@@ -375,6 +377,20 @@ def axpy(dst, src, g, win=None):
     else:
         lib().or_axpy_windowed(d, s, np.ascontiguousarray(win, np.float32), g, d.size)
     return d
+
+
+def bench_kernel(op, n, reps, native=False):
+    """Seconds per call of one scalar OLA kernel (0 axpy, 1 axpy_windowed,
+    2 normalize_and_clear) on n elements, timed over `reps` calls in C."""
+    import time
+    rng = np.random.default_rng(12345)
+    d, s = rng.uniform(-1, 1, n).astype(np.float32), rng.uniform(-1, 1, n).astype(np.float32)
+    w, o = rng.uniform(0.5, 1, n).astype(np.float32), np.zeros(n, np.float32)
+    L = lib(native)
+    L.or_bench_kernel(op, n, max(1, reps // 10), d, s, w, o)
+    t0 = time.perf_counter()
+    L.or_bench_kernel(op, n, reps, d, s, w, o)
+    return (time.perf_counter() - t0) / reps
 
 
 def normalize_and_clear(acc, norm, eps):
