@@ -885,66 +885,7 @@ struct crlot_fft_plan {
     size_t stage_floats = 0;
 };
 
-namespace {
-// One resident K_call<E> per (device, size), shared by the size's plans (so a
-// forward on one plan object and the inverse on another -- the reference's
-// e2e_benchmark uses one plan, multi-channel callers two -- share the
-// speculation), with its own copy of the size's FFT tables.
-struct FftCallShared {
-    std::mutex mu;
-    crlot::CallServer* srv = nullptr;
-    float* d_tw = nullptr;  // pass twiddles, super twiddles (device, owned)
-    float* d_st = nullptr;
-    struct Spec {           // the inverse speculated after the last forward
-        bool valid = false;
-        uint64_t index = 0;
-        int batch = 0;
-        crlot::CallSlot slot;
-    } spec;
-};
-std::mutex g_fft_shared_mu;
-FftCallShared* g_fft_shared[64][6] = {};  // [device][log2(E)]
 
-void stop_shared_servers() {
-    for (auto& row : g_fft_shared)
-        for (FftCallShared* s : row)
-            if (s && s->srv) (void)s->srv->stop();
-    crlot::stop_free_function_servers();
-}
-
-FftCallShared* fft_shared(const crlot_fft_plan* p, int* rc) {
-    const int dev = p->inner->device;
-    int lg = 0;
-    while ((2 << lg) < p->e) ++lg;  // e = 2, 4, ..., 32 -> 0..4
-    if (dev < 0 || dev >= 64 || lg > 5) {
-        *rc = fail(CRLOT_EUNSUPPORTED, "call server slot");
-        return nullptr;
-    }
-    std::lock_guard<std::mutex> lk(g_fft_shared_mu);
-    FftCallShared*& s = g_fft_shared[dev][lg];
-    if (!s) {
-        static const bool hooked = [] { return std::atexit(stop_shared_servers) == 0; }();
-        (void)hooked;
-        FftCallShared* n = new FftCallShared();
-        const int P = 64 * p->e;
-        const std::vector<float> tw = crlot::build_pass_twiddles(2 * P);
-        hipError_t e;
-        if ((e = hipMalloc(&n->d_tw, sizeof(float) * tw.size())) ||
-            (e = hipMalloc(&n->d_st, sizeof(float) * 2 * P)) ||
-            (e = hipMemcpy(n->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
-            (e = hipMemcpy(n->d_st, p->inner->d_st, sizeof(float) * 2 * P, hipMemcpyDeviceToDevice))) {
-            *rc = hip_fail(e, "call server tables");
-            return nullptr;
-        }
-        const size_t row = size_t(2 * P + 2) * 2;
-        *rc = crlot::CallServer::create(dev, p->e, 4, 4 * row, 4 * row, 4 * row, &n->srv);
-        if (*rc != CRLOT_OK) return nullptr;
-        s = n;
-    }
-    *rc = CRLOT_OK;
-    return s;
-}
-}  // namespace
 
 int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
     if (!d || !out) return fail(CRLOT_EINVAL, "null argument");
@@ -1142,21 +1083,28 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     const size_t nin = size_t(batch) * size_t(in_len * in_w), nout = size_t(batch) * size_t(out_len * out_w);
     p->pack.resize(std::max(nin, nout));
     gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
-    FftCallShared* sh = fft_shared(p, &rc);
+    crlot::SharedServer* sh = crlot::shared_server(p->inner->device, p->e, &rc);
     if (!sh) return rc;
     std::lock_guard<std::mutex> slk(sh->mu);
     crlot::CallServer* sv = sh->srv;
-    if (kind == 1 && sh->spec.valid && sh->spec.index == sv->submitted() && sh->spec.batch == batch &&
-        std::memcmp(p->pack.data(), sh->spec.slot.out, sizeof(float) * nin) == 0) {
+    if (kind == 1 && sh->fft.valid && sh->fft.index == sv->submitted() && sh->fft.batch == batch &&
+        std::memcmp(p->pack.data(), sh->fft.slot.out, sizeof(float) * nin) == 0) {
         // the spectrum the last forward returned, unchanged: its inverse is in the speculation slot
-        sh->spec.valid = false;
-        if ((rc = sv->wait_spec(sh->spec.index)) != CRLOT_OK) return rc;
-        scatter(sh->spec.slot.spec, out, batch, out_len, out_w, ld_out, inc_out);
+        sh->fft.valid = false;
+        if ((rc = sv->wait_spec(sh->fft.index)) != CRLOT_OK) return rc;
+        scatter(sh->fft.slot.spec, out, batch, out_len, out_w, ld_out, inc_out);
         return CRLOT_OK;
     }
-    sh->spec.valid = false;
+    sh->fft.valid = false;
+    sh->chain.valid = false;
     const bool spec = kind == 0 && batch <= 4 && p->e <= 16;
-    if ((rc = sv->grow(nin, nout, spec ? size_t(batch) * size_t(n) : 0)) != CRLOT_OK) return rc;
+    // chained speculation: a single frame whose inverse an OLA object pushed last time
+    crlot::ChainPred pred;
+    const bool chain = spec && batch == 1 && sh->target.predict && sh->target.predict(sh->target.owner, &pred) &&
+                       pred.N == n && pred.n > 0;
+    if ((rc = sv->grow(nin, nout, spec ? size_t(batch) * size_t(n) + (chain ? size_t(pred.n) : 0) : 0)) !=
+        CRLOT_OK)
+        return rc;
     crlot::CallSlot sl;
     if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
     sv->put(sl.in, p->pack.data(), nin);
@@ -1168,14 +1116,31 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     r.p1 = sh->d_st;
     r.f0 = kind < 2 ? p->inner->geo.inv_n : 1.0f / float(p->nfft);
     if (spec) r.flags = crlot::kCallSpec;
+    if (chain) {
+        r.flags |= crlot::kCallChain;
+        r.p2 = pred.ring;
+        r.p3 = pred.den;
+        r.p4 = pred.win;
+        r.j[0] = pred.R;
+        r.j[1] = pred.start % pred.R;
+        r.j[2] = pred.rp % pred.R;
+        r.j[3] = pred.n;
+        r.f1 = pred.gain;
+    }
     if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
     if ((rc = sv->wait(sl.index)) != CRLOT_OK) return rc;
     scatter(sl.out, out, batch, out_len, out_w, ld_out, inc_out);
     if (spec) {
-        sh->spec.valid = true;
-        sh->spec.index = sl.index;
-        sh->spec.batch = batch;
-        sh->spec.slot = sl;
+        sh->fft.valid = true;
+        sh->fft.index = sl.index;
+        sh->fft.batch = batch;
+        sh->fft.slot = sl;
+    }
+    if (chain) {
+        sh->chain.valid = true;
+        sh->chain.index = sl.index;
+        sh->chain.pred = pred;
+        sh->chain.slot = sl;
     }
     return CRLOT_OK;
 }

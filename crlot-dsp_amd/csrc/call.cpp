@@ -18,8 +18,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstring>
 #include <string>
+#include <vector>
 
 namespace crlot {
 int set_error(int code, const std::string& msg);  // abi.cpp
@@ -164,7 +166,7 @@ int CallServer::grow(size_t in_cap, size_t out_cap, size_t spec_cap) {
     rc = alloc(std::max(in_cap, in_cap_), std::max(out_cap, out_cap_), std::max(spec_cap, spec_cap_));
     if (rc != CRLOT_OK) return rc;
     q_ = q;
-    hctl_->done = hctl_->spec_done = q;
+    hctl_->done = hctl_->spec_done = hctl_->chain_done = q;
     store_ctl(&ctl_->seq, q);
     return CRLOT_OK;
 }
@@ -232,10 +234,40 @@ int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
     }
 }
 
-int CallServer::drain() {
-    if (q_ == 0) return CRLOT_OK;
-    int rc = wait_counter(&hctl_->done, q_);
+int CallServer::defer(const CallReq::Pend& p) {
+    const bool merge = pend_.flags == 0 ||
+                       (p.flags == kPendClear && pend_.flags == kPendCommit && pend_.ring == p.ring && pend_.R == p.R);
+    if (!merge) {
+        int rc = flush();
+        if (rc != CRLOT_OK) return rc;
+    }
+    if (pend_.flags == 0) {
+        pend_ = p;
+    } else {  // a clear behind the pending commit of the same ring
+        pend_.flags |= kPendClear;
+        pend_.rp = p.rp;
+        pend_.n = p.n;
+    }
+    return CRLOT_OK;
+}
+
+int CallServer::flush() {
+    if (pend_.flags == 0) return CRLOT_OK;
+    CallSlot sl;
+    int rc = next_slot(&sl);
     if (rc != CRLOT_OK) return rc;
+    CallReq r{};
+    r.op = 0;
+    r.win_off = -1;
+    return submit(r, sl);  // carries pend_
+}
+
+int CallServer::drain() {
+    int rc = flush();
+    if (rc != CRLOT_OK) return rc;
+    if (q_ == 0) return CRLOT_OK;
+    if ((rc = wait_counter(&hctl_->done, q_)) != CRLOT_OK) return rc;
+    if (last_chain_ && (rc = wait_counter(&hctl_->chain_done, last_chain_)) != CRLOT_OK) return rc;
     for (int i = 0; i < depth_; ++i)
         if (spec_req_[size_t(i)]) {
             rc = wait_counter(&hctl_->spec_done, spec_req_[size_t(i)]);
@@ -281,6 +313,9 @@ int CallServer::submit(CallReq& r, const CallSlot& sl) {
         r.flags |= kCallAcquire;
         acquire_next_ = false;
     }
+    r.pend = pend_;
+    pend_ = CallReq::Pend{};
+    if (r.flags & kCallChain) last_chain_ = q_ + 1;
     const int k = int(q_ % uint64_t(depth_));
     if (wc_inputs_)
         copy_wc(reinterpret_cast<float*>(reqs_ + k), reinterpret_cast<const float*>(&r), sizeof(CallReq) / 4);
@@ -302,6 +337,7 @@ int CallServer::submit(CallReq& r, const CallSlot& sl) {
 
 int CallServer::wait(uint64_t index) { return wait_counter(&hctl_->done, index); }
 int CallServer::wait_spec(uint64_t index) { return wait_counter(&hctl_->spec_done, index); }
+int CallServer::wait_chain(uint64_t index) { return wait_counter(&hctl_->chain_done, index); }
 
 // ------------------------------------------------------------------ shared servers
 // One E = 0 server per device for the free functions (dsp::axpy & co).
@@ -331,6 +367,57 @@ std::mutex& free_function_mutex() { return g_free_mu; }
 void stop_free_function_servers() {
     for (CallServer* s : g_free)
         if (s) (void)s->stop();
+}
+
+namespace {
+std::mutex g_shared_mu;
+SharedServer* g_shared[64][6] = {};  // [device][log2(E / 2)]
+
+void stop_shared_servers() {
+    for (auto& row : g_shared)
+        for (SharedServer* s : row)
+            if (s && s->srv) (void)s->srv->stop();
+}
+}  // namespace
+
+SharedServer* shared_server(int device, int e, int* rc) {
+    int lg = 0;
+    while ((2 << lg) < e) ++lg;  // e = 2, 4, ..., 32 -> 0..4
+    if (device < 0 || device >= 64 || lg > 5 || (2 << lg) != e) {
+        *rc = fail(CRLOT_EUNSUPPORTED, "call server slot");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(g_shared_mu);
+    SharedServer*& s = g_shared[device][lg];
+    if (!s) {
+        static const bool hooked = [] { return std::atexit(stop_shared_servers) == 0; }();
+        (void)hooked;
+        DeviceGuard g(device);
+        SharedServer* n = new SharedServer();
+        n->e = e;
+        const int P = 64 * e;
+        const std::vector<float> tw = build_pass_twiddles(2 * P);
+        std::vector<float> st(2 * size_t(P));
+        for (int t = 0; t < P; ++t) {  // exp(-i pi (t/P + 1/2)), as crlot_plan_create
+            const double ps = -M_PI * (double(t) / double(P) + 0.5);
+            st[2 * size_t(t)] = float(std::cos(ps));
+            st[2 * size_t(t) + 1] = float(std::sin(ps));
+        }
+        hipError_t err;
+        if ((err = hipMalloc(&n->d_tw, sizeof(float) * tw.size())) ||
+            (err = hipMalloc(&n->d_st, sizeof(float) * st.size())) ||
+            (err = hipMemcpy(n->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
+            (err = hipMemcpy(n->d_st, st.data(), sizeof(float) * st.size(), hipMemcpyHostToDevice))) {
+            *rc = hip_fail(err, "call server tables");
+            return nullptr;
+        }
+        const size_t row = size_t(2 * P + 2) * 2;
+        *rc = CallServer::create(device, e, 8, 4 * row, 4 * row, 4 * row, &n->srv);
+        if (*rc != CRLOT_OK) return nullptr;
+        s = n;
+    }
+    *rc = CRLOT_OK;
+    return s;
 }
 
 }  // namespace crlot

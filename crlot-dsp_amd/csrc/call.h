@@ -42,6 +42,11 @@ class CallServer {
     int submit(CallReq& r, const CallSlot& sl);
     int wait(uint64_t index);       // request `index` completed (its out slot is readable)
     int wait_spec(uint64_t index);  // ... and its speculation slot
+    int wait_chain(uint64_t index); // ... and its chained produce block (kCallChain)
+    // Ring work deferred onto the next request (CallReq::Pend): a commit and
+    // then a clear of one ring; anything that cannot merge flushes first.
+    int defer(const CallReq::Pend& p);
+    int flush();                    // post the deferred work now (an op-0 request)
     int drain();                    // every submitted request (and speculation) completed
     int stop();                     // kernel gone (requests already completed stay so)
     // the next request runs an agent-scope acquire first (the object's device
@@ -80,6 +85,8 @@ class CallServer {
     size_t in_cap_ = 0, out_cap_ = 0, spec_cap_ = 0;
     uint64_t q_ = 0;                   // requests submitted
     std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
+    uint64_t last_chain_ = 0;          // the last request with a chained produce
+    CallReq::Pend pend_{};             // deferred ring work (flags 0: none)
     uint64_t idle_ticks_ = 0;
     double tick_ns_ = 10.0;
 };
@@ -87,5 +94,50 @@ class CallServer {
 // atexit: stop the per-device free-function servers (their kernels would
 // otherwise idle out after the process began tearing the runtime down)
 void stop_free_function_servers();
+
+// The produce block an OLA object expects after its next push, as the forward
+// FFT of the frame it will push is being submitted (the chain of the drop-in
+// per-frame loop: forward -> inverse -> push_frame_AoS(inverse output) ->
+// produce).  Filled by the object (objects.cpp) through ChainTarget::predict.
+struct ChainPred {
+    float* ring = nullptr;
+    const float* den = nullptr;
+    const float* win = nullptr;  // the object's window (apply_window_inside) or null
+    int64_t R = 0, N = 0;
+    int64_t start = 0;           // predicted push start (absolute sample)
+    int64_t rp = 0, n = 0;       // predicted produce: read position (absolute) and count
+    float gain = 1.0f;
+};
+struct ChainTarget {
+    const void* owner = nullptr;             // the OLA object
+    bool (*predict)(const void* owner, ChainPred* out) = nullptr;
+};
+
+// One resident K_call<E> per (device, E), shared by every FFT plan of size
+// N = 128 E on the device and by the OLA objects of frame size N there, so a
+// frame's calls sit in ONE queue and the forward can speculate on the push and
+// produce that follow it.  Callers hold `mu` around their requests.
+struct SharedServer {
+    std::mutex mu;
+    CallServer* srv = nullptr;
+    int e = 0;
+    float* d_tw = nullptr;  // the size's pass twiddles and super twiddles (device, owned)
+    float* d_st = nullptr;
+    struct FftSpec {        // the inverse speculated after the last forward
+        bool valid = false;
+        uint64_t index = 0;
+        int batch = 0;
+        CallSlot slot;      // slot.out: the spectrum returned; slot.spec: its inverse
+    } fft;
+    struct Chain {          // the produce speculated after that inverse, for `target`
+        bool valid = false;
+        uint64_t index = 0;
+        ChainPred pred;
+        CallSlot slot;      // chained produce block at slot.spec + N
+    } chain;
+    ChainTarget target;     // the OLA object that pushed the last speculated inverse
+};
+// the shared server of (device, e) (created on first use; never destroyed)
+SharedServer* shared_server(int device, int e, int* rc);
 
 }  // namespace crlot

@@ -88,8 +88,9 @@ struct CallLds {
     static constexpr int TW = E > 0 ? dev::twiddle_table_size(E) : 1;
     static constexpr bool SPEC = E > 0 && E <= 16;
     static constexpr int SP = SPEC ? P + 1 : 0;
+    static constexpr int CH = SPEC ? 2 * P : 0;  // the chained frame (one speculated inverse, floats)
     static constexpr size_t bytes = sizeof(cf) * (size_t(TW) + 2 * P + size_t(kCallWaves) * (P + SP)) +
-                                    sizeof(float) * kCallPre + sizeof(CallReq) + 16;
+                                    sizeof(float) * (kCallPre + CH) + sizeof(CallReq) + 16;
 };
 
 // ---- FFTs, one wave per transform (k_rfft / k_irfft / k_cfft's arithmetic)
@@ -140,7 +141,7 @@ __device__ __forceinline__ void call_rfft(const CallIn<PRE>& in, int64_t off, fl
 // inverse real FFT: spectrum X (bins 0..P) given by get(k) -> out[0..N) (host memory)
 template <int E, typename G>
 __device__ __forceinline__ void call_irfft(G get, float* out, cf* buf, const cf* tw, const cf* st, float inv_n,
-                                           int lane) {
+                                           int lane, float* lds_copy = nullptr) {
     constexpr int P = 64 * E;
     cf v[E];
 #pragma unroll
@@ -159,8 +160,9 @@ __device__ __forceinline__ void call_irfft(G get, float* out, cf* buf, const cf*
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int i0 = 2 * (lane + 64 * m);
-        *reinterpret_cast<float2*>(out + i0) =
-            make_float2(dev::sanit(v[m].r * inv_n), dev::sanit(v[m].i * inv_n));
+        const float2 o = make_float2(dev::sanit(v[m].r * inv_n), dev::sanit(v[m].i * inv_n));
+        *reinterpret_cast<float2*>(out + i0) = o;
+        if (lds_copy) *reinterpret_cast<float2*>(lds_copy + i0) = o;
     }
 }
 
@@ -195,7 +197,8 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     cf* bufs = sth + P;
     cf* specs = bufs + kCallWaves * P;
     float* pre = reinterpret_cast<float*>(specs + kCallWaves * CallLds<E>::SP);
-    CallReq* rq = reinterpret_cast<CallReq*>(pre + kCallPre);
+    float* chainbuf = pre + kCallPre;  // the frame a chained forward kept for the push that follows
+    CallReq* rq = reinterpret_cast<CallReq*>(chainbuf + CallLds<E>::CH);
     uint32_t* cmd = reinterpret_cast<uint32_t*>(rq + 1);
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         {
             const uint64_t* pin = reinterpret_cast<const uint64_t*>(a.in_arena + int64_t(slot) * a.in_cap);
             const uint64_t v0 = ld_sys64(pin + t), v1 = ld_sys64(pin + kCallBlock + t);
-            if (t < 16)
+            if (t < int(sizeof(CallReq) / 8))
                 reinterpret_cast<uint64_t*>(rq)[t] = ld_sys64(reinterpret_cast<const uint64_t*>(src) + t);
             reinterpret_cast<uint64_t*>(pre)[t] = v0;
             reinterpret_cast<uint64_t*>(pre)[kCallBlock + t] = v1;
@@ -254,6 +257,33 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         }
         if (r.flags & kCallAcquire)  // device-form calls ran on streams since the last request
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (r.pend.flags) {
+            // deferred ring work: the push of the kept frame (the push's arithmetic on
+            // the frame bits the host compared), then a served produce's clear
+            float* ring = r.pend.ring;
+            const int64_t R = r.pend.R;
+            if constexpr (CallLds<E>::CH > 0) {
+                if (r.pend.flags & kPendCommit) {
+                    const float* wobj = r.pend.win;
+                    for (int64_t j = t; j < r.pend.len; j += kCallBlock) {
+                        int64_t p = r.pend.start + j;
+                        if (p >= R) p -= R;
+                        const float s = chainbuf[j];
+                        ring[p] = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[j], 0.0f), r.pend.gain, ring[p])
+                                       : __builtin_fmaf(s, r.pend.gain, ring[p]);
+                    }
+                    __syncthreads();
+                }
+            }
+            if (r.pend.flags & kPendClear) {
+                for (int64_t q = t; q < r.pend.n; q += kCallBlock) {
+                    int64_t p = r.pend.rp + q;
+                    if (p >= R) p -= R;
+                    ring[p] = 0.0f;
+                }
+            }
+            __syncthreads();
+        }
         const float* in = a.in_arena + r.in_off;  // r.in_off is the slot's start
         // the input floats this request reads: when they fit the prefetched 4 KB,
         // every read comes from LDS
@@ -477,10 +507,41 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 if (CallLds<E>::SPEC && r.op == kCallRfft) {
                     // inverse of the spectrum just written (the same bits, from LDS;
                     // call_irfft is the inverse call's code)
+                    const bool chain = (r.flags & kCallChain) != 0 && r.batch == 1;
                     dev::wave_lds_fence();
                     for (int b = wave; b < r.batch; b += kCallWaves)
                         call_irfft<E>([&](int k) { return spb[k]; }, so + int64_t(b) * 2 * P, buf, tw, st, r.f0,
-                                      lane);
+                                      lane, chain ? chainbuf : nullptr);
+                    if (chain) {
+                        // publish the inverse first: the host's inverse call waits for it
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                        __syncthreads();
+                        if (t == 0) st_sys64(&a.hctl->spec_done, my);
+                        // the produce(n) block at rp after pushing that frame at start: the
+                        // push's arithmetic (axpy_windowed / axpy) on the ring as it stands
+                        __syncthreads();
+                        float* ring = r.p2;
+                        const float* den = r.p3;
+                        const float* wobj = r.p4;
+                        const int64_t R = r.j[0], start = r.j[1], rp = r.j[2], n = r.j[3];
+                        float* co = so + 2 * P;
+                        for (int64_t q = t; q < n; q += kCallBlock) {
+                            int64_t p = rp + q;
+                            if (p >= R) p -= R;
+                            int64_t d = p - start;
+                            if (d < 0) d += R;
+                            float v = ring[p];
+                            if (d < 2 * P) {
+                                const float s = chainbuf[d];
+                                v = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[d], 0.0f), r.f1, v)
+                                         : __builtin_fmaf(s, r.f1, v);
+                            }
+                            co[q] = v / den[p];
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                        __syncthreads();
+                        if (t == 0) st_sys64(&a.hctl->chain_done, my);
+                    }
                 }
             }
             CALL_PH(2);

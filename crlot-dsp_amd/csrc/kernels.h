@@ -207,19 +207,39 @@ enum : uint32_t {
     kCallRfft = 1, kCallIrfft, kCallCfft, kCallIcfft,  // IFftPlan forward / inverse / _complex
     kCallOlaAdd, kCallOlaProduce,                      // OLAAccumulator add_frame_SoA|push_frame_AoS / produce
     kCallAxpy, kCallAxpyWin, kCallNormalize            // dsp::axpy / axpy_windowed / normalize_and_clear
-};
-enum : uint32_t { kCallSpec = 1, kCallClearOnly = 2, kCallAcquire = 4 };
-struct alignas(128) CallReq {
+};  // op 0: nothing but the request's deferred ring work (CallPend)
+// kCallChain (on a speculating forward): also keep the speculated inverse frame
+// and compute the produce block the target OLA object would give after pushing it
+enum : uint32_t { kCallSpec = 1, kCallClearOnly = 2, kCallAcquire = 4, kCallChain = 8 };
+struct alignas(512) CallReq {
     uint32_t op, flags;
     int32_t batch, channels;
     int64_t in_off, out_off, spec_off, win_off;  // floats into in_arena (device) / out_arena (host); win_off < 0: none
     const float* p0;  // FFT: pass twiddles   | OLA add: the object's window (nullable)
     const float* p1;  // FFT: super twiddles  | OLA: den = max(norm, eps)
-    float* p2;        // OLA: ring [C][R]
+    float* p2;        // OLA (and chain): ring [C][R]
     int64_t i[6];     // OLA: R, ring start / read pos, len, AoS?, speculated read pos, speculated count
-    float f0, f1;     // FFT: 1/N (1/P complex) | OLA add: gain | axpy: g | normalize: eps
+    float f0, f1;     // FFT: 1/N (1/P complex) | OLA add: gain | axpy: g | normalize: eps; f1: chain gain
+    const float* p3;  // chain: den
+    const float* p4;  // chain: the object's window (nullable)
+    int64_t j[8];     // chain: R, push start (ring pos), produce read pos, produce count
+    uint64_t pad[6];
+    // Ring work the host deferred onto this request, applied before it (in this
+    // order): the push of the frame the last chained forward kept (kPendCommit),
+    // then the clear of a produce block served from a speculation (kPendClear).
+    struct Pend {
+        uint32_t flags;
+        float gain;
+        float* ring;
+        const float* win;   // commit: the object's window or null
+        int64_t R, start, len;  // commit: ring position and length
+        int64_t rp, n;          // clear: ring position and length (mono)
+        uint64_t pad[2];
+    } pend;
+    uint64_t pad2[22];
 };
-static_assert(sizeof(CallReq) == 128, "one descriptor = one 128-byte line");
+enum : uint32_t { kPendCommit = 1, kPendClear = 2 };
+static_assert(sizeof(CallReq) == 512, "one descriptor = 64 lanes x 8 bytes");
 struct alignas(64) CallCtl {  // fine-grained device memory, written by the host (BAR)
     uint64_t seq;             // requests submitted
     uint64_t pad0[7];
@@ -231,6 +251,8 @@ struct alignas(64) CallHostCtl {  // pinned host memory, written by the kernel
     uint64_t pad0[7];
     uint64_t spec_done;           // requests whose speculation slot is written
     uint64_t pad1[7];
+    uint64_t chain_done;          // forwards whose chained produce block is written
+    uint64_t pad2[7];
     uint64_t ph[8];               // -DCRLOT_CALL_PHASES builds: the last request's phase stamps
 };
 struct CallArgs {

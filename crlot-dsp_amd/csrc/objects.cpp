@@ -195,10 +195,15 @@ struct crlot_ola {
     // host-pointer calls run on a resident call server (call_rt.hip); device-form
     // calls on streams.  Switching between the two drains the other side first.
     crlot::CallServer* srv = nullptr;
+    crlot::SharedServer* shared = nullptr;  // frame sizes 256..4096 (powers of two): the size's
+                                      // server, shared with the FFT plans (chained speculation)
     int mode = 0;                     // 0 none yet, 1 streams, 2 call server
+    int64_t last_start = -1;          // start_sample and gain of the last host push
+    float last_gain = 1.0f;
     int64_t last_req_n = 0;           // n of the last produce(): the next one's prediction
     struct Spec {                     // produce block speculated after the last add
         bool valid = false;
+        bool chain = false;           // computed by a chained forward (its chain_done)
         uint64_t index = 0;
         int64_t rp = 0, n = 0;
         crlot::CallSlot slot;
@@ -211,10 +216,27 @@ struct crlot_ola {
 
 namespace {
 
+// Held around an object's requests on a shared server.
+struct ServerLock {
+    std::mutex* m = nullptr;
+    explicit ServerLock(crlot_ola* o) : m(o->shared ? &o->shared->mu : nullptr) {
+        if (m) m->lock();
+    }
+    ~ServerLock() {
+        if (m) m->unlock();
+    }
+};
+
 void ola_free(crlot_ola* o) {
     if (!o) return;
     DeviceGuard g(o->device);
-    delete o->srv;  // waits for its requests, stops the kernel
+    if (o->shared) {
+        std::lock_guard<std::mutex> lk(o->shared->mu);
+        if (o->shared->target.owner == o) o->shared->target = crlot::ChainTarget{};
+        if (o->mode == 2) (void)o->srv->drain();  // its requests touch this object's rings
+    } else {
+        delete o->srv;  // waits for its requests, stops the kernel
+    }
     if (o->own) (void)hipStreamSynchronize(o->own);
     if (o->last_set && o->last) (void)hipStreamSynchronize(o->last);
     for (auto& s : o->slot) {
@@ -233,6 +255,7 @@ void ola_free(crlot_ola* o) {
 // one and after every request of the call server.
 hipError_t use_stream(crlot_ola* o, hipStream_t s) {
     if (o->mode == 2) {
+        ServerLock lk(o);
         if (o->srv->drain() != CRLOT_OK) return hipErrorLaunchFailure;
         o->spec.valid = false;
     }
@@ -322,9 +345,15 @@ int add_common(crlot_ola* o, const float* d_src, int64_t cs, int64_t js, const f
 int to_server(crlot_ola* o) {
     if (!o->srv) {
         const size_t C = size_t(o->C()), N = size_t(o->N()), R = size_t(o->R);
-        const size_t blk = std::min(R, std::max<size_t>(N, 1024));
-        int rc = crlot::CallServer::create(o->device, 0, 8, C * N + N, C * blk, C * blk, &o->srv);
-        if (rc != CRLOT_OK) return rc;
+        const bool pow2 = N >= 256 && N <= 4096 && (N & (N - 1)) == 0;
+        int rc = CRLOT_OK;
+        if (pow2 && (o->shared = crlot::shared_server(o->device, int(N / 128), &rc)) != nullptr) {
+            o->srv = o->shared->srv;
+        } else {
+            const size_t blk = std::min(R, std::max<size_t>(N, 1024));
+            rc = crlot::CallServer::create(o->device, 0, 8, C * N + N, C * blk, C * blk, &o->srv);
+            if (rc != CRLOT_OK) return rc;
+        }
     }
     if (o->mode == 1) {
         hipError_t e = o->last_set ? hipStreamSynchronize(o->last) : hipSuccess;
@@ -333,6 +362,74 @@ int to_server(crlot_ola* o) {
     }
     o->mode = 2;
     return CRLOT_OK;
+}
+
+// ChainTarget::predict: the push and produce this object's next frame will make,
+// if it keeps the drop-in loop's rhythm (mono, whole frames at start + H, the
+// object's own window or none, produce(n) of the previous count)
+bool ola_predict(const void* owner, crlot::ChainPred* out) {
+    const crlot_ola* o = static_cast<const crlot_ola*>(owner);
+    if (o->C() != 1 || o->mode != 2 || o->last_start < 0) return false;
+    out->ring = o->d_ring;
+    out->den = o->d_den;
+    out->win = (o->cfg.apply_window_inside && !o->window.empty()) ? o->d_win : nullptr;
+    out->R = o->R;
+    out->N = o->N();
+    out->start = o->last_start + o->H();
+    out->rp = o->read_pos;
+    const int64_t produced_after = std::max(o->produced, out->start + o->N());
+    const int64_t avail = produced_after > o->read_pos ? produced_after - o->read_pos : 0;
+    out->n = std::min({o->last_req_n > 0 ? o->last_req_n : o->H(), avail, o->R});
+    out->gain = o->last_gain;
+    return true;
+}
+
+// The frame being pushed is the inverse the shared server speculated after the
+// last forward, pushed where the chain predicted: commit it without a payload;
+// the produce block the chain computed becomes this object's speculation.
+// Returns 1 when it committed, 0 when the push must take the ordinary path.
+int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, int64_t start_sample,
+                   int64_t start_off, int64_t eff, float gain) {
+    crlot::SharedServer* sh = o->shared;
+    if (!sh || o->C() != 1 || o->mode != 2) return 0;
+    crlot::CallServer* sv = sh->srv;
+    const int64_t N = o->N();
+    // learn the association: this object pushes the frames the server speculates
+    if (sh->target.owner != o && sh->fft.index + 4 > sv->submitted() && start_off == 0 && eff == N &&
+        sh->fft.slot.spec && std::memcmp(frame, sh->fft.slot.spec, sizeof(float) * size_t(N)) == 0) {
+        sh->target.owner = o;
+        sh->target.predict = ola_predict;
+        return 0;
+    }
+    const crlot::ChainPred& pd = sh->chain.pred;
+    const float* want_win = (uw && !caller_win) ? o->d_win : nullptr;
+    if (!(sh->chain.valid && sh->chain.index == sv->submitted() && sh->target.owner == o && start_off == 0 &&
+          eff == N && start_sample == pd.start && gain == pd.gain && !caller_win && want_win == pd.win &&
+          pd.rp == o->read_pos && std::memcmp(frame, sh->chain.slot.spec, sizeof(float) * size_t(N)) == 0))
+        return 0;
+    sh->chain.valid = false;
+    // the push itself rides on the next request (the server keeps the frame in LDS)
+    crlot::CallReq::Pend pe{};
+    pe.flags = crlot::kPendCommit;
+    pe.ring = o->d_ring;
+    pe.win = pd.win;
+    pe.R = o->R;
+    pe.start = start_sample % o->R;
+    pe.len = N;
+    pe.gain = gain;
+    int rc = sv->defer(pe);
+    if (rc != CRLOT_OK) return rc;
+    o->spec.valid = true;
+    o->spec.chain = true;
+    o->spec.index = sh->chain.index;
+    o->spec.rp = pd.rp;
+    o->spec.n = pd.n;
+    o->spec.slot = sh->chain.slot;
+    o->spec.slot.spec += N;  // the chained produce block follows the speculated frame
+    o->produced = std::max(o->produced, start_sample + eff);  // :114
+    o->last_start = start_sample;
+    o->last_gain = gain;
+    return 1;
 }
 
 // add_frame_SoA (rows = ch channel pointers) / push_frame_AoS (rows[0] = the
@@ -383,11 +480,14 @@ int server_add(crlot_ola* o, const float* const* rows, int64_t ch, bool aos, con
     }
     if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
     o->spec.valid = spec;
+    o->spec.chain = false;
     o->spec.index = sl.index;
     o->spec.rp = o->read_pos;
     o->spec.n = pn;
     o->spec.slot = sl;
     if (ch == C) o->produced = std::max(o->produced, start_sample + eff);  // :114
+    o->last_start = start_sample;
+    o->last_gain = gain;
     return CRLOT_OK;
 }
 
@@ -473,9 +573,15 @@ int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const f
     const bool caller_win = uw && !o->cfg.apply_window_inside;
     std::vector<const float*> rows;
     for (int64_t c = 0; c < ok; ++c) rows.push_back(ch_frames[c] + start_off);
-    int rc = server_add(o, rows.data(), ok, false, caller_win ? window + start_off : nullptr,
-                        (uw && !caller_win) ? o->d_win + start_off : nullptr, start_sample, eff, gain);
+    int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
+    ServerLock lk(o);
+    rc = ok == o->C() ? try_chain_push(o, rows[0], uw, caller_win, start_sample, start_off, eff, gain) : 0;
+    if (rc < 0) return rc;
+    if (rc == 0)
+        rc = server_add(o, rows.data(), ok, false, caller_win ? window + start_off : nullptr,
+                        (uw && !caller_win) ? o->d_win + start_off : nullptr, start_sample, eff, gain);
+    if (rc < 0) return rc;
     return ok < o->C() ? fail(CRLOT_EINVAL, "Channel frame pointer cannot be null") : CRLOT_OK;
 }
 
@@ -493,6 +599,13 @@ int crlot_ola_push_frame_aos(crlot_ola* o, const float* interleaved, const float
     const bool uw = use_window(o, window != nullptr);
     const bool caller_win = uw && !o->cfg.apply_window_inside;
     const float* src = interleaved + start_off * o->C();
+    int rc = to_server(o);
+    if (rc != CRLOT_OK) return rc;
+    ServerLock lk(o);
+    // (a mono AoS frame is the SoA one; the window is read from index 0 as for start_off 0)
+    rc = try_chain_push(o, src, uw, caller_win, start_sample, start_off == 0 ? 0 : -1, eff, gain);
+    if (rc < 0) return rc;
+    if (rc == 1) return CRLOT_OK;
     return server_add(o, &src, o->C(), true, caller_win ? window : nullptr, (uw && !caller_win) ? o->d_win : nullptr,
                       start_sample, eff, gain);
 }
@@ -549,6 +662,7 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
     DeviceGuard g(o->device);
     int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
+    ServerLock lk(o);
     crlot::CallServer* sv = o->srv;
     const int64_t C = o->C();
     const bool hit = o->spec.valid && o->spec.index == sv->submitted() && o->spec.rp == o->read_pos &&
@@ -567,14 +681,25 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
     r.i[2] = len;
     if (hit) {
         // served from the block speculated after the last add (the same bits); the
-        // ring is cleared by a request behind it
-        if ((rc = sv->wait_spec(o->spec.index)) != CRLOT_OK) return rc;
+        // ring is cleared by the next request (mono: deferred onto it)
+        if ((rc = o->spec.chain ? sv->wait_chain(o->spec.index) : sv->wait_spec(o->spec.index)) != CRLOT_OK)
+            return rc;
         for (int64_t c = 0; c < C; ++c)
             std::memcpy(ch_out[c], o->spec.slot.spec + c * len, sizeof(float) * size_t(len));
-        crlot::CallSlot sl;
-        if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
-        r.flags = crlot::kCallClearOnly;
-        if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+        if (C == 1) {
+            crlot::CallReq::Pend pe{};
+            pe.flags = crlot::kPendClear;
+            pe.ring = o->d_ring;
+            pe.R = o->R;
+            pe.rp = o->read_pos % o->R;
+            pe.n = len;
+            if ((rc = sv->defer(pe)) != CRLOT_OK) return rc;
+        } else {
+            crlot::CallSlot sl;
+            if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
+            r.flags = crlot::kCallClearOnly;
+            if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+        }
     } else {
         crlot::CallSlot sl;
         if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
@@ -636,6 +761,9 @@ int crlot_ola_reset(crlot_ola* o) {
     o->host_peak = 0.0f;
     o->flushing = false;
     o->window.clear();
+    o->last_start = -1;
+    o->last_req_n = 0;
+    o->spec.valid = false;
     return upload_norm(o, o->own);
 }
 
@@ -672,7 +800,10 @@ int crlot_ola_norm_table(const crlot_ola* o, float* out) {
 int crlot_ola_synchronize(crlot_ola* o) {
     if (!o) return fail(CRLOT_EINVAL, "null OLA object");
     DeviceGuard g(o->device);
-    if (o->mode == 2) return o->srv->drain();
+    if (o->mode == 2) {
+        ServerLock lk(o);
+        return o->srv->drain();
+    }
     hipError_t e = o->last_set ? hipStreamSynchronize(o->last) : hipSuccess;
     return e == hipSuccess ? CRLOT_OK : hip_fail(e, "sync");
 }
