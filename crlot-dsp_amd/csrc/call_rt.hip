@@ -492,6 +492,11 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         // reader is its speculated produce: it publishes once, with the speculation.
         CALL_PH(0);
         my += 1;
+        // (A chained forward publishing its spectrum, inverse and produce block
+        // behind one fence measured 12.2 us per e2e frame against 11.4 us with
+        // three publishes: the host waits for the spectrum first.)
+        const bool chained =
+            CallLds<E>::SPEC && spec && r.op == kCallRfft && (r.flags & kCallChain) != 0 && r.batch == 1;
         const bool merged = spec && r.op == kCallOlaAdd;
         if (!merged) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -507,7 +512,23 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 if (CallLds<E>::SPEC && r.op == kCallRfft) {
                     // inverse of the spectrum just written (the same bits, from LDS;
                     // call_irfft is the inverse call's code)
-                    const bool chain = (r.flags & kCallChain) != 0 && r.batch == 1;
+                    const bool chain = chained;
+                    // the chained produce's ring and den values, loaded under the inverse
+                    constexpr int KC = 4;
+                    float rv[KC], dv[KC];
+                    if (chain) {
+#pragma unroll
+                        for (int k = 0; k < KC; ++k) {
+                            const int64_t q = t + int64_t(k) * kCallBlock;
+                            rv[k] = dv[k] = 1.0f;
+                            if (q < r.j[3]) {
+                                int64_t p = r.j[2] + q;
+                                if (p >= r.j[0]) p -= r.j[0];
+                                rv[k] = r.p2[p];
+                                dv[k] = r.p3[p];
+                            }
+                        }
+                    }
                     dev::wave_lds_fence();
                     for (int b = wave; b < r.batch; b += kCallWaves)
                         call_irfft<E>([&](int k) { return spb[k]; }, so + int64_t(b) * 2 * P, buf, tw, st, r.f0,
@@ -525,18 +546,27 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                         const float* wobj = r.p4;
                         const int64_t R = r.j[0], start = r.j[1], rp = r.j[2], n = r.j[3];
                         float* co = so + 2 * P;
-                        for (int64_t q = t; q < n; q += kCallBlock) {
+                        auto one = [&](int64_t q, float v, float dn) {
                             int64_t p = rp + q;
                             if (p >= R) p -= R;
                             int64_t d = p - start;
                             if (d < 0) d += R;
-                            float v = ring[p];
                             if (d < 2 * P) {
                                 const float s = chainbuf[d];
                                 v = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[d], 0.0f), r.f1, v)
                                          : __builtin_fmaf(s, r.f1, v);
                             }
-                            co[q] = v / den[p];
+                            co[q] = v / dn;
+                        };
+#pragma unroll
+                        for (int k = 0; k < KC; ++k) {
+                            const int64_t q = t + int64_t(k) * kCallBlock;
+                            if (q < n) one(q, rv[k], dv[k]);
+                        }
+                        for (int64_t q = t + int64_t(KC) * kCallBlock; q < n; q += kCallBlock) {
+                            int64_t p = rp + q;
+                            if (p >= R) p -= R;
+                            one(q, ring[p], den[p]);
                         }
                         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                         __syncthreads();
@@ -545,12 +575,14 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 }
             }
             CALL_PH(2);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            CALL_PH(3);
-            __syncthreads();
-            if (t == 0) {
-                if (merged) st_sys64(&a.hctl->done, my);
-                st_sys64(&a.hctl->spec_done, my);
+            if (!chained) {  // (a chained forward published each part as it went)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                CALL_PH(3);
+                __syncthreads();
+                if (t == 0) {
+                    if (merged) st_sys64(&a.hctl->done, my);
+                    st_sys64(&a.hctl->spec_done, my);
+                }
             }
         }
         t_last = wall_clock64();
