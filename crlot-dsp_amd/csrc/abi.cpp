@@ -355,7 +355,7 @@ int ensure_workspace(crlot::Scratch* sc, int64_t bytes) {
 
 bool pair_plan(const crlot_plan* p) {
     return p->pairing && (p->geo.n == 480 || p->geo.n == 512 || p->geo.n == 960 || p->geo.n == 1024 ||
-                          p->geo.n == 2048 || p->geo.n == 4096);
+                          p->geo.n == 2048 || p->geo.n == 4096 || crlot::pairn_size(p->geo.n));
 }
 
 // K_pair's per-walker flags: at most one walker per frame and stream.
@@ -488,8 +488,10 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     if ((n == 1024 && h % 128 == 0 && ring % h == 0) || (n == 512 && h % 128 == 0 && ring % h == 0) ||
         (n == 2048 && h % 256 == 0 && ring % h == 0) ||
         (n == 4096 && h % 512 == 0 && ring % h == 0) ||
-        crlot::pair15_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair15 tables
+        crlot::pair15_supported(n, h, ring) ||
+        crlot::pairn_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair15 / K_pairN tables
         const std::vector<float> ptw = (n == 960 || n == 480) ? crlot::build_pair15_twiddles(n)
+                                       : crlot::pairn_size(n) ? crlot::build_pairn_twiddles(n)
                                        : n == 1024 ? crlot::build_pair_twiddles()
                                        : n == 512  ? crlot::build_pair512_twiddles()
                                        : n == 2048 ? crlot::build_pair2k_twiddles()
@@ -708,6 +710,20 @@ static int roundtrip_impl(crlot_plan* p, crlot::Scratch* sc, const float* d_x, f
             if (e != hipSuccess) return hip_fail(e, "pair (N = 15 L) kernel launch");
             e = crlot::launch_fused_any(p->geo, tp, p->d_twany, d_x, d_y, n_streams, T, ld_x, ld_y, F, s,
                                         tp.pflags, nch, per);
+            if (e != hipSuccess) return hip_fail(e, "fused (any size) kernel launch");
+            return CRLOT_OK;
+        }
+        // N = 320 ... 1764 with factors 2, 3, 5, 7 (K_pairN), then the same redo
+        if (p->pairing && t.ptw && p->geo.pad_mode == 0 &&
+            crlot::pairn_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < lim && out_len < lim) {
+            const int rcf = ensure_pair_flags(p, sc, n_streams, F);
+            if (rcf != CRLOT_OK) return rcf;
+            const crlot::DevTables tp = tables(p, sc);
+            int nch = 0;
+            e = crlot::launch_pairn(p->geo, tp, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, &nch, s);
+            if (e != hipSuccess) return hip_fail(e, "pair (N = 2^a 3^b 5^c 7^d) kernel launch");
+            e = crlot::launch_fused_any(p->geo, tp, p->d_twany, d_x, d_y, n_streams, T, ld_x, ld_y, F, s,
+                                        tp.pflags, nch, 1);
             if (e != hipSuccess) return hip_fail(e, "fused (any size) kernel launch");
             return CRLOT_OK;
         }

@@ -10,7 +10,9 @@
 // wave's 64 lanes): x_r = src[j + r P/R] * W_{Ns R}^{r (j mod Ns)}, a length-R
 // DFT, dst[(j / Ns) Ns R + j mod Ns + r Ns] = y.  Factors follow kiss_fft's
 // kf_factor order (4s, then 2s, then odd primes).  Radix 2/3/4/5 butterflies
-// are written out (the kf_bfly2/3/4/5 formulas); any other prime R uses an
+// are written out (the kf_bfly2/3/4/5 formulas), radix 7 as the symmetric
+// odd-prime DFT (kissfft's generic butterfly computes the same sums in another
+// order: a tolerance claim like every FFT here); any other prime R uses an
 // O(R^2) DFT that streams its inputs from LDS, so no size is excluded.
 // Twiddles come from per-pass tables in global memory (L1/L2-resident; no
 // integer division or modulo in the butterfly loop); the inverse conjugates
@@ -83,6 +85,32 @@ __device__ __forceinline__ void pass_r(const cf* __restrict__ src, cf* __restric
             x[0] = cadd(x[0], s);
             x[1] = cadd(h, e);
             x[2] = csub(h, e);
+        } else if constexpr (R == 7) {
+            // y_s = x0 + sum_q cos(2 pi qs/7) (x_q + x_{7-q}) -/+ i sum_q sin(2 pi qs/7) (x_q - x_{7-q})
+            // (kissfft runs 7 through kf_bfly_generic: the same sums, another order)
+            constexpr float c1 = 0.62348980185873353053f, c2 = -0.22252093395631440429f,
+                            c3 = -0.90096886790241912624f;
+            constexpr float s1 = 0.78183148246802980871f, s2 = 0.97492791218182360702f,
+                            s3 = 0.43388373911755812048f;
+            const cf x0 = x[0];
+            const cf t1 = cadd(x[1], x[6]), t2 = cadd(x[2], x[5]), t3 = cadd(x[3], x[4]);
+            const cf u1 = csub(x[1], x[6]), u2 = csub(x[2], x[5]), u3 = csub(x[3], x[4]);
+            auto lin = [](const cf& b, float k1, const cf& p, float k2, const cf& q, float k3, const cf& r) {
+                return cf{__builtin_fmaf(k3, r.r, __builtin_fmaf(k2, q.r, __builtin_fmaf(k1, p.r, b.r))),
+                          __builtin_fmaf(k3, r.i, __builtin_fmaf(k2, q.i, __builtin_fmaf(k1, p.i, b.i)))};
+            };
+            const cf z = {0.0f, 0.0f};
+            const cf a1 = lin(x0, c1, t1, c2, t2, c3, t3), b1 = lin(z, s1, u1, s2, u2, s3, u3);
+            const cf a2 = lin(x0, c2, t1, c3, t2, c1, t3), b2 = lin(z, s2, u1, -s3, u2, -s1, u3);
+            const cf a3 = lin(x0, c3, t1, c1, t2, c2, t3), b3 = lin(z, s3, u1, -s1, u2, s2, u3);
+            x[0] = cadd(cadd(x0, t1), cadd(t2, t3));
+            const cf e1 = mul_mi<INV>(b1), e2 = mul_mi<INV>(b2), e3 = mul_mi<INV>(b3);
+            x[1] = cadd(a1, e1);
+            x[6] = csub(a1, e1);
+            x[2] = cadd(a2, e2);
+            x[5] = csub(a2, e2);
+            x[3] = cadd(a3, e3);
+            x[4] = csub(a3, e3);
         } else {
             static_assert(R == 5, "radix");
             // kf_bfly5 with ya = W5^1, yb = W5^2
@@ -145,6 +173,7 @@ __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p
         case 3: pass_r<INV, 3>(src, dst, tw, p, d, lane); break;
         case 4: pass_r<INV, 4>(src, dst, tw, p, d, lane); break;
         case 5: pass_r<INV, 5>(src, dst, tw, p, d, lane); break;
+        case 7: pass_r<INV, 7>(src, dst, tw, p, d, lane); break;
         default: pass_generic<INV>(src, dst, tw, p, d, lane); break;
     }
 }

@@ -135,6 +135,14 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
                          int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks,
                          int* streams_per_walk, hipStream_t stream);
 std::vector<float> build_pair15_twiddles(int n);
+// K_pairN (pair_n.hip): frame pairs for N in {320, 400, 640, 882, 1000, 1764}
+// (fft_pairn.h), paired regime only; flags per walker in t.pflags like K_pair15,
+// n_chunks walkers per stream.  Tables: t.ptw = build_pairn_twiddles(N).
+bool pairn_size(int n);
+bool pairn_supported(int n, int h, int ring_len);
+hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams, int64_t T,
+                        int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks, hipStream_t stream);
+std::vector<float> build_pairn_twiddles(int n);
 hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
                           const float* in, float* out, int batch, int64_t ld_in, int64_t inc_in,
                           int64_t ld_out, int64_t inc_out, hipStream_t stream);

@@ -2347,7 +2347,7 @@ dev::any::Plan make_any_plan(int p) {
         d.off = off;
         d.rcp_ns = 1.0f / float(ns);
         off += (d.r - 1) * ns;
-        const bool special = d.r == 2 || d.r == 3 || d.r == 4 || d.r == 5;
+        const bool special = d.r == 2 || d.r == 3 || d.r == 4 || d.r == 5 || d.r == 7;
         d.woff = special ? 0 : off;
         if (!special) off += d.r;
         ns *= d.r;
@@ -2370,7 +2370,7 @@ std::vector<float> build_any_twiddles(int p) {
     for (int r : f) {
         for (int q = 1; q < r; ++q)
             for (int jm = 0; jm < ns; ++jm) push(-2.0 * M_PI * double(q) * double(jm) / double(ns * r));
-        if (!(r == 2 || r == 3 || r == 4 || r == 5))
+        if (!(r == 2 || r == 3 || r == 4 || r == 5 || r == 7))
             for (int e = 0; e < r; ++e) push(-2.0 * M_PI * double(e) / double(r));
         ns *= r;
     }

@@ -511,7 +511,8 @@ def test_oboe_wav_roundtrip(pkg, oracle, torch_cuda):
 
 # ------------------------------------------------------------------ any frame size
 @pytest.mark.parametrize("n,h,mode", [(960, 240, 0), (480, 120, 1), (1000, 250, 0), (998, 499, 0),
-                                      (128, 32, 0), (6, 2, 0), (1536, 384, 0), (6000, 1500, 0)])
+                                      (128, 32, 0), (6, 2, 0), (1536, 384, 0), (6000, 1500, 0),
+                                      (882, 441, 0), (1764, 441, 0), (882, 441, 1), (1764, 441, 1)])
 def test_roundtrip_any_size_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
     """Frame sizes kissfft accepts beyond the power-of-two kernels (20 / 10 ms at
     48 kHz, P = 499 prime, N < 256, N > 4096) through the mixed-radix path."""
@@ -1020,7 +1021,7 @@ def test_pair15_vs_oracle_and_chunking(pkg, oracle, torch_cuda, n, h, mode, T):
     assert np.array_equal(bits(y1[0]), bits(y[3]))
 
 
-@pytest.mark.parametrize("n,h", [(960, 240), (480, 120)])
+@pytest.mark.parametrize("n,h", [(960, 240), (480, 120), (882, 441), (1764, 441), (1000, 250)])
 def test_pair15_spectral_gain(pkg, oracle, torch_cuda, n, h):
     """K_pair15 applies a spectral gain per complex bin (the spectral hook): the
     paired result equals the per-frame kernels' within float32 rounding on clean
@@ -1044,7 +1045,7 @@ def test_pair15_spectral_gain(pkg, oracle, torch_cuda, n, h):
         assert_close(y[s_], y_pf[s_], float(np.max(np.abs(x[s_]))), f"stream {s_} paired vs per-frame")
 
 
-@pytest.mark.parametrize("n,h", [(960, 240), (480, 120)])
+@pytest.mark.parametrize("n,h", [(960, 240), (480, 120), (882, 441), (1764, 441), (640, 320)])
 def test_pair15_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda, n, h):
     """A stream with a sample outside the paired range (NaN, 1e30, 1e-35) is
     recomputed whole by the per-frame walker -- equal bit for bit to the plan with
@@ -1068,3 +1069,31 @@ def test_pair15_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda, n, 
     ref = oracle.roundtrip_batch(x[[0, 3]], n, h, nthreads=2)
     assert_close(y[0], ref[0], float(np.max(np.abs(x[0]))), "clean stream")
     assert_close(y[3], ref[1], float(np.max(np.abs(x[0]))), "tiny sample stream")
+
+
+# ------------------------------------------------------------------ K_pairN (N = 2^a 3^b 5^c 7^d frame pairs)
+@pytest.mark.parametrize("n,h,mode,T", [(882, 441, 0, 48_000), (882, 441, 1, 44_101), (882, 294, 0, 30_011),
+                                        (882, 147, 0, 9_999), (1764, 441, 0, 48_000), (1764, 441, 1, 40_000),
+                                        (1764, 882, 0, 30_007), (1000, 250, 0, 20_000), (640, 320, 0, 20_011),
+                                        (400, 160, 0, 16_000), (320, 160, 1, 9_999), (320, 80, 0, 700),
+                                        (882, 441, 0, 500)])
+def test_pairn_vs_oracle_and_chunking(pkg, oracle, torch_cuda, n, h, mode, T):
+    """Frame sizes with factors 2, 3, 5, 7 (882 / 1764 = 20 / 40 ms at 44.1 kHz,
+    1000, 640, 400, 320) in pairs through one N-point complex transform per wave
+    (fft_pairn.h, radix 7 written out): the oracle within the float32 tolerance,
+    the Framer's frame counts, and bits independent of the batch a stream is in."""
+    torch = torch_cuda
+    x = oracle.synth_streams(5, T, config_id=71 + h + n)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode)
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    assert y.shape == (5, oracle.frame_count(T, n, h, mode) * h)
+    ref = oracle.roundtrip_batch(x, n, h, mode=mode, nthreads=4)
+    for s_ in range(5):
+        assert_close(y[s_], ref[s_], float(np.max(np.abs(x))), f"N={n} H={h} stream {s_}")
+    y1 = host(plan.roundtrip(xd[3:4].contiguous()))
+    assert np.array_equal(bits(y1[0]), bits(y[3]))
+    plan.set_frame_pairing(False)  # the per-frame walker agrees within rounding
+    y_pf = host(plan.roundtrip(xd))
+    for s_ in range(5):
+        assert_close(y[s_], y_pf[s_], float(np.max(np.abs(x))), f"N={n} H={h} paired vs per-frame {s_}")
