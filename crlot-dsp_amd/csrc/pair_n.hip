@@ -30,61 +30,122 @@ namespace fk {
 
 namespace {
 
-__host__ __device__ inline int pn_ring(int n, int h) {
+// OLA ring floats of a walk: the live span H ceil(N/H), rounded up to a power of
+// two (a position wraps with one AND) unless lean (one compare and subtract)
+__host__ __device__ inline int pn_ring(int n, int h, bool lean) {
     const int span = h * ((n + h - 1) / h);
+    if (lean) return span;
     int r = 1;
     while (r < span) r <<= 1;
     return r;
 }
 
 // LDS: [twiddles tw_len cf][wa N f][ws N f] | per wave [buffer N cf][ring RL f]
-size_t pn_tables(int n) { return sizeof(dev::pc) * size_t(dev::pn_factor(n).tw_len) + sizeof(float) * 2 * size_t(n); }
-size_t pn_per_wave(int n, int h) { return sizeof(dev::pc) * size_t(n) + sizeof(float) * size_t(pn_ring(n, h)); }
+// CRLOT_PN_PLAN=V (A/B): the alternative radix list V of fft_pairn.h for 882 / 1764
+int pn_variant(int n) {
+    static const int v = [] {
+        const char* e = std::getenv("CRLOT_PN_PLAN");
+        const int x = e ? std::atoi(e) : 0;
+        return x >= 0 && x < 4 ? x : 0;
+    }();
+    return (n == 882 || n == 1764) ? v : 0;
+}
+// CRLOT_PN_WIDE=0/1 (A/B): one or two waves per transform at 882 / 1764 (default
+// below: two at 1764)
+int pn_halves(int n) {
+    static const int w = [] {
+        const char* e = std::getenv("CRLOT_PN_WIDE");
+        return e ? (e[0] == '1' ? 2 : 1) : 0;
+    }();
+    if (n != 882 && n != 1764) return 1;
+    return w ? w : (n == 1764 ? 2 : 1);
+}
+// CRLOT_PN_LEAN=0/1 (A/B): the two-wave walk's LDS without the windows and with an
+// exact-size ring (one more walk per CU at 1764)
+bool pn_lean(int n) {
+    static const int l = [] {
+        const char* e = std::getenv("CRLOT_PN_LEAN");
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
+    }();
+    if (pn_halves(n) != 2) return false;
+    return l == 1;  // measured at 1764/441: 62.7k lean vs 98.0k (the windows and the prefetch matter more)
+}
+int pn_key(int n) {
+    return n + 100000 * pn_variant(n) + 1000000 * (pn_halves(n) - 1) + 10000000 * (pn_lean(n) ? 1 : 0);
+}
+size_t pn_tables(int n) {
+    return sizeof(dev::pc) * size_t(dev::pn_factor(pn_key(n)).tw_len) + (pn_lean(n) ? 0 : sizeof(float) * 2 * size_t(n));
+}
+size_t pn_per_walk(int n, int h) {
+    return sizeof(dev::pc) * size_t(n) + sizeof(float) * size_t(pn_ring(n, h, pn_lean(n)));
+}
 
-// waves per workgroup (one workgroup per CU): as many walks as the LDS holds, <= 16
-int pn_waves(int n, int h) {
+// walks per workgroup (one workgroup per CU): as many as the LDS holds, <= 16 waves
+int pn_walks(int n, int h) {
     const size_t budget = 160 * 1024;
-    const size_t t = pn_tables(n), w = pn_per_wave(n, h);
+    const size_t t = pn_tables(n), w = pn_per_walk(n, h);
     if (t + w > budget) return 0;
-    return int(std::min<size_t>(16, (budget - t) / w));
+    return int(std::min<size_t>(16 / pn_halves(n), (budget - t) / w));
 }
 
 }  // namespace
 
 // register budget per size: waves per SIMD (the launch puts at most 4 x WPE waves
 // in its one workgroup per CU)
-constexpr int pn_wpe(int n) { return n <= 640 ? 4 : n <= 1000 ? 3 : 2; }
+constexpr int pn_wpe(int key) {
+    const int n = key % 100000, halves = 1 + (key % 10000000) / 1000000;
+    if (key >= 10000000) return 4;  // lean: 7 walks (14 waves) per CU at 1764
+    return n <= 400 * halves ? 4 : n <= 1000 * halves ? 3 : 2;
+}
 
-template <int N, bool HAS_GAIN>
-__global__ __launch_bounds__(256 * pn_wpe(N)) __attribute__((amdgpu_waves_per_eu(pn_wpe(N))))
+template <int K, bool HAS_GAIN>  // K: plan key (fft_pairn.h pn_factor), N = K % 100000
+__global__ __launch_bounds__(256 * pn_wpe(K)) __attribute__((amdgpu_waves_per_eu(pn_wpe(K))))
 void k_pairn(const FusedArgs a) {
-    constexpr int E = (N + 63) / 64;  // rows per lane (the last one partial when N % 64 != 0)
-    constexpr int LAST = N - 64 * (E - 1);  // lanes of the last row
-    constexpr dev::PnFac FAC = dev::pn_factor(N);
+    constexpr int N = K % 100000;
+    constexpr int L = dev::pn_lanes(K), HALVES = L / 64;  // lanes (waves) per transform
+    constexpr int E = (N + L - 1) / L;      // natural-order rows per lane (the last partial)
+    constexpr int LAST = N - L * (E - 1);   // lanes of the last row
+    constexpr bool LEAN = K >= 10000000;
+    constexpr dev::PnFac FAC = dev::pn_factor(K);
     static_assert(FAC.rest == 1, "N must factor into 2, 3, 5, 7");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int W = blockDim.x >> 6;
+    const int t = threadIdx.x % L, pw = __builtin_amdgcn_readfirstlane(threadIdx.x / L);  // lane / walk in the workgroup
+    const int half = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) % HALVES);
+    const int PPW = int(blockDim.x) / L;  // walks per workgroup
     const int H = a.hop;
-    const int RL = pn_ring(N, H), RM = RL - 1;
+    const int RL = pn_ring(N, H, LEAN), RM = RL - 1;
+    // ring position of block offset o (< N + H) past frame k's start kb = (k H) mod RL
+    auto rpos = [&](int kb, int o) {
+        if constexpr (LEAN) {
+            int p = kb + o;
+            p -= p >= RL ? RL : 0;
+            return p >= RL ? p - RL : p;
+        } else {
+            return (kb + o) & RM;
+        }
+    };
+    auto rbase = [&](int k) { return LEAN ? (k * H) % RL : k * H; };
     const int NB = (N + H - 1) / H;
     dev::pc* tw = reinterpret_cast<dev::pc*>(smem);
-    float* wa = reinterpret_cast<float*>(tw + FAC.tw_len);
-    float* ws = wa + N;
-    dev::pc* buf = reinterpret_cast<dev::pc*>(ws + N) + size_t(wave) * N;
-    float* ring = reinterpret_cast<float*>(reinterpret_cast<dev::pc*>(ws + N) + size_t(W) * N) + size_t(wave) * RL;
+    float* wl = reinterpret_cast<float*>(tw + FAC.tw_len);  // LDS windows (not lean)
+    float* wend = LEAN ? wl : wl + 2 * N;
+    const float* wa = LEAN ? a.t.wa : wl;
+    const float* ws = LEAN ? a.t.ws : wl + N;
+    dev::pc* buf = reinterpret_cast<dev::pc*>(wend) + size_t(pw) * N;
+    float* ring = reinterpret_cast<float*>(reinterpret_cast<dev::pc*>(wend) + size_t(PPW) * N) + size_t(pw) * RL;
     {
         const dev::pc* g = reinterpret_cast<const dev::pc*>(a.t.ptw);
         for (int i = threadIdx.x; i < FAC.tw_len; i += blockDim.x) tw[i] = g[i];
-        for (int i = threadIdx.x; i < N; i += blockDim.x) {
-            wa[i] = a.t.wa[i];
-            ws[i] = a.t.ws[i];
-        }
+        if constexpr (!LEAN)
+            for (int i = threadIdx.x; i < N; i += blockDim.x) {
+                wl[i] = a.t.wa[i];
+                wl[N + i] = a.t.ws[i];
+            }
     }
     __syncthreads();
-    const int gw = blockIdx.x * W + wave;
-    if (gw >= a.n_streams * a.n_chunks) return;
+    const int gw = blockIdx.x * PPW + pw;  // this walk
+    if (gw >= a.n_streams * a.n_chunks) return;  // (both waves of a walk together)
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -95,29 +156,38 @@ void k_pairn(const FusedArgs a) {
     const float g = a.gain, inv_n = a.inv_n;
     const int ring_blocks = a.ring_blocks;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
-    auto valid = [&](int m) { return m + 1 < E || lane < LAST; };
+    auto valid = [&](int m) { return m + 1 < E || t < LAST; };
 
-    for (int i = lane; i < RL; i += 64) ring[i] = 0.0f;
-    dev::wave_lds_fence();
+    for (int i = t; i < RL; i += L) ring[i] = 0.0f;
+    dev::pn_fence<K>();
 
-    // frame k: x[origin + lane + 64 m] (samples outside [0, T) read 0: the
-    // descriptor's range check, a negative offset wraps past it)
-    auto load_frame = [&](float (&f)[E], int origin) {
+    using P0 = dev::PnPass<K, 0>;
+    using PL = dev::PnPass<K, FAC.n - 1>;
+    // frame k as the first pass reads it: register [it][q] of lane t holds sample
+    // j + q M0 (j = t + L it); samples outside [0, T) read 0 (the descriptor's
+    // range check; a negative offset wraps past it)
+    auto load_frame = [&](float (&f)[P0::ITS][P0::R], int origin) {
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int v = valid(m) ? (origin + lane + 64 * m) * 4 : 0x7ffffff0;
-            f[m] = dev::bload1(rx, v, 0);
+        for (int it = 0; it < P0::ITS; ++it) {
+            const int j = t + L * it;
+#pragma unroll
+            for (int q = 0; q < P0::R; ++q) {
+                const int v = P0::live(it, j) ? (origin + j + q * P0::M) * 4 : 0x7ffffff0;
+                f[it][q] = dev::bload1(rx, v, 0);
+            }
         }
     };
     bool bad = false;
-    auto check = [&](const float (&f)[E]) {
+    auto check = [&](const float (&f)[P0::ITS][P0::R]) {
         uint32_t mx = 0u, mn = ~0u;
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const uint32_t w = __builtin_bit_cast(uint32_t, f[m]) & 0x7fffffffu;
-            mx = max(mx, w);
-            mn = min(mn, w - 1u);
-        }
+        for (int it = 0; it < P0::ITS; ++it)
+#pragma unroll
+            for (int q = 0; q < P0::R; ++q) {
+                const uint32_t w = __builtin_bit_cast(uint32_t, f[it][q]) & 0x7fffffffu;
+                mx = max(mx, w);
+                mn = min(mn, w - 1u);
+            }
         bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
     };
     // produce(H) of block k: ring / den (Markstein with {den, 1/den} when the plan
@@ -125,19 +195,19 @@ void k_pairn(const FusedArgs a) {
     const float2* const dr2 = reinterpret_cast<const float2*>(a.t.den_rden);
     const __amdgpu_buffer_rsrc_t rden = dev::make_rsrc(dr2, uint32_t(ring_blocks * H) * 8u);
     auto produce = [&](int k) {
-        const int base = k * H;
+        const int base = k * H, kb = rbase(k);
         const int dbase = (k % ring_blocks) * H;
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
         if (dr2) {
-            for (int j0 = lane; j0 < H; j0 += 4 * 64) {
+            for (int j0 = t; j0 < H; j0 += 4 * L) {
                 float2 d[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) d[i] = dev::bload2(rden, (j0 + 64 * i) * 8, dbase * 8);
+                for (int i = 0; i < 4; ++i) d[i] = dev::bload2(rden, (j0 + L * i) * 8, dbase * 8);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int j = j0 + 64 * i;
+                    const int j = j0 + L * i;
                     if (j < H) {
-                        const int pos = (base + j) & RM;
+                        const int pos = rpos(kb, j);
                         const float v = ring[pos];
                         ring[pos] = 0.0f;
                         const float o = mk_div(v, d[i].x, d[i].y);
@@ -147,106 +217,137 @@ void k_pairn(const FusedArgs a) {
                 }
             }
         } else {
-            for (int j = lane; j < H; j += 64) {
-                const int pos = (base + j) & RM;
+            for (int j = t; j < H; j += L) {
+                const int pos = rpos(kb, j);
                 const float v = ring[pos];
                 ring[pos] = 0.0f;
                 const float o = v / a.t.den[dbase + j];
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rk, (base + j) * 4, 0, 0);
             }
         }
-        dev::wave_lds_fence();
+        // no fence: the next push (frame k+1) adds only to blocks after k, and the
+        // clears are ordered before any later reuse of their positions by the
+        // fences of the next pair's transforms
     };
 
-    float fa[E], fb[E];
-#ifndef CRLOT_PN_NOPREFETCH
-    load_frame(fa, fs * H - a.pad);
-    load_frame(fb, (fs + 1) * H - a.pad);
-#endif
+    // the next pair's frames load during this pair's transforms, except at 1764
+    // points: 56 more VGPRs than the walk has (measured: the compiler spills them)
+    constexpr bool PF = N < 1500 || (L == 128 && !LEAN);
+    float fa[P0::ITS][P0::R], fb[P0::ITS][P0::R];
+    if constexpr (PF) {
+        load_frame(fa, fs * H - a.pad);
+        load_frame(fb, (fs + 1) * H - a.pad);
+    }
     for (int k = fs; k < f1; k += 2) {
-#ifdef CRLOT_PN_NOPREFETCH
-        load_frame(fa, k * H - a.pad);
-        load_frame(fb, (k + 1) * H - a.pad);
-#endif
+        if constexpr (!PF) {
+            load_frame(fa, k * H - a.pad);
+            load_frame(fb, (k + 1) * H - a.pad);
+        }
         check(fa);
         check(fb);
         const bool partner = k + 1 < a.F;  // frame k+1 past the last: imaginary part 0
+        const int ln = dev::pn_opaque(t);
+        {
+            // the first forward pass straight from the frame registers
+            dev::pc x[P0::ITS][P0::R];
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            if (valid(m)) {
-                const int n = lane + 64 * m;
-                const float w = wa[n];
-                buf[n] = dev::pc_mk(fa[m] * w, partner ? fb[m] * w : 0.0f);
+            for (int it = 0; it < P0::ITS; ++it) {
+                const int j = P0::bf(ln, it);
+#pragma unroll
+                for (int q = 0; q < P0::R; ++q) {
+                    const float w = wa[j + q * P0::M];
+                    x[it][q] = dev::pc_mk(fa[it][q] * w, partner ? fb[it][q] * w : 0.0f);
+                }
+                dev::pn_bfly<false, K, 0>(x[it], tw, j);
             }
+            if constexpr (PF) {  // the next pair's frames, in flight during this pair's transforms
+                load_frame(fa, (k + 2) * H - a.pad);
+                load_frame(fb, (k + 3) * H - a.pad);
+            }
+            dev::pn_pass_store<K, 0>(buf, ln, x);
+            dev::pn_fence<K>();
         }
-        // the next pair's frames, in flight during this pair's transforms
-#ifndef CRLOT_PN_NOPREFETCH
-        load_frame(fa, (k + 2) * H - a.pad);
-        load_frame(fb, (k + 3) * H - a.pad);
-#endif
-        dev::wave_lds_fence();
-        dev::pn_fft<false, N>(buf, tw, lane);
+        dev::pn_passes<false, K, 1, FAC.n>(buf, tw, ln);
         if constexpr (HAS_GAIN) {  // real gain, symmetric over the N bins (L2-resident table)
 #pragma unroll
             for (int m = 0; m < E; ++m) {
                 if (valid(m)) {
-                    const int n = lane + 64 * m;
+                    const int n = ln + L * m;
                     buf[n] = buf[n] * a.t.gain[n <= N / 2 ? n : N - n];
                 }
             }
-            dev::wave_lds_fence();
+            dev::pn_fence<K>();
         }
-        dev::pn_fft<true, N>(buf, tw, lane);
-        // push frame k (the real part) and k+1 (the imaginary part) straight from
-        // the buffer: o = v (1/N), then o * ws; the output sanitize threshold
-        // 1e-30 = 2^-99.66: exponents <= -99 flag the walk
+        dev::pn_passes<true, K, 0, FAC.n - 1>(buf, tw, ln);
+        // the last inverse pass into registers, pushed from there: frame k the real
+        // part, frame k+1 the imaginary part; o = v (1/N), then o * ws; the output
+        // sanitize threshold 1e-30 = 2^-99.66: exponents <= -99 flag the walk
+        dev::pc y[PL::ITS][PL::R];
+        dev::pn_pass_compute<true, K, FAC.n - 1>(buf, tw, ln, y);
+        const int kb0 = rbase(k), kb1 = rbase(k + 1);
         {
             int e = 0;
-            const int base = k * H + lane;
 #pragma unroll
-            for (int m = 0; m < E; ++m) {
-                if (valid(m)) {
-                    const int n = lane + 64 * m;
-                    const dev::pc v = buf[n] * dev::pc{inv_n, inv_n};
-                    e = min(e, min(__builtin_amdgcn_frexp_expf(v.x), __builtin_amdgcn_frexp_expf(v.y)));
-                    const int pos = (base + 64 * m) & RM;
-                    ring[pos] = __builtin_fmaf(v.x * ws[n], g, ring[pos]);
+            for (int it = 0; it < PL::ITS; ++it) {
+                const int j = ln + L * it;
+                if (PL::live(it, j)) {
+#pragma unroll
+                    for (int q = 0; q < PL::R; ++q) {
+                        y[it][q] = y[it][q] * dev::pc{inv_n, inv_n};
+                        e = min(e, min(__builtin_amdgcn_frexp_expf(y[it][q].x),
+                                       __builtin_amdgcn_frexp_expf(y[it][q].y)));
+                        const int n = PL::out(j, q);
+                        const int pos = rpos(kb0, n);
+                        ring[pos] = __builtin_fmaf(y[it][q].x * ws[n], g, ring[pos]);
+                    }
                 }
             }
             bad |= e <= -99;
         }
-        dev::wave_lds_fence();
+        dev::pn_fence<K>();
         produce(k);
-        {
-            const int base = (k + 1) * H + lane;
 #pragma unroll
-            for (int m = 0; m < E; ++m) {
-                if (valid(m)) {
-                    const int n = lane + 64 * m;
-                    const dev::pc v = buf[n] * dev::pc{inv_n, inv_n};
-                    const int pos = (base + 64 * m) & RM;
-                    ring[pos] = __builtin_fmaf(v.y * ws[n], g, ring[pos]);
+        for (int it = 0; it < PL::ITS; ++it) {
+            const int j = ln + L * it;
+            if (PL::live(it, j)) {
+#pragma unroll
+                for (int q = 0; q < PL::R; ++q) {
+                    const int n = PL::out(j, q);
+                    const int pos = rpos(kb1, n);
+                    ring[pos] = __builtin_fmaf(y[it][q].y * ws[n], g, ring[pos]);
                 }
             }
         }
-        dev::wave_lds_fence();
+        dev::pn_fence<K>();
         if (k + 1 < f1) produce(k + 1);
     }
+    // one flag per wave: [stream][chunk][half] (the redo ORs a stream's flags)
     const uint64_t bal = __builtin_amdgcn_ballot_w64(bad);
-    if (lane == 0) a.t.pflags[gw] = bal != 0 ? 1u : 0u;
+    if (lane == 0) a.t.pflags[gw * HALVES + half] = bal != 0 ? 1u : 0u;
 }
 
 namespace {
 // the instantiated sizes
 template <typename F>
-bool pn_dispatch(int n, F&& f) {
-    switch (n) {
+bool pn_dispatch(int key, F&& f) {
+    switch (key) {
         case 320: f(std::integral_constant<int, 320>{}); return true;
         case 400: f(std::integral_constant<int, 400>{}); return true;
         case 640: f(std::integral_constant<int, 640>{}); return true;
         case 882: f(std::integral_constant<int, 882>{}); return true;
         case 1000: f(std::integral_constant<int, 1000>{}); return true;
         case 1764: f(std::integral_constant<int, 1764>{}); return true;
+        case 1000882: f(std::integral_constant<int, 1000882>{}); return true;
+        case 1001764: f(std::integral_constant<int, 1001764>{}); return true;
+        case 11001764: f(std::integral_constant<int, 11001764>{}); return true;
+#ifdef CRLOT_PN_VARIANTS
+        case 100882: f(std::integral_constant<int, 100882>{}); return true;
+        case 200882: f(std::integral_constant<int, 200882>{}); return true;
+        case 300882: f(std::integral_constant<int, 300882>{}); return true;
+        case 101764: f(std::integral_constant<int, 101764>{}); return true;
+        case 201764: f(std::integral_constant<int, 201764>{}); return true;
+        case 301764: f(std::integral_constant<int, 301764>{}); return true;
+#endif
         default: return false;
     }
 }
@@ -261,7 +362,7 @@ bool pairn_size(int n) {
 bool pairn_supported(int n, int h, int ring_len) {
     if (!pairn_size(n)) return false;
     if (h < 32 || h > n || ring_len % h != 0) return false;
-    return fk::pn_waves(n, h) >= 1;
+    return fk::pn_walks(n, h) >= 1;
 }
 
 hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams, int64_t T,
@@ -286,26 +387,27 @@ hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, f
     a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     a.gain = g.gain;
-    const int W = std::min(pn_waves(g.n, g.h), 4 * pn_wpe(g.n));
+    const int halves = pn_halves(g.n);
+    const int walks = std::min(pn_walks(g.n, g.h), 4 * pn_wpe(pn_key(g.n)) / halves);  // per workgroup
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
     // chunks: about two resident rounds of walkers, each >= 48 frames
-    const int64_t resident = int64_t(cus) * W;
+    const int64_t resident = int64_t(cus) * walks;
     const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + n_streams - 1) / n_streams));
     a.M = int((F + n - 1) / n);
     a.n_chunks = int((F + a.M - 1) / a.M);
-    const int64_t waves = int64_t(n_streams) * a.n_chunks;
-    if (t.pflags_len < waves) return hipErrorInvalidValue;
-    *n_chunks = a.n_chunks;
-    const size_t lds = pn_tables(g.n) + size_t(W) * pn_per_wave(g.n, g.h);
+    const int64_t total = int64_t(n_streams) * a.n_chunks;  // walks
+    if (t.pflags_len < total * halves) return hipErrorInvalidValue;
+    *n_chunks = a.n_chunks * halves;  // flags per stream (one per wave)
+    const size_t lds = pn_tables(g.n) + size_t(walks) * pn_per_walk(g.n, g.h);
     hipError_t e = hipSuccess;
-    pn_dispatch(g.n, [&](auto nc) {
+    pn_dispatch(pn_key(g.n), [&](auto nc) {
         constexpr int NN = decltype(nc)::value;
         auto k = t.gain ? k_pairn<NN, true> : k_pairn<NN, false>;
         if ((e = set_lds(k, lds)) != hipSuccess) return;
-        hipLaunchKernelGGL(k, dim3(unsigned((waves + W - 1) / W)), dim3(64 * W), lds, stream, a);
+        hipLaunchKernelGGL(k, dim3(unsigned((total + walks - 1) / walks)), dim3(64 * halves * walks), lds, stream, a);
         e = hipGetLastError();
     });
     return e;
@@ -313,7 +415,7 @@ hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, f
 
 // W_{ns r}^{q jm} per pass of fft_pairn.h's factorisation, float pairs
 std::vector<float> build_pairn_twiddles(int n) {
-    const dev::PnFac f = dev::pn_factor(n);
+    const dev::PnFac f = dev::pn_factor(fk::pn_key(n));
     std::vector<float> t(2 * size_t(f.tw_len));
     for (int i = 0; i < f.n; ++i)
         for (int q = 1; q < f.r[i]; ++q)
