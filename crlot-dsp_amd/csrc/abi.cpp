@@ -890,6 +890,13 @@ int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t 
 struct crlot_fft_plan {
     int domain = CRLOT_FFT_REAL;
     int nfft = 0;
+    int device = 0;
+    // the inner STFT plan (its tables serve the device-form calls and the staged
+    // host path), created on first use: host-pointer calls of sizes the call
+    // server runs never need it, and a plan's tables cost more to build than the
+    // reference's FFT plan does (the harness constructs plans inside its loops)
+    crlot_plan_desc pd{};
+    std::mutex inner_mu;
     crlot_plan* inner = nullptr;
     // host-pointer calls (crlot_fft_*_host): the call server shared by every
     // plan of this size on the device, or staged launches for sizes it has no
@@ -922,27 +929,44 @@ int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
     pd.hop_size = pd.frame_size / 4 > 0 ? pd.frame_size / 4 : 1;
     pd.window_type = CRLOT_WIN_RECT;
     pd.device = d->device;
-    crlot_plan* inner = nullptr;
-    const int rc = crlot_plan_create(&pd, &inner);
-    if (rc != CRLOT_OK) return rc;
+    if (!real && pd.frame_size > 16384) return fail(CRLOT_EUNSUPPORTED, "complex FFT size");
+    int dev = d->device;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return fail(CRLOT_EHIP, "no HIP device");
     crlot_fft_plan* p = new crlot_fft_plan();
     p->domain = d->domain;
     p->nfft = d->nfft;
-    p->inner = inner;
-    p->e = (!inner->generic && is_pow2(pd.frame_size) && pd.frame_size >= 256 && pd.frame_size <= 4096)
+    p->device = dev;
+    pd.device = dev;
+    p->pd = pd;
+    p->e = (is_pow2(pd.frame_size) && pd.frame_size >= 256 && pd.frame_size <= 4096)
                ? pd.frame_size / 128  // K_call<E>, E = P / 64
                : 0;
+    if (p->e == 0) {  // staged host calls need the tables anyway: fail at construction as before
+        const int rc = crlot_plan_create(&p->pd, &p->inner);
+        if (rc != CRLOT_OK) {
+            delete p;
+            return rc;
+        }
+    }
     *out = p;
     return CRLOT_OK;
+}
+
+// the inner plan, created on first use (NULL and the error set on failure)
+static crlot_plan* fft_inner(crlot_fft_plan* p, int* rc) {
+    std::lock_guard<std::mutex> lk(p->inner_mu);
+    *rc = CRLOT_OK;
+    if (!p->inner) *rc = crlot_plan_create(&p->pd, &p->inner);
+    return p->inner;
 }
 
 void crlot_fft_plan_destroy(crlot_fft_plan* p) {
     if (!p) return;
     {
-        DeviceGuard g(p->inner->device);
+        DeviceGuard g(p->device);
         if (p->d_stage) (void)hipFree(p->d_stage);
     }
-    crlot_plan_destroy(p->inner);
+    if (p->inner) crlot_plan_destroy(p->inner);
     delete p;
 }
 
@@ -964,16 +988,20 @@ static int fft_domain_check(const crlot_fft_plan* p, int want) {
 
 int crlot_fft_forward(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, void* stream) {
-    const int rc = fft_domain_check(p, CRLOT_FFT_REAL);
+    int rc = fft_domain_check(p, CRLOT_FFT_REAL);
     if (rc != CRLOT_OK) return rc;
-    return crlot_rfft_batched(p->inner, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+    crlot_plan* q = fft_inner(p, &rc);
+    if (!q) return rc;
+    return crlot_rfft_batched(q, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, stream);
 }
 
 int crlot_fft_inverse(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
                       int64_t ld_in, int64_t inc_in, int64_t ld_out, int64_t inc_out, void* stream) {
-    const int rc = fft_domain_check(p, CRLOT_FFT_REAL);
+    int rc = fft_domain_check(p, CRLOT_FFT_REAL);
     if (rc != CRLOT_OK) return rc;
-    return crlot_irfft_batched(p->inner, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, stream);
+    crlot_plan* q = fft_inner(p, &rc);
+    if (!q) return rc;
+    return crlot_irfft_batched(q, d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out, stream);
 }
 
 static int cfft_common(crlot_fft_plan* p, const float* d_in, float* d_out, int32_t batch,
@@ -984,7 +1012,8 @@ static int cfft_common(crlot_fft_plan* p, const float* d_in, float* d_out, int32
     if (batch < 0 || inc_in < 1 || inc_out < 1) return fail(CRLOT_EINVAL, "bad batch/stride");
     if (batch == 0) return CRLOT_OK;
     if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
-    const crlot_plan* q = p->inner;
+    const crlot_plan* q = fft_inner(p, &rc);
+    if (!q) return rc;
     DeviceGuard g(q->device);
     hipError_t e = q->generic
                        ? crlot::launch_fft_any(inverse ? 3 : 2, p->nfft, 1.0f / float(p->nfft),
@@ -1087,7 +1116,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     if (batch == 0) return CRLOT_OK;
     if (!in || !out) return fail(CRLOT_EINVAL, "null buffer");
     std::lock_guard<std::mutex> lk(p->mu);
-    DeviceGuard g(p->inner->device);
+    DeviceGuard g(p->device);
     const int64_t n = p->nfft, bins = n / 2 + 1;
     // element counts and widths of the input / output rows
     const int64_t in_len = kind == 0 ? n : kind == 1 ? bins : n, out_len = kind == 0 ? bins : kind == 1 ? n : n;
@@ -1099,7 +1128,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     const size_t nin = size_t(batch) * size_t(in_len * in_w), nout = size_t(batch) * size_t(out_len * out_w);
     p->pack.resize(std::max(nin, nout));
     gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
-    crlot::SharedServer* sh = crlot::shared_server(p->inner->device, p->e, &rc);
+    crlot::SharedServer* sh = crlot::shared_server(p->device, p->e, &rc);
     if (!sh) return rc;
     std::lock_guard<std::mutex> slk(sh->mu);
     crlot::CallServer* sv = sh->srv;
@@ -1130,7 +1159,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     r.win_off = -1;
     r.p0 = sh->d_tw;
     r.p1 = sh->d_st;
-    r.f0 = kind < 2 ? p->inner->geo.inv_n : 1.0f / float(p->nfft);
+    r.f0 = 1.0f / float(p->nfft);  // the inverse's 1/N (real: the plan's inv_n, frame = nfft)
     if (spec) r.flags = crlot::kCallSpec;
     if (chain) {
         r.flags |= crlot::kCallChain;

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -23,6 +24,7 @@
 #include <vector>
 
 #include "call.h"
+#include "respool.h"
 #include "crlot_dsp.h"
 #include "kernels.h"
 
@@ -237,17 +239,21 @@ void ola_free(crlot_ola* o) {
     } else {
         delete o->srv;  // waits for its requests, stops the kernel
     }
-    if (o->own) (void)hipStreamSynchronize(o->own);
     if (o->last_set && o->last) (void)hipStreamSynchronize(o->last);
+    if (o->own) (void)hipStreamSynchronize(o->own);
+    // resources back to the pools (respool.h): device blocks stream-ordered on
+    // the object's own stream, which then serves the next object
     for (auto& s : o->slot) {
         if (s.ev) (void)hipEventDestroy(s.ev);
-        if (s.h) (void)hipHostFree(s.h);
+        crlot::pool_pinned_put(s.h, s.cap * sizeof(float));
     }
-    for (float* p : {o->d_ring, o->d_den, o->d_win})
-        if (p) (void)hipFree(p);
-    if (o->d_peak) (void)hipFree(o->d_peak);
+    if (o->own) {
+        for (void* p : {static_cast<void*>(o->d_ring), static_cast<void*>(o->d_den), static_cast<void*>(o->d_win),
+                        static_cast<void*>(o->d_peak)})
+            crlot::pool_free(p, o->own);
+    }
     if (o->order) (void)hipEventDestroy(o->order);
-    if (o->own) (void)hipStreamDestroy(o->own);
+    crlot::pool_stream_put(o->device, o->own);
     delete o;
 }
 
@@ -281,11 +287,14 @@ hipError_t take_slot(crlot_ola* o, size_t floats, crlot_ola::Slot** out) {
     }
     if (!s.ev && (e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if (s.cap < floats) {
-        if (s.h) (void)hipHostFree(s.h);
+        crlot::pool_pinned_put(s.h, s.cap * sizeof(float));
         s.h = nullptr;
         s.cap = 0;
-        if ((e = hipHostMalloc(reinterpret_cast<void**>(&s.h), floats * sizeof(float))) != hipSuccess) return e;
-        s.cap = floats;
+        void* hb = nullptr;
+        size_t cap = 0;
+        if ((e = crlot::pool_pinned(floats * sizeof(float), &hb, &cap)) != hipSuccess) return e;
+        s.h = static_cast<float*>(hb);
+        s.cap = cap / sizeof(float);
     }
     *out = &s;
     return hipSuccess;
@@ -520,10 +529,16 @@ int crlot_ola_create(const crlot_ola_config* cfg, crlot_ola** out) {
     o->norm.assign(size_t(o->R), 1.0f);
     const size_t C = size_t(o->C()), R = size_t(o->R), N = size_t(o->N());
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&o->own, hipStreamNonBlocking)) ||
+    auto dmalloc = [&](auto** ptr, size_t bytes) {
+        void* v = nullptr;
+        const hipError_t r = crlot::pool_malloc(o->device, &v, bytes, o->own);
+        *ptr = static_cast<std::remove_pointer_t<decltype(ptr)>>(v);
+        return r;
+    };
+    if ((e = crlot::pool_stream(o->device, &o->own)) ||
         (e = hipEventCreateWithFlags(&o->order, hipEventDisableTiming)) ||
-        (e = hipMalloc(&o->d_ring, sizeof(float) * C * R)) || (e = hipMalloc(&o->d_den, sizeof(float) * R)) ||
-        (e = hipMalloc(&o->d_win, sizeof(float) * N)) || (e = hipMalloc(&o->d_peak, sizeof(unsigned)))) {
+        (e = dmalloc(&o->d_ring, sizeof(float) * C * R)) || (e = dmalloc(&o->d_den, sizeof(float) * R)) ||
+        (e = dmalloc(&o->d_win, sizeof(float) * N)) || (e = dmalloc(&o->d_peak, sizeof(unsigned)))) {
         ola_free(o);
         return e == hipErrorOutOfMemory ? fail(CRLOT_ENOMEM, "OLA object allocation")
                                         : hip_fail(e, "OLA object allocation");
@@ -620,7 +635,7 @@ int crlot_ola_add_frame_soa_device(crlot_ola* o, const float* d_frames, int64_t 
     if (!clamp(o, start_off, size, &eff)) return CRLOT_OK;
     if (o->C() > 1 && ld_frames < o->N()) return fail(CRLOT_EINVAL, "leading dimension too small");
     DeviceGuard g(o->device);
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : o->own;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream (crlot_dsp.h)
     hipError_t e = use_stream(o, s);
     if (e != hipSuccess) return hip_fail(e, "stream order");
     const bool uw = use_window(o, d_window != nullptr);
@@ -637,7 +652,7 @@ int crlot_ola_push_frame_aos_device(crlot_ola* o, const float* d_interleaved, co
     int64_t eff = 0;
     if (!clamp(o, start_off, size, &eff)) return CRLOT_OK;
     DeviceGuard g(o->device);
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : o->own;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream (crlot_dsp.h)
     hipError_t e = use_stream(o, s);
     if (e != hipSuccess) return hip_fail(e, "stream order");
     const bool uw = use_window(o, d_window != nullptr);
@@ -729,7 +744,7 @@ int crlot_ola_produce_device(crlot_ola* o, float* d_out, int64_t ld_out, int64_t
     if (o->C() > 1 && ld_out < n) return fail(CRLOT_EINVAL, "leading dimension too small");
     const int64_t len = std::min(n, o->R);
     DeviceGuard g(o->device);
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : o->own;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream (crlot_dsp.h)
     hipError_t e = use_stream(o, s);
     if (e != hipSuccess) return hip_fail(e, "stream order");
     e = crlot::launch_ola_produce(o->d_ring, int(o->C()), o->R, o->d_den, d_out, ld_out, o->read_pos % o->R,
@@ -928,25 +943,34 @@ int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, in
         *out = q;
         return CRLOT_OK;
     }
-    float* d_x = nullptr;
+    void* d_x = nullptr;
+    void* d_f = nullptr;
     hipStream_t s = nullptr;
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) ||
-        (e = hipMalloc(&q->d_frames, sizeof(float) * nf)) ||
-        (len > 0 && (e = hipMalloc(&d_x, sizeof(float) * size_t(len)))) ||
+    if ((e = crlot::pool_stream(q->device, &s)) ||
+        (e = crlot::pool_malloc(q->device, &d_f, sizeof(float) * nf, s)) ||
+        (len > 0 && (e = crlot::pool_malloc(q->device, &d_x, sizeof(float) * size_t(len), s))) ||
         (len > 0 && (e = hipMemcpyAsync(d_x, in, sizeof(float) * size_t(len), hipMemcpyHostToDevice, s))) ||
-        (e = crlot::launch_fq_frames(d_x, len, len, 1, q->d_frames, q->f, q->n, q->h,
-                                     center ? frame_size / 2 : 0, pad_mode, s)) ||
-        (e = hipMemcpyAsync(q->frames.data(), q->d_frames, sizeof(float) * nf, hipMemcpyDeviceToHost, s)) ||
-        (e = hipStreamSynchronize(s))) {
-        if (d_x) (void)hipFree(d_x);
-        if (s) (void)hipStreamDestroy(s);
-        if (q->d_frames) (void)hipFree(q->d_frames);
+        (e = crlot::launch_fq_frames(static_cast<const float*>(d_x), len, len, 1, static_cast<float*>(d_f), q->f,
+                                     q->n, q->h, center ? frame_size / 2 : 0, pad_mode, s)) ||
+        (e = hipMemcpyAsync(q->frames.data(), d_f, sizeof(float) * nf, hipMemcpyDeviceToHost, s))) {
+        crlot::pool_free(d_x, s);
+        crlot::pool_free(d_f, s);
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            crlot::pool_stream_put(q->device, s);
+        }
         delete q;
         return e == hipErrorOutOfMemory ? fail(CRLOT_ENOMEM, "FrameQueue allocation") : hip_fail(e, "FrameQueue");
     }
-    if (d_x) (void)hipFree(d_x);
-    (void)hipStreamDestroy(s);
+    crlot::pool_free(d_x, s);
+    q->d_frames = static_cast<float*>(d_f);
+    e = hipStreamSynchronize(s);  // frames on the host; d_frames usable from any stream
+    crlot::pool_stream_put(q->device, s);
+    if (e != hipSuccess) {
+        crlot_framequeue_destroy(q);
+        return hip_fail(e, "FrameQueue");
+    }
     *out = q;
     return CRLOT_OK;
 }
@@ -954,7 +978,17 @@ int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, in
 void crlot_framequeue_destroy(crlot_framequeue* q) {
     if (!q) return;
     DeviceGuard g(q->device);
-    if (q->d_frames) (void)hipFree(q->d_frames);
+    if (q->d_frames) {
+        // (the caller finished its device-side reads of the frames, as with any
+        // buffer it frees: stream-ordered release on a pooled stream)
+        hipStream_t s = nullptr;
+        if (crlot::pool_stream(q->device, &s) == hipSuccess) {
+            crlot::pool_free(q->d_frames, s);
+            crlot::pool_stream_put(q->device, s);
+        } else {
+            (void)hipFree(q->d_frames);
+        }
+    }
     delete q;
 }
 
