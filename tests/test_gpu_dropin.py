@@ -276,3 +276,49 @@ def test_ola_host_calls_speculated_produce(pkg, oracle, torch_cuda):
         for ca, cb in zip(a, b):
             assert ca.shape == cb.shape and np.array_equal(bits(ca), bits(cb))
     assert ola.produced_samples() == ref.produced and ola.read_pos() == ref.read_pos
+
+
+@pytest.mark.gpu
+def test_chained_speculation_hits_and_misses(pkg, oracle, torch_cuda):
+    """The e2e loop's rhythm (forward -> inverse -> push_frame_AoS(inverse) ->
+    produce(H)) on one FFT plan and one mono OLA object, with the rhythm broken
+    on purpose: a pushed frame one bit off the speculated inverse, another gain,
+    another produce count, an extra forward between inverse and push, a push at
+    an unexpected position.  Every produce is bit-identical to the oracle's
+    OLAAccumulator fed the frames actually pushed, whichever of the chained,
+    speculated or computed paths served it."""
+    n, h = 1024, 256
+    rng = np.random.default_rng(33)
+    w = oracle.window(oracle.HANN, n)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                        apply_window_inside=True)
+    ola = pkg.OLAAccumulator(cfg)
+    ola.set_window(w)
+    ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ref.set_window(w)
+    start = 0
+    for k in range(96):
+        x = (rng.standard_normal(n) * w).astype(np.float32)
+        y = fft.inverse_host(fft.forward_host(x[None]))[0]
+        case = k % 8
+        gain, m = 1.0, h
+        if case == 3:
+            y = y.copy()
+            y[k % n] = np.nextafter(y[k % n], np.float32(np.inf))  # one bit off
+        elif case == 4:
+            gain = 0.5
+        elif case == 5:
+            m = h // 2 if k % 16 == 5 else 2 * h
+        elif case == 6:
+            fft.forward_host(rng.standard_normal((1, n)).astype(np.float32))  # an unrelated call
+        elif case == 7 and k % 16 == 7:
+            start += 3  # a push off the rhythm
+        ola.push_frame_AoS(y, None, start, 0, n, gain)
+        ref.push_frame_aos(y, start, 0, n, gain)
+        got, chans = ola.produce(m)
+        want = ref.produce(m)
+        assert got == len(want[0]), k
+        assert np.array_equal(bits(chans[0][:got]), bits(want[0])), k
+        start += h
+    assert ola.produced_samples() == ref.produced and ola.read_pos() == ref.read_pos
