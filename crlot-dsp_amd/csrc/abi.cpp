@@ -490,7 +490,8 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
         (n == 4096 && h % 512 == 0 && ring % h == 0) ||
         crlot::pair15_supported(n, h, ring) ||
         crlot::pairn_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair15 / K_pairN tables
-        const std::vector<float> ptw = (n == 960 || n == 480) ? crlot::build_pair15_twiddles(n)
+        const std::vector<float> ptw = ((n == 960 || n == 480) && !crlot::pairn_over_pair15(n))
+                                           ? crlot::build_pair15_twiddles(n)
                                        : crlot::pairn_size(n) ? crlot::build_pairn_twiddles(n)
                                        : n == 1024 ? crlot::build_pair_twiddles()
                                        : n == 512  ? crlot::build_pair512_twiddles()
@@ -699,7 +700,7 @@ static int roundtrip_impl(crlot_plan* p, crlot::Scratch* sc, const float* d_x, f
     if (p->generic && crlot::fused_any_fits(p->geo.n, p->geo.h) && ld_x < (int64_t(1) << 40)) {
         // N = 960 / 480 frame pairs (K_pair15), then the per-frame walker over the streams it flagged
         const int64_t lim = int64_t(1) << 27;
-        if (p->pairing && t.ptw && p->geo.pad_mode == 0 &&
+        if (p->pairing && t.ptw && p->geo.pad_mode == 0 && !crlot::pairn_over_pair15(p->geo.n) &&
             crlot::pair15_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < lim && out_len < lim &&
             ld_x < lim && ld_y < lim) {
             const int rcf = ensure_pair_flags(p, sc, n_streams, F);

@@ -2,7 +2,7 @@
 // whose factors are 2, 3, 5 and 7, in ONE LDS buffer of N elements: the
 // frame-pair transform of the sizes that neither the register-resident
 // power-of-two kernels nor K_pair15 (N = 15 L) take -- 882 and 1764 (20 / 40 ms
-// at 44.1 kHz), 1000, 640, 400, 320.
+// at 44.1 kHz), 1920 (40 ms at 48 kHz), 1000, 640, 400, 320.
 //
 // Stockham autosort over a short list of composite radices (882 = 9 x 7 x 14,
 // 1764 = 9 x 14 x 14, 1000 = 10 x 10 x 10 ...): pass i with radix R and sub-length
@@ -112,6 +112,13 @@ __host__ __device__ constexpr PnFac pn_factor(int K) {
     // {12,7,21} 69.6k Msamples/s; profiles/r03_pn_plans.jsonl)
     constexpr int p882[4][3] = {{9, 7, 14}, {7, 7, 18}, {14, 7, 9}, {18, 7, 7}};
     constexpr int p1764[4][3] = {{9, 14, 14}, {7, 7, 36}, {14, 14, 9}, {12, 7, 21}};
+    // 960 / 480 run on K_pair15 (register-resident: 194-197k / 197-203k against
+    // 139k / 120k for the best lists here, profiles/r03_pn15_ab.jsonl); these
+    // lists serve the -DCRLOT_PN_15 A/B build.  1920/480 (two waves per
+    // transform): {15,8,16} 83.6k, {8,15,16} 75.8k, {16,15,8} 66.2k Msamples/s.
+    constexpr int p960[4][3] = {{15, 8, 8}, {8, 8, 15}, {10, 12, 8}, {12, 10, 8}};
+    constexpr int p480[4][3] = {{8, 6, 10}, {10, 6, 8}, {6, 8, 10}, {15, 4, 8}};
+    constexpr int p1920[4][3] = {{15, 8, 16}, {8, 15, 16}, {16, 15, 8}, {12, 10, 16}};
     constexpr int p1000[3] = {10, 10, 10};
     constexpr int p640[3] = {8, 8, 10}, p400[3] = {8, 5, 10}, p320[3] = {8, 8, 5};
     if (V > 3) {
@@ -122,6 +129,9 @@ __host__ __device__ constexpr PnFac pn_factor(int K) {
     switch (N) {
         case 882: return pn_plan_of(N, p882[V], 3);
         case 1764: return pn_plan_of(N, p1764[V], 3);
+        case 960: return pn_plan_of(N, p960[V], 3);
+        case 480: return pn_plan_of(N, p480[V], 3);
+        case 1920: return pn_plan_of(N, p1920[V], 3);
         case 1000: return pn_plan_of(N, p1000, 3);
         case 640: return pn_plan_of(N, p640, 3);
         case 400: return pn_plan_of(N, p400, 3);

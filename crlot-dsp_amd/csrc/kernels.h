@@ -139,6 +139,7 @@ std::vector<float> build_pair15_twiddles(int n);
 // (fft_pairn.h), paired regime only; flags per walker in t.pflags like K_pair15,
 // n_chunks walkers per stream.  Tables: t.ptw = build_pairn_twiddles(N).
 bool pairn_size(int n);
+bool pairn_over_pair15(int n);
 bool pairn_supported(int n, int h, int ring_len);
 hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams, int64_t T,
                         int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks, hipStream_t stream);

@@ -1,6 +1,7 @@
 // pair_n.hip -- K_pairN: the frame-pair round trip for frame sizes with small
 // prime factors outside the register-resident kernels: 882 and 1764 (20 / 40 ms
-// at 44.1 kHz), 1000, 640, 400, 320.  One transform per wave.
+// at 44.1 kHz), 1920 (40 ms at 48 kHz), 1000, 640, 400, 320.  One transform per
+// wave, or per two waves at 1764 and 1920.
 //
 // Frames 2j and 2j+1 of a stream travel as one N-point complex transform,
 // z = x_2j w + i x_2j+1 w (as K_pair15 and the power-of-two pair kernels do:
@@ -48,7 +49,7 @@ int pn_variant(int n) {
         const int x = e ? std::atoi(e) : 0;
         return x >= 0 && x < 4 ? x : 0;
     }();
-    return (n == 882 || n == 1764) ? v : 0;
+    return (n == 882 || n == 1764 || n == 960 || n == 480 || n == 1920) ? v : 0;
 }
 // CRLOT_PN_WIDE=0/1 (A/B): one or two waves per transform at 882 / 1764 (default
 // below: two at 1764)
@@ -57,8 +58,8 @@ int pn_halves(int n) {
         const char* e = std::getenv("CRLOT_PN_WIDE");
         return e ? (e[0] == '1' ? 2 : 1) : 0;
     }();
-    if (n != 882 && n != 1764) return 1;
-    return w ? w : (n == 1764 ? 2 : 1);
+    if (n != 882 && n != 1764 && n != 960 && n != 1920) return 1;
+    return w ? w : (n >= 1500 ? 2 : 1);
 }
 // CRLOT_PN_LEAN=0/1 (A/B): the two-wave walk's LDS without the windows and with an
 // exact-size ring (one more walk per CU at 1764)
@@ -340,6 +341,19 @@ bool pn_dispatch(int key, F&& f) {
         case 1000882: f(std::integral_constant<int, 1000882>{}); return true;
         case 1001764: f(std::integral_constant<int, 1001764>{}); return true;
         case 11001764: f(std::integral_constant<int, 11001764>{}); return true;
+        case 1001920: f(std::integral_constant<int, 1001920>{}); return true;
+#ifdef CRLOT_PN_15
+        case 960: f(std::integral_constant<int, 960>{}); return true;
+        case 480: f(std::integral_constant<int, 480>{}); return true;
+        case 100960: f(std::integral_constant<int, 100960>{}); return true;
+        case 200960: f(std::integral_constant<int, 200960>{}); return true;
+        case 300960: f(std::integral_constant<int, 300960>{}); return true;
+        case 100480: f(std::integral_constant<int, 100480>{}); return true;
+        case 200480: f(std::integral_constant<int, 200480>{}); return true;
+        case 300480: f(std::integral_constant<int, 300480>{}); return true;
+        case 1101920: f(std::integral_constant<int, 1101920>{}); return true;
+        case 1201920: f(std::integral_constant<int, 1201920>{}); return true;
+#endif
 #ifdef CRLOT_PN_VARIANTS
         case 100882: f(std::integral_constant<int, 100882>{}); return true;
         case 200882: f(std::integral_constant<int, 200882>{}); return true;
@@ -356,7 +370,17 @@ bool pn_dispatch(int key, F&& f) {
 }  // namespace fk
 
 bool pairn_size(int n) {
-    return fk::pn_dispatch(n, [](auto) {});
+    return fk::pn_dispatch(fk::pn_key(n), [](auto) {});
+}
+
+// K_pairN in place of K_pair15 at N = 960 / 480 (CRLOT_PN_OVER15=1, A/B builds
+// with -DCRLOT_PN_15)
+bool pairn_over_pair15(int n) {
+    static const bool v = [] {
+        const char* e = std::getenv("CRLOT_PN_OVER15");
+        return e && e[0] == '1';
+    }();
+    return v && (n == 960 || n == 480) && pairn_size(n);
 }
 
 bool pairn_supported(int n, int h, int ring_len) {

@@ -1076,7 +1076,7 @@ def test_pair15_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda, n, 
                                         (882, 147, 0, 9_999), (1764, 441, 0, 48_000), (1764, 441, 1, 40_000),
                                         (1764, 882, 0, 30_007), (1000, 250, 0, 20_000), (640, 320, 0, 20_011),
                                         (400, 160, 0, 16_000), (320, 160, 1, 9_999), (320, 80, 0, 700),
-                                        (882, 441, 0, 500)])
+                                        (882, 441, 0, 500), (1920, 480, 0, 48_000), (1920, 960, 1, 30_001)])
 def test_pairn_vs_oracle_and_chunking(pkg, oracle, torch_cuda, n, h, mode, T):
     """Frame sizes with factors 2, 3, 5, 7 (882 / 1764 = 20 / 40 ms at 44.1 kHz,
     1000, 640, 400, 320) in pairs through one N-point complex transform per wave
