@@ -75,5 +75,40 @@ int main() {
                     mode == 0 ? 1024 : 64, p50(rtt), p50(ph[0]), p50(ph[2]), p50(ph[3]));
     }
     delete sv;
+
+    // the shared E = 8 server (N = 1024): a forward real FFT with its speculated
+    // inverse, as IFftPlan::forward issues it
+    int rc = 0;
+    SharedServer* sh = shared_server(0, 8, &rc);
+    if (!sh) return 9;
+    CallServer* fs = sh->srv;
+    std::vector<float> x(N);
+    for (int64_t i = 0; i < N; ++i) x[size_t(i)] = float((i * 37) % 101) / 101.0f - 0.5f;
+    std::vector<double> rtt, rtt_spec, ph[4];
+    for (int it = 0; it < 3000; ++it) {
+        CallSlot sl;
+        if (fs->next_slot(&sl) != CRLOT_OK) return 10;
+        const auto t0 = std::chrono::steady_clock::now();
+        fs->put(sl.in, x.data(), size_t(N));
+        CallReq r{};
+        r.op = kCallRfft;
+        r.batch = 1;
+        r.win_off = -1;
+        r.p0 = sh->d_tw;
+        r.p1 = sh->d_st;
+        r.f0 = 1.0f / float(N);
+        r.flags = kCallSpec;
+        if (fs->submit(r, sl) != CRLOT_OK || fs->wait(sl.index) != CRLOT_OK) return 11;
+        const auto t1 = std::chrono::steady_clock::now();
+        if (fs->wait_spec(sl.index) != CRLOT_OK) return 12;
+        const auto t2 = std::chrono::steady_clock::now();
+        rtt.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+        rtt_spec.push_back(std::chrono::duration<double, std::micro>(t2 - t0).count());
+        const CallHostCtl* h = fs->host_ctl();
+        for (int i = 0; i < 4; ++i) ph[i].push_back(double(__atomic_load_n(&h->ph[i], __ATOMIC_ACQUIRE)) * tick);
+    }
+    std::printf("{\"rfft1024_spec\": {\"host_done_us_p50\": %.2f, \"host_spec_us_p50\": %.2f, \"dev_compute_us\": %.2f, "
+                "\"dev_fence_end_us\": %.2f, \"dev_spec_end_us\": %.2f, \"dev_spec_fence_end_us\": %.2f}}\n",
+                p50(rtt), p50(rtt_spec), p50(ph[0]), p50(ph[1]), p50(ph[2]), p50(ph[3]));
     return 0;
 }
