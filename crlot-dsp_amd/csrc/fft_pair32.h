@@ -88,20 +88,27 @@ constexpr int kP32T = 31 * 32;
 __host__ __device__ constexpr int pair32_t_index(int k1, int l) {
     return k1 == 31 ? 960 + l : ((k1 - 1) >> 1) * 64 + 2 * l + ((k1 - 1) & 1);
 }
+// (in groups of 8 twiddles: all 31 loaded at once would hold 62 VGPRs beside
+// the walk's 160 of data, hops and OLA blocks)
 template <bool INV>
 __device__ __forceinline__ void pair32_tw_apply(pc (&v)[32], const pc* t, int lane) {
     const float4* t4 = reinterpret_cast<const float4*>(t + 2 * (lane & 31));
-    pc w[31];
 #pragma unroll
-    for (int j = 0; j < 15; ++j) {
-        const float4 q = t4[j * 32];
-        w[2 * j] = pc_mk(q.x, q.y);
-        w[2 * j + 1] = pc_mk(q.z, q.w);
+    for (int g = 0; g < 4; ++g) {
+        pc w[8];
+        const int jn = g < 3 ? 4 : 3;  // b128 pairs in this group (15 in all)
+#pragma unroll
+        for (int j = 0; j < jn; ++j) {
+            const float4 q = t4[(4 * g + j) * 32];
+            w[2 * j] = pc_mk(q.x, q.y);
+            w[2 * j + 1] = pc_mk(q.z, q.w);
+        }
+        if (g == 3) w[6] = t[960 + (lane & 31)];
+        const int cnt = g < 3 ? 8 : 7;
+#pragma unroll
+        for (int i = 0; i < cnt; ++i) v[1 + 8 * g + i] = pc_tw<INV>(v[1 + 8 * g + i], w[i]);
+        __builtin_amdgcn_sched_barrier(0);
     }
-    w[30] = t[960 + (lane & 31)];
-    constexpr int idx[31] = {1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16,
-                             17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31};
-    pc_tw_run<INV>(v, idx, [&](int i) { return w[i]; });
 }
 
 // Forward: natural z[l + 32 m] -> X at (lane k1, register k2) = bin k1 + 32 k2.

@@ -583,6 +583,9 @@ constexpr bool pair_hot() {
     return SH == 4;
 }
 
+bool pair32_enabled();                                            // pair32.hip (experiment)
+hipError_t launch_pair32(const FusedArgs& a, hipStream_t stream);
+
 template <int SH, bool ILV>
 hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     constexpr int NB = 16 / SH, W = kPairWaves;
@@ -594,6 +597,11 @@ hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     if ((e = set_lds(kf, lds)) != hipSuccess) return e;
     if (!a.t.pflags || a.t.pflags_len < waves) return hipErrorInvalidValue;
     if constexpr (pair_hot<SH>()) {
+        if (!ILV && pair32_enabled() && a.pad_mode == 0 && a.t.hot && !a.t.gain) {
+            if ((e = launch_pair32(a, stream)) != hipSuccess) return e;
+            hipLaunchKernelGGL(kf, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
+            return hipGetLastError();
+        }
         if (a.pad_mode == 0 && a.t.hot && (!a.t.gain || CRLOT_PAIR_REG_TW)) {
             auto k = a.t.gain ? k_stft_ola_pair<SH, NB, W, ILV, CRLOT_PAIR_REG_TW != 0> : k_stft_ola_pair<SH, NB, W, ILV, false>;
             if ((e = set_lds(k, lds)) != hipSuccess) return e;
