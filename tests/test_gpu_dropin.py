@@ -322,3 +322,36 @@ def test_chained_speculation_hits_and_misses(pkg, oracle, torch_cuda):
         assert np.array_equal(bits(chans[0][:got]), bits(want[0])), k
         start += h
     assert ola.produced_samples() == ref.produced and ola.read_pos() == ref.read_pos
+
+
+@pytest.mark.gpu
+def test_objects_constructed_in_a_loop_reuse_pooled_resources(pkg, oracle, torch_cuda):
+    """performance_benchmark.cc:181-210 constructs FrameQueue, OLAAccumulator and
+    an FFT plan per iteration: with the resource pools (streams, pinned blocks,
+    stream-ordered device memory) every reconstructed object still starts clean
+    -- a zeroed ring, its own frames -- and each iteration's output equals the
+    oracle's OLA fed the same frames, bit for bit."""
+    n, h, L = 1024, 512, 8192
+    rng = np.random.default_rng(55)
+    w = oracle.window(oracle.HANN, n)
+    for it in range(24):
+        x = rng.standard_normal(L).astype(np.float32)
+        fq = pkg.FrameQueue(x, n, h, True, pkg.PAD_CONSTANT)
+        fft = pkg.FftPlan(n, pkg.FFT_REAL)
+        cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                            apply_window_inside=True)
+        ola = pkg.OLAAccumulator(cfg)
+        ola.set_window(w)
+        ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+        ref.set_window(w)
+        for i in range(fq.getNumFrames()):
+            y = fft.inverse_host(fft.forward_host(fq.getFrame(i)[None]))[0]
+            ola.push_frame_AoS(y, None, i * h, 0, n, 1.0)
+            ref.push_frame_aos(y, i * h, 0, n, 1.0)
+            got, chans = ola.produce(h)
+            want = ref.produce(h)
+            assert got == len(want[0])
+            assert np.array_equal(bits(chans[0][:got]), bits(want[0])), (it, i)
+        ola.close()
+        fft.close()
+        fq.close()
