@@ -362,7 +362,9 @@ bool pair_plan(const crlot_plan* p) {
 int ensure_pair_flags(const crlot_plan* p, crlot::Scratch* sc, int32_t n_streams, int64_t F) {
     if (!pair_plan(p)) return CRLOT_OK;
     int64_t have = sc->pflags_len * int64_t(sizeof(uint32_t));
-    const int rc = grow_on_stream(&sc->pflags, &have, int64_t(n_streams) * F * int64_t(sizeof(uint32_t)), sc->s,
+    // (two-wave walks of K_pairN keep a flag per wave: two per chunk, F >= chunks)
+    const int rc = grow_on_stream(&sc->pflags, &have,
+                                  int64_t(n_streams) * std::max<int64_t>(F, 2) * int64_t(sizeof(uint32_t)), sc->s,
                                   "pair flag");
     sc->pflags_len = have / int64_t(sizeof(uint32_t));
     return rc;
@@ -651,7 +653,7 @@ int crlot_plan_reserve(crlot_plan* p, int64_t bytes) {
 static void scratch_need(const crlot_plan* p, int32_t n_streams, int64_t T, int32_t channels, int64_t* flags,
                          int64_t* work, int64_t* planes) {
     const int64_t F = frames_for(p, T), S = int64_t(n_streams) * channels, L = F * p->geo.h;
-    *flags = pair_plan(p) ? S * F : 0;
+    *flags = pair_plan(p) ? S * std::max<int64_t>(F, 2) : 0;  // as ensure_pair_flags
     const bool direct_ilv = channels > 1 && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0;
     *planes = (channels > 1 && !direct_ilv) ? S * (T + L) * int64_t(sizeof(float)) : 0;
     static const float probe[2] = {0.f, 0.f};
