@@ -1098,4 +1098,5 @@ def test_pairn_vs_oracle_and_chunking(pkg, oracle, torch_cuda, n, h, mode, T):
     plan.set_frame_pairing(False)  # the per-frame walker agrees within rounding
     y_pf = host(plan.roundtrip(xd))
     for s_ in range(5):
-        assert_close(y[s_], y_pf[s_], float(np.max(np.abs(x))), f"N={n} H={h} paired vs per-frame {s_}")
+        assert_close(y[s_], y_pf[s_], float(np.max(np.abs(x))), f"N={n} H={h} paired vs per-frame {s_}",
+                     xnorm=float(np.linalg.norm(x[s_].astype(np.float64))))
