@@ -18,8 +18,8 @@ FLAGS = ["-std=c++17", "-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fn
 
 # (source, mangled-name substring, frame pairs per loop iteration, label)
 KERNELS = [
-    ("pair1k.hip", "k_stft_ola_pairILi4ELi4ELi4ELb0EEE", 4, "K_pair 1024/256 (headline)"),
-    ("pair_hot.hip", "k_pair_wg_hotINS0_12_GLOBAL__N_15Geo4kELi4ELi4EEE", 4, "K_pair4k hot 4096/1024 (config 3)"),
+    ("pair1k.hip", "k_stft_ola_pairILi4ELi4ELi4ELb0ELb0EEE", 4, "K_pair 1024/256 (headline)"),
+    ("pair_hot.hip", "k_pair_wg_hotINS0_12_GLOBAL__N_15Geo4kELi4ELi4ELb0EEE", 4, "K_pair4k hot 4096/1024 (config 3)"),
     ("pair_hot.hip", "k_pair512_hotILi2ELi4ELi4EEE", None, "K_pair512 hot 512/128"),
     ("pair_any.hip", "k_pair15_hotILi64ELi4ELb0E", None, "K_pair15 960/240"),
     ("pair_any.hip", "k_pair15_hotILi32ELi2ELb0E", None, "K_pair15 480/120"),
