@@ -66,6 +66,12 @@ struct PairLds {
 #ifndef CRLOT_PAIR_ST_AUX
 #define CRLOT_PAIR_ST_AUX 2
 #endif
+#ifndef CRLOT_PAIR_HOT2
+#define CRLOT_PAIR_HOT2 1  // ... and at H = 128
+#endif
+#ifndef CRLOT_PAIR_HOT8
+#define CRLOT_PAIR_HOT8 1  // the paired-only walker at H = 512 too
+#endif
 #ifndef CRLOT_PAIR_MIN_WAVES
 #define CRLOT_PAIR_MIN_WAVES (CRLOT_PAIR_REG_TW ? 3 : 4)
 #endif
@@ -79,7 +85,7 @@ struct PairLds {
 // register (the register held a block already produced).
 template <int NB>
 struct PairRot {
-    static constexpr int R = NB == 1 ? 4 : NB == 2 ? 8 : NB == 4 ? 8 : 16;
+    static constexpr int R = NB == 1 ? 4 : NB == 2 ? 6 : NB == 4 ? 8 : 16;
     static constexpr int U = R / 2;
     static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
 };
@@ -300,6 +306,8 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         if constexpr (U > 2) {
             if (k + 4 >= f1) break;
             step(std::integral_constant<int, 2>(), k + 4);
+        }
+        if constexpr (U > 3) {
             if (k + 6 >= f1) break;
             step(std::integral_constant<int, 3>(), k + 6);
         }
@@ -574,13 +582,15 @@ bool pair_nofix() {
 #endif
 }
 
-// The paired-only walker where it holds its registers without spilling: hops
-// of 256 (SH = 4; SH = 8 spills 9 VGPRs), with or without a spectral gain (the
-// gain table overlays the twiddle table, so only with register twiddles).
+// The paired-only walker at hops of 128, 256 and 512, with or without a spectral
+// gain (the gain table overlays the twiddle table, so only with register
+// twiddles).  H = 512 keeps 6 hop slots (a few VGPR spills, outside the hot
+// path's cost: +10 % over the two-regime walker, profiles/r03_pair_hot_hops_ab.jsonl);
+// H = 128 spills more and gains 1.5 %.
 // Other hops and reflect / edge padding run the two-regime walker over every chunk.
 template <int SH>
 constexpr bool pair_hot() {
-    return SH == 4;
+    return (SH == 2 && CRLOT_PAIR_HOT2) || SH == 4 || (SH == 8 && CRLOT_PAIR_HOT8);
 }
 
 bool pair32_enabled();                                            // pair32.hip (experiment)

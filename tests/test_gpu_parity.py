@@ -154,7 +154,8 @@ def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
         assert not np.array_equal(bits(y), bits(yu))  # the pair kernel really ran
 
 
-@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128), (2048, 512)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128), (2048, 512), (1024, 512),
+                                 (1024, 128)])
 def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch, n, h):
     """Pairs are aligned to even frames, so a stream's output bits do not depend on
     how its frames are chunked over waves nor on the batch it is processed in."""
@@ -941,7 +942,8 @@ def test_roundtrip_interleaved_direct_pair_walker(pkg, oracle, torch_cuda, h, C_
 
 @pytest.mark.parametrize("n,h,T", [(4096, 1024, 123_457), (4096, 512, 60_000), (4096, 2048, 70_001),
                                    (2048, 512, 80_003), (2048, 512, 33_000), (1024, 256, 50_000),
-                                   (512, 128, 40_001), (512, 256, 25_000)])
+                                   (512, 128, 40_001), (512, 256, 25_000), (1024, 512, 50_001),
+                                   (1024, 512, 6_000), (1024, 128, 30_001)])
 def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h, T):
     """The paired-only hot walkers (K_pair, K_pair4k, K_pair2k, K_pair512) and the two-regime walkers
     they fall back to agree bit for bit: pairing mode 2 sends the plan through the
@@ -966,7 +968,8 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
 
 
 @pytest.mark.parametrize("n,h,T,ilv", [(1024, 256, 50_000, 1), (1024, 256, 33_001, 3), (1024, 256, 2_000, 1),
-                                       (4096, 1024, 123_457, 1), (4096, 1024, 9_000, 1)])
+                                       (4096, 1024, 123_457, 1), (4096, 1024, 9_000, 1), (1024, 512, 40_000, 1),
+                                       (1024, 128, 20_000, 1)])
 def test_pair_hot_walker_spectral_gain_equals_two_regime(pkg, oracle, torch_cuda, n, h, T, ilv):
     """The hot walkers of K_pair (and K_pair4k at H = 1024) apply a spectral gain
     (the spectral hook) with the two-regime walker's operation: bit-identical to
