@@ -456,9 +456,11 @@ def suite_e2e(pkg, torch, dev):
     t = np.arange(48000) / 48000.0
     x = (0.5 * np.sin(2 * np.pi * 440 * t) + 0.3 * np.sin(2 * np.pi * 880 * t)
          + 0.2 * np.sin(2 * np.pi * 1320 * t)).astype(np.float32)
-    for h in (256, 512):
-        g = _harness("e2e_bench", h, 200)
-        cpu_us, F = _cpu_loop_us(O, native, x, 1024, h)
+    # the reference's frame (1024) at its two hops, then 20 ms frames at 48 / 44.1 kHz
+    # (the any-size call server)
+    for n, h in ((1024, 256), (1024, 512), (960, 480), (960, 240), (882, 441)):
+        g = _harness("e2e_bench", h, 200, n)
+        cpu_us, F = _cpu_loop_us(O, native, x, n, h)
         g["cpu_oracle_1thread"] = {"ms_per_iteration": round(cpu_us / 1e3, 4), "us_per_frame": round(cpu_us / F, 3),
                                    "x_realtime": round(1e6 / cpu_us, 1)}
         res["runs"].append(g)

@@ -941,8 +941,11 @@ int crlot_fft_plan_create(const crlot_fft_desc* d, crlot_fft_plan** out) {
     p->device = dev;
     pd.device = dev;
     p->pd = pd;
+    const int P = pd.frame_size / 2;  // complex points of the transform
     p->e = (is_pow2(pd.frame_size) && pd.frame_size >= 256 && pd.frame_size <= 4096)
                ? pd.frame_size / 128  // K_call<E>, E = P / 64
+           : (crlot::any_supported(P) && crlot::call_any_waves(P) > 0)
+               ? -P  // K_call<-1>: the any-size server of P (fft_any.h)
                : 0;
     if (p->e == 0) {  // staged host calls need the tables anyway: fail at construction as before
         const int rc = crlot_plan_create(&p->pd, &p->inner);
@@ -1145,7 +1148,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     }
     sh->fft.valid = false;
     sh->chain.valid = false;
-    const bool spec = kind == 0 && batch <= 4 && p->e <= 16;
+    const bool spec = kind == 0 && (p->e < 0 ? batch <= sh->any_waves : batch <= 4 && p->e <= 16);
     // chained speculation: a single frame whose inverse an OLA object pushed last time
     crlot::ChainPred pred;
     const bool chain = spec && batch == 1 && sh->target.predict && sh->target.predict(sh->target.owner, &pred) &&
@@ -1162,6 +1165,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     r.win_off = -1;
     r.p0 = sh->d_tw;
     r.p1 = sh->d_st;
+    r.p5 = sh->d_plan;  // (any size: the pass plan; null otherwise)
     r.f0 = 1.0f / float(p->nfft);  // the inverse's 1/N (real: the plan's inv_n, frame = nfft)
     if (spec) r.flags = crlot::kCallSpec;
     if (chain) {

@@ -20,6 +20,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -373,14 +374,68 @@ namespace {
 std::mutex g_shared_mu;
 SharedServer* g_shared[64][6] = {};  // [device][log2(E / 2)]
 
+std::map<std::pair<int, int>, SharedServer*> g_shared_any;  // (device, P): any-size FFT servers
+
 void stop_shared_servers() {
     for (auto& row : g_shared)
         for (SharedServer* s : row)
             if (s && s->srv) (void)s->srv->stop();
+    for (auto& kv : g_shared_any)
+        if (kv.second && kv.second->srv) (void)kv.second->srv->stop();
+}
+}  // namespace
+
+namespace {
+SharedServer* shared_server_any(int device, int P, int* rc) {
+    std::lock_guard<std::mutex> lk(g_shared_mu);
+    auto it = g_shared_any.find({device, P});
+    if (it != g_shared_any.end() && it->second) {  // (every call after the first: no table work)
+        *rc = CRLOT_OK;
+        return it->second;
+    }
+    const int waves = call_any_waves(P);
+    if (device < 0 || device >= 64 || waves == 0 || !any_supported(P)) {
+        *rc = fail(CRLOT_EUNSUPPORTED, "call server slot");
+        return nullptr;
+    }
+    SharedServer*& s = g_shared_any[{device, P}];
+    if (!s) {
+        static const bool hooked = [] { return std::atexit(stop_shared_servers) == 0; }();
+        (void)hooked;
+        DeviceGuard g(device);
+        SharedServer* n = new SharedServer();
+        n->e = -P;
+        n->any_waves = waves;
+        const std::vector<float> tw = build_any_twiddles(P);
+        const std::vector<uint8_t> plan = build_any_plan_blob(P);
+        std::vector<float> st(2 * size_t(P));
+        for (int t = 0; t < P; ++t) {  // exp(-i pi (t/P + 1/2)), as crlot_plan_create
+            const double ps = -M_PI * (double(t) / double(P) + 0.5);
+            st[2 * size_t(t)] = float(std::cos(ps));
+            st[2 * size_t(t) + 1] = float(std::sin(ps));
+        }
+        hipError_t err;
+        if ((err = hipMalloc(&n->d_tw, sizeof(float) * tw.size())) ||
+            (err = hipMalloc(&n->d_st, sizeof(float) * st.size())) ||
+            (err = hipMalloc(&n->d_plan, plan.size())) ||
+            (err = hipMemcpy(n->d_tw, tw.data(), sizeof(float) * tw.size(), hipMemcpyHostToDevice)) ||
+            (err = hipMemcpy(n->d_st, st.data(), sizeof(float) * st.size(), hipMemcpyHostToDevice)) ||
+            (err = hipMemcpy(n->d_plan, plan.data(), plan.size(), hipMemcpyHostToDevice))) {
+            *rc = hip_fail(err, "call server tables");
+            return nullptr;
+        }
+        const size_t row = size_t(2 * P + 2) * 2;
+        *rc = CallServer::create(device, -P, 8, 4 * row, 4 * row, 4 * row, &n->srv);
+        if (*rc != CRLOT_OK) return nullptr;
+        s = n;
+    }
+    *rc = CRLOT_OK;
+    return s;
 }
 }  // namespace
 
 SharedServer* shared_server(int device, int e, int* rc) {
+    if (e < 0) return shared_server_any(device, -e, rc);
     int lg = 0;
     while ((2 << lg) < e) ++lg;  // e = 2, 4, ..., 32 -> 0..4
     if (device < 0 || device >= 64 || lg > 5 || (2 << lg) != e) {

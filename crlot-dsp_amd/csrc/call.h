@@ -123,6 +123,8 @@ struct SharedServer {
     int e = 0;
     float* d_tw = nullptr;  // the size's pass twiddles and super twiddles (device, owned)
     float* d_st = nullptr;
+    void* d_plan = nullptr; // e < 0 (any size): the Stockham pass plan (device, owned)
+    int any_waves = 0;      // ... and how many transforms one request runs at once
     struct FftSpec {        // the inverse speculated after the last forward
         bool valid = false;
         uint64_t index = 0;
@@ -137,7 +139,8 @@ struct SharedServer {
     } chain;
     ChainTarget target;     // the OLA object that pushed the last speculated inverse
 };
-// the shared server of (device, e) (created on first use; never destroyed)
+// the shared server of (device, e) (created on first use; never destroyed);
+// e < 0: the FFT-only server of complex size P = -e (any size, call_any_waves)
 SharedServer* shared_server(int device, int e, int* rc);
 
 }  // namespace crlot

@@ -27,6 +27,7 @@
 // Exit conditions every thread reaches: `stop` (host 1, or 2 written by the
 // kernel itself on idle), or no request for `idle_ticks` of the 100 MHz clock;
 // the host relaunches on the next call (call.cpp).
+#include "fft_any.h"
 #include "fft_wave.h"
 #include "kernels.h"
 
@@ -42,6 +43,7 @@ constexpr int kCallWaves = kCallBlock / 64;
 // its descriptor (the slot's place is known before the descriptor is read), so a
 // call of up to 4 KB of input pays one memory latency, not two
 constexpr int kCallPre = 4 * kCallBlock;
+constexpr size_t kAnyPlanBytes = (sizeof(dev::any::Plan) + 15) / 16 * 16;
 
 // input float i (and i + 1) of the request: from the prefetched copy in LDS
 // when the whole input fits it (PRE, decided once per request), else memory
@@ -82,6 +84,10 @@ __device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
 // LDS: [tw TW cf][st P cf][sth P cf][bufs kCallWaves x P cf][spec kCallWaves x (P+1) cf][req 128 B][cmd]
 // (the speculation buffers hold each wave's spectrum for the speculative
 // inverse; N = 4096 plans go without speculation to stay within 160 KB)
+// E < 0 (any size, fft_any.h): the request's static part first, then per FFT
+// wave its Stockham buffers A, B (P cf each) and the spectrum S (P + 1 cf) kept
+// for the speculated inverse, P = CallArgs::any_p at run time; tables stay in
+// global memory (L2)
 template <int E>
 struct CallLds {
     static constexpr int P = E > 0 ? 64 * E : 1;
@@ -187,6 +193,35 @@ __device__ __forceinline__ void call_cfft(const CallIn<PRE>& in, int64_t off, fl
     }
 }
 
+// any size: fft_any.h's fft with the pass plan read from LDS into scalar
+// registers (the plan in global memory cost a scalar-cache miss per pass)
+// WG: the whole workgroup runs each pass (thread t of kCallBlock, barriers
+// between passes); else one wave (lane of 64, wave fences)
+__device__ __forceinline__ void any_sync(bool wg) {
+    if (wg)
+        __syncthreads();
+    else
+        dev::wave_lds_fence();
+}
+template <bool INV, bool WG>
+__device__ __forceinline__ const cf* any_fft(cf* x, cf* y, const dev::any::Plan* pl, const cf* tw, int lane) {
+    const int n = __builtin_amdgcn_readfirstlane(pl->n_pass), p = __builtin_amdgcn_readfirstlane(pl->p);
+    for (int i = 0; i < n; ++i) {
+        dev::any::PassDesc d;
+        d.r = __builtin_amdgcn_readfirstlane(pl->pass[i].r);
+        d.ns = __builtin_amdgcn_readfirstlane(pl->pass[i].ns);
+        d.off = __builtin_amdgcn_readfirstlane(pl->pass[i].off);
+        d.woff = __builtin_amdgcn_readfirstlane(pl->pass[i].woff);
+        d.rcp_ns = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, pl->pass[i].rcp_ns)));
+        dev::any::pass<INV>(x, y, tw, p, d, lane, WG ? kCallBlock : 64);
+        any_sync(WG);
+        cf* t = x;
+        x = y;
+        y = t;
+    }
+    return x;
+}
+
 template <int E>
 __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     constexpr int P = CallLds<E>::P, TW = CallLds<E>::TW;
@@ -196,10 +231,19 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     cf* sth = st + P;
     cf* bufs = sth + P;
     cf* specs = bufs + kCallWaves * P;
-    float* pre = reinterpret_cast<float*>(specs + kCallWaves * CallLds<E>::SP);
+    constexpr bool ANY = E < 0;
+    float* pre = ANY ? reinterpret_cast<float*>(smem) : reinterpret_cast<float*>(specs + kCallWaves * CallLds<E>::SP);
     float* chainbuf = pre + kCallPre;  // the frame a chained forward kept for the push that follows
     CallReq* rq = reinterpret_cast<CallReq*>(chainbuf + CallLds<E>::CH);
     uint32_t* cmd = reinterpret_cast<uint32_t*>(rq + 1);
+    // ANY: [plan][tw any_tw cf][st P cf][chain frame 2P f][per wave A, B (P cf), S (P + 1 cf)]
+    dev::any::Plan* const aplan = reinterpret_cast<dev::any::Plan*>(reinterpret_cast<char*>(cmd) + 16);
+    cf* const dyn = reinterpret_cast<cf*>(reinterpret_cast<char*>(aplan) + (ANY ? kAnyPlanBytes : 0));
+    cf* const atw = dyn;
+    cf* const ast = atw + (ANY ? a.any_tw : 0);
+    float* const achain = reinterpret_cast<float*>(ast + (ANY ? a.any_p : 0));
+    cf* const awaves = reinterpret_cast<cf*>(achain + (ANY ? 2 * a.any_p : 0));
+    float* const chainp = ANY ? achain : chainbuf;  // the kept frame of a chained forward
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     cf* buf = bufs + wave * P;
@@ -262,13 +306,13 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             // the frame bits the host compared), then a served produce's clear
             float* ring = r.pend.ring;
             const int64_t R = r.pend.R;
-            if constexpr (CallLds<E>::CH > 0) {
+            if constexpr (CallLds<E>::CH > 0 || ANY) {
                 if (r.pend.flags & kPendCommit) {
                     const float* wobj = r.pend.win;
                     for (int64_t j = t; j < r.pend.len; j += kCallBlock) {
                         int64_t p = r.pend.start + j;
                         if (p >= R) p -= R;
-                        const float s = chainbuf[j];
+                        const float s = chainp[j];
                         ring[p] = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[j], 0.0f), r.pend.gain, ring[p])
                                        : __builtin_fmaf(s, r.pend.gain, ring[p]);
                     }
@@ -284,13 +328,15 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             }
             __syncthreads();
         }
+        CALL_PH(4);  // deferred ring work done
         const float* in = a.in_arena + r.in_off;  // r.in_off is the slot's start
         // the input floats this request reads: when they fit the prefetched 4 KB,
         // every read comes from LDS
+        const int64_t Pr = ANY ? a.any_p : P;  // complex points of an FFT request
         const int64_t need = r.op == kCallOlaAdd ? r.i[2] * r.channels + (r.win_off >= 0 ? r.i[2] : 0)
-                             : r.op == kCallRfft ? int64_t(r.batch) * 2 * P
-                             : r.op == kCallIrfft ? int64_t(r.batch) * (2 * P + 2)
-                             : (r.op == kCallCfft || r.op == kCallIcfft) ? int64_t(r.batch) * 2 * P
+                             : r.op == kCallRfft ? int64_t(r.batch) * 2 * Pr
+                             : r.op == kCallIrfft ? int64_t(r.batch) * (2 * Pr + 2)
+                             : (r.op == kCallCfft || r.op == kCallIcfft) ? int64_t(r.batch) * 2 * Pr
                              : (r.op == kCallAxpy || r.op == kCallNormalize) ? 2 * r.i[0]
                              : r.op == kCallAxpyWin ? 3 * r.i[0] : 0;
         const bool pre_all = need <= kCallPre;
@@ -353,6 +399,94 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                         call_cfft<E, true>(cin, int64_t(b) * 2 * P, out + int64_t(b) * 2 * P, buf, tw, r.f0, lane);
                 }
                 });
+            }
+        }
+        if constexpr (ANY) {
+            // any size: k_fft_any's arithmetic (Stockham passes of fft_any.h through the
+            // wave's A / B buffers, rsplit / rmerge), one transform per wave, the
+            // first any_waves waves; tables and the pass plan from global memory
+            // (r.p0 twiddles, r.p1 super twiddles, r.p3 the plan: uniform loads)
+            if (r.op >= kCallRfft && r.op <= kCallIcfft) {
+                const int Pn = a.any_p, W = a.any_waves;
+                if (r.p0 != staged_tw) {  // the server's plan and tables into LDS, once
+                    const cf* g0 = reinterpret_cast<const cf*>(r.p0);
+                    const cf* g1 = reinterpret_cast<const cf*>(r.p1);
+                    const uint32_t* gp = reinterpret_cast<const uint32_t*>(r.p5);
+                    for (int i = t; i < int(sizeof(dev::any::Plan) / 4); i += kCallBlock)
+                        reinterpret_cast<uint32_t*>(aplan)[i] = gp[i];
+                    for (int i = t; i < a.any_tw; i += kCallBlock) atw[i] = g0[i];
+                    for (int i = t; i < Pn; i += kCallBlock) ast[i] = g1[i];
+                    staged_tw = r.p0;
+                    __syncthreads();
+                }
+                const cf* gtw = atw;
+                const cf* gst = ast;
+                // one transform (the per-call case): the whole workgroup runs each pass
+                // between barriers; several: one wave each, the first any_waves waves
+                const bool wg = r.batch == 1;
+                const int tid = wg ? t : lane, nth = wg ? kCallBlock : 64;
+                cf* A = awaves + size_t(wg ? 0 : wave) * (3 * Pn + 1);
+                cf* B = A + Pn;
+                cf* S = B + Pn;
+                spec = r.op == kCallRfft && (r.flags & kCallSpec) != 0 && r.batch <= W;
+                if (wg || wave < W) {
+                    with_in([&](const auto& cin) {
+                    for (int b = wg ? 0 : wave; b < r.batch; b += W) {
+                        if (r.op == kCallRfft) {
+                            const int64_t x = int64_t(b) * 2 * Pn;
+                            for (int i = tid; i < Pn; i += nth) {
+                                const float2 v = cin.at2(x + 2 * i);
+                                A[i] = {dev::sanit(v.x), dev::sanit(v.y)};
+                            }
+                            any_sync(wg);
+                            const cf* z = wg ? any_fft<false, true>(A, B, aplan, gtw, t)
+                                             : any_fft<false, false>(A, B, aplan, gtw, lane);
+                            float* sp = out + int64_t(b) * (2 * Pn + 2);
+                            for (int k = tid; k < Pn; k += nth) {
+                                cf xk, xp;
+                                dev::any::rsplit(z, Pn, gst, k, xk, xp);
+                                *reinterpret_cast<float2*>(sp + 2 * k) = make_float2(xk.r, xk.i);
+                                if (spec) S[k] = xk;
+                                if (k == 0) {
+                                    *reinterpret_cast<float2*>(sp + 2 * Pn) = make_float2(xp.r, xp.i);
+                                    if (spec) S[Pn] = xp;
+                                }
+                            }
+                        } else if (r.op == kCallIrfft) {
+                            const int64_t x = int64_t(b) * (2 * Pn + 2);
+                            for (int k = tid; k < Pn; k += nth) {
+                                const float2 u = cin.at2(x + 2 * k), w = cin.at2(x + 2 * (Pn - k));
+                                A[k] = dev::any::rmerge(cf{u.x, u.y}, cf{w.x, w.y}, gst[k], k);
+                            }
+                            any_sync(wg);
+                            const cf* z = wg ? any_fft<true, true>(A, B, aplan, gtw, t)
+                                             : any_fft<true, false>(A, B, aplan, gtw, lane);
+                            float* o = out + int64_t(b) * 2 * Pn;
+                            for (int i = tid; i < Pn; i += nth)
+                                *reinterpret_cast<float2*>(o + 2 * i) =
+                                    make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0));
+                        } else {
+                            const int64_t x = int64_t(b) * 2 * Pn;
+                            for (int i = tid; i < Pn; i += nth) {
+                                const float2 v = cin.at2(x + 2 * i);
+                                A[i] = {v.x, v.y};
+                            }
+                            any_sync(wg);
+                            const bool inv = r.op == kCallIcfft;
+                            const cf* z = inv ? (wg ? any_fft<true, true>(A, B, aplan, gtw, t)
+                                                    : any_fft<true, false>(A, B, aplan, gtw, lane))
+                                              : (wg ? any_fft<false, true>(A, B, aplan, gtw, t)
+                                                    : any_fft<false, false>(A, B, aplan, gtw, lane));
+                            float* o = out + int64_t(b) * 2 * Pn;
+                            for (int i = tid; i < Pn; i += nth)
+                                *reinterpret_cast<float2*>(o + 2 * i) =
+                                    inv ? make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0))
+                                        : make_float2(z[i].r, z[i].i);
+                        }
+                        any_sync(wg);  // A / B are rewritten by the next transform
+                    }
+                    });
+                }
             }
         }
         if (r.op == kCallOlaAdd) {
@@ -496,7 +630,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         // behind one fence measured 12.2 us per e2e frame against 11.4 us with
         // three publishes: the host waits for the spectrum first.)
         const bool chained =
-            CallLds<E>::SPEC && spec && r.op == kCallRfft && (r.flags & kCallChain) != 0 && r.batch == 1;
+            (CallLds<E>::SPEC || ANY) && spec && r.op == kCallRfft && (r.flags & kCallChain) != 0 && r.batch == 1;
         const bool merged = spec && r.op == kCallOlaAdd;
         if (!merged) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -508,70 +642,94 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         // ---- speculation after the publish (the host is already running)
         if (spec) {
             float* so = a.out_arena + r.spec_off;
-            if constexpr (E > 0) {
-                if (CallLds<E>::SPEC && r.op == kCallRfft) {
-                    // inverse of the spectrum just written (the same bits, from LDS;
-                    // call_irfft is the inverse call's code)
-                    const bool chain = chained;
-                    // the chained produce's ring and den values, loaded under the inverse
-                    constexpr int KC = 4;
-                    float rv[KC], dv[KC];
-                    if (chain) {
+            if ((CallLds<E>::SPEC || ANY) && r.op == kCallRfft) {
+                // inverse of the spectrum just written (the same bits, from LDS; the
+                // inverse call's code), kept in LDS too for a chained produce
+                const bool chain = chained;
+                const int64_t Nf = 2 * Pr;  // frame floats
+                // the chained produce's ring and den values, loaded under the inverse
+                constexpr int KC = 4;
+                float rv[KC], dv[KC];
+                if (chain) {
 #pragma unroll
-                        for (int k = 0; k < KC; ++k) {
-                            const int64_t q = t + int64_t(k) * kCallBlock;
-                            rv[k] = dv[k] = 1.0f;
-                            if (q < r.j[3]) {
-                                int64_t p = r.j[2] + q;
-                                if (p >= r.j[0]) p -= r.j[0];
-                                rv[k] = r.p2[p];
-                                dv[k] = r.p3[p];
-                            }
+                    for (int k = 0; k < KC; ++k) {
+                        const int64_t q = t + int64_t(k) * kCallBlock;
+                        rv[k] = dv[k] = 1.0f;
+                        if (q < r.j[3]) {
+                            int64_t p = r.j[2] + q;
+                            if (p >= r.j[0]) p -= r.j[0];
+                            rv[k] = r.p2[p];
+                            dv[k] = r.p3[p];
                         }
                     }
-                    dev::wave_lds_fence();
+                }
+                dev::wave_lds_fence();
+                if constexpr (E > 0) {
                     for (int b = wave; b < r.batch; b += kCallWaves)
                         call_irfft<E>([&](int k) { return spb[k]; }, so + int64_t(b) * 2 * P, buf, tw, st, r.f0,
-                                      lane, chain ? chainbuf : nullptr);
-                    if (chain) {
-                        // publish the inverse first: the host's inverse call waits for it
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                        __syncthreads();
-                        if (t == 0) st_sys64(&a.hctl->spec_done, my);
-                        // the produce(n) block at rp after pushing that frame at start: the
-                        // push's arithmetic (axpy_windowed / axpy) on the ring as it stands
-                        __syncthreads();
-                        float* ring = r.p2;
-                        const float* den = r.p3;
-                        const float* wobj = r.p4;
-                        const int64_t R = r.j[0], start = r.j[1], rp = r.j[2], n = r.j[3];
-                        float* co = so + 2 * P;
-                        auto one = [&](int64_t q, float v, float dn) {
-                            int64_t p = rp + q;
-                            if (p >= R) p -= R;
-                            int64_t d = p - start;
-                            if (d < 0) d += R;
-                            if (d < 2 * P) {
-                                const float s = chainbuf[d];
-                                v = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[d], 0.0f), r.f1, v)
-                                         : __builtin_fmaf(s, r.f1, v);
+                                      lane, chain ? chainp : nullptr);
+                }
+                if constexpr (ANY) {
+                    const bool wg = r.batch == 1;  // as the forward: its S buffer
+                    if (wg || wave < a.any_waves) {
+                        const int Pn = a.any_p, tid = wg ? t : lane, nth = wg ? kCallBlock : 64;
+                        cf* A = awaves + size_t(wg ? 0 : wave) * (3 * Pn + 1);
+                        cf* B = A + Pn;
+                        const cf* S = B + Pn;
+                        for (int b = wg ? 0 : wave; b < r.batch; b += a.any_waves) {  // (batch <= any_waves)
+                            any_sync(wg);  // the forward's S writes
+                            for (int k = tid; k < Pn; k += nth) A[k] = dev::any::rmerge(S[k], S[Pn - k], ast[k], k);
+                            any_sync(wg);
+                            const cf* z = wg ? any_fft<true, true>(A, B, aplan, atw, t)
+                                             : any_fft<true, false>(A, B, aplan, atw, lane);
+                            float* o = so + int64_t(b) * 2 * Pn;
+                            for (int i = tid; i < Pn; i += nth) {
+                                const float2 v = make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0));
+                                *reinterpret_cast<float2*>(o + 2 * i) = v;
+                                if (chain) *reinterpret_cast<float2*>(chainp + 2 * i) = v;
                             }
-                            co[q] = v / dn;
-                        };
-#pragma unroll
-                        for (int k = 0; k < KC; ++k) {
-                            const int64_t q = t + int64_t(k) * kCallBlock;
-                            if (q < n) one(q, rv[k], dv[k]);
+                            any_sync(wg);
                         }
-                        for (int64_t q = t + int64_t(KC) * kCallBlock; q < n; q += kCallBlock) {
-                            int64_t p = rp + q;
-                            if (p >= R) p -= R;
-                            one(q, ring[p], den[p]);
-                        }
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                        __syncthreads();
-                        if (t == 0) st_sys64(&a.hctl->chain_done, my);
                     }
+                }
+                if (chain) {
+                    // publish the inverse first: the host's inverse call waits for it
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                    __syncthreads();
+                    if (t == 0) st_sys64(&a.hctl->spec_done, my);
+                    // the produce(n) block at rp after pushing that frame at start: the
+                    // push's arithmetic (axpy_windowed / axpy) on the ring as it stands
+                    __syncthreads();
+                    float* ring = r.p2;
+                    const float* den = r.p3;
+                    const float* wobj = r.p4;
+                    const int64_t R = r.j[0], start = r.j[1], rp = r.j[2], n = r.j[3];
+                    float* co = so + Nf;
+                    auto one = [&](int64_t q, float v, float dn) {
+                        int64_t p = rp + q;
+                        if (p >= R) p -= R;
+                        int64_t d = p - start;
+                        if (d < 0) d += R;
+                        if (d < Nf) {
+                            const float s = chainp[d];
+                            v = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[d], 0.0f), r.f1, v)
+                                     : __builtin_fmaf(s, r.f1, v);
+                        }
+                        co[q] = v / dn;
+                    };
+#pragma unroll
+                    for (int k = 0; k < KC; ++k) {
+                        const int64_t q = t + int64_t(k) * kCallBlock;
+                        if (q < n) one(q, rv[k], dv[k]);
+                    }
+                    for (int64_t q = t + int64_t(KC) * kCallBlock; q < n; q += kCallBlock) {
+                        int64_t p = rp + q;
+                        if (p >= R) p -= R;
+                        one(q, ring[p], den[p]);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                    __syncthreads();
+                    if (t == 0) st_sys64(&a.hctl->chain_done, my);
                 }
             }
             CALL_PH(2);
@@ -591,7 +749,24 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
 
 }  // namespace
 
+// any size: FFT waves whose A, B, S buffers fit beside the static part (0: none)
+// (tables: the twiddles of build_any_twiddles and P super twiddles; the chained
+// frame: 2P floats)
+static size_t call_any_fixed(int p) {
+    return CallLds<-1>::bytes + kAnyPlanBytes + sizeof(cf) * (build_any_twiddles(p).size() / 2 + size_t(p)) +
+           sizeof(float) * 2 * size_t(p);
+}
+int call_any_waves(int p) {
+    if (p < 1 || p > 8192) return 0;
+    const size_t per = sizeof(cf) * (3 * size_t(p) + 1), fixed = call_any_fixed(p), cap = 160 * 1024;
+    return fixed >= cap ? 0 : int(std::min<size_t>(kCallWaves, (cap - fixed) / per));
+}
+
 size_t call_lds_bytes(int e) {
+    if (e < 0) {
+        const int w = call_any_waves(-e);
+        return w ? call_any_fixed(-e) + sizeof(cf) * (3 * size_t(-e) + 1) * size_t(w) : 0;
+    }
     switch (e) {
         case 0: return CallLds<0>::bytes;
         case 2: return CallLds<2>::bytes;
@@ -607,7 +782,15 @@ hipError_t launch_call(int e, const CallArgs& a, hipStream_t s) {
     const size_t lds = call_lds_bytes(e);
     if (!lds) return hipErrorInvalidValue;
     void (*k)(const CallArgs) = nullptr;
-    switch (e) {
+    CallArgs b = a;
+    if (e < 0) {
+        b.any_p = -e;
+        b.any_waves = call_any_waves(-e);
+        b.any_tw = int(build_any_twiddles(-e).size() / 2);
+        k = k_call<-1>;
+    }
+    switch (e < 0 ? -1 : e) {
+        case -1: break;
         case 0: k = k_call<0>; break;
         case 2: k = k_call<2>; break;
         case 4: k = k_call<4>; break;
@@ -621,7 +804,7 @@ hipError_t launch_call(int e, const CallArgs& a, hipStream_t s) {
                                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
         if (err != hipSuccess) return err;
     }
-    hipLaunchKernelGGL(k, dim3(1), dim3(kCallBlock), lds, s, a);
+    hipLaunchKernelGGL(k, dim3(1), dim3(kCallBlock), lds, s, b);
     return hipGetLastError();
 }
 

@@ -56,14 +56,17 @@ __device__ __forceinline__ cf twv(const cf* tw, int i) {
 }
 
 // One Stockham pass with a compile-time radix R (2, 3, 4, 5), src -> dst.
+// (lane: this thread's first butterfly, step: the threads sharing the pass --
+// one wave, or a whole workgroup between barriers; every butterfly computes the
+// same whoever runs it)
 template <bool INV, int R>
 __device__ __forceinline__ void pass_r(const cf* __restrict__ src, cf* __restrict__ dst,
                                        const cf* __restrict__ tw, int p, const PassDesc& d,
-                                       int lane) {
+                                       int lane, int step = 64) {
     const int ns = d.ns;
     const int m = p / R;  // butterflies
     const cf* twp = tw + d.off;
-    for (int j = lane; j < m; j += 64) {
+    for (int j = lane; j < m; j += step) {
         const int jb = fdiv(j, ns, d.rcp_ns);
         const int jm = j - jb * ns;
         const int ob = jb * ns * R + jm;
@@ -142,11 +145,11 @@ __device__ __forceinline__ void pass_r(const cf* __restrict__ src, cf* __restric
 // Any other (prime) radix: y_s = sum_q (x_q W^{q jm}) W_r^{q s}, inputs re-read per output.
 template <bool INV>
 __device__ __noinline__ void pass_generic(const cf* src, cf* dst, const cf* tw, int p,
-                                          const PassDesc d, int lane) {
+                                          const PassDesc d, int lane, int step = 64) {
     const int r = d.r, ns = d.ns;
     const int m = p / r;
     const cf* wr = tw + d.woff;
-    for (int j = lane; j < m; j += 64) {
+    for (int j = lane; j < m; j += step) {
         const int jb = fdiv(j, ns, d.rcp_ns);
         const int jm = j - jb * ns;
         const int ob = jb * ns * r + jm;
@@ -167,14 +170,14 @@ __device__ __noinline__ void pass_generic(const cf* src, cf* dst, const cf* tw, 
 
 template <bool INV>
 __device__ __forceinline__ void pass(const cf* src, cf* dst, const cf* tw, int p, const PassDesc& d,
-                                     int lane) {
+                                     int lane, int step = 64) {
     switch (d.r) {
-        case 2: pass_r<INV, 2>(src, dst, tw, p, d, lane); break;
-        case 3: pass_r<INV, 3>(src, dst, tw, p, d, lane); break;
-        case 4: pass_r<INV, 4>(src, dst, tw, p, d, lane); break;
-        case 5: pass_r<INV, 5>(src, dst, tw, p, d, lane); break;
-        case 7: pass_r<INV, 7>(src, dst, tw, p, d, lane); break;
-        default: pass_generic<INV>(src, dst, tw, p, d, lane); break;
+        case 2: pass_r<INV, 2>(src, dst, tw, p, d, lane, step); break;
+        case 3: pass_r<INV, 3>(src, dst, tw, p, d, lane, step); break;
+        case 4: pass_r<INV, 4>(src, dst, tw, p, d, lane, step); break;
+        case 5: pass_r<INV, 5>(src, dst, tw, p, d, lane, step); break;
+        case 7: pass_r<INV, 7>(src, dst, tw, p, d, lane, step); break;
+        default: pass_generic<INV>(src, dst, tw, p, d, lane, step); break;
     }
 }
 
@@ -190,6 +193,27 @@ __device__ __forceinline__ cf* fft(cf* a, cf* b, const Plan& pl, const cf* tw, i
         b = t;
     }
     return a;
+}
+
+// kiss_fftr split of bin k < P from the P-point FFT z of the packed real frame:
+// X[k], and X[P] when k = 0 (st: exp(-i pi (k/P + 1/2))).  k_fft_any's forward
+// and the call server's (call_rt.hip) share it, so their spectra are bit-identical.
+__device__ __forceinline__ void rsplit(const cf* z, int p, const cf* st, int k, cf& xk, cf& xp) {
+    const cf zk = z[k];
+    const cf fpnk = conj(z[(p - k) % p]);
+    const cf f1 = cadd(zk, fpnk), f2 = csub(zk, fpnk);
+    const cf w = st[k];
+    const cf t = cmul(f2, cf{w.r * 0.5f, w.i * 0.5f});
+    xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)};
+    if (k == 0) dc_split(zk, xk, xp);
+}
+// kiss_fftri merge of bins xk = X[k], xpk = X[P-k] into Z[k] (w = st[k])
+__device__ __forceinline__ cf rmerge(const cf& xk, const cf& xpk, const cf& w, int k) {
+    const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+    const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+    return k == 0 ? dc_merge(xk, xpk)
+                  : cf{__builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r)),
+                       __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i))};
 }
 
 // kiss_fftr split -> gain -> kiss_fftri merge, src (Z) -> dst (Z'), with the

@@ -106,6 +106,7 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
 // transform (N/2 for the real kinds, nfft for the complex ones); inv_scale = 1/nfft.
 bool any_supported(int p);
 std::vector<float> build_any_twiddles(int p);
+std::vector<uint8_t> build_any_plan_blob(int p);  // dev::any::Plan bytes (fft_any.h)
 hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* twany,
                             const float* x, int n_streams, int64_t T, int64_t ld_x, int64_t F,
                             float* frames, float* spec, hipStream_t stream);
@@ -232,7 +233,8 @@ struct alignas(512) CallReq {
     const float* p3;  // chain: den
     const float* p4;  // chain: the object's window (nullable)
     int64_t j[8];     // chain: R, push start (ring pos), produce read pos, produce count
-    uint64_t pad[6];
+    const void* p5;   // FFT of any size (K_call<-1>): the pass plan (dev::any::Plan, device)
+    uint64_t pad[5];
     // Ring work the host deferred onto this request, applied before it (in this
     // order): the push of the frame the last chained forward kept (kPendCommit),
     // then the clear of a produce block served from a speculation (kPendClear).
@@ -274,9 +276,12 @@ struct CallArgs {
     int64_t in_cap = 0;             // floats per input slot (slot q % depth at q * in_cap)
     uint64_t first = 0;             // requests completed before this launch
     uint64_t idle_ticks = 0;
+    int any_p = 0, any_waves = 0, any_tw = 0;  // e < 0: complex points, FFT waves, twiddles (launch_call)
 };
-// e = 0 (OLA / kernel ops only) or the FFT's E = P / 64 in {2, 4, 8, 16, 32}
+// e = 0 (OLA / kernel ops only), the FFT's E = P / 64 in {2, 4, 8, 16, 32}, or
+// -P for any other complex size P (fft_any.h; call_any_waves(P) > 0)
 size_t call_lds_bytes(int e);
+int call_any_waves(int p);
 hipError_t launch_call(int e, const CallArgs& a, hipStream_t s);
 
 // dsp::axpy / axpy_windowed (win != nullptr) / normalize_and_clear over `batch`

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "fft_any.h"
 #include "fft_pair.h"
@@ -1634,12 +1635,7 @@ __global__ __launch_bounds__(512) void k_fft_any(const AnyArgs a) {
             const cf xk = {in[int64_t(2 * k) * a.inc_in], in[int64_t(2 * k) * a.inc_in + 1]};
             const int pk = p - k;
             const cf xpk = {in[int64_t(2 * pk) * a.inc_in], in[int64_t(2 * pk) * a.inc_in + 1]};
-            const cf w = st[k];
-            const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
-            const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
-            A[k] = k == 0 ? dev::dc_merge(xk, xpk)
-                          : cf{__builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r)),
-                               __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i))};
+            A[k] = dev::any::rmerge(xk, xpk, st[k], k);
         }
     } else {
         for (int i = lane; i < p; i += 64)
@@ -1649,13 +1645,8 @@ __global__ __launch_bounds__(512) void k_fft_any(const AnyArgs a) {
     cf* z = dev::any::fft<(KIND == 1 || KIND == 3)>(A, B, a.pl, tw, lane);
     if (KIND == 0) {  // kiss_fftr split: X[k], k <= P
         for (int k = lane; k < p; k += 64) {
-            const cf zk = z[k];
-            const cf fpnk = dev::conj(z[(p - k) % p]);
-            const cf f1 = dev::cadd(zk, fpnk), f2 = dev::csub(zk, fpnk);
-            const cf w = st[k];
-            const cf t = dev::cmul(f2, cf{w.r * 0.5f, w.i * 0.5f});
-            cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)}, xp;
-            if (k == 0) dev::dc_split(zk, xk, xp);
+            cf xk, xp;
+            dev::any::rsplit(z, p, st, k, xk, xp);
             out[int64_t(2 * k) * a.inc_out] = xk.r;
             out[int64_t(2 * k) * a.inc_out + 1] = xk.i;
             if (k == 0) {
@@ -2353,6 +2344,14 @@ dev::any::Plan make_any_plan(int p) {
         ns *= d.r;
     }
     return pl;
+}
+
+// the plan as the call server reads it from device memory (call_rt.hip)
+std::vector<uint8_t> build_any_plan_blob(int p) {
+    const dev::any::Plan pl = make_any_plan(p);
+    std::vector<uint8_t> b(sizeof(pl));
+    std::memcpy(b.data(), &pl, sizeof(pl));
+    return b;
 }
 
 bool any_supported(int p) {

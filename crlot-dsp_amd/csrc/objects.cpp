@@ -197,7 +197,7 @@ struct crlot_ola {
     // host-pointer calls run on a resident call server (call_rt.hip); device-form
     // calls on streams.  Switching between the two drains the other side first.
     crlot::CallServer* srv = nullptr;
-    crlot::SharedServer* shared = nullptr;  // frame sizes 256..4096 (powers of two): the size's
+    crlot::SharedServer* shared = nullptr;  // powers of two 256..4096, and other even sizes the any-size server holds: the size's
                                       // server, shared with the FFT plans (chained speculation)
     int mode = 0;                     // 0 none yet, 1 streams, 2 call server
     int64_t last_start = -1;          // start_sample and gain of the last host push
@@ -355,8 +355,11 @@ int to_server(crlot_ola* o) {
     if (!o->srv) {
         const size_t C = size_t(o->C()), N = size_t(o->N()), R = size_t(o->R);
         const bool pow2 = N >= 256 && N <= 4096 && (N & (N - 1)) == 0;
+        // other even sizes: the any-size server of the FFT plans of this frame size
+        const bool any = !pow2 && N % 2 == 0 && crlot::any_supported(int(N / 2)) && crlot::call_any_waves(int(N / 2)) > 0;
         int rc = CRLOT_OK;
-        if (pow2 && (o->shared = crlot::shared_server(o->device, int(N / 128), &rc)) != nullptr) {
+        if ((pow2 || any) &&
+            (o->shared = crlot::shared_server(o->device, pow2 ? int(N / 128) : -int(N / 2), &rc)) != nullptr) {
             o->srv = o->shared->srv;
         } else {
             const size_t blk = std::min(R, std::max<size_t>(N, 1024));

@@ -15,7 +15,8 @@
 //   fft1024         IFftPlan::forward alone, p50 us (:187-205, 10000 calls)
 //   quality         SNR and cross-correlation delay exactly as :77-128 compute
 //                   them, on the streaming-interleaved output
-// Usage: e2e_bench [hop=256] [iterations=200]
+//   (fft_forward_us_p50: the same at the frame size given, 1024 by default)
+// Usage: e2e_bench [hop=256] [iterations=200] [frame=1024]
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -35,11 +36,12 @@ static double us_since(clk::time_point t0) {
     return std::chrono::duration<double, std::micro>(clk::now() - t0).count();
 }
 
-static double p50(std::vector<double> v) {
+static double pct(std::vector<double> v, double q) {
     if (v.empty()) return 0.0;
     std::sort(v.begin(), v.end());
-    return v[v.size() / 2];
+    return v[size_t(q * double(v.size() - 1))];
 }
+static double p50(const std::vector<double>& v) { return pct(v, 0.5); }
 
 // e2e_benchmark.cc:77-100
 static double calculate_snr(const std::vector<float>& original, const std::vector<float>& processed) {
@@ -105,7 +107,7 @@ struct Pipeline {
 int main(int argc, char** argv) {
     const size_t H = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 256;
     const int iters = argc > 2 ? std::atoi(argv[2]) : 200;
-    const size_t N = 1024, T = 48000;
+    const size_t N = argc > 3 ? std::strtoul(argv[3], nullptr, 10) : 1024, T = 48000;
     const double sr = 48000.0;
     std::vector<float> x(T);
     for (size_t i = 0; i < T; ++i) {
@@ -212,13 +214,15 @@ int main(int argc, char** argv) {
             "\"harness_order\": {\"ms_p50\": %.4f, \"x_realtime\": %.2f, \"us_per_frame\": %.3f}, "
             "\"per_call_us_p50\": {\"pop_window\": %.3f, \"forward\": %.3f, \"inverse\": %.3f, \"push_frame_AoS\": "
             "%.3f, \"produce\": %.3f}, "
-            "\"fft1024_forward_us_p50\": %.3f, "
+            "\"forward_us_p10_p90\": [%.3f, %.3f], \"inverse_us_p10_p90\": [%.3f, %.3f], "
+            "\"fft_forward_us_p50\": %.3f, "
             "\"quality\": {\"snr_db\": %.4f, \"delay_ms\": %.4f}}\n",
             // 1 s of audio per iteration: x real-time = 1 s / iteration time; the
             // reference's reporter prints (48000 / ms) * 1000 under that name (:311-317)
             N, H, T, frames, iters, it_p50 / 1e3, 1e6 / it_p50, 48000.0 / (it_p50 / 1e3) * 1000.0,
             it_p50 / double(frames), double(T) / it_p50, ho_p50 / 1e3, 1e6 / ho_p50, ho_p50 / double(frames), p50(t_pop),
-            p50(t_fwd), p50(t_inv), p50(t_push), p50(t_prod), p50(f_us), snr, delay);
+            p50(t_fwd), p50(t_inv), p50(t_push), p50(t_prod), pct(t_fwd, 0.1), pct(t_fwd, 0.9), pct(t_inv, 0.1),
+            pct(t_inv, 0.9), p50(f_us), snr, delay);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 4;

@@ -82,3 +82,19 @@ def test_e2e_loop_two_channels_interleaved(tmp_path, torch_cuda, oracle, e2e_gol
         if c < ys.shape[0]:
             ref = ys[c]
             assert np.linalg.norm(y2[c] - ref) <= 1e-6 * max(np.linalg.norm(ref), np.linalg.norm(xs[c]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h", [(960, 240), (882, 441), (1920, 480)])
+def test_e2e_loop_any_size_vs_oracle(tmp_path, torch_cuda, oracle, n, h):
+    """The e2e loop at 20 / 40 ms frames (48 and 44.1 kHz): the FFT plan and the
+    OLA object share the any-size call server (fft_any.h passes, chained
+    speculation); the output is the oracle's round trip within the parity
+    tolerance and the oracle's OLAAccumulator fed the loop's frames bit for bit."""
+    x = oracle.synth_streams(1, 30_000, config_id=91)[0]
+    y, frames = run_loop(tmp_path, x, x.size, 1, n, h, "zpad")
+    ref = oracle.roundtrip(x, n, h)
+    assert y.shape[1] == ref.size
+    assert np.linalg.norm(y[0] - ref) <= 1e-6 * max(np.linalg.norm(ref), np.linalg.norm(x))
+    assert np.max(np.abs(y[0] - ref)) <= 4e-6 * float(np.max(np.abs(x)))
+    assert np.array_equal(y, oracle_ola(oracle, frames, n, h, 1))

@@ -209,6 +209,40 @@ def test_fft_host_calls_equal_device_kernels(pkg, oracle, torch_cuda, nfft):
         assert np.array_equal(bits(y3), bits(y_dev)), (nfft, B)
 
 
+@pytest.mark.parametrize("nfft", [960, 882, 480, 1764, 1920, 1000, 130, 6, 2, 8192, 16384])
+def test_fft_host_calls_any_size(pkg, oracle, torch_cuda, nfft):
+    """Sizes outside the power-of-two call kernels run on the any-size call
+    server (K_call<-1>: fft_any.h's passes, one transform per wave; 16384 has no
+    room for its buffers and stages through launches): the launched k_fft_any's
+    bits for forward, inverse and the complex forms, the speculated inverse
+    served only for the unchanged spectrum, the kissfft restatement within the
+    parity tolerance."""
+    torch = torch_cuda
+    rng = np.random.default_rng(nfft + 5)
+    plan = pkg.FftPlan(nfft)
+    for B in (1, 3, 4, 9):
+        x = rng.standard_normal((B, nfft)).astype(np.float32)
+        X = plan.forward_host(x)
+        assert np.array_equal(X.view(np.uint32), host(plan.forward(dev(torch, x))).view(np.uint32)), (nfft, B)
+        ref = oracle.bench_rfft(x, nfft)
+        assert np.linalg.norm(X - ref) <= 1e-6 * np.linalg.norm(ref), (nfft, B)
+        y_dev = host(plan.inverse(dev(torch, X)))
+        assert np.array_equal(bits(plan.inverse_host(X)), bits(y_dev)), (nfft, B)  # speculated when B <= waves
+        X2 = X.copy()
+        X2[:, nfft // 4] *= 0.5
+        plan.forward_host(x)
+        y2 = plan.inverse_host(X2)
+        assert np.array_equal(bits(y2), bits(host(plan.inverse(dev(torch, X2))))), (nfft, B)
+        assert np.linalg.norm(y_dev - x) <= 1e-5 * np.linalg.norm(x), (nfft, B)
+    if nfft <= 8192:
+        cp = pkg.FftPlan(nfft, domain=pkg.FFT_COMPLEX)
+        z = (rng.standard_normal((3, nfft)) + 1j * rng.standard_normal((3, nfft))).astype(np.complex64)
+        Z = cp.forward_complex_host(z)
+        assert np.array_equal(Z.view(np.uint32), host(cp.forward_complex(dev(torch, z))).view(np.uint32)), nfft
+        zi = cp.inverse_complex_host(Z)
+        assert np.array_equal(zi.view(np.uint32), host(cp.inverse_complex(dev(torch, Z))).view(np.uint32)), nfft
+
+
 def test_fft_host_strides_complex_and_fallback(pkg, oracle, torch_cuda):
     """The reference's stride semantics (kissfft_adapter.cc:97-98, 139-140): batch b
     at b*stride*len, element i at i*stride, untouched elements kept; the complex
@@ -235,7 +269,7 @@ def test_fft_host_strides_complex_and_fallback(pkg, oracle, torch_cuda):
         zi = cp.inverse_complex_host(Z)
         assert np.array_equal(zi.view(np.uint32), host(cp.inverse_complex(dev(torch, Z))).view(np.uint32)), nc
         assert np.linalg.norm(zi - z) <= 1e-5 * np.linalg.norm(z), nc
-    p960 = pkg.FftPlan(960)  # mixed radix: staged launches
+    p960 = pkg.FftPlan(960)  # mixed radix: the any-size call server
     x = rng.standard_normal((2, 960)).astype(np.float32)
     X = p960.forward_host(x)
     assert np.array_equal(X.view(np.uint32), host(p960.forward(dev(torch, x))).view(np.uint32))
@@ -279,15 +313,16 @@ def test_ola_host_calls_speculated_produce(pkg, oracle, torch_cuda):
 
 
 @pytest.mark.gpu
-def test_chained_speculation_hits_and_misses(pkg, oracle, torch_cuda):
+@pytest.mark.parametrize("n,h", [(1024, 256), (960, 240), (882, 441)])
+def test_chained_speculation_hits_and_misses(pkg, oracle, torch_cuda, n, h):
     """The e2e loop's rhythm (forward -> inverse -> push_frame_AoS(inverse) ->
     produce(H)) on one FFT plan and one mono OLA object, with the rhythm broken
     on purpose: a pushed frame one bit off the speculated inverse, another gain,
     another produce count, an extra forward between inverse and push, a push at
     an unexpected position.  Every produce is bit-identical to the oracle's
     OLAAccumulator fed the frames actually pushed, whichever of the chained,
-    speculated or computed paths served it."""
-    n, h = 1024, 256
+    speculated or computed paths served it.  960 and 882 run on the any-size
+    call server (fft_any.h), which the OLA object shares with the FFT plan."""
     rng = np.random.default_rng(33)
     w = oracle.window(oracle.HANN, n)
     fft = pkg.FftPlan(n, pkg.FFT_REAL)
