@@ -1360,6 +1360,16 @@ struct crlot_stream_rt {
     uint64_t idle_ticks = 0;
     double tick_ns = 10.0;
     int64_t timeout_us = 2000000;
+    // Shapes K_stream_rt has no instantiation for (N outside 256..2048 powers of
+    // two, H % 128 != 0: 960/480, 882/441 ...): the same slot / submit / wait
+    // contract over the per-launch stream object -- per hop an H2D copy of the
+    // slot, the hop kernel, a D2H copy into the output slot, an event -- so every
+    // frame size the plan supports streams from host memory, bit-identical to
+    // crlot_stream_push_hop (no resident kernel, a launch per hop).
+    crlot_stream* lm = nullptr;
+    float* d_io = nullptr;             // [depth][in C*H | out C*H]
+    std::vector<hipEvent_t> lev;       // per slot: the hop's D2H done
+    std::vector<int32_t> lem;          // per slot: samples per channel the hop emitted
 };
 
 namespace {
@@ -1481,9 +1491,35 @@ int crlot_stream_rt_create(crlot_plan* p, int32_t channels, int32_t interleaved,
     if (depth > 64) return fail(CRLOT_EINVAL, "depth must be 1..64");
     if (p->boundary == CRLOT_FRAMEQUEUE)
         return fail(CRLOT_EINVAL, "FrameQueue framing is whole-signal; stream with ZERO_PAD/DROP");
-    if (!crlot::fused_supported(p->geo.n, p->geo.h) || p->geo.n > 2048)
-        return fail(CRLOT_EUNSUPPORTED, "resident streaming needs N in 256..2048, H % 128 == 0, N % H == 0");
     DeviceGuard g(p->device);
+    if (!crlot::fused_supported(p->geo.n, p->geo.h) || p->geo.n > 2048) {  // launch mode (struct comment)
+        crlot_stream_rt* st = new crlot_stream_rt();
+        st->plan = p;
+        st->channels = channels;
+        st->interleaved = interleaved ? 1 : 0;
+        st->depth = depth;
+        int rc = crlot_stream_create(p, channels, &st->lm);
+        if (rc != CRLOT_OK) {
+            delete st;
+            return rc;
+        }
+        const size_t hop = size_t(channels) * size_t(p->geo.h);
+        st->lev.assign(size_t(depth), nullptr);
+        st->lem.assign(size_t(depth), 0);
+        hipError_t e = hipStreamCreateWithFlags(&st->s, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&st->in_ring), sizeof(float) * hop * depth);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&st->out_ring), sizeof(float) * hop * depth);
+        if (e == hipSuccess) e = hipMalloc(&st->d_io, sizeof(float) * 2 * hop * depth);
+        for (int i = 0; e == hipSuccess && i < depth; ++i) e = hipEventCreateWithFlags(&st->lev[size_t(i)], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            crlot_stream_rt_destroy(st);
+            return hip_fail(e, "stream (launch mode) allocation");
+        }
+        std::memset(st->in_ring, 0, sizeof(float) * hop * depth);
+        std::memset(st->out_ring, 0, sizeof(float) * hop * depth);
+        *out = st;
+        return CRLOT_OK;
+    }
     crlot_stream_rt* st = new crlot_stream_rt();
     st->plan = p;
     st->channels = channels;
@@ -1526,6 +1562,18 @@ int crlot_stream_rt_create(crlot_plan* p, int32_t channels, int32_t interleaved,
 void crlot_stream_rt_destroy(crlot_stream_rt* st) {
     if (!st) return;
     DeviceGuard g(st->plan->device);
+    if (st->lm || st->d_io) {  // launch mode
+        if (st->s) (void)hipStreamSynchronize(st->s);
+        for (hipEvent_t ev : st->lev)
+            if (ev) (void)hipEventDestroy(ev);
+        if (st->d_io) (void)hipFree(st->d_io);
+        if (st->in_ring) (void)hipHostFree(st->in_ring);
+        if (st->out_ring) (void)hipHostFree(st->out_ring);
+        if (st->s) (void)hipStreamDestroy(st->s);
+        crlot_stream_destroy(st->lm);
+        delete st;
+        return;
+    }
     {
         std::lock_guard<std::mutex> lk(st->plan->mu);
         auto& v = st->plan->residents;
@@ -1544,6 +1592,12 @@ void crlot_stream_rt_destroy(crlot_stream_rt* st) {
 int crlot_stream_rt_reset(crlot_stream_rt* st) {
     if (!st) return fail(CRLOT_EINVAL, "null stream");
     DeviceGuard g(st->plan->device);
+    if (st->lm) {
+        hipError_t e = hipStreamSynchronize(st->s);
+        if (e != hipSuccess) return hip_fail(e, "stream (launch mode)");
+        st->q = 0;
+        return crlot_stream_reset(st->lm);
+    }
     int rc = rt_stop(st);
     if (rc != CRLOT_OK) return rc;
     hipError_t e = hipMemsetAsync(st->d_state, 0, sizeof(float) * st->state_floats, st->s);
@@ -1557,6 +1611,11 @@ int crlot_stream_rt_reset(crlot_stream_rt* st) {
 float* crlot_stream_rt_input_slot(crlot_stream_rt* st) {
     if (!st) return nullptr;
     DeviceGuard g(st->plan->device);
+    if (st->lm) {  // the slot is free once hop q - depth's copies completed
+        const size_t slot = size_t(st->q % st->depth);
+        if (st->q >= uint64_t(st->depth) && hipEventSynchronize(st->lev[slot]) != hipSuccess) return nullptr;
+        return st->in_ring + slot * size_t(st->channels) * size_t(st->plan->geo.h);
+    }
     // the slot of hop q is free once hop q - depth has completed
     if (st->q >= uint64_t(st->depth) && rt_wait_done(st, st->q - st->depth + 1) != CRLOT_OK) return nullptr;
     const size_t hop = size_t(st->channels) * size_t(st->plan->geo.h);
@@ -1566,6 +1625,27 @@ float* crlot_stream_rt_input_slot(crlot_stream_rt* st) {
 int crlot_stream_rt_submit(crlot_stream_rt* st, int64_t* hop_index) {
     if (!st) return fail(CRLOT_EINVAL, "null stream");
     DeviceGuard g(st->plan->device);
+    if (st->lm) {
+        const size_t slot = size_t(st->q % st->depth), hop = size_t(st->channels) * size_t(st->plan->geo.h);
+        if (st->q >= uint64_t(st->depth)) {
+            hipError_t e = hipEventSynchronize(st->lev[slot]);
+            if (e != hipSuccess) return hip_fail(e, "stream (launch mode)");
+        }
+        float* din = st->d_io + 2 * slot * hop;
+        float* dout = din + hop;
+        hipError_t e = hipMemcpyAsync(din, st->in_ring + slot * hop, sizeof(float) * hop, hipMemcpyHostToDevice, st->s);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync");
+        int32_t em = 0;
+        int rc = crlot_stream_push_hop(st->lm, din, dout, &em, st->s);
+        if (rc != CRLOT_OK) return rc;
+        if ((e = hipMemcpyAsync(st->out_ring + slot * hop, dout, sizeof(float) * hop, hipMemcpyDeviceToHost, st->s)) ||
+            (e = hipEventRecord(st->lev[slot], st->s)))
+            return hip_fail(e, "stream (launch mode)");
+        st->lem[slot] = em;
+        if (hop_index) *hop_index = int64_t(st->q);
+        st->q += 1;
+        return CRLOT_OK;
+    }
     if (st->q >= uint64_t(st->depth)) {
         int rc = rt_wait_done(st, st->q - st->depth + 1);
         if (rc != CRLOT_OK) return rc;
@@ -1594,6 +1674,14 @@ int crlot_stream_rt_wait(crlot_stream_rt* st, int64_t hop_index, const float** o
     if (!st || hop_index < 0 || uint64_t(hop_index) >= st->q) return fail(CRLOT_EINVAL, "bad hop index");
     if (uint64_t(hop_index) + st->depth < st->q) return fail(CRLOT_EINVAL, "hop slot already reused");
     DeviceGuard g(st->plan->device);
+    if (st->lm) {
+        const size_t slot = size_t(uint64_t(hop_index) % st->depth);
+        hipError_t e = hipEventSynchronize(st->lev[slot]);
+        if (e != hipSuccess) return hip_fail(e, "stream (launch mode)");
+        if (emitted) *emitted = st->lem[slot];
+        if (out && st->lem[slot]) *out = st->out_ring + slot * size_t(st->channels) * size_t(st->plan->geo.h);
+        return CRLOT_OK;
+    }
     int rc = rt_wait_done(st, uint64_t(hop_index) + 1);
     if (rc != CRLOT_OK) return rc;
     const int64_t nb = st->plan->geo.n / st->plan->geo.h;
@@ -1634,6 +1722,11 @@ int crlot_stream_rt_push_hop(crlot_stream_rt* st, const float* h_in, float* h_ou
 int crlot_stream_rt_info(const crlot_stream_rt* st, int64_t* hops, double* last_device_ns, int32_t* running) {
     if (!st) return fail(CRLOT_EINVAL, "null stream");
     if (hops) *hops = int64_t(st->q);
+    if (st->lm) {  // launch mode: no resident kernel, no device stamps
+        if (last_device_ns) *last_device_ns = 0.0;
+        if (running) *running = 0;
+        return CRLOT_OK;
+    }
     if (last_device_ns) {
         uint64_t mx = 0;
         for (int w = 0; w < st->wgs; ++w) mx = std::max(mx, __atomic_load_n(&st->ctl->ticks[w], __ATOMIC_ACQUIRE));
@@ -1645,6 +1738,10 @@ int crlot_stream_rt_info(const crlot_stream_rt* st, int64_t* hops, double* last_
 
 int crlot_stream_rt_phases(const crlot_stream_rt* st, double* ns8) {
     if (!st || !ns8) return fail(CRLOT_EINVAL, "bad argument");
+    if (st->lm) {
+        for (int i = 0; i < 8; ++i) ns8[i] = 0.0;
+        return CRLOT_OK;
+    }
     for (int i = 0; i < 8; ++i) ns8[i] = double(__atomic_load_n(&st->ctl->phase[i], __ATOMIC_ACQUIRE)) * st->tick_ns;
     return CRLOT_OK;
 }
@@ -1653,6 +1750,7 @@ int crlot_stream_rt_set_idle_timeout(crlot_stream_rt* st, double seconds, double
     if (!st || !(seconds > 0.0) || !(hop_timeout_seconds > 0.0)) return fail(CRLOT_EINVAL, "bad argument");
     st->idle_ticks = uint64_t(seconds * 1e9 / st->tick_ns);
     st->timeout_us = int64_t(hop_timeout_seconds * 1e6);
+    if (st->lm) return CRLOT_OK;  // (launch mode: nothing resident to time out)
     return rt_stop(st);  // the next hop relaunches with the new timeout
 }
 

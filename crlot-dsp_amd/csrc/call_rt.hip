@@ -27,6 +27,9 @@
 // Exit conditions every thread reaches: `stop` (host 1, or 2 written by the
 // kernel itself on idle), or no request for `idle_ticks` of the 100 MHz clock;
 // the host relaunches on the next call (call.cpp).
+#include <map>
+#include <mutex>
+
 #include "fft_any.h"
 #include "fft_wave.h"
 #include "kernels.h"
@@ -752,8 +755,16 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
 // any size: FFT waves whose A, B, S buffers fit beside the static part (0: none)
 // (tables: the twiddles of build_any_twiddles and P super twiddles; the chained
 // frame: 2P floats)
+static int any_tw_len(int p) {  // float pairs of build_any_twiddles(p), built once per size
+    static std::mutex mu;
+    static std::map<int, int> len;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = len.find(p);
+    if (it == len.end()) it = len.emplace(p, int(build_any_twiddles(p).size() / 2)).first;
+    return it->second;
+}
 static size_t call_any_fixed(int p) {
-    return CallLds<-1>::bytes + kAnyPlanBytes + sizeof(cf) * (build_any_twiddles(p).size() / 2 + size_t(p)) +
+    return CallLds<-1>::bytes + kAnyPlanBytes + sizeof(cf) * (size_t(any_tw_len(p)) + size_t(p)) +
            sizeof(float) * 2 * size_t(p);
 }
 int call_any_waves(int p) {
@@ -786,7 +797,7 @@ hipError_t launch_call(int e, const CallArgs& a, hipStream_t s) {
     if (e < 0) {
         b.any_p = -e;
         b.any_waves = call_any_waves(-e);
-        b.any_tw = int(build_any_twiddles(-e).size() / 2);
+        b.any_tw = any_tw_len(-e);
         k = k_call<-1>;
     }
     switch (e < 0 ? -1 : e) {

@@ -289,6 +289,10 @@ int crlot_stream_push_hop(crlot_stream* st, const float* d_hop_in, float* d_hop_
  * reset / destroy / a plan table update) and is relaunched by the next hop; a
  * hipDeviceSynchronize elsewhere in the process therefore waits at most that
  * idle time.  N in 256..2048, H % 128 == 0, N % H == 0, channels 1..1024.
+ * Every other shape the plan streams (960/480, 882/441 ...) gets the same
+ * contract in launch mode: per hop an H2D copy of the slot, the per-launch hop
+ * kernel (crlot_stream_push_hop's, bit-identical), a D2H copy and an event; no
+ * resident kernel (info reports last_device_ns 0, running 0).
  *   push_hop      copy h_in into the next slot, submit, wait, copy the H output
  *                 samples per channel into h_out (*emitted = 0 or H); h_in /
  *                 h_out are [H][C] interleaved PCM if `interleaved`, else [C][H]

@@ -802,6 +802,69 @@ def test_stream_rt_equals_batched_drop(pkg, oracle, torch_cuda, n, h, C_, interl
     st.close()
 
 
+@pytest.mark.parametrize("n,h,C_,interleaved", [(960, 480, 3, True), (960, 240, 8, False), (882, 441, 2, True),
+                                                (480, 120, 64, False), (4096, 1024, 2, False)])
+def test_stream_rt_launch_mode_any_size(pkg, oracle, torch_cuda, n, h, C_, interleaved):
+    """Host-buffer streaming at shapes without a resident instantiation (20 / 10 ms
+    frames at 48 / 44.1 kHz, N = 4096) runs in launch mode: the per-launch Stream's
+    bits hop for hop, the batched DROP round trip's bits over the whole signal,
+    both PCM layouts, reset, and the zero-copy slot API with hops in flight."""
+    import ctypes
+    torch = torch_cuda
+    hops = 24
+    x = oracle.synth_streams(C_, hops * h, config_id=49)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.DROP, frame_pairing=False)
+    ref = pkg.Stream(plan, C_)
+    want = []
+    for q in range(hops):
+        o, em = ref.push_hop(dev(torch, x[:, q * h:(q + 1) * h]))
+        want.append(host(o).copy() if em else None)
+    ref.close()
+    st = pkg.StreamRT(plan, C_, interleaved=interleaved)
+    got = []
+    for q in range(hops):
+        hop = x[:, q * h:(q + 1) * h]
+        out, em = st.push_hop(np.ascontiguousarray(hop.T if interleaved else hop))
+        assert (em != 0) == (want[q] is not None), q
+        got.append((out.T if interleaved else out).copy() if em else None)
+        if em:
+            assert np.array_equal(bits(got[-1]), bits(want[q])), q
+    inf = st.info()
+    assert inf["hops"] == hops and not inf["running"]
+    y_batch = host(plan.roundtrip(dev(torch, x)))
+    y_rt = np.concatenate([g for g in got if g is not None], axis=1)
+    if n <= 2048:  # the batched walkers share the hop kernel's arithmetic up to 2048
+        assert np.array_equal(bits(y_rt), bits(y_batch[:, :y_rt.shape[1]]))
+    for c in range(C_):
+        assert_close(y_rt[c], y_batch[c, :y_rt.shape[1]], float(np.max(np.abs(x[c]))), f"channel {c} vs batched")
+    st.reset()
+    o, em = st.push_hop(np.ascontiguousarray(x[:, :h].T if interleaved else x[:, :h]))
+    assert (em != 0) == (want[0] is not None)
+    st.close()
+    # zero-copy slots, several hops in flight
+    st = pkg.StreamRT(plan, C_, depth=3)
+    L = pkg.lib()
+    pending = []
+    for q in range(hops):
+        slot = L.crlot_stream_rt_input_slot(st._h)
+        assert slot
+        buf = np.ctypeslib.as_array(ctypes.cast(slot, ctypes.POINTER(ctypes.c_float)), shape=(C_, h))
+        buf[:] = x[:, q * h:(q + 1) * h]
+        qi = ctypes.c_int64()
+        assert L.crlot_stream_rt_submit(st._h, ctypes.byref(qi)) == 0
+        pending.append(qi.value)
+        if len(pending) == 3 or q == hops - 1:
+            for pq in pending:
+                op, em = ctypes.c_void_p(), ctypes.c_int32()
+                assert L.crlot_stream_rt_wait(st._h, pq, ctypes.byref(op), ctypes.byref(em)) == 0
+                assert (em.value != 0) == (want[pq] is not None), pq
+                if em.value:
+                    o = np.ctypeslib.as_array(ctypes.cast(op, ctypes.POINTER(ctypes.c_float)), shape=(C_, h)).copy()
+                    assert np.array_equal(bits(o), bits(want[pq])), pq
+            pending = []
+    st.close()
+
+
 def test_stream_rt_idle_exit_reset_and_table_update(pkg, oracle, torch_cuda):
     """Exit/relaunch paths keep the bits: an idle exit mid-stream (state saved to
     HBM and restored), reset(), and a spectral-gain update mid-stream (the kernel
