@@ -1633,7 +1633,10 @@ int crlot_stream_rt_submit(crlot_stream_rt* st, int64_t* hop_index) {
         }
         float* din = st->d_io + 2 * slot * hop;
         float* dout = din + hop;
-        hipError_t e = hipMemcpyAsync(din, st->in_ring + slot * hop, sizeof(float) * hop, hipMemcpyHostToDevice, st->s);
+        // the object's own stream: order it behind a pending async table upload (as rt_launch does)
+        hipError_t e = st->plan->stage_pending ? hipStreamWaitEvent(st->s, st->plan->stage_ev, 0) : hipSuccess;
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(din, st->in_ring + slot * hop, sizeof(float) * hop, hipMemcpyHostToDevice, st->s);
         if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync");
         int32_t em = 0;
         int rc = crlot_stream_push_hop(st->lm, din, dout, &em, st->s);
