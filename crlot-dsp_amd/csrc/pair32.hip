@@ -3,8 +3,8 @@
 // transpose, no lane-bit swap), two walks per wave (the two halves walk the
 // same chunk of streams 2u and 2u+1, so every branch is uniform).
 //
-// A timing experiment for VERDICT r02 item 3 (CRLOT_PAIR32=1 selects it at
-// N = 1024, H = 256): its FFT rounds differently from the fix-up walker's, so a
+// A timing experiment for VERDICT r02 item 3 (in -DCRLOT_PAIR32_EXPERIMENT builds
+// CRLOT_PAIR32=1 selects it at N = 1024, H = 256): its FFT rounds differently from the fix-up walker's, so a
 // chunk the fix-up walker redoes would not match its neighbours bit for bit --
 // the release path keeps K_pair.  Lane hl of half h holds sample hl + 32 q of
 // each hop (q < 8), frame sample hl + 32 m (m < 32); everything else is K_pair's
@@ -202,12 +202,18 @@ void k_stft_ola_pair32(const FusedArgs a) {
     }
 }
 
+// Experiment builds only (-DCRLOT_PAIR32_EXPERIMENT, e.g. `make variant`): then
+// CRLOT_PAIR32=1 selects this walker.  The release library always runs K_pair.
 bool pair32_enabled() {
+#ifdef CRLOT_PAIR32_EXPERIMENT
     static const bool v = [] {
         const char* e = std::getenv("CRLOT_PAIR32");
         return e && e[0] == '1';
     }();
     return v;
+#else
+    return false;
+#endif
 }
 
 hipError_t launch_pair32(const FusedArgs& a, hipStream_t stream) {

@@ -1,4 +1,5 @@
 # Half-wave K_pair walker (CRLOT_PAIR32=1, pair32.hip) vs K_pair at the headline
+# (needs a library built with -DCRLOT_PAIR32_EXPERIMENT: make -C crlot-dsp_amd/csrc with pair32.o rebuilt under that flag)
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1

@@ -1,4 +1,5 @@
 # GRBM cycles, VALU / LDS instruction counts and waves: K_pair vs the half-wave walker
+# (needs a library built with -DCRLOT_PAIR32_EXPERIMENT: make -C crlot-dsp_amd/csrc with pair32.o rebuilt under that flag)
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/p32_pmc
