@@ -71,6 +71,7 @@ struct crlot_plan {
     bool fast_ok = false;     // both exact rewrites valid for the current tables
     bool den_mk_ok = false;   // every den in [2^-40, 2^40]: Markstein division exact
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
+    bool pair30 = false;      // N = 1920, even hop: the pair tables are K_pair30's (two 960-point halves)
     float* d_twany = nullptr; // per-pass twiddles of the mixed-radix path (aliases d_tw when generic)
     float* d_twany_own = nullptr;  // ... or its own table (power-of-two plans, any-shape streams)
     // Launch scratch, one slot per HIP stream (crlot::Scratch): K_pair's regime
@@ -490,10 +491,12 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
     if ((n == 1024 && h % 128 == 0 && ring % h == 0) || (n == 512 && h % 128 == 0 && ring % h == 0) ||
         (n == 2048 && h % 256 == 0 && ring % h == 0) ||
         (n == 4096 && h % 512 == 0 && ring % h == 0) ||
-        crlot::pair15_supported(n, h, ring) ||
-        crlot::pairn_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair15 / K_pairN tables
+        crlot::pair15_supported(n, h, ring) || crlot::pair30_supported(n, h, ring) ||
+        crlot::pairn_supported(n, h, ring)) {  // K_pair / K_pair512 / K_pair2k / K_pair4k / K_pair15 / K_pair30 / K_pairN tables
+        p->pair30 = crlot::pair30_supported(n, h, ring);
         const std::vector<float> ptw = ((n == 960 || n == 480) && !crlot::pairn_over_pair15(n))
                                            ? crlot::build_pair15_twiddles(n)
+                                       : p->pair30            ? crlot::build_pair30_twiddles()
                                        : crlot::pairn_size(n) ? crlot::build_pairn_twiddles(n)
                                        : n == 1024 ? crlot::build_pair_twiddles()
                                        : n == 512  ? crlot::build_pair512_twiddles()
@@ -716,8 +719,21 @@ static int roundtrip_impl(crlot_plan* p, crlot::Scratch* sc, const float* d_x, f
             if (e != hipSuccess) return hip_fail(e, "fused (any size) kernel launch");
             return CRLOT_OK;
         }
+        // N = 1920 with an even hop: two 960-point transforms on two waves (K_pair30), the same redo
+        if (p->pairing && t.ptw && p->geo.pad_mode == 0 && p->pair30 && T < lim && out_len < lim) {
+            const int rcf = ensure_pair_flags(p, sc, n_streams, F);
+            if (rcf != CRLOT_OK) return rcf;
+            const crlot::DevTables tp = tables(p, sc);
+            int nch = 0;
+            e = crlot::launch_pair30(p->geo, tp, d_x, d_y, n_streams, T, ld_x, ld_y, F, out_len, &nch, s);
+            if (e != hipSuccess) return hip_fail(e, "pair (N = 1920) kernel launch");
+            e = crlot::launch_fused_any(p->geo, tp, p->d_twany, d_x, d_y, n_streams, T, ld_x, ld_y, F, s,
+                                        tp.pflags, nch, 1);
+            if (e != hipSuccess) return hip_fail(e, "fused (any size) kernel launch");
+            return CRLOT_OK;
+        }
         // N = 320 ... 1764 with factors 2, 3, 5, 7 (K_pairN), then the same redo
-        if (p->pairing && t.ptw && p->geo.pad_mode == 0 &&
+        if (p->pairing && t.ptw && p->geo.pad_mode == 0 && !p->pair30 &&
             crlot::pairn_supported(p->geo.n, p->geo.h, p->geo.ring_len) && T < lim && out_len < lim) {
             const int rcf = ensure_pair_flags(p, sc, n_streams, F);
             if (rcf != CRLOT_OK) return rcf;

@@ -145,6 +145,12 @@ bool pairn_supported(int n, int h, int ring_len);
 hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams, int64_t T,
                         int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks, hipStream_t stream);
 std::vector<float> build_pairn_twiddles(int n);
+// K_pair30 (pair30.hip): N = 1920 frame pairs as two 960-point transforms on two
+// waves, even hops; flags per walk as launch_pairn.  Tables: t.ptw = build_pair30_twiddles().
+bool pair30_supported(int n, int h, int ring_len);
+hipError_t launch_pair30(const Geometry& g, const DevTables& t, const float* x, float* y, int n_streams, int64_t T,
+                         int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len, int* n_chunks, hipStream_t stream);
+std::vector<float> build_pair30_twiddles();
 hipError_t launch_fft_any(int kind, int p, float inv_scale, const DevTables& t, const float* twany,
                           const float* in, float* out, int batch, int64_t ld_in, int64_t inc_in,
                           int64_t ld_out, int64_t inc_out, hipStream_t stream);

@@ -1138,6 +1138,42 @@ def test_pair15_flagged_stream_falls_back_per_frame(pkg, oracle, torch_cuda, n, 
 
 
 # ------------------------------------------------------------------ K_pairN (N = 2^a 3^b 5^c 7^d frame pairs)
+@pytest.mark.parametrize("h,mode,T,gain", [(480, 0, 48_000, False), (960, 1, 30_001, False), (240, 0, 20_011, False),
+                                         (384, 0, 9_999, False), (480, 0, 30_000, True), (640, 1, 1_000, False),
+                                         (1920, 0, 12_000, False), (480, 0, 100, False)])
+def test_pair30_vs_oracle_flags_and_gain(pkg, oracle, torch_cuda, h, mode, T, gain):
+    """N = 1920 (40 ms at 48 kHz), even hops: frame pairs through two 960-point
+    transforms on two waves (K_pair30, decimation in time, one LDS exchange): the
+    oracle within the float32 tolerance, a stream with a 1e25 burst redone by the
+    per-frame walker (its bits = pairing off), bits independent of the batch, and
+    the spectral hook against the per-frame walker's gain step."""
+    torch = torch_cuda
+    n = 1920
+    x = oracle.synth_streams(5, T, config_id=301 + h)
+    if T > 5000:
+        x[2, T // 3:T // 3 + 3] = 1e25
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode)
+    if gain:
+        plan.set_spectral_gain((0.25 + np.abs(np.cos(np.arange(n // 2 + 1) * 0.01))).astype(np.float32))
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    assert y.shape == (5, oracle.frame_count(T, n, h, mode) * h)
+    y1 = host(plan.roundtrip(xd[3:4].contiguous()))
+    assert np.array_equal(bits(y1[0]), bits(y[3]))
+    plan.set_frame_pairing(False)
+    y_pf = host(plan.roundtrip(xd))
+    if T > 5000:
+        assert np.array_equal(bits(y[2]), bits(y_pf[2]))  # the flagged stream: the per-frame walker's bits
+    for s_ in (0, 1, 3, 4):
+        xn = float(np.linalg.norm(x[s_].astype(np.float64)))
+        assert_close(y[s_], y_pf[s_], float(np.max(np.abs(x[s_]))), f"H={h} paired vs per-frame {s_}", xnorm=xn)
+    if not gain:
+        ref = oracle.roundtrip_batch(x[[0, 4]], n, h, mode=mode, nthreads=2)
+        for i, s_ in enumerate((0, 4)):
+            assert_close(y[s_], ref[i], float(np.max(np.abs(x[s_]))), f"H={h} stream {s_}",
+                         xnorm=float(np.linalg.norm(x[s_].astype(np.float64))))
+
+
 @pytest.mark.parametrize("n,h,mode,T", [(882, 441, 0, 48_000), (882, 441, 1, 44_101), (882, 294, 0, 30_011),
                                         (882, 147, 0, 9_999), (1764, 441, 0, 48_000), (1764, 441, 1, 40_000),
                                         (1764, 882, 0, 30_007), (1000, 250, 0, 20_000), (640, 320, 0, 20_011),
