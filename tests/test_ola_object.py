@@ -249,7 +249,7 @@ def test_aos_soa_equivalence_grid(torch_cuda, pkg, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,h,c", [(1024, 1024, 1), (2048, 256, 2), (4096, 512, 4)])
+@pytest.mark.parametrize("n,h,c", [(1024, 1024, 1), (2048, 256, 2), (4096, 512, 4), (960, 240, 2), (882, 441, 3)])
 def test_aos_soa_edge_cases(torch_cuda, pkg, oracle, n, h, c):
     """:551-635: impulse on channel 0, H = N and H = N/8."""
     w = hann(n)
