@@ -1464,8 +1464,11 @@ int rt_wait_done(crlot_stream_rt* st, uint64_t hops) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
         if (rt_done_min(st) >= hops) return CRLOT_OK;
-        if ((spin & 1023) == 1023) {
-            if (!rt_running(st)) {
+        // stop == 2: a workgroup's idle timer expired and the grid is leaving; wait
+        // for it at once rather than at the next periodic liveness check
+        const bool leaving = __atomic_load_n(&st->ctl->stop, __ATOMIC_ACQUIRE) == 2;
+        if (leaving || (spin & 1023) == 1023) {
+            if (leaving || !rt_running(st)) {
                 if (st->launched) {  // gone: surface a fault, else relaunch
                     hipError_t e = hipEventSynchronize(st->ev);
                     if (e != hipSuccess) return hip_fail(e, "resident stream kernel");
@@ -1676,7 +1679,7 @@ int crlot_stream_rt_submit(crlot_stream_rt* st, int64_t* hop_index) {
     __atomic_store_n(&st->ctl->seq, st->q + 1, __ATOMIC_RELEASE);
     if (hop_index) *hop_index = int64_t(st->q);
     st->q += 1;
-    if (!rt_running(st)) {
+    if (__atomic_load_n(&st->ctl->stop, __ATOMIC_ACQUIRE) == 2 || !rt_running(st)) {  // gone or leaving (idle)
         if (st->launched) {
             hipError_t e = hipEventSynchronize(st->ev);
             if (e != hipSuccess) return hip_fail(e, "resident stream kernel");
