@@ -207,8 +207,11 @@ int pair_waves_per_cu();
 hipError_t launch_pair(int sh, const FusedArgs& a, int64_t waves, hipStream_t stream);
 // K_pair4k's paired-only hot walker (pair_hot.hip), H = 256 * sh; writes pflags per workgroup.
 hipError_t launch_pair4k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
+// ... at three workgroups per CU (one exchange buffer, windows from L2; no gain)
+hipError_t launch_pair4k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
 // ... and K_pair2k's (H = 128 * sh)
 hipError_t launch_pair2k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
+hipError_t launch_pair2k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
 // ... and K_pair512's (H = 64 * sh, sh = 2 or 4; w waves per workgroup, flags per wave)
 hipError_t launch_pair512_hot(int sh, const FusedArgs& a, int64_t waves, int w, hipStream_t stream);
 

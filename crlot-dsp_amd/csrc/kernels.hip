@@ -1847,6 +1847,15 @@ static bool pair4k_hot_disabled() {
     }();
     return v;
 }
+// K_pair4k's / K_pair2k's hot walker: CRLOT_PAIR4K_HOT=3 the three-waves-per-SIMD
+// one (k_pair_wg_hot3), =2 the two-wave one (A/Bs; bit-identical)
+static bool pair4k_hot3() {
+    static const bool v = [] {
+        const char* e = std::getenv("CRLOT_PAIR4K_HOT");
+        return e && e[0] == '3';
+    }();
+    return v;
+}
 
 // K_pair512: N = 512, H = 64 SH, 4 independent waves per workgroup.
 template <int SH>
@@ -1907,7 +1916,9 @@ void chunk_override(int64_t F, FusedArgs& a) {
 }
 int fused_resident_waves();
 hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_streams, hipStream_t stream) {
-    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 4, a.n_chunks, a.M);
+    const bool hot = g.h == 512 && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot;
+    const bool hot3 = hot && pair4k_hot3();  // six two-wave workgroups per CU, else four
+    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * (hot3 ? 6 : 4), a.n_chunks, a.M);
     chunk_override(F, a);
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
@@ -1918,8 +1929,8 @@ hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_stream
     if (!a.t.pflags || a.t.pflags_len < grid) return hipErrorInvalidValue;
     // the paired-only hot walker where it holds its registers (H = 512), then the
     // two-regime walker over the chunks it flagged; otherwise the latter alone
-    if (g.h == 512 && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
-        hipError_t e = launch_pair2k_hot(4, a, grid, stream);
+    if (hot) {
+        hipError_t e = hot3 ? launch_pair2k_hot3(4, a, grid, stream) : launch_pair2k_hot(4, a, grid, stream);
         if (e != hipSuccess) return e;
     } else {
         a.fix_all = 1;
@@ -2266,16 +2277,21 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
     a.inv_n = g.inv_n;
     a.gain = g.gain;
     if (g.n == 4096 && t.ptw4 && t.pden4 && t.wsn && t.rden && (g.h == 512 || g.h == 1024 || g.h == 2048)) {
-        // K_pair4k: whole resident rounds of workgroups (two per CU)
-        choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * 2, a.n_chunks, a.M);
+        // K_pair4k: whole resident rounds of workgroups (three per CU with the
+        // three-workgroup hot walker, else two)
+        const bool hot = (!t.gain || g.h == 1024) && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot;
+        const bool hot3 = hot && !t.gain && pair4k_hot3();
+        choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * (hot3 ? 3 : 2), a.n_chunks,
+                             a.M);
         chunk_override(F, a);
         const int64_t grid4 = int64_t(n_streams) * a.n_chunks;
         if (!t.pflags || t.pflags_len < grid4) return hipErrorInvalidValue;
         // the paired-only hot walker, then the two-regime walker over the chunks it
         // flagged; reflect/edge padding, or a spectral gain at H != 1024: the
         // two-regime walker alone
-        if ((!t.gain || g.h == 1024) && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot) {
-            hipError_t e = launch_pair4k_hot(g.h / 256, a, grid4, stream);
+        if (hot) {
+            hipError_t e = hot3 ? launch_pair4k_hot3(g.h / 256, a, grid4, stream)
+                                : launch_pair4k_hot(g.h / 256, a, grid4, stream);
             if (e != hipSuccess) return e;
         } else {
             a.fix_all = 1;
