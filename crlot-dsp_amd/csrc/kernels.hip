@@ -1916,7 +1916,7 @@ void chunk_override(int64_t F, FusedArgs& a) {
 }
 int fused_resident_waves();
 hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_streams, hipStream_t stream) {
-    const bool hot = g.h == 512 && !a.t.gain && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot;
+    const bool hot = g.h == 512 && !a.t.gain && g.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot;
     const bool hot3 = hot && pair4k_hot3();  // six two-wave workgroups per CU, else four
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * (hot3 ? 6 : 4), a.n_chunks, a.M);
     chunk_override(F, a);
@@ -2280,7 +2280,7 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
         // K_pair4k: whole resident rounds of workgroups (three per CU with the
         // three-workgroup hot walker, else two)
         const bool hot = (!t.gain || g.h == 1024) && a.pad_mode == 0 && !pair4k_hot_disabled() && a.t.hot;
-        const bool hot3 = hot && !t.gain && pair4k_hot3();
+        const bool hot3 = hot && !t.gain && g.h == 1024 && pair4k_hot3();
         choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * (hot3 ? 3 : 2), a.n_chunks,
                              a.M);
         chunk_override(F, a);

@@ -491,21 +491,32 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(3, 3))) vo
         return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, z + m * (4 * L), 0));
     };
 
+    // vmcnt retires in order and counts stores: the synthesis window is loaded
+    // before the step's hop prefetch, and the next pair's analysis window before
+    // this pair's output stores, so neither wait drains a store or a prefetch
+    float wan[E];
+    {
+        int z = 0;
+        asm volatile("" : "+s"(z));
+#pragma unroll
+        for (int m = 0; m < E; ++m) wan[m] = win(rwa, z, m);
+    }
     auto step = [&](auto phc, int k) {
         constexpr int PH = decltype(phc)::value;
         constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
         int z = 0;
         asm volatile("" : "+s"(z));
+        float wsr[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) wsr[m] = win(rws, z, m);
         load_hop_wg0<L, SH>(xr[(S0 + NB + 1) % R], rx, t, (k + NB + 1) * H - a.pad);
         load_hop_wg0<L, SH>(xr[(S0 + NB + 2) % R], rx, t, (k + NB + 2) * H - a.pad);
         const bool partner = k + 1 < a.F;  // as the two-regime walker
         dev::pc v[E];
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const float w = win(rwa, z, m);
-            v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * w,
-                              partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * w : 0.0f);
-        }
+        for (int m = 0; m < E; ++m)
+            v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wan[m],
+                              partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wan[m] : 0.0f);
         // forward (G::fwd with one buffer)
         dev::pdft16<false>(v);
         dev::pc_tw_run<false>(v, idx, [&](int i) { return w1[i]; });
@@ -543,10 +554,9 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(3, 3))) vo
             bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= G::MIN_EXP;
         }
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const float w = win(rws, z, m);
-            v[m] = v[m] * dev::pc{w, w};
-        }
+        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{wsr[m], wsr[m]};
+#pragma unroll
+        for (int m = 0; m < E; ++m) wan[m] = win(rwa, z, m);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + m / SH) % NB][m % SH];
@@ -602,12 +612,8 @@ hipError_t launch_wg_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t 
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(G::L), lds, stream, a);
         return hipGetLastError();
     };
-    switch (sh) {
-        case 2: return go(k_pair_wg_hot3<G, 2, 8>);
-        case 4: return go(k_pair_wg_hot3<G, 4, 4>);
-        case 8: return go(k_pair_wg_hot3<G, 8, 2>);
-        default: return hipErrorInvalidValue;
-    }
+    // H = 4 L only: the other hops' rotation slots spill 60-100 VGPRs at 168
+    return sh == 4 ? go(k_pair_wg_hot3<G, 4, 4>) : hipErrorInvalidValue;
 }
 hipError_t launch_pair4k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
     return launch_wg_hot3<Geo4k>(sh, a, grid, stream);
