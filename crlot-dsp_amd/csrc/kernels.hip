@@ -1847,14 +1847,19 @@ static bool pair4k_hot_disabled() {
     }();
     return v;
 }
-// K_pair4k's / K_pair2k's hot walker: CRLOT_PAIR4K_HOT=3 the three-waves-per-SIMD
-// one (k_pair_wg_hot3), =2 the two-wave one (A/Bs; bit-identical)
+// K_pair4k's / K_pair2k's hot walker at three waves per SIMD (k_pair_wg_hot3,
+// measured slower: DESIGN.md section 5) only in -DCRLOT_PAIR_WG_HOT3_EXPERIMENT
+// builds with CRLOT_PAIR4K_HOT=3 (A/Bs; bit-identical)
 static bool pair4k_hot3() {
+#ifdef CRLOT_PAIR_WG_HOT3_EXPERIMENT
     static const bool v = [] {
         const char* e = std::getenv("CRLOT_PAIR4K_HOT");
         return e && e[0] == '3';
     }();
     return v;
+#else
+    return false;
+#endif
 }
 
 // K_pair512: N = 512, H = 64 SH, 4 independent waves per workgroup.

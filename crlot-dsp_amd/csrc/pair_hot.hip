@@ -79,7 +79,7 @@ __device__ __forceinline__ void tw_all(dev::pc (&v)[16], const TW& w) {
 struct Geo4k {
     static constexpr int N = 4096, L = 256, KS = 304, ROWS_PER_WAVE = 4, SIDE = 16, MIN_EXP = -87;  // 1e-30 N = 2^-87.66
     using Tw = dev::Pair4kTw;
-    using X = XchgRows<16>;
+    using X = XchgRows<SIDE>;
     static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
         dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
     }
@@ -126,7 +126,7 @@ struct Geo4k {
 struct Geo2k {
     static constexpr int N = 2048, L = 128, KS = 152, ROWS_PER_WAVE = 8, SIDE = 8, MIN_EXP = -88;  // 1e-30 N = 2^-88.66
     using Tw = dev::Pair2kTw;
-    using X = XchgRows<8>;
+    using X = XchgRows<SIDE>;
     static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
         dev::pair2k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
     }
@@ -408,6 +408,10 @@ hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t s
 //   * both windows read per pair from the tables (L2-resident) instead of 32
 //     registers;
 // so <= 168 VGPRs and 40.8 KB (4k) / 20.4 KB (2k) of LDS.
+// Measured slower (4096/1024 196k vs 228k Msamples/s, 2048/512
+// 196k vs 234k), so it is built only with -DCRLOT_PAIR_WG_HOT3_EXPERIMENT
+// (then CRLOT_PAIR4K_HOT=3 selects it); the release library has stubs.
+#ifdef CRLOT_PAIR_WG_HOT3_EXPERIMENT
 template <typename G, int SH, int NB>
 __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_pair_wg_hot3(const FusedArgs a) {
     constexpr int E = 16, L = G::L, H = L * SH, KS = G::KS, SIDE = G::SIDE;
@@ -621,6 +625,10 @@ hipError_t launch_pair4k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStrea
 hipError_t launch_pair2k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
     return launch_wg_hot3<Geo2k>(sh, a, grid, stream);
 }
+#else
+hipError_t launch_pair4k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { return hipErrorInvalidValue; }
+hipError_t launch_pair2k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { return hipErrorInvalidValue; }
+#endif  // CRLOT_PAIR_WG_HOT3_EXPERIMENT
 
 // ---- N = 512: one wave per chunk (W per workgroup, independent), lane l holds
 // samples l + 64 m (m < 8); flags per wave.
