@@ -158,10 +158,23 @@ def load_pmc_traffic(workload_key: str):
     return (None if stale else best.get("hbm_bytes_per_launch")), meta
 
 
-def timed_phase(plan, x, y, steps: int, warmup: int, D, dev, torch):
-    """Warm-up, then `steps` round trips bracketed by barrier + synchronize;
-    returns (wall seconds max over ranks, mean kernel ms on the launch stream)."""
+RAMP_S = 0.25  # untimed clock ramp before the warm-up steps (reported as clock_ramp_steps)
+
+
+def timed_phase(plan, x, y, steps: int, warmup: int, D, dev, torch, ramp: dict = None):
+    """Clock ramp (untimed round trips for RAMP_S seconds: an idle MI355X takes
+    ~100-200 ms to reach its loaded clock, longer than a few warm-up steps), then
+    `warmup` untimed steps, then `steps` round trips bracketed by barrier +
+    synchronize; returns (wall seconds max over ranks, mean kernel ms on the
+    launch stream)."""
     stream = torch.cuda.current_stream(dev)
+    n_ramp, t_end = 0, time.perf_counter() + RAMP_S
+    while time.perf_counter() < t_end:
+        plan.roundtrip(x, y)
+        torch.cuda.synchronize(dev)
+        n_ramp += 1
+    if ramp is not None:
+        ramp["clock_ramp_steps"] = n_ramp
     for _ in range(warmup):
         plan.roundtrip(x, y)
     torch.cuda.synchronize(dev)
@@ -571,7 +584,8 @@ def main():
     # ---- weak phase (headline): S streams per rank
     x = synth_device(torch, S, T, dev, 0xC0FFEE + rank)
     y = torch.empty((S, L), dtype=torch.float32, device=dev)
-    elapsed_max, kern_ms = timed_phase(plan, x, y, args.steps, args.warmup, D, dev, torch)
+    ramp = {}
+    elapsed_max, kern_ms = timed_phase(plan, x, y, args.steps, args.warmup, D, dev, torch, ramp)
     del x, y
 
     samples_step_rank = S * T
@@ -618,6 +632,8 @@ def main():
             "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "clock_ramp": {"seconds": RAMP_S, "steps": ramp.get("clock_ramp_steps"),
+                           "note": "untimed round trips before the warm-up steps while the GPU clock ramps"},
             "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
