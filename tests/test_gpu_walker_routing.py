@@ -1,0 +1,51 @@
+"""The paired-only hot walkers actually run where DESIGN.md section 3 says they do.
+
+The hot walkers and the two-regime walkers give identical bits (the parity tests
+prove that), so a dispatch predicate that silently stops choosing the hot walker
+is invisible to every parity test: it only costs throughput.  This happened once
+(round 3: K_pair2k's predicate read an unset pad mode and 2048/512 fell from
+234k to 195k Msamples/s).  Here each shape is timed with the default routing and
+with pairing mode 2 (`crlot_plan_set_frame_pairing(plan, 2)`: the two-regime
+walkers alone) on the same input in interleaved groups; the default must be
+clearly faster.  Measured gaps on MI355X: 1024/256 281k vs 210k, 2048/512 234k
+vs 195k, 4096/1024 228k vs 192k: the 7 % bar leaves room
+for box-to-box noise.  The outputs of the two routes are also compared bit for bit.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,h", [(1024, 256), (2048, 512), (4096, 1024)])
+def test_hot_walker_is_dispatched(pkg, torch_cuda, n, h):
+    torch = torch_cuda
+    S, T = 512, 240_000
+    g = torch.Generator(device="cuda").manual_seed(n + h)
+    x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
+    hot = pkg.Plan(frame_size=n, hop_size=h)
+    two = pkg.Plan(frame_size=n, hop_size=h)
+    two.set_frame_pairing(2)
+    y_hot = hot.roundtrip(x)
+    y_two = two.roundtrip(x)
+    torch.cuda.synchronize()
+    assert np.array_equal(y_hot.cpu().numpy().view(np.uint32), y_two.cpu().numpy().view(np.uint32))
+
+    def group(plan, y, reps=8):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            plan.roundtrip(x, y)
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    for _ in range(3):  # clock ramp
+        group(hot, y_hot), group(two, y_two)
+    t_hot, t_two = [], []
+    for _ in range(5):
+        t_hot.append(group(hot, y_hot))
+        t_two.append(group(two, y_two))
+    m_hot, m_two = float(np.median(t_hot)), float(np.median(t_two))
+    print(f"{n}/{h}: hot {m_hot:.3f} ms, two-regime {m_two:.3f} ms ({m_two / m_hot:.3f}x)")
+    assert m_hot * 1.07 < m_two, (m_hot, m_two)
