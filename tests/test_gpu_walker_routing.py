@@ -7,9 +7,9 @@ is invisible to every parity test: it only costs throughput.  This happened once
 234k to 195k Msamples/s).  Here each shape is timed with the default routing and
 with pairing mode 2 (`crlot_plan_set_frame_pairing(plan, 2)`: the two-regime
 walkers alone) on the same input in interleaved groups; the default must be
-clearly faster.  Measured gaps on MI355X: 1024/256 281k vs 210k, 2048/512 234k
-vs 195k, 4096/1024 228k vs 192k: the 7 % bar leaves room
-for box-to-box noise.  The outputs of the two routes are also compared bit for bit.
+clearly faster.  Measured on MI355X at this size: 1.11x (1024/256), 1.22x
+(2048/512), 1.20x (4096/1024); a walker that is not dispatched gives 1.00x, so
+the 5 % bar separates the two with room for noise.  The outputs of the two routes are also compared bit for bit.
 """
 import numpy as np
 import pytest
@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("n,h", [(1024, 256), (2048, 512), (4096, 1024)])
 def test_hot_walker_is_dispatched(pkg, torch_cuda, n, h):
     torch = torch_cuda
-    S, T = 512, 240_000
+    S, T = 1024, 240_000
     g = torch.Generator(device="cuda").manual_seed(n + h)
     x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
     hot = pkg.Plan(frame_size=n, hop_size=h)
@@ -48,4 +48,4 @@ def test_hot_walker_is_dispatched(pkg, torch_cuda, n, h):
         t_two.append(group(two, y_two))
     m_hot, m_two = float(np.median(t_hot)), float(np.median(t_two))
     print(f"{n}/{h}: hot {m_hot:.3f} ms, two-regime {m_two:.3f} ms ({m_two / m_hot:.3f}x)")
-    assert m_hot * 1.07 < m_two, (m_hot, m_two)
+    assert m_hot * 1.05 < m_two, (m_hot, m_two)
