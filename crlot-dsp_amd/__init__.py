@@ -55,6 +55,17 @@ class PlanDesc(C.Structure):
     ]
 
 
+class LaunchInfo(C.Structure):
+    """crlot_launch_info (include/crlot_dsp.h): what a plan's last call on a stream launched."""
+    _fields_ = [
+        ("n_kernels", C.c_int32),
+        ("kernels", C.c_int32 * 8),
+        ("grid", C.c_int64 * 8),
+        ("n_chunks", C.c_int32),
+        ("reserved", C.c_int32),
+    ]
+
+
 class OlaConfigC(C.Structure):
     """crlot_ola_config (include/crlot_dsp.h) = dsp::OLAConfig + device."""
     _fields_ = [
@@ -104,6 +115,9 @@ def lib():
         "crlot_plan_upload_tables_async": ([vp, vp, vp, vp], C.c_int),
         "crlot_plan_set_spectral_gain_async": ([vp, vp, vp], C.c_int),
         "crlot_plan_set_frame_pairing": ([vp, i32], C.c_int),
+        "crlot_plan_set_chunks": ([vp, i32], C.c_int),
+        "crlot_plan_last_launch": ([vp, vp, C.POINTER(LaunchInfo)], C.c_int),
+        "crlot_kernel_name": ([i32], C.c_char_p),
         "crlot_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
         "crlot_frame_count": ([vp, i64], i64),
         "crlot_output_length": ([vp, i64], i64),
@@ -201,6 +215,11 @@ def lib():
         fn.restype = rest
     _lib = L
     return L
+
+
+def kernel_name(kernel_id: int) -> str:
+    """Name of a CRLOT_K_* launch-record id (crlot_kernel_name)."""
+    return lib().crlot_kernel_name(int(kernel_id)).decode()
 
 
 def _check(rc: int, what: str = "") -> int:
@@ -360,6 +379,25 @@ class Plan:
         False selects the per-frame kernels, bit-identical to stages + ola_gather;
         2 pairs through the two-regime walkers only (hot walkers off, same bits)."""
         _check(lib().crlot_plan_set_frame_pairing(self._h, 2 if enable == 2 else int(bool(enable))))
+
+    def set_chunks(self, chunks_per_stream: int = 0):
+        """Force the chunked walkers to split every stream into this many chunks
+        (min(n, F); 0 restores the library's choice).  Output bits never depend
+        on it; parity tests use it to move the chunk seams (crlot_plan_set_chunks)."""
+        _check(lib().crlot_plan_set_chunks(self._h, int(chunks_per_stream)), "crlot_plan_set_chunks")
+
+    def last_launch(self, stream: int | None = None) -> dict:
+        """What the last call on `stream` (default: the current torch stream)
+        launched: {"kernels": [names in launch order], "grid": [...],
+        "n_chunks": chunks per stream, "n_kernels": count} (crlot_plan_last_launch)."""
+        s = self._cur_stream() if stream is None else stream
+        info = LaunchInfo()
+        _check(lib().crlot_plan_last_launch(self._h, s, C.byref(info)), "crlot_plan_last_launch")
+        k = min(info.n_kernels, 8)
+        return {"n_kernels": info.n_kernels,
+                "kernels": [kernel_name(info.kernels[i]) for i in range(k)],
+                "grid": [int(info.grid[i]) for i in range(k)],
+                "n_chunks": info.n_chunks}
 
     def set_spectral_gain(self, gain=None):
         g = None if gain is None else np.ascontiguousarray(gain, np.float32)

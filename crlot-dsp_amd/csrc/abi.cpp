@@ -13,6 +13,8 @@
 #include <mutex>
 
 #include <algorithm>
+#include <atomic>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -68,6 +70,10 @@ struct crlot_plan {
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
     bool pairing = true;      // crlot_plan_set_frame_pairing
     bool hot = true;          // ... 2: pairing with the two-regime walkers only
+    std::atomic<int> chunks{0};  // crlot_plan_set_chunks (0: the library's chunking)
+    // crlot_plan_last_launch: what the last call on each stream launched
+    std::mutex rec_mu;
+    std::map<hipStream_t, crlot::LaunchRecord> last;
     bool fast_ok = false;     // both exact rewrites valid for the current tables
     bool den_mk_ok = false;   // every den in [2^-40, 2^40]: Markstein division exact
     bool generic = false;     // N outside the power-of-two kernels: fft_any.h path
@@ -118,6 +124,28 @@ struct DeviceGuard {
     }
 };
 
+// Installs the plan's launch knobs on this thread for one ABI call and stores
+// what the call launched as the plan's record for `s` (crlot_plan_last_launch).
+struct LaunchScope {
+    crlot_plan* p;
+    hipStream_t s;
+    crlot::LaunchCtl ctl;
+    crlot::LaunchCtl* prev;
+    LaunchScope(crlot_plan* plan, void* stream) : p(plan), s(static_cast<hipStream_t>(stream)) {
+        ctl.chunks = p->chunks.load(std::memory_order_relaxed);
+        prev = crlot::launch_ctl();
+        crlot::set_launch_ctl(&ctl);
+    }
+    ~LaunchScope() {
+        crlot::set_launch_ctl(prev);
+        std::lock_guard<std::mutex> lk(p->rec_mu);
+        if (p->last.size() >= 64 && !p->last.count(s)) p->last.erase(p->last.begin());
+        p->last[s] = ctl.rec;
+    }
+    LaunchScope(const LaunchScope&) = delete;
+    LaunchScope& operator=(const LaunchScope&) = delete;
+};
+
 crlot::DevTables tables(const crlot_plan* p, const crlot::Scratch* sc = nullptr) {
     crlot::DevTables t;
     t.wa = p->d_wa;
@@ -127,7 +155,7 @@ crlot::DevTables tables(const crlot_plan* p, const crlot::Scratch* sc = nullptr)
     t.st = p->d_st;
     t.gain = p->has_gain ? p->d_gain : nullptr;
     static const bool exact_div = [] {
-        const char* e = std::getenv("CRLOT_EXACT_DIV");
+        const char* e = crlot::ab_env("CRLOT_EXACT_DIV");
         return e && e[0] == '1';
     }();
     if (p->fast_ok && !exact_div) {
@@ -599,6 +627,31 @@ int crlot_plan_set_frame_pairing(crlot_plan* p, int32_t enable) {
     return CRLOT_OK;
 }
 
+int crlot_plan_set_chunks(crlot_plan* p, int32_t chunks) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (chunks < 0) return fail(CRLOT_EINVAL, "chunks per stream must be >= 0");
+    p->chunks.store(chunks, std::memory_order_relaxed);
+    return CRLOT_OK;
+}
+
+int crlot_plan_last_launch(const crlot_plan* p, void* stream, crlot_launch_info* out) {
+    if (!p || !out) return fail(CRLOT_EINVAL, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    crlot_plan* q = const_cast<crlot_plan*>(p);
+    std::lock_guard<std::mutex> lk(q->rec_mu);
+    const auto it = q->last.find(static_cast<hipStream_t>(stream));
+    if (it == q->last.end()) return CRLOT_OK;
+    const crlot::LaunchRecord& r = it->second;
+    static_assert(crlot::kLaunchRecordMax == 8, "crlot_launch_info holds 8 launches");
+    out->n_kernels = r.n;
+    for (int i = 0; i < std::min(r.n, crlot::kLaunchRecordMax); ++i) {
+        out->kernels[i] = r.id[i];
+        out->grid[i] = r.grid[i];
+    }
+    out->n_chunks = r.n_chunks;
+    return CRLOT_OK;
+}
+
 int crlot_plan_info(const crlot_plan* p, int32_t* n, int32_t* h, int32_t* ring) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (n) *n = p->geo.n;
@@ -768,6 +821,7 @@ int crlot_roundtrip(crlot_plan* p, const float* d_x, float* d_y, int32_t n_strea
                     int64_t ld_x, int64_t ld_y, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "negative size");
+    LaunchScope ls(p, stream);
     const int64_t F = frames_for(p, T);
     // nothing to emit (n_streams == 0, T == 0, or DROP with T < N: the Framer never yields)
     if (n_streams == 0 || F == 0) return CRLOT_OK;
@@ -785,6 +839,7 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
                                 int32_t channels, int64_t T, int64_t ld_x, int64_t ld_y, void* stream) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (n_groups < 0 || T < 0 || channels <= 0 || channels > 64) return fail(CRLOT_EINVAL, "bad size");
+    LaunchScope ls(p, stream);
     const int64_t F = frames_for(p, T);
     if (n_groups == 0 || F == 0) return CRLOT_OK;
     if ((!d_x && T > 0) || !d_y) return fail(CRLOT_EINVAL, "null buffer");
@@ -805,7 +860,7 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
     // / 113k Msamples/s at C = 2 / 4 / 5 / 6 / 8, three passes 153k / 157k / 153k /
     // 150k / 144k)
     static const bool three_pass = [] {
-        const char* v = std::getenv("CRLOT_ILV_3PASS");  // A/B: always deinterleave -> planes -> interleave
+        const char* v = crlot::ab_env("CRLOT_ILV_3PASS");  // A/B: always deinterleave -> planes -> interleave
         return v && v[0] == '1';
     }();
     if (!three_pass && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0 && aligned4(d_x) &&
@@ -836,6 +891,7 @@ int crlot_roundtrip_stages(crlot_plan* p, const float* d_x, int32_t n_streams, i
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (n_streams < 0 || T < 0 || ld_x < T) return fail(CRLOT_EINVAL, "bad size");
     if ((!d_x && T > 0) || !d_frames) return fail(CRLOT_EINVAL, "null buffer");
+    LaunchScope ls(p, stream);
     const int64_t F = frames_for(p, T);
     if (F == 0 || n_streams == 0) return CRLOT_OK;
     DeviceGuard g(p->device);
@@ -859,6 +915,7 @@ int crlot_ola_gather(crlot_plan* p, const float* d_frames, float* d_y, int32_t n
     if (ld_frames < p->geo.n || ld_y < out_len)
         return fail(CRLOT_EINVAL, "leading dimension too small");
     DeviceGuard g(p->device);
+    LaunchScope ls(p, stream);
     hipError_t e = crlot::launch_ola_gather(p->geo, tables(p), d_frames, ld_frames, d_y,
                                             n_streams, F, ld_y, out_len,
                                             static_cast<hipStream_t>(stream));
@@ -874,6 +931,7 @@ int crlot_rfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t b
     if (batch == 0) return CRLOT_OK;
     if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
     DeviceGuard g(p->device);
+    LaunchScope ls(p, stream);
     hipError_t e = p->generic
                        ? crlot::launch_fft_any(0, p->geo.n / 2, p->geo.inv_n, tables(p), p->d_twany,
                                                d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out,
@@ -892,6 +950,7 @@ int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t 
     if (batch == 0) return CRLOT_OK;
     if (!d_in || !d_out) return fail(CRLOT_EINVAL, "null buffer");
     DeviceGuard g(p->device);
+    LaunchScope ls(p, stream);
     hipError_t e = p->generic
                        ? crlot::launch_fft_any(1, p->geo.n / 2, p->geo.inv_n, tables(p), p->d_twany,
                                                d_in, d_out, batch, ld_in, inc_in, ld_out, inc_out,

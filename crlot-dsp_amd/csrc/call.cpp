@@ -13,6 +13,7 @@
 // host-visible, the input side falls back to pinned host memory (the kernel's
 // system-scope loads read either).
 #include "call.h"
+#include "ab.h"
 
 #include <immintrin.h>
 
@@ -115,7 +116,7 @@ int CallServer::alloc(size_t in_cap, size_t out_cap, size_t spec_cap) {
     hipError_t err;
     const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
     static const bool host_inputs = [] {
-        const char* v = std::getenv("CRLOT_CALL_HOST_INPUTS");  // A/B: inputs in pinned host memory
+        const char* v = ab_env("CRLOT_CALL_HOST_INPUTS");  // A/B: inputs in pinned host memory
         return v && v[0] == '1';
     }();
     void* d = nullptr;

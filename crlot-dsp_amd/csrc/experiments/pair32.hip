@@ -14,7 +14,7 @@
 #include <cmath>
 #include <cstdlib>
 
-#include "fft_pair32.h"
+#include "experiments/fft_pair32.h"
 #include "fused_common.h"
 
 namespace crlot {
@@ -207,7 +207,7 @@ void k_stft_ola_pair32(const FusedArgs a) {
 bool pair32_enabled() {
 #ifdef CRLOT_PAIR32_EXPERIMENT
     static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PAIR32");
+        const char* e = ab_env("CRLOT_PAIR32");
         return e && e[0] == '1';
     }();
     return v;
@@ -223,6 +223,7 @@ hipError_t launch_pair32(const FusedArgs& a, hipStream_t stream) {
     const size_t lds = P32Lds::bytes;
     hipError_t e = set_lds(k_stft_ola_pair32, lds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_EXPERIMENT, (waves + kP32Waves - 1) / kP32Waves);
     hipLaunchKernelGGL(k_stft_ola_pair32, dim3(unsigned((waves + kP32Waves - 1) / kP32Waves)), dim3(64 * kP32Waves),
                        lds, stream, a);
     return hipGetLastError();

@@ -6,6 +6,9 @@
 #include <cstdint>
 #include <vector>
 
+#include "ab.h"
+#include "crlot_dsp.h"
+
 namespace crlot {
 
 // Device-resident per-plan tables.
@@ -47,6 +50,30 @@ struct DevTables {
     // chunk (crlot_plan_set_frame_pairing(plan, 2): parity diagnostics)
     int hot = 1;
 };
+
+// Launch knobs and the record of what one ABI call launched (crlot_plan_set_chunks,
+// crlot_plan_last_launch).  The ABI installs a LaunchCtl on the calling thread for
+// the duration of a call (LaunchScope in abi.cpp); the launch functions read the
+// knobs from it and append every kernel they launch.  Kernel ids: CRLOT_K_* in
+// include/crlot_dsp.h.
+constexpr int kLaunchRecordMax = 8;
+struct LaunchRecord {
+    int32_t n = 0;                      // kernels launched (first kLaunchRecordMax kept)
+    int32_t id[kLaunchRecordMax] = {};  // CRLOT_K_* in launch order
+    int64_t grid[kLaunchRecordMax] = {};  // workgroups of each launch
+    int32_t n_chunks = 0;               // chunks per stream of the walk (0: not a chunked walk)
+};
+struct LaunchCtl {
+    int chunks = 0;  // chunks per stream forced on the chunked walkers (0: the chooser's)
+    LaunchRecord rec;
+};
+LaunchCtl* launch_ctl();                  // the calling thread's, or nullptr
+void set_launch_ctl(LaunchCtl* c);
+void note_launch(int32_t id, int64_t grid);  // no-op without a LaunchCtl
+void note_chunks(int64_t n_chunks);
+// chunks per stream a walker over F frames uses given its chooser's dflt: the
+// plan's knob clamped to [1, max_chunks] (max_chunks <= F), else dflt
+int64_t chunks_or(int64_t dflt, int64_t max_chunks);
 
 // Tables of the frame-pair transform (fft_pair.h) for N = 1024, float pairs.
 std::vector<float> build_pair_twiddles();

@@ -1826,6 +1826,7 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
         const size_t lds2 = Lds<E>::bytes + sizeof(cf) * kWaves * 64 * E;
         hipError_t e2 = set_lds(k2, lds2);
         if (e2 != hipSuccess) return e2;
+        note_launch(CRLOT_K_FUSED2, grid);
         hipLaunchKernelGGL(k2, dim3(unsigned(grid)), dim3(kBlock), lds2, stream, a);
         return hipGetLastError();
     }
@@ -1835,6 +1836,7 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     const size_t lds = Lds<E>::bytes;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_FUSED, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
     return hipGetLastError();
 }
@@ -1842,7 +1844,7 @@ hipError_t fused_es(const FusedArgs& a, int64_t grid, hipStream_t stream) {
 // CRLOT_PAIR4K_NOHOT=1 (A/B, N = 4096, 2048 and 512): the two-regime walker alone over every chunk.
 static bool pair4k_hot_disabled() {
     static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PAIR4K_NOHOT");
+        const char* e = ab_env("CRLOT_PAIR4K_NOHOT");
         return e && e[0] == '1';
     }();
     return v;
@@ -1853,7 +1855,7 @@ static bool pair4k_hot_disabled() {
 static bool pair4k_hot3() {
 #ifdef CRLOT_PAIR_WG_HOT3_EXPERIMENT
     static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PAIR4K_HOT");
+        const char* e = ab_env("CRLOT_PAIR4K_HOT");
         return e && e[0] == '3';
     }();
     return v;
@@ -1880,6 +1882,7 @@ hipError_t pair512_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     } else {
         b.fix_all = 1;
     }
+    note_launch(CRLOT_K_PAIR512, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * kP512Waves), lds, stream, b);
     return hipGetLastError();
 }
@@ -1899,23 +1902,16 @@ hipError_t pair2k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream) {
     auto k = a.t.gain ? k_stft_ola_pair2k<SH, NB, true> : k_stft_ola_pair2k<SH, NB, false>;
     hipError_t e = set_lds(k, kPair2kLds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_PAIR2K, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(128), kPair2kLds, stream, a);
     return hipGetLastError();
 }
 void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int& n_chunks, int& m);
-// CRLOT_CHUNKS (tuning override: chunks per stream), read once per process so
-// the launch path does no environment lookups.
-int chunks_env() {
-    static const int v = [] {
-        const char* e = std::getenv("CRLOT_CHUNKS");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
+// The plan's chunk knob (crlot_plan_set_chunks, via the call's LaunchCtl)
+// replaces the chooser's chunking: min(knob, F) chunks per stream.
 void chunk_override(int64_t F, FusedArgs& a) {
-    const int c = chunks_env();
-    if (c <= 0) return;
-    const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F, c));
+    const int64_t n = chunks_or(0, F);
+    if (n <= 0) return;
     a.M = int((F + n - 1) / n);
     a.n_chunks = int((F + a.M - 1) / a.M);
 }
@@ -1925,6 +1921,7 @@ hipError_t launch_pair2k(const Geometry& g, FusedArgs a, int64_t F, int n_stream
     const bool hot3 = hot && pair4k_hot3();  // six two-wave workgroups per CU, else four
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * (hot3 ? 6 : 4), a.n_chunks, a.M);
     chunk_override(F, a);
+    note_chunks(a.n_chunks);
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
     a.pad_mode = g.pad_mode;
@@ -2026,7 +2023,7 @@ void choose_chunks_rounds(int64_t F, int n_streams, int halo, int resident, int&
 // frames per workgroup walk (halo NB-1 frames recomputed); CRLOT_WG_CHUNK overrides
 int wg_chunk_target() {
     static const int v = [] {
-        const char* e = std::getenv("CRLOT_WG_CHUNK");
+        const char* e = ab_env("CRLOT_WG_CHUNK");
         const int x = e ? std::atoi(e) : 0;
         return x > 0 ? x : 128;
     }();
@@ -2154,6 +2151,7 @@ hipError_t launch_fused(const Geometry& g, const DevTables& t, const float* x, f
         choose_chunks(F, n_streams, g.n / g.h, resident, a.n_chunks, a.M);
     chunk_override(F, a);
 #endif
+    note_chunks(a.n_chunks);
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
     a.pad_mode = g.pad_mode;
@@ -2202,6 +2200,7 @@ hipError_t launch_pair_interleaved(const Geometry& g, const DevTables& t, const 
     choose_chunks_rounds(F, a.n_streams, g.n / g.h + 1, fused_resident_waves() * pair_waves_per_cu() / 16,
                          a.n_chunks, a.M);
     chunk_override(F, a);
+    note_chunks(a.n_chunks);
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
     a.pad_mode = g.pad_mode;
@@ -2217,6 +2216,7 @@ static hipError_t pair4k_sh(const FusedArgs& a, int64_t grid, hipStream_t stream
     auto k = a.t.gain ? k_stft_ola_pair4k<SH, NB, true> : k_stft_ola_pair4k<SH, NB, false>;
     hipError_t e = set_lds(k, kPair4kLds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_PAIR4K, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(256), kPair4kLds, stream, a);
     return hipGetLastError();
 }
@@ -2229,6 +2229,7 @@ static hipError_t fused_wg_ls(const FusedArgs& a, int64_t grid, hipStream_t stre
     const size_t lds = sizeof(cf) * 3 * 8 * L;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_FUSED_WG, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(L), lds, stream, a);
     return hipGetLastError();
 }
@@ -2248,7 +2249,7 @@ static hipError_t fused_wg_l(int s, const FusedArgs& a, int64_t grid, hipStream_
 // per-wave E = 16 kernel, which is the default there).
 bool fused_wg_supported(int n, int h) {
     static const bool wg2048 = [] {
-        const char* e = std::getenv("CRLOT_WG_2048");
+        const char* e = ab_env("CRLOT_WG_2048");
         return e && e[0] == '1';
     }();
     if (n != 4096 && !(n == 2048 && wg2048)) return false;
@@ -2276,6 +2277,8 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
     a.n_chunks = int((F + target - 1) / target);
     a.M = int((F + a.n_chunks - 1) / a.n_chunks);
     a.n_chunks = int((F + a.M - 1) / a.M);
+    chunk_override(F, a);
+    note_chunks(a.n_chunks);
     a.ring_blocks = g.ring_len / g.h;
     a.pad = g.pad;
     a.pad_mode = g.pad_mode;
@@ -2289,6 +2292,7 @@ hipError_t launch_fused_wg(const Geometry& g, const DevTables& t, const float* x
         choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * (hot3 ? 3 : 2), a.n_chunks,
                              a.M);
         chunk_override(F, a);
+        note_chunks(a.n_chunks);
         const int64_t grid4 = int64_t(n_streams) * a.n_chunks;
         if (!t.pflags || t.pflags_len < grid4) return hipErrorInvalidValue;
         // the paired-only hot walker, then the two-regime walker over the chunks it
@@ -2413,12 +2417,14 @@ static bool any_lds_tables(int p, int tw_len) {
 }
 
 template <typename K>
-static hipError_t launch_any(K kernel, AnyArgs& a, int64_t items, hipStream_t stream, bool tables) {
+static hipError_t launch_any(K kernel, AnyArgs& a, int64_t items, hipStream_t stream, bool tables,
+                             int32_t id = CRLOT_K_FFT_ANY) {
     a.waves_per_block = any_waves_per_block(a.pl.p);
     const size_t lds = any_lds_bytes(a.pl.p, a.tw_len, a.waves_per_block, tables);
     hipError_t e = set_lds(kernel, lds);
     if (e != hipSuccess) return e;
     const int64_t grid = (items + a.waves_per_block - 1) / a.waves_per_block;
+    note_launch(id, grid);
     hipLaunchKernelGGL(kernel, dim3(unsigned(grid)), dim3(64 * a.waves_per_block), lds, stream, a);
     return hipGetLastError();
 }
@@ -2446,10 +2452,10 @@ hipError_t launch_synth_any(const Geometry& g, const DevTables& t, const float* 
     a.tw_len = int(build_any_twiddles(a.pl.p).size() / 2);
     const bool tb = any_lds_tables(a.pl.p, a.tw_len);
     if (tb)
-        return t.gain ? launch_any(k_synth_any<true, true>, a, items, stream, true)
-                      : launch_any(k_synth_any<false, true>, a, items, stream, true);
-    return t.gain ? launch_any(k_synth_any<true, false>, a, items, stream, false)
-                  : launch_any(k_synth_any<false, false>, a, items, stream, false);
+        return t.gain ? launch_any(k_synth_any<true, true>, a, items, stream, true, CRLOT_K_SYNTH_ANY)
+                      : launch_any(k_synth_any<false, true>, a, items, stream, true, CRLOT_K_SYNTH_ANY);
+    return t.gain ? launch_any(k_synth_any<true, false>, a, items, stream, false, CRLOT_K_SYNTH_ANY)
+                  : launch_any(k_synth_any<false, false>, a, items, stream, false, CRLOT_K_SYNTH_ANY);
 }
 
 hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* twany,
@@ -2502,6 +2508,7 @@ hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* 
     auto k = t.gain ? k_stft_ola_any<true> : k_stft_ola_any<false>;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_FUSED_ANY, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * w), lds, stream, f);
     return hipGetLastError();
 }
@@ -2595,11 +2602,13 @@ static hipError_t synth_e(const SynthArgs& a, int64_t grid, hipStream_t stream) 
         auto k = a.t.gain ? k_synth_frames<E, true, true> : k_synth_frames<E, false, true>;
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
+        note_launch(CRLOT_K_SYNTH, grid);
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
     } else {
         auto k = a.t.gain ? k_synth_frames<E, true, false> : k_synth_frames<E, false, false>;
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
+        note_launch(CRLOT_K_SYNTH, grid);
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
     }
     return hipGetLastError();
@@ -2653,7 +2662,7 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
     a.n_streams = n_streams;
     a.gain = g.gain;
     static const int gv = [] {  // A/B: CRLOT_GATHER=2 the per-sample-grid kernel
-        const char* e = std::getenv("CRLOT_GATHER");
+        const char* e = ab_env("CRLOT_GATHER");
         return e ? std::atoi(e) : 3;
     }();
     if (gv == 3 && n_streams <= 65535 && F < (int64_t(1) << 31) && out_len <= F * g.h &&
@@ -2662,10 +2671,11 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
         auto kg = nb <= 4 ? k_ola_gather_blk<4> : k_ola_gather_blk<8>;
         const int threads = g.h >= 256 ? 256 : (g.h + 63) / 64 * 64;
         static const int bpb_env = [] {
-            const char* e = std::getenv("CRLOT_GATHER_BPB");
+            const char* e = ab_env("CRLOT_GATHER_BPB");
             return e ? std::atoi(e) : 0;
         }();
         const int bpb = bpb_env > 0 ? bpb_env : std::max(1, 1024 / g.h);  // >= 1024 outputs per workgroup
+        note_launch(CRLOT_K_GATHER, (F + bpb - 1) / bpb * n_streams);
         hipLaunchKernelGGL(kg, dim3(unsigned((F + bpb - 1) / bpb), unsigned(n_streams)), dim3(threads), 0, stream,
                            a, bpb);
         return hipGetLastError();
@@ -2674,12 +2684,14 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
         // one sample per thread (two per thread measured 5-15 % slower: occupancy)
         auto kg = (g.n + g.h - 1) / g.h <= 4 ? k_ola_gather2<1, 4> : k_ola_gather2<1, 8>;
         const int64_t per_block = 256;
+        note_launch(CRLOT_K_GATHER, (out_len + per_block - 1) / per_block * n_streams);
         hipLaunchKernelGGL(kg, dim3(unsigned((out_len + per_block - 1) / per_block), unsigned(n_streams)),
                            dim3(256), 0, stream, a);
         return hipGetLastError();
     }
     const int64_t total = int64_t(n_streams) * out_len;
     const int64_t grid = (total + 255) / 256;
+    note_launch(CRLOT_K_GATHER, grid);
     hipLaunchKernelGGL(k_ola_gather, dim3(unsigned(grid)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
@@ -2691,6 +2703,7 @@ static hipError_t fft_e(const FftArgs& a, hipStream_t stream) {
     auto k = CPLX ? k_cfft<E, INV> : INV ? k_irfft<E> : k_rfft<E>;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_FFT, grid);
     hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a);
     return hipGetLastError();
 }

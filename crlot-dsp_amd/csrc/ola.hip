@@ -263,6 +263,7 @@ hipError_t launch_deinterleave(const float* x, int64_t ld_x, float* planes, int 
     if (groups <= 0 || T <= 0) return hipSuccess;
     const int tr = ilv_rows(C);
     const size_t lds = sizeof(float) * size_t(tr) * (C + 1);
+    note_launch(CRLOT_K_DEINTERLEAVE, (T + tr - 1) / tr * groups);
     hipLaunchKernelGGL(k_deinterleave, dim3(unsigned((T + tr - 1) / tr), unsigned(groups)), dim3(256), lds, s,
                        x, ld_x, planes, T, C);
     return hipGetLastError();
@@ -273,6 +274,7 @@ hipError_t launch_interleave(const float* planes, int64_t L, float* y, int64_t l
     if (groups <= 0 || L <= 0) return hipSuccess;
     const int tr = ilv_rows(C);
     const size_t lds = sizeof(float) * size_t(tr) * (C + 1);
+    note_launch(CRLOT_K_INTERLEAVE, (L + tr - 1) / tr * groups);
     hipLaunchKernelGGL(k_interleave, dim3(unsigned((L + tr - 1) / tr), unsigned(groups)), dim3(256), lds, s,
                        planes, L, y, ld_y, C);
     return hipGetLastError();

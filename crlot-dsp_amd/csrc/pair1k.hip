@@ -573,7 +573,7 @@ int pair_waves_per_cu() {
 bool pair_nofix() {
 #ifdef CRLOT_PAIR_NOFIX_DIAG
     static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PAIR_NOFIX");
+        const char* e = ab_env("CRLOT_PAIR_NOFIX");
         return e && e[0] == '1';
     }();
     return v;
@@ -593,8 +593,10 @@ constexpr bool pair_hot() {
     return (SH == 2 && CRLOT_PAIR_HOT2) || SH == 4 || (SH == 8 && CRLOT_PAIR_HOT8);
 }
 
-bool pair32_enabled();                                            // pair32.hip (experiment)
+#ifdef CRLOT_PAIR32_EXPERIMENT
+bool pair32_enabled();                                            // experiments/pair32.hip
 hipError_t launch_pair32(const FusedArgs& a, hipStream_t stream);
+#endif
 
 template <int SH, bool ILV>
 hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
@@ -607,23 +609,29 @@ hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
     if ((e = set_lds(kf, lds)) != hipSuccess) return e;
     if (!a.t.pflags || a.t.pflags_len < waves) return hipErrorInvalidValue;
     if constexpr (pair_hot<SH>()) {
+#ifdef CRLOT_PAIR32_EXPERIMENT
         if (!ILV && pair32_enabled() && a.pad_mode == 0 && a.t.hot && !a.t.gain) {
             if ((e = launch_pair32(a, stream)) != hipSuccess) return e;
+            note_launch(CRLOT_K_PAIR_FIX, grid);
             hipLaunchKernelGGL(kf, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
             return hipGetLastError();
         }
+#endif
         if (a.pad_mode == 0 && a.t.hot && (!a.t.gain || CRLOT_PAIR_REG_TW)) {
             auto k = a.t.gain ? k_stft_ola_pair<SH, NB, W, ILV, CRLOT_PAIR_REG_TW != 0> : k_stft_ola_pair<SH, NB, W, ILV, false>;
             if ((e = set_lds(k, lds)) != hipSuccess) return e;
+            note_launch(CRLOT_K_PAIR_HOT, grid);
             hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             if (pair_nofix()) return hipSuccess;  // diagnostics only: flagged chunks stay wrong
+            note_launch(CRLOT_K_PAIR_FIX, grid);
             hipLaunchKernelGGL(kf, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
             return hipGetLastError();
         }
     }
     FusedArgs b = a;
     b.fix_all = 1;
+    note_launch(CRLOT_K_PAIR_ALL, grid);
     hipLaunchKernelGGL(kf, dim3(unsigned(grid)), dim3(64 * W), lds, stream, b);
     return hipGetLastError();
 }

@@ -276,23 +276,25 @@ hipError_t launch_pair30(const Geometry& g, const DevTables& t, const float* x, 
     // synthesis window read from L1 (profiles/r03_pair30_ab.jsonl); CRLOT_P30_VARIANT=1
     // selects the 2-wave form (A/B).  The gain walker needs the 2-wave budget.
     static const int venv = [] {
-        const char* e = std::getenv("CRLOT_P30_VARIANT");
+        const char* e = ab_env("CRLOT_P30_VARIANT");
         return e ? std::atoi(e) : 0;
     }();
     const int wpe = t.gain || venv == 1 ? 2 : 3;
     const int64_t walks_per_cu = std::min<int64_t>(int64_t(160 * 1024 / lds), 2 * wpe);
     const int64_t resident = int64_t(cus) * walks_per_cu;
-    const int64_t nc = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + n_streams - 1) / n_streams));
+    const int64_t nc = chunks_or(std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + n_streams - 1) / n_streams)), F);
     a.M = int((F + nc - 1) / nc);
     a.n_chunks = int((F + a.M - 1) / a.M);
     const int64_t walks = int64_t(n_streams) * a.n_chunks;
     if (t.pflags_len < walks) return hipErrorInvalidValue;
     *n_chunks = a.n_chunks;
+    note_chunks(a.n_chunks);
     auto k = t.gain      ? k_pair30_hot<true, 2, true, false>
              : venv == 1 ? k_pair30_hot<false, 2, true, true>
                          : k_pair30_hot<false, 3, false, true>;
     hipError_t e = set_lds(k, lds);
     if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_PAIR30, walks);
     hipLaunchKernelGGL(k, dim3(unsigned(walks)), dim3(128), lds, stream, a);
     return hipGetLastError();
 }

@@ -394,7 +394,7 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
                          int* streams_per_walk, hipStream_t stream) {
     using namespace fk;
     static const int venv = [] {
-        const char* e = std::getenv("CRLOT_P15_VARIANT");
+        const char* e = ab_env("CRLOT_P15_VARIANT");
         const int v = e ? std::atoi(e) : -1;
         return v >= 0 && v < 5 ? v : -1;
     }();
@@ -412,7 +412,7 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
     // H <= 4 L: a block is at most 4 rows of the walk, its divisors are fetched
     // ahead (CRLOT_P15_DPRE=0 keeps the row loop, A/B)
     static const bool dpre_env = [] {
-        const char* e = std::getenv("CRLOT_P15_DPRE");
+        const char* e = ab_env("CRLOT_P15_DPRE");
         return !(e && e[0] == '0');
     }();
     const bool dpre = dpre_env && t.den_rden != nullptr && g.h <= 4 * (g.n / 15);
@@ -441,16 +441,18 @@ hipError_t launch_pair15(const Geometry& g, const DevTables& t, const float* x, 
     const int64_t wpc = std::min<int64_t>(W * int64_t(160 * 1024 / lds), 4 * kP15Shapes[v].wpe);  // waves per CU
     const int64_t resident = int64_t(cus) * std::max<int64_t>(W, wpc);
     const int64_t units = (n_streams + halves - 1) / halves;
-    const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + units - 1) / units));
+    const int64_t n = chunks_or(std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + units - 1) / units)), F);
     a.M = int((F + n - 1) / n);
     a.n_chunks = int((F + a.M - 1) / a.M);
     const int64_t waves = units * a.n_chunks;
     if (t.pflags_len < waves) return hipErrorInvalidValue;
     *n_chunks = a.n_chunks;
     *streams_per_walk = halves;
+    note_chunks(a.n_chunks);
     hipError_t e = hipSuccess;
     auto go = [&](auto k, int w) {
         if ((e = set_lds(k, lds)) != hipSuccess) return;
+        note_launch(CRLOT_K_PAIR15, (waves + w - 1) / w);
         hipLaunchKernelGGL(k, dim3(unsigned((waves + w - 1) / w)), dim3(64 * w), lds, stream, a);
         e = hipGetLastError();
     };

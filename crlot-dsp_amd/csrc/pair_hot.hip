@@ -374,6 +374,7 @@ hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t s
     auto go = [&](auto k) {
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
+        note_launch(G::N == 4096 ? CRLOT_K_PAIR4K_HOT : CRLOT_K_PAIR2K_HOT, grid);
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(G::L), lds, stream, a);
         return hipGetLastError();
     };
@@ -393,238 +394,10 @@ hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t s
     }
 }
 
-// ---- N = 4096 / 2048 at three waves per SIMD (three 4k / six 2k workgroups per CU).
-// k_pair_wg_hot<Geo4k> needs 224-226 VGPRs and two exchange buffers (78 KB), so
-// only two workgroups fit a CU and the SIMD idles at every barrier (2k: four
-// workgroups, the same two waves per SIMD).  This walker
-// runs the same operations in the same order (bit-identical) with
-//   * ONE exchange buffer at two barriers per pair: the inverse exchange reads
-//     column t of every row and the next forward exchange writes column t of
-//     every row, and both are lane t's own accesses, so no barrier is needed
-//     between them; the forward reads and the transposes stay in the wave's own
-//     rows, which only its own inverse writes touch;
-//   * the second-stage twiddles (W256^{x k2}: 16 distinct values per k2; 2k:
-//     W128, 8) in LDS after the buffer;
-//   * both windows read per pair from the tables (L2-resident) instead of 32
-//     registers;
-// so <= 168 VGPRs and 40.8 KB (4k) / 20.4 KB (2k) of LDS.
-// Measured slower (4096/1024 196k vs 228k Msamples/s, 2048/512
-// 196k vs 234k), so it is built only with -DCRLOT_PAIR_WG_HOT3_EXPERIMENT
-// (then CRLOT_PAIR4K_HOT=3 selects it); the release library has stubs.
+// ---- N = 4096 / 2048 at three waves per SIMD: a measured negative result kept
+// outside the release library (experiments/pair_wg_hot3.inc); stubs here.
 #ifdef CRLOT_PAIR_WG_HOT3_EXPERIMENT
-template <typename G, int SH, int NB>
-__global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_pair_wg_hot3(const FusedArgs a) {
-    constexpr int E = 16, L = G::L, H = L * SH, KS = G::KS, SIDE = G::SIDE;
-    constexpr int R = RotWg<NB>::R, U = RotWg<NB>::U;
-    static_assert(NB * SH == E, "N = NB * H");
-    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    dev::pc* A = reinterpret_cast<dev::pc*>(smem);
-    dev::pc* W2 = A + 16 * KS;  // [k2 - 1][x], as the device table's tail
-    const int t = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-
-    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
-    const int f0 = c * a.M;
-    const int f1 = min(a.F, f0 + a.M);
-    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
-    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
-    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
-    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
-    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
-    const __amdgpu_buffer_rsrc_t rwa = dev::make_rsrc(a.t.wa, 4u * G::N);
-    const __amdgpu_buffer_rsrc_t rws = dev::make_rsrc(a.t.wsn, 4u * G::N);
-    const float g = a.gain;
-    const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
-
-    const dev::pc* gtw = reinterpret_cast<const dev::pc*>(a.t.ptw4);
-    if (t < 15 * SIDE) W2[t] = gtw[15 * L + t];
-    dev::pc w1[15];
-#pragma unroll
-    for (int k = 1; k < 16; ++k) w1[k - 1] = gtw[(k - 1) * L + t];
-    __syncthreads();
-    const dev::pc* w2 = W2 + (t % SIDE);
-    const auto w2f = [&](int i) { return w2[SIDE * i]; };
-    dev::pc* own = A + KS * G::ROWS_PER_WAVE * wave;
-    constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-
-    bool bad = false;
-    auto hop_check = [&](const float (&h)[SH]) {
-        uint32_t mx = 0u, mn = ~0u;
-#pragma unroll
-        for (int q = 0; q < SH; ++q) {
-            const uint32_t u = __builtin_bit_cast(uint32_t, h[q]) & 0x7fffffffu;
-            mx = max(mx, u);
-            mn = min(mn, u - 1u);
-        }
-        bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
-    };
-    float xr[R][SH];
-#pragma unroll
-    for (int h = 0; h <= NB; ++h) {
-        load_hop_wg0<L, SH>(xr[h], rx, t, (fs + h) * H - a.pad);
-        hop_check(xr[h]);
-    }
-    float acc[NB][SH];
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-#pragma unroll
-        for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
-
-    auto emit = [&](const float (&av)[SH], int k, const float (&dr)[2 * SH]) {
-        int ex_lo = 0, ex_hi = 0;
-#pragma unroll
-        for (int q = 0; q < SH; ++q) {
-            const int e = __builtin_amdgcn_frexp_expf(av[q]);
-            ex_lo = min(ex_lo, e);
-            ex_hi = max(ex_hi, e);
-        }
-        bad |= !((ex_lo >= -63) & (ex_hi <= 65));
-        float o[SH];
-#pragma unroll
-        for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
-        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-#pragma unroll
-        for (int q = 0; q < SH; ++q)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
-                                                  k * (4 * H) + q * (4 * L), CRLOT_HOT_AUX);
-    };
-    // window value m of this lane; the opaque zero keeps the loads inside the
-    // loop (hoisted out they would hold the 32 registers this walker frees)
-    auto win = [&](__amdgpu_buffer_rsrc_t r, int z, int m) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, t * 4, z + m * (4 * L), 0));
-    };
-
-    // vmcnt retires in order and counts stores: the synthesis window is loaded
-    // before the step's hop prefetch, and the next pair's analysis window before
-    // this pair's output stores, so neither wait drains a store or a prefetch
-    float wan[E];
-    {
-        int z = 0;
-        asm volatile("" : "+s"(z));
-#pragma unroll
-        for (int m = 0; m < E; ++m) wan[m] = win(rwa, z, m);
-    }
-    auto step = [&](auto phc, int k) {
-        constexpr int PH = decltype(phc)::value;
-        constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
-        int z = 0;
-        asm volatile("" : "+s"(z));
-        float wsr[E];
-#pragma unroll
-        for (int m = 0; m < E; ++m) wsr[m] = win(rws, z, m);
-        load_hop_wg0<L, SH>(xr[(S0 + NB + 1) % R], rx, t, (k + NB + 1) * H - a.pad);
-        load_hop_wg0<L, SH>(xr[(S0 + NB + 2) % R], rx, t, (k + NB + 2) * H - a.pad);
-        const bool partner = k + 1 < a.F;  // as the two-regime walker
-        dev::pc v[E];
-#pragma unroll
-        for (int m = 0; m < E; ++m)
-            v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wan[m],
-                              partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wan[m] : 0.0f);
-        // forward (G::fwd with one buffer)
-        dev::pdft16<false>(v);
-        dev::pc_tw_run<false>(v, idx, [&](int i) { return w1[i]; });
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) A[KS * k1 + t] = v[k1];
-        __syncthreads();
-        {
-            const dev::pc* rb = A + KS * (t / SIDE) + (t % SIDE);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] = rb[SIDE * r];
-        }
-        G::fwd_tail(v, own, w2f, t & 63);
-
-        // inverse (G::inv with one buffer)
-        G::inv_head(v, own, w2f, t & 63);
-        {
-            dev::pc* wb = A + KS * (t / SIDE) + (t % SIDE);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) wb[SIDE * r] = v[r];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) v[k1] = A[KS * k1 + t];
-        dev::pc_tw_run<true>(v, idx, [&](int i) { return w1[i]; });
-        // the divisors late: during the inverse they would hold 16 registers
-        float dr0[2 * SH], dr1[2 * SH];
-        load_den_wg<L, SH>(dr0, rp, t, k % a.ring_blocks);
-        load_den_wg<L, SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
-        dev::pdft16<true>(v);
-        {
-            int e[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int m = 0; m < E; ++m)
-                e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
-            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= G::MIN_EXP;
-        }
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{wsr[m], wsr[m]};
-#pragma unroll
-        for (int m = 0; m < E; ++m) wan[m] = win(rwa, z, m);
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            float& r = acc[(B0 + m / SH) % NB][m % SH];
-            r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
-        }
-        emit(acc[B0], k, dr0);
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
-            r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
-        }
-        emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
-        hop_check(xr[(S0 + NB + 1) % R]);
-        hop_check(xr[(S0 + NB + 2) % R]);
-    };
-    for (int k = fs; k < f1; k += 2 * U) {
-        step(std::integral_constant<int, 0>(), k);
-        if (k + 2 >= f1) break;
-        step(std::integral_constant<int, 1>(), k + 2);
-        if (k + 4 >= f1) break;
-        step(std::integral_constant<int, 2>(), k + 4);
-        if (k + 6 >= f1) break;
-        step(std::integral_constant<int, 3>(), k + 6);
-        if constexpr (U > 4) {
-            if (k + 8 >= f1) break;
-            step(std::integral_constant<int, 4>(), k + 8);
-            if (k + 10 >= f1) break;
-            step(std::integral_constant<int, 5>(), k + 10);
-            if (k + 12 >= f1) break;
-            step(std::integral_constant<int, 6>(), k + 12);
-            if (k + 14 >= f1) break;
-            step(std::integral_constant<int, 7>(), k + 14);
-        }
-    }
-    const bool any_bad = __syncthreads_or(bad);
-    if (t == 0) a.t.pflags[blockIdx.x] = any_bad ? 1u : 0u;
-}
-
-template <typename G>
-constexpr size_t hot3_lds() {
-    return sizeof(dev::pc) * (16 * G::KS + 15 * G::SIDE);
-}
-static_assert(3 * 4 / (Geo4k::L / 64) * hot3_lds<Geo4k>() <= 160 * 1024, "three waves per SIMD (4k)");
-static_assert(3 * 4 / (Geo2k::L / 64) * hot3_lds<Geo2k>() <= 160 * 1024, "three waves per SIMD (2k)");
-
-template <typename G>
-hipError_t launch_wg_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
-    if (a.t.gain) return hipErrorInvalidValue;
-    constexpr size_t lds = hot3_lds<G>();
-    auto go = [&](auto k) {
-        hipError_t e = set_lds(k, lds);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(G::L), lds, stream, a);
-        return hipGetLastError();
-    };
-    // H = 4 L only: the other hops' rotation slots spill 60-100 VGPRs at 168
-    return sh == 4 ? go(k_pair_wg_hot3<G, 4, 4>) : hipErrorInvalidValue;
-}
-hipError_t launch_pair4k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
-    return launch_wg_hot3<Geo4k>(sh, a, grid, stream);
-}
-hipError_t launch_pair2k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
-    return launch_wg_hot3<Geo2k>(sh, a, grid, stream);
-}
+#include "experiments/pair_wg_hot3.inc"
 #else
 hipError_t launch_pair4k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { return hipErrorInvalidValue; }
 hipError_t launch_pair2k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { return hipErrorInvalidValue; }
@@ -775,6 +548,7 @@ hipError_t launch_pair512_hot(int sh, const FusedArgs& a, int64_t waves, int w, 
     auto go = [&](auto k) {
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
+        note_launch(CRLOT_K_PAIR512_HOT, grid);
         hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * W), lds, stream, a);
         return hipGetLastError();
     };

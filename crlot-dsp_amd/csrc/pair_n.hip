@@ -45,7 +45,7 @@ __host__ __device__ inline int pn_ring(int n, int h, bool lean) {
 // CRLOT_PN_PLAN=V (A/B): the alternative radix list V of fft_pairn.h for 882 / 1764
 int pn_variant(int n) {
     static const int v = [] {
-        const char* e = std::getenv("CRLOT_PN_PLAN");
+        const char* e = ab_env("CRLOT_PN_PLAN");
         const int x = e ? std::atoi(e) : 0;
         return x >= 0 && x < 4 ? x : 0;
     }();
@@ -55,7 +55,7 @@ int pn_variant(int n) {
 // below: two at 1764)
 int pn_halves(int n) {
     static const int w = [] {
-        const char* e = std::getenv("CRLOT_PN_WIDE");
+        const char* e = ab_env("CRLOT_PN_WIDE");
         return e ? (e[0] == '1' ? 2 : 1) : 0;
     }();
     if (n != 882 && n != 1764 && n != 960 && n != 1920) return 1;
@@ -65,7 +65,7 @@ int pn_halves(int n) {
 // exact-size ring (one more walk per CU at 1764)
 bool pn_lean(int n) {
     static const int l = [] {
-        const char* e = std::getenv("CRLOT_PN_LEAN");
+        const char* e = ab_env("CRLOT_PN_LEAN");
         return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
     if (pn_halves(n) != 2) return false;
@@ -377,7 +377,7 @@ bool pairn_size(int n) {
 // with -DCRLOT_PN_15)
 bool pairn_over_pair15(int n) {
     static const bool v = [] {
-        const char* e = std::getenv("CRLOT_PN_OVER15");
+        const char* e = ab_env("CRLOT_PN_OVER15");
         return e && e[0] == '1';
     }();
     return v && (n == 960 || n == 480) && pairn_size(n);
@@ -419,18 +419,22 @@ hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, f
         cus = 256;
     // chunks: about two resident rounds of walkers, each >= 48 frames
     const int64_t resident = int64_t(cus) * walks;
-    const int64_t n = std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + n_streams - 1) / n_streams));
+    // (a forced chunking keeps a flag per wave within the F-per-stream flag rows)
+    const int64_t n = chunks_or(std::max<int64_t>(1, std::min<int64_t>(F / 48, (2 * resident + n_streams - 1) / n_streams)),
+                                std::max<int64_t>(1, F / halves));
     a.M = int((F + n - 1) / n);
     a.n_chunks = int((F + a.M - 1) / a.M);
     const int64_t total = int64_t(n_streams) * a.n_chunks;  // walks
     if (t.pflags_len < total * halves) return hipErrorInvalidValue;
     *n_chunks = a.n_chunks * halves;  // flags per stream (one per wave)
+    note_chunks(a.n_chunks);
     const size_t lds = pn_tables(g.n) + size_t(walks) * pn_per_walk(g.n, g.h);
     hipError_t e = hipSuccess;
     pn_dispatch(pn_key(g.n), [&](auto nc) {
         constexpr int NN = decltype(nc)::value;
         auto k = t.gain ? k_pairn<NN, true> : k_pairn<NN, false>;
         if ((e = set_lds(k, lds)) != hipSuccess) return;
+        note_launch(CRLOT_K_PAIRN, (total + walks - 1) / walks);
         hipLaunchKernelGGL(k, dim3(unsigned((total + walks - 1) / walks)), dim3(64 * halves * walks), lds, stream, a);
         e = hipGetLastError();
     });

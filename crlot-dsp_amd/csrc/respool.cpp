@@ -1,5 +1,6 @@
 // respool.cpp -- see respool.h.
 #include "respool.h"
+#include "ab.h"
 
 #include <cstdint>
 #include <cstdlib>
@@ -76,7 +77,7 @@ void pool_pinned_put(void* p, size_t cap) {
 
 bool no_pool() {
     static const bool v = [] {
-        const char* e = std::getenv("CRLOT_NO_POOL");  // diagnostic: plain hipMalloc / hipFree
+        const char* e = crlot::ab_env("CRLOT_NO_POOL");  // diagnostic: plain hipMalloc / hipFree
         return e && e[0] == '1';
     }();
     return v;

@@ -131,6 +131,56 @@ int crlot_plan_set_spectral_gain_async(crlot_plan* plan, const float* gain, void
  * chunk (their paired-only hot walkers off): bit-identical to 1, for parity
  * diagnostics.  Other values: CRLOT_EINVAL. */
 int crlot_plan_set_frame_pairing(crlot_plan* plan, int32_t enable);
+/* Chunks per stream the chunked walkers of crlot_roundtrip /
+ * crlot_roundtrip_interleaved split every stream into (every frame-pair walker
+ * and the per-frame fused walkers).  0 (default) lets the library choose (whole
+ * resident rounds of the device); n > 0 forces min(n, F) chunks (min(n, F/2) on
+ * the two-wave K_pairN walks).  Output bits never depend on it (each chunk
+ * recomputes its warm-up frames); it exists so parity tests can move the chunk
+ * seams, and the launch record below reports the chunking a call used.
+ * Negative: CRLOT_EINVAL. */
+int crlot_plan_set_chunks(crlot_plan* plan, int32_t chunks_per_stream);
+/* What the plan's last call on `stream` launched: kernels in launch order
+ * (CRLOT_K_* ids below; the first 8 are kept, n_kernels counts all), the
+ * workgroups of each launch, and the chunks per stream of the walk (0 when the
+ * call ran no chunked walker).  Recorded by crlot_roundtrip,
+ * crlot_roundtrip_interleaved, crlot_roundtrip_stages, crlot_ola_gather and
+ * the batched FFTs; a call that failed records what it launched before failing.
+ * No call on `stream` yet: n_kernels = 0. */
+#define CRLOT_K_PAIR_HOT 1       /* K_pair paired-only walker, N = 1024 */
+#define CRLOT_K_PAIR_FIX 2       /* K_pair two-regime walker: the flagged chunks after the hot walker */
+#define CRLOT_K_PAIR_ALL 3       /* K_pair two-regime walker over every chunk */
+#define CRLOT_K_PAIR512_HOT 4
+#define CRLOT_K_PAIR512 5        /* two-regime walker, N = 512 (flagged chunks or all, see fix_all) */
+#define CRLOT_K_PAIR2K_HOT 6
+#define CRLOT_K_PAIR2K 7
+#define CRLOT_K_PAIR4K_HOT 8
+#define CRLOT_K_PAIR4K 9
+#define CRLOT_K_FUSED 10         /* per-frame fused walker, one frame per wave in flight */
+#define CRLOT_K_FUSED2 11        /* ... two frames per wave in flight */
+#define CRLOT_K_FUSED_WG 12      /* per-frame workgroup walker, N = 4096 */
+#define CRLOT_K_PAIR15 13        /* N = 960 / 480 pairs */
+#define CRLOT_K_PAIRN 14         /* N = 320 ... 1764 pairs (2, 3, 5, 7 factors) */
+#define CRLOT_K_PAIR30 15        /* N = 1920 pairs, even hops */
+#define CRLOT_K_FUSED_ANY 16     /* any-size per-frame walker (all streams, or the flagged ones) */
+#define CRLOT_K_SYNTH 17         /* staged path: frames */
+#define CRLOT_K_SYNTH_ANY 18
+#define CRLOT_K_GATHER 19        /* staged path: overlap-add gather */
+#define CRLOT_K_DEINTERLEAVE 20
+#define CRLOT_K_INTERLEAVE 21
+#define CRLOT_K_FFT 22           /* batched rfft / irfft / cfft */
+#define CRLOT_K_FFT_ANY 23
+#define CRLOT_K_EXPERIMENT 99    /* experiment builds only */
+typedef struct crlot_launch_info {
+    int32_t n_kernels;
+    int32_t kernels[8];
+    int64_t grid[8];
+    int32_t n_chunks;
+    int32_t reserved;
+} crlot_launch_info;
+int crlot_plan_last_launch(const crlot_plan* plan, void* stream, crlot_launch_info* out);
+/* Name of a CRLOT_K_* id ("k_pair_hot", ...); "unknown" otherwise. */
+const char* crlot_kernel_name(int32_t kernel_id);
 int crlot_plan_info(const crlot_plan* plan, int32_t* frame_size, int32_t* hop_size,
                     int32_t* ring_len);
 /* Frames of a T-sample stream: Framer whole push (framer.cc:88-117) or

@@ -1,4 +1,5 @@
-"""Chunks-per-stream sweep in one process (CRLOT_CHUNKS is read at every launch).
+"""Chunks-per-stream sweep in one process (crlot_plan_set_chunks per setting; the
+launch record confirms the chunking each run used).
 usage: python scripts/sweep_inproc.py [S T N H] [n1,n2,...]"""
 import json
 import os
@@ -39,14 +40,13 @@ def main():
         plan = pkg.Plan(frame_size=N, hop_size=H, frame_pairing=pairing)
         y = torch.empty((S, plan.output_length(T)), device="cuda")
         for n in ns:
-            if n:
-                os.environ["CRLOT_CHUNKS"] = str(n)
-            else:
-                os.environ.pop("CRLOT_CHUNKS", None)
+            plan.set_chunks(n)
             ms = timeit(plan, x, y, torch)
-            print(json.dumps({"pairing": pairing, "chunks": n or "auto", "ms": round(ms, 4),
+            rec = plan.last_launch()
+            print(json.dumps({"pairing": pairing, "chunks": n or "auto", "n_chunks": rec["n_chunks"],
+                              "kernels": rec["kernels"], "ms": round(ms, 4),
                               "Msamples_s": round(S * T / ms / 1e3, 1)}), flush=True)
-        os.environ.pop("CRLOT_CHUNKS", None)
+        plan.set_chunks(0)
 
 
 if __name__ == "__main__":

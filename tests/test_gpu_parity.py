@@ -22,6 +22,14 @@ REL_L2 = 1e-6
 MAX_ABS = 4e-6
 
 
+def expected_chunks(F, forced):
+    """Chunks per stream a forced chunking gives: min(forced, F) chunks of
+    ceil(F / n) frames, which can merge into fewer (crlot_plan_set_chunks)."""
+    n = max(1, min(forced, F))
+    m = -(-F // n)
+    return -(-F // m)
+
+
 def bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
@@ -156,9 +164,11 @@ def test_frame_pair_kernel_vs_oracle(pkg, oracle, torch_cuda, n, h, mode):
 
 @pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (512, 128), (2048, 512), (1024, 512),
                                  (1024, 128)])
-def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkeypatch, n, h):
+def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, n, h):
     """Pairs are aligned to even frames, so a stream's output bits do not depend on
-    how its frames are chunked over waves nor on the batch it is processed in."""
+    how its frames are chunked over waves nor on the batch it is processed in.
+    The chunking is forced per plan (crlot_plan_set_chunks) and the launch record
+    must show that it really changed."""
     torch = torch_cuda
     T = 60_000
     x = oracle.synth_streams(5, T, config_id=12)
@@ -167,15 +177,23 @@ def test_frame_pair_bits_independent_of_chunking(pkg, oracle, torch_cuda, monkey
     y = host(plan.roundtrip(xd))
     for s in (0, 3):
         assert np.array_equal(bits(host(plan.roundtrip(xd[s:s + 1].contiguous()))[0]), bits(y[s]))
-    for chunks in ("1", "2", "3", "7", "40"):
-        monkeypatch.setenv("CRLOT_CHUNKS", chunks)
-        assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(y)), chunks
-    monkeypatch.delenv("CRLOT_CHUNKS")
+    F = plan.frame_count(T)
+    default_chunks = plan.last_launch()["n_chunks"]
+    seen = {default_chunks}
+    for chunks in (1, 2, 3, 7, 40):
+        plan.set_chunks(chunks)
+        yc = host(plan.roundtrip(xd))
+        got = plan.last_launch()["n_chunks"]
+        assert got == expected_chunks(F, chunks), (chunks, got)
+        seen.add(got)
+        assert np.array_equal(bits(yc), bits(y)), chunks
+    plan.set_chunks(0)
+    assert len(seen) >= 5, seen  # the sweep moved the seams
 
 
 @pytest.mark.parametrize("n,h,burst_hop", [(1024, 256, 82), (1024, 256, 83), (4096, 1024, 20), (4096, 1024, 21),
                                            (512, 128, 150), (512, 128, 151), (2048, 512, 40), (2048, 512, 41)])
-def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, n, h, burst_hop, monkeypatch):
+def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, n, h, burst_hop):
     """K_pair's unpaired regime: a hop of huge samples (1e25, beyond px_hi) makes
     the pairs that contain it transform each frame alone, as the reference does,
     so a neighbour sharing a pair with a burst frame keeps its own accuracy.  The
@@ -200,10 +218,77 @@ def test_frame_pair_regimes_isolate_frames(pkg, oracle, torch_cuda, n, h, burst_
     assert d.max() <= MAX_ABS * 0.5, d.max()
     burst = ~clean
     assert rel_l2(y[burst], ref[burst]) <= REL_L2
-    for chunks in ("1", "3", "16"):
-        monkeypatch.setenv("CRLOT_CHUNKS", chunks)
-        assert np.array_equal(bits(host(plan.roundtrip(xd))[0]), bits(y)), chunks
-    monkeypatch.delenv("CRLOT_CHUNKS")
+    F = plan.frame_count(T)
+    for chunks in (1, 3, 16):
+        plan.set_chunks(chunks)
+        yc = host(plan.roundtrip(xd))[0]
+        assert plan.last_launch()["n_chunks"] == expected_chunks(F, chunks), chunks
+        assert np.array_equal(bits(yc), bits(y)), chunks
+    plan.set_chunks(0)
+
+
+# (frame, hop, the pair walker that must run, the walker that redoes flagged work)
+SEAM_WALKERS = [
+    (1024, 256, "k_pair_hot", "k_pair_fix"),
+    (4096, 1024, "k_pair4k_hot", "k_pair4k"),
+    (512, 128, "k_pair512_hot", "k_pair512"),
+    (2048, 512, "k_pair2k_hot", "k_pair2k"),
+    (960, 240, "k_pair15", "k_fused_any"),
+    (480, 120, "k_pair15", "k_fused_any"),
+    (882, 441, "k_pairn", "k_fused_any"),
+    (1764, 441, "k_pairn", "k_fused_any"),
+    (1920, 480, "k_pair30", "k_fused_any"),
+]
+
+
+@pytest.mark.parametrize("kind", ["huge", "nan"])
+@pytest.mark.parametrize("n,h,walker,redo", SEAM_WALKERS)
+def test_burst_on_chunk_seam(pkg, oracle, torch_cuda, n, h, walker, redo, kind):
+    """A hop of 1e25 (beyond the paired range) or NaN samples placed exactly on a
+    chunk seam of every pair walker: the burst's frames leave the paired regime on
+    both sides of the seam, the redo walker recomputes them, and the output bits
+    are the same under every chunking (the default's and three forced ones, one
+    of which puts the seam inside the burst's hop).  NaN is sanitised to 0 before
+    the FFT (kissfft_adapter.cc:102-110), so that output matches the oracle
+    everywhere; the 1e25 output matches it away from the burst's blocks and
+    relative to its own scale inside them."""
+    torch = torch_cuda
+    T = 48 * h + h // 2
+    x = oracle.synth_streams(2, T, config_id=n + h).copy()
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    F = plan.frame_count(T)
+    chunkings = (3, 4, 5)
+    seams = {c: -(-F // expected_chunks(F, c)) for c in chunkings}  # first seam = frames per chunk
+    # stream 0: the burst hop starts on the 4-chunk seam; stream 1: on the 5-chunk one
+    bursts = [seams[4], seams[5]]
+    val = np.float32(np.nan) if kind == "nan" else np.float32(1e25)
+    for s, b in enumerate(bursts):
+        x[s, b * h:(b + 1) * h] = val if kind == "nan" else x[s, b * h:(b + 1) * h] * val
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    info = plan.last_launch()
+    assert walker in info["kernels"] and redo in info["kernels"], info
+    assert np.all(np.isfinite(y))
+    for c in chunkings:
+        plan.set_chunks(c)
+        yc = host(plan.roundtrip(xd))
+        info = plan.last_launch()
+        assert info["n_chunks"] == expected_chunks(F, c) and walker in info["kernels"], (c, info)
+        assert np.array_equal(bits(yc), bits(y)), (c, kind)
+    plan.set_chunks(0)
+    ref = oracle.roundtrip_batch(x, n, h, nthreads=2)
+    xs = np.where(np.isfinite(x), x, 0.0).astype(np.float32)
+    reach = -(-n // h)  # output blocks one frame spans
+    for s, b in enumerate(bursts):
+        clean = np.ones(y.shape[1], bool)
+        if kind == "huge":
+            clean[max(0, b - reach + 1) * h:(b + reach) * h] = False
+            assert rel_l2(y[s][~clean], ref[s][~clean]) <= REL_L2, (s, b)
+        xq = xs[s].copy()
+        xq[b * h:(b + 1) * h] = 0.0  # the scale of the samples outside the burst
+        xmax = float(np.max(np.abs(xq)))
+        d = np.abs(y[s][clean].astype(np.float64) - ref[s][clean])
+        assert d.max() <= MAX_ABS * xmax, (s, b, kind, d.max())
 
 
 @pytest.mark.parametrize("scale", [1e-25, 1e25, 1.0])

@@ -14,7 +14,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "fft_pair32.h"
+#include "experiments/fft_pair32.h"
 
 using namespace crlot::dev;
 
