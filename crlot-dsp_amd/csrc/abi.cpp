@@ -1214,7 +1214,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     std::lock_guard<std::mutex> slk(sh->mu);
     crlot::CallServer* sv = sh->srv;
     if (kind == 1 && sh->fft.valid && sh->fft.index == sv->submitted() && sh->fft.batch == batch &&
-        std::memcmp(p->pack.data(), sh->fft.slot.out, sizeof(float) * nin) == 0) {
+        sv->live(sh->fft.slot) && std::memcmp(p->pack.data(), sh->fft.slot.out, sizeof(float) * nin) == 0) {
         // the spectrum the last forward returned, unchanged: its inverse is in the speculation slot
         sh->fft.valid = false;
         if ((rc = sv->wait_spec(sh->fft.index)) != CRLOT_OK) return rc;

@@ -107,6 +107,7 @@ int CallServer::create(int device, int e, int depth, size_t in_cap, size_t out_c
 
 int CallServer::alloc(size_t in_cap, size_t out_cap, size_t spec_cap) {
     // >= 1024 floats: the kernel fetches the first 4 KB of a slot with its descriptor
+    ++gen_;
     in_cap_ = align_up(std::max<size_t>(in_cap, 1024), 32);
     out_cap_ = align_up(std::max<size_t>(out_cap, 64), 32);
     spec_cap_ = align_up(spec_cap, 32);
@@ -230,7 +231,12 @@ int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
             }
             const auto us =
                 std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
-            if (us > 5000000) return fail(CRLOT_EHIP, "call server: request timed out");
+            if (us > 5000000) {
+                // the request is still in flight in the resident kernel: no later call
+                // may read a slot or speculation it could still write
+                broken_ = true;
+                return fail(CRLOT_EHIP, "call server: request timed out (server disabled)");
+            }
         }
         _mm_pause();
     }
@@ -291,6 +297,7 @@ int CallServer::next_slot(CallSlot* sl) {
         spec_req_[size_t(k)] = 0;
     }
     sl->index = q_ + 1;
+    sl->gen = gen_;
     sl->in = in_ + size_t(k) * in_cap_;
     sl->out = out_ + size_t(k) * out_cap_;
     sl->spec = out_ + size_t(depth_) * out_cap_ + size_t(k) * spec_cap_;
@@ -308,6 +315,7 @@ void CallServer::put(float* dst, const float* src, size_t n) {
 }
 
 int CallServer::submit(CallReq& r, const CallSlot& sl) {
+    if (broken_) return fail(CRLOT_EHIP, "call server: disabled after a timed-out request");
     r.in_off = sl.in_off;
     r.out_off = sl.out_off;
     r.spec_off = sl.spec_off;

@@ -16,6 +16,7 @@ namespace crlot {
 // memory or pinned host memory; out / spec: pinned host memory) and offsets.
 struct CallSlot {
     uint64_t index = 0;  // 1-based request number: done >= index once it completed
+    uint64_t gen = 0;    // arena generation the views point into (CallServer::live)
     float* in = nullptr;
     float* out = nullptr;
     float* spec = nullptr;
@@ -53,6 +54,9 @@ class CallServer {
     // state was written by kernels on other streams since the last request)
     void acquire_next() { acquire_next_ = true; }
     uint64_t submitted() const { return q_; }
+    // the slot's views still point into the current arenas (grow() reallocates
+    // them: a speculation recorded before a grow is gone)
+    bool live(const CallSlot& s) const { return s.gen == gen_ && gen_ != 0; }
     uint64_t done() const { return __atomic_load_n(&hctl_->done, __ATOMIC_ACQUIRE); }
     int device() const { return device_; }
     const CallHostCtl* host_ctl() const { return hctl_; }  // diagnostics (phase stamps)
@@ -84,6 +88,8 @@ class CallServer {
     float* out_ = nullptr;
     size_t in_cap_ = 0, out_cap_ = 0, spec_cap_ = 0;
     uint64_t q_ = 0;                   // requests submitted
+    uint64_t gen_ = 0;                 // arena generation (bumped by every allocation)
+    bool broken_ = false;              // a request timed out: the server refuses new work
     std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
     uint64_t last_chain_ = 0;          // the last request with a chained produce
     CallReq::Pend pend_{};             // deferred ring work (flags 0: none)

@@ -256,6 +256,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
 
     uint64_t my = a.first;
     uint64_t t_last = wall_clock64();
+    uint64_t chain_req = 0;  // the chained forward (1-based) whose kept frame this launch holds in LDS
     for (;;) {
         // ---- wait for request `my` (thread 0 polls device memory, the workgroup follows)
         if (t == 0) {
@@ -312,10 +313,15 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             if constexpr (CallLds<E>::CH > 0 || ANY) {
                 if (r.pend.flags & kPendCommit) {
                     const float* wobj = r.pend.win;
+                    // the LDS copy only survives within the launch that kept it (the
+                    // kernel may have idled out and been relaunched since); else the
+                    // same bits from the forward's speculation slot in host memory
+                    const bool lds = chain_req != 0 && chain_req == r.pend.src_index;
+                    const float* hsrc = a.out_arena + r.pend.src_off;
                     for (int64_t j = t; j < r.pend.len; j += kCallBlock) {
                         int64_t p = r.pend.start + j;
                         if (p >= R) p -= R;
-                        const float s = chainp[j];
+                        const float s = lds ? chainp[j] : ld_sys32(hsrc + j);
                         ring[p] = wobj ? __builtin_fmaf(__builtin_fmaf(s, wobj[j], 0.0f), r.pend.gain, ring[p])
                                        : __builtin_fmaf(s, r.pend.gain, ring[p]);
                     }
@@ -696,6 +702,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                     }
                 }
                 if (chain) {
+                    chain_req = my;
                     // publish the inverse first: the host's inverse call waits for it
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                     __syncthreads();

@@ -278,7 +278,12 @@ struct alignas(512) CallReq {
         const float* win;   // commit: the object's window or null
         int64_t R, start, len;  // commit: ring position and length
         int64_t rp, n;          // clear: ring position and length (mono)
-        uint64_t pad[2];
+        // commit: the chained forward that kept the frame (1-based request
+        // number) and the frame's copy in out_arena (its speculated inverse,
+        // floats from out_arena): a kernel launched after that forward has lost
+        // the LDS copy and reads this one
+        uint64_t src_index;
+        int64_t src_off;
     } pend;
     uint64_t pad2[22];
 };

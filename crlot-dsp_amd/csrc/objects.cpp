@@ -408,7 +408,7 @@ int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, i
     const int64_t N = o->N();
     // learn the association: this object pushes the frames the server speculates
     if (sh->target.owner != o && sh->fft.index + 4 > sv->submitted() && start_off == 0 && eff == N &&
-        sh->fft.slot.spec && std::memcmp(frame, sh->fft.slot.spec, sizeof(float) * size_t(N)) == 0) {
+        sh->fft.slot.spec && sv->live(sh->fft.slot) && std::memcmp(frame, sh->fft.slot.spec, sizeof(float) * size_t(N)) == 0) {
         sh->target.owner = o;
         sh->target.predict = ola_predict;
         return 0;
@@ -417,7 +417,7 @@ int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, i
     const float* want_win = (uw && !caller_win) ? o->d_win : nullptr;
     if (!(sh->chain.valid && sh->chain.index == sv->submitted() && sh->target.owner == o && start_off == 0 &&
           eff == N && start_sample == pd.start && gain == pd.gain && !caller_win && want_win == pd.win &&
-          pd.rp == o->read_pos && std::memcmp(frame, sh->chain.slot.spec, sizeof(float) * size_t(N)) == 0))
+          pd.rp == o->read_pos && sv->live(sh->chain.slot) && std::memcmp(frame, sh->chain.slot.spec, sizeof(float) * size_t(N)) == 0))
         return 0;
     sh->chain.valid = false;
     // the push itself rides on the next request (the server keeps the frame in LDS)
@@ -429,6 +429,8 @@ int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, i
     pe.start = start_sample % o->R;
     pe.len = N;
     pe.gain = gain;
+    pe.src_index = sh->chain.index;
+    pe.src_off = sh->chain.slot.spec_off;  // the speculated inverse = the frame pushed
     int rc = sv->defer(pe);
     if (rc != CRLOT_OK) return rc;
     o->spec.valid = true;
@@ -684,7 +686,7 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
     crlot::CallServer* sv = o->srv;
     const int64_t C = o->C();
     const bool hit = o->spec.valid && o->spec.index == sv->submitted() && o->spec.rp == o->read_pos &&
-                     o->spec.n == len;
+                     o->spec.n == len && sv->live(o->spec.slot);
     o->spec.valid = false;
     if (!hit && (rc = sv->grow(size_t(C * o->N() + o->N()), size_t(C * len), size_t(C * len))) != CRLOT_OK)
         return rc;

@@ -15,6 +15,7 @@ std::mutex g_mu;
 std::map<int, std::vector<hipStream_t>> g_streams;          // free streams per device
 std::map<size_t, std::vector<void*>> g_pinned;              // free pinned blocks per size class
 bool g_pool_set[64] = {};
+hipMemPool_t g_pool[64] = {};
 
 size_t size_class(size_t bytes) {
     size_t c = 256;
@@ -83,20 +84,36 @@ bool no_pool() {
     return v;
 }
 
+// Stream-ordered device memory from a pool private to this library (one per
+// device), so frees stay cached for the next object's allocation without
+// changing the process-wide default pool's release policy.  The pool keeps up
+// to kKeepBytes of freed memory; beyond that it returns memory to the device at
+// the next synchronisation.  Devices where the pool cannot be created fall back
+// to the default pool, untouched.
+constexpr uint64_t kKeepBytes = uint64_t(256) << 20;
+
 hipError_t pool_malloc(int device, void** out, size_t bytes, hipStream_t s) {
     if (no_pool()) return hipMalloc(out, bytes);
+    hipMemPool_t mp = nullptr;
     if (device >= 0 && device < 64) {
         std::lock_guard<std::mutex> lk(g_mu);
         if (!g_pool_set[device]) {
-            hipMemPool_t mp = nullptr;
-            if (hipDeviceGetDefaultMemPool(&mp, device) == hipSuccess && mp) {
-                uint64_t keep = UINT64_MAX;
-                (void)hipMemPoolSetAttribute(mp, hipMemPoolAttrReleaseThreshold, &keep);
+            hipMemPoolProps props{};
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = device;
+            if (hipMemPoolCreate(&g_pool[device], &props) == hipSuccess && g_pool[device]) {
+                uint64_t keep = kKeepBytes;
+                (void)hipMemPoolSetAttribute(g_pool[device], hipMemPoolAttrReleaseThreshold, &keep);
+            } else {
+                g_pool[device] = nullptr;
             }
             g_pool_set[device] = true;
         }
+        mp = g_pool[device];
     }
-    return hipMallocAsync(out, bytes, s);
+    return mp ? hipMallocFromPoolAsync(out, bytes, mp, s) : hipMallocAsync(out, bytes, s);
 }
 
 void pool_free(void* p, hipStream_t s) {

@@ -390,3 +390,77 @@ def test_objects_constructed_in_a_loop_reuse_pooled_resources(pkg, oracle, torch
         ola.close()
         fft.close()
         fq.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h", [(1024, 256), (960, 240)])
+def test_chained_push_survives_call_server_idle_exit(pkg, oracle, torch_cuda, n, h):
+    """The chained push rides on the next request (the call kernel kept the frame
+    in LDS).  The call kernel exits after 20 ms without a request; a real-time
+    48 kHz stream waits a whole hop (21 ms at 1024) between frames, so the commit
+    often runs in a relaunched kernel whose LDS no longer holds the frame.  It must
+    then read the frame's copy from the speculation slot: with pauses longer than
+    the idle timeout at every point of the rhythm, every produce is bit-identical
+    to the oracle's OLAAccumulator."""
+    import time
+    rng = np.random.default_rng(77)
+    w = oracle.window(oracle.HANN, n)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                        apply_window_inside=True)
+    ola = pkg.OLAAccumulator(cfg)
+    ola.set_window(w)
+    ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ref.set_window(w)
+    for k in range(24):
+        x = (rng.standard_normal(n) * w).astype(np.float32)
+        spec = fft.forward_host(x[None])
+        if k % 4 == 1:
+            time.sleep(0.03)
+        y = fft.inverse_host(spec)[0]
+        if k % 4 == 2:
+            time.sleep(0.03)
+        ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+        ref.push_frame_aos(y, k * h, 0, n, 1.0)
+        if k % 4 == 3:
+            time.sleep(0.03)
+        got, chans = ola.produce(h)
+        want = ref.produce(h)
+        assert got == len(want[0]), k
+        assert np.array_equal(bits(chans[0][:got]), bits(want[0])), k
+        if k % 2 == 0:
+            time.sleep(0.03)  # the commit of this frame runs after an idle exit
+    assert ola.produced_samples() == ref.produced
+
+
+@pytest.mark.gpu
+def test_speculation_dropped_when_shared_server_grows(pkg, oracle, torch_cuda):
+    """A wide OLA object of the same frame size grows the shared call server
+    (reallocating its arenas) between a forward and the push of its inverse: the
+    speculation recorded before the growth points into freed memory and must not
+    be used; the narrow object's output stays bit-identical to the oracle."""
+    n, h = 1024, 256
+    rng = np.random.default_rng(78)
+    w = oracle.window(oracle.HANN, n)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    mk = lambda c: pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=c, eps=1e-8,
+                                 apply_window_inside=True)
+    ola = pkg.OLAAccumulator(mk(1))
+    ola.set_window(w)
+    ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ref.set_window(w)
+    for k in range(12):
+        x = (rng.standard_normal(n) * w).astype(np.float32)
+        y = fft.inverse_host(fft.forward_host(x[None]))[0]
+        if k in (3, 7):
+            c = 24 + 8 * k  # wider than any object before: the server grows
+            wide = pkg.OLAAccumulator(mk(c))
+            wide.set_window(w)
+            wide.push_frame_AoS(rng.standard_normal(n * c).astype(np.float32), None, 0, 0, n, 1.0)
+            wide.produce(h)
+            wide.close()
+        ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+        ref.push_frame_aos(y, k * h, 0, n, 1.0)
+        got, chans = ola.produce(h)
+        want = ref.produce(h)
+        assert np.array_equal(bits(chans[0][:got]), bits(want[0])), k
