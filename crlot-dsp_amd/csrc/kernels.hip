@@ -2502,6 +2502,11 @@ hipError_t launch_fused_any(const Geometry& g, const DevTables& t, const float* 
     const int nb = (g.n + g.h - 1) / g.h;
     const int resident = fused_resident_waves() / 16 * per_cu * w;  // CUs x walkers per CU
     choose_chunks(F, n_streams, nb, resident, f.n_chunks, f.M);
+    if (const int64_t c = chunks_or(0, F); c > 0) {  // the plan's chunk knob
+        f.M = int((F + c - 1) / c);
+        f.n_chunks = int((F + f.M - 1) / f.M);
+    }
+    if (!mask) note_chunks(f.n_chunks);  // (a redo walk keeps the pair walker's record)
     const size_t lds = tables + size_t(w) * per_wave;
     const int64_t waves = int64_t(n_streams) * f.n_chunks;
     const int64_t grid = (waves + w - 1) / w;

@@ -704,6 +704,18 @@ static void ring_split(size_t cap, size_t start, size_t len, size_t* s1, size_t*
     }
 }
 
+/* exported for the pins against the reference's compiled ring_buffer.cc */
+void or_ring_split(size_t cap, size_t start, size_t len, size_t* s1, size_t* l1, size_t* l2) {
+    ring_split(cap, start, len, s1, l1, l2);
+}
+
+/* ola::deinterleave_to_scratch (aos_to_soa.cc:7-18): [i][ch] -> [ch][i] */
+void or_deinterleave(const float* x, size_t n, size_t channels, float* scratch) {
+    if (!x || !scratch || n == 0 || channels == 0) return;
+    for (size_t ch = 0; ch < channels; ++ch)
+        for (size_t i = 0; i < n; ++i) scratch[ch * n + i] = x[i * channels + ch];
+}
+
 /* OLAAccumulator::add_frame_SoA (OLAAccumulator.cc:54-122) */
 void or_ola_add_frame_soa(or_ola* o, const float* const* ch, const float* window,
                           size_t start_sample, size_t start_off, size_t size, float gain) {
@@ -740,9 +752,7 @@ void or_ola_push_frame_aos(or_ola* o, const float* x, const float* window, size_
     if (start_off >= o->n) return;
     size_t eff = size;
     if (start_off + size > o->n) eff = o->n - start_off;
-    const float* src = x + start_off * o->c;
-    for (size_t ch = 0; ch < o->c; ++ch)
-        for (size_t i = 0; i < eff; ++i) o->scratch[ch * eff + i] = src[i * o->c + ch];
+    or_deinterleave(x + start_off * o->c, eff, o->c, o->scratch);
     const float* ptrs[64] = {0};
     const float** chp = o->c <= 64 ? ptrs : (const float**)malloc(sizeof(float*) * o->c);
     for (size_t ch = 0; ch < o->c; ++ch) chp[ch] = o->scratch + ch * eff;

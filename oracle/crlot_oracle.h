@@ -83,6 +83,10 @@ void or_adapter_inverse_complex(or_kfft_cfg* inv, int nfft, const float* in, flo
 void or_axpy(float* dst, const float* src, float g, size_t n);
 void or_axpy_windowed(float* dst, const float* src, const float* win, float g, size_t n);
 void or_normalize_and_clear(float* out, float* acc, const float* norm, float eps, size_t n);
+/* RingBuffer::split (ring_buffer.cc:44-85): first span [s1, s1+l1), second [0, l2) */
+void or_ring_split(size_t cap, size_t start, size_t len, size_t* s1, size_t* l1, size_t* l2);
+/* ola::deinterleave_to_scratch (aos_to_soa.cc:7-18) */
+void or_deinterleave(const float* x, size_t n, size_t channels, float* scratch);
 void or_bench_kernel(int op, size_t n, int64_t reps, float* dst, const float* src, const float* win,
                      float* out);
 

@@ -57,6 +57,10 @@ def lib(native: bool = False):
     L.or_axpy_windowed.restype = None
     L.or_normalize_and_clear.argtypes = [_f32p, _f32p, _f32p, C.c_float, sz]
     L.or_normalize_and_clear.restype = None
+    L.or_ring_split.argtypes = [sz, sz, sz, C.POINTER(sz), C.POINTER(sz), C.POINTER(sz)]
+    L.or_ring_split.restype = None
+    L.or_deinterleave.argtypes = [_f32p, sz, sz, _f32p]
+    L.or_deinterleave.restype = None
     L.or_framer_new.argtypes = [sz, sz, sz, C.c_int]
     L.or_framer_new.restype = C.c_void_p
     L.or_framer_free.argtypes = [C.c_void_p]
@@ -391,6 +395,22 @@ def bench_kernel(op, n, reps, native=False):
     t0 = time.perf_counter()
     L.or_bench_kernel(op, n, reps, d, s, w, o)
     return (time.perf_counter() - t0) / reps
+
+
+def ring_split(cap, start, length):
+    """RingBuffer::split (ring_buffer.cc:44-85) -> (first start, first len, second len)."""
+    s1, l1, l2 = C.c_size_t(), C.c_size_t(), C.c_size_t()
+    lib().or_ring_split(cap, start, length, C.byref(s1), C.byref(l1), C.byref(l2))
+    return s1.value, l1.value, l2.value
+
+
+def deinterleave(x, n, channels):
+    """ola::deinterleave_to_scratch (aos_to_soa.cc:7-18): n frames of `channels`
+    interleaved floats -> channel-major scratch."""
+    a = np.ascontiguousarray(x, np.float32)
+    out = np.zeros(n * channels, np.float32)
+    lib().or_deinterleave(a, n, channels, out)
+    return out
 
 
 def normalize_and_clear(acc, norm, eps):

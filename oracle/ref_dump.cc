@@ -2,7 +2,10 @@
 //
 // TEST INFRASTRUCTURE ONLY.  Built by oracle/Makefile (target `ref`) from
 // /root/reference/dsp/window/WindowLUT.cc, dsp/ola/norm_builder.cc,
-// dsp/frame/framer.cc and dsp/frame/FrameQueue.cc compiled unchanged with the reference's release flags
+// dsp/frame/framer.cc, dsp/frame/FrameQueue.cc, dsp/ola/kernels.cc (its scalar
+// kernels; the Highway dispatchers are dropped by --gc-sections, nothing stands
+// in for them), dsp/ring/ring_buffer.cc, dsp/ola/aos_to_soa.cc and
+// dsp/base/aligned_alloc.cc compiled unchanged with the reference's release flags
 // (-std=c++17 -O3 -DNDEBUG -march=native, scripts/run_all.sh:12).  No stand-in
 // headers or libraries are involved: those translation units need only
 // the C++ standard library.  Output goes to a directory of raw little-endian
@@ -15,9 +18,14 @@
 #include <string>
 #include <vector>
 
+#include <random>
+
 #include "dsp/frame/FrameQueue.h"
 #include "dsp/frame/framer.h"
+#include "dsp/ola/aos_to_soa.h"
+#include "dsp/ola/kernels.h"
 #include "dsp/ola/norm_builder.h"
+#include "dsp/ring/ring_buffer.h"
 #include "dsp/window/WindowLUT.h"
 
 static std::string g_dir;
@@ -174,6 +182,76 @@ static void framequeues() {
     }
 }
 
+// The OLA stage's arithmetic (kernels.cc:18-36 scalar kernels, the ones
+// kernels_test.cc pins the Highway versions to within 1 ULP), RingBuffer::split
+// (ring_buffer.cc:44-85) and deinterleave_to_scratch (aos_to_soa.cc:7-18) on
+// seeded data: inputs and outputs, so the oracle's restatements are pinned bit
+// for bit to the reference's own compiled code.
+static void ola_primitives() {
+    std::mt19937 rng(42);  // kernels_test.cc:219
+    std::uniform_real_distribution<float> u(-10.0f, 10.0f);
+    const size_t sizes[] = {0, 1, 7, 16, 255, 1024, 4097};
+    const float gains[] = {1.0f, 0.5f, -1.25f, 3.0e-5f};
+    for (size_t n : sizes)
+        for (int gi = 0; gi < 4; ++gi) {
+            std::vector<float> dst(n), src(n), win(n);
+            for (size_t i = 0; i < n; ++i) dst[i] = u(rng), src[i] = u(rng), win[i] = u(rng) * 0.1f;
+            char name[96];
+            std::snprintf(name, sizeof name, "k_n%zu_g%d", n, gi);
+            dump_f32(std::string(name) + "_dst", dst.data(), n);
+            dump_f32(std::string(name) + "_src", src.data(), n);
+            dump_f32(std::string(name) + "_win", win.data(), n);
+            dump_f32(std::string(name) + "_gain", &gains[gi], 1);
+            std::vector<float> a = dst, w = dst;
+            dsp::axpy_scalar(a.data(), src.data(), gains[gi], n);
+            dsp::axpy_windowed_scalar(w.data(), src.data(), win.data(), gains[gi], n);
+            dump_f32(std::string(name) + "_axpy", a.data(), n);
+            dump_f32(std::string(name) + "_axpyw", w.data(), n);
+            // normalize_and_clear: norm around eps (both sides of the guard) and large
+            const float eps = gi == 3 ? 1e-8f : 1e-3f;
+            std::vector<float> acc = dst, norm(n), out(n);
+            for (size_t i = 0; i < n; ++i) {
+                const float r = std::fabs(u(rng));
+                norm[i] = (i % 3 == 0) ? eps * r * 0.1f : (i % 3 == 1 ? eps * (1.0f + r) : r);
+            }
+            dump_f32(std::string(name) + "_norm", norm.data(), n);
+            dump_f32(std::string(name) + "_eps", &eps, 1);
+            dsp::normalize_and_clear_scalar(out.data(), acc.data(), norm.data(), eps, n);
+            dump_f32(std::string(name) + "_out", out.data(), n);
+            dump_f32(std::string(name) + "_acc", acc.data(), n);
+        }
+    // RingBuffer::split spans, as (first offset, first len, second offset, second len)
+    const size_t caps[] = {1, 8, 100, 6144, 11264};
+    std::vector<uint64_t> rows;
+    for (size_t cap : caps) {
+        dsp::ring::RingBuffer<float> rb(cap);
+        const float* base = rb.split(0, 1).first.data();
+        const size_t starts[] = {0, 1, cap - 1, cap, cap + 3, 7 * cap + cap / 2, 123457};
+        const size_t lens[] = {0, 1, cap / 2, cap - 1, cap, cap + 1, 3 * cap};
+        for (size_t s : starts)
+            for (size_t l : lens) {
+                const auto sp = rb.split(s, l);
+                rows.push_back(cap), rows.push_back(s), rows.push_back(l);
+                rows.push_back(sp.first.size() ? uint64_t(sp.first.data() - base) : 0);
+                rows.push_back(sp.first.size());
+                rows.push_back(sp.second.size() ? uint64_t(sp.second.data() - base) : 0);
+                rows.push_back(sp.second.size());
+            }
+    }
+    dump_u64("ring_split_rows", rows);
+    // deinterleave_to_scratch
+    for (size_t c : {1, 2, 3, 5, 16}) {
+        const size_t n = 1000 + c;
+        std::vector<float> x(n * c), s(n * c, -1.0f);
+        for (float& v : x) v = u(rng);
+        dsp::ola::deinterleave_to_scratch(x.data(), n, c, s.data());
+        char name[64];
+        std::snprintf(name, sizeof name, "deint_c%zu", c);
+        dump_f32(std::string(name) + "_x", x.data(), x.size());
+        dump_f32(std::string(name) + "_s", s.data(), s.size());
+    }
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) {
         std::fprintf(stderr, "usage: ref_dump OUTDIR\n");
@@ -186,6 +264,7 @@ int main(int argc, char** argv) {
     norms();
     framers();
     framequeues();
+    ola_primitives();
     std::fclose(g_manifest);
     return 0;
 }

@@ -464,3 +464,40 @@ def test_speculation_dropped_when_shared_server_grows(pkg, oracle, torch_cuda):
         got, chans = ola.produce(h)
         want = ref.produce(h)
         assert np.array_equal(bits(chans[0][:got]), bits(want[0])), k
+
+
+@pytest.mark.gpu
+def test_device_kernels_bit_exact_vs_reference_build(pkg, torch_cuda, ref_tables):
+    """The batched device forms and the host-pointer forms of dsp::axpy /
+    axpy_windowed / normalize_and_clear against the outputs of the reference's
+    own kernels.cc scalar kernels compiled here (ref_tables.npz k_* fixtures):
+    bit for bit, where kernels_test.cc:214-429 allows the Highway versions 1 ULP."""
+    import re
+    torch = torch_cuda
+    n_checked = 0
+    for key in ref_tables.files:
+        m = re.match(r"(k_n(\d+)_g\d)_dst$", key)
+        if not m or int(m[2]) == 0:
+            continue
+        k = m[1]
+        dst, src, win, norm = (ref_tables[f"{k}_{s}"] for s in ("dst", "src", "win", "norm"))
+        g = float(ref_tables[f"{k}_gain"][0])
+        eps = float(ref_tables[f"{k}_eps"][0])
+        d = dev(torch, dst)
+        pkg.axpy(d, dev(torch, src), g)
+        assert np.array_equal(bits(host(d)), bits(ref_tables[f"{k}_axpy"])), k
+        d = dev(torch, dst)
+        pkg.axpy(d, dev(torch, src), g, dev(torch, win))
+        assert np.array_equal(bits(host(d)), bits(ref_tables[f"{k}_axpyw"])), k
+        acc, out = dev(torch, dst), torch.empty(dst.size, dtype=torch.float32, device="cuda")
+        pkg.normalize_and_clear(out, acc, dev(torch, norm), eps)
+        assert np.array_equal(bits(host(out)), bits(ref_tables[f"{k}_out"])), k
+        assert np.array_equal(bits(host(acc)), bits(ref_tables[f"{k}_acc"])), k
+        h = dst.copy()
+        pkg.axpy_host(h, src, g, win)
+        assert np.array_equal(bits(h), bits(ref_tables[f"{k}_axpyw"])), k
+        ha, ho = dst.copy(), np.empty_like(dst)
+        pkg.normalize_and_clear_host(ho, ha, norm, eps)
+        assert np.array_equal(bits(ho), bits(ref_tables[f"{k}_out"])), k
+        n_checked += 1
+    assert n_checked == 24

@@ -1,7 +1,9 @@
 """Pin the oracle (CPU restatement) before trusting it.
 
 1. bit-exact against the reference's own compiled WindowLUT.cc / norm_builder.cc /
-   framer.cc outputs (tests/golden/ref_tables.npz, via oracle/_ref/ref_dump);
+   framer.cc / FrameQueue.cc outputs and its OLA primitives -- the scalar kernels
+   of kernels.cc, RingBuffer::split (ring_buffer.cc) and deinterleave_to_scratch
+   (aos_to_soa.cc) -- (tests/golden/ref_tables.npz, via oracle/_ref/ref_dump);
 2. kissfft restatement bit-exact against an independent kissfft build
    (tests/golden/kiss_gst.npz);
 3. the reference's own known-answer tests, re-expressed:
@@ -122,6 +124,50 @@ def test_framequeue_bit_exact_vs_reference(oracle, ref_tables):
         assert np.array_equal(got.reshape(-1), ref_tables[base + "_frames"]), base
         n += 1
     assert n == 48
+
+
+def test_ola_kernels_bit_exact_vs_reference(oracle, ref_tables):
+    """axpy_scalar / axpy_windowed_scalar / normalize_and_clear_scalar
+    (kernels.cc:18-36), compiled from the reference unchanged, against the
+    oracle's or_axpy / or_axpy_windowed / or_normalize_and_clear on the same
+    seeded data (mt19937(42) U(-10, 10) as kernels_test.cc:219; norms on both
+    sides of the eps guard)."""
+    n_checked = 0
+    for key in ref_tables.files:
+        m = re.match(r"(k_n\d+_g\d)_dst$", key)
+        if not m:
+            continue
+        k = m[1]
+        dst, src, win = (ref_tables[f"{k}_{s}"] for s in ("dst", "src", "win"))
+        g = float(ref_tables[f"{k}_gain"][0])
+        assert np.array_equal(bits(oracle.axpy(dst, src, g)), bits(ref_tables[f"{k}_axpy"])), k
+        assert np.array_equal(bits(oracle.axpy(dst, src, g, win)), bits(ref_tables[f"{k}_axpyw"])), k
+        out, acc = oracle.normalize_and_clear(dst, ref_tables[f"{k}_norm"], float(ref_tables[f"{k}_eps"][0]))
+        assert np.array_equal(bits(out), bits(ref_tables[f"{k}_out"])), k
+        assert np.array_equal(bits(acc), bits(ref_tables[f"{k}_acc"])), k
+        n_checked += 1
+    assert n_checked == 28
+
+
+def test_ring_split_vs_reference(oracle, ref_tables):
+    """RingBuffer::split (ring_buffer.cc:44-85): start mod capacity, length
+    clamped to the capacity, at most two spans -- the oracle's ring_split, which
+    its add_frame_SoA / produce use, gives the same spans for every case."""
+    rows = ref_tables["ring_split_rows"].reshape(-1, 7).astype(np.int64)
+    assert len(rows) == 5 * 7 * 7
+    for cap, start, length, o1, l1, o2, l2 in rows:
+        s1, m1, m2 = oracle.ring_split(int(cap), int(start), int(length))
+        assert (m1, m2) == (l1, l2), (cap, start, length)
+        if l1:
+            assert s1 == o1, (cap, start, length)
+        assert o2 == 0  # the second span always starts at the ring's origin
+
+
+def test_deinterleave_vs_reference(oracle, ref_tables):
+    """deinterleave_to_scratch (aos_to_soa.cc:7-18), push_frame_AoS's first step."""
+    for c in (1, 2, 3, 5, 16):
+        x = ref_tables[f"deint_c{c}_x"]
+        assert np.array_equal(bits(oracle.deinterleave(x, x.size // c, c)), bits(ref_tables[f"deint_c{c}_s"])), c
 
 
 def test_reflect101_is_the_reference_mixed_rule(oracle):
