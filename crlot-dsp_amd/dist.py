@@ -13,10 +13,13 @@ external launcher.  The parent never touches the GPU.
 """
 from __future__ import annotations
 
+import datetime
 import os
+import signal
 import socket
 import subprocess
 import sys
+import time
 
 _backend = None
 
@@ -40,15 +43,54 @@ def init_kwargs(backend: str, device=None) -> dict:
     return {"device_id": device} if (backend == "nccl" and device is not None) else {}
 
 
-def init(backend: str, device=None):
+INIT_TIMEOUT_S = 120.0
+
+
+def init(backend: str, device=None, timeout_s: float = INIT_TIMEOUT_S):
+    """Join the process group.  `timeout_s` bounds the rendezvous and every
+    collective: a rank that never arrives fails the others in bounded time
+    instead of leaving them blocked in RCCL."""
     global _backend
     import torch.distributed as dist
     rank, world, _ = env_rank_world()
     kw = init_kwargs(backend, device)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group(backend, **kw)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
     _backend = backend
     return rank, world
+
+
+def device_key(device=None) -> int:
+    """An id of the physical device a rank runs on (PCI domain / bus / device
+    when torch reports them, else the ordinal), so ranks can count distinct GPUs."""
+    if device is None:
+        return -1
+    import torch
+    try:
+        p = torch.cuda.get_device_properties(device)
+        dom, bus, dv = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+        if bus is not None:
+            return (int(dom or 0) << 16) | (int(bus) << 8) | int(dv or 0)
+    except Exception:  # noqa: BLE001 -- an id is a report, never fatal
+        pass
+    return int(getattr(device, "index", device) or 0)
+
+
+def observed_world(device=None) -> dict:
+    """What the process group really holds, seen from every rank: the backend,
+    the world size the group reports and the distinct devices its ranks run on
+    (an all-gather of device_key over the group)."""
+    import torch
+    import torch.distributed as dist
+    key = device_key(device)
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return {"backend": _backend or "none", "world": 1, "devices": 1 if key >= 0 else 0, "device_keys": [key]}
+    world = dist.get_world_size()
+    t = torch.tensor([key], dtype=torch.int64, device=reduce_device(device))
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    keys = [int(v.item()) for v in out]
+    return {"backend": dist.get_backend(), "world": world, "devices": len(set(keys)), "device_keys": keys}
 
 
 def stream_range(total_streams: int, world: int, rank: int):
@@ -94,26 +136,46 @@ def free_port() -> int:
     return port
 
 
-def launch(n: int, argv: list[str], timeout: float | None = None) -> int:
-    """Run `python argv...` as n ranks on this node; returns the worst exit code.
+def _stop(procs, grace: float = 5.0):
+    """SIGTERM every live child, SIGKILL what is still alive after `grace` s."""
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    t_end = time.monotonic() + grace
+    for p in procs:
+        while p.poll() is None and time.monotonic() < t_end:
+            time.sleep(0.05)
+        if p.poll() is None:
+            p.kill()
+            p.wait()
 
+
+def launch(n: int, argv: list[str], timeout: float | None = None, poll_s: float = 0.1) -> int:
+    """Run `python argv...` as n ranks on this node; returns 0 when every rank
+    succeeded, else the exit code of the first rank that failed.
+
+    All children are polled together: the first non-zero exit stops the other
+    ranks at once (they would otherwise wait in a collective for the dead rank),
+    and `timeout` (seconds, None: no limit) stops the whole job with 124.
     Children are fresh processes started before anything in this process has
     touched the GPU (no exec from a GPU-initialised process)."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()),
                WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
     procs = []
-    for r in range(n):
-        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable] + argv, env=e))
-    rc = 0
+    t0 = time.monotonic()
     try:
-        for p in procs:
-            code = p.wait(timeout=timeout)
-            if code != 0 and rc == 0:
-                rc = code
+        for r in range(n):
+            e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen([sys.executable] + argv, env=e))
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                return bad[0]
+            if all(c == 0 for c in codes):
+                return 0
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                return 124
+            time.sleep(poll_s)
     finally:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-                p.wait()
-    return rc
+        _stop(procs)

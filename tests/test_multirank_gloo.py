@@ -111,7 +111,8 @@ def test_nccl_init_arguments_and_reduce_device(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "8")
     monkeypatch.setenv("RANK", "5")
     assert D.init("nccl", dev) == (5, 8)
-    assert calls == [("nccl", {"device_id": dev})]
+    import datetime
+    assert calls == [("nccl", {"device_id": dev, "timeout": datetime.timedelta(seconds=D.INIT_TIMEOUT_S)})]
     assert D.reduce_device(dev) == dev and D.reduce_device(None) == "cpu"
     D.init("gloo", dev)  # already initialised: no second group
     assert len(calls) == 1 and D.reduce_device(dev) == "cpu"
@@ -121,3 +122,71 @@ def test_nccl_init_arguments_and_reduce_device(monkeypatch):
     monkeypatch.setattr(dist, "all_reduce", lambda t, op=None: seen.append((t.device.type, op)))
     assert D.max_over_ranks(1.5, None) == 1.5
     assert seen == [("cpu", dist.ReduceOp.MAX)]
+
+
+FAILER = r'''
+import os, sys, time
+import importlib.util
+spec = importlib.util.spec_from_file_location("crlot_dist", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+D = importlib.util.module_from_spec(spec); spec.loader.exec_module(D)
+rank, world = D.init("gloo", timeout_s=600)
+if rank == 1:
+    sys.exit(3)  # dies before the barrier
+D.barrier()      # rank 0 would wait here for the dead rank
+obs = D.observed_world()
+D.finalize()
+'''
+
+OBSERVER = r'''
+import os, sys, json
+import importlib.util
+spec = importlib.util.spec_from_file_location("crlot_dist", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+D = importlib.util.module_from_spec(spec); spec.loader.exec_module(D)
+rank, world = D.init("gloo")
+obs = D.observed_world(rank % 2)   # stand-in device ordinals: two distinct "devices"
+json.dump(obs, open(os.path.join(OUT, f"obs_{rank}.json"), "w"))
+D.finalize()
+'''
+
+
+def _load_dist():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("crlot_dist_t", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+    D = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(D)
+    return D
+
+
+def test_launch_fails_fast_when_a_rank_dies(tmp_path):
+    """dist.launch polls every rank: rank 1 exiting with 3 before the barrier
+    stops rank 0 (blocked in the barrier) and the launcher returns 3 within
+    seconds, not after the collective timeout."""
+    import time
+    D = _load_dist()
+    script = tmp_path / "failer.py"
+    script.write_text(f"ROOT = {ROOT!r}\n" + FAILER)
+    t0 = time.monotonic()
+    rc = D.launch(2, [str(script)], timeout=120)
+    dt = time.monotonic() - t0
+    assert rc == 3 and dt < 10, (rc, dt)
+
+
+def test_launch_timeout_returns_124(tmp_path):
+    D = _load_dist()
+    script = tmp_path / "sleeper.py"
+    script.write_text("import time\ntime.sleep(60)\n")
+    assert D.launch(2, [str(script)], timeout=1.0) == 124
+
+
+def test_observed_world_counts_ranks_and_devices(tmp_path):
+    """observed_world all-gathers each rank's device id: the bench line's record
+    of what the process group really held (world size, distinct devices)."""
+    import json
+    D = _load_dist()
+    script = tmp_path / "obs.py"
+    script.write_text(f"ROOT = {ROOT!r}\nOUT = {str(tmp_path)!r}\n" + OBSERVER)
+    assert D.launch(2, [str(script)], timeout=120) == 0
+    for r in range(2):
+        o = json.load(open(tmp_path / f"obs_{r}.json"))
+        assert o["world"] == 2 and o["backend"] == "gloo" and o["devices"] == 2, o
+        assert o["device_keys"] == [0, 1], o
