@@ -85,8 +85,12 @@ def cpu_share() -> int:
     return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
 
 
-def cpu_baseline(n_streams: int = 1024):
-    """Oracle restatement of the reference CPU path on this host (kind "port")."""
+CPU_REPS = 5  # timed repetitions after one warm-up, median reported (BASELINE.md:51)
+
+
+def cpu_baseline(n_streams: int = 1024, reps: int = CPU_REPS):
+    """Oracle restatement of the reference CPU path on this host (kind "port"):
+    one untimed warm-up pass, then `reps` timed passes, median (BASELINE.md:51)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     native = False
@@ -98,14 +102,18 @@ def cpu_baseline(n_streams: int = 1024):
         pass
     threads = cpu_share()
     x = O.synth_streams(n_streams, T_LEN, config_id=2)
-    O.roundtrip_batch(x[:threads], N_FFT, HOP, nthreads=threads, native=native)  # warm-up
-    t0 = time.perf_counter()
-    O.roundtrip_batch(x, N_FFT, HOP, nthreads=threads, native=native)
-    dt = time.perf_counter() - t0
-    x1 = x[:4]
-    t1 = time.perf_counter()
-    O.roundtrip_batch(x1, N_FFT, HOP, nthreads=1, native=native)
-    dt1 = time.perf_counter() - t1
+
+    def median_time(xs, nthreads):
+        O.roundtrip_batch(xs, N_FFT, HOP, nthreads=nthreads, native=native)  # warm-up
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            O.roundtrip_batch(xs, N_FFT, HOP, nthreads=nthreads, native=native)
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts)), ts
+
+    dt, ts = median_time(x, threads)
+    dt1, ts1 = median_time(x[:4], 1)
     single = 4 * T_LEN / dt1 / 1e6
     cpu_model = ""
     try:
@@ -124,8 +132,11 @@ def cpu_baseline(n_streams: int = 1024):
         "sample": f"{n_streams} of the 1024 streams x {T_LEN} samples (the N=1 workload) on "
                   f"{threads} pthreads (this host's CPU share: OMP_NUM_THREADS / affinity), "
                   f"oracle/crlot_oracle.c -O3{' -march=native' if native else ''} "
-                  f"(kissfft-algorithm + scalar-FMA OLA restatement), {dt:.2f} s; "
-                  f"single thread on 4 streams, {dt1:.2f} s",
+                  f"(kissfft-algorithm + scalar-FMA OLA restatement), 1 warm-up + {reps} timed "
+                  f"passes, median {dt:.2f} s; single thread on 4 streams, median {dt1:.3f} s",
+        "reps": reps,
+        "rep_seconds": [round(t, 4) for t in ts],
+        "single_thread_rep_seconds": [round(t, 4) for t in ts1],
         "single_thread_value": round(single, 3),
         "host_cpus": ncpu,
         "all_cpus_linear_bound": round(single * ncpu, 1),
@@ -575,6 +586,7 @@ def main():
     torch.cuda.set_device(dev)
     shared = local_world > n_dev
     rank, world = D.init("gloo" if shared else "nccl", dev)
+    observed = D.observed_world(dev)  # what the process group really holds (all ranks agree)
 
     pkg = load_pkg()
     plan = pkg.Plan(frame_size=N_FFT, hop_size=HOP, device=dev.index)
@@ -628,7 +640,7 @@ def main():
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": min(world, n_dev),   # distinct devices (ranks may share one on a 1-GPU box)
+            "n_gpus": observed["devices"],  # distinct devices (ranks may share one on a 1-GPU box)
             "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -674,6 +686,14 @@ def main():
                         "the same launches in SURVEY 8d flops",
             },
             "strong_scaling": strong,
+            "dist": {
+                "backend": observed["backend"],
+                "world_observed": observed["world"],
+                "devices_observed": observed["devices"],
+                "device_keys": observed["device_keys"],
+                "note": "all-gathered over the process group before the timed phases: the world "
+                        "size the group reports and the distinct devices (PCI ids) its ranks ran on",
+            },
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -627,6 +627,20 @@ int crlot_plan_set_frame_pairing(crlot_plan* p, int32_t enable) {
     return CRLOT_OK;
 }
 
+const char* crlot_device_target(void) {
+    thread_local std::string name;
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        name = "none";
+    } else {
+        name = prop.gcnArchName;
+        const size_t colon = name.find(':');  // "gfx950:sramecc+:xnack-" -> "gfx950"
+        if (colon != std::string::npos) name.resize(colon);
+    }
+    return name.c_str();
+}
+
 int crlot_plan_set_chunks(crlot_plan* p, int32_t chunks) {
     if (!p) return fail(CRLOT_EINVAL, "null plan");
     if (chunks < 0) return fail(CRLOT_EINVAL, "chunks per stream must be >= 0");

@@ -87,22 +87,11 @@ extern "C" int64_t crlot_ring_len(int64_t frame_size, int64_t hop) {
     return (min_overlaps + 20) * hop;
 }
 
-extern "C" int crlot_norm_table(const float* window, int64_t n, int64_t h, int64_t ring_len,
-                                int32_t apply_window_inside, float eps, float* out) {
-    if (n <= 0 || h <= 0 || ring_len <= 0 || out == nullptr) return CRLOT_EINVAL;
-    if (window == nullptr || !apply_window_inside) {
-        for (int64_t i = 0; i < ring_len; ++i) out[i] = 1.0f;
-        return CRLOT_OK;
-    }
-    if (h == n) {
-        for (int64_t i = 0; i < ring_len; ++i) {
-            const float w = window[i % n];
-            out[i] = w > eps ? w : eps;  // std::max(window_[i % N], eps)
-        }
-        return CRLOT_OK;
-    }
-    // build_norm_linear: frame starts k*H, k in [floor(-N/H), ceil((R+N-1)/H)],
-    // accumulated in ascending k, each start split into <= 2 ring spans.
+// norm_builder.cc:8-52 build_norm_linear: frame starts k*H, k in
+// [floor(-N/H), ceil((R+N-1)/H)], accumulated in ascending k, each start split
+// into <= 2 ring spans.
+extern "C" int crlot_build_norm_linear(float* out, const float* window, int64_t ring_len, int64_t n, int64_t h) {
+    if (n <= 0 || h <= 0 || ring_len <= 0 || out == nullptr || window == nullptr) return CRLOT_EINVAL;
     for (int64_t i = 0; i < ring_len; ++i) out[i] = 0.0f;
     const int64_t R = ring_len;
     const int64_t a = -n;
@@ -121,4 +110,21 @@ extern "C" int crlot_norm_table(const float* window, int64_t n, int64_t h, int64
         for (int64_t i = 0; i < second; ++i) out[i] += window[first + i];
     }
     return CRLOT_OK;
+}
+
+extern "C" int crlot_norm_table(const float* window, int64_t n, int64_t h, int64_t ring_len,
+                                int32_t apply_window_inside, float eps, float* out) {
+    if (n <= 0 || h <= 0 || ring_len <= 0 || out == nullptr) return CRLOT_EINVAL;
+    if (window == nullptr || !apply_window_inside) {
+        for (int64_t i = 0; i < ring_len; ++i) out[i] = 1.0f;
+        return CRLOT_OK;
+    }
+    if (h == n) {
+        for (int64_t i = 0; i < ring_len; ++i) {
+            const float w = window[i % n];
+            out[i] = w > eps ? w : eps;  // std::max(window_[i % N], eps)
+        }
+        return CRLOT_OK;
+    }
+    return crlot_build_norm_linear(out, window, ring_len, n, h);
 }

@@ -535,6 +535,12 @@ int crlot_window_table(int32_t type, int64_t n, int32_t periodic, int32_t norm, 
 int64_t crlot_ring_len(int64_t frame_size, int64_t hop);
 int crlot_norm_table(const float* window, int64_t frame_size, int64_t hop, int64_t ring_len,
                      int32_t apply_window_inside, float eps, float* out);
+/* dsp::ola::build_norm_linear (norm_builder.cc:8-52): the raw linear sum of the
+ * window over every frame start that reaches the ring (no eps, no H == N case) */
+int crlot_build_norm_linear(float* norm, const float* window, int64_t ring_len, int64_t frame_size, int64_t hop);
+/* The device the calling thread's HIP context uses, as an ISA name ("gfx950");
+ * the target of the dsp::get_current_target() drop-in */
+const char* crlot_device_target(void);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,6 @@
 // e2e_loop: the reference harness's pipeline (bench/e2e_benchmark.cc:42-76 set-up,
-// :138-186 loop) written against the drop-in classes of include/crlot_dsp.hpp
-// exactly as the harness writes it against dsp::*, in the streaming-interleaved
+// :138-186 loop) written against the reference's own headers (include/ref/dsp/...: the
+// drop-in classes of include/crlot_dsp.hpp under the names dsp::*), in the streaming-interleaved
 // order (push frame k, then produce(H)):
 //
 //   Framer::push(x, T) -> while pop(frame): p = frame * w -> IFftPlan::forward
@@ -21,10 +21,16 @@
 #include <string>
 #include <vector>
 
-#include "../../include/crlot_dsp.hpp"
+// The reference harness's own includes and using-directives (bench/e2e_benchmark.cc:8-15),
+// resolved by the drop-in headers under include/ref (-I include/ref): no source edit.
+#include "dsp/ola/OLAAccumulator.h"
+#include "dsp/window/WindowLUT.h"
+#include "dsp/frame/framer.h"
+#include "dsp/fft/api/fft_api.h"
+#include "io/wav.h"
 
-using namespace crlot::dsp;
-using namespace crlot::dsp::fft;
+using namespace dsp;
+using namespace dsp::fft;
 
 static std::vector<float> read_f32(const char* path, size_t n) {
     std::vector<float> v(n);

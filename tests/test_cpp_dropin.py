@@ -98,3 +98,19 @@ def test_e2e_loop_any_size_vs_oracle(tmp_path, torch_cuda, oracle, n, h):
     assert np.linalg.norm(y[0] - ref) <= 1e-6 * max(np.linalg.norm(ref), np.linalg.norm(x))
     assert np.max(np.abs(y[0] - ref)) <= 4e-6 * float(np.max(np.abs(x)))
     assert np.array_equal(y, oracle_ola(oracle, frames, n, h, 1))
+
+
+@pytest.mark.gpu
+def test_kernels_loop_reference_header(torch_cuda):
+    """tests/cpp/kernels_loop: kernels_benchmark.cc's scalar / "Highway" / default
+    triple and kernels_test.cc's 1-ULP bar, compiled against the reference's own
+    "dsp/ola/kernels.h" path (include/ref): the device kernels behind axpy_hwy and
+    axpy agree with the scalar kernels within 1 ULP (in fact bit for bit)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "kernels_loop")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "target gfx950" in r.stdout and r.stdout.strip().endswith("OK"), r.stdout
+    assert all(" ulp axpy 0 windowed 0 normalize 0 " in ln for ln in r.stdout.splitlines() if ln.startswith("n ")), \
+        r.stdout
