@@ -165,8 +165,25 @@ def load_pmc_traffic(workload_key: str):
     stale = best.get("src_hash") != cur
     meta = {"file": os.path.relpath(best_f, ROOT), "kernel": best.get("kernel"),
             "profile_src_hash": best.get("src_hash"), "src_hash": cur, "stale": stale,
-            "hbm_over_algorithmic": best.get("hbm_over_algorithmic")}
+            "hbm_over_algorithmic": best.get("hbm_over_algorithmic"),
+            "valu_issue": None if stale else best.get("valu_issue")}
     return (None if stale else best.get("hbm_bytes_per_launch")), meta
+
+
+def valu_block(fps, achieved_tf, issue, kern_ms):
+    """roofline.valu: the launches priced in SURVEY 8d flops against the FP32
+    vector peak, plus -- from the same kernel sources' PMC profile -- the VALU
+    busy fraction (instruction cycles per SIMD / kernel cycles) and the FP32
+    flops the hardware counted (SQ_INSTS_VALU_FLOPS_FP32) at this run's time."""
+    v = {"flop_per_sample": round(fps, 1), "achieved_tflops": round(achieved_tf, 2),
+         "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4)}
+    if issue:
+        v["busy_frac_pmc"] = None if issue.get("busy_frac") is None else round(issue["busy_frac"], 4)
+        if issue.get("fp32_flops_per_launch"):
+            tf = issue["fp32_flops_per_launch"] / (kern_ms * 1e-3) / 1e12
+            v["counted_fp32_tflops"] = round(tf, 2)
+            v["counted_frac"] = round(tf / VALU_PEAK_TFLOPS, 4)
+    return v
 
 
 RAMP_S = 0.25  # untimed clock ramp before the warm-up steps (reported as clock_ramp_steps)
@@ -675,12 +692,7 @@ def main():
                 "traffic_source": traffic_meta,
                 "kernel_ms": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": BYTES_PER_SAMPLE * samples_step_rank,
-                "valu": {
-                    "flop_per_sample": round(fps, 1),
-                    "achieved_tflops": round(achieved_tf, 2),
-                    "peak_tflops": VALU_PEAK_TFLOPS,
-                    "frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4),
-                },
+                "valu": valu_block(fps, achieved_tf, traffic_meta.get("valu_issue"), kern_ms),
                 "note": "frac is the metric's HBM-roofline fraction (8 B/sample); the kernel "
                         "is bound on the VALU issue (DESIGN.md section 5), valu.frac prices "
                         "the same launches in SURVEY 8d flops",

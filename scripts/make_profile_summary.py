@@ -89,6 +89,25 @@ def hbm_of(p):
 pmc = {}
 for sub in ("fetch", "write", "sq", "lds"):
     pmc.update(counters(sub, kname))
+valu_pass = counters("valu", kname)  # its own pass: SQ_INSTS_VALU / GRBM_GUI_ACTIVE again, same launches
+for k, v in valu_pass.items():
+    pmc.setdefault(k, v)
+
+
+def valu_issue(p, simds=1024, xcds=8, lanes=64):
+    """VALU busy fraction of the dominant kernel from the valu pass: VALU
+    instruction cycles per SIMD (SQ_THREAD_CYCLES_VALU is thread-cycles summed
+    over SIMDs; / 64 lanes for full waves) over the kernel's cycles
+    (GRBM_GUI_ACTIVE sums the 8 XCDs' clocks), and the FP32 flops actually
+    executed (SQ_INSTS_VALU_FLOPS_FP32) per launch."""
+    if not {"SQ_THREAD_CYCLES_VALU", "GRBM_GUI_ACTIVE"} <= set(p):
+        return None
+    kcyc = p["GRBM_GUI_ACTIVE"] / xcds
+    busy = p["SQ_THREAD_CYCLES_VALU"] / lanes / simds
+    out = {"valu_cycles_per_simd": busy, "kernel_cycles": kcyc, "busy_frac": busy / kcyc if kcyc else None}
+    if "SQ_INSTS_VALU_FLOPS_FP32" in p:
+        out["fp32_flops_per_launch"] = p["SQ_INSTS_VALU_FLOPS_FP32"]
+    return out
 S, T, N, H = 1024, 480000, 1024, 256
 alg_read = S * T * 4
 alg_write = S * T * 4
@@ -122,6 +141,7 @@ out = {
     "fetch_bytes_corrected": None if "FETCH_SIZE" not in pmc else 2 * pmc["FETCH_SIZE"] * 1024,
     "write_bytes": None if "WRITE_SIZE" not in pmc else pmc["WRITE_SIZE"] * 1024,
     "headline_grid": grid,
+    "valu_issue": valu_issue(valu_pass) if valu_pass else None,
     "aux_kernels": aux,
     "note": __doc__.strip(),
 }

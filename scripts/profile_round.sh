@@ -20,4 +20,5 @@ run fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --stats -d $OUT/fetch -o
 run write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --stats -d $OUT/write -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
 run sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY --kernel-trace --stats -d $OUT/sq -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
 run lds 300 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace --stats -d $OUT/lds -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
+run valu 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --stats -d $OUT/valu -o run --output-format csv -- python3 scripts/prof_driver.py --reps 3
 echo "== done"
