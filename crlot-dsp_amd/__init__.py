@@ -116,6 +116,8 @@ def lib():
         "crlot_plan_set_spectral_gain_async": ([vp, vp, vp], C.c_int),
         "crlot_plan_set_frame_pairing": ([vp, i32], C.c_int),
         "crlot_plan_set_chunks": ([vp, i32], C.c_int),
+        "crlot_set_call_speculation": ([i32], C.c_int),
+        "crlot_call_speculation_stats": ([C.POINTER(i64)], C.c_int),
         "crlot_plan_last_launch": ([vp, vp, C.POINTER(LaunchInfo)], C.c_int),
         "crlot_kernel_name": ([i32], C.c_char_p),
         "crlot_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
@@ -215,6 +217,19 @@ def lib():
         fn.restype = rest
     _lib = L
     return L
+
+
+def set_call_speculation(mode: int):
+    """1: per-call speculation of the call kernel only; 2 (default): the whole
+    per-frame drop-in loop batched on the device as well (crlot_set_call_speculation)."""
+    _check(lib().crlot_set_call_speculation(int(mode)), "crlot_set_call_speculation")
+
+
+def call_speculation_stats() -> dict:
+    """Process-wide counters of the batched speculation (crlot_call_speculation_stats)."""
+    v = (C.c_int64 * 6)()
+    _check(lib().crlot_call_speculation_stats(v), "crlot_call_speculation_stats")
+    return dict(zip(("batches", "forwards", "inverses", "pushes", "produces", "rebuilds"), list(v)))
 
 
 def kernel_name(kernel_id: int) -> str:

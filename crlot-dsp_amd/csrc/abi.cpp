@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "batch.h"
 #include "call.h"
 #include "crlot_dsp.h"
 #include "kernels.h"
@@ -1227,6 +1228,19 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     if (!sh) return rc;
     std::lock_guard<std::mutex> slk(sh->mu);
     crlot::CallServer* sv = sh->srv;
+    // the batched speculation of the whole per-frame loop (batch.h): contiguous
+    // single real frames only
+    if (kind < 2 && batch == 1 && inc_in == 1 && inc_out == 1 && crlot::spec_mode() >= 2) {
+        int brc = 0;
+        if (kind == 0) {
+            int irc = CRLOT_OK;
+            crlot_plan* inner = fft_inner(p, &irc);
+            brc = inner ? crlot::batch_forward(sh, inner, n, in, out) : 0;
+        } else {
+            brc = crlot::batch_inverse(sh, n, in, out);
+        }
+        if (brc != 0) return brc < 0 ? brc : CRLOT_OK;
+    }
     if (kind == 1 && sh->fft.valid && sh->fft.index == sv->submitted() && sh->fft.batch == batch &&
         sv->live(sh->fft.slot) && std::memcmp(p->pack.data(), sh->fft.slot.out, sizeof(float) * nin) == 0) {
         // the spectrum the last forward returned, unchanged: its inverse is in the speculation slot

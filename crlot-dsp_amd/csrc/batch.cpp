@@ -1,0 +1,258 @@
+// batch.cpp -- batched speculation of the per-frame drop-in loop (batch.h).
+#include "batch.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "call.h"
+#include "kernels.h"
+
+namespace crlot {
+int set_error(int code, const std::string& msg);  // abi.cpp
+}
+
+namespace crlot {
+namespace {
+
+int hip_fail(hipError_t e, const char* what) {
+    return set_error(CRLOT_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+std::atomic<int> g_mode{2};
+// crlot_call_speculation_stats: batches started, forwards / inverses / pushes /
+// produces served from a batch, OLA rings rebuilt
+std::atomic<int64_t> g_stats[6];
+
+std::mutex g_win_mu;
+std::vector<std::vector<float>> g_windows;  // newest first
+constexpr size_t kMaxWindows = 16;
+
+// grow-only device and pinned buffers
+hipError_t dgrow(float** p, size_t* cap, size_t need) {
+    if (*cap >= need) return hipSuccess;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, sizeof(float) * need);
+    if (e == hipSuccess) *cap = need;
+    return e;
+}
+hipError_t hgrow(float** p, size_t* cap, size_t need) {
+    if (*cap >= need) return hipSuccess;
+    if (*p) (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipHostMalloc(p, sizeof(float) * need, hipHostMallocDefault);
+    if (e == hipSuccess) *cap = need;
+    return e;
+}
+
+// the forward input of frame j, as the loop forms it on the host (frame * w)
+bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
+    const int64_t L = int64_t(b.sig.size()), base = j * b.h;
+    for (int64_t i = 0; i < b.n; ++i) {
+        const int64_t t = base + i;
+        const float v = (t < L ? b.sig[size_t(t)] : 0.0f) * b.win[size_t(i)];
+        if (std::memcmp(&v, in + i, sizeof(float)) != 0) return false;
+    }
+    return true;
+}
+
+// run frames 0 .. M-1 of the found chain: products, forward, inverse; results to pinned memory
+int run_chain(BatchSpec* b, crlot_plan* inner) {
+    const size_t L = b->sig.size(), N = size_t(b->n), M = size_t(b->M), row = N + 2;
+    hipError_t e;
+    if (!b->s && (e = hipStreamCreateWithFlags(&b->s, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(e, "batch stream");
+    if (!b->ev && (e = hipEventCreateWithFlags(&b->ev, hipEventDisableTiming)) != hipSuccess)
+        return hip_fail(e, "batch event");
+    if ((e = dgrow(&b->d_sig, &b->c_sig, L + N)) || (e = dgrow(&b->d_p, &b->c_p, M * N)) ||
+        (e = dgrow(&b->d_spec, &b->c_spec, M * row)) || (e = dgrow(&b->d_r, &b->c_r, M * N)) ||
+        (e = hgrow(&b->h_stage, &b->c_hs, L + N)) || (e = hgrow(&b->h_spec, &b->c_hspec, M * row)) ||
+        (e = hgrow(&b->h_r, &b->c_hr, M * N)))
+        return hip_fail(e, "batch buffers");
+    std::memcpy(b->h_stage, b->sig.data(), sizeof(float) * L);
+    std::memcpy(b->h_stage + L, b->win.data(), sizeof(float) * N);
+    if ((e = hipMemcpyAsync(b->d_sig, b->h_stage, sizeof(float) * (L + N), hipMemcpyHostToDevice, b->s)) ||
+        (e = launch_windowed_frames(b->d_sig, int64_t(L), b->d_sig + L, b->d_p, b->M, b->n, b->h, b->s)))
+        return hip_fail(e, "batch frames");
+    int rc = crlot_rfft_batched(inner, b->d_p, b->d_spec, int32_t(M), int64_t(N), 1, int64_t(row), 1, b->s);
+    if (rc == CRLOT_OK)
+        rc = crlot_irfft_batched(inner, b->d_spec, b->d_r, int32_t(M), int64_t(row), 1, int64_t(N), 1, b->s);
+    if (rc != CRLOT_OK) return rc;
+    if ((e = hipMemcpyAsync(b->h_spec, b->d_spec, sizeof(float) * M * row, hipMemcpyDeviceToHost, b->s)) ||
+        (e = hipMemcpyAsync(b->h_r, b->d_r, sizeof(float) * M * N, hipMemcpyDeviceToHost, b->s)) ||
+        (e = hipEventRecord(b->ev, b->s)) || (e = hipEventSynchronize(b->ev)))
+        return hip_fail(e, "batch results");
+    return CRLOT_OK;
+}
+
+}  // namespace
+
+int spec_mode() { return g_mode.load(std::memory_order_relaxed); }
+void spec_count(int what) { g_stats[what].fetch_add(1, std::memory_order_relaxed); }
+
+void note_window(const float* w, int64_t n) {
+    if (!w || n <= 0) return;
+    std::lock_guard<std::mutex> lk(g_win_mu);
+    for (size_t i = 0; i < g_windows.size(); ++i) {
+        const auto& v = g_windows[i];
+        if (int64_t(v.size()) == n && std::memcmp(v.data(), w, sizeof(float) * size_t(n)) == 0) {
+            std::rotate(g_windows.begin(), g_windows.begin() + int64_t(i), g_windows.begin() + int64_t(i) + 1);
+            return;
+        }
+    }
+    g_windows.insert(g_windows.begin(), std::vector<float>(w, w + n));
+    if (g_windows.size() > kMaxWindows) g_windows.pop_back();
+}
+
+std::vector<std::vector<float>> windows_of_size(int64_t n) {
+    std::lock_guard<std::mutex> lk(g_win_mu);
+    std::vector<std::vector<float>> out;
+    for (const auto& v : g_windows)
+        if (int64_t(v.size()) == n) out.push_back(v);
+    return out;
+}
+
+int batch_abort(SharedServer* sh) {
+    BatchSpec* b = sh->batch;
+    if (!b) return CRLOT_OK;
+    b->active = false;
+    b->inv_ready = b->pushed = -1;
+    if (b->ola) {
+        const int rc = ola_materialize_locked(b->ola);  // detaches it
+        b->ola = nullptr;
+        return rc;
+    }
+    return CRLOT_OK;
+}
+
+int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* in, float* out) {
+    if (spec_mode() < 2) return 0;
+    if (!sh->batch) sh->batch = new BatchSpec();
+    BatchSpec* b = sh->batch;
+    const size_t row = size_t(n) + 2;
+    if (b->active && b->n == n) {
+        const int64_t j = b->next_fwd;
+        if (j < b->M && input_matches(*b, j, in)) {
+            std::memcpy(out, b->h_spec + size_t(j) * row, sizeof(float) * row);
+            b->next_fwd = j + 1;
+            b->inv_ready = j;
+            spec_count(kStatForward);
+            if (b->next_fwd == b->M) b->active = false;  // last frame: its inverse / push / produce still served
+            return 1;
+        }
+    }
+    // a forward the batch did not predict: end it, then try to start one here
+    if (b->active || b->ola) {
+        const int rc = batch_abort(sh);
+        if (rc != CRLOT_OK) return rc;
+    }
+    b->inv_ready = b->pushed = -1;
+    std::vector<float> sig;
+    int64_t hop = 0, M = 0;
+    if (!inner || !framer_last_signal(n, &sig, &hop, &M) || M < 4) return 0;
+    const std::vector<std::vector<float>> wins = windows_of_size(n);
+    const std::vector<float>* found = nullptr;
+    for (const auto& w : wins) {
+        bool ok = true;
+        for (int64_t i = 0; i < n && ok; ++i) {
+            const float v = (i < int64_t(sig.size()) ? sig[size_t(i)] : 0.0f) * w[size_t(i)];
+            ok = std::memcmp(&v, in + i, sizeof(float)) == 0;
+        }
+        if (ok) {
+            found = &w;
+            break;
+        }
+    }
+    if (!found) return 0;
+    b->gen += 1;
+    b->n = n;
+    b->h = hop;
+    b->M = M;
+    b->sig.swap(sig);
+    b->win = *found;
+    b->next_fwd = 0;
+    b->y_ready = b->y_waited = false;
+    b->ola = nullptr;
+    const int rc = run_chain(b, inner);
+    if (rc != CRLOT_OK) {
+        b->active = false;
+        return rc;
+    }
+    sh->fft.valid = false;  // the call server's own per-call speculation is not used meanwhile
+    sh->chain.valid = false;
+    b->active = true;
+    spec_count(kStatStart);
+    spec_count(kStatForward);
+    std::memcpy(out, b->h_spec, sizeof(float) * row);
+    b->next_fwd = 1;
+    b->inv_ready = 0;
+    return 1;
+}
+
+int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out) {
+    BatchSpec* b = sh->batch;
+    if (!b || spec_mode() < 2 || b->n != n || b->inv_ready < 0) return 0;
+    const int64_t j = b->inv_ready;
+    const size_t row = size_t(n) + 2;
+    if (std::memcmp(in, b->h_spec + size_t(j) * row, sizeof(float) * row) != 0) return 0;
+    std::memcpy(out, b->h_r + size_t(j) * size_t(n), sizeof(float) * size_t(n));
+    b->inv_ready = -1;
+    b->pushed = j;
+    spec_count(kStatInverse);
+    return 1;
+}
+
+int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
+                 float gain, hipStream_t tables_stream) {
+    BatchSpec* b = sh->batch;
+    const size_t F = size_t(b->M - j0), len = F * size_t(b->h);
+    hipError_t e;
+    if ((e = hipStreamSynchronize(tables_stream)) != hipSuccess) return hip_fail(e, "OLA tables");
+    if ((e = dgrow(&b->d_y, &b->c_y, len)) || (e = hgrow(&b->h_y, &b->c_hy, len))) return hip_fail(e, "batch buffers");
+    Geometry g;
+    g.n = int(b->n);
+    g.h = int(b->h);
+    g.ring_len = int(R);
+    g.gain = gain;
+    DevTables t;
+    t.ws = d_ws;
+    t.den = d_den;
+    if ((e = launch_ola_gather(g, t, b->d_r + size_t(j0) * size_t(b->n), b->n, b->d_y, 1, int64_t(F),
+                               int64_t(len), int64_t(len), b->s)) ||
+        (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * len, hipMemcpyDeviceToHost, b->s)) ||
+        (e = hipEventRecord(b->ev, b->s)))
+        return hip_fail(e, "batch overlap-add");
+    b->ola = o;
+    b->j0 = j0;
+    b->gain = gain;
+    b->y_ready = true;
+    b->y_waited = false;
+    return CRLOT_OK;
+}
+
+int batch_wait_y(BatchSpec* b) {
+    if (b->y_waited) return CRLOT_OK;
+    const hipError_t e = hipEventSynchronize(b->ev);
+    if (e != hipSuccess) return hip_fail(e, "batch overlap-add");
+    b->y_waited = true;
+    return CRLOT_OK;
+}
+
+}  // namespace crlot
+
+extern "C" int crlot_call_speculation_stats(int64_t* out6) {
+    if (!out6) return crlot::set_error(CRLOT_EINVAL, "null argument");
+    for (int i = 0; i < 6; ++i) out6[i] = crlot::g_stats[i].load(std::memory_order_relaxed);
+    return CRLOT_OK;
+}
+
+extern "C" int crlot_set_call_speculation(int32_t mode) {
+    if (mode < 1 || mode > 2) return crlot::set_error(CRLOT_EINVAL, "speculation mode is 1 or 2");
+    crlot::g_mode.store(mode, std::memory_order_relaxed);
+    return CRLOT_OK;
+}

@@ -1,0 +1,96 @@
+// batch.h -- batched speculation of the reference's per-frame drop-in loop
+// (internal; batch.cpp, hooks in abi.cpp fft_host and objects.cpp).
+//
+// bench/e2e_benchmark.cc:138-186 runs, per frame k of a signal pushed whole
+// into a Framer:  pop -> p = frame * w -> IFftPlan::forward(p) -> inverse ->
+// OLAAccumulator::push_frame_AoS(inverse, k H) -> produce(H).  Every call of
+// that loop is a function of the signal, the window and the OLA object's
+// tables, all known once the first forward arrives.  So at the first forward
+// whose input is (bit for bit) the last popped Framer frame times a window
+// table the library built, the library runs the WHOLE remaining chain as one
+// batch on the device (analysis products, forward and inverse transforms of
+// every frame; after the first push, the overlap-add of every frame with the
+// object's window and divisors), copies the results to pinned host memory, and
+// serves each later call from there -- but only after checking that the call's
+// input bits and arguments are exactly the ones predicted, and with the very
+// kernels (K_rfft / K_irfft / the gather's fma chain) whose bits equal the call
+// kernel's.  The first call that differs ends the batch; the OLA object's
+// device ring is then rebuilt from the frames it was served (materialize), so
+// the next call sees exactly the state the individual calls would have left.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "crlot_dsp.h"
+
+struct crlot_ola;
+struct crlot_plan;
+
+namespace crlot {
+
+struct SharedServer;
+
+// The remaining frames of the most recently popped mono Framer, as a signal:
+// frame j (j = 0: the frame just popped) = sig[j H : j H + N], zeros past the
+// end, j < *frames.  Returns false when there is none (objects.cpp).
+bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_t* frames);
+// Window tables the library built (crlot_window_table) or was handed
+// (OLAAccumulator::set_window), newest first, for the speculation's search.
+void note_window(const float* w, int64_t n);
+std::vector<std::vector<float>> windows_of_size(int64_t n);
+
+// 1: the per-call speculation of the call server only; 2 (default): batched
+// speculation of the whole loop too (crlot_set_call_speculation)
+int spec_mode();
+enum { kStatStart = 0, kStatForward, kStatInverse, kStatPush, kStatProduce, kStatRebuild };
+void spec_count(int what);
+
+struct BatchSpec {
+    bool active = false;     // frames are being served
+    uint64_t gen = 0;        // bumped by every start
+    int64_t n = 0, h = 0, M = 0;
+    std::vector<float> sig;  // host copy of the remaining signal (verifies forward inputs)
+    std::vector<float> win;  // the analysis window found
+    int64_t next_fwd = 0;    // frame whose forward comes next
+    int64_t inv_ready = -1;  // frame whose forward was served and whose inverse may be asked
+    int64_t pushed = -1;     // last frame whose inverse was served (push candidate)
+    // device / pinned buffers (grow-only)
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    float* d_sig = nullptr;
+    float* d_p = nullptr;    // [M][N] analysis products, then reused
+    float* d_spec = nullptr; // [M][N + 2] spectra (interleaved complex)
+    float* d_r = nullptr;    // [M][N] inverse frames = push inputs
+    float* d_y = nullptr;    // [M][H] produce blocks (after attach)
+    float* h_stage = nullptr;
+    float* h_spec = nullptr;
+    float* h_r = nullptr;
+    float* h_y = nullptr;
+    size_t c_sig = 0, c_p = 0, c_spec = 0, c_r = 0, c_y = 0, c_hs = 0, c_hspec = 0, c_hr = 0, c_hy = 0;  // capacities
+    // the OLA object the batch's inverses are pushed to (objects.cpp)
+    crlot_ola* ola = nullptr;
+    int64_t j0 = 0;          // first frame pushed to it
+    float gain = 1.0f;
+    bool y_ready = false;    // h_y holds blocks j0 .. M-1 (event ev)
+    bool y_waited = false;
+};
+
+// abi.cpp fft_host, under sh->mu: a contiguous batch-1 real forward / inverse.
+// 1: served into `out`; 0: not (take the ordinary path); < 0: error.
+int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* in, float* out);
+int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out);
+// ends the batch (a call it does not predict); an attached OLA object is
+// materialized first (objects.cpp ola_materialize_locked)
+int batch_abort(SharedServer* sh);
+// objects.cpp, under sh->mu
+int ola_materialize_locked(crlot_ola* o);
+// the batch's gather for an OLA object attaching at frame j0 (objects.cpp passes
+// its tables): produce blocks of frames j0 .. M-1 into h_y
+int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
+                 float gain, hipStream_t tables_stream);
+int batch_wait_y(BatchSpec* b);
+
+}  // namespace crlot

@@ -144,6 +144,7 @@ struct SharedServer {
         CallSlot slot;      // chained produce block at slot.spec + N
     } chain;
     ChainTarget target;     // the OLA object that pushed the last speculated inverse
+    struct BatchSpec* batch = nullptr;  // batched speculation of the whole loop (batch.h)
 };
 // the shared server of (device, e) (created on first use; never destroyed);
 // e < 0: the FFT-only server of complex size P = -e (any size, call_any_waves)

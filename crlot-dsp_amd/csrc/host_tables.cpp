@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "batch.h"
 #include "crlot_dsp.h"
 
 namespace {
@@ -78,6 +79,7 @@ extern "C" int crlot_window_table(int32_t type, int64_t n, int32_t periodic, int
         }
     }
     if (norm != CRLOT_NORM_NONE) normalize(out, n, norm);
+    crlot::note_window(out, n);  // a table the batched speculation may meet (batch.h)
     return CRLOT_OK;
 }
 

@@ -328,6 +328,10 @@ hipError_t launch_axpy(float* dst, int64_t ld_dst, const float* src, int64_t ld_
                        int64_t n, int64_t batch, hipStream_t s);
 hipError_t launch_normalize_and_clear(float* out, int64_t ld_out, float* acc, int64_t ld_acc, const float* norm,
                                       float eps, int64_t n, int64_t batch, hipStream_t s);
+// p[k][j] = x[k H + j] * w[j] (0 * w[j] past T), k < F: the host loop's analysis
+// products for the batched drop-in speculation (batch.cpp)
+hipError_t launch_windowed_frames(const float* x, int64_t T, const float* w, float* p, int64_t F, int64_t N,
+                                  int64_t H, hipStream_t s);
 // dsp::FrameQueue frames on the device: [stream][F][N] from x [stream][ld_x]
 hipError_t launch_fq_frames(const float* x, int64_t T, int64_t ld_x, int n_streams, float* frames, int64_t F,
                             int64_t N, int64_t H, int64_t pad, int pad_mode, hipStream_t s);

@@ -23,6 +23,9 @@
 #include <string>
 #include <vector>
 
+#include <mutex>
+
+#include "batch.h"
 #include "call.h"
 #include "respool.h"
 #include "crlot_dsp.h"
@@ -60,6 +63,7 @@ struct crlot_framer {
     bool ready = false;           // set_params called (framer.cc:31)
     std::vector<float> buf;       // interleaved samples
     int64_t wr = 0, rd = 0;       // positions in samples (not frames)
+    std::vector<float> last;      // the frame pop() returned last (batched speculation, batch.h)
 
     void clear() {                // Framer::reset (framer.cc:76-86)
         buf.clear();
@@ -77,6 +81,36 @@ struct crlot_framer {
     }
 };
 
+namespace {
+// the Framer that popped last (batch.h framer_last_signal); cleared when it changes or dies
+std::mutex g_pop_mu;
+const crlot_framer* g_last_pop = nullptr;
+void forget_framer(const crlot_framer* f) {
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    if (g_last_pop == f) g_last_pop = nullptr;
+}
+}  // namespace
+
+namespace crlot {
+bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_t* frames) {
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    const crlot_framer* f = g_last_pop;
+    if (!f || f->c != 1 || f->n != n || int64_t(f->last.size()) != n) return false;
+    // frame 0 = the frame popped last; frame j >= 1 starts (j - 1) H into the
+    // unread buffer, which begins H samples into frame 0 (framer.cc:164-167)
+    const int64_t h = f->h, rest = f->wr - f->rd;
+    if (h > n) return false;
+    *hop = h;
+    // frame j exists while j H < L (ZERO_PAD, padded) or j H + N <= L (DROP)
+    const int64_t L = h + rest;
+    *frames = f->mode == CRLOT_ZERO_PAD ? (L + h - 1) / h : (L >= n ? (L - n) / h + 1 : 1);
+    sig->resize(size_t(L));
+    std::memcpy(sig->data(), f->last.data(), sizeof(float) * size_t(h));
+    if (rest > 0) std::memcpy(sig->data() + h, f->buf.data() + f->rd, sizeof(float) * size_t(rest));
+    return true;
+}
+}  // namespace crlot
+
 extern "C" {
 
 int crlot_framer_create(crlot_framer** out) {
@@ -85,7 +119,10 @@ int crlot_framer_create(crlot_framer** out) {
     return CRLOT_OK;
 }
 
-void crlot_framer_destroy(crlot_framer* f) { delete f; }
+void crlot_framer_destroy(crlot_framer* f) {
+    forget_framer(f);
+    delete f;
+}
 
 int crlot_framer_set_params(crlot_framer* f, int64_t frame_size, int64_t hop_size, int64_t channels,
                             int32_t boundary_mode) {
@@ -101,6 +138,7 @@ int crlot_framer_set_params(crlot_framer* f, int64_t frame_size, int64_t hop_siz
     f->mode = boundary_mode;
     f->ready = true;
     f->clear();
+    forget_framer(f);
     return CRLOT_OK;
 }
 
@@ -115,6 +153,7 @@ int crlot_framer_push(crlot_framer* f, const float* interleaved, int64_t frames)
         f->buf.resize(size_t(std::max<int64_t>(need, 2 * int64_t(f->buf.size()))), 0.0f);
     std::memcpy(f->buf.data() + f->wr, interleaved, sizeof(float) * size_t(add));
     f->wr = need;
+    forget_framer(f);  // the frames after the last pop changed
     return 1;
 }
 
@@ -129,6 +168,11 @@ int crlot_framer_pop(crlot_framer* f, float* out) {
         if (f->mode == CRLOT_DROP) return 0;
         std::memcpy(out, f->buf.data() + f->rd, sizeof(float) * size_t(have));
         std::fill(out + have, out + len, 0.0f);
+    }
+    if (f->c == 1) {  // kept for the batched speculation (batch.h)
+        f->last.assign(out, out + len);
+        std::lock_guard<std::mutex> lk(g_pop_mu);
+        g_last_pop = f;
     }
     f->rd = std::min(f->rd + f->h * f->c, f->wr);
     if (f->rd > int64_t(f->buf.size()) / 2) {  // compaction once half the buffer is consumed
@@ -148,6 +192,7 @@ int64_t crlot_framer_available(const crlot_framer* f) {
 int crlot_framer_reset(crlot_framer* f) {
     if (!f) return fail(CRLOT_EINVAL, "null framer");
     f->clear();
+    forget_framer(f);
     return CRLOT_OK;
 }
 
@@ -211,6 +256,15 @@ struct crlot_ola {
         crlot::CallSlot slot;
     } spec;
 
+    // batched speculation (batch.h): no add since creation / reset, and the
+    // batch this object is attached to while its ring is virtual (its pushes
+    // and produces served from the batch: the device ring untouched since)
+    bool pristine = true;
+    crlot::BatchSpec* vb = nullptr;
+    uint64_t vgen = 0;
+    int64_t vread = 0;   // samples produced from the batch (absolute, from the attach)
+    int64_t vlast = -1;  // last batch frame pushed
+
     int64_t N() const { return cfg.frame_size; }
     int64_t H() const { return cfg.hop_size; }
     int64_t C() const { return cfg.channels; }
@@ -234,6 +288,8 @@ void ola_free(crlot_ola* o) {
     DeviceGuard g(o->device);
     if (o->shared) {
         std::lock_guard<std::mutex> lk(o->shared->mu);
+        if (o->vb && o->vb->ola == o) o->vb->ola = nullptr;  // nothing to rebuild: the object goes
+        o->vb = nullptr;
         if (o->shared->target.owner == o) o->shared->target = crlot::ChainTarget{};
         if (o->mode == 2) (void)o->srv->drain();  // its requests touch this object's rings
     } else {
@@ -343,6 +399,7 @@ int add_common(crlot_ola* o, const float* d_src, int64_t cs, int64_t js, const f
     hipError_t e = crlot::launch_ola_add(o->d_ring, int(nch), o->R, d_src, cs, js, d_win,
                                          start_sample % o->R, len, gain, s);
     if (e != hipSuccess) return hip_fail(e, "OLA add kernel launch");
+    o->pristine = false;
     if (nch < o->C()) return CRLOT_OK;  // caller reports the null channel
     o->produced = std::max(o->produced, start_sample + eff);  // :114
     return CRLOT_OK;
@@ -493,6 +550,7 @@ int server_add(crlot_ola* o, const float* const* rows, int64_t ch, bool aos, con
         r.i[5] = pn;
     }
     if ((rc = sv->submit(r, sl)) != CRLOT_OK) return rc;
+    o->pristine = false;
     o->spec.valid = spec;
     o->spec.chain = false;
     o->spec.index = sl.index;
@@ -506,7 +564,102 @@ int server_add(crlot_ola* o, const float* const* rows, int64_t ch, bool aos, con
 }
 
 
+// ---- batched speculation (batch.h), all under the shared server's lock
+
+// A mono host push of the inverse frame the batch just served, at the loop's
+// rhythm: recorded without touching the device (the first one attaches the
+// object, whose ring must be untouched, and computes the produce blocks of
+// every remaining frame with the object's window and divisors).  1: served.
+int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_sample, int64_t start_off,
+               int64_t eff, float gain) {
+    crlot::BatchSpec* b = o->shared ? o->shared->batch : nullptr;
+    if (!b || crlot::spec_mode() < 2 || b->pushed < 0 || o->C() != 1 || b->n != o->N()) return 0;
+    const int64_t j = b->pushed, N = o->N();
+    if (start_off != 0 || eff != N || caller_win || !o->cfg.apply_window_inside || o->window.empty() ||
+        o->flushing || std::memcmp(frame, b->h_r + size_t(j) * size_t(N), sizeof(float) * size_t(N)) != 0)
+        return 0;
+    if (o->vb) {
+        if (o->vb != b || b->ola != o || o->vgen != b->gen || j != o->vlast + 1 ||
+            start_sample != (j - b->j0) * b->h || !(gain == b->gain))
+            return 0;
+    } else {
+        if (!o->pristine || start_sample != 0 || o->read_pos != 0 || o->produced != 0) return 0;
+        if (b->ola) {  // another object rode this batch: rebuild its ring first
+            const int rc = crlot::ola_materialize_locked(b->ola);
+            if (rc != CRLOT_OK) return rc;
+        }
+        const int rc = crlot::batch_attach(o->shared, o, j, o->R, o->d_win, o->d_den, gain, o->own);
+        if (rc != CRLOT_OK) return rc;
+        o->vb = b;
+        o->vgen = b->gen;
+        o->vread = 0;
+    }
+    b->pushed = -1;
+    crlot::spec_count(crlot::kStatPush);
+    o->vlast = j;
+    o->pristine = false;
+    o->spec.valid = false;
+    o->produced = std::max(o->produced, start_sample + eff);  // :114
+    o->last_start = start_sample;
+    o->last_gain = gain;
+    return 1;
+}
+
+// A mono host produce of n (already clamped to the available count) inside the
+// blocks the batch's pushes have finalised.  1: served into out.
+int batch_produce(crlot_ola* o, float* out, int64_t n) {
+    crlot::BatchSpec* b = o->vb;
+    if (!b || crlot::spec_mode() < 2 || b->ola != o || o->vgen != b->gen || o->flushing || o->C() != 1) return 0;
+    const int64_t final_end = (o->vlast - b->j0 + 1) * b->h;  // positions no later frame reaches
+    if (o->vread + n > final_end || o->read_pos != o->vread % o->R) return 0;
+    const int rc = crlot::batch_wait_y(b);
+    if (rc != CRLOT_OK) return rc;
+    std::memcpy(out, b->h_y + o->vread, sizeof(float) * size_t(n));
+    o->vread += n;
+    crlot::spec_count(crlot::kStatProduce);
+    return 1;
+}
+
+// the object's ring when a live batch no longer serves it: zero ring + the
+// batch frames it was served, from the read position on (the cleared part of
+// each push is exactly what its produces removed), in push order
+int ola_materialize(crlot_ola* o) {
+    crlot::BatchSpec* b = o->vb;
+    if (!b) return CRLOT_OK;
+    o->vb = nullptr;
+    if (b->ola == o) b->ola = nullptr;
+    if (o->vgen != b->gen) return fail(CRLOT_ERUNTIME, "OLA object: batched speculation state lost");
+    crlot::spec_count(crlot::kStatRebuild);
+    crlot::CallServer* sv = o->srv;
+    int rc = sv ? sv->drain() : CRLOT_OK;
+    if (rc != CRLOT_OK) return rc;
+    const int64_t N = o->N(), h = b->h;
+    for (int64_t k = b->j0; k <= o->vlast; ++k) {
+        const int64_t rel = (k - b->j0) * h, off = std::max<int64_t>(0, o->vread - rel);
+        if (off >= N) continue;
+        const hipError_t e = crlot::launch_ola_add(o->d_ring, 1, o->R, b->d_r + size_t(k) * size_t(N) + off, N, 1,
+                                                   o->d_win + off, (rel + off) % o->R, N - off, b->gain, o->own);
+        if (e != hipSuccess) return hip_fail(e, "OLA rebuild");
+    }
+    const hipError_t e = hipStreamSynchronize(o->own);
+    if (e != hipSuccess) return hip_fail(e, "OLA rebuild");
+    if (sv) sv->acquire_next();
+    o->spec.valid = false;
+    return CRLOT_OK;
+}
+
+// entry points outside the speculated loop: rebuild a virtual ring first
+int ensure_real(crlot_ola* o) {
+    if (!o->vb) return CRLOT_OK;
+    ServerLock lk(o);
+    return ola_materialize(o);
+}
+
 }  // namespace
+
+namespace crlot {
+int ola_materialize_locked(crlot_ola* o) { return ola_materialize(o); }
+}  // namespace crlot
 
 extern "C" {
 
@@ -571,6 +724,9 @@ int crlot_ola_set_window(crlot_ola* o, const float* w, int32_t wlen) {
     if (!w) return fail(CRLOT_EINVAL, "Window pointer cannot be null");
     if (int64_t(wlen) != o->N()) return fail(CRLOT_EINVAL, "Window size must match frame size");
     DeviceGuard g(o->device);
+    int rc = ensure_real(o);
+    if (rc != CRLOT_OK) return rc;
+    crlot::note_window(w, wlen);
     o->window.assign(w, w + wlen);
     hipError_t e = use_stream(o, o->own);
     if (e != hipSuccess) return hip_fail(e, "stream order");
@@ -596,6 +752,7 @@ int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const f
     int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
     ServerLock lk(o);
+    if (o->vb && (rc = ola_materialize(o)) != CRLOT_OK) return rc;
     rc = ok == o->C() ? try_chain_push(o, rows[0], uw, caller_win, start_sample, start_off, eff, gain) : 0;
     if (rc < 0) return rc;
     if (rc == 0)
@@ -622,6 +779,9 @@ int crlot_ola_push_frame_aos(crlot_ola* o, const float* interleaved, const float
     int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
     ServerLock lk(o);
+    rc = batch_push(o, src, window != nullptr, start_sample, start_off, eff, gain);
+    if (rc != 0) return rc < 0 ? rc : CRLOT_OK;
+    if (o->vb && (rc = ola_materialize(o)) != CRLOT_OK) return rc;
     // (a mono AoS frame is the SoA one; the window is read from index 0 as for start_off 0)
     rc = try_chain_push(o, src, uw, caller_win, start_sample, start_off == 0 ? 0 : -1, eff, gain);
     if (rc < 0) return rc;
@@ -640,6 +800,7 @@ int crlot_ola_add_frame_soa_device(crlot_ola* o, const float* d_frames, int64_t 
     if (!clamp(o, start_off, size, &eff)) return CRLOT_OK;
     if (o->C() > 1 && ld_frames < o->N()) return fail(CRLOT_EINVAL, "leading dimension too small");
     DeviceGuard g(o->device);
+    if (const int rc = ensure_real(o); rc != CRLOT_OK) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream (crlot_dsp.h)
     hipError_t e = use_stream(o, s);
     if (e != hipSuccess) return hip_fail(e, "stream order");
@@ -657,6 +818,7 @@ int crlot_ola_push_frame_aos_device(crlot_ola* o, const float* d_interleaved, co
     int64_t eff = 0;
     if (!clamp(o, start_off, size, &eff)) return CRLOT_OK;
     DeviceGuard g(o->device);
+    if (const int rc = ensure_real(o); rc != CRLOT_OK) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream (crlot_dsp.h)
     hipError_t e = use_stream(o, s);
     if (e != hipSuccess) return hip_fail(e, "stream order");
@@ -683,6 +845,17 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
     int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
     ServerLock lk(o);
+    if (o->vb) {
+        rc = batch_produce(o, ch_out[0], n);
+        if (rc < 0) return rc;
+        if (rc == 0 && (rc = ola_materialize(o)) != CRLOT_OK) return rc;
+        if (rc == 1) {
+            o->read_pos = (o->read_pos + n) % o->R;  // :213
+            for (int64_t i = 0; i < n; ++i) o->host_peak = std::max(o->host_peak, std::fabs(ch_out[0][i]));
+            if (n_out) *n_out = n;
+            return CRLOT_OK;
+        }
+    }
     crlot::CallServer* sv = o->srv;
     const int64_t C = o->C();
     const bool hit = o->spec.valid && o->spec.index == sv->submitted() && o->spec.rp == o->read_pos &&
@@ -749,6 +922,7 @@ int crlot_ola_produce_device(crlot_ola* o, float* d_out, int64_t ld_out, int64_t
     if (o->C() > 1 && ld_out < n) return fail(CRLOT_EINVAL, "leading dimension too small");
     const int64_t len = std::min(n, o->R);
     DeviceGuard g(o->device);
+    if (const int rc = ensure_real(o); rc != CRLOT_OK) return rc;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the default stream (crlot_dsp.h)
     hipError_t e = use_stream(o, s);
     if (e != hipSuccess) return hip_fail(e, "stream order");
@@ -772,6 +946,11 @@ int crlot_ola_flush(crlot_ola* o) {
 int crlot_ola_reset(crlot_ola* o) {
     if (!o) return fail(CRLOT_EINVAL, "null OLA object");
     DeviceGuard g(o->device);
+    if (o->vb) {  // the ring is zeroed below: a virtual one needs no rebuild
+        ServerLock lk(o);
+        if (o->vb->ola == o) o->vb->ola = nullptr;
+        o->vb = nullptr;
+    }
     hipError_t e = use_stream(o, o->own);
     if (e != hipSuccess) return hip_fail(e, "stream order");
     if ((e = hipMemsetAsync(o->d_ring, 0, sizeof(float) * size_t(o->C() * o->R), o->own)) ||
@@ -784,6 +963,7 @@ int crlot_ola_reset(crlot_ola* o) {
     o->last_start = -1;
     o->last_req_n = 0;
     o->spec.valid = false;
+    o->pristine = true;
     return upload_norm(o, o->own);
 }
 
@@ -820,6 +1000,7 @@ int crlot_ola_norm_table(const crlot_ola* o, float* out) {
 int crlot_ola_synchronize(crlot_ola* o) {
     if (!o) return fail(CRLOT_EINVAL, "null OLA object");
     DeviceGuard g(o->device);
+    if (const int rc = ensure_real(o); rc != CRLOT_OK) return rc;
     if (o->mode == 2) {
         ServerLock lk(o);
         return o->srv->drain();

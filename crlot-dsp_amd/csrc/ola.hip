@@ -218,7 +218,28 @@ __global__ void __launch_bounds__(256) k_fq_frames(const float* __restrict__ x, 
     frames[s * F * N + e] = v;
 }
 
+// Batched drop-in speculation (batch.cpp): the analysis products the e2e loop
+// forms on the host, p[k][j] = frame_k[j] * w[j] with frame_k[j] = x[k H + j]
+// (zero past T), one plain multiply each -- the same product, so the same bits.
+__global__ void __launch_bounds__(256) k_windowed_frames(const float* __restrict__ x, int64_t T,
+                                                         const float* __restrict__ w, float* __restrict__ p,
+                                                         int64_t F, int64_t N, int64_t H) {
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (e >= F * N) return;
+    const int64_t k = e / N, j = e - k * N;
+    const int64_t idx = k * H + j;
+    p[e] = (idx < T ? x[idx] : 0.0f) * w[j];
+}
+
 }  // namespace
+
+hipError_t launch_windowed_frames(const float* x, int64_t T, const float* w, float* p, int64_t F, int64_t N,
+                                  int64_t H, hipStream_t s) {
+    if (F <= 0 || N <= 0) return hipSuccess;
+    if (F * N > (int64_t(1) << 40)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_windowed_frames, dim3(unsigned((F * N + 255) / 256)), dim3(256), 0, s, x, T, w, p, F, N, H);
+    return hipGetLastError();
+}
 
 hipError_t launch_axpy(float* dst, int64_t ld_dst, const float* src, int64_t ld_src, const float* win, float g,
                        int64_t n, int64_t batch, hipStream_t s) {

@@ -140,6 +140,21 @@ int crlot_plan_set_frame_pairing(crlot_plan* plan, int32_t enable);
  * seams, and the launch record below reports the chunking a call used.
  * Negative: CRLOT_EINVAL. */
 int crlot_plan_set_chunks(crlot_plan* plan, int32_t chunks_per_stream);
+/* Speculation of the host-pointer drop-in calls (IFftPlan forward / inverse,
+ * OLAAccumulator push / produce), process-wide.  1: each forward also computes
+ * the inverse and the produce block that follow it on the call kernel.  2
+ * (default): in addition, when a forward's input is bit for bit the frame a
+ * dsp::Framer just popped times a window table the library built, the whole
+ * remaining loop of that Framer's signal runs as one batch on the device and
+ * the following calls are served from it after a bitwise check of each call's
+ * input and arguments; the first call that differs ends the batch and the OLA
+ * object's ring is rebuilt from the frames it was served.  Results are the
+ * same bits in both modes.  Other values: CRLOT_EINVAL. */
+int crlot_set_call_speculation(int32_t mode);
+/* Process-wide counters of the batched speculation: [0] batches started, [1]
+ * forwards, [2] inverses, [3] pushes, [4] produces served from a batch, [5] OLA
+ * rings rebuilt after a call the batch did not predict. */
+int crlot_call_speculation_stats(int64_t* out6);
 /* What the plan's last call on `stream` launched: kernels in launch order
  * (CRLOT_K_* ids below; the first 8 are kept, n_kernels counts all), the
  * workgroups of each launch, and the chunks per stream of the walk (0 when the

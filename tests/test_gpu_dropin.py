@@ -501,3 +501,131 @@ def test_device_kernels_bit_exact_vs_reference_build(pkg, torch_cuda, ref_tables
         assert np.array_equal(bits(ho), bits(ref_tables[f"{k}_out"])), k
         n_checked += 1
     assert n_checked == 24
+
+
+def _e2e_loop(pkg, oracle, x, n, h, breaks=None, window=None):
+    """bench/e2e_benchmark.cc:138-186 through the drop-in objects, streaming-
+    interleaved; `breaks` maps a frame index to a deviation from the rhythm.
+    Returns (spectra, inverse frames, produced blocks, pushed frames)."""
+    breaks = breaks or {}
+    w = pkg.window_table(pkg.HANN, n) if window is None else window
+    fr = pkg.Framer()
+    fr.set_params(n, h, 1, pkg.ZERO_PAD)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                        apply_window_inside=True)
+    ola = pkg.OLAAccumulator(cfg)
+    ola.set_window(w)
+    fr.push(x)
+    specs, invs, outs, pushed = [], [], [], []
+    k = 0
+    start = 0
+    while True:
+        f = fr.pop()
+        if f is None:
+            break
+        p = (f * w).astype(np.float32)
+        b = breaks.get(k)
+        if b == "input":
+            p = p.copy()
+            p[k % n] = np.nextafter(p[k % n], np.float32(np.inf))
+        X = fft.forward_host(p[None])
+        if b == "extra_forward":
+            fft.forward_host((p * np.float32(0.5))[None])
+        y = fft.inverse_host(X)[0]
+        gain = 0.5 if b == "gain" else 1.0
+        if b == "device_push":
+            import torch
+            ola.push_frame_AoS_device(torch.from_numpy(y.copy()).cuda(), None, start, 0, n, gain)
+            torch.cuda.synchronize()
+        else:
+            ola.push_frame_AoS(y, None, start, 0, n, gain)
+        m = h // 2 if b == "short_produce" else h
+        got, chans = ola.produce(m)
+        specs.append(np.asarray(X).copy())
+        invs.append(y.copy())
+        outs.append(chans[0][:got].copy())
+        pushed.append((y.copy(), start, gain, m))
+        start += h
+        k += 1
+    ola.close()
+    fft.close()
+    fr.close()
+    return specs, invs, outs, pushed
+
+
+def _oracle_outputs(oracle, n, h, w, pushed):
+    ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ref.set_window(w)
+    out = []
+    for y, start, gain, m in pushed:
+        ref.push_frame_aos(y, start, 0, n, gain)
+        out.append(ref.produce(m)[0])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h", [(1024, 256), (1024, 512), (960, 240), (882, 441)])
+def test_batched_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, h):
+    """The e2e loop served from the batched speculation gives, call by call, the
+    bits the per-call path (crlot_set_call_speculation(1)) gives: spectra,
+    inverse frames and every produced block; and the produced blocks are the
+    oracle OLAAccumulator's fed the same frames, bit for bit.  The counters show
+    the batch really served the loop."""
+    x = oracle.synth(48_000, n + h)
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_loop(pkg, oracle, x, n, h)
+        pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats()
+        b = _e2e_loop(pkg, oracle, x, n, h)
+        s1 = pkg.call_speculation_stats()
+    finally:
+        pkg.set_call_speculation(2)
+    F = len(a[0])
+    assert len(b[0]) == F
+    for k in range(F):
+        assert np.array_equal(bits(a[0][k]), bits(b[0][k])), ("spectrum", k)
+        assert np.array_equal(bits(a[1][k]), bits(b[1][k])), ("inverse", k)
+        assert np.array_equal(bits(a[2][k]), bits(b[2][k])), ("produce", k)
+    ref = _oracle_outputs(oracle, n, h, pkg.window_table(pkg.HANN, n), b[3])
+    for k in range(F):
+        assert np.array_equal(bits(b[2][k]), bits(ref[k])), ("oracle", k)
+    served = {key: s1[key] - s0[key] for key in s1}
+    assert served["batches"] == 1 and served["forwards"] == F and served["inverses"] == F, served
+    assert served["pushes"] == F and served["produces"] == F and served["rebuilds"] == 0, served
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("brk", ["input", "extra_forward", "gain", "short_produce", "device_push"])
+def test_batched_loop_falls_back_on_a_broken_rhythm(pkg, oracle, torch_cuda, brk):
+    """One call off the predicted rhythm mid-stream (a forward input one bit off,
+    an unrelated forward, another gain, a shorter produce, a push through the
+    device form): the batch ends there, the OLA ring is rebuilt from the frames
+    it was served, and every later call (the per-call path, and a new batch
+    where the rhythm resumes) still gives the per-call path's bits and the
+    oracle's blocks."""
+    n, h = 1024, 256
+    x = oracle.synth(48_000, 7)
+    breaks = {60: brk, 61: brk} if brk == "short_produce" else {60: brk}
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_loop(pkg, oracle, x, n, h, breaks)
+        pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats()
+        b = _e2e_loop(pkg, oracle, x, n, h, breaks)
+        s1 = pkg.call_speculation_stats()
+    finally:
+        pkg.set_call_speculation(2)
+    F = len(a[0])
+    for k in range(F):
+        assert np.array_equal(bits(a[1][k]), bits(b[1][k])), ("inverse", k)
+        assert np.array_equal(bits(a[2][k]), bits(b[2][k])), ("produce", k)
+    ref = _oracle_outputs(oracle, n, h, pkg.window_table(pkg.HANN, n), b[3])
+    for k in range(F):
+        assert np.array_equal(bits(b[2][k]), bits(ref[k])), ("oracle", k)
+    served = {key: s1[key] - s0[key] for key in s1}
+    if brk == "short_produce":  # still inside the finalised blocks: served, nothing rebuilt
+        assert served["rebuilds"] == 0 and served["produces"] == F, served
+    else:
+        assert served["rebuilds"] == 1 and served["forwards"] >= 60, served
