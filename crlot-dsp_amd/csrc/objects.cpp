@@ -582,6 +582,10 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
         if (o->vb != b || b->ola != o || o->vgen != b->gen || j != o->vlast + 1 ||
             start_sample != (j - b->j0) * b->h || !(gain == b->gain))
             return 0;
+        // a push reaching R samples past the oldest unread one wraps onto unread
+        // ring data (the harness's push-everything-first order): the
+        // batch's overlap-add does not alias, the ring does -- leave it to the ring
+        if (start_sample + N > o->vread + o->R) return 0;
     } else {
         if (!o->pristine || start_sample != 0 || o->read_pos != 0 || o->produced != 0) return 0;
         if (b->ola) {  // another object rode this batch: rebuild its ring first

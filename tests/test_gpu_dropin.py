@@ -629,3 +629,59 @@ def test_batched_loop_falls_back_on_a_broken_rhythm(pkg, oracle, torch_cuda, brk
         assert served["rebuilds"] == 0 and served["produces"] == F, served
     else:
         assert served["rebuilds"] == 1 and served["forwards"] >= 60, served
+
+
+@pytest.mark.gpu
+def test_batched_loop_keeps_ring_aliasing_of_the_harness_order(pkg, oracle, torch_cuda):
+    """bench/e2e_benchmark.cc's literal order pushes every frame before the
+    produce loop, so the 6144-sample OLA ring wraps onto unread data.
+    The batch's overlap-add does not alias; the pushes that would wrap are left to
+    the ring, so the output keeps the reference's aliasing: the same bits as the
+    per-call path and as the oracle OLAAccumulator fed the same calls."""
+    n, h = 1024, 256
+    x = oracle.synth(48_000, 11)
+    w = pkg.window_table(pkg.HANN, n)
+
+    def run():
+        fr = pkg.Framer()
+        fr.set_params(n, h, 1, pkg.ZERO_PAD)
+        fft = pkg.FftPlan(n, pkg.FFT_REAL)
+        ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1,
+                                               eps=1e-8, apply_window_inside=True))
+        ola.set_window(w)
+        fr.push(x)
+        frames, k = [], 0
+        while True:
+            f = fr.pop()
+            if f is None:
+                break
+            y = fft.inverse_host(fft.forward_host((f * w).astype(np.float32)[None]))[0]
+            ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+            frames.append(y.copy())
+            k += 1
+        out = []
+        while True:
+            got, chans = ola.produce(48_000)
+            if got == 0 or sum(len(o) for o in out) >= 48_000:
+                break
+            out.append(chans[0][:got].copy())
+        ola.close()
+        fft.close()
+        fr.close()
+        return frames, np.concatenate(out)
+
+    try:
+        pkg.set_call_speculation(1)
+        fa, ya = run()
+        pkg.set_call_speculation(2)
+        fb, yb = run()
+    finally:
+        pkg.set_call_speculation(2)
+    assert all(np.array_equal(bits(a), bits(b)) for a, b in zip(fa, fb))
+    assert np.array_equal(bits(ya), bits(yb))
+    ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ref.set_window(w)
+    for k, y in enumerate(fb):
+        ref.push_frame_aos(y, k * h, 0, n, 1.0)
+    r = ref.produce(48_000)[0]
+    assert np.array_equal(bits(yb[:r.size]), bits(r))
