@@ -96,17 +96,19 @@ for k, v in valu_pass.items():
 
 def valu_issue(p, simds=1024, xcds=8, lanes=64):
     """VALU busy fraction of the dominant kernel from the valu pass: VALU
-    instruction cycles per SIMD (SQ_THREAD_CYCLES_VALU is thread-cycles summed
-    over SIMDs; / 64 lanes for full waves) over the kernel's cycles
-    (GRBM_GUI_ACTIVE sums the 8 XCDs' clocks), and the FP32 flops actually
-    executed (SQ_INSTS_VALU_FLOPS_FP32) per launch."""
+    cycles per SIMD over the kernel's cycles.  SQ_THREAD_CYCLES_VALU counts
+    quad-cycles (4 clocks: one wave64 VALU instruction, packed or not, on a
+    16-lane SIMD) times active lanes, summed over the SIMDs: / 64 lanes (full
+    waves) x 4 / 1024 SIMDs; it equals SQ_ACTIVE_INST_VALU x 64 here.
+    GRBM_GUI_ACTIVE sums the 8 XCDs' clocks.  Also the FP32 flops the counter
+    reports (SQ_INSTS_VALU_FLOPS_FP32, per wave instruction: x 64 lanes)."""
     if not {"SQ_THREAD_CYCLES_VALU", "GRBM_GUI_ACTIVE"} <= set(p):
         return None
     kcyc = p["GRBM_GUI_ACTIVE"] / xcds
-    busy = p["SQ_THREAD_CYCLES_VALU"] / lanes / simds
+    busy = p["SQ_THREAD_CYCLES_VALU"] / lanes * 4 / simds
     out = {"valu_cycles_per_simd": busy, "kernel_cycles": kcyc, "busy_frac": busy / kcyc if kcyc else None}
     if "SQ_INSTS_VALU_FLOPS_FP32" in p:
-        out["fp32_flops_per_launch"] = p["SQ_INSTS_VALU_FLOPS_FP32"]
+        out["fp32_flops_per_launch"] = p["SQ_INSTS_VALU_FLOPS_FP32"] * lanes
     return out
 S, T, N, H = 1024, 480000, 1024, 256
 alg_read = S * T * 4
