@@ -172,6 +172,8 @@ crlot::DevTables tables(const crlot_plan* p, const crlot::Scratch* sc = nullptr)
             t.ptw = p->d_ptw;
             t.pden = p->d_pden;
         }
+        const int n = p->geo.n;
+        if (n == 512 || n == 1024 || n == 2048 || n == 4096) t.pden2 = p->d_pden + 2 * p->geo.ring_len;
         if (sc) {
             t.pflags = sc->pflags;
             t.pflags_len = sc->pflags_len;
@@ -317,6 +319,19 @@ int upload_window_tables(crlot_plan* p, hipStream_t s) {
                     pd[at + q] = den[size_t(b) * h + l + lanes * q];
                     pd[at + sh + q] = rden[size_t(b) * h + l + lanes * q];
                 }
+        if (p->geo.n == 512 || p->geo.n == 1024 || p->geo.n == 2048 || p->geo.n == 4096) {
+            // block-pair rows for the hot walkers (DevTables::pden2)
+            pd.resize(den.size() * 6);
+            for (int b = 0; b < blocks; ++b)
+                for (int l = 0; l < lanes; ++l)
+                    for (int q = 0; q < sh; ++q)
+                        for (int j = 0; j < 2; ++j) {
+                            const size_t src = size_t((b + j) % blocks) * h + l + lanes * q;
+                            const size_t at = den.size() * 2 + (size_t(b) * lanes + l) * 4 * sh;
+                            pd[at + 2 * q + j] = den[src];
+                            pd[at + 2 * sh + 2 * q + j] = rden[src];
+                        }
+        }
         up.add(p->d_pden, pd.data(), sizeof(float) * pd.size());
     }
     up.add(p->d_wa, wa.data(), sizeof(float) * n);
@@ -392,9 +407,10 @@ bool pair_plan(const crlot_plan* p) {
 int ensure_pair_flags(const crlot_plan* p, crlot::Scratch* sc, int32_t n_streams, int64_t F) {
     if (!pair_plan(p)) return CRLOT_OK;
     int64_t have = sc->pflags_len * int64_t(sizeof(uint32_t));
-    // (two-wave walks of K_pairN keep a flag per wave: two per chunk, F >= chunks)
+    // (two-wave walks of K_pairN keep a flag per wave: two per chunk, F >= chunks;
+    // K_pair's hot walker two words per walker)
     const int rc = grow_on_stream(&sc->pflags, &have,
-                                  int64_t(n_streams) * std::max<int64_t>(F, 2) * int64_t(sizeof(uint32_t)), sc->s,
+                                  2 * int64_t(n_streams) * std::max<int64_t>(F, 2) * int64_t(sizeof(uint32_t)), sc->s,
                                   "pair flag");
     sc->pflags_len = have / int64_t(sizeof(uint32_t));
     return rc;
@@ -531,7 +547,7 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
                                        : n == 512  ? crlot::build_pair512_twiddles()
                                        : n == 2048 ? crlot::build_pair2k_twiddles()
                                                    : crlot::build_pair4k_twiddles();
-        if ((e = hipMalloc(&p->d_pden, sizeof(float) * 2 * ring)) ||
+        if ((e = hipMalloc(&p->d_pden, sizeof(float) * ((n == 512 || n == 1024 || n == 2048 || n == 4096) ? 6 : 2) * ring)) ||
             (e = hipMalloc(&p->d_ptw, sizeof(float) * ptw.size())) ||
             (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {
             free_plan(p);
@@ -724,7 +740,7 @@ int crlot_plan_reserve(crlot_plan* p, int64_t bytes) {
 static void scratch_need(const crlot_plan* p, int32_t n_streams, int64_t T, int32_t channels, int64_t* flags,
                          int64_t* work, int64_t* planes) {
     const int64_t F = frames_for(p, T), S = int64_t(n_streams) * channels, L = F * p->geo.h;
-    *flags = pair_plan(p) ? S * std::max<int64_t>(F, 2) : 0;  // as ensure_pair_flags
+    *flags = pair_plan(p) ? 2 * S * std::max<int64_t>(F, 2) : 0;  // as ensure_pair_flags
     const bool direct_ilv = channels > 1 && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0;
     *planes = (channels > 1 && !direct_ilv) ? S * (T + L) * int64_t(sizeof(float)) : 0;
     static const float probe[2] = {0.f, 0.f};

@@ -88,6 +88,68 @@ __device__ __forceinline__ pc pc_mulc(pc a, pc w) {
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(w), "v"(p));
     return r;
 }
+// min(|a|, |b|, c) in one instruction (finite operands)
+__device__ __forceinline__ float min3_abs(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, |%1|, |%2|, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// min(e, frexp exponents of the 14 values a[0..7) .x/.y), computed only when some
+// lane has smin < thr: a wave-uniform skip written inside one asm block, so the
+// register allocator sees straight-line code (a C++ branch here costs the walker
+// VGPR spills).
+__device__ __forceinline__ int frexp_min_if(const pc* a, float smin, int e, float thr = 0x1p-89f) {
+    int t0, t1;
+    asm volatile("v_cmp_gt_f32 vcc, %[th], %[sm]\n\t"
+                 "s_cbranch_vccz .Lfx_skip%=\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x0]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y0]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x1]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y1]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x2]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y2]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x3]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y3]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x4]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y4]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x5]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y5]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 "v_frexp_exp_i32_f32 %[t0], %[x6]\n\t"
+                 "v_frexp_exp_i32_f32 %[t1], %[y6]\n\t"
+                 "v_min3_i32 %[e], %[t0], %[t1], %[e]\n\t"
+                 ".Lfx_skip%=:"
+                 : [e] "+v"(e), [t0] "=&v"(t0), [t1] "=&v"(t1)
+                 : [sm] "v"(smin), [th] "s"(thr), [x0] "v"(a[0].x), [y0] "v"(a[0].y), [x1] "v"(a[1].x), [y1] "v"(a[1].y), [x2] "v"(a[2].x), [y2] "v"(a[2].y), [x3] "v"(a[3].x), [y3] "v"(a[3].y), [x4] "v"(a[4].x), [y4] "v"(a[4].y), [x5] "v"(a[5].x), [y5] "v"(a[5].y), [x6] "v"(a[6].x), [y6] "v"(a[6].y)
+                 : "vcc");
+    return e;
+}
+// The output sanitize's threshold test of the hot walkers, screened: the
+// smallest frexp exponent over the E registers' 2E values (zero's being 0), as
+// min over every value would give wherever it can reach 2^MIN_EXP.  The window-edge
+// registers (0 and E-1: the taps a window zeroes, whose outputs are often exact
+// zeros) take the exact test; elsewhere min |v| >= thr on every lane (half a
+// v_min3 per value) proves the test passes, and only a wave where some lane fails
+// the screen (exact zero outputs: silence, zero-padded stream ends; or a tiny
+// one) runs the exact test on the interior registers as well.
+template <int E>
+__device__ __forceinline__ int out_min_exp_screened(const pc (&v)[E], float thr) {
+    static_assert(E == 8 || E == 16, "registers");
+    const int e0 = min(min(__builtin_amdgcn_frexp_expf(v[0].x), __builtin_amdgcn_frexp_expf(v[0].y)),
+                       min(__builtin_amdgcn_frexp_expf(v[E - 1].x), __builtin_amdgcn_frexp_expf(v[E - 1].y)));
+    float s2[2] = {0x1p100f, 0x1p100f};
+#pragma unroll
+    for (int m = 1; m < E - 1; ++m) s2[m & 1] = min3_abs(v[m].x, v[m].y, s2[m & 1]);
+    const float sm = __builtin_fminf(s2[0], s2[1]);
+    int e = frexp_min_if(v + 1, sm, e0, thr);
+    if constexpr (E == 16) e = frexp_min_if(v + 8, sm, e, thr);
+    return e;
+}
 template <bool INV>
 __device__ __forceinline__ pc pc_tw(pc a, pc w) { return INV ? pc_mulc(a, w) : pc_mul(a, w); }
 

@@ -33,6 +33,11 @@ struct DevTables {
     // K_pair per-block divisors: [ring_len/H][64 lanes][den (SH) | rden (SH)], SH = H/64,
     // den at block offset lane + 64 q (nullptr when the pair kernel is off).
     const float* pden = nullptr;
+    // ... and the same divisors by block pair: [ring_len/H][L lanes][(den_k, den_k+1) (SH pairs) |
+    // (rden_k, rden_k+1) (SH pairs)] for every block k (k+1 modulo the ring), so the hot walkers
+    // divide the blocks of a frame pair with packed operations (N = 512, 1024, 2048, 4096;
+    // L = 64, 64, 128, 256).
+    const float* pden2 = nullptr;
     // K_pair paired regime: samples x with x == 0 or px_lo <= |x| <= px_hi keep
     // sanitize(x * wa) == x * wa and the transforms finite (kernels.hip K_pair).
     float px_lo = 0.f, px_hi = 0.f;

@@ -4,9 +4,11 @@
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "fft_pair.h"
 #include "fused_common.h"
+#include "ola_pair.h"
 
 namespace crlot {
 
@@ -72,6 +74,14 @@ struct PairLds {
 #ifndef CRLOT_PAIR_HOT8
 #define CRLOT_PAIR_HOT8 1  // the paired-only walker at H = 512 too
 #endif
+#ifndef CRLOT_PAIR_PK2
+#define CRLOT_PAIR_PK2 2  // the hot walker's packing: bit 0 hop-slot pairs (window products; spills, measured slower), bit 1 block pairs (OLA adds, divisions)
+#endif
+#define CRLOT_PAIR_PKX (CRLOT_PAIR_PK2 & 1)
+#ifndef CRLOT_PAIR_OSCREEN
+#define CRLOT_PAIR_OSCREEN 1  // output-sanitize screen (v_min3 over |v|) off the window-edge registers, the exact test only where it fails
+#endif
+#define CRLOT_PAIR_PKA ((CRLOT_PAIR_PK2 >> 1) & 1)
 #ifndef CRLOT_PAIR_MIN_WAVES
 #define CRLOT_PAIR_MIN_WAVES (CRLOT_PAIR_REG_TW ? 3 : 4)
 #endif
@@ -83,6 +93,16 @@ struct PairLds {
 // compile-time constant: no register shifting, and the block a frame opens (its
 // last, k+NB-1 for frame k) starts from a literal zero instead of a cleared
 // register (the register held a block already produced).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>()), ...);
+}
+// f(integral_constant<int, i>) for i = 0 .. n-1
+template <int n, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_(f, std::make_integer_sequence<int, n>());
+}
+
 template <int NB>
 struct PairRot {
     static constexpr int R = NB == 1 ? 4 : NB == 2 ? 6 : NB == 4 ? 8 : 16;
@@ -158,68 +178,124 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
         }
     };
     const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + wid.yo, span_bytes(a.out_len, cs));
+#if CRLOT_PAIR_PKA
+    const __amdgpu_buffer_rsrc_t rp2 = dev::make_rsrc(a.t.pden2, uint32_t(a.ring_blocks * H) * 16u);
+#else
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+#endif
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
-    // xr[slot][q]: sample lane + 64 q of the hop in that slot; bit j of hopok:
-    // hop k + j (k = the current pair) keeps the paired regime
+    // XR(slot, q): sample lane + 64 q of the hop in that slot; bit j of hopok:
+    // hop k + j (k = the current pair) keeps the paired regime.  PK2: slots 2i and
+    // 2i+1 share a register pair (the pair's frames k, k+1 start on even slots), and
+    // so do OLA blocks 2i and 2i+1, so half the window products, half the OLA adds
+    // and every division of a frame pair run as packed operations, lane for lane
+    // the same IEEE operations as the scalar ones.
+#if CRLOT_PAIR_PKX
+    dev::pc xr2[R / 2][SH];
+#define XR(s, q) xr2[(s) / 2][q][(s) % 2]
+#else
     float xr[R][SH];
-    uint32_t hopok = 0;
+#define XR(s, q) xr[s][q]
+#endif
+#if CRLOT_PAIR_PKA
+    dev::pc acc2[NB / 2][SH];
+#define CRLOT_ACC(b, q) acc2[(b) / 2][q][(b) % 2]
 #pragma unroll
-    for (int h = 0; h <= NB; ++h) {
-        load_hop(xr[h], (fs + h) * H - a.pad);
-        hopok |= hop_ok_bits<SH>(xr[h], xlo_b, xhi_b) << h;
-    }
+    for (int j = 0; j < NB / 2; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc2[j][q] = dev::pc{0.f, 0.f};
+#else
     float acc[NB][SH];
+#define CRLOT_ACC(b, q) acc[b][q]
 #pragma unroll
     for (int j = 0; j < NB; ++j)
 #pragma unroll
         for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
+#endif
+    auto load_slot = [&](auto sc, int origin) {
+        constexpr int s = decltype(sc)::value;
+        float t[SH];
+        load_hop(t, origin);
+#pragma unroll
+        for (int q = 0; q < SH; ++q) XR(s, q) = t[q];
+    };
+    uint32_t hopok = 0;
+    auto slot_ok = [&](auto sc, int at) {
+        constexpr int s = decltype(sc)::value;
+        uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+        for (int q = 0; q < SH; ++q) {  // hop_ok_bits (fused_common.h)
+            const uint32_t u = __builtin_bit_cast(uint32_t, XR(s, q)) & 0x7fffffffu;
+            mx = max(mx, u);
+            mn = min(mn, u - 1u);
+        }
+        hopok |= (__builtin_amdgcn_ballot_w64((mx > xhi_b) | (mn < xlo_b - 1u)) == 0 ? 1u : 0u) << at;
+    };
+    static_for<NB + 1>([&](auto hc) {
+        constexpr int h = decltype(hc)::value;
+        load_slot(hc, (fs + h) * H - a.pad);
+        slot_ok(hc, h);
+    });
 
-    bool bad = false;  // this walk needs k_stft_ola_pair_fix: a pair left the paired regime or a division its exact range
-    // produce(H) of block k (values av): IEEE av / den by Markstein's correction.
+    // bad: the current pair needs k_stft_ola_pair_fix (it left the paired regime,
+    // an output fell below the sanitize threshold or a block outside Markstein's
+    // range).  Flagged pairs (frame offsets from fs) gather in two clusters, A and
+    // B: one within 2 NB frames of A's last joins A while B is empty, later ones
+    // open or extend B; the fix-up walker redoes the blocks each cluster touches.
     // The divisions run for warm-up blocks too, only their stores are dropped
     // (zero-size descriptor), so the divisor loads are used unconditionally and
     // vmcnt bookkeeping stays exact at the next wait.
-    auto emit = [&](const float (&av)[SH], int k, const float (&dr)[2 * SH]) {
-        // Markstein is exact for acc = 0 and |acc| in [2^-64, 2^64] (finite sums
-        // here): frexp exponents in [-63, 65], zero's being 0; any lane outside
-        // flags the walk for the IEEE division of the fix-up walker
-        int ex_lo = 0, ex_hi = 0;
-#pragma unroll
-        for (int q = 0; q < SH; ++q) {
-            const int e = __builtin_amdgcn_frexp_expf(av[q]);
-            ex_lo = min(ex_lo, e);
-            ex_hi = max(ex_hi, e);
-        }
-        const bool ok = (ex_lo >= -63) & (ex_hi <= 65);
-        float o[SH];
-#pragma unroll
-        for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
-        // outside Markstein's exact range the fix-up walker redoes the chunk with
-        // the IEEE division (a block of sums below 2^-64 or above 2^64)
-        bad |= !ok;
+    bool bad = false;
+    uint32_t a0 = ~0u, a1 = 0u, b0 = ~0u, b1 = 0u;
+    // (k = -1: past the chunk, dropped like a warm-up store)
+    auto store_block = [&](int k, const float (&o)[SH]) {
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
 #pragma unroll
         for (int q = 0; q < SH; ++q)
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * (4 * cs),
                                                   (k * (4 * H) + q * 256) * cs, ILV ? 0 : CRLOT_PAIR_ST_AUX);
     };
+#if !CRLOT_PAIR_PKA
+    // produce(H) of block k: IEEE acc / den by Markstein's correction.
+    // Markstein is exact for acc = 0 and |acc| in [2^-64, 2^64] (finite sums
+    // here): frexp exponents in [-63, 65], zero's being 0; any lane outside flags
+    // the walk for the IEEE division of the fix-up walker (a block of sums below
+    // 2^-64 or above 2^64)
+    auto mk_range = [&](const auto& sums) {
+        constexpr int n = sizeof(sums) / sizeof(float);
+        int ex_lo = 0, ex_hi = 0;
+#pragma unroll
+        for (int q = 0; q < n; ++q) {
+            const int e = __builtin_amdgcn_frexp_expf(sums[q]);
+            ex_lo = min(ex_lo, e);
+            ex_hi = max(ex_hi, e);
+        }
+        bad |= !((ex_lo >= -63) & (ex_hi <= 65));
+    };
+    auto emit = [&](int b, int k, const float (&dr)[2 * SH]) {
+        mk_range(acc[b]);
+        float o[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) o[q] = mk_div(acc[b][q], dr[q], dr[SH + q]);
+        store_block(k, o);
+    };
+#endif
 
     constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;  // hops k .. k+NB
 
     // One pair (frames k, k+1) at unroll position PH: hop k in slot S0, frame
-    // k's first block in acc[B0].
+    // k's first block in acc[B0] (both even).
     auto step = [&](auto phc, int k) {
         constexpr int PH = decltype(phc)::value;
         constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
         // prefetch hops k+NB+1, k+NB+2 for the next pairs (their slots are free)
-        load_hop(xr[(S0 + NB + 1) % R], (k + NB + 1) * H - a.pad);
-        load_hop(xr[(S0 + NB + 2) % R], (k + NB + 2) * H - a.pad);
+        load_slot(std::integral_constant<int, (S0 + NB + 1) % R>(), (k + NB + 1) * H - a.pad);
+        load_slot(std::integral_constant<int, (S0 + NB + 2) % R>(), (k + NB + 2) * H - a.pad);
         const bool paired = (hopok & kPairHops) == kPairHops;
-        bad |= !paired;
+        bad = !paired;
         {
             // z = frame k * w + i frame k+1 * w
             dev::pc v[E];
@@ -229,9 +305,13 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                 const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    const int m = 4 * m4 + u;
-                    v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wv[u],
-                                      xr[(S0 + 1 + m / SH) % R][m % SH] * wv[u]);
+                    const int m = 4 * m4 + u, s = (S0 + m / SH) % R;
+#if CRLOT_PAIR_PKX
+                    if ((m / SH) % 2 == 0)  // hops k + 2i, k + 2i + 1 share a register pair
+                        v[m] = xr2[s / 2][m % SH] * dev::pc{wv[u], wv[u]};
+                    else
+#endif
+                        v[m] = dev::pc_mk(XR(s, m % SH) * wv[u], XR((s + 1) % R, m % SH) * wv[u]);
                 }
             }
             // (frame k+1 = F past the last frame of an odd count still transforms
@@ -245,9 +325,14 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             // both blocks' divisors (L2-resident table) during the inverse, before
             // this pair's stores: vmcnt retires in order, so a load issued after
             // a store would also wait for that store
+#if CRLOT_PAIR_PKA
+            dev::pc d2[SH], r2[SH];  // (den_k, den_k+1) q and (rden_k, rden_k+1) q (DevTables::pden2)
+            load_den_pair<64, SH>(d2, r2, rp2, lane, k % a.ring_blocks);
+#else
             float dr0[2 * SH], dr1[2 * SH];
             load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
             load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+#endif
             dev::pair_fft_inv(v, buf, tw1, tw2, lane);
             // output sanitize (kissfft_adapter.cc:156-163): finite here, so only its
             // threshold |v| < 1e-30 N (= 2^-89.66 N / 1024) can act, and only on a
@@ -255,6 +340,9 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             // one such value sends the walk to k_stft_ola_pair_fix (a value in
             // [1e-30 N, 2^-89) too, harmlessly), otherwise the sanitize is the identity.
             static_assert(N == 1024, "threshold exponent");
+#if CRLOT_PAIR_OSCREEN  // (the same test, screened: fft_pair.h)
+            bad |= dev::out_min_exp_screened(v, 0x1p-89f) <= -89;
+#else
             {
                 int e[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -262,6 +350,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                     e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
                 bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -89;
             }
+#endif
             // push_frame_AoS of both frames: fma(fma(o, w, 0), g, acc), the window
             // product of both parts in one packed multiply (v * (w, w) gives -0
             // only where fma(o, w, 0) gives +0, and fma(-0, g, acc) == fma(+0, g, acc))
@@ -274,27 +363,51 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                 v[4 * m4 + 2] = v[4 * m4 + 2] * dev::pc{wh.x, wh.x};
                 v[4 * m4 + 3] = v[4 * m4 + 3] * dev::pc{wh.y, wh.y};
             }
+#if CRLOT_PAIR_PKA
+            // (ola_pair.h: both frames' adds, then the produce of blocks k and k+1)
+            ola_pair_push<E, SH, NB, B0>(acc2, v, g);
+            {
+                float o0[SH], o1[SH];
+                bad |= !mk_div_pair<SH>(acc2[B0 / 2], d2, r2, o0, o1);
+                store_block(k, o0);
+                store_block(k + 1 < f1 ? k + 1 : -1, o1);  // (past the chunk when k+1 == f1)
+            }
+            ola_pair_open<E, SH, NB, B0>(acc2, v, g);
+#else
             // frame k -> blocks k .. k+NB-1 (the last opens), produce block k
 #pragma unroll
             for (int m = 0; m < E; ++m) {
-                float& r = acc[(B0 + m / SH) % NB][m % SH];
-                r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
+                CRLOT_ACC((B0 + m / SH) % NB, m % SH) =
+                    __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : CRLOT_ACC((B0 + m / SH) % NB, m % SH));
             }
-            emit(acc[B0], k, dr0);
+            emit(B0, k, dr0);
             // frame k+1 -> blocks k+1 .. k+NB (k+NB opens in acc[B0]), produce block k+1
             // (past the chunk when k+1 == f1: dropped like a warm-up store)
 #pragma unroll
             for (int m = 0; m < E; ++m) {
-                float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
-                r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
+                CRLOT_ACC((B0 + 1 + m / SH) % NB, m % SH) =
+                    __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : CRLOT_ACC((B0 + 1 + m / SH) % NB, m % SH));
             }
-            emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
+            emit((B0 + 1) % NB, k + 1 < f1 ? k + 1 : -1, dr1);
+#endif
+        }
+        {  // (selects, no branch: wave-uniform scalar state)
+            const bool f = __builtin_amdgcn_ballot_w64(bad) != 0;
+            const uint32_t o = uint32_t(k - fs);
+            const bool new_a = f & (a0 == ~0u);
+            const bool to_a = f & !new_a & (b0 == ~0u) & (o <= a1 + 2 * NB);
+            const bool to_b = f & !new_a & !to_a;
+            a0 = new_a ? o : a0;
+            a1 = (new_a | to_a) ? o : a1;
+            b0 = (to_b & (b0 == ~0u)) ? o : b0;
+            b1 = to_b ? o : b1;
         }
 #ifdef CRLOT_ABL_NOHOPCHK  // timing-only ablation
         hopok = ~0u;
 #else
-        hopok = (hopok | hop_ok_bits<SH>(xr[(S0 + NB + 1) % R], xlo_b, xhi_b) << (NB + 1) |
-                 hop_ok_bits<SH>(xr[(S0 + NB + 2) % R], xlo_b, xhi_b) << (NB + 2)) >> 2;
+        slot_ok(std::integral_constant<int, (S0 + NB + 1) % R>(), NB + 1);
+        slot_ok(std::integral_constant<int, (S0 + NB + 2) % R>(), NB + 2);
+        hopok >>= 2;
 #endif
     };
     for (int k = fs; k < f1; k += 2 * U) {
@@ -322,9 +435,19 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             step(std::integral_constant<int, 7>(), k + 14);
         }
     }
-    const bool any_bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-    if (lane == 0) a.t.pflags[gw] = any_bad ? 1u : 0u;
+    // flag words of the walker (cluster A at gw, B at gw + walkers): pair offsets
+    // from fs + 1 of its first and last pair, 16 bits each; 1 = the whole chunk
+    // (offsets that do not fit), 0 = nothing to redo
+    const uint32_t pl = (b0 != ~0u ? b1 : a1) / 2u + 1u;
+    const uint32_t fa = a0 == ~0u ? 0u : pl >= 0xffffu ? 1u : (a0 / 2u + 1u) | (a1 / 2u + 1u) << 16;
+    const uint32_t fb = (b0 == ~0u || pl >= 0xffffu) ? 0u : (b0 / 2u + 1u) | (b1 / 2u + 1u) << 16;
+    if (lane == 0) {
+        a.t.pflags[gw] = fa;
+        a.t.pflags[gw + a.n_streams * a.n_chunks] = fb;
+    }
 }
+#undef CRLOT_ACC
+#undef XR
 
 
 // K_pair fix-up walker k_stft_ola_pair_fix: the walk with both regimes, run
@@ -387,9 +510,27 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     const WalkId wid = walk_id<ILV>(a, gw);
     const int c = wid.c;
     const int cs = ILV ? a.cs : 1;  // interleaved groups: zero padding only (host-checked)
-    const int f0 = c * a.M;
-    const int f1 = min(a.F, f0 + a.M);
-    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
+    // Block ranges to redo.  The hot walker's flag words name up to two clusters of
+    // pairs it could not finish (first and last pair, offsets from its walk start
+    // + 1, low / high halves; 1: the whole chunk): the blocks a cluster touches,
+    // [k_first, k_last + NB], are redone from NB-1 frames of warm-up before them.
+    const int c0 = c * a.M, c1 = min(a.F, c0 + a.M);
+    int rng[2][2] = {{c0, c1}, {c0, c0}};
+    {
+        const uint32_t fa = a.fix_all ? 1u : a.t.pflags[gw];
+        if (fa > 1u) {
+            const uint32_t fb = a.t.pflags[gw + a.n_streams * a.n_chunks];
+            const int ws0 = max(0, c0 - (NB - 1)) & ~1;
+            const uint32_t fl[2] = {fa, fb};
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                if (fl[r] > 1u) {
+                    rng[r][0] = max(c0, ws0 + 2 * int((fl[r] & 0xffffu) - 1u));
+                    rng[r][1] = min(c1, ws0 + 2 * int((fl[r] >> 16) - 1u) + NB + 1);
+                }
+        }
+    }
+    int f0 = c0, f1 = c1;  // the range being redone
     const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + wid.xo, span_bytes(a.T, cs));
     const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + wid.yo, span_bytes(a.out_len, cs));
     const HopRsrc<ILV ? SH : 1> rxq = hop_rsrc<ILV ? SH : 1>(a.x + wid.xo, ILV ? a.T : 0, cs);
@@ -404,6 +545,11 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
+    for (int r = 0; r < 2; ++r) {
+    f0 = rng[r][0];
+    f1 = rng[r][1];
+    if (f0 >= f1) continue;
+    const int fs = max(0, f0 - (NB - 1)) & ~1;  // pairs start on even frames
     // xin[h*SH + q]: hop (k + h), h = 0..NB, sample lane + 64 q of the hop;
     // bit h of hopok: hop k + h keeps the paired regime
     float xin[E + SH];
@@ -550,6 +696,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
 #pragma unroll
         for (int q = 0; q < 2 * SH; ++q) xin[E - SH + q] = nxt[q];
     }
+    }  // ranges
 }
 
 
@@ -618,6 +765,8 @@ hipError_t pair_sh(const FusedArgs& a, int64_t waves, hipStream_t stream) {
         }
 #endif
         if (a.pad_mode == 0 && a.t.hot && (!a.t.gain || CRLOT_PAIR_REG_TW)) {
+            if (CRLOT_PAIR_PKA && !a.t.pden2) return hipErrorInvalidValue;
+            if (a.t.pflags_len < 2 * waves) return hipErrorInvalidValue;  // two flag words per walker
             auto k = a.t.gain ? k_stft_ola_pair<SH, NB, W, ILV, CRLOT_PAIR_REG_TW != 0> : k_stft_ola_pair<SH, NB, W, ILV, false>;
             if ((e = set_lds(k, lds)) != hipSuccess) return e;
             note_launch(CRLOT_K_PAIR_HOT, grid);

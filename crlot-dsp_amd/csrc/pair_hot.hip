@@ -28,6 +28,7 @@
 #include "fft_pair4k.h"
 #include "fft_pair512.h"
 #include "fused_common.h"
+#include "ola_pair.h"
 
 namespace crlot {
 namespace fk {
@@ -40,6 +41,14 @@ namespace {
 #ifndef CRLOT_HOT_AUX
 #define CRLOT_HOT_AUX 0
 #endif
+// The OLA stage on block pairs (ola_pair.h) and the screened output-sanitize test
+// (fft_pair.h out_min_exp_screened), as K_pair's hot walker (pair1k.hip).
+#ifndef CRLOT_HOT_PK
+#define CRLOT_HOT_PK 1
+#endif
+
+// 2^e as a float (e a normal exponent)
+constexpr float pow2f(int e) { return __builtin_bit_cast(float, uint32_t(127 + e) << 23); }
 
 // Exchange rows: a wave's own rows hold its 1152-element transpose buffer, and
 // the row stride keeps the lane groups of a 32-lane b64 access on distinct
@@ -230,7 +239,11 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
     const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+#if CRLOT_HOT_PK
+    const __amdgpu_buffer_rsrc_t rp2 = dev::make_rsrc(a.t.pden2, uint32_t(a.ring_blocks * H) * 16u);
+#else
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
+#endif
     const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
@@ -271,6 +284,20 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         load_hop_wg0<L, SH>(xr[h], rx, t, (fs + h) * H - a.pad);
         hop_check(xr[h]);
     }
+    auto store_block = [&](int k, const float (&o)[SH]) {  // (k = -1: dropped)
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
+                                                  k * (4 * H) + q * (4 * L), CRLOT_HOT_AUX);
+    };
+#if CRLOT_HOT_PK
+    dev::pc acc2[NB / 2][SH];
+#pragma unroll
+    for (int j = 0; j < NB / 2; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc2[j][q] = dev::pc{0.f, 0.f};
+#else
     float acc[NB][SH];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
@@ -291,12 +318,9 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         float o[SH];
 #pragma unroll
         for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
-        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-#pragma unroll
-        for (int q = 0; q < SH; ++q)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, t * 4,
-                                                  k * (4 * H) + q * (4 * L), CRLOT_HOT_AUX);
+        store_block(k, o);
     };
+#endif
 
     auto step = [&](auto phc, int k) {
         constexpr int PH = decltype(phc)::value;
@@ -314,12 +338,20 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #pragma unroll
             for (int d = 0; d < E; ++d) v[d] = v[d] * gr[d];
         }
+#if CRLOT_HOT_PK
+        dev::pc d2[SH], r2[SH];
+        load_den_pair<L, SH>(d2, r2, rp2, t, k % a.ring_blocks);
+#else
         float dr0[2 * SH], dr1[2 * SH];
         load_den_wg<L, SH>(dr0, rp, t, k % a.ring_blocks);
         load_den_wg<L, SH>(dr1, rp, t, (k + 1) % a.ring_blocks);
+#endif
         G::inv(v, B, tw, t, wave);
         // output sanitize: finite here, so only its threshold |v| < 1e-30 N can
         // act; frexp exponents <= G::MIN_EXP flag the chunk
+#if CRLOT_HOT_PK
+        bad |= dev::out_min_exp_screened(v, pow2f(G::MIN_EXP)) <= G::MIN_EXP;
+#else
         {
             int e[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -327,8 +359,19 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
                 e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
             bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= G::MIN_EXP;
         }
+#endif
 #pragma unroll
         for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
+#if CRLOT_HOT_PK
+        ola_pair_push<E, SH, NB, B0>(acc2, v, g);
+        {
+            float o0[SH], o1[SH];
+            bad |= !mk_div_pair<SH>(acc2[B0 / 2], d2, r2, o0, o1);
+            store_block(k, o0);
+            store_block(k + 1 < f1 ? k + 1 : -1, o1);
+        }
+        ola_pair_open<E, SH, NB, B0>(acc2, v, g);
+#else
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + m / SH) % NB][m % SH];
@@ -341,6 +384,7 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
             r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
         }
         emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
+#endif
         hop_check(xr[(S0 + NB + 1) % R]);
         hop_check(xr[(S0 + NB + 2) % R]);
     };
@@ -406,7 +450,7 @@ hipError_t launch_pair2k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { ret
 // ---- N = 512: one wave per chunk (W per workgroup, independent), lane l holds
 // samples l + 64 m (m < 8); flags per wave.
 template <int SH, int NB, int W>
-__global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
+__global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) {  // (4 waves per SIMD)
     constexpr int E = 8, N = 512, H = 64 * SH;
     constexpr int R = RotWg<NB>::R, U = RotWg<NB>::U;
     static_assert(NB * SH == E, "N = NB * H");
@@ -425,7 +469,11 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
     const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, uint32_t(a.T) * 4u);
     const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+#if CRLOT_HOT_PK
+    const __amdgpu_buffer_rsrc_t rp2 = dev::make_rsrc(a.t.pden2, uint32_t(a.ring_blocks * H) * 16u);
+#else
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+#endif
     const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
@@ -454,6 +502,20 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
         load_hop_w<SH>(xr[h], rx, lane, (fs + h) * H - a.pad);
         hop_check(xr[h]);
     }
+    auto store_block = [&](int k, const float (&o)[SH]) {  // (k = -1: dropped)
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int q = 0; q < SH; ++q)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
+                                                  k * (4 * H) + q * 256, CRLOT_HOT_AUX);
+    };
+#if CRLOT_HOT_PK
+    dev::pc acc2[NB / 2][SH];
+#pragma unroll
+    for (int j = 0; j < NB / 2; ++j)
+#pragma unroll
+        for (int q = 0; q < SH; ++q) acc2[j][q] = dev::pc{0.f, 0.f};
+#else
     float acc[NB][SH];
 #pragma unroll
     for (int j = 0; j < NB; ++j)
@@ -471,12 +533,9 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
         float o[SH];
 #pragma unroll
         for (int q = 0; q < SH; ++q) o[q] = mk_div(av[q], dr[q], dr[SH + q]);
-        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-#pragma unroll
-        for (int q = 0; q < SH; ++q)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[q]), rk, lane * 4,
-                                                  k * (4 * H) + q * 256, CRLOT_HOT_AUX);
+        store_block(k, o);
     };
+#endif
     auto step = [&](auto phc, int k) {
         constexpr int PH = decltype(phc)::value;
         constexpr int S0 = (2 * PH) % R, B0 = (2 * PH) % NB;
@@ -489,19 +548,39 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
             v[m] = dev::pc_mk(xr[(S0 + m / SH) % R][m % SH] * wa[m],
                               partner ? xr[(S0 + 1 + m / SH) % R][m % SH] * wa[m] : 0.0f);
         dev::pair512_fwd(v, buf, tw, lane);
+#if CRLOT_HOT_PK
+        dev::pc d2[SH], r2[SH];
+        load_den_pair<64, SH>(d2, r2, rp2, lane, k % a.ring_blocks);
+#else
         float dr0[2 * SH], dr1[2 * SH];
         load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
         load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+#endif
         dev::pair512_inv(v, buf, tw, lane);
-        {  // output sanitize threshold 1e-30 N = 2^-90.66: frexp exponents <= -90 flag the chunk
+        // output sanitize threshold 1e-30 N = 2^-90.66: frexp exponents <= -90 flag the chunk
+#if CRLOT_HOT_PK
+        bad |= dev::out_min_exp_screened(v, pow2f(-90)) <= -90;
+#else
+        {
             int e[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int m = 0; m < E; ++m)
                 e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
             bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -90;
         }
+#endif
 #pragma unroll
         for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
+#if CRLOT_HOT_PK
+        ola_pair_push<E, SH, NB, B0>(acc2, v, g);
+        {
+            float o0[SH], o1[SH];
+            bad |= !mk_div_pair<SH>(acc2[B0 / 2], d2, r2, o0, o1);
+            store_block(k, o0);
+            store_block(k + 1 < f1 ? k + 1 : -1, o1);
+        }
+        ola_pair_open<E, SH, NB, B0>(acc2, v, g);
+#else
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + m / SH) % NB][m % SH];
@@ -514,6 +593,7 @@ __global__ __launch_bounds__(64 * W) void k_pair512_hot(const FusedArgs a) {
             r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
         }
         emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
+#endif
         hop_check(xr[(S0 + NB + 1) % R]);
         hop_check(xr[(S0 + NB + 2) % R]);
     };

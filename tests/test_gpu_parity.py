@@ -1115,6 +1115,42 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     assert np.array_equal(bits(y_hot), bits(y_gain1))
 
 
+@pytest.mark.parametrize("h", [128, 256, 512])
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_pair_hot_walker_partial_redo(pkg, oracle, torch_cuda, h, chunks):
+    """K_pair's hot walker flags the first and last pair of a chunk it cannot
+    finish (out-of-range samples, outputs under the sanitize threshold's screen --
+    exact zeros from zero-padded stream ends or silence -- or block sums outside
+    Markstein's range), and the fix-up walker redoes only the blocks those pairs
+    touch.  Bursts far apart in one long chunk, silence (exempt), isolated exact
+    zeros, tiny and huge samples, sums near the Markstein limits: the result is
+    bit-identical to the two-regime walker over every chunk and within the oracle's
+    float32 tolerance."""
+    torch = torch_cuda
+    n, T = 1024, 60_001
+    x = oracle.synth_streams(6, T, config_id=79)
+    x[0, 1_000:1_005] = 1e25                 # early burst ...
+    x[0, 52_000] = np.nan                    # ... and a late one in the same chunk
+    x[1, 10_000:30_000] = 0.0                # silence (the screen exempts all-zero pairs)
+    x[1, 40_000:40_300] = 0.0                # a short gap: pairs with some zero hops
+    x[2, ::997] = 0.0                        # isolated exact zeros
+    x[3, 20_000:20_020] = 1e-33              # tiny samples: outside the paired range
+    x[4, 30_000:31_000] *= 2.0 ** -70        # quiet: block sums below Markstein's range
+    x[5, 5_000:5_100] *= 2.0 ** 65           # loud (|x| <= 2^64, still paired): block sums above 2^64
+    xd = dev(torch, x)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_chunks(chunks)
+    y_hot = host(plan.roundtrip(xd))
+    assert plan.last_launch()["kernels"] == ["k_pair_hot", "k_pair_fix"]
+    plan.set_frame_pairing(2)
+    y_fix = host(plan.roundtrip(xd))
+    plan.set_chunks(0)
+    plan.set_frame_pairing(1)
+    assert np.array_equal(bits(y_hot), bits(y_fix))
+    for s in (1, 2):  # the finite, ordinary streams against the oracle
+        assert_close(y_hot[s], oracle.roundtrip(x[s], n, h), 1.0, f"stream {s}")
+
+
 @pytest.mark.parametrize("n,h,T,ilv", [(1024, 256, 50_000, 1), (1024, 256, 33_001, 3), (1024, 256, 2_000, 1),
                                        (4096, 1024, 123_457, 1), (4096, 1024, 9_000, 1), (1024, 512, 40_000, 1),
                                        (1024, 128, 20_000, 1)])
