@@ -225,10 +225,15 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     uint32_t hopok = 0;
     auto slot_ok = [&](auto sc, int at) {
         constexpr int s = decltype(sc)::value;
+        // (each sample copied to a scalar before the bit cast: a bit cast applied to a
+        // vector element directly is miscompiled by this clang)
+        float h[SH];
+#pragma unroll
+        for (int q = 0; q < SH; ++q) h[q] = XR(s, q);
         uint32_t mx = 0u, mn = ~0u;
 #pragma unroll
         for (int q = 0; q < SH; ++q) {  // hop_ok_bits (fused_common.h)
-            const uint32_t u = __builtin_bit_cast(uint32_t, XR(s, q)) & 0x7fffffffu;
+            const uint32_t u = __builtin_bit_cast(uint32_t, h[q]) & 0x7fffffffu;
             mx = max(mx, u);
             mn = min(mn, u - 1u);
         }
