@@ -130,16 +130,16 @@ __device__ __forceinline__ int frexp_min_if(const pc* a, float smin, int e, floa
     return e;
 }
 // The output sanitize's threshold test of the hot walkers, screened: the
-// smallest frexp exponent over the E registers' 2E values (zero's being 0), as
+// smallest frexp exponent over the first E registers' 2E values (zero's being 0), as
 // min over every value would give wherever it can reach 2^MIN_EXP.  The window-edge
 // registers (0 and E-1: the taps a window zeroes, whose outputs are often exact
 // zeros) take the exact test; elsewhere min |v| >= thr on every lane (half a
 // v_min3 per value) proves the test passes, and only a wave where some lane fails
 // the screen (exact zero outputs: silence, zero-padded stream ends; or a tiny
 // one) runs the exact test on the interior registers as well.
-template <int E>
-__device__ __forceinline__ int out_min_exp_screened(const pc (&v)[E], float thr) {
-    static_assert(E == 8 || E == 16, "registers");
+template <int E, int NV>
+__device__ __forceinline__ int out_min_exp_screened(const pc (&v)[NV], float thr) {
+    static_assert((E == 8 || E == 15 || E == 16) && NV >= E, "registers");
     const int e0 = min(min(__builtin_amdgcn_frexp_expf(v[0].x), __builtin_amdgcn_frexp_expf(v[0].y)),
                        min(__builtin_amdgcn_frexp_expf(v[E - 1].x), __builtin_amdgcn_frexp_expf(v[E - 1].y)));
     float s2[2] = {0x1p100f, 0x1p100f};
@@ -147,7 +147,7 @@ __device__ __forceinline__ int out_min_exp_screened(const pc (&v)[E], float thr)
     for (int m = 1; m < E - 1; ++m) s2[m & 1] = min3_abs(v[m].x, v[m].y, s2[m & 1]);
     const float sm = __builtin_fminf(s2[0], s2[1]);
     int e = frexp_min_if(v + 1, sm, e0, thr);
-    if constexpr (E == 16) e = frexp_min_if(v + 8, sm, e, thr);
+    if constexpr (E > 8) e = frexp_min_if(v + 8, sm, e, thr);  // (E = 15: v[8..14])
     return e;
 }
 template <bool INV>

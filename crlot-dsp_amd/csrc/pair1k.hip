@@ -346,7 +346,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             // [1e-30 N, 2^-89) too, harmlessly), otherwise the sanitize is the identity.
             static_assert(N == 1024, "threshold exponent");
 #if CRLOT_PAIR_OSCREEN  // (the same test, screened: fft_pair.h)
-            bad |= dev::out_min_exp_screened(v, 0x1p-89f) <= -89;
+            bad |= dev::out_min_exp_screened<E>(v, 0x1p-89f) <= -89;
 #else
             {
                 int e[4] = {0, 0, 0, 0};

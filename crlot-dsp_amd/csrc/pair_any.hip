@@ -325,15 +325,11 @@ void k_pair15_hot(const FusedArgs a) {
         }
         P15<L>::inv(v, buf, tw, lane);
         // o = v / N; its sanitize threshold 1e-30 = 2^-99.66: frexp exponents <= -99 flag the walk
-        {
-            int e[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int m = 0; m < E; ++m) {
-                v[m] = v[m] * dev::pc{inv_n, inv_n};
-                e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
-            }
-            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -99;
-        }
+        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{inv_n, inv_n};
+        // (screened: fft_pair.h out_min_exp_screened; the window-edge taps n < L and
+        // n >= N - L sit in registers 0 and E-1)
+        bad |= dev::out_min_exp_screened<E>(v, 0x1p-99f) <= -99;
         float p[E];
 #pragma unroll
         for (int m4 = 0; m4 < 4; ++m4) {

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
         // output sanitize: finite here, so only its threshold |v| < 1e-30 N can
         // act; frexp exponents <= G::MIN_EXP flag the chunk
 #if CRLOT_HOT_PK
-        bad |= dev::out_min_exp_screened(v, pow2f(G::MIN_EXP)) <= G::MIN_EXP;
+        bad |= dev::out_min_exp_screened<E>(v, pow2f(G::MIN_EXP)) <= G::MIN_EXP;
 #else
         {
             int e[4] = {0, 0, 0, 0};
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) { 
         dev::pair512_inv(v, buf, tw, lane);
         // output sanitize threshold 1e-30 N = 2^-90.66: frexp exponents <= -90 flag the chunk
 #if CRLOT_HOT_PK
-        bad |= dev::out_min_exp_screened(v, pow2f(-90)) <= -90;
+        bad |= dev::out_min_exp_screened<E>(v, pow2f(-90)) <= -90;
 #else
         {
             int e[4] = {0, 0, 0, 0};

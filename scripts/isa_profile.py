@@ -39,17 +39,26 @@ def loop_hist(asm, pat):
             loops.append((labels[mm.group(1)], i))
     a, b = max(loops, key=lambda t: t[1] - t[0])
     c = collections.Counter()
+    skip = False  # inside a frexp_min_if fallback: skipped unless the output screen fails
     for l in body[a:b + 1]:
         t = l.strip().split()
+        if not t:
+            continue
+        if t[0] == "s_cbranch_vccz" and ".Lfx_skip" in l:
+            skip = True
+        elif t[0].startswith(".Lfx_skip"):
+            skip = False
         if t and not t[0].startswith((".", ";")):
-            c[t[0]] += 1
+            c[("fallback:" if skip and t[0] != "s_cbranch_vccz" else "") + t[0]] += 1
     return m.group(1), c
 
 
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     out = {"tag": tag, "note": "main loop = the longest backward branch span of the kernel; "
-           "counts are static instructions in it (every one issues once per iteration)", "kernels": []}
+           "counts are static instructions in it (every one issues once per iteration), except the "
+           "exact sanitize test inside the frexp_min_if asm blocks, which runs only when the output "
+           "screen fails (loop_valu_fallback_skipped, not in loop_valu)", "kernels": []}
     asm_cache = {}
     with tempfile.TemporaryDirectory() as td:
         for src, pat, pairs, label in KERNELS:
@@ -63,6 +72,8 @@ def main():
             if c is None:
                 print("not found:", pat, file=sys.stderr)
                 continue
+            fb = sum(v for k, v in c.items() if k.startswith("fallback:v_"))
+            c = collections.Counter({k: v for k, v in c.items() if not k.startswith("fallback:")})
             valu = sum(v for k, v in c.items() if k.startswith("v_"))
             pk = sum(v for k, v in c.items() if k.startswith("v_pk_"))
             perm = sum(v for k, v in c.items() if "permlane" in k)
@@ -72,6 +83,7 @@ def main():
                    "loop_barriers": c.get("s_barrier", 0),
                    "loop_salu": sum(v for k, v in c.items() if k.startswith("s_")),
                    "loop_vmem": sum(v for k, v in c.items() if k.startswith(("buffer_", "global_"))),
+                   "loop_valu_fallback_skipped": fb,
                    "top": dict(c.most_common(30))}
             if pairs:
                 rec["pairs_per_iteration"] = pairs

@@ -1103,6 +1103,7 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     x = oracle.synth_streams(6, T, config_id=71)
     x[2, T // 3:T // 3 + 5] = 1e25   # unpaired regime: that chunk is redone
     x[4, T // 2] = 1e-33              # tiny sample: also outside the paired range
+    quiet_with_zeros(x[5], T // 4, 3 * n)  # paired, but some outputs under the sanitize threshold
     xd = dev(torch, x)
     plan = pkg.Plan(frame_size=n, hop_size=h)
     y_hot = host(plan.roundtrip(xd))
@@ -1113,6 +1114,18 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     plan.set_spectral_gain(np.ones(n // 2 + 1, np.float32))
     y_gain1 = host(plan.roundtrip(xd))
     assert np.array_equal(bits(y_hot), bits(y_gain1))
+
+
+def quiet_with_zeros(row, at, length):
+    """A paired-regime stretch whose round trip has outputs under the sanitize
+    threshold: samples of 2-4e-25 (above px_lo, so no hop leaves the paired regime)
+    with an exact zero every 97 samples, whose taps come back as round-off of about
+    1e-29 -- nonzero and below 1e-30 N.  The hot walkers' output screen fails there
+    and only the exact test behind it (fft_pair.h frexp_min_if) can flag the pair."""
+    rng = np.random.default_rng(at)
+    seg = rng.uniform(2e-25, 4e-25, length).astype(np.float32) * rng.choice([-1.0, 1.0], length).astype(np.float32)
+    seg[::97] = 0.0
+    row[at:at + length] = seg
 
 
 @pytest.mark.parametrize("h", [128, 256, 512])
@@ -1137,6 +1150,7 @@ def test_pair_hot_walker_partial_redo(pkg, oracle, torch_cuda, h, chunks):
     x[3, 20_000:20_020] = 1e-33              # tiny samples: outside the paired range
     x[4, 30_000:31_000] *= 2.0 ** -70        # quiet: block sums below Markstein's range
     x[5, 5_000:5_100] *= 2.0 ** 65           # loud (|x| <= 2^64, still paired): block sums above 2^64
+    quiet_with_zeros(x[5], 40_000, 4_000)    # outputs under the sanitize threshold, paired inputs
     xd = dev(torch, x)
     plan = pkg.Plan(frame_size=n, hop_size=h)
     plan.set_chunks(chunks)
