@@ -23,6 +23,9 @@ SIZES = [0, 1, 7, 8, 15, 16, 31, 32, 63, 64, 127, 128, 255, 256, 511, 512, 1023,
 
 
 def bits(a):
+    """Bit patterns of a float32 array; complex64 spectra as their (re, im) pairs."""
+    if np.iscomplexobj(a):
+        return np.ascontiguousarray(a, np.complex64).view(np.float32).view(np.uint32)
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
