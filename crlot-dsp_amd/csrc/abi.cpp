@@ -173,7 +173,7 @@ crlot::DevTables tables(const crlot_plan* p, const crlot::Scratch* sc = nullptr)
             t.pden = p->d_pden;
         }
         const int n = p->geo.n;
-        if (n == 512 || n == 1024 || n == 2048 || n == 4096) t.pden2 = p->d_pden + 2 * p->geo.ring_len;
+        if (p->d_pden && (n == 512 || n == 1024 || n == 2048 || n == 4096)) t.pden2 = p->d_pden + 2 * p->geo.ring_len;
         if (sc) {
             t.pflags = sc->pflags;
             t.pflags_len = sc->pflags_len;

@@ -415,6 +415,7 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 template <typename G>
 hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream) {
     constexpr size_t lds = hot_lds<G>();
+    if (CRLOT_HOT_PK && !a.t.pden2) return hipErrorInvalidValue;  // the block-pair divisor rows
     auto go = [&](auto k) {
         hipError_t e = set_lds(k, lds);
         if (e != hipSuccess) return e;
@@ -622,7 +623,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) { 
 
 hipError_t launch_pair512_hot(int sh, const FusedArgs& a, int64_t waves, int w, hipStream_t stream) {
     constexpr int W = 4;
-    if (w != W) return hipErrorInvalidValue;
+    if (w != W || (CRLOT_HOT_PK && !a.t.pden2)) return hipErrorInvalidValue;
     const size_t lds = sizeof(dev::pc) * dev::kP512Buf * W;
     const int64_t grid = (waves + W - 1) / W;
     auto go = [&](auto k) {
