@@ -74,7 +74,21 @@ bool pn_lean(int n) {
 int pn_key(int n) {
     return n + 100000 * pn_variant(n) + 1000000 * (pn_halves(n) - 1) + 10000000 * (pn_lean(n) ? 1 : 0);
 }
+// N = 1764 as two 882-point halves on two waves (experiments/pairn_dit.inc,
+// -DCRLOT_PN_DIT_EXPERIMENT builds only: measured 14 % slower than the two-wave
+// 1764-point transform)
+constexpr int kDitHalf = 882;  // the half transform's plan key (one wave, fft_pairn.h)
+bool pn_dit(int n) {
+#ifdef CRLOT_PN_DIT_EXPERIMENT
+    return n == 2 * kDitHalf && pn_halves(n) == 2 && !pn_lean(n) && pn_variant(n) == 0;
+#else
+    (void)n;
+    return false;
+#endif
+}
 size_t pn_tables(int n) {
+    if (pn_dit(n))  // half-plan twiddles | W1764^k (k < 882) | windows
+        return sizeof(dev::pc) * size_t(dev::pn_factor(kDitHalf).tw_len + kDitHalf) + sizeof(float) * 2 * size_t(n);
     return sizeof(dev::pc) * size_t(dev::pn_factor(pn_key(n)).tw_len) + (pn_lean(n) ? 0 : sizeof(float) * 2 * size_t(n));
 }
 size_t pn_per_walk(int n, int h) {
@@ -327,6 +341,10 @@ void k_pairn(const FusedArgs a) {
     if (lane == 0) a.t.pflags[gw * HALVES + half] = bal != 0 ? 1u : 0u;
 }
 
+#ifdef CRLOT_PN_DIT_EXPERIMENT
+#include "experiments/pairn_dit.inc"
+#endif
+
 namespace {
 // the instantiated sizes
 template <typename F>
@@ -430,6 +448,15 @@ hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, f
     note_chunks(a.n_chunks);
     const size_t lds = pn_tables(g.n) + size_t(walks) * pn_per_walk(g.n, g.h);
     hipError_t e = hipSuccess;
+#ifdef CRLOT_PN_DIT_EXPERIMENT
+    if (pn_dit(g.n)) {  // 1764 = 2 x 882 on two waves (k_pairn_dit)
+        auto k = t.gain ? k_pairn_dit<true> : k_pairn_dit<false>;
+        if ((e = set_lds(k, lds)) != hipSuccess) return e;
+        note_launch(CRLOT_K_PAIRN, (total + walks - 1) / walks);
+        hipLaunchKernelGGL(k, dim3(unsigned((total + walks - 1) / walks)), dim3(128 * walks), lds, stream, a);
+        return hipGetLastError();
+    }
+#endif
     pn_dispatch(pn_key(g.n), [&](auto nc) {
         constexpr int NN = decltype(nc)::value;
         auto k = t.gain ? k_pairn<NN, true> : k_pairn<NN, false>;
@@ -442,9 +469,17 @@ hipError_t launch_pairn(const Geometry& g, const DevTables& t, const float* x, f
 }
 
 // W_{ns r}^{q jm} per pass of fft_pairn.h's factorisation, float pairs
+// (1764 by decimation in time: the 882-point plan's, then W1764^k for k < 882)
 std::vector<float> build_pairn_twiddles(int n) {
-    const dev::PnFac f = dev::pn_factor(fk::pn_key(n));
+    const bool dit = fk::pn_dit(n);
+    const dev::PnFac f = dev::pn_factor(dit ? fk::kDitHalf : fk::pn_key(n));
     std::vector<float> t(2 * size_t(f.tw_len));
+    if (dit)
+        for (int k = 0; k < n / 2; ++k) {
+            const double ph = -2.0 * M_PI * double(k) / double(n);
+            t.push_back(float(std::cos(ph)));
+            t.push_back(float(std::sin(ph)));
+        }
     for (int i = 0; i < f.n; ++i)
         for (int q = 1; q < f.r[i]; ++q)
             for (int jm = 0; jm < f.ns[i]; ++jm) {
