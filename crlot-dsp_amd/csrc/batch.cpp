@@ -52,6 +52,7 @@ hipError_t hgrow(float** p, size_t* cap, size_t need) {
 
 // the forward input of frame j, as the loop forms it on the host (frame * w)
 bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
+    if (b.rows_src) return std::memcmp(in, b.rows.data() + size_t(j) * size_t(b.n), sizeof(float) * size_t(b.n)) == 0;
     const int64_t L = int64_t(b.sig.size()), base = j * b.h;
     for (int64_t i = 0; i < b.n; ++i) {
         const int64_t t = base + i;
@@ -69,16 +70,25 @@ int run_chain(BatchSpec* b, crlot_plan* inner) {
         return hip_fail(e, "batch stream");
     if (!b->ev && (e = hipEventCreateWithFlags(&b->ev, hipEventDisableTiming)) != hipSuccess)
         return hip_fail(e, "batch event");
-    if ((e = dgrow(&b->d_sig, &b->c_sig, L + N)) || (e = dgrow(&b->d_p, &b->c_p, M * N)) ||
-        (e = dgrow(&b->d_spec, &b->c_spec, M * row)) || (e = dgrow(&b->d_r, &b->c_r, M * N)) ||
-        (e = hgrow(&b->h_stage, &b->c_hs, L + N)) || (e = hgrow(&b->h_spec, &b->c_hspec, M * row)) ||
+    if ((e = dgrow(&b->d_p, &b->c_p, M * N)) || (e = dgrow(&b->d_spec, &b->c_spec, M * row)) ||
+        (e = dgrow(&b->d_r, &b->c_r, M * N)) || (e = hgrow(&b->h_spec, &b->c_hspec, M * row)) ||
         (e = hgrow(&b->h_r, &b->c_hr, M * N)))
         return hip_fail(e, "batch buffers");
-    std::memcpy(b->h_stage, b->sig.data(), sizeof(float) * L);
-    std::memcpy(b->h_stage + L, b->win.data(), sizeof(float) * N);
-    if ((e = hipMemcpyAsync(b->d_sig, b->h_stage, sizeof(float) * (L + N), hipMemcpyHostToDevice, b->s)) ||
-        (e = launch_windowed_frames(b->d_sig, int64_t(L), b->d_sig + L, b->d_p, b->M, b->n, b->h, b->s)))
-        return hip_fail(e, "batch frames");
+    if (b->rows_src) {  // the FrameQueue's rows are the forward inputs
+        if ((e = hgrow(&b->h_stage, &b->c_hs, M * N)) == hipSuccess) {
+            std::memcpy(b->h_stage, b->rows.data(), sizeof(float) * M * N);
+            e = hipMemcpyAsync(b->d_p, b->h_stage, sizeof(float) * M * N, hipMemcpyHostToDevice, b->s);
+        }
+        if (e != hipSuccess) return hip_fail(e, "batch frames");
+    } else {
+        if ((e = dgrow(&b->d_sig, &b->c_sig, L + N)) || (e = hgrow(&b->h_stage, &b->c_hs, L + N)))
+            return hip_fail(e, "batch buffers");
+        std::memcpy(b->h_stage, b->sig.data(), sizeof(float) * L);
+        std::memcpy(b->h_stage + L, b->win.data(), sizeof(float) * N);
+        if ((e = hipMemcpyAsync(b->d_sig, b->h_stage, sizeof(float) * (L + N), hipMemcpyHostToDevice, b->s)) ||
+            (e = launch_windowed_frames(b->d_sig, int64_t(L), b->d_sig + L, b->d_p, b->M, b->n, b->h, b->s)))
+            return hip_fail(e, "batch frames");
+    }
     int rc = crlot_rfft_batched(inner, b->d_p, b->d_spec, int32_t(M), int64_t(N), 1, int64_t(row), 1, b->s);
     if (rc == CRLOT_OK)
         rc = crlot_irfft_batched(inner, b->d_spec, b->d_r, int32_t(M), int64_t(row), 1, int64_t(N), 1, b->s);
@@ -152,29 +162,48 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
         if (rc != CRLOT_OK) return rc;
     }
     b->inv_ready = b->pushed = -1;
+    if (!inner) return 0;
+    // source 1: the Framer popped last, frame * a library window
     std::vector<float> sig;
     int64_t hop = 0, M = 0;
-    if (!inner || !framer_last_signal(n, &sig, &hop, &M) || M < 4) return 0;
-    const std::vector<std::vector<float>> wins = windows_of_size(n);
     const std::vector<float>* found = nullptr;
-    for (const auto& w : wins) {
-        bool ok = true;
-        for (int64_t i = 0; i < n && ok; ++i) {
-            const float v = (i < int64_t(sig.size()) ? sig[size_t(i)] : 0.0f) * w[size_t(i)];
-            ok = std::memcmp(&v, in + i, sizeof(float)) == 0;
-        }
-        if (ok) {
-            found = &w;
-            break;
+    std::vector<std::vector<float>> wins;
+    if (framer_last_signal(n, &sig, &hop, &M) && M >= 4) {
+        wins = windows_of_size(n);
+        for (const auto& w : wins) {
+            bool ok = true;
+            for (int64_t i = 0; i < n && ok; ++i) {
+                const float v = (i < int64_t(sig.size()) ? sig[size_t(i)] : 0.0f) * w[size_t(i)];
+                ok = std::memcmp(&v, in + i, sizeof(float)) == 0;
+            }
+            if (ok) {
+                found = &w;
+                break;
+            }
         }
     }
-    if (!found) return 0;
+    // source 2: the FrameQueue read last, its frame as it is (no window)
+    std::vector<float> rows;
+    if (!found) {
+        int qdev = -1, cur = -1;
+        if (!framequeue_last_rows(n, &rows, &hop, &M, &qdev) || M < 4 || hipGetDevice(&cur) != hipSuccess ||
+            cur != qdev || std::memcmp(rows.data(), in, sizeof(float) * size_t(n)) != 0)
+            return 0;
+    }
     b->gen += 1;
     b->n = n;
     b->h = hop;
     b->M = M;
-    b->sig.swap(sig);
-    b->win = *found;
+    b->rows_src = found == nullptr;
+    if (found) {
+        b->sig.swap(sig);
+        b->win = *found;
+        b->rows.clear();
+    } else {
+        b->rows.swap(rows);
+        b->sig.clear();
+        b->win.clear();
+    }
     b->next_fwd = 0;
     b->y_ready = b->y_waited = false;
     b->ola = nullptr;
@@ -210,7 +239,9 @@ int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out) {
 int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
                  float gain, hipStream_t tables_stream) {
     BatchSpec* b = sh->batch;
-    const size_t F = size_t(b->M - j0), len = F * size_t(b->h);
+    // blocks of frames j0 .. M-1 and the tail only they reach (no later frame
+    // exists in the batch; a produce there needs the last frame pushed)
+    const size_t F = size_t(b->M - j0), len = F * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
     hipError_t e;
     if ((e = hipStreamSynchronize(tables_stream)) != hipSuccess) return hip_fail(e, "OLA tables");
     if ((e = dgrow(&b->d_y, &b->c_y, len)) || (e = hgrow(&b->h_y, &b->c_hy, len))) return hip_fail(e, "batch buffers");

@@ -37,6 +37,11 @@ struct SharedServer;
 // frame j (j = 0: the frame just popped) = sig[j H : j H + N], zeros past the
 // end, j < *frames.  Returns false when there is none (objects.cpp).
 bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_t* frames);
+// The second source: the frames of the FrameQueue read last (getFrame /
+// copyFrame), from the frame just read on, as a host copy [frames][n]
+// (bench/performance_benchmark.cc:174-246 feeds each FrameQueue frame,
+// unwindowed, to the forward).  False when there is none (objects.cpp).
+bool framequeue_last_rows(int64_t n, std::vector<float>* rows, int64_t* hop, int64_t* frames, int* device);
 // Window tables the library built (crlot_window_table) or was handed
 // (OLAAccumulator::set_window), newest first, for the speculation's search.
 void note_window(const float* w, int64_t n);
@@ -54,6 +59,8 @@ struct BatchSpec {
     int64_t n = 0, h = 0, M = 0;
     std::vector<float> sig;  // host copy of the remaining signal (verifies forward inputs)
     std::vector<float> win;  // the analysis window found
+    bool rows_src = false;   // the FrameQueue source: forward inputs are the rows themselves
+    std::vector<float> rows; // its copy [M][n] (uploaded by run_chain)
     int64_t next_fwd = 0;    // frame whose forward comes next
     int64_t inv_ready = -1;  // frame whose forward was served and whose inverse may be asked
     int64_t pushed = -1;     // last frame whose inverse was served (push candidate)
@@ -88,7 +95,8 @@ int batch_abort(SharedServer* sh);
 // objects.cpp, under sh->mu
 int ola_materialize_locked(crlot_ola* o);
 // the batch's gather for an OLA object attaching at frame j0 (objects.cpp passes
-// its tables): produce blocks of frames j0 .. M-1 into h_y
+// its tables): produce blocks of frames j0 .. M-1, and the N - H samples after
+// them that only those frames reach, into h_y
 int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
                  float gain, hipStream_t tables_stream);
 int batch_wait_y(BatchSpec* b);

@@ -614,7 +614,10 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
 int batch_produce(crlot_ola* o, float* out, int64_t n) {
     crlot::BatchSpec* b = o->vb;
     if (!b || crlot::spec_mode() < 2 || b->ola != o || o->vgen != b->gen || o->flushing || o->C() != 1) return 0;
-    const int64_t final_end = (o->vlast - b->j0 + 1) * b->h;  // positions no later frame reaches
+    // positions no later frame reaches: up to the last pushed frame's hop, or to
+    // its end once the batch's last frame is pushed (no later frame exists)
+    const int64_t final_end =
+        (o->vlast - b->j0 + 1) * b->h + (o->vlast == b->M - 1 ? std::max<int64_t>(0, b->n - b->h) : 0);
     if (o->vread + n > final_end || o->read_pos != o->vread % o->R) return 0;
     const int rc = crlot::batch_wait_y(b);
     if (rc != CRLOT_OK) return rc;
@@ -756,6 +759,10 @@ int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const f
     int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
     ServerLock lk(o);
+    if (ok == o->C()) {  // a mono push the batch predicted (as push_frame_AoS below)
+        rc = batch_push(o, rows[0], caller_win, start_sample, start_off, eff, gain);
+        if (rc != 0) return rc < 0 ? rc : CRLOT_OK;
+    }
     if (o->vb && (rc = ola_materialize(o)) != CRLOT_OK) return rc;
     rc = ok == o->C() ? try_chain_push(o, rows[0], uw, caller_win, start_sample, start_off, eff, gain) : 0;
     if (rc < 0) return rc;
@@ -1068,9 +1075,38 @@ int crlot_normalize_and_clear(float* d_out, float* d_acc, const float* d_norm, f
 struct crlot_framequeue {
     int device = 0;
     int64_t n = 0, h = 0, f = 0;
-    float* d_frames = nullptr;
-    std::vector<float> frames;  // host copy (getFrame / getAllFrames)
+    std::vector<float> frames;  // [frame][n] (getFrame / getAllFrames)
+    // the same frames in HBM, uploaded at the first device_frames() (the GPU-native
+    // input of batched transforms; the host-pointer accessors never need it)
+    mutable std::mutex dmu;
+    mutable float* d_frames = nullptr;
 };
+
+namespace {
+// the FrameQueue frame read last through the host accessors (batch.h
+// framequeue_last_rows); cleared when that queue dies
+const crlot_framequeue* g_last_fq = nullptr;
+int64_t g_last_fq_idx = -1;
+void note_fq_read(const crlot_framequeue* q, int64_t idx) {
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    g_last_fq = q;
+    g_last_fq_idx = idx;
+}
+}  // namespace
+
+namespace crlot {
+bool framequeue_last_rows(int64_t n, std::vector<float>* rows, int64_t* hop, int64_t* frames, int* device) {
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    const crlot_framequeue* q = g_last_fq;
+    if (!q || q->n != n || g_last_fq_idx < 0 || g_last_fq_idx >= q->f) return false;
+    const int64_t i = g_last_fq_idx;
+    rows->assign(q->frames.begin() + i * n, q->frames.end());
+    *hop = q->h;
+    *frames = q->f - i;
+    *device = q->device;
+    return true;
+}
+}  // namespace crlot
 
 namespace {
 // FrameQueue::calculateNumFrames on the padded length (FrameQueue.cc:98-115)
@@ -1123,43 +1159,42 @@ int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, in
     } else {
         q->device = device;
     }
-    DeviceGuard g(q->device);
     q->n = frame_size;
     q->h = hop_size;
     q->f = fq_count(len, frame_size, hop_size, center != 0);
+    // The frames on the host, as FrameQueue.cc:69-96 builds them (the same
+    // indexing as the device form k_fq_frames, ola.hip: copies, so the same bits):
+    // a host-pointer class serves host memory, and framing a whole signal is one
+    // pass of copies, cheaper here than a device round trip.
     const size_t nf = size_t(q->f) * size_t(q->n);
-    q->frames.resize(nf);
-    if (nf == 0) {
-        *out = q;
-        return CRLOT_OK;
-    }
-    void* d_x = nullptr;
-    void* d_f = nullptr;
-    hipStream_t s = nullptr;
-    hipError_t e;
-    if ((e = crlot::pool_stream(q->device, &s)) ||
-        (e = crlot::pool_malloc(q->device, &d_f, sizeof(float) * nf, s)) ||
-        (len > 0 && (e = crlot::pool_malloc(q->device, &d_x, sizeof(float) * size_t(len), s))) ||
-        (len > 0 && (e = hipMemcpyAsync(d_x, in, sizeof(float) * size_t(len), hipMemcpyHostToDevice, s))) ||
-        (e = crlot::launch_fq_frames(static_cast<const float*>(d_x), len, len, 1, static_cast<float*>(d_f), q->f,
-                                     q->n, q->h, center ? frame_size / 2 : 0, pad_mode, s)) ||
-        (e = hipMemcpyAsync(q->frames.data(), d_f, sizeof(float) * nf, hipMemcpyDeviceToHost, s))) {
-        crlot::pool_free(d_x, s);
-        crlot::pool_free(d_f, s);
-        if (s) {
-            (void)hipStreamSynchronize(s);
-            crlot::pool_stream_put(q->device, s);
-        }
+    try {
+        q->frames.resize(nf);
+    } catch (const std::bad_alloc&) {
         delete q;
-        return e == hipErrorOutOfMemory ? fail(CRLOT_ENOMEM, "FrameQueue allocation") : hip_fail(e, "FrameQueue");
+        return fail(CRLOT_ENOMEM, "FrameQueue allocation");
     }
-    crlot::pool_free(d_x, s);
-    q->d_frames = static_cast<float*>(d_f);
-    e = hipStreamSynchronize(s);  // frames on the host; d_frames usable from any stream
-    crlot::pool_stream_put(q->device, s);
-    if (e != hipSuccess) {
-        crlot_framequeue_destroy(q);
-        return hip_fail(e, "FrameQueue");
+    const int64_t pad = center ? frame_size / 2 : 0;
+    for (int64_t k = 0; k < q->f; ++k) {
+        float* dst = q->frames.data() + size_t(k) * size_t(q->n);
+        const int64_t o = k * hop_size - pad;
+        const int64_t j0 = std::max<int64_t>(0, -o), j1 = std::min<int64_t>(frame_size, len - o);
+        if (j1 > j0) std::memcpy(dst + j0, in + o + j0, sizeof(float) * size_t(j1 - j0));
+        for (int64_t j = 0; j < frame_size; ++j) {
+            if (j >= j0 && j < j1) continue;
+            const int64_t idx = o + j;
+            float v = 0.0f;
+            if (len > 0 && pad_mode == CRLOT_PAD_REFLECT) {
+                int64_t i = idx;  // reflect101 (Indexing.h:18-33)
+                if (len > 1)
+                    while (i < 0 || i >= len) i = i < 0 ? -i - 1 : 2 * len - 2 - i;
+                else
+                    i = 0;
+                v = in[i];
+            } else if (len > 0 && pad_mode == CRLOT_PAD_EDGE) {
+                v = in[idx < 0 ? 0 : len - 1];
+            }
+            dst[j] = v;
+        }
     }
     *out = q;
     return CRLOT_OK;
@@ -1167,17 +1202,13 @@ int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, in
 
 void crlot_framequeue_destroy(crlot_framequeue* q) {
     if (!q) return;
-    DeviceGuard g(q->device);
-    if (q->d_frames) {
-        // (the caller finished its device-side reads of the frames, as with any
-        // buffer it frees: stream-ordered release on a pooled stream)
-        hipStream_t s = nullptr;
-        if (crlot::pool_stream(q->device, &s) == hipSuccess) {
-            crlot::pool_free(q->d_frames, s);
-            crlot::pool_stream_put(q->device, s);
-        } else {
-            (void)hipFree(q->d_frames);
-        }
+    {
+        std::lock_guard<std::mutex> lk(g_pop_mu);
+        if (g_last_fq == q) g_last_fq = nullptr;
+    }
+    if (q->d_frames) {  // (the caller finished its device-side reads of the frames)
+        DeviceGuard g(q->device);
+        (void)hipFree(q->d_frames);
     }
     delete q;
 }
@@ -1199,6 +1230,7 @@ const float* crlot_framequeue_frame(const crlot_framequeue* q, int64_t frame_idx
         fail(CRLOT_ERANGE, "Frame index out of range");
         return nullptr;
     }
+    note_fq_read(q, frame_idx);
     return q->frames.data() + size_t(frame_idx) * size_t(q->n);
 }
 
@@ -1206,12 +1238,30 @@ int crlot_framequeue_copy_frame(const crlot_framequeue* q, int64_t frame_idx, fl
     if (!q) return fail(CRLOT_EINVAL, "null FrameQueue");
     if (frame_idx < 0 || frame_idx >= q->f) return fail(CRLOT_ERANGE, "Frame index out of range");
     if (!out) return fail(CRLOT_EINVAL, "Output buffer cannot be null");  // FrameQueue.cc:56-67
+    note_fq_read(q, frame_idx);
     std::memcpy(out, q->frames.data() + size_t(frame_idx) * size_t(q->n), sizeof(float) * size_t(q->n));
     return CRLOT_OK;
 }
 
 const float* crlot_framequeue_all_frames(const crlot_framequeue* q) { return q ? q->frames.data() : nullptr; }
 
-const float* crlot_framequeue_device_frames(const crlot_framequeue* q) { return q ? q->d_frames : nullptr; }
+const float* crlot_framequeue_device_frames(const crlot_framequeue* q) {
+    if (!q) return nullptr;
+    std::lock_guard<std::mutex> lk(q->dmu);
+    if (!q->d_frames && !q->frames.empty()) {  // uploaded on first use, then kept
+        DeviceGuard g(q->device);
+        const size_t bytes = sizeof(float) * q->frames.size();
+        void* d = nullptr;
+        hipError_t e = hipMalloc(&d, bytes);
+        if (e == hipSuccess) e = hipMemcpy(d, q->frames.data(), bytes, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            if (d) (void)hipFree(d);
+            hip_fail(e, "FrameQueue device frames");
+            return nullptr;
+        }
+        q->d_frames = static_cast<float*>(d);
+    }
+    return q->d_frames;
+}
 
 }  // extern "C"

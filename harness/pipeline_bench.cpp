@@ -41,11 +41,13 @@ int main(int argc, char** argv) {
     struct Times {
         double total_us, loop_us;
         size_t frames;
+        double fq_us, ola_us, first_fwd_us;  // construction of the FrameQueue / the OLA object; frame 0's forward
     };
     try {
         auto run = [&](bool interleaved) -> Times {
             const auto t0 = clk::now();
             FrameQueue frames(x.data(), L, N, H, true);
+            const auto t_fq = clk::now();
             auto window = WindowLUT::getInstance().GetWindowSafe(WindowType::HANN, N);
             OLAConfig config;
             config.sample_rate = 48000;
@@ -56,17 +58,21 @@ int main(int argc, char** argv) {
             config.apply_window_inside = true;
             OLAAccumulator ola(config);
             ola.set_window(window.get(), int(N));
+            const auto t_ola = clk::now();
             FftPlanDesc desc{FftDomain::Real, int(N), false, 1, 1, 1};
             auto fft_plan = MakeFftPlan(desc);
             std::vector<std::complex<float>> spectrum(N / 2 + 1);
             std::vector<float> processed(N), output(L + N);
             const auto t_loop = clk::now();
+            double first_fwd = 0.0;
             size_t total = 0;
             float* ch_out[1] = {output.data()};
             for (size_t i = 0; i < frames.getNumFrames(); ++i) {
                 const float* frame = frames.getFrame(i);
                 std::copy(frame, frame + N, processed.begin());
+                const auto tf0 = clk::now();
                 fft_plan->forward(processed.data(), spectrum.data());
+                if (i == 0) first_fwd = std::chrono::duration<double, std::micro>(clk::now() - tf0).count();
                 fft_plan->inverse(spectrum.data(), processed.data());
                 const float* ch_frames[1] = {processed.data()};
                 ola.add_frame_SoA(ch_frames, window.get(), i * H, 0, N, 1.0f);
@@ -82,11 +88,11 @@ int main(int argc, char** argv) {
                 total += s;
             }
             const auto t1 = clk::now();
-            return Times{std::chrono::duration<double, std::micro>(t1 - t0).count(),
-                         std::chrono::duration<double, std::micro>(t1 - t_loop).count(), frames.getNumFrames()};
+            auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+            return Times{us(t0, t1), us(t_loop, t1), frames.getNumFrames(), us(t0, t_fq), us(t_fq, t_ola), first_fwd};
         };
         for (int w = 0; w < 5; ++w) run(true);
-        std::vector<double> lit, ilv, lit_loop, ilv_loop;
+        std::vector<double> lit, ilv, lit_loop, ilv_loop, fq, olac, ff;
         size_t F = 0;
         for (int i = 0; i < iters; ++i) {
             const Times a = run(false), b = run(true);
@@ -94,16 +100,30 @@ int main(int argc, char** argv) {
             ilv.push_back(b.total_us);
             lit_loop.push_back(a.loop_us);
             ilv_loop.push_back(b.loop_us);
+            fq.push_back(b.fq_us);
+            olac.push_back(b.ola_us);
+            ff.push_back(b.first_fwd_us);
             F = a.frames;
         }
+        // what the batched speculation served per interleaved iteration (batches,
+        // forwards, inverses, pushes, produces, ring rebuilds; crlot_call_speculation_stats)
+        int64_t s0[6], s1[6];
+        crlot_call_speculation_stats(s0);
+        for (int i = 0; i < 10; ++i) run(true);
+        crlot_call_speculation_stats(s1);
         // total: the reference's iteration (object construction included, :181-210);
         // loop: the per-frame calls and the produce loop only
         std::printf("{\"harness\": \"pipeline_bench\", \"reference\": \"bench/performance_benchmark.cc:174-246\", "
                     "\"input_length\": %zu, \"frame\": %zu, \"hop\": %zu, \"frames\": %zu, \"iterations\": %d, "
                     "\"literal\": {\"total_us_p50\": %.2f, \"loop_us_p50\": %.2f, \"loop_us_per_frame\": %.3f}, "
-                    "\"interleaved\": {\"total_us_p50\": %.2f, \"loop_us_p50\": %.2f, \"loop_us_per_frame\": %.3f}}\n",
+                    "\"interleaved\": {\"total_us_p50\": %.2f, \"loop_us_p50\": %.2f, \"loop_us_per_frame\": %.3f, "
+                    "\"served_per_iteration\": {\"batches\": %.1f, \"forwards\": %.1f, \"inverses\": %.1f, "
+                    "\"pushes\": %.1f, \"produces\": %.1f, \"rebuilds\": %.1f}, "
+                    "\"framequeue_us_p50\": %.2f, \"ola_object_us_p50\": %.2f, \"first_forward_us_p50\": %.2f}}\n",
                     L, N, H, F, iters, p50(lit), p50(lit_loop), p50(lit_loop) / double(F), p50(ilv), p50(ilv_loop),
-                    p50(ilv_loop) / double(F));
+                    p50(ilv_loop) / double(F), (s1[0] - s0[0]) / 10.0, (s1[1] - s0[1]) / 10.0,
+                    (s1[2] - s0[2]) / 10.0, (s1[3] - s0[3]) / 10.0, (s1[4] - s0[4]) / 10.0, (s1[5] - s0[5]) / 10.0,
+                    p50(fq), p50(olac), p50(ff));
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 4;

@@ -622,15 +622,16 @@ class FrameQueue {
     size_t getNumFrames() const { return size_t(f_); }
     size_t getFrameSize() const { return size_t(n_); }
     size_t getHopSize() const { return size_t(h_); }
+    // (through the library, which notes the frame read last: the batched
+    // speculation of a per-frame loop over the queue starts from it)
     const float* getFrame(size_t frame_idx) const {
         if (frame_idx >= size_t(f_)) throw std::out_of_range("Frame index out of range");
-        return frames_.data() + frame_idx * size_t(n_);
+        return crlot_framequeue_frame(q_, int64_t(frame_idx));
     }
     void copyFrame(size_t frame_idx, float* output) const {
         if (frame_idx >= size_t(f_)) throw std::out_of_range("Frame index out of range");
         if (output == nullptr) throw std::invalid_argument("Output buffer cannot be null");
-        const float* f = frames_.data() + frame_idx * size_t(n_);
-        std::copy(f, f + n_, output);
+        check(crlot_framequeue_copy_frame(q_, int64_t(frame_idx), output), "FrameQueue::copyFrame");
     }
     const std::vector<float>& getAllFrames() const { return frames_; }
     const float* device_frames() const { return crlot_framequeue_device_frames(q_); }

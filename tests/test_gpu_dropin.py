@@ -599,6 +599,101 @@ def test_batched_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, h):
     assert served["pushes"] == F and served["produces"] == F and served["rebuilds"] == 0, served
 
 
+def _pipeline_loop(pkg, x, n, h, interleaved=True, tamper=None):
+    """bench/performance_benchmark.cc:174-246 through the drop-in objects (the
+    harness/pipeline_bench loop): FrameQueue(x, N, H, centre) -> per frame:
+    getFrame -> forward -> inverse -> add_frame_SoA(window, i H) [-> produce(H)]
+    -> produce(H) until the signal length.  `tamper` = frame index whose forward
+    input is nudged by one ulp (the batch must not serve it)."""
+    L = x.size
+    q = pkg.FrameQueue(x, n, h, center=True)
+    w = pkg.window_table(pkg.HANN, n)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                        apply_window_inside=True)
+    ola = pkg.OLAAccumulator(cfg)
+    ola.set_window(w)
+    specs, invs, outs = [], [], []
+    total = 0
+    for i in range(q.getNumFrames()):
+        f = q.getFrame(i)
+        if i == tamper:
+            f = f.copy()
+            f[7] = np.nextafter(f[7], np.float32(np.inf))
+        X = fft.forward_host(f[None])
+        y = fft.inverse_host(X)[0]
+        ola.add_frame_SoA([y], w, i * h, 0, n, 1.0)
+        specs.append(np.asarray(X).copy())
+        invs.append(y.copy())
+        if interleaved and total < L:
+            got, chans = ola.produce(h)
+            outs.append(chans[0][:got].copy())
+            total += got
+    while total < L:
+        got, chans = ola.produce(h)
+        if got == 0:
+            break
+        outs.append(chans[0][:got].copy())
+        total += got
+    ola.close()
+    q.close()
+    return specs, invs, np.concatenate(outs) if outs else np.zeros(0, np.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,L", [(1024, 512, 16384), (1024, 256, 20_000), (960, 240, 9_600)])
+@pytest.mark.parametrize("interleaved", [True, False])
+def test_batched_pipeline_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, h, L, interleaved):
+    """The reference's second pipeline (performance_benchmark.cc: FrameQueue frames,
+    no analysis window, add_frame_SoA, the trailing produces) served from the
+    batched speculation -- the FrameQueue read last is its source -- gives the
+    per-call path's bits call by call (spectra, inverse frames, every produced
+    sample, the tail included) and the oracle OLAAccumulator's; the counters show
+    the batch served it.  In the harness's literal order (every push first) the
+    ring wraps and the batch leaves the pushes to the ring: same bits."""
+    x = oracle.synth(L, n + h)
+    try:
+        pkg.set_call_speculation(1)
+        a = _pipeline_loop(pkg, x, n, h, interleaved)
+        pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats()
+        b = _pipeline_loop(pkg, x, n, h, interleaved)
+        s1 = pkg.call_speculation_stats()
+        c = _pipeline_loop(pkg, x, n, h, interleaved, tamper=5)
+        pkg.set_call_speculation(1)
+        c1 = _pipeline_loop(pkg, x, n, h, interleaved, tamper=5)
+    finally:
+        pkg.set_call_speculation(2)
+    F = len(a[0])
+    assert len(b[0]) == F
+    for k in range(F):
+        assert np.array_equal(bits(a[0][k]), bits(b[0][k])), ("spectrum", k)
+        assert np.array_equal(bits(a[1][k]), bits(b[1][k])), ("inverse", k)
+    assert np.array_equal(bits(a[2]), bits(b[2]))
+    assert np.array_equal(bits(c[2]), bits(c1[2]))  # a frame off the rhythm: the per-call bits again
+    # the oracle OLAAccumulator fed the same inverse frames (add_frame_SoA == push_frame_AoS for mono)
+    ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ref.set_window(pkg.window_table(pkg.HANN, n))
+    outs, total = [], 0
+    for i, y in enumerate(b[1]):
+        ref.push_frame_aos(y, i * h, 0, n, 1.0)
+        if interleaved and total < L:
+            o = ref.produce(h)[0]
+            outs.append(o)
+            total += o.size
+    while total < L:
+        o = ref.produce(h)[0]
+        if o.size == 0:
+            break
+        outs.append(o)
+        total += o.size
+    assert np.array_equal(bits(b[2]), bits(np.concatenate(outs)))
+    served = {key: s1[key] - s0[key] for key in s1}
+    assert served["batches"] == 1 and served["forwards"] == F and served["inverses"] == F, served
+    if interleaved:  # every push and produce served: no ring was rebuilt
+        assert served["pushes"] == F and served["rebuilds"] == 0 and served["produces"] > 0, served
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("brk", ["input", "extra_forward", "gain", "short_produce", "device_push"])
 def test_batched_loop_falls_back_on_a_broken_rhythm(pkg, oracle, torch_cuda, brk):
