@@ -1179,6 +1179,25 @@ int crlot_fft_inverse_complex(crlot_fft_plan* p, const float* d_in, float* d_out
 // and a launch.  Element i of batch b at [b*ld + i*inc] as the device forms.
 }  // extern "C"
 
+namespace crlot {
+// batch.h: the plan's forward then inverse of `batch` contiguous rows in one
+// launch (k_rfft_irfft: K_rfft's and K_irfft's bits); CRLOT_EUNSUPPORTED where
+// the plan has no such kernel (any-size plans, 4096)
+int plan_rfft_irfft(crlot_plan* p, const float* in, float* spec, float* r, float* r_host, int32_t batch,
+                    void* stream) {
+    if (!p || batch <= 0 || !in || !spec || !r) return set_error(CRLOT_EINVAL, "rfft_irfft arguments");
+    if (p->generic || p->geo.n > 2048) return CRLOT_EUNSUPPORTED;
+    DeviceGuard g(p->device);
+    LaunchScope ls(p, stream);
+    const int64_t n = p->geo.n;
+    const hipError_t e = launch_rfft_irfft(p->geo, tables(p), in, n, spec, n + 2, r, r_host, n, batch,
+                                           static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "rfft_irfft kernel launch");
+    return CRLOT_OK;
+}
+}  // namespace crlot
+
+
 namespace {
 
 // gather / scatter between strided caller memory and dense [batch][len] rows

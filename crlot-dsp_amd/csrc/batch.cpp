@@ -3,10 +3,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
 
+#include "ab.h"
 #include "call.h"
 #include "kernels.h"
 
@@ -22,6 +26,7 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 std::atomic<int> g_mode{2};
+constexpr float kOne = 1.0f;
 // crlot_call_speculation_stats: batches started, forwards / inverses / pushes /
 // produces served from a batch, OLA rings rebuilt
 std::atomic<int64_t> g_stats[6];
@@ -50,9 +55,76 @@ hipError_t hgrow(float** p, size_t* cap, size_t need) {
     return e;
 }
 
+// A/B (CRLOT_BATCH_ZC, default 3): bit 0, the first forward of a FrameQueue
+// batch reads the pinned rows over the host link instead of after a copy engine
+// upload
+int zc_mode() {
+    static const int v = [] {
+        const char* e = ab_env("CRLOT_BATCH_ZC");
+        return e ? std::atoi(e) : 3;
+    }();
+    return v;
+}
+bool zero_copy_in() { return (zc_mode() & 1) != 0; }
+// (CRLOT_BATCH_ZC bit 1: the chain's kernels write the host copies of their
+// results themselves)
+bool zero_copy_out() { return (zc_mode() & 2) != 0; }
+// A/B (CRLOT_BATCH_FUSE=0): forward and inverse as two launches
+bool fuse_fft() {
+    static const bool v = [] {
+        const char* e = ab_env("CRLOT_BATCH_FUSE");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+// A/B builds (CRLOT_BATCH_TRACE=1): the phases of batch starts, summed, printed
+// at exit: source search + rows copy, enqueue, wait
+#ifdef CRLOT_AB_SWITCHES
+// phases of each start: 0 source search + rows copy, 1 stream/tables/buffers,
+// 2 upload, 3 forward launch, 4 inverse launch, 5 overlap-add launches, 6 copy
+// back + record, 7 wait; medians printed at exit
+struct BatchTrace {
+    std::vector<double> us[8];
+    ~BatchTrace() {
+        if (us[0].empty()) return;
+        std::fprintf(stderr, "batch_trace starts=%zu median_us:", us[0].size());
+        for (auto& v : us) {
+            std::sort(v.begin(), v.end());
+            std::fprintf(stderr, " %.2f", v.empty() ? 0.0 : v[v.size() / 2]);
+        }
+        std::fprintf(stderr, "\n");
+    }
+};
+BatchTrace g_trace;
+bool trace_on() {
+    static const bool v = [] {
+        const char* e = ab_env("CRLOT_BATCH_TRACE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+using tclk = std::chrono::steady_clock;
+struct PhaseClock {
+    tclk::time_point t = tclk::now();
+    void lap(int i) {
+        if (!trace_on()) return;
+        const auto n = tclk::now();
+        g_trace.us[i].push_back(std::chrono::duration<double, std::micro>(n - t).count());
+        t = n;
+    }
+};
+thread_local PhaseClock g_pc;
+#define CRLOT_LAP(i) g_pc.lap(i)
+#define CRLOT_LAP_START() (g_pc.t = tclk::now())
+#else
+#define CRLOT_LAP(i) ((void)0)
+#define CRLOT_LAP_START() ((void)0)
+#endif
+
 // the forward input of frame j, as the loop forms it on the host (frame * w)
 bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
-    if (b.rows_src) return std::memcmp(in, b.rows.data() + size_t(j) * size_t(b.n), sizeof(float) * size_t(b.n)) == 0;
+    if (b.rows_src) return std::memcmp(in, b.h_stage + size_t(j) * size_t(b.n), sizeof(float) * size_t(b.n)) == 0;
     const int64_t L = int64_t(b.sig.size()), base = j * b.h;
     for (int64_t i = 0; i < b.n; ++i) {
         const int64_t t = base + i;
@@ -62,25 +134,49 @@ bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
     return true;
 }
 
-// run frames 0 .. M-1 of the found chain: products, forward, inverse; results to pinned memory
+// run frames 0 .. M-1 of the found chain: products, forward, inverse (and the
+// overlap-add of a fresh OLA object); results to pinned memory in one copy
 int run_chain(BatchSpec* b, crlot_plan* inner) {
     const size_t L = b->sig.size(), N = size_t(b->n), M = size_t(b->M), row = N + 2;
+    const size_t ylen = M * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
     hipError_t e;
     if (!b->s && (e = hipStreamCreateWithFlags(&b->s, hipStreamNonBlocking)) != hipSuccess)
         return hip_fail(e, "batch stream");
     if (!b->ev && (e = hipEventCreateWithFlags(&b->ev, hipEventDisableTiming)) != hipSuccess)
         return hip_fail(e, "batch event");
-    if ((e = dgrow(&b->d_p, &b->c_p, M * N)) || (e = dgrow(&b->d_spec, &b->c_spec, M * row)) ||
-        (e = dgrow(&b->d_r, &b->c_r, M * N)) || (e = hgrow(&b->h_spec, &b->c_hspec, M * row)) ||
-        (e = hgrow(&b->h_r, &b->c_hr, M * N)))
+    // the overlap-add of a fresh OLA object, both ways its produces may come
+    // (after each push; after every push, the ring wrapped), in the same round trip
+    b->spec_y = b->spec_used = false;
+    int dev = -1;
+    const bool fresh = hipGetDevice(&dev) == hipSuccess && fresh_ola(b->n, b->h, dev, b->s, &b->spec_ola);
+    const size_t R = fresh ? size_t(b->spec_ola.R) : 0, blk = M * row + M * N + ylen + R;
+    const size_t had = b->c_hblk;
+    if ((e = dgrow(&b->d_p, &b->c_p, M * N)) || (e = dgrow(&b->d_blk, &b->c_blk, blk)) ||
+        (e = hgrow(&b->h_blk, &b->c_hblk, blk)) || (fresh && (e = dgrow(&b->d_acc, &b->c_acc, R))))
         return hip_fail(e, "batch buffers");
-    if (b->rows_src) {  // the FrameQueue's rows are the forward inputs
-        if ((e = hgrow(&b->h_stage, &b->c_hs, M * N)) == hipSuccess) {
-            std::memcpy(b->h_stage, b->rows.data(), sizeof(float) * M * N);
-            e = hipMemcpyAsync(b->d_p, b->h_stage, sizeof(float) * M * N, hipMemcpyHostToDevice, b->s);
-        }
-        if (e != hipSuccess) return hip_fail(e, "batch frames");
+    if (b->c_hblk != had || !b->m_blk) {
+        void* m = nullptr;
+        b->m_blk = hipHostGetDevicePointer(&m, b->h_blk, 0) == hipSuccess ? static_cast<float*>(m) : nullptr;
+    }
+    b->d_spec = b->d_blk;
+    b->d_r = b->d_spec + M * row;
+    b->d_y = b->d_r + M * N;
+    b->h_spec = b->h_blk;
+    b->h_r = b->h_spec + M * row;
+    b->h_y = b->h_r + M * N;
+    // zero-copy (default): the kernels read the pinned rows and write the host
+    // copies of their results themselves -- no copy engine, one dependent launch
+    // fewer per copy
+    const bool zc_out = zero_copy_out() && b->m_blk;
+    CRLOT_LAP(1);
+    const float* d_in = b->d_p;
+    if (b->rows_src) {  // the FrameQueue's rows (already in h_stage) are the forward inputs
+        if (zero_copy_in() && b->m_stage)
+            d_in = b->m_stage;
+        else if ((e = hipMemcpyAsync(b->d_p, b->h_stage, sizeof(float) * M * N, hipMemcpyHostToDevice, b->s)))
+            return hip_fail(e, "batch frames");
     } else {
+        b->m_stage = nullptr;  // (h_stage may move; the rows source maps it again)
         if ((e = dgrow(&b->d_sig, &b->c_sig, L + N)) || (e = hgrow(&b->h_stage, &b->c_hs, L + N)))
             return hip_fail(e, "batch buffers");
         std::memcpy(b->h_stage, b->sig.data(), sizeof(float) * L);
@@ -89,14 +185,45 @@ int run_chain(BatchSpec* b, crlot_plan* inner) {
             (e = launch_windowed_frames(b->d_sig, int64_t(L), b->d_sig + L, b->d_p, b->M, b->n, b->h, b->s)))
             return hip_fail(e, "batch frames");
     }
-    int rc = crlot_rfft_batched(inner, b->d_p, b->d_spec, int32_t(M), int64_t(N), 1, int64_t(row), 1, b->s);
-    if (rc == CRLOT_OK)
-        rc = crlot_irfft_batched(inner, b->d_spec, b->d_r, int32_t(M), int64_t(row), 1, int64_t(N), 1, b->s);
+    CRLOT_LAP(2);
+    // forward + inverse: one launch where the plan has the fused kernel
+    bool spec_r_host = false;
+    int rc = fuse_fft() ? plan_rfft_irfft(inner, d_in, zc_out ? b->m_blk : b->d_spec, b->d_r,
+                                          zc_out ? b->m_blk + M * row : nullptr, int32_t(M), b->s)
+                        : CRLOT_EUNSUPPORTED;
+    if (rc == CRLOT_OK) {
+        spec_r_host = zc_out;
+    } else if (rc == CRLOT_EUNSUPPORTED) {
+        rc = crlot_rfft_batched(inner, d_in, b->d_spec, int32_t(M), int64_t(N), 1, int64_t(row), 1, b->s);
+        CRLOT_LAP(3);
+        if (rc == CRLOT_OK)
+            rc = crlot_irfft_batched(inner, b->d_spec, b->d_r, int32_t(M), int64_t(row), 1, int64_t(N), 1, b->s);
+    }
     if (rc != CRLOT_OK) return rc;
-    if ((e = hipMemcpyAsync(b->h_spec, b->d_spec, sizeof(float) * M * row, hipMemcpyDeviceToHost, b->s)) ||
-        (e = hipMemcpyAsync(b->h_r, b->d_r, sizeof(float) * M * N, hipMemcpyDeviceToHost, b->s)) ||
-        (e = hipEventRecord(b->ev, b->s)) || (e = hipEventSynchronize(b->ev)))
+    CRLOT_LAP(4);
+    if (!spec_r_host &&
+        (e = hipMemcpyAsync(b->h_blk, b->d_blk, sizeof(float) * (M * row + M * N), hipMemcpyDeviceToHost, b->s)))
         return hip_fail(e, "batch results");
+    if (fresh) {
+        Geometry g;
+        g.n = int(b->n);
+        g.h = int(b->h);
+        g.ring_len = int(R);
+        g.gain = 1.0f;
+        DevTables t;
+        t.ws = b->spec_ola.d_win;
+        t.den = b->spec_ola.d_den;
+        float* yout = zc_out ? b->m_blk + (M * row + M * N) : b->d_y;
+        if ((e = launch_ola_gather_wrap(g, t, b->d_r, b->n, b->M, int64_t(ylen), b->d_acc, yout + ylen, b->s, yout)) ||
+            (!zc_out && (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * (ylen + R), hipMemcpyDeviceToHost, b->s))))
+            return hip_fail(e, "batch overlap-add");
+    }
+    CRLOT_LAP(5);
+    if ((e = hipEventRecord(b->ev, b->s))) return hip_fail(e, "batch results");
+    CRLOT_LAP(6);
+    if ((e = hipEventSynchronize(b->ev))) return hip_fail(e, "batch results");
+    CRLOT_LAP(7);
+    b->spec_y = fresh;
     return CRLOT_OK;
 }
 
@@ -163,6 +290,7 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     }
     b->inv_ready = b->pushed = -1;
     if (!inner) return 0;
+    CRLOT_LAP_START();
     // source 1: the Framer popped last, frame * a library window
     std::vector<float> sig;
     int64_t hop = 0, M = 0;
@@ -182,12 +310,25 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
             }
         }
     }
-    // source 2: the FrameQueue read last, its frame as it is (no window)
-    std::vector<float> rows;
+    // source 2: the FrameQueue read last, its frame as it is (no window),
+    // copied straight into the pinned staging block the upload reads
     if (!found) {
         int qdev = -1, cur = -1;
-        if (!framequeue_last_rows(n, &rows, &hop, &M, &qdev) || M < 4 || hipGetDevice(&cur) != hipSuccess ||
-            cur != qdev || std::memcmp(rows.data(), in, sizeof(float) * size_t(n)) != 0)
+        hipError_t he = hipSuccess;
+        auto dst = [&](size_t floats) -> float* {
+            const size_t had = b->c_hs;
+            he = hgrow(&b->h_stage, &b->c_hs, floats);
+            if (he != hipSuccess) return nullptr;
+            if (b->c_hs != had || !b->m_stage) {
+                void* m = nullptr;
+                b->m_stage = hipHostGetDevicePointer(&m, b->h_stage, 0) == hipSuccess ? static_cast<float*>(m) : nullptr;
+            }
+            return b->h_stage;
+        };
+        const bool got = framequeue_last_rows(n, &hop, &M, &qdev, dst);
+        if (he != hipSuccess) return hip_fail(he, "batch buffers");
+        if (!got || M < 4 || hipGetDevice(&cur) != hipSuccess || cur != qdev ||
+            std::memcmp(b->h_stage, in, sizeof(float) * size_t(n)) != 0)
             return 0;
     }
     b->gen += 1;
@@ -198,15 +339,14 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     if (found) {
         b->sig.swap(sig);
         b->win = *found;
-        b->rows.clear();
     } else {
-        b->rows.swap(rows);
         b->sig.clear();
         b->win.clear();
     }
     b->next_fwd = 0;
     b->y_ready = b->y_waited = false;
     b->ola = nullptr;
+    CRLOT_LAP(0);
     const int rc = run_chain(b, inner);
     if (rc != CRLOT_OK) {
         b->active = false;
@@ -237,14 +377,24 @@ int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out) {
 }
 
 int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
-                 float gain, hipStream_t tables_stream) {
+                 float gain, hipStream_t tables_stream, uint64_t tgen) {
     BatchSpec* b = sh->batch;
+    if (b->spec_y && b->spec_ola.o == o && b->spec_ola.tgen == tgen && b->spec_ola.R == R && j0 == 0 &&
+        std::memcmp(&gain, &kOne, sizeof(float)) == 0) {  // computed with the chain (run_chain)
+        b->ola = o;
+        b->j0 = 0;
+        b->gain = gain;
+        b->y_ready = b->y_waited = true;
+        b->spec_used = true;
+        b->ya = b->h_y + (size_t(b->M) * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h)));
+        return CRLOT_OK;
+    }
+    b->spec_used = false;
     // blocks of frames j0 .. M-1 and the tail only they reach (no later frame
     // exists in the batch; a produce there needs the last frame pushed)
     const size_t F = size_t(b->M - j0), len = F * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
     hipError_t e;
     if ((e = hipStreamSynchronize(tables_stream)) != hipSuccess) return hip_fail(e, "OLA tables");
-    if ((e = dgrow(&b->d_y, &b->c_y, len)) || (e = hgrow(&b->h_y, &b->c_hy, len))) return hip_fail(e, "batch buffers");
     Geometry g;
     g.n = int(b->n);
     g.h = int(b->h);
@@ -271,6 +421,30 @@ int batch_wait_y(BatchSpec* b) {
     const hipError_t e = hipEventSynchronize(b->ev);
     if (e != hipSuccess) return hip_fail(e, "batch overlap-add");
     b->y_waited = true;
+    return CRLOT_OK;
+}
+
+int batch_alias(BatchSpec* b, int64_t R, const float* d_ws, const float* d_den) {
+    if (b->spec_used) return CRLOT_OK;  // computed with the chain (b->ya)
+    const int64_t F = b->M - b->j0, len = F * b->h + std::max<int64_t>(0, b->n - b->h);
+    hipError_t e;
+    if ((e = dgrow(&b->d_acc, &b->c_acc, size_t(R))) || (e = dgrow(&b->d_ya, &b->c_ya, size_t(R))) ||
+        (e = hgrow(&b->h_ya, &b->c_hya, size_t(R))))
+        return hip_fail(e, "batch buffers");
+    Geometry g;
+    g.n = int(b->n);
+    g.h = int(b->h);
+    g.ring_len = int(R);
+    g.gain = b->gain;
+    DevTables t;
+    t.ws = d_ws;
+    t.den = d_den;
+    if ((e = launch_ola_gather_wrap(g, t, b->d_r + size_t(b->j0) * size_t(b->n), b->n, F, len, b->d_acc, b->d_ya,
+                                    b->s)) ||
+        (e = hipMemcpyAsync(b->h_ya, b->d_ya, sizeof(float) * size_t(R), hipMemcpyDeviceToHost, b->s)) ||
+        (e = hipEventRecord(b->ev, b->s)) || (e = hipEventSynchronize(b->ev)))
+        return hip_fail(e, "batch overlap-add (wrapped)");
+    b->ya = b->h_ya;
     return CRLOT_OK;
 }
 

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "crlot_dsp.h"
@@ -38,10 +39,26 @@ struct SharedServer;
 // end, j < *frames.  Returns false when there is none (objects.cpp).
 bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_t* frames);
 // The second source: the frames of the FrameQueue read last (getFrame /
-// copyFrame), from the frame just read on, as a host copy [frames][n]
-// (bench/performance_benchmark.cc:174-246 feeds each FrameQueue frame,
-// unwindowed, to the forward).  False when there is none (objects.cpp).
-bool framequeue_last_rows(int64_t n, std::vector<float>* rows, int64_t* hop, int64_t* frames, int* device);
+// copyFrame), from the frame just read on, copied [frames][n] into the buffer
+// dst(floats) returns (bench/performance_benchmark.cc:174-246 feeds each
+// FrameQueue frame, unwindowed, to the forward).  False when there is none, or
+// dst returns null (objects.cpp).
+bool framequeue_last_rows(int64_t n, int64_t* hop, int64_t* frames, int* device,
+                          const std::function<float*(size_t)>& dst);
+// The OLA object whose window was set last, when it is a mono, untouched,
+// apply_window_inside object of frame n, hop h on `device` (the harness builds it
+// before the loop, performance_benchmark.cc:195-197): its device window and
+// divisors, with `s` ordered after their upload, so a new batch can compute that
+// object's overlap-add speculatively (its first push is then served without a
+// device round trip).  tgen: its tables' generation (OLA upload_norm).
+struct FreshOla {
+    crlot_ola* o = nullptr;
+    const float* d_win = nullptr;
+    const float* d_den = nullptr;
+    int64_t R = 0;
+    uint64_t tgen = 0;
+};
+bool fresh_ola(int64_t n, int64_t h, int device, hipStream_t s, FreshOla* out);
 // Window tables the library built (crlot_window_table) or was handed
 // (OLAAccumulator::set_window), newest first, for the speculation's search.
 void note_window(const float* w, int64_t n);
@@ -60,29 +77,44 @@ struct BatchSpec {
     std::vector<float> sig;  // host copy of the remaining signal (verifies forward inputs)
     std::vector<float> win;  // the analysis window found
     bool rows_src = false;   // the FrameQueue source: forward inputs are the rows themselves
-    std::vector<float> rows; // its copy [M][n] (uploaded by run_chain)
     int64_t next_fwd = 0;    // frame whose forward comes next
     int64_t inv_ready = -1;  // frame whose forward was served and whose inverse may be asked
     int64_t pushed = -1;     // last frame whose inverse was served (push candidate)
-    // device / pinned buffers (grow-only)
+    // device / pinned buffers (grow-only).  The chain's results share one block
+    // each side (one copy back): spectra [M][N + 2] (interleaved complex),
+    // inverse frames [M][N] (= push inputs), produce blocks [M H + N - H] (after
+    // attach), and the fresh object's wrapped produce [R] (spec_ola)
     hipStream_t s = nullptr;
     hipEvent_t ev = nullptr;
     float* d_sig = nullptr;
-    float* d_p = nullptr;    // [M][N] analysis products, then reused
-    float* d_spec = nullptr; // [M][N + 2] spectra (interleaved complex)
-    float* d_r = nullptr;    // [M][N] inverse frames = push inputs
-    float* d_y = nullptr;    // [M][H] produce blocks (after attach)
-    float* h_stage = nullptr;
+    float* d_p = nullptr;    // [M][N] analysis products
+    float* d_blk = nullptr;
+    float* h_blk = nullptr;
+    float* m_blk = nullptr;    // h_blk / h_stage as the device addresses them (mapped pinned memory)
+    float* m_stage = nullptr;
+    float* d_spec = nullptr; // views into d_blk / h_blk
+    float* d_r = nullptr;
+    float* d_y = nullptr;
     float* h_spec = nullptr;
     float* h_r = nullptr;
     float* h_y = nullptr;
-    size_t c_sig = 0, c_p = 0, c_spec = 0, c_r = 0, c_y = 0, c_hs = 0, c_hspec = 0, c_hr = 0, c_hy = 0;  // capacities
+    float* d_acc = nullptr;  // [R] ring slots of a push-everything-first object (batch_alias)
+    float* d_ya = nullptr;   // [R] their produce (batch_alias without spec_ola)
+    float* h_ya = nullptr;
+    const float* ya = nullptr;  // the wrapped produce in use (h_ya or in h_blk)
+    float* h_stage = nullptr;  // the FrameQueue source: its rows [M][n] (verifies forward inputs)
+    size_t c_sig = 0, c_p = 0, c_blk = 0, c_hblk = 0, c_hs = 0, c_acc = 0, c_ya = 0, c_hya = 0;  // capacities
     // the OLA object the batch's inverses are pushed to (objects.cpp)
     crlot_ola* ola = nullptr;
     int64_t j0 = 0;          // first frame pushed to it
     float gain = 1.0f;
     bool y_ready = false;    // h_y holds blocks j0 .. M-1 (event ev)
     bool y_waited = false;
+    // the overlap-add computed with the chain for a fresh OLA object (fresh_ola),
+    // gain 1 and j0 = 0: h_y and the wrapped d_acc / h_ya, used if it attaches so
+    FreshOla spec_ola;
+    bool spec_y = false;     // computed with this batch
+    bool spec_used = false;  // the attached object is the one it was computed for
 };
 
 // abi.cpp fft_host, under sh->mu: a contiguous batch-1 real forward / inverse.
@@ -98,7 +130,15 @@ int ola_materialize_locked(crlot_ola* o);
 // its tables): produce blocks of frames j0 .. M-1, and the N - H samples after
 // them that only those frames reach, into h_y
 int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
-                 float gain, hipStream_t tables_stream);
+                 float gain, hipStream_t tables_stream, uint64_t tgen);
 int batch_wait_y(BatchSpec* b);
+// abi.cpp: the plan's K_rfft + K_irfft in one launch (CRLOT_EUNSUPPORTED: none)
+int plan_rfft_irfft(crlot_plan* p, const float* in, float* spec, float* r, float* r_host, int32_t batch,
+                    void* stream);
+// the attached object's ring once every batch frame j0 .. M-1 was pushed with no
+// produce between, the later pushes wrapping onto unread slots (the reference
+// harness's order, bench/performance_benchmark.cc:212-231): slots into d_acc,
+// their produce into h_ya (waited for)
+int batch_alias(BatchSpec* b, int64_t R, const float* d_ws, const float* d_den);
 
 }  // namespace crlot

@@ -132,6 +132,18 @@ hipError_t launch_synth_frames(const Geometry& g, const DevTables& t, const floa
 hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float* frames,
                              int64_t ld_frames, float* y, int n_streams, int64_t F,
                              int64_t ld_y, int64_t out_len, hipStream_t stream);
+// the ring slots [0, ring_len) after F frames pushed from position 0 with no
+// produce between (len = F h + max(0, n - h) positions; later positions wrap
+// onto earlier slots): acc = the slots, y = acc / den (k_ola_gather_wrap);
+// y_blocks (nullable): launch_ola_gather's produce blocks [len] too, same launch
+hipError_t launch_ola_gather_wrap(const Geometry& g, const DevTables& t, const float* frames, int64_t ld_frames,
+                                  int64_t F, int64_t len, float* acc, float* y, hipStream_t stream,
+                                  float* y_blocks = nullptr);
+// K_rfft then K_irfft of `batch` contiguous rows (power-of-two n, 256..2048) in
+// one launch (k_rfft_irfft): spectra [batch][ld_spec], inverse frames into r
+// (and r_host when not null), rows ld_r apart
+hipError_t launch_rfft_irfft(const Geometry& g, const DevTables& t, const float* in, int64_t ld_in, float* spec,
+                             int64_t ld_spec, float* r, float* r_host, int64_t ld_r, int batch, hipStream_t stream);
 
 // Any-size path (fft_any.h): any P = N/2 in 1..8192.  twany = build_any_twiddles(P)
 // on device.  kind: 0 rfft, 1 irfft, 2 cfft, 3 icfft; p = complex points of the

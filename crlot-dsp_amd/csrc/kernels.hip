@@ -1101,6 +1101,43 @@ __global__ __launch_bounds__(256) void k_ola_gather(const GatherArgs a) {
     a.y[s * a.ld_y + n] = acc / d;
 }
 
+// The ring a push-everything-first loop leaves (bench/performance_benchmark.cc
+// :212-231 pushes every frame, then produces): positions n and n + R share ring
+// slot n (RingBuffer::split wraps, OLAAccumulator.cc:86-107), and since R > N
+// the frames reaching n all precede the ones reaching n + R.  So slot p's sum is
+// k_ola_gather's chain over position p continued over p + R, p + 2R, ..., in
+// ascending frame order as the adds arrived.  acc[p]: the slot (what the ring
+// holds), y[p]: the produce of it (acc / den[p]).  frames: F frames at hops from
+// position 0, len = F h + max(0, N - h) positions.
+__device__ __forceinline__ float gather_chain(const GatherArgs& a, int64_t n, float acc) {
+    int64_t kmax = n / a.h;
+    if (kmax > a.F - 1) kmax = a.F - 1;
+    const int64_t kmin = n - a.n + 1 <= 0 ? 0 : (n - a.n + a.h) / a.h;
+    for (int64_t k = kmin; k <= kmax; ++k) {
+        const int64_t off = n - k * a.h;
+        acc = __builtin_fmaf(__builtin_fmaf(a.frames[k * a.ld_frames + off], a.ws[off], 0.0f), a.gain, acc);
+    }
+    return acc;
+}
+
+// y_len > 0: threads [0, y_len) first give k_ola_gather's produce blocks into
+// a.y (the same chain and division), the next R threads the wrapped slots into
+// acc_out / ya -- both overlap-adds of a batch in one launch
+__global__ __launch_bounds__(256) void k_ola_gather_wrap(const GatherArgs a, float* __restrict__ acc_out,
+                                                         float* ya, int64_t len, int64_t y_len) {
+    int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (p < y_len) {
+        a.y[p] = gather_chain(a, p, 0.0f) / a.den[p % a.ring_len];
+        return;
+    }
+    p -= y_len;
+    if (p >= a.ring_len) return;
+    float acc = 0.0f;
+    for (int64_t n = p; n < len; n += a.ring_len) acc = gather_chain(a, n, acc);
+    acc_out[p] = acc;
+    ya[p] = acc / a.den[p];
+}
+
 // The same arithmetic with a (sample block, stream) grid and no 64-bit
 // division: each 256-sample block's first sample n0 is split by h and ring_len
 // once (uniform), each thread finishes its quotient in float with one
@@ -1302,6 +1339,83 @@ __global__ __launch_bounds__(kBlock) void k_irfft(const FftArgs a) {
         const int64_t i0 = 2 * (lane + 64 * m);
         out[i0 * a.inc_out] = dev::sanit(v[m].r * a.inv_n);
         out[(i0 + 1) * a.inc_out] = dev::sanit(v[m].i * a.inv_n);
+    }
+}
+
+// The batched speculation's forward and inverse in one launch (batch.cpp
+// run_chain): K_rfft's arithmetic to the spectrum -- written out, and handed
+// through LDS to K_irfft's arithmetic -- so the bits of both kernels with one
+// dependent launch less.  r_host (nullable): a second copy of the inverse
+// frames, e.g. in host-mapped memory.
+template <int E>
+__global__ __launch_bounds__(kBlock) void k_rfft_irfft(const FftArgs a, float* __restrict__ r, float* r_host,
+                                                       int64_t ld_r) {
+    constexpr int P = 64 * E;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* st = tw + P;
+    cf* sth = st + P;
+    cf* bufs = sth + P;
+    load_tables<E>(a.t, tw, st, sth, nullptr, nullptr, false);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    cf* buf = bufs + wave * xbuf_elems<P>();
+    cf* xs = bufs + kWaves * xbuf_elems<P>() + wave * (P + 1);  // the spectrum, X[0 .. P]
+    const int64_t b = int64_t(blockIdx.x) * kWaves + wave;
+    if (b >= a.batch) return;
+    const float* in = a.in + b * a.ld_in;
+    cf v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int64_t i0 = 2 * (lane + 64 * m);
+        v[m].r = dev::sanit(in[i0]);
+        v[m].i = dev::sanit(in[i0 + 1]);
+    }
+    dev::fft_wave<E, false>(v, buf, tw, lane);
+#pragma unroll
+    for (int m = 0; m < E; ++m) buf[lane + 64 * m] = v[m];
+    dev::wave_lds_fence();
+    float* out = a.out + b * a.ld_out;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {  // (k_rfft's split)
+        const int k = lane + 64 * m;
+        const cf zk = v[m];
+        const cf fpnk = dev::conj(buf[(P - k) & (P - 1)]);
+        const cf f1 = dev::cadd(zk, fpnk);
+        const cf f2 = dev::csub(zk, fpnk);
+        const cf t = dev::cmul(f2, sth[k]);
+        cf xk = {__builtin_fmaf(f1.r, 0.5f, t.r), __builtin_fmaf(f1.i, 0.5f, t.i)}, xp;
+        if (k == 0) dev::dc_split(zk, xk, xp);
+        out[2 * k] = xk.r;
+        out[2 * k + 1] = xk.i;
+        xs[k] = xk;
+        if (k == 0) {
+            out[2 * P] = xp.r;
+            out[2 * P + 1] = xp.i;
+            xs[P] = xp;
+        }
+    }
+    dev::wave_lds_fence();
+#pragma unroll
+    for (int m = 0; m < E; ++m) {  // (k_irfft's merge)
+        const int k = lane + 64 * m;
+        const cf xk = xs[k];
+        const cf xpk = xs[P - k];
+        const cf w = st[k];
+        const cf fek = {xk.r + xpk.r, xk.i - xpk.i};
+        const cf tmp = {xk.r - xpk.r, xk.i + xpk.i};
+        v[m].r = __builtin_fmaf(tmp.r, w.r, __builtin_fmaf(tmp.i, w.i, fek.r));
+        v[m].i = __builtin_fmaf(tmp.i, w.r, __builtin_fmaf(-tmp.r, w.i, fek.i));
+        if (k == 0) v[m] = dev::dc_merge(xk, xpk);
+    }
+    dev::fft_wave<E, true>(v, buf, tw, lane);
+    float* ro = r + b * ld_r;
+    float* rh = r_host ? r_host + b * ld_r : nullptr;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int64_t i0 = 2 * (lane + 64 * m);
+        const float2 q = make_float2(dev::sanit(v[m].r * a.inv_n), dev::sanit(v[m].i * a.inv_n));
+        *reinterpret_cast<float2*>(ro + i0) = q;
+        if (rh) *reinterpret_cast<float2*>(rh + i0) = q;
     }
 }
 
@@ -2699,6 +2813,62 @@ hipError_t launch_ola_gather(const Geometry& g, const DevTables& t, const float*
     note_launch(CRLOT_K_GATHER, grid);
     hipLaunchKernelGGL(k_ola_gather, dim3(unsigned(grid)), dim3(256), 0, stream, a);
     return hipGetLastError();
+}
+
+hipError_t launch_ola_gather_wrap(const Geometry& g, const DevTables& t, const float* frames, int64_t ld_frames,
+                                  int64_t F, int64_t len, float* acc, float* y, hipStream_t stream, float* y_blocks) {
+    if (F <= 0 || len <= 0 || g.ring_len <= 0 || g.n > g.ring_len) return hipErrorInvalidValue;
+    GatherArgs a{};
+    a.frames = frames;
+    a.ws = t.ws;
+    a.den = t.den;
+    a.y = y_blocks;
+    a.ld_frames = ld_frames;
+    a.F = F;
+    a.n = g.n;
+    a.h = g.h;
+    a.ring_len = g.ring_len;
+    a.n_streams = 1;
+    a.gain = g.gain;
+    const int64_t y_len = y_blocks ? len : 0;
+    const int64_t grid = (y_len + int64_t(g.ring_len) + 255) / 256;
+    note_launch(CRLOT_K_GATHER, grid);
+    hipLaunchKernelGGL(k_ola_gather_wrap, dim3(unsigned(grid)), dim3(256), 0, stream, a, acc, y, len, y_len);
+    return hipGetLastError();
+}
+
+template <int E>
+static hipError_t rfft_irfft_e(const FftArgs& a, float* r, float* r_host, int64_t ld_r, hipStream_t stream) {
+    constexpr int P = 64 * E;
+    const size_t lds = lds_bytes_fft<E>() + sizeof(cf) * kWaves * (P + 1);
+    const int64_t grid = (int64_t(a.batch) + kWaves - 1) / kWaves;
+    hipError_t e = set_lds(k_rfft_irfft<E>, lds);
+    if (e != hipSuccess) return e;
+    note_launch(CRLOT_K_FFT, grid);
+    hipLaunchKernelGGL(k_rfft_irfft<E>, dim3(unsigned(grid)), dim3(kBlock), lds, stream, a, r, r_host, ld_r);
+    return hipGetLastError();
+}
+
+hipError_t launch_rfft_irfft(const Geometry& g, const DevTables& t, const float* in, int64_t ld_in, float* spec,
+                             int64_t ld_spec, float* r, float* r_host, int64_t ld_r, int batch, hipStream_t stream) {
+    if (batch <= 0) return hipErrorInvalidValue;
+    FftArgs a;
+    a.t = t;
+    a.in = in;
+    a.out = spec;
+    a.ld_in = ld_in;
+    a.inc_in = 1;
+    a.ld_out = ld_spec;
+    a.inc_out = 1;
+    a.batch = batch;
+    a.inv_n = g.inv_n;
+    switch (e_of(g.n)) {
+        case 2: return rfft_irfft_e<2>(a, r, r_host, ld_r, stream);
+        case 4: return rfft_irfft_e<4>(a, r, r_host, ld_r, stream);
+        case 8: return rfft_irfft_e<8>(a, r, r_host, ld_r, stream);
+        case 16: return rfft_irfft_e<16>(a, r, r_host, ld_r, stream);
+        default: return hipErrorInvalidValue;  // (4096: the spectra would not fit LDS beside the tables)
+    }
 }
 
 template <int E, bool INV, bool CPLX = false>

@@ -16,10 +16,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -264,6 +267,9 @@ struct crlot_ola {
     uint64_t vgen = 0;
     int64_t vread = 0;   // samples produced from the batch (absolute, from the attach)
     int64_t vlast = -1;  // last batch frame pushed
+    uint64_t tgen = 0;   // bumped by every table upload (upload_norm; batch.h fresh_ola)
+    bool valias = false; // a push wrapped onto unread slots (no produce yet): batch_alias serves the produces
+    bool vya = false;    // batch_alias ran (its slots are the ring, minus the ones read since)
 
     int64_t N() const { return cfg.frame_size; }
     int64_t H() const { return cfg.hop_size; }
@@ -283,8 +289,16 @@ struct ServerLock {
     }
 };
 
+// the OLA object whose window was set last (batch.h fresh_ola)
+std::mutex g_fresh_mu;
+crlot_ola* g_fresh_ola = nullptr;
+
 void ola_free(crlot_ola* o) {
     if (!o) return;
+    {
+        std::lock_guard<std::mutex> lk(g_fresh_mu);
+        if (g_fresh_ola == o) g_fresh_ola = nullptr;
+    }
     DeviceGuard g(o->device);
     if (o->shared) {
         std::lock_guard<std::mutex> lk(o->shared->mu);
@@ -300,15 +314,13 @@ void ola_free(crlot_ola* o) {
     // resources back to the pools (respool.h): device blocks stream-ordered on
     // the object's own stream, which then serves the next object
     for (auto& s : o->slot) {
-        if (s.ev) (void)hipEventDestroy(s.ev);
+        crlot::pool_event_put(o->device, s.ev);
         crlot::pool_pinned_put(s.h, s.cap * sizeof(float));
     }
     if (o->own) {
-        for (void* p : {static_cast<void*>(o->d_ring), static_cast<void*>(o->d_den), static_cast<void*>(o->d_win),
-                        static_cast<void*>(o->d_peak)})
-            crlot::pool_free(p, o->own);
+        crlot::pool_free(o->d_ring, o->own);  // the object's one device block (crlot_ola_create)
     }
-    if (o->order) (void)hipEventDestroy(o->order);
+    crlot::pool_event_put(o->device, o->order);
     crlot::pool_stream_put(o->device, o->own);
     delete o;
 }
@@ -341,7 +353,7 @@ hipError_t take_slot(crlot_ola* o, size_t floats, crlot_ola::Slot** out) {
         if ((e = hipEventSynchronize(s.ev)) != hipSuccess) return e;
         s.pending = false;
     }
-    if (!s.ev && (e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if (!s.ev && (e = crlot::pool_event(o->device, &s.ev)) != hipSuccess) return e;
     if (s.cap < floats) {
         crlot::pool_pinned_put(s.h, s.cap * sizeof(float));
         s.h = nullptr;
@@ -358,7 +370,10 @@ hipError_t take_slot(crlot_ola* o, size_t floats, crlot_ola::Slot** out) {
 
 // OLAAccumulator::initialize_normalization (OLAAccumulator.cc:260-288) -> den
 // on the device, ordered on the object's current stream.
+std::atomic<uint64_t> g_tgen{0};  // process-wide: a new object at a freed one's address never repeats a tgen
+
 int upload_norm(crlot_ola* o, hipStream_t s) {
+    o->tgen = g_tgen.fetch_add(1, std::memory_order_relaxed) + 1;
     const bool has_w = !o->window.empty();
     crlot_norm_table(has_w ? o->window.data() : nullptr, o->N(), o->H(), o->R,
                      o->cfg.apply_window_inside, o->cfg.eps, o->norm.data());
@@ -584,19 +599,25 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
             return 0;
         // a push reaching R samples past the oldest unread one wraps onto unread
         // ring data (the harness's push-everything-first order): the
-        // batch's overlap-add does not alias, the ring does -- leave it to the ring
-        if (start_sample + N > o->vread + o->R) return 0;
+        // batch's overlap-add does not alias, the ring does.  Before any produce
+        // the wrapped ring is still a function of the frames (batch_alias);
+        // after one, leave it to the ring
+        if (start_sample + N > o->vread + o->R) {
+            if (o->vread != 0) return 0;
+            o->valias = true;
+        }
     } else {
         if (!o->pristine || start_sample != 0 || o->read_pos != 0 || o->produced != 0) return 0;
         if (b->ola) {  // another object rode this batch: rebuild its ring first
             const int rc = crlot::ola_materialize_locked(b->ola);
             if (rc != CRLOT_OK) return rc;
         }
-        const int rc = crlot::batch_attach(o->shared, o, j, o->R, o->d_win, o->d_den, gain, o->own);
+        const int rc = crlot::batch_attach(o->shared, o, j, o->R, o->d_win, o->d_den, gain, o->own, o->tgen);
         if (rc != CRLOT_OK) return rc;
         o->vb = b;
         o->vgen = b->gen;
         o->vread = 0;
+        o->valias = o->vya = false;
     }
     b->pushed = -1;
     crlot::spec_count(crlot::kStatPush);
@@ -614,11 +635,31 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
 int batch_produce(crlot_ola* o, float* out, int64_t n) {
     crlot::BatchSpec* b = o->vb;
     if (!b || crlot::spec_mode() < 2 || b->ola != o || o->vgen != b->gen || o->flushing || o->C() != 1) return 0;
+    // (a read longer than the ring is clamped by RingBuffer::split: the ring's path)
+    if (n > o->R || o->read_pos != o->vread % o->R) return 0;
+    if (o->valias) {
+        // every frame pushed, none produced between: slot p holds the wrapped sum
+        // until read at position p, zero after (normalize_and_clear), so the
+        // reads give y[p] for p < R and 0 / den beyond
+        if (o->vlast != b->M - 1) return 0;
+        if (!o->vya) {
+            const int rc = crlot::batch_alias(b, o->R, o->d_win, o->d_den);
+            if (rc != CRLOT_OK) return rc;
+            o->vya = true;
+        }
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t t = o->vread + i;
+            out[i] = t < o->R ? b->ya[t] : 0.0f;
+        }
+        o->vread += n;
+        crlot::spec_count(crlot::kStatProduce);
+        return 1;
+    }
     // positions no later frame reaches: up to the last pushed frame's hop, or to
     // its end once the batch's last frame is pushed (no later frame exists)
     const int64_t final_end =
         (o->vlast - b->j0 + 1) * b->h + (o->vlast == b->M - 1 ? std::max<int64_t>(0, b->n - b->h) : 0);
-    if (o->vread + n > final_end || o->read_pos != o->vread % o->R) return 0;
+    if (o->vread + n > final_end) return 0;
     const int rc = crlot::batch_wait_y(b);
     if (rc != CRLOT_OK) return rc;
     std::memcpy(out, b->h_y + o->vread, sizeof(float) * size_t(n));
@@ -640,6 +681,16 @@ int ola_materialize(crlot_ola* o) {
     crlot::CallServer* sv = o->srv;
     int rc = sv ? sv->drain() : CRLOT_OK;
     if (rc != CRLOT_OK) return rc;
+    if (o->valias && o->vya) {  // the wrapped slots, the ones read since cleared
+        const int64_t z = std::min(o->vread, o->R);
+        hipError_t e = hipMemcpyAsync(o->d_ring, b->d_acc, sizeof(float) * size_t(o->R), hipMemcpyDeviceToDevice, o->own);
+        if (e == hipSuccess && z > 0) e = hipMemsetAsync(o->d_ring, 0, sizeof(float) * size_t(z), o->own);
+        if (e == hipSuccess) e = hipStreamSynchronize(o->own);
+        if (e != hipSuccess) return hip_fail(e, "OLA rebuild");
+        if (sv) sv->acquire_next();
+        o->spec.valid = false;
+        return CRLOT_OK;
+    }
     const int64_t N = o->N(), h = b->h;
     for (int64_t k = b->j0; k <= o->vlast; ++k) {
         const int64_t rel = (k - b->j0) * h, off = std::max<int64_t>(0, o->vread - rel);
@@ -694,28 +745,31 @@ int crlot_ola_create(const crlot_ola_config* cfg, crlot_ola** out) {
     o->norm.assign(size_t(o->R), 1.0f);
     const size_t C = size_t(o->C()), R = size_t(o->R), N = size_t(o->N());
     hipError_t e;
-    auto dmalloc = [&](auto** ptr, size_t bytes) {
-        void* v = nullptr;
-        const hipError_t r = crlot::pool_malloc(o->device, &v, bytes, o->own);
-        *ptr = static_cast<std::remove_pointer_t<decltype(ptr)>>(v);
-        return r;
-    };
-    if ((e = crlot::pool_stream(o->device, &o->own)) ||
-        (e = hipEventCreateWithFlags(&o->order, hipEventDisableTiming)) ||
-        (e = dmalloc(&o->d_ring, sizeof(float) * C * R)) || (e = dmalloc(&o->d_den, sizeof(float) * R)) ||
-        (e = dmalloc(&o->d_win, sizeof(float) * N)) || (e = dmalloc(&o->d_peak, sizeof(unsigned)))) {
+    // one device block: ring [C][R], peak, den [R], window [N] (256-byte
+    // aligned parts; ring and peak adjacent, so one memset clears both)
+    auto up = [](size_t bytes) { return (bytes + 255) & ~size_t(255); };
+    const size_t b_ring = up(sizeof(float) * C * R), b_peak = 256, b_den = up(sizeof(float) * R);
+    void* blk = nullptr;
+    if ((e = crlot::pool_stream(o->device, &o->own)) || (e = crlot::pool_event(o->device, &o->order)) ||
+        (e = crlot::pool_malloc(o->device, &blk, b_ring + b_peak + b_den + up(sizeof(float) * N), o->own))) {
         ola_free(o);
         return e == hipErrorOutOfMemory ? fail(CRLOT_ENOMEM, "OLA object allocation")
                                         : hip_fail(e, "OLA object allocation");
     }
-    if ((e = hipMemsetAsync(o->d_ring, 0, sizeof(float) * C * R, o->own)) ||
-        (e = hipMemsetAsync(o->d_peak, 0, sizeof(unsigned), o->own))) {
+    char* base = static_cast<char*>(blk);
+    o->d_ring = reinterpret_cast<float*>(base);
+    o->d_peak = reinterpret_cast<unsigned*>(base + b_ring);
+    o->d_den = reinterpret_cast<float*>(base + b_ring + b_peak);
+    o->d_win = reinterpret_cast<float*>(base + b_ring + b_peak + b_den);
+    if ((e = hipMemsetAsync(o->d_ring, 0, b_ring + sizeof(unsigned), o->own))) {
         ola_free(o);
         return hip_fail(e, "OLA object init");
     }
     (void)use_stream(o, o->own);
-    int rc = upload_norm(o, o->own);  // no window yet: all ones
-    if (rc == CRLOT_OK && (e = hipStreamSynchronize(o->own)) != hipSuccess) rc = hip_fail(e, "OLA init");
+    // no window yet: all ones.  Not waited for: every later use of the ring and
+    // tables is ordered after it on the object's stream (use_stream), and a
+    // device failure surfaces at the next synchronising call
+    int rc = upload_norm(o, o->own);
     if (rc != CRLOT_OK) {
         ola_free(o);
         return rc;
@@ -737,7 +791,12 @@ int crlot_ola_set_window(crlot_ola* o, const float* w, int32_t wlen) {
     o->window.assign(w, w + wlen);
     hipError_t e = use_stream(o, o->own);
     if (e != hipSuccess) return hip_fail(e, "stream order");
-    return upload_norm(o, o->own);
+    rc = upload_norm(o, o->own);
+    if (rc == CRLOT_OK) {
+        std::lock_guard<std::mutex> lk(g_fresh_mu);
+        g_fresh_ola = o;
+    }
+    return rc;
 }
 
 int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const float* window,
@@ -1072,10 +1131,17 @@ int crlot_normalize_and_clear(float* d_out, float* d_acc, const float* d_norm, f
 // on the device (k_fq_frames, ola.hip) and kept there (device_frames: the
 // GPU-native input of batched transforms); the reference's host-pointer
 // accessors read a host copy taken at construction.
+constexpr size_t kFqPinnedMax = size_t(16) << 20;
+
 struct crlot_framequeue {
     int device = 0;
     int64_t n = 0, h = 0, f = 0;
-    std::vector<float> frames;  // [frame][n] (getFrame / getAllFrames)
+    // [frame][n] (getFrame / getAllFrames): a pooled pinned block up to
+    // kFqPinnedMax bytes (no page faults on a fresh queue, a direct DMA for the
+    // device copy), plain heap memory beyond
+    float* frames = nullptr;
+    size_t count = 0, cap = 0;
+    bool pinned = false;
     // the same frames in HBM, uploaded at the first device_frames() (the GPU-native
     // input of batched transforms; the host-pointer accessors never need it)
     mutable std::mutex dmu;
@@ -1095,12 +1161,34 @@ void note_fq_read(const crlot_framequeue* q, int64_t idx) {
 }  // namespace
 
 namespace crlot {
-bool framequeue_last_rows(int64_t n, std::vector<float>* rows, int64_t* hop, int64_t* frames, int* device) {
+bool fresh_ola(int64_t n, int64_t h, int device, hipStream_t s, FreshOla* out) {
+    std::lock_guard<std::mutex> lk(g_fresh_mu);
+    crlot_ola* o = g_fresh_ola;
+    if (!o || !o->pristine || o->vb || o->mode == 2 || o->flushing || o->C() != 1 || o->N() != n || o->H() != h ||
+        o->device != device || !o->cfg.apply_window_inside || o->window.empty() || o->R < o->N())
+        return false;
+    // s after the tables' upload (the object's current stream; use_stream's pattern)
+    if (hipEventRecord(o->order, o->last_set ? o->last : o->own) != hipSuccess ||
+        hipStreamWaitEvent(s, o->order, 0) != hipSuccess)
+        return false;
+    out->o = o;
+    out->d_win = o->d_win;
+    out->d_den = o->d_den;
+    out->R = o->R;
+    out->tgen = o->tgen;
+    return true;
+}
+
+bool framequeue_last_rows(int64_t n, int64_t* hop, int64_t* frames, int* device,
+                          const std::function<float*(size_t)>& dst) {
     std::lock_guard<std::mutex> lk(g_pop_mu);
     const crlot_framequeue* q = g_last_fq;
     if (!q || q->n != n || g_last_fq_idx < 0 || g_last_fq_idx >= q->f) return false;
     const int64_t i = g_last_fq_idx;
-    rows->assign(q->frames.begin() + i * n, q->frames.end());
+    const size_t floats = size_t(q->f - i) * size_t(n);
+    float* d = dst(floats);
+    if (!d) return false;
+    std::memcpy(d, q->frames + size_t(i) * size_t(n), sizeof(float) * floats);
     *hop = q->h;
     *frames = q->f - i;
     *device = q->device;
@@ -1167,15 +1255,23 @@ int crlot_framequeue_create(const float* in, int64_t len, int64_t frame_size, in
     // a host-pointer class serves host memory, and framing a whole signal is one
     // pass of copies, cheaper here than a device round trip.
     const size_t nf = size_t(q->f) * size_t(q->n);
-    try {
-        q->frames.resize(nf);
-    } catch (const std::bad_alloc&) {
-        delete q;
-        return fail(CRLOT_ENOMEM, "FrameQueue allocation");
+    q->count = nf;
+    if (nf > 0) {
+        void* hb = nullptr;
+        if (sizeof(float) * nf <= kFqPinnedMax && crlot::pool_pinned(sizeof(float) * nf, &hb, &q->cap) == hipSuccess) {
+            q->frames = static_cast<float*>(hb);
+            q->pinned = true;
+        } else {
+            q->frames = new (std::nothrow) float[nf];
+            if (!q->frames) {
+                delete q;
+                return fail(CRLOT_ENOMEM, "FrameQueue allocation");
+            }
+        }
     }
     const int64_t pad = center ? frame_size / 2 : 0;
     for (int64_t k = 0; k < q->f; ++k) {
-        float* dst = q->frames.data() + size_t(k) * size_t(q->n);
+        float* dst = q->frames + size_t(k) * size_t(q->n);
         const int64_t o = k * hop_size - pad;
         const int64_t j0 = std::max<int64_t>(0, -o), j1 = std::min<int64_t>(frame_size, len - o);
         if (j1 > j0) std::memcpy(dst + j0, in + o + j0, sizeof(float) * size_t(j1 - j0));
@@ -1210,6 +1306,10 @@ void crlot_framequeue_destroy(crlot_framequeue* q) {
         DeviceGuard g(q->device);
         (void)hipFree(q->d_frames);
     }
+    if (q->pinned)
+        crlot::pool_pinned_put(q->frames, q->cap);
+    else
+        delete[] q->frames;
     delete q;
 }
 
@@ -1231,7 +1331,7 @@ const float* crlot_framequeue_frame(const crlot_framequeue* q, int64_t frame_idx
         return nullptr;
     }
     note_fq_read(q, frame_idx);
-    return q->frames.data() + size_t(frame_idx) * size_t(q->n);
+    return q->frames + size_t(frame_idx) * size_t(q->n);
 }
 
 int crlot_framequeue_copy_frame(const crlot_framequeue* q, int64_t frame_idx, float* out) {
@@ -1239,21 +1339,21 @@ int crlot_framequeue_copy_frame(const crlot_framequeue* q, int64_t frame_idx, fl
     if (frame_idx < 0 || frame_idx >= q->f) return fail(CRLOT_ERANGE, "Frame index out of range");
     if (!out) return fail(CRLOT_EINVAL, "Output buffer cannot be null");  // FrameQueue.cc:56-67
     note_fq_read(q, frame_idx);
-    std::memcpy(out, q->frames.data() + size_t(frame_idx) * size_t(q->n), sizeof(float) * size_t(q->n));
+    std::memcpy(out, q->frames + size_t(frame_idx) * size_t(q->n), sizeof(float) * size_t(q->n));
     return CRLOT_OK;
 }
 
-const float* crlot_framequeue_all_frames(const crlot_framequeue* q) { return q ? q->frames.data() : nullptr; }
+const float* crlot_framequeue_all_frames(const crlot_framequeue* q) { return q ? q->frames : nullptr; }
 
 const float* crlot_framequeue_device_frames(const crlot_framequeue* q) {
     if (!q) return nullptr;
     std::lock_guard<std::mutex> lk(q->dmu);
-    if (!q->d_frames && !q->frames.empty()) {  // uploaded on first use, then kept
+    if (!q->d_frames && q->count > 0) {  // uploaded on first use, then kept
         DeviceGuard g(q->device);
-        const size_t bytes = sizeof(float) * q->frames.size();
+        const size_t bytes = sizeof(float) * q->count;
         void* d = nullptr;
         hipError_t e = hipMalloc(&d, bytes);
-        if (e == hipSuccess) e = hipMemcpy(d, q->frames.data(), bytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(d, q->frames, bytes, hipMemcpyHostToDevice);
         if (e != hipSuccess) {
             if (d) (void)hipFree(d);
             hip_fail(e, "FrameQueue device frames");

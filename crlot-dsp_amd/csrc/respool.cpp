@@ -13,6 +13,7 @@ namespace {
 
 std::mutex g_mu;
 std::map<int, std::vector<hipStream_t>> g_streams;          // free streams per device
+std::map<int, std::vector<hipEvent_t>> g_events;           // free events per device
 std::map<size_t, std::vector<void*>> g_pinned;              // free pinned blocks per size class
 bool g_pool_set[64] = {};
 hipMemPool_t g_pool[64] = {};
@@ -48,6 +49,29 @@ void pool_stream_put(int device, hipStream_t s) {
         v.push_back(s);
     else
         (void)hipStreamDestroy(s);
+}
+
+hipError_t pool_event(int device, hipEvent_t* out) {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto& v = g_events[device];
+        if (!v.empty()) {
+            *out = v.back();
+            v.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipEventCreateWithFlags(out, hipEventDisableTiming);
+}
+
+void pool_event_put(int device, hipEvent_t ev) {
+    if (!ev) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto& v = g_events[device];
+    if (v.size() < 4 * kMaxFree)
+        v.push_back(ev);
+    else
+        (void)hipEventDestroy(ev);
 }
 
 hipError_t pool_pinned(size_t bytes, void** out, size_t* cap) {

@@ -17,6 +17,10 @@ namespace crlot {
 hipError_t pool_stream(int device, hipStream_t* out);
 void pool_stream_put(int device, hipStream_t s);
 
+// A timing-disabled event of `device` (created on first use, reused after put).
+hipError_t pool_event(int device, hipEvent_t* out);
+void pool_event_put(int device, hipEvent_t ev);
+
 // A pinned host block of at least `bytes` (*cap: its size; power-of-two classes).
 hipError_t pool_pinned(size_t bytes, void** out, size_t* cap);
 void pool_pinned_put(void* p, size_t cap);

@@ -42,6 +42,7 @@ int main(int argc, char** argv) {
         double total_us, loop_us;
         size_t frames;
         double fq_us, ola_us, first_fwd_us;  // construction of the FrameQueue / the OLA object; frame 0's forward
+        double part_us[5];                   // loop totals: getFrame + copy, forward (frames >= 1), inverse, add, produce
     };
     try {
         auto run = [&](bool interleaved) -> Times {
@@ -64,22 +65,36 @@ int main(int argc, char** argv) {
             std::vector<std::complex<float>> spectrum(N / 2 + 1);
             std::vector<float> processed(N), output(L + N);
             const auto t_loop = clk::now();
-            double first_fwd = 0.0;
+            double first_fwd = 0.0, part[5] = {0, 0, 0, 0, 0};
+            auto lap = [](clk::time_point& t, double& acc) {
+                const auto n = clk::now();
+                acc += std::chrono::duration<double, std::micro>(n - t).count();
+                t = n;
+            };
             size_t total = 0;
             float* ch_out[1] = {output.data()};
             for (size_t i = 0; i < frames.getNumFrames(); ++i) {
+                auto tp = clk::now();
                 const float* frame = frames.getFrame(i);
                 std::copy(frame, frame + N, processed.begin());
-                const auto tf0 = clk::now();
+                lap(tp, part[0]);
                 fft_plan->forward(processed.data(), spectrum.data());
-                if (i == 0) first_fwd = std::chrono::duration<double, std::micro>(clk::now() - tf0).count();
+                if (i == 0) {
+                    first_fwd = std::chrono::duration<double, std::micro>(clk::now() - tp).count();
+                    tp = clk::now();
+                } else {
+                    lap(tp, part[1]);
+                }
                 fft_plan->inverse(spectrum.data(), processed.data());
+                lap(tp, part[2]);
                 const float* ch_frames[1] = {processed.data()};
                 ola.add_frame_SoA(ch_frames, window.get(), i * H, 0, N, 1.0f);
+                lap(tp, part[3]);
                 if (interleaved && total < L) {
                     ch_out[0] = output.data() + total;
                     total += ola.produce(ch_out, H);
                 }
+                lap(tp, part[4]);
             }
             while (total < L) {
                 ch_out[0] = output.data() + total;
@@ -89,10 +104,11 @@ int main(int argc, char** argv) {
             }
             const auto t1 = clk::now();
             auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-            return Times{us(t0, t1), us(t_loop, t1), frames.getNumFrames(), us(t0, t_fq), us(t_fq, t_ola), first_fwd};
+            return Times{us(t0, t1), us(t_loop, t1), frames.getNumFrames(), us(t0, t_fq), us(t_fq, t_ola), first_fwd,
+                         {part[0], part[1], part[2], part[3], part[4]}};
         };
         for (int w = 0; w < 5; ++w) run(true);
-        std::vector<double> lit, ilv, lit_loop, ilv_loop, fq, olac, ff;
+        std::vector<double> lit, ilv, lit_loop, ilv_loop, fq, olac, ff, part[5];
         size_t F = 0;
         for (int i = 0; i < iters; ++i) {
             const Times a = run(false), b = run(true);
@@ -103,6 +119,7 @@ int main(int argc, char** argv) {
             fq.push_back(b.fq_us);
             olac.push_back(b.ola_us);
             ff.push_back(b.first_fwd_us);
+            for (int q = 0; q < 5; ++q) part[q].push_back(b.part_us[q]);
             F = a.frames;
         }
         // what the batched speculation served per interleaved iteration (batches,
@@ -119,11 +136,14 @@ int main(int argc, char** argv) {
                     "\"interleaved\": {\"total_us_p50\": %.2f, \"loop_us_p50\": %.2f, \"loop_us_per_frame\": %.3f, "
                     "\"served_per_iteration\": {\"batches\": %.1f, \"forwards\": %.1f, \"inverses\": %.1f, "
                     "\"pushes\": %.1f, \"produces\": %.1f, \"rebuilds\": %.1f}, "
-                    "\"framequeue_us_p50\": %.2f, \"ola_object_us_p50\": %.2f, \"first_forward_us_p50\": %.2f}}\n",
+                    "\"framequeue_us_p50\": %.2f, \"ola_object_us_p50\": %.2f, \"first_forward_us_p50\": %.2f, "
+                    "\"loop_parts_us_p50\": {\"get_copy\": %.2f, \"forward_rest\": %.2f, \"inverse\": %.2f, "
+                    "\"add\": %.2f, \"produce\": %.2f}}}\n",
                     L, N, H, F, iters, p50(lit), p50(lit_loop), p50(lit_loop) / double(F), p50(ilv), p50(ilv_loop),
                     p50(ilv_loop) / double(F), (s1[0] - s0[0]) / 10.0, (s1[1] - s0[1]) / 10.0,
                     (s1[2] - s0[2]) / 10.0, (s1[3] - s0[3]) / 10.0, (s1[4] - s0[4]) / 10.0, (s1[5] - s0[5]) / 10.0,
-                    p50(fq), p50(olac), p50(ff));
+                    p50(fq), p50(olac), p50(ff), p50(part[0]), p50(part[1]), p50(part[2]), p50(part[3]),
+                    p50(part[4]));
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 4;

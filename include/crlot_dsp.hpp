@@ -613,8 +613,6 @@ class FrameQueue {
                                                center ? 1 : 0, int32_t(pad_mode), device, &q_);
         if (rc != CRLOT_OK) check(rc, "FrameQueue");
         check(crlot_framequeue_info(q_, &f_, &n_, &h_), "FrameQueue");
-        const float* a = crlot_framequeue_all_frames(q_);
-        frames_.assign(a, a + size_t(f_ * n_));
     }
     ~FrameQueue() { crlot_framequeue_destroy(q_); }
     FrameQueue(const FrameQueue&) = delete;
@@ -633,13 +631,21 @@ class FrameQueue {
         if (output == nullptr) throw std::invalid_argument("Output buffer cannot be null");
         check(crlot_framequeue_copy_frame(q_, int64_t(frame_idx), output), "FrameQueue::copyFrame");
     }
-    const std::vector<float>& getAllFrames() const { return frames_; }
+    // (a copy made at the first call: most callers read frames one at a time)
+    const std::vector<float>& getAllFrames() const {
+        std::call_once(all_once_, [this] {
+            const float* a = crlot_framequeue_all_frames(q_);
+            if (a) frames_.assign(a, a + size_t(f_ * n_));
+        });
+        return frames_;
+    }
     const float* device_frames() const { return crlot_framequeue_device_frames(q_); }
 
    private:
     crlot_framequeue* q_ = nullptr;
     int64_t f_ = 0, n_ = 0, h_ = 0;
-    std::vector<float> frames_;
+    mutable std::once_flag all_once_;
+    mutable std::vector<float> frames_;
 };
 
 // dsp::axpy / axpy_windowed / normalize_and_clear (kernels.h:28-53): the

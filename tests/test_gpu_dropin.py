@@ -599,7 +599,7 @@ def test_batched_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, h):
     assert served["pushes"] == F and served["produces"] == F and served["rebuilds"] == 0, served
 
 
-def _pipeline_loop(pkg, x, n, h, interleaved=True, tamper=None):
+def _pipeline_loop(pkg, x, n, h, interleaved=True, tamper=None, gain=1.0):
     """bench/performance_benchmark.cc:174-246 through the drop-in objects (the
     harness/pipeline_bench loop): FrameQueue(x, N, H, centre) -> per frame:
     getFrame -> forward -> inverse -> add_frame_SoA(window, i H) [-> produce(H)]
@@ -622,7 +622,7 @@ def _pipeline_loop(pkg, x, n, h, interleaved=True, tamper=None):
             f[7] = np.nextafter(f[7], np.float32(np.inf))
         X = fft.forward_host(f[None])
         y = fft.inverse_host(X)[0]
-        ola.add_frame_SoA([y], w, i * h, 0, n, 1.0)
+        ola.add_frame_SoA([y], w, i * h, 0, n, gain)
         specs.append(np.asarray(X).copy())
         invs.append(y.copy())
         if interleaved and total < L:
@@ -650,7 +650,8 @@ def test_batched_pipeline_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, 
     per-call path's bits call by call (spectra, inverse frames, every produced
     sample, the tail included) and the oracle OLAAccumulator's; the counters show
     the batch served it.  In the harness's literal order (every push first) the
-    ring wraps and the batch leaves the pushes to the ring: same bits."""
+    ring wraps onto unread slots; the batch serves that order too (the wrapped
+    slots, k_ola_gather_wrap): same bits."""
     x = oracle.synth(L, n + h)
     try:
         pkg.set_call_speculation(1)
@@ -690,8 +691,82 @@ def test_batched_pipeline_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, 
     assert np.array_equal(bits(b[2]), bits(np.concatenate(outs)))
     served = {key: s1[key] - s0[key] for key in s1}
     assert served["batches"] == 1 and served["forwards"] == F and served["inverses"] == F, served
-    if interleaved:  # every push and produce served: no ring was rebuilt
-        assert served["pushes"] == F and served["rebuilds"] == 0 and served["produces"] > 0, served
+    # every push and produce served, in either order: no ring was rebuilt
+    assert served["pushes"] == F and served["rebuilds"] == 0 and served["produces"] > 0, served
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("interleaved", [True, False])
+def test_batched_pipeline_other_gain(pkg, oracle, torch_cuda, interleaved):
+    """Pushes with gain 0.5: the overlap-add the batch computed with its chain
+    (gain 1, for the OLA object whose window was set last) is not used; the
+    attach computes it with the pushes' gain: the per-call path's bits."""
+    n, h, L = 1024, 512, 16384
+    x = oracle.synth(L, 13)
+    try:
+        pkg.set_call_speculation(1)
+        a = _pipeline_loop(pkg, x, n, h, interleaved, gain=0.5)
+        pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats()
+        b = _pipeline_loop(pkg, x, n, h, interleaved, gain=0.5)
+        s1 = pkg.call_speculation_stats()
+    finally:
+        pkg.set_call_speculation(2)
+    assert np.array_equal(bits(a[2]), bits(b[2]))
+    served = {key: s1[key] - s0[key] for key in s1}
+    assert served["pushes"] == len(a[0]) and served["rebuilds"] == 0 and served["produces"] > 0, served
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("reads", [0, 3, 30])
+def test_wrapped_batch_rebuilds_the_ring_mid_read(pkg, oracle, torch_cuda, reads):
+    """The push-everything-first order, then `reads` produces of H, then a call
+    the batch did not predict (one more push, past the signal): the ring is
+    rebuilt from the wrapped slots with the ones already read cleared, and every
+    later produce has the per-call path's bits (reads = 0: the rebuild happens
+    before any wrapped produce, from the frames)."""
+    n, h, L = 1024, 512, 16384
+    x = oracle.synth(L, 11)
+    extra = oracle.synth(n, 12)
+
+    def run():
+        q = pkg.FrameQueue(x, n, h, center=True)
+        w = pkg.window_table(pkg.HANN, n)
+        fft = pkg.FftPlan(n, pkg.FFT_REAL)
+        cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                            apply_window_inside=True)
+        ola = pkg.OLAAccumulator(cfg)
+        ola.set_window(w)
+        F = q.getNumFrames()
+        for i in range(F):
+            y = fft.inverse_host(fft.forward_host(q.getFrame(i)[None]))[0]
+            ola.add_frame_SoA([y], w, i * h, 0, n, 1.0)
+        outs = []
+        for _ in range(reads):
+            got, chans = ola.produce(h)
+            outs.append(chans[0][:got].copy())
+        ola.add_frame_SoA([extra], w, F * h, 0, n, 1.0)
+        for _ in range(60):
+            got, chans = ola.produce(h)
+            if got == 0:
+                break
+            outs.append(chans[0][:got].copy())
+        ola.close()
+        q.close()
+        return np.concatenate(outs)
+
+    try:
+        pkg.set_call_speculation(1)
+        a = run()
+        pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats()
+        b = run()
+        s1 = pkg.call_speculation_stats()
+    finally:
+        pkg.set_call_speculation(2)
+    assert a.size == b.size and np.array_equal(bits(a), bits(b))
+    served = {key: s1[key] - s0[key] for key in s1}
+    assert served["batches"] == 1 and served["rebuilds"] == 1 and served["produces"] == reads, served
 
 
 @pytest.mark.gpu
