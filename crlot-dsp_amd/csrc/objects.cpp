@@ -377,16 +377,26 @@ int upload_norm(crlot_ola* o, hipStream_t s) {
     const bool has_w = !o->window.empty();
     crlot_norm_table(has_w ? o->window.data() : nullptr, o->N(), o->H(), o->R,
                      o->cfg.apply_window_inside, o->cfg.eps, o->norm.data());
-    crlot_ola::Slot* sl = nullptr;
-    hipError_t e = take_slot(o, size_t(o->R + o->N()), &sl);
-    if (e != hipSuccess) return hip_fail(e, "staging");
     const float eps = o->cfg.eps;
+    hipError_t e;
+    if (!has_w) {  // no window: all ones (crlot_norm_table), a fill, no staging
+        const float one = 1.0f > eps ? 1.0f : eps;  // normalize_and_clear's guard (kernels.cc:32)
+        unsigned bits = 0;
+        std::memcpy(&bits, &one, sizeof(bits));
+        if ((e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(o->d_den), int(bits), size_t(o->R), s)))
+            return hip_fail(e, "table upload");
+        return CRLOT_OK;
+    }
+    // den and window are adjacent on the device (crlot_ola_create): one copy
+    // from a staging slot laid out the same way
+    const size_t wo = size_t(o->d_win - o->d_den);
+    crlot_ola::Slot* sl = nullptr;
+    if ((e = take_slot(o, wo + size_t(o->N()), &sl)) != hipSuccess) return hip_fail(e, "staging");
     for (int64_t i = 0; i < o->R; ++i)  // normalize_and_clear's guard (kernels.cc:32)
         sl->h[i] = (o->norm[i] > eps) ? o->norm[i] : eps;
-    if (has_w) std::memcpy(sl->h + o->R, o->window.data(), sizeof(float) * size_t(o->N()));
-    if ((e = hipMemcpyAsync(o->d_den, sl->h, sizeof(float) * size_t(o->R), hipMemcpyHostToDevice, s)) ||
-        (has_w && (e = hipMemcpyAsync(o->d_win, sl->h + o->R, sizeof(float) * size_t(o->N()),
-                                      hipMemcpyHostToDevice, s))) ||
+    if (has_w) std::memcpy(sl->h + wo, o->window.data(), sizeof(float) * size_t(o->N()));
+    const size_t floats = has_w ? wo + size_t(o->N()) : size_t(o->R);
+    if ((e = hipMemcpyAsync(o->d_den, sl->h, sizeof(float) * floats, hipMemcpyHostToDevice, s)) ||
         (e = hipEventRecord(sl->ev, s)))
         return hip_fail(e, "table upload");
     sl->pending = true;
