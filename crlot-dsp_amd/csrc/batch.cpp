@@ -125,13 +125,18 @@ thread_local PhaseClock g_pc;
 // the forward input of frame j, as the loop forms it on the host (frame * w)
 bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
     if (b.rows_src) return std::memcmp(in, b.h_stage + size_t(j) * size_t(b.n), sizeof(float) * size_t(b.n)) == 0;
-    const int64_t L = int64_t(b.sig.size()), base = j * b.h;
-    for (int64_t i = 0; i < b.n; ++i) {
-        const int64_t t = base + i;
-        const float v = (t < L ? b.sig[size_t(t)] : 0.0f) * b.win[size_t(i)];
-        if (std::memcmp(&v, in + i, sizeof(float)) != 0) return false;
-    }
-    return true;
+    // the products into a scratch row, then one compare (a loop the compiler
+    // vectorises; the same IEEE products)
+    const int64_t L = int64_t(b.sig.size()), base = j * b.h, n = b.n;
+    const int64_t lim = std::max<int64_t>(0, std::min<int64_t>(n, L - base));
+    thread_local std::vector<float> row;
+    if (int64_t(row.size()) < n) row.resize(size_t(n));
+    float* r = row.data();
+    const float* sg = b.sig.data() + (lim > 0 ? base : 0);
+    const float* w = b.win.data();
+    for (int64_t i = 0; i < lim; ++i) r[i] = sg[i] * w[i];
+    for (int64_t i = lim; i < n; ++i) r[i] = 0.0f * w[i];
+    return std::memcmp(r, in, sizeof(float) * size_t(n)) == 0;
 }
 
 // run frames 0 .. M-1 of the found chain: products, forward, inverse (and the

@@ -645,19 +645,22 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
 int batch_produce(crlot_ola* o, float* out, int64_t n) {
     crlot::BatchSpec* b = o->vb;
     if (!b || crlot::spec_mode() < 2 || b->ola != o || o->vgen != b->gen || o->flushing || o->C() != 1) return 0;
-    // (a read longer than the ring is clamped by RingBuffer::split: the ring's path)
-    if (n > o->R || o->read_pos != o->vread % o->R) return 0;
+    if (o->read_pos != o->vread % o->R) return 0;
     if (o->valias) {
         // every frame pushed, none produced between: slot p holds the wrapped sum
         // until read at position p, zero after (normalize_and_clear), so the
-        // reads give y[p] for p < R and 0 / den beyond
+        // reads give y[p] for p < R and 0 / den beyond (position t reads slot
+        // t mod R, already read and cleared once t >= R).  A read longer than
+        // the ring (e2e_benchmark.cc's produce(T)) is clamped to it by
+        // RingBuffer::split: R outputs, out[R, n) untouched, every slot cleared
         if (o->vlast != b->M - 1) return 0;
         if (!o->vya) {
             const int rc = crlot::batch_alias(b, o->R, o->d_win, o->d_den);
             if (rc != CRLOT_OK) return rc;
             o->vya = true;
         }
-        for (int64_t i = 0; i < n; ++i) {
+        const int64_t m = std::min(n, o->R);
+        for (int64_t i = 0; i < m; ++i) {
             const int64_t t = o->vread + i;
             out[i] = t < o->R ? b->ya[t] : 0.0f;
         }
@@ -669,7 +672,8 @@ int batch_produce(crlot_ola* o, float* out, int64_t n) {
     // its end once the batch's last frame is pushed (no later frame exists)
     const int64_t final_end =
         (o->vlast - b->j0 + 1) * b->h + (o->vlast == b->M - 1 ? std::max<int64_t>(0, b->n - b->h) : 0);
-    if (o->vread + n > final_end) return 0;
+    // (a read longer than the ring is clamped by RingBuffer::split: the ring's path)
+    if (n > o->R || o->vread + n > final_end) return 0;
     const int rc = crlot::batch_wait_y(b);
     if (rc != CRLOT_OK) return rc;
     std::memcpy(out, b->h_y + o->vread, sizeof(float) * size_t(n));

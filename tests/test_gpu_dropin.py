@@ -807,10 +807,12 @@ def test_batched_loop_falls_back_on_a_broken_rhythm(pkg, oracle, torch_cuda, brk
 @pytest.mark.gpu
 def test_batched_loop_keeps_ring_aliasing_of_the_harness_order(pkg, oracle, torch_cuda):
     """bench/e2e_benchmark.cc's literal order pushes every frame before the
-    produce loop, so the 6144-sample OLA ring wraps onto unread data.
-    The batch's overlap-add does not alias; the pushes that would wrap are left to
-    the ring, so the output keeps the reference's aliasing: the same bits as the
-    per-call path and as the oracle OLAAccumulator fed the same calls."""
+    produce loop, so the 6144-sample OLA ring wraps onto unread data,
+    and its produce(T) reads past the ring's capacity (RingBuffer::split clamps
+    it: R outputs, the rest of the caller's buffer untouched).  The batch serves
+    both (the wrapped slots, k_ola_gather_wrap), keeping the reference's
+    aliasing: the same bits as the per-call path -- the untouched tail included --
+    and as the oracle OLAAccumulator fed the same calls."""
     n, h = 1024, 256
     x = oracle.synth(48_000, 11)
     w = pkg.window_table(pkg.HANN, n)
@@ -834,7 +836,7 @@ def test_batched_loop_keeps_ring_aliasing_of_the_harness_order(pkg, oracle, torc
             k += 1
         out = []
         while True:
-            got, chans = ola.produce(48_000)
+            got, chans = ola.produce(48_000, [np.full(48_000, 7.0, np.float32)])
             if got == 0 or sum(len(o) for o in out) >= 48_000:
                 break
             out.append(chans[0][:got].copy())
@@ -847,14 +849,20 @@ def test_batched_loop_keeps_ring_aliasing_of_the_harness_order(pkg, oracle, torc
         pkg.set_call_speculation(1)
         fa, ya = run()
         pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats()
         fb, yb = run()
+        s1 = pkg.call_speculation_stats()
     finally:
         pkg.set_call_speculation(2)
     assert all(np.array_equal(bits(a), bits(b)) for a, b in zip(fa, fb))
     assert np.array_equal(bits(ya), bits(yb))
+    assert np.all(yb[6144:48_000] == 7.0)  # the clamped read left the caller's tail alone
+    served = {key: s1[key] - s0[key] for key in s1}
+    assert served["pushes"] == len(fb) and served["produces"] == 2 and served["rebuilds"] == 0, served
     ref = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
     ref.set_window(w)
     for k, y in enumerate(fb):
         ref.push_frame_aos(y, k * h, 0, n, 1.0)
-    r = ref.produce(48_000)[0]
-    assert np.array_equal(bits(yb[:r.size]), bits(r))
+    r = np.full(48_000, 7.0, np.float32)
+    got = ref.produce_into(48_000, [r])
+    assert np.array_equal(bits(yb[:got]), bits(r[:got]))
