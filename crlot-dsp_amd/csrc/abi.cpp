@@ -1277,14 +1277,12 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
                                inc_out);
     }
     const size_t nin = size_t(batch) * size_t(in_len * in_w), nout = size_t(batch) * size_t(out_len * out_w);
-    p->pack.resize(std::max(nin, nout));
-    gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
     crlot::SharedServer* sh = crlot::shared_server(p->device, p->e, &rc);
     if (!sh) return rc;
     std::lock_guard<std::mutex> slk(sh->mu);
     crlot::CallServer* sv = sh->srv;
     // the batched speculation of the whole per-frame loop (batch.h): contiguous
-    // single real frames only
+    // single real frames only (read in place: no packing)
     if (kind < 2 && batch == 1 && inc_in == 1 && inc_out == 1 && crlot::spec_mode() >= 2) {
         int brc = 0;
         if (kind == 0) {
@@ -1296,6 +1294,8 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
         }
         if (brc != 0) return brc < 0 ? brc : CRLOT_OK;
     }
+    p->pack.resize(std::max(nin, nout));
+    gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
     if (kind == 1 && sh->fft.valid && sh->fft.index == sv->submitted() && sh->fft.batch == batch &&
         sv->live(sh->fft.slot) && std::memcmp(p->pack.data(), sh->fft.slot.out, sizeof(float) * nin) == 0) {
         // the spectrum the last forward returned, unchanged: its inverse is in the speculation slot

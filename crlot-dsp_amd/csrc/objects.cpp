@@ -289,6 +289,17 @@ struct ServerLock {
     }
 };
 
+// max |x[i]| folded as update_peak_meter's std::max chain does (a NaN never
+// wins a std::max(acc, NaN), so any grouping gives the same value): four lanes
+float peak_of(const float* x, int64_t n) {
+    float m[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int64_t i = 0;
+    for (; i + 4 <= n; i += 4)
+        for (int q = 0; q < 4; ++q) m[q] = std::max(m[q], std::fabs(x[i + q]));
+    for (; i < n; ++i) m[0] = std::max(m[0], std::fabs(x[i]));
+    return std::max(std::max(m[0], m[1]), std::max(m[2], m[3]));
+}
+
 // the OLA object whose window was set last (batch.h fresh_ola)
 std::mutex g_fresh_mu;
 crlot_ola* g_fresh_ola = nullptr;
@@ -827,8 +838,10 @@ int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const f
     DeviceGuard g(o->device);
     const bool uw = use_window(o, window != nullptr);
     const bool caller_win = uw && !o->cfg.apply_window_inside;
-    std::vector<const float*> rows;
-    for (int64_t c = 0; c < ok; ++c) rows.push_back(ch_frames[c] + start_off);
+    const float* rows_small[8];  // (no allocation for up to 8 channels)
+    std::vector<const float*> rows_big(ok > 8 ? size_t(ok) : 0);
+    const float** rows = ok > 8 ? rows_big.data() : rows_small;
+    for (int64_t c = 0; c < ok; ++c) rows[c] = ch_frames[c] + start_off;
     int rc = to_server(o);
     if (rc != CRLOT_OK) return rc;
     ServerLock lk(o);
@@ -840,7 +853,7 @@ int crlot_ola_add_frame_soa(crlot_ola* o, const float* const* ch_frames, const f
     rc = ok == o->C() ? try_chain_push(o, rows[0], uw, caller_win, start_sample, start_off, eff, gain) : 0;
     if (rc < 0) return rc;
     if (rc == 0)
-        rc = server_add(o, rows.data(), ok, false, caller_win ? window + start_off : nullptr,
+        rc = server_add(o, rows, ok, false, caller_win ? window + start_off : nullptr,
                         (uw && !caller_win) ? o->d_win + start_off : nullptr, start_sample, eff, gain);
     if (rc < 0) return rc;
     return ok < o->C() ? fail(CRLOT_EINVAL, "Channel frame pointer cannot be null") : CRLOT_OK;
@@ -935,7 +948,7 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
         if (rc == 0 && (rc = ola_materialize(o)) != CRLOT_OK) return rc;
         if (rc == 1) {
             o->read_pos = (o->read_pos + n) % o->R;  // :213
-            for (int64_t i = 0; i < n; ++i) o->host_peak = std::max(o->host_peak, std::fabs(ch_out[0][i]));
+            o->host_peak = std::max(o->host_peak, peak_of(ch_out[0], n));
             if (n_out) *n_out = n;
             return CRLOT_OK;
         }
@@ -985,10 +998,7 @@ int crlot_ola_produce(crlot_ola* o, float* const* ch_out, int64_t n, int64_t* n_
         for (int64_t c = 0; c < C; ++c) std::memcpy(ch_out[c], sl.out + c * len, sizeof(float) * size_t(len));
     }
     o->read_pos = (o->read_pos + n) % o->R;  // :213
-    for (int64_t i = 0; i < n; ++i) {        // update_peak_meter (:289-295), channel 0
-        const float a = std::fabs(ch_out[0][i]);
-        o->host_peak = std::max(o->host_peak, a);
-    }
+    o->host_peak = std::max(o->host_peak, peak_of(ch_out[0], n));  // update_peak_meter (:289-295), channel 0
     if (n_out) *n_out = n;
     return CRLOT_OK;
 }
