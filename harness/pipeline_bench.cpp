@@ -43,10 +43,10 @@ int main(int argc, char** argv) {
         size_t frames;
         double fq_us, ola_us, first_fwd_us;  // construction of the FrameQueue / the OLA object; frame 0's forward
         double part_us[5];                   // loop totals: getFrame + copy, forward (frames >= 1), inverse, add, produce
+        double destroy_us;                   // the objects' destruction (inside total_us)
     };
     try {
-        auto run = [&](bool interleaved) -> Times {
-            const auto t0 = clk::now();
+        auto run_objects = [&](bool interleaved, clk::time_point t0) -> Times {
             FrameQueue frames(x.data(), L, N, H, true);
             const auto t_fq = clk::now();
             auto window = WindowLUT::getInstance().GetWindowSafe(WindowType::HANN, N);
@@ -105,10 +105,20 @@ int main(int argc, char** argv) {
             const auto t1 = clk::now();
             auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
             return Times{us(t0, t1), us(t_loop, t1), frames.getNumFrames(), us(t0, t_fq), us(t_fq, t_ola), first_fwd,
-                         {part[0], part[1], part[2], part[3], part[4]}};
+                         {part[0], part[1], part[2], part[3], part[4]}, 0.0};
+        };
+        // the reference's iteration ends with its objects' destruction (the loop
+        // body's scope, performance_benchmark.cc:179-243): timed too
+        auto run = [&](bool interleaved) -> Times {
+            const auto t0 = clk::now();
+            Times t = run_objects(interleaved, t0);
+            const double end = std::chrono::duration<double, std::micro>(clk::now() - t0).count();
+            t.destroy_us = end - t.total_us;
+            t.total_us = end;
+            return t;
         };
         for (int w = 0; w < 5; ++w) run(true);
-        std::vector<double> lit, ilv, lit_loop, ilv_loop, fq, olac, ff, part[5];
+        std::vector<double> lit, ilv, lit_loop, ilv_loop, fq, olac, ff, part[5], dst;
         size_t F = 0;
         for (int i = 0; i < iters; ++i) {
             const Times a = run(false), b = run(true);
@@ -120,6 +130,7 @@ int main(int argc, char** argv) {
             olac.push_back(b.ola_us);
             ff.push_back(b.first_fwd_us);
             for (int q = 0; q < 5; ++q) part[q].push_back(b.part_us[q]);
+            dst.push_back(b.destroy_us);
             F = a.frames;
         }
         // what the batched speculation served per interleaved iteration (batches,
@@ -128,7 +139,8 @@ int main(int argc, char** argv) {
         crlot_call_speculation_stats(s0);
         for (int i = 0; i < 10; ++i) run(true);
         crlot_call_speculation_stats(s1);
-        // total: the reference's iteration (object construction included, :181-210);
+        // total: the reference's iteration (object construction and destruction
+        // included, :179-243);
         // loop: the per-frame calls and the produce loop only
         std::printf("{\"harness\": \"pipeline_bench\", \"reference\": \"bench/performance_benchmark.cc:174-246\", "
                     "\"input_length\": %zu, \"frame\": %zu, \"hop\": %zu, \"frames\": %zu, \"iterations\": %d, "
@@ -138,12 +150,12 @@ int main(int argc, char** argv) {
                     "\"pushes\": %.1f, \"produces\": %.1f, \"rebuilds\": %.1f}, "
                     "\"framequeue_us_p50\": %.2f, \"ola_object_us_p50\": %.2f, \"first_forward_us_p50\": %.2f, "
                     "\"loop_parts_us_p50\": {\"get_copy\": %.2f, \"forward_rest\": %.2f, \"inverse\": %.2f, "
-                    "\"add\": %.2f, \"produce\": %.2f}}}\n",
+                    "\"add\": %.2f, \"produce\": %.2f}, \"destroy_us_p50\": %.2f}}\n",
                     L, N, H, F, iters, p50(lit), p50(lit_loop), p50(lit_loop) / double(F), p50(ilv), p50(ilv_loop),
                     p50(ilv_loop) / double(F), (s1[0] - s0[0]) / 10.0, (s1[1] - s0[1]) / 10.0,
                     (s1[2] - s0[2]) / 10.0, (s1[3] - s0[3]) / 10.0, (s1[4] - s0[4]) / 10.0, (s1[5] - s0[5]) / 10.0,
                     p50(fq), p50(olac), p50(ff), p50(part[0]), p50(part[1]), p50(part[2]), p50(part[3]),
-                    p50(part[4]));
+                    p50(part[4]), p50(dst));
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 4;
