@@ -1025,9 +1025,12 @@ struct crlot_fft_plan {
 // constructs an FFT plan per iteration (bench/performance_benchmark.cc:188-210)
 // pays for the tables once per process, as the reference's FFT plan costs next
 // to nothing to construct.  Kept until the process ends.
+static std::mutex g_inner_mu;
+static std::map<std::pair<int, int>, crlot_plan*> g_inner;  // (device, frame size)
+
 static int shared_inner(const crlot_plan_desc& pd, crlot_plan** out) {
-    static std::mutex mu;
-    static std::map<std::pair<int, int>, crlot_plan*> plans;  // (device, frame size)
+    std::mutex& mu = g_inner_mu;
+    auto& plans = g_inner;
     std::lock_guard<std::mutex> lk(mu);
     const auto key = std::make_pair(pd.device, pd.frame_size);
     auto it = plans.find(key);

@@ -141,7 +141,37 @@ bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
 
 // run frames 0 .. M-1 of the found chain: products, forward, inverse (and the
 // overlap-add of a fresh OLA object); results to pinned memory in one copy
-int run_chain(BatchSpec* b, crlot_plan* inner) {
+// the overlap-add of a fresh OLA object (fresh_ola) after the chain's inverse
+// frames, both ways its produces may come (after each push; after every push,
+// the ring wrapped): into the result block (zero-copy: its host side)
+hipError_t launch_spec_ola(BatchSpec* b, int dev, bool zc_out) {
+    b->spec_y = b->spec_used = false;
+    if (!fresh_ola(b->n, b->h, dev, b->s, &b->spec_ola)) return hipSuccess;
+    const size_t N = size_t(b->n), M = size_t(b->M), row = N + 2, R = size_t(b->spec_ola.R);
+    const size_t ylen = M * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
+    if (M * row + M * N + ylen + R > b->c_blk || M * row + M * N + ylen + R > b->c_hblk) return hipSuccess;
+    hipError_t e;
+    if ((e = dgrow(&b->d_acc, &b->c_acc, R))) return e;
+    Geometry g;
+    g.n = int(b->n);
+    g.h = int(b->h);
+    g.ring_len = int(R);
+    g.gain = 1.0f;
+    DevTables t;
+    t.ws = b->spec_ola.d_win;
+    t.den = b->spec_ola.d_den;
+    float* yout = zc_out ? b->m_blk + (M * row + M * N) : b->d_y;
+    if ((e = launch_ola_gather_wrap(g, t, b->d_r, b->n, b->M, int64_t(ylen), b->d_acc, yout + ylen, b->s, yout)) ||
+        (!zc_out && (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * (ylen + R), hipMemcpyDeviceToHost, b->s))))
+        return e;
+    b->spec_y = true;
+    return hipSuccess;
+}
+
+// frames 0 .. M-1 of the found chain: products, forward, inverse (and the
+// overlap-add of a fresh OLA object), results to pinned memory; enqueued on
+// b->s up to the event b->ev (run_chain waits for it)
+int launch_chain(BatchSpec* b, crlot_plan* inner) {
     const size_t L = b->sig.size(), N = size_t(b->n), M = size_t(b->M), row = N + 2;
     const size_t ylen = M * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
     hipError_t e;
@@ -149,15 +179,14 @@ int run_chain(BatchSpec* b, crlot_plan* inner) {
         return hip_fail(e, "batch stream");
     if (!b->ev && (e = hipEventCreateWithFlags(&b->ev, hipEventDisableTiming)) != hipSuccess)
         return hip_fail(e, "batch event");
-    // the overlap-add of a fresh OLA object, both ways its produces may come
-    // (after each push; after every push, the ring wrapped), in the same round trip
     b->spec_y = b->spec_used = false;
     int dev = -1;
-    const bool fresh = hipGetDevice(&dev) == hipSuccess && fresh_ola(b->n, b->h, dev, b->s, &b->spec_ola);
-    const size_t R = fresh ? size_t(b->spec_ola.R) : 0, blk = M * row + M * N + ylen + R;
+    if ((e = hipGetDevice(&dev))) return hip_fail(e, "batch device");
+    // room for a fresh object's overlap-adds, whenever one comes (its ring: crlot_ring_len)
+    const size_t R = size_t(crlot_ring_len(b->n, b->h)), blk = M * row + M * N + ylen + R;
     const size_t had = b->c_hblk;
     if ((e = dgrow(&b->d_p, &b->c_p, M * N)) || (e = dgrow(&b->d_blk, &b->c_blk, blk)) ||
-        (e = hgrow(&b->h_blk, &b->c_hblk, blk)) || (fresh && (e = dgrow(&b->d_acc, &b->c_acc, R))))
+        (e = hgrow(&b->h_blk, &b->c_hblk, blk)))
         return hip_fail(e, "batch buffers");
     if (b->c_hblk != had || !b->m_blk) {
         void* m = nullptr;
@@ -209,28 +238,22 @@ int run_chain(BatchSpec* b, crlot_plan* inner) {
     if (!spec_r_host &&
         (e = hipMemcpyAsync(b->h_blk, b->d_blk, sizeof(float) * (M * row + M * N), hipMemcpyDeviceToHost, b->s)))
         return hip_fail(e, "batch results");
-    if (fresh) {
-        Geometry g;
-        g.n = int(b->n);
-        g.h = int(b->h);
-        g.ring_len = int(R);
-        g.gain = 1.0f;
-        DevTables t;
-        t.ws = b->spec_ola.d_win;
-        t.den = b->spec_ola.d_den;
-        float* yout = zc_out ? b->m_blk + (M * row + M * N) : b->d_y;
-        if ((e = launch_ola_gather_wrap(g, t, b->d_r, b->n, b->M, int64_t(ylen), b->d_acc, yout + ylen, b->s, yout)) ||
-            (!zc_out && (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * (ylen + R), hipMemcpyDeviceToHost, b->s))))
-            return hip_fail(e, "batch overlap-add");
-    }
+    if ((e = launch_spec_ola(b, dev, zc_out))) return hip_fail(e, "batch overlap-add");
     CRLOT_LAP(5);
     if ((e = hipEventRecord(b->ev, b->s))) return hip_fail(e, "batch results");
     CRLOT_LAP(6);
-    if ((e = hipEventSynchronize(b->ev))) return hip_fail(e, "batch results");
-    CRLOT_LAP(7);
-    b->spec_y = fresh;
     return CRLOT_OK;
 }
+
+int run_chain(BatchSpec* b, crlot_plan* inner) {
+    const int rc = launch_chain(b, inner);
+    if (rc != CRLOT_OK) return rc;
+    const hipError_t e = hipEventSynchronize(b->ev);
+    if (e != hipSuccess) return hip_fail(e, "batch results");
+    CRLOT_LAP(7);
+    return CRLOT_OK;
+}
+
 
 }  // namespace
 
@@ -294,8 +317,8 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
         if (rc != CRLOT_OK) return rc;
     }
     b->inv_ready = b->pushed = -1;
-    if (!inner) return 0;
     CRLOT_LAP_START();
+    if (!inner) return 0;
     // source 1: the Framer popped last, frame * a library window
     std::vector<float> sig;
     int64_t hop = 0, M = 0;
