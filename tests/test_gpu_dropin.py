@@ -641,7 +641,8 @@ def _pipeline_loop(pkg, x, n, h, interleaved=True, tamper=None, gain=1.0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,h,L", [(1024, 512, 16384), (1024, 256, 20_000), (960, 240, 9_600)])
+@pytest.mark.parametrize("n,h,L", [(1024, 512, 16384), (1024, 256, 20_000), (960, 240, 9_600), (256, 64, 6_000),
+                                   (512, 128, 8_000), (2048, 512, 30_000), (4096, 1024, 50_000)])
 @pytest.mark.parametrize("interleaved", [True, False])
 def test_batched_pipeline_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, h, L, interleaved):
     """The reference's second pipeline (performance_benchmark.cc: FrameQueue frames,
@@ -649,7 +650,8 @@ def test_batched_pipeline_loop_equals_per_call_path(pkg, oracle, torch_cuda, n, 
     batched speculation -- the FrameQueue read last is its source -- gives the
     per-call path's bits call by call (spectra, inverse frames, every produced
     sample, the tail included) and the oracle OLAAccumulator's; the counters show
-    the batch served it.  In the harness's literal order (every push first) the
+    the batch served it (256-2048: the fused forward+inverse launch; 960 and
+    4096: the two-launch chain).  In the harness's literal order (every push first) the
     ring wraps onto unread slots; the batch serves that order too (the wrapped
     slots, k_ola_gather_wrap): same bits."""
     x = oracle.synth(L, n + h)
