@@ -115,13 +115,13 @@ bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 
 struct DeviceGuard {
     int prev = -1;
+    bool moved = false;  // (restore only what this guard changed: one runtime query per call)
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (dev >= 0 && dev != prev) (void)hipSetDevice(dev);
+        if (dev >= 0 && dev != prev) moved = hipSetDevice(dev) == hipSuccess;
     }
     ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+        if (moved && prev >= 0) (void)hipSetDevice(prev);
     }
 };
 
