@@ -98,6 +98,12 @@ struct crlot_plan {
     bool stage_pending = false;
 };
 
+namespace crlot {
+// batch.cpp: a forward the running batch predicted, served with no device call
+// (1), else 0 with nothing changed -- the full batch_forward then decides
+int batch_serve_forward(SharedServer* sh, int64_t n, const float* in, float* out);
+}  // namespace crlot
+
 namespace {
 
 thread_local std::string g_err;
@@ -1012,6 +1018,7 @@ struct crlot_fft_plan {
     // instantiation for
     std::mutex mu;
     int e = 0;                          // K_call instantiation (0: staged launches)
+    crlot::SharedServer* sh = nullptr;  // its shared server once looked up (never destroyed)
     std::vector<float> pack;            // strided <-> dense staging
     float* d_stage = nullptr;           // staged-launch buffers (device)
     size_t stage_floats = 0;
@@ -1270,8 +1277,14 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     if (batch == 0) return CRLOT_OK;
     if (!in || !out) return fail(CRLOT_EINVAL, "null buffer");
     std::lock_guard<std::mutex> lk(p->mu);
-    DeviceGuard g(p->device);
     const int64_t n = p->nfft, bins = n / 2 + 1;
+    // a call the running batch serves touches no device state: no device switch
+    if (p->sh && kind < 2 && batch == 1 && inc_in == 1 && inc_out == 1 && crlot::spec_mode() >= 2) {
+        std::lock_guard<std::mutex> slk(p->sh->mu);
+        const int brc = kind == 0 ? crlot::batch_serve_forward(p->sh, n, in, out) : crlot::batch_inverse(p->sh, n, in, out);
+        if (brc != 0) return brc < 0 ? brc : CRLOT_OK;
+    }
+    DeviceGuard g(p->device);
     // element counts and widths of the input / output rows
     const int64_t in_len = kind == 0 ? n : kind == 1 ? bins : n, out_len = kind == 0 ? bins : kind == 1 ? n : n;
     const int in_w = kind == 0 ? 1 : 2, out_w = kind == 1 ? 1 : 2;
@@ -1282,6 +1295,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     const size_t nin = size_t(batch) * size_t(in_len * in_w), nout = size_t(batch) * size_t(out_len * out_w);
     crlot::SharedServer* sh = crlot::shared_server(p->device, p->e, &rc);
     if (!sh) return rc;
+    p->sh = sh;
     std::lock_guard<std::mutex> slk(sh->mu);
     crlot::CallServer* sv = sh->srv;
     // the batched speculation of the whole per-frame loop (batch.h): contiguous

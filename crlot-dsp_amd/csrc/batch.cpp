@@ -295,22 +295,26 @@ int batch_abort(SharedServer* sh) {
     return CRLOT_OK;
 }
 
+int batch_serve_forward(SharedServer* sh, int64_t n, const float* in, float* out) {
+    BatchSpec* b = sh->batch;
+    if (!b || spec_mode() < 2 || !b->active || b->n != n) return 0;
+    const int64_t j = b->next_fwd;
+    if (j >= b->M || !input_matches(*b, j, in)) return 0;
+    const size_t row = size_t(n) + 2;
+    std::memcpy(out, b->h_spec + size_t(j) * row, sizeof(float) * row);
+    b->next_fwd = j + 1;
+    b->inv_ready = j;
+    spec_count(kStatForward);
+    if (b->next_fwd == b->M) b->active = false;  // last frame: its inverse / push / produce still served
+    return 1;
+}
+
 int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* in, float* out) {
     if (spec_mode() < 2) return 0;
     if (!sh->batch) sh->batch = new BatchSpec();
     BatchSpec* b = sh->batch;
     const size_t row = size_t(n) + 2;
-    if (b->active && b->n == n) {
-        const int64_t j = b->next_fwd;
-        if (j < b->M && input_matches(*b, j, in)) {
-            std::memcpy(out, b->h_spec + size_t(j) * row, sizeof(float) * row);
-            b->next_fwd = j + 1;
-            b->inv_ready = j;
-            spec_count(kStatForward);
-            if (b->next_fwd == b->M) b->active = false;  // last frame: its inverse / push / produce still served
-            return 1;
-        }
-    }
+    if (batch_serve_forward(sh, n, in, out)) return 1;
     // a forward the batch did not predict: end it, then try to start one here
     if (b->active || b->ola) {
         const int rc = batch_abort(sh);
