@@ -245,11 +245,112 @@ __device__ __forceinline__ pc rot16_b(pc a, pc m) {
     return (pc){h, h} * m;  // J = 2, 6
 }
 
+// ---- FMA-fused (Goedecker) butterflies.  A twiddle w = C (1 + i T) (C = Re w,
+// T = Im w / Re w) is applied as y = x + T (i x): ONE v_pk_fma_f32 whose
+// operand swap and signs are op_sel / neg modifiers; C is left pending and
+// multiplies the next butterfly's add as an fma, so a twiddled radix-4
+// butterfly costs 11 packed operations instead of 14 (3 rotations of 2 + 8
+// adds).  The constants sit in SGPR pairs (K[SEL] picks a half).
+// b + (NEG ? -K[SEL] : K[SEL]) * a
+template <int SEL, bool NEG>
+__device__ __forceinline__ pc pk_fmak(pc a, pc k, pc b) {
+    pc r;
+    if constexpr (SEL == 0 && !NEG)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    else if constexpr (SEL == 0 && NEG)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    else if constexpr (SEL == 1 && !NEG)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[0,1,0] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    return r;
+}
+// (b.x + sl K[SEL] a.y, b.y + sh K[SEL] a.x), sl = NL ? -1 : 1, sh = NH ? -1 : 1
+template <int SEL, bool NL, bool NH>
+__device__ __forceinline__ pc pk_fmasw(pc a, pc k, pc b) {
+    static_assert(NL != NH, "one half negated");
+    pc r;
+    if constexpr (SEL == 0 && NL)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    else if constexpr (SEL == 0 && NH)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    else if constexpr (SEL == 1 && NL)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "s"(k), "v"(b));
+    return r;
+}
+// y = x + T (i x) with T = +K[SEL] (POS) or -K[SEL]
+template <int SEL, bool POS>
+__device__ __forceinline__ pc pk_yform(pc x, pc k) { return pk_fmasw<SEL, POS, !POS>(x, k, x); }
+// b + K[SEL] m(a) (PLUS) or b - K[SEL] m(a); m = multiply by -i (forward) / +i (inverse)
+template <bool INV, bool PLUS, int SEL>
+__device__ __forceinline__ pc pk_fma_mi(pc a, pc k, pc b) { return pk_fmasw<SEL, PLUS == INV, PLUS != INV>(a, k, b); }
+// y = x + T (i x) for T = +1 (POS) / -1: one v_pk_add_f32
+template <bool POS>
+__device__ __forceinline__ pc pk_yform1(pc x) { return POS ? pk_add_sw_nl(x, x) : pk_add_sw_nh(x, x); }
+
+// 16-point DFT constants: cos(pi/8), sin(pi/8); tan(pi/8), tan(3 pi/8); sqrt(1/2)
+__device__ __forceinline__ pc k16_cs() { return (pc){0.92387953251128675613f, 0.38268343236508977173f}; }
+__device__ __forceinline__ pc k16_tt() { return (pc){0.41421356237309504880f, 2.41421356237309504880f}; }
+__device__ __forceinline__ pc k16_h() { return (pc){0.70710678118654752440f, 0.70710678118654752440f}; }
+
 // In-place 16-point DFT, natural order in and out: X[k] = sum_n x[n] W16^{+-nk}.
-// n = 4 n1 + n2, k = k1 + 4 k2: four DFT4 over n1, twiddles W16^{n2 k1}, four
-// DFT4 over n2 (outputs renamed in registers, no data movement).
+// n = 4 n1 + n2, k = k1 + 4 k2: four DFT4 over n1, then four DFT4 over n2 whose
+// inputs carry W16^{n2 k1} -- in the Goedecker form above (72 packed operations,
+// 80 with explicit rotations); outputs renamed in registers, no data movement.
+//   k1 = 1: W^1 = C1 (1 -+ i t8), W^2 = h (1 -+ i), W^3 = S1 (1 -+ i t38)
+//   k1 = 2: W^2 (x9 + m x11), W^4 = m (free), as h (1 -+ i)
+//   k1 = 3: W^3, W^6 = -h (1 +- i), W^9 = -C1 (1 -+ i t8)
+// (upper signs forward; C1 = cos pi/8, S1 = sin pi/8, t8 = tan pi/8, t38 = tan 3pi/8)
 template <bool INV>
-__device__ __forceinline__ void pdft16(pc (&x)[16]) {
+__device__ __forceinline__ void pdft16_fma(pc (&x)[16]) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) pdft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
+    const pc kcs = k16_cs(), ktt = k16_tt(), kh = k16_h();
+    // the twiddled inputs' forms: k1 = 1 (x5, x6, x7), k1 = 3 (x13, x14, x15), k1 = 2 (x9 +- m x11)
+    const pc y5 = pk_yform<0, INV>(x[5], ktt);   // T = -+ t8
+    const pc y13 = pk_yform<1, INV>(x[13], ktt);  // T = -+ t38
+    const pc p = pc_add_mi<INV>(x[9], x[11]);
+    const pc y6 = pk_yform1<INV>(x[6]);           // T = -+ 1
+    const pc y14 = pk_yform1<!INV>(x[14]);        // T = +- 1
+    const pc q = pc_sub_mi<INV>(x[9], x[11]);
+    const pc y7 = pk_yform<1, INV>(x[7], ktt);   // T = -+ t38
+    const pc y15 = pk_yform<0, INV>(x[15], ktt);  // T = -+ t8
+    const pc yp = pk_yform1<INV>(p), yq = pk_yform1<INV>(q);
+    // first adds: u0 +- u2 and (u1 +- u3) / C(u1)
+    const pc a0 = pk_fmak<0, false>(y6, kh, x[4]), a1 = pk_fmak<0, true>(y6, kh, x[4]);
+    const pc b0 = pk_fmak<0, true>(y14, kh, x[12]), b1 = pk_fmak<0, false>(y14, kh, x[12]);
+    const pc c0 = pc_add_mi<INV>(x[8], x[10]), c1 = pc_sub_mi<INV>(x[8], x[10]);
+    const pc a2 = pk_fmak<0, false>(y7, ktt, y5), a3 = pk_fmak<0, true>(y7, ktt, y5);      // R = S1 / C1 = t8
+    const pc b2 = pk_fmak<1, true>(y15, ktt, y13), b3 = pk_fmak<1, false>(y15, ktt, y13);  // R = -C1 / S1 = -t38
+    pdft4<INV>(x[0], x[1], x[2], x[3]);
+    // outputs: X[k1 + 4 k2] at x[4 k1 + k2]
+    x[4] = pk_fmak<0, false>(a2, kcs, a0);
+    x[12] = pk_fmak<1, false>(b2, kcs, b0);
+    x[8] = pk_fmak<0, false>(yp, kh, c0);
+    x[6] = pk_fmak<0, true>(a2, kcs, a0);
+    x[14] = pk_fmak<1, true>(b2, kcs, b0);
+    x[10] = pk_fmak<0, true>(yp, kh, c0);
+    x[5] = pk_fma_mi<INV, true, 0>(a3, kcs, a1);
+    x[13] = pk_fma_mi<INV, true, 1>(b3, kcs, b1);
+    x[9] = pk_fma_mi<INV, true, 0>(yq, kh, c1);
+    x[7] = pk_fma_mi<INV, false, 0>(a3, kcs, a1);
+    x[15] = pk_fma_mi<INV, false, 1>(b3, kcs, b1);
+    x[11] = pk_fma_mi<INV, false, 0>(yq, kh, c1);
+    pc y[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1)
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) y[k1 + 4 * k2] = x[4 * k1 + k2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = y[i];
+}
+
+// The same DFT with explicit rotations (80 packed operations); kept for A/B
+// builds (-DCRLOT_PDFT16_CLASSIC).
+template <bool INV>
+__device__ __forceinline__ void pdft16_rot(pc (&x)[16]) {
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) pdft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
     // a[n2][k1] now at x[n2 + 4 k1]; multiply by W16^{n2 k1} (first halves of the
@@ -285,6 +386,15 @@ __device__ __forceinline__ void pdft16(pc (&x)[16]) {
         for (int k2 = 0; k2 < 4; ++k2) y[k1 + 4 * k2] = x[4 * k1 + k2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = y[i];
+}
+
+template <bool INV>
+__device__ __forceinline__ void pdft16(pc (&x)[16]) {
+#ifdef CRLOT_PDFT16_CLASSIC
+    pdft16_rot<INV>(x);
+#else
+    pdft16_fma<INV>(x);
+#endif
 }
 
 // Swap lane bit 4 with register bit 2 and lane bit 5 with register bit 3
