@@ -118,6 +118,9 @@ def lib():
         "crlot_plan_set_chunks": ([vp, i32], C.c_int),
         "crlot_set_call_speculation": ([i32], C.c_int),
         "crlot_call_speculation_stats": ([C.POINTER(i64)], C.c_int),
+        "crlot_call_speculation_stats_ex": ([C.POINTER(i64), i32], C.c_int),
+        "crlot_call_batch_capacity": ([C.POINTER(i64), C.POINTER(i64), C.POINTER(i64), C.POINTER(i64)], C.c_int),
+        "crlot_test_inject": ([i32, i32], C.c_int),
         "crlot_plan_last_launch": ([vp, vp, C.POINTER(LaunchInfo)], C.c_int),
         "crlot_kernel_name": ([i32], C.c_char_p),
         "crlot_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
@@ -230,6 +233,35 @@ def call_speculation_stats() -> dict:
     v = (C.c_int64 * 6)()
     _check(lib().crlot_call_speculation_stats(v), "crlot_call_speculation_stats")
     return dict(zip(("batches", "forwards", "inverses", "pushes", "produces", "rebuilds"), list(v)))
+
+
+SPEC_STATS = ("batches", "forwards", "inverses", "pushes", "produces", "rebuilds", "frames", "windows", "declined")
+
+
+def call_speculation_stats_ex() -> dict:
+    """All counters of the batched speculation (crlot_call_speculation_stats_ex):
+    the six above plus frames transformed by batch chains, window continuations and
+    declined speculations."""
+    v = (C.c_int64 * len(SPEC_STATS))()
+    _check(lib().crlot_call_speculation_stats_ex(v, len(SPEC_STATS)), "crlot_call_speculation_stats_ex")
+    return dict(zip(SPEC_STATS, list(v)))
+
+
+def call_batch_capacity() -> dict:
+    """Bounds of the batched speculation (crlot_call_batch_capacity): frames per
+    window, device / pinned bytes held now, pinned peak since load."""
+    v = [C.c_int64() for _ in range(4)]
+    _check(lib().crlot_call_batch_capacity(*[C.byref(x) for x in v]), "crlot_call_batch_capacity")
+    return dict(zip(("window_frames", "device_bytes", "pinned_bytes", "pinned_peak"), [x.value for x in v]))
+
+
+INJECT_BATCH_ALLOC = 1
+
+
+def test_inject(what: int, count: int):
+    """Test-only fault injection (crlot_test_inject): INJECT_BATCH_ALLOC fails the
+    next `count` buffer allocations of the batched speculation."""
+    _check(lib().crlot_test_inject(int(what), int(count)), "crlot_test_inject")
 
 
 def kernel_name(kernel_id: int) -> str:

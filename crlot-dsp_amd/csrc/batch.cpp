@@ -29,29 +29,55 @@ std::atomic<int> g_mode{2};
 constexpr float kOne = 1.0f;
 // crlot_call_speculation_stats: batches started, forwards / inverses / pushes /
 // produces served from a batch, OLA rings rebuilt
-std::atomic<int64_t> g_stats[6];
+std::atomic<int64_t> g_stats[kStatCount];
 
 std::mutex g_win_mu;
 std::vector<std::vector<float>> g_windows;  // newest first
 constexpr size_t kMaxWindows = 16;
 
+// crlot_test_inject(CRLOT_INJECT_BATCH_ALLOC, k): the next k batch buffer
+// allocations fail (tests of the fail-soft path)
+std::atomic<int> g_fail_alloc{0};
+bool injected_failure() {
+    int v = g_fail_alloc.load(std::memory_order_relaxed);
+    while (v > 0)
+        if (g_fail_alloc.compare_exchange_weak(v, v - 1, std::memory_order_relaxed)) return true;
+    return false;
+}
+
+// bytes the batches hold (crlot_call_batch_capacity): device, pinned, pinned peak
+std::atomic<int64_t> g_dev_bytes{0}, g_pin_bytes{0}, g_pin_peak{0};
+
 // grow-only device and pinned buffers
 hipError_t dgrow(float** p, size_t* cap, size_t need) {
     if (*cap >= need) return hipSuccess;
+    if (injected_failure()) return hipErrorOutOfMemory;
     if (*p) (void)hipFree(*p);
+    g_dev_bytes.fetch_sub(int64_t(*cap * sizeof(float)));
     *p = nullptr;
     *cap = 0;
     hipError_t e = hipMalloc(p, sizeof(float) * need);
-    if (e == hipSuccess) *cap = need;
+    if (e == hipSuccess) {
+        *cap = need;
+        g_dev_bytes.fetch_add(int64_t(need * sizeof(float)));
+    }
     return e;
 }
 hipError_t hgrow(float** p, size_t* cap, size_t need) {
     if (*cap >= need) return hipSuccess;
+    if (injected_failure()) return hipErrorOutOfMemory;
     if (*p) (void)hipHostFree(*p);
+    g_pin_bytes.fetch_sub(int64_t(*cap * sizeof(float)));
     *p = nullptr;
     *cap = 0;
     hipError_t e = hipHostMalloc(p, sizeof(float) * need, hipHostMallocDefault);
-    if (e == hipSuccess) *cap = need;
+    if (e == hipSuccess) {
+        *cap = need;
+        const int64_t now = g_pin_bytes.fetch_add(int64_t(need * sizeof(float))) + int64_t(need * sizeof(float));
+        int64_t pk = g_pin_peak.load();
+        while (now > pk && !g_pin_peak.compare_exchange_weak(pk, now)) {
+        }
+    }
     return e;
 }
 
@@ -124,10 +150,11 @@ thread_local PhaseClock g_pc;
 
 // the forward input of frame j, as the loop forms it on the host (frame * w)
 bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
-    if (b.rows_src) return std::memcmp(in, b.h_stage + size_t(j) * size_t(b.n), sizeof(float) * size_t(b.n)) == 0;
+    if (b.rows_src)
+        return std::memcmp(in, b.h_stage + size_t(j - b.wb) * size_t(b.n), sizeof(float) * size_t(b.n)) == 0;
     // the products into a scratch row, then one compare (a loop the compiler
-    // vectorises; the same IEEE products)
-    const int64_t L = int64_t(b.sig.size()), base = j * b.h, n = b.n;
+    // vectorises; the same IEEE products); sig starts at frame wb
+    const int64_t L = int64_t(b.sig.size()), base = (j - b.wb) * b.h, n = b.n;
     const int64_t lim = std::max<int64_t>(0, std::min<int64_t>(n, L - base));
     thread_local std::vector<float> row;
     if (int64_t(row.size()) < n) row.resize(size_t(n));
@@ -139,17 +166,49 @@ bool input_matches(const BatchSpec& b, int64_t j, const float* in) {
     return std::memcmp(r, in, sizeof(float) * size_t(n)) == 0;
 }
 
-// run frames 0 .. M-1 of the found chain: products, forward, inverse (and the
-// overlap-add of a fresh OLA object); results to pinned memory in one copy
-// the overlap-add of a fresh OLA object (fresh_ola) after the chain's inverse
-// frames, both ways its produces may come (after each push; after every push,
-// the ring wrapped): into the result block (zero-copy: its host side)
+// The result block laid out for `rows` frames (spectra [rows][N + 2], inverse
+// frames [rows][N], produce blocks [rows H + N - H], a fresh object's wrapped
+// produce [R]) and its views.
+size_t y_floats(const BatchSpec* b, size_t rows) {
+    return rows * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
+}
+void set_views(BatchSpec* b) {
+    const size_t N = size_t(b->n), rows = b->rows_cap, row = N + 2;
+    b->d_spec = b->d_blk;
+    b->d_r = b->d_spec + rows * row;
+    b->d_y = b->d_r + rows * N;
+    b->h_spec = b->h_blk;
+    b->h_r = b->h_spec + rows * row;
+    b->h_y = b->h_r + rows * N;
+}
+// buffers for `rows` frames (whatever they held is dropped when they grow)
+hipError_t ensure_rows(BatchSpec* b, size_t rows) {
+    const size_t N = size_t(b->n), R = size_t(crlot_ring_len(b->n, b->h));
+    const size_t blk = rows * (N + 2) + rows * N + y_floats(b, rows) + R;
+    const size_t had = b->c_hblk;
+    hipError_t e;
+    if ((e = dgrow(&b->d_p, &b->c_p, rows * N)) || (e = dgrow(&b->d_blk, &b->c_blk, blk)) ||
+        (e = hgrow(&b->h_blk, &b->c_hblk, blk)))
+        return e;
+    if (b->c_hblk != had || !b->m_blk) {
+        void* m = nullptr;
+        b->m_blk = hipHostGetDevicePointer(&m, b->h_blk, 0) == hipSuccess ? static_cast<float*>(m) : nullptr;
+    }
+    b->rows_cap = rows;
+    set_views(b);
+    return hipSuccess;
+}
+
+// the overlap-add of a fresh OLA object (fresh_ola) after the first window's
+// inverse frames, both ways its produces may come (after each push; after every
+// push, the ring wrapped -- meaningful for a one-window batch only): into the
+// result block (zero-copy: its host side)
 hipError_t launch_spec_ola(BatchSpec* b, int dev, bool zc_out) {
     b->spec_y = b->spec_used = false;
-    if (!fresh_ola(b->n, b->h, dev, b->s, &b->spec_ola)) return hipSuccess;
-    const size_t N = size_t(b->n), M = size_t(b->M), row = N + 2, R = size_t(b->spec_ola.R);
-    const size_t ylen = M * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
-    if (M * row + M * N + ylen + R > b->c_blk || M * row + M * N + ylen + R > b->c_hblk) return hipSuccess;
+    if (b->cb != 0 || !fresh_ola(b->n, b->h, dev, b->s, &b->spec_ola)) return hipSuccess;
+    const size_t N = size_t(b->n), rows = b->rows_cap, row = N + 2, R = size_t(b->spec_ola.R);
+    const size_t F = size_t(b->we), ylen = y_floats(b, F);
+    if (rows * row + rows * N + y_floats(b, rows) + R > std::min(b->c_blk, b->c_hblk)) return hipSuccess;
     hipError_t e;
     if ((e = dgrow(&b->d_acc, &b->c_acc, R))) return e;
     Geometry g;
@@ -160,20 +219,58 @@ hipError_t launch_spec_ola(BatchSpec* b, int dev, bool zc_out) {
     DevTables t;
     t.ws = b->spec_ola.d_win;
     t.den = b->spec_ola.d_den;
-    float* yout = zc_out ? b->m_blk + (M * row + M * N) : b->d_y;
-    if ((e = launch_ola_gather_wrap(g, t, b->d_r, b->n, b->M, int64_t(ylen), b->d_acc, yout + ylen, b->s, yout)) ||
+    float* yout = zc_out ? b->m_blk + (rows * row + rows * N) : b->d_y;
+    if ((e = launch_ola_gather_wrap(g, t, b->d_r, b->n, int64_t(F), int64_t(ylen), b->d_acc, yout + ylen, b->s,
+                                    yout)) ||
         (!zc_out && (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * (ylen + R), hipMemcpyDeviceToHost, b->s))))
         return e;
     b->spec_y = true;
     return hipSuccess;
 }
 
-// frames 0 .. M-1 of the found chain: products, forward, inverse (and the
-// overlap-add of a fresh OLA object), results to pinned memory; enqueued on
-// b->s up to the event b->ev (run_chain waits for it)
-int launch_chain(BatchSpec* b, crlot_plan* inner) {
-    const size_t L = b->sig.size(), N = size_t(b->n), M = size_t(b->M), row = N + 2;
-    const size_t ylen = M * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
+// the attached object's produce blocks over the buffer's frames [cb, we): the
+// window's positions from wb on are complete (the carried frames reach the
+// first ones)
+hipError_t launch_ola_window(BatchSpec* b, bool zc_out) {
+    const size_t N = size_t(b->n), rows = b->rows_cap, row = N + 2;
+    const int64_t F = b->we - b->cb;
+    const size_t ylen = y_floats(b, size_t(F));
+    // the gather divides position p by den[p mod R] from its own origin, frame cb's
+    // start, which sits (cb - j0) H into the object's ring: a rotated copy of the
+    // divisors puts that origin at index 0
+    const size_t R = size_t(b->ola_R), off = size_t((b->cb - b->j0) * b->h) % R;
+    hipError_t e;
+    if ((e = dgrow(&b->d_den_rot, &b->c_den_rot, R)) ||
+        (e = hipMemcpyAsync(b->d_den_rot, b->ola_den + off, sizeof(float) * (R - off), hipMemcpyDeviceToDevice, b->s)) ||
+        (off > 0 && (e = hipMemcpyAsync(b->d_den_rot + (R - off), b->ola_den, sizeof(float) * off,
+                                        hipMemcpyDeviceToDevice, b->s))))
+        return e;
+    Geometry g;
+    g.n = int(b->n);
+    g.h = int(b->h);
+    g.ring_len = int(R);
+    g.gain = b->gain;
+    DevTables t;
+    t.ws = b->ola_ws;
+    t.den = b->d_den_rot;
+    float* yout = zc_out ? b->m_blk + (rows * row + rows * N) : b->d_y;
+    if ((e = launch_ola_gather(g, t, b->d_r, b->n, yout, 1, F, int64_t(ylen), int64_t(ylen), b->s)) ||
+        (!zc_out && (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * ylen, hipMemcpyDeviceToHost, b->s))))
+        return e;
+    b->y_base = (b->cb - b->j0) * b->h;
+    b->y_lo = (b->wb - b->j0) * b->h;
+    b->y_ready = true;
+    b->y_waited = false;
+    return hipSuccess;
+}
+
+// the window's new frames [wb, we) (carry frames before them already in rows
+// [0, carry) of d_r): products, forward, inverse, and the overlap-add of the
+// attached object (continuing) or of a fresh one (first window); results to
+// pinned memory; enqueued on b->s up to the event b->ev (run_chain waits for it)
+int launch_chain(BatchSpec* b, crlot_plan* inner, int64_t carry) {
+    const size_t N = size_t(b->n), F = size_t(b->we - b->wb), rows = b->rows_cap, row = N + 2;
+    const size_t L = b->sig.size();
     hipError_t e;
     if (!b->s && (e = hipStreamCreateWithFlags(&b->s, hipStreamNonBlocking)) != hipSuccess)
         return hip_fail(e, "batch stream");
@@ -182,22 +279,7 @@ int launch_chain(BatchSpec* b, crlot_plan* inner) {
     b->spec_y = b->spec_used = false;
     int dev = -1;
     if ((e = hipGetDevice(&dev))) return hip_fail(e, "batch device");
-    // room for a fresh object's overlap-adds, whenever one comes (its ring: crlot_ring_len)
-    const size_t R = size_t(crlot_ring_len(b->n, b->h)), blk = M * row + M * N + ylen + R;
-    const size_t had = b->c_hblk;
-    if ((e = dgrow(&b->d_p, &b->c_p, M * N)) || (e = dgrow(&b->d_blk, &b->c_blk, blk)) ||
-        (e = hgrow(&b->h_blk, &b->c_hblk, blk)))
-        return hip_fail(e, "batch buffers");
-    if (b->c_hblk != had || !b->m_blk) {
-        void* m = nullptr;
-        b->m_blk = hipHostGetDevicePointer(&m, b->h_blk, 0) == hipSuccess ? static_cast<float*>(m) : nullptr;
-    }
-    b->d_spec = b->d_blk;
-    b->d_r = b->d_spec + M * row;
-    b->d_y = b->d_r + M * N;
-    b->h_spec = b->h_blk;
-    b->h_r = b->h_spec + M * row;
-    b->h_y = b->h_r + M * N;
+    if (size_t(carry) + F > rows) return set_error(CRLOT_ERUNTIME, "batch window exceeds its buffers");
     // zero-copy (default): the kernels read the pinned rows and write the host
     // copies of their results themselves -- no copy engine, one dependent launch
     // fewer per copy
@@ -207,7 +289,7 @@ int launch_chain(BatchSpec* b, crlot_plan* inner) {
     if (b->rows_src) {  // the FrameQueue's rows (already in h_stage) are the forward inputs
         if (zero_copy_in() && b->m_stage)
             d_in = b->m_stage;
-        else if ((e = hipMemcpyAsync(b->d_p, b->h_stage, sizeof(float) * M * N, hipMemcpyHostToDevice, b->s)))
+        else if ((e = hipMemcpyAsync(b->d_p, b->h_stage, sizeof(float) * F * N, hipMemcpyHostToDevice, b->s)))
             return hip_fail(e, "batch frames");
     } else {
         b->m_stage = nullptr;  // (h_stage may move; the rows source maps it again)
@@ -216,44 +298,164 @@ int launch_chain(BatchSpec* b, crlot_plan* inner) {
         std::memcpy(b->h_stage, b->sig.data(), sizeof(float) * L);
         std::memcpy(b->h_stage + L, b->win.data(), sizeof(float) * N);
         if ((e = hipMemcpyAsync(b->d_sig, b->h_stage, sizeof(float) * (L + N), hipMemcpyHostToDevice, b->s)) ||
-            (e = launch_windowed_frames(b->d_sig, int64_t(L), b->d_sig + L, b->d_p, b->M, b->n, b->h, b->s)))
+            (e = launch_windowed_frames(b->d_sig, int64_t(L), b->d_sig + L, b->d_p, int64_t(F), b->n, b->h, b->s)))
             return hip_fail(e, "batch frames");
     }
     CRLOT_LAP(2);
     // forward + inverse: one launch where the plan has the fused kernel
+    const size_t c = size_t(carry);
+    float* spec_dev = b->d_spec + c * row;
+    float* r_dev = b->d_r + c * N;
     bool spec_r_host = false;
-    int rc = fuse_fft() ? plan_rfft_irfft(inner, d_in, zc_out ? b->m_blk : b->d_spec, b->d_r,
-                                          zc_out ? b->m_blk + M * row : nullptr, int32_t(M), b->s)
+    int rc = fuse_fft() ? plan_rfft_irfft(inner, d_in, zc_out ? b->m_blk + c * row : spec_dev, r_dev,
+                                          zc_out ? b->m_blk + rows * row + c * N : nullptr, int32_t(F), b->s)
                         : CRLOT_EUNSUPPORTED;
     if (rc == CRLOT_OK) {
         spec_r_host = zc_out;
     } else if (rc == CRLOT_EUNSUPPORTED) {
-        rc = crlot_rfft_batched(inner, d_in, b->d_spec, int32_t(M), int64_t(N), 1, int64_t(row), 1, b->s);
+        rc = crlot_rfft_batched(inner, d_in, spec_dev, int32_t(F), int64_t(N), 1, int64_t(row), 1, b->s);
         CRLOT_LAP(3);
         if (rc == CRLOT_OK)
-            rc = crlot_irfft_batched(inner, b->d_spec, b->d_r, int32_t(M), int64_t(row), 1, int64_t(N), 1, b->s);
+            rc = crlot_irfft_batched(inner, spec_dev, r_dev, int32_t(F), int64_t(row), 1, int64_t(N), 1, b->s);
     }
     if (rc != CRLOT_OK) return rc;
     CRLOT_LAP(4);
     if (!spec_r_host &&
-        (e = hipMemcpyAsync(b->h_blk, b->d_blk, sizeof(float) * (M * row + M * N), hipMemcpyDeviceToHost, b->s)))
+        ((e = hipMemcpyAsync(b->h_spec + c * row, spec_dev, sizeof(float) * F * row, hipMemcpyDeviceToHost, b->s)) ||
+         (e = hipMemcpyAsync(b->h_r + c * N, r_dev, sizeof(float) * F * N, hipMemcpyDeviceToHost, b->s))))
         return hip_fail(e, "batch results");
-    if ((e = launch_spec_ola(b, dev, zc_out))) return hip_fail(e, "batch overlap-add");
+    if ((e = b->ola ? launch_ola_window(b, zc_out) : launch_spec_ola(b, dev, zc_out)))
+        return hip_fail(e, "batch overlap-add");
     CRLOT_LAP(5);
     if ((e = hipEventRecord(b->ev, b->s))) return hip_fail(e, "batch results");
     CRLOT_LAP(6);
+    g_stats[kStatFrames].fetch_add(int64_t(F), std::memory_order_relaxed);
     return CRLOT_OK;
 }
 
-int run_chain(BatchSpec* b, crlot_plan* inner) {
-    const int rc = launch_chain(b, inner);
+int run_chain(BatchSpec* b, crlot_plan* inner, int64_t carry) {
+    const int rc = launch_chain(b, inner, carry);
     if (rc != CRLOT_OK) return rc;
     const hipError_t e = hipEventSynchronize(b->ev);
     if (e != hipSuccess) return hip_fail(e, "batch results");
+    if (b->ola) b->y_waited = true;
     CRLOT_LAP(7);
     return CRLOT_OK;
 }
 
+// frame 0 of a source against the caller's input: (frame * w) bit for bit, for
+// one of the library's windows
+const std::vector<float>* window_match(const float* frame0, const float* in, int64_t n,
+                                       const std::vector<std::vector<float>>& wins) {
+    for (const auto& w : wins) {
+        bool ok = true;
+        for (int64_t i = 0; i < n && ok; ++i) {
+            const float v = frame0[i] * w[size_t(i)];
+            ok = std::memcmp(&v, in + i, sizeof(float)) == 0;
+        }
+        if (ok) return &w;
+    }
+    return nullptr;
+}
+
+// the pinned staging rows of the FrameQueue source (mapped for zero-copy reads)
+float* stage_rows(BatchSpec* b, size_t floats, hipError_t* he) {
+    const size_t had = b->c_hs;
+    *he = hgrow(&b->h_stage, &b->c_hs, floats);
+    if (*he != hipSuccess) return nullptr;
+    if (b->c_hs != had || !b->m_stage) {
+        void* m = nullptr;
+        b->m_stage = hipHostGetDevicePointer(&m, b->h_stage, 0) == hipSuccess ? static_cast<float*>(m) : nullptr;
+    }
+    return b->h_stage;
+}
+
+// A speculation that could not start or continue: the caller's own path runs.
+// Clears the error a failed allocation or launch recorded.
+int decline(BatchSpec* b) {
+    b->active = false;
+    b->inv_ready = b->pushed = -1;
+    b->we = b->next_fwd;  // nothing more is served from this batch
+    b->M = b->we;
+    (void)hipGetLastError();
+    g_stats[kStatDeclined].fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+
+// The next window of a running batch: the forward of frame we, read from the
+// same source.  1: served; 0: not a continuation (or declined); < 0: error.
+int continue_window(SharedServer* sh, BatchSpec* b, crlot_plan* inner, int64_t n, const float* in, float* out) {
+    int64_t hop = 0, F = 0, total = 0;
+    uint64_t src = 0;
+    if (!b->rows_src) {
+        std::vector<float> sig;
+        const std::vector<float>* w = &b->win;
+        auto accept = [&](const float* f0, int64_t h) { return h == b->h && window_match(f0, in, n, {*w}) != nullptr; };
+        if (!framer_last_signal(n, kBatchWindow, accept, &sig, &hop, &F, &total, &src)) return 0;
+        if (src != b->source || total != b->M - b->we) return 0;
+        b->sig.swap(sig);
+    } else {
+        int qdev = -1;
+        int64_t first = 0;
+        hipError_t he = hipSuccess;
+        auto accept = [&](const float* r0) { return std::memcmp(r0, in, sizeof(float) * size_t(n)) == 0; };
+        auto dst = [&](size_t floats) { return stage_rows(b, floats, &he); };
+        const bool got = framequeue_last_rows(n, kBatchWindow, accept, &hop, &F, &total, &qdev, &src, &first, dst);
+        if (he != hipSuccess) return decline(b);
+        if (!got) return 0;
+        if (src != b->source || first != b->src_first + b->we || hop != b->h) return 0;
+    }
+    // the attached object: carry its last frames' inverse outputs over, or rebuild
+    // its ring now, while the frames it needs are still in the buffers
+    int64_t carry = 0;
+    if (b->ola) {
+        const int64_t P = (b->n + b->h - 1) / b->h - 1, first = std::max(b->we - P, b->j0);
+        const bool keep = P <= kBatchWarm && first >= b->cb && b->row(first) >= size_t(b->we - first) &&
+                          size_t(b->we - first) + size_t(F) <= b->rows_cap && ola_can_continue(b->ola, b);
+        if (keep) {
+            carry = b->we - first;
+        } else {
+            crlot_ola* o = b->ola;
+            b->ola = nullptr;
+            const int rc = ola_materialize_locked(o);
+            if (rc != CRLOT_OK) return rc;
+        }
+    }
+    if (carry > 0) {
+        const hipError_t e = hipMemcpyAsync(b->d_r, b->d_r + b->row(b->we - carry) * size_t(n),
+                                            sizeof(float) * size_t(carry) * size_t(n), hipMemcpyDeviceToDevice, b->s);
+        if (e != hipSuccess) {
+            crlot_ola* o = b->ola;  // (its frames are still in place)
+            b->ola = nullptr;
+            const int rc = ola_materialize_locked(o);
+            return rc != CRLOT_OK ? rc : decline(b);
+        }
+    }
+    b->cb = b->we - carry;
+    b->wb = b->we;
+    b->we = b->wb + F;
+    b->next_fwd = b->wb;
+    b->pushed = -1;
+    if (size_t(carry) + size_t(F) > b->rows_cap || run_chain(b, inner, carry) != CRLOT_OK) {
+        if (b->ola) {  // the frames it still needs are the carried rows [0, carry)
+            crlot_ola* o = b->ola;
+            b->ola = nullptr;
+            const int rc = ola_materialize_locked(o);
+            if (rc != CRLOT_OK) return rc;
+        }
+        return decline(b);
+    }
+    sh->fft.valid = false;
+    sh->chain.valid = false;
+    b->active = true;
+    spec_count(kStatWindows);
+    spec_count(kStatForward);
+    std::memcpy(out, b->h_spec + b->row(b->wb) * (size_t(n) + 2), sizeof(float) * (size_t(n) + 2));
+    b->next_fwd = b->wb + 1;
+    b->inv_ready = b->wb;
+    if (b->next_fwd == b->we) b->active = false;
+    return 1;
+}
 
 }  // namespace
 
@@ -299,13 +501,13 @@ int batch_serve_forward(SharedServer* sh, int64_t n, const float* in, float* out
     BatchSpec* b = sh->batch;
     if (!b || spec_mode() < 2 || !b->active || b->n != n) return 0;
     const int64_t j = b->next_fwd;
-    if (j >= b->M || !input_matches(*b, j, in)) return 0;
+    if (j >= b->we || !input_matches(*b, j, in)) return 0;
     const size_t row = size_t(n) + 2;
-    std::memcpy(out, b->h_spec + size_t(j) * row, sizeof(float) * row);
+    std::memcpy(out, b->h_spec + b->row(j) * row, sizeof(float) * row);
     b->next_fwd = j + 1;
     b->inv_ready = j;
     spec_count(kStatForward);
-    if (b->next_fwd == b->M) b->active = false;  // last frame: its inverse / push / produce still served
+    if (b->next_fwd == b->we) b->active = false;  // window end: its inverse / push / produce still served
     return 1;
 }
 
@@ -315,58 +517,50 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     BatchSpec* b = sh->batch;
     const size_t row = size_t(n) + 2;
     if (batch_serve_forward(sh, n, in, out)) return 1;
+    CRLOT_LAP_START();
+    if (!inner) return 0;
+    // the next window of the running batch
+    if (b->gen != 0 && b->n == n && b->next_fwd == b->we && b->we < b->M) {
+        const int rc = continue_window(sh, b, inner, n, in, out);
+        if (rc != 0) return rc;
+    }
     // a forward the batch did not predict: end it, then try to start one here
     if (b->active || b->ola) {
         const int rc = batch_abort(sh);
         if (rc != CRLOT_OK) return rc;
     }
     b->inv_ready = b->pushed = -1;
-    CRLOT_LAP_START();
-    if (!inner) return 0;
-    // source 1: the Framer popped last, frame * a library window
+    b->M = b->we = b->next_fwd = 0;
+    // source 1: the Framer popped last, frame * a library window (the window
+    // search on frame 0 before anything is copied)
     std::vector<float> sig;
-    int64_t hop = 0, M = 0;
+    int64_t hop = 0, F = 0, total = 0, first = 0;
+    uint64_t src = 0;
     const std::vector<float>* found = nullptr;
-    std::vector<std::vector<float>> wins;
-    if (framer_last_signal(n, &sig, &hop, &M) && M >= 4) {
-        wins = windows_of_size(n);
-        for (const auto& w : wins) {
-            bool ok = true;
-            for (int64_t i = 0; i < n && ok; ++i) {
-                const float v = (i < int64_t(sig.size()) ? sig[size_t(i)] : 0.0f) * w[size_t(i)];
-                ok = std::memcmp(&v, in + i, sizeof(float)) == 0;
-            }
-            if (ok) {
-                found = &w;
-                break;
-            }
-        }
+    std::vector<std::vector<float>> wins = windows_of_size(n);
+    {
+        auto accept = [&](const float* f0, int64_t) { return (found = window_match(f0, in, n, wins)) != nullptr; };
+        if (!framer_last_signal(n, kBatchWindow, accept, &sig, &hop, &F, &total, &src) || total < 4) found = nullptr;
     }
     // source 2: the FrameQueue read last, its frame as it is (no window),
     // copied straight into the pinned staging block the upload reads
     if (!found) {
         int qdev = -1, cur = -1;
         hipError_t he = hipSuccess;
-        auto dst = [&](size_t floats) -> float* {
-            const size_t had = b->c_hs;
-            he = hgrow(&b->h_stage, &b->c_hs, floats);
-            if (he != hipSuccess) return nullptr;
-            if (b->c_hs != had || !b->m_stage) {
-                void* m = nullptr;
-                b->m_stage = hipHostGetDevicePointer(&m, b->h_stage, 0) == hipSuccess ? static_cast<float*>(m) : nullptr;
-            }
-            return b->h_stage;
-        };
-        const bool got = framequeue_last_rows(n, &hop, &M, &qdev, dst);
-        if (he != hipSuccess) return hip_fail(he, "batch buffers");
-        if (!got || M < 4 || hipGetDevice(&cur) != hipSuccess || cur != qdev ||
-            std::memcmp(b->h_stage, in, sizeof(float) * size_t(n)) != 0)
-            return 0;
+        auto accept = [&](const float* r0) { return std::memcmp(r0, in, sizeof(float) * size_t(n)) == 0; };
+        auto dst = [&](size_t floats) { return stage_rows(b, floats, &he); };
+        const bool got = framequeue_last_rows(n, kBatchWindow, accept, &hop, &F, &total, &qdev, &src, &first, dst);
+        if (he != hipSuccess) return decline(b);
+        if (!got || total < 4 || hipGetDevice(&cur) != hipSuccess || cur != qdev) return 0;
     }
     b->gen += 1;
     b->n = n;
     b->h = hop;
-    b->M = M;
+    b->M = total;
+    b->cb = b->wb = 0;
+    b->we = F;
+    b->source = src;
+    b->src_first = first;
     b->rows_src = found == nullptr;
     if (found) {
         b->sig.swap(sig);
@@ -379,11 +573,10 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     b->y_ready = b->y_waited = false;
     b->ola = nullptr;
     CRLOT_LAP(0);
-    const int rc = run_chain(b, inner);
-    if (rc != CRLOT_OK) {
-        b->active = false;
-        return rc;
-    }
+    // buffers for one window, plus the frames a continuing object carries over
+    // when the batch has more than one
+    const size_t rows = size_t(F) + (total > F ? size_t(kBatchWarm) : 0);
+    if (ensure_rows(b, rows) != hipSuccess || run_chain(b, inner, 0) != CRLOT_OK) return decline(b);
     sh->fft.valid = false;  // the call server's own per-call speculation is not used meanwhile
     sh->chain.valid = false;
     b->active = true;
@@ -392,6 +585,7 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     std::memcpy(out, b->h_spec, sizeof(float) * row);
     b->next_fwd = 1;
     b->inv_ready = 0;
+    if (b->next_fwd == b->we) b->active = false;
     return 1;
 }
 
@@ -400,8 +594,8 @@ int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out) {
     if (!b || spec_mode() < 2 || b->n != n || b->inv_ready < 0) return 0;
     const int64_t j = b->inv_ready;
     const size_t row = size_t(n) + 2;
-    if (std::memcmp(in, b->h_spec + size_t(j) * row, sizeof(float) * row) != 0) return 0;
-    std::memcpy(out, b->h_r + size_t(j) * size_t(n), sizeof(float) * size_t(n));
+    if (std::memcmp(in, b->h_spec + b->row(j) * row, sizeof(float) * row) != 0) return 0;
+    std::memcpy(out, b->h_r + b->row(j) * size_t(n), sizeof(float) * size_t(n));
     b->inv_ready = -1;
     b->pushed = j;
     spec_count(kStatInverse);
@@ -411,20 +605,24 @@ int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out) {
 int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const float* d_ws, const float* d_den,
                  float gain, hipStream_t tables_stream, uint64_t tgen) {
     BatchSpec* b = sh->batch;
+    b->ola_ws = d_ws;
+    b->ola_den = d_den;
+    b->ola_R = R;
     if (b->spec_y && b->spec_ola.o == o && b->spec_ola.tgen == tgen && b->spec_ola.R == R && j0 == 0 &&
         std::memcmp(&gain, &kOne, sizeof(float)) == 0) {  // computed with the chain (run_chain)
         b->ola = o;
         b->j0 = 0;
         b->gain = gain;
         b->y_ready = b->y_waited = true;
+        b->y_base = b->y_lo = 0;
         b->spec_used = true;
-        b->ya = b->h_y + (size_t(b->M) * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h)));
+        b->ya = b->h_y + y_floats(b, size_t(b->we));
         return CRLOT_OK;
     }
     b->spec_used = false;
-    // blocks of frames j0 .. M-1 and the tail only they reach (no later frame
-    // exists in the batch; a produce there needs the last frame pushed)
-    const size_t F = size_t(b->M - j0), len = F * size_t(b->h) + size_t(std::max<int64_t>(0, b->n - b->h));
+    // blocks of the window's frames j0 .. we-1 and the tail only they reach (no
+    // later frame is in the window; a produce there needs the last frame pushed)
+    const size_t F = size_t(b->we - j0), len = y_floats(b, F);
     hipError_t e;
     if ((e = hipStreamSynchronize(tables_stream)) != hipSuccess) return hip_fail(e, "OLA tables");
     Geometry g;
@@ -435,7 +633,7 @@ int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const fl
     DevTables t;
     t.ws = d_ws;
     t.den = d_den;
-    if ((e = launch_ola_gather(g, t, b->d_r + size_t(j0) * size_t(b->n), b->n, b->d_y, 1, int64_t(F),
+    if ((e = launch_ola_gather(g, t, b->d_r + b->row(j0) * size_t(b->n), b->n, b->d_y, 1, int64_t(F),
                                int64_t(len), int64_t(len), b->s)) ||
         (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * len, hipMemcpyDeviceToHost, b->s)) ||
         (e = hipEventRecord(b->ev, b->s)))
@@ -445,6 +643,7 @@ int batch_attach(SharedServer* sh, crlot_ola* o, int64_t j0, int64_t R, const fl
     b->gain = gain;
     b->y_ready = true;
     b->y_waited = false;
+    b->y_base = b->y_lo = 0;
     return CRLOT_OK;
 }
 
@@ -458,6 +657,7 @@ int batch_wait_y(BatchSpec* b) {
 
 int batch_alias(BatchSpec* b, int64_t R, const float* d_ws, const float* d_den) {
     if (b->spec_used) return CRLOT_OK;  // computed with the chain (b->ya)
+    if (!b->single()) return set_error(CRLOT_ERUNTIME, "wrapped ring of a windowed batch");
     const int64_t F = b->M - b->j0, len = F * b->h + std::max<int64_t>(0, b->n - b->h);
     hipError_t e;
     if ((e = dgrow(&b->d_acc, &b->c_acc, size_t(R))) || (e = dgrow(&b->d_ya, &b->c_ya, size_t(R))) ||
@@ -471,7 +671,7 @@ int batch_alias(BatchSpec* b, int64_t R, const float* d_ws, const float* d_den) 
     DevTables t;
     t.ws = d_ws;
     t.den = d_den;
-    if ((e = launch_ola_gather_wrap(g, t, b->d_r + size_t(b->j0) * size_t(b->n), b->n, F, len, b->d_acc, b->d_ya,
+    if ((e = launch_ola_gather_wrap(g, t, b->d_r + b->row(b->j0) * size_t(b->n), b->n, F, len, b->d_acc, b->d_ya,
                                     b->s)) ||
         (e = hipMemcpyAsync(b->h_ya, b->d_ya, sizeof(float) * size_t(R), hipMemcpyDeviceToHost, b->s)) ||
         (e = hipEventRecord(b->ev, b->s)) || (e = hipEventSynchronize(b->ev)))
@@ -485,6 +685,28 @@ int batch_alias(BatchSpec* b, int64_t R, const float* d_ws, const float* d_den) 
 extern "C" int crlot_call_speculation_stats(int64_t* out6) {
     if (!out6) return crlot::set_error(CRLOT_EINVAL, "null argument");
     for (int i = 0; i < 6; ++i) out6[i] = crlot::g_stats[i].load(std::memory_order_relaxed);
+    return CRLOT_OK;
+}
+
+extern "C" int crlot_call_speculation_stats_ex(int64_t* out, int32_t count) {
+    if (!out || count < 0) return crlot::set_error(CRLOT_EINVAL, "null argument");
+    for (int i = 0; i < count; ++i)
+        out[i] = i < crlot::kStatCount ? crlot::g_stats[i].load(std::memory_order_relaxed) : 0;
+    return CRLOT_OK;
+}
+
+extern "C" int crlot_call_batch_capacity(int64_t* window_frames, int64_t* device_bytes, int64_t* pinned_bytes,
+                                         int64_t* pinned_peak) {
+    if (window_frames) *window_frames = crlot::kBatchWindow;
+    if (device_bytes) *device_bytes = crlot::g_dev_bytes.load();
+    if (pinned_bytes) *pinned_bytes = crlot::g_pin_bytes.load();
+    if (pinned_peak) *pinned_peak = crlot::g_pin_peak.load();
+    return CRLOT_OK;
+}
+
+extern "C" int crlot_test_inject(int32_t what, int32_t count) {
+    if (what != CRLOT_INJECT_BATCH_ALLOC || count < 0) return crlot::set_error(CRLOT_EINVAL, "unknown injection");
+    crlot::g_fail_alloc.store(count, std::memory_order_relaxed);
     return CRLOT_OK;
 }
 

@@ -34,17 +34,32 @@ namespace crlot {
 
 struct SharedServer;
 
-// The remaining frames of the most recently popped mono Framer, as a signal:
-// frame j (j = 0: the frame just popped) = sig[j H : j H + N], zeros past the
-// end, j < *frames.  Returns false when there is none (objects.cpp).
-bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_t* frames);
+// Batches are bounded: at most kBatchWindow frames are transformed per chain, in
+// windows.  When the callers reach a window's end the next forward starts the
+// next window from the same source (its frames continue the logical signal),
+// carrying the last frames' inverse outputs over on the device so that an
+// attached OLA object's overlap-add continues across the seam; device and pinned
+// buffers therefore hold at most kBatchWindow + kBatchWarm frames.
+constexpr int64_t kBatchWindow = 512;
+constexpr int64_t kBatchWarm = 63;  // warm-up frames kept: ceil(N / H) - 1 for H >= N / 64
+
+// The most recently popped mono Framer: accept(frame 0, hop) decides on the frame
+// popped last (nothing is copied before), then the signal of its first
+// max_frames frames is copied: frame j (j = 0: the frame just popped) =
+// sig[j H : j H + N], zeros past the end.  *frames = frames covered, *total =
+// frames the Framer still holds (from the popped one on), *source identifies the
+// Framer.  False when there is none or accept refuses (objects.cpp).
+bool framer_last_signal(int64_t n, int64_t max_frames, const std::function<bool(const float*, int64_t)>& accept,
+                        std::vector<float>* sig, int64_t* hop, int64_t* frames, int64_t* total, uint64_t* source);
 // The second source: the frames of the FrameQueue read last (getFrame /
-// copyFrame), from the frame just read on, copied [frames][n] into the buffer
-// dst(floats) returns (bench/performance_benchmark.cc:174-246 feeds each
-// FrameQueue frame, unwindowed, to the forward).  False when there is none, or
-// dst returns null (objects.cpp).
-bool framequeue_last_rows(int64_t n, int64_t* hop, int64_t* frames, int* device,
-                          const std::function<float*(size_t)>& dst);
+// copyFrame), from the frame just read on (bench/performance_benchmark.cc:174-246
+// feeds each FrameQueue frame, unwindowed, to the forward): accept(row 0) first,
+// then at most max_frames rows copied [frames][n] into the buffer dst(floats)
+// returns.  *first = the row's index in its queue.  False when there is none,
+// accept refuses or dst returns null (objects.cpp).
+bool framequeue_last_rows(int64_t n, int64_t max_frames, const std::function<bool(const float*)>& accept,
+                          int64_t* hop, int64_t* frames, int64_t* total, int* device, uint64_t* source,
+                          int64_t* first, const std::function<float*(size_t)>& dst);
 // The OLA object whose window was set last, when it is a mono, untouched,
 // apply_window_inside object of frame n, hop h on `device` (the harness builds it
 // before the loop, performance_benchmark.cc:195-197): its device window and
@@ -67,27 +82,36 @@ std::vector<std::vector<float>> windows_of_size(int64_t n);
 // 1: the per-call speculation of the call server only; 2 (default): batched
 // speculation of the whole loop too (crlot_set_call_speculation)
 int spec_mode();
-enum { kStatStart = 0, kStatForward, kStatInverse, kStatPush, kStatProduce, kStatRebuild };
+enum { kStatStart = 0, kStatForward, kStatInverse, kStatPush, kStatProduce, kStatRebuild, kStatFrames, kStatWindows,
+       kStatDeclined, kStatCount };
 void spec_count(int what);
 
 struct BatchSpec {
-    bool active = false;     // frames are being served
-    uint64_t gen = 0;        // bumped by every start
-    int64_t n = 0, h = 0, M = 0;
-    std::vector<float> sig;  // host copy of the remaining signal (verifies forward inputs)
+    bool active = false;     // frames of the current window are being served
+    uint64_t gen = 0;        // bumped by every start (not by a window continuation)
+    int64_t n = 0, h = 0;
+    int64_t M = 0;           // frames of the whole batch (the source's frames at the start)
+    // the window: frames [wb, we) are served; the buffers hold frames [cb, we)
+    // (cb < wb: inverse outputs carried over from the previous window, for the
+    // attached object's overlap-add); buffer row of frame j = j - cb
+    int64_t cb = 0, wb = 0, we = 0;
+    uint64_t source = 0;     // the Framer / FrameQueue the frames come from
+    int64_t src_first = 0;   // FrameQueue: queue index of frame 0 of the batch
+    std::vector<float> sig;  // host copy of the window's signal from frame wb on (verifies forward inputs)
     std::vector<float> win;  // the analysis window found
     bool rows_src = false;   // the FrameQueue source: forward inputs are the rows themselves
     int64_t next_fwd = 0;    // frame whose forward comes next
     int64_t inv_ready = -1;  // frame whose forward was served and whose inverse may be asked
     int64_t pushed = -1;     // last frame whose inverse was served (push candidate)
-    // device / pinned buffers (grow-only).  The chain's results share one block
-    // each side (one copy back): spectra [M][N + 2] (interleaved complex),
-    // inverse frames [M][N] (= push inputs), produce blocks [M H + N - H] (after
-    // attach), and the fresh object's wrapped produce [R] (spec_ola)
+    // device / pinned buffers (grow-only, at most kBatchWindow + kBatchWarm
+    // frames).  The chain's results share one block each side (one copy back):
+    // spectra [rows][N + 2] (interleaved complex), inverse frames [rows][N] (=
+    // push inputs), produce blocks [rows H + N - H] (after attach), and the fresh
+    // object's wrapped produce [R] (spec_ola)
     hipStream_t s = nullptr;
     hipEvent_t ev = nullptr;
     float* d_sig = nullptr;
-    float* d_p = nullptr;    // [M][N] analysis products
+    float* d_p = nullptr;    // [rows][N] analysis products
     float* d_blk = nullptr;
     float* h_blk = nullptr;
     float* m_blk = nullptr;    // h_blk / h_stage as the device addresses them (mapped pinned memory)
@@ -102,20 +126,34 @@ struct BatchSpec {
     float* d_ya = nullptr;   // [R] their produce (batch_alias without spec_ola)
     float* h_ya = nullptr;
     const float* ya = nullptr;  // the wrapped produce in use (h_ya or in h_blk)
-    float* h_stage = nullptr;  // the FrameQueue source: its rows [M][n] (verifies forward inputs)
-    size_t c_sig = 0, c_p = 0, c_blk = 0, c_hblk = 0, c_hs = 0, c_acc = 0, c_ya = 0, c_hya = 0;  // capacities
+    float* h_stage = nullptr;  // the FrameQueue source: its rows of the window (verifies forward inputs)
+    float* d_den_rot = nullptr;  // [R] the attached object's divisors from the window's origin on
+    size_t c_sig = 0, c_p = 0, c_blk = 0, c_hblk = 0, c_hs = 0, c_acc = 0, c_ya = 0, c_hya = 0, c_den_rot = 0;
+    size_t rows_cap = 0;     // frames the result block was laid out for
     // the OLA object the batch's inverses are pushed to (objects.cpp)
     crlot_ola* ola = nullptr;
     int64_t j0 = 0;          // first frame pushed to it
     float gain = 1.0f;
-    bool y_ready = false;    // h_y holds blocks j0 .. M-1 (event ev)
+    const float* ola_ws = nullptr;  // its device window and divisors, ring length (batch_attach)
+    const float* ola_den = nullptr;
+    int64_t ola_R = 0;
+    bool y_ready = false;    // h_y holds the object's produce blocks (event ev)
     bool y_waited = false;
+    int64_t y_base = 0;      // position (from j0 H) of h_y[0]
+    int64_t y_lo = 0;        // first position h_y holds completely (the window's carried frames reach it)
     // the overlap-add computed with the chain for a fresh OLA object (fresh_ola),
     // gain 1 and j0 = 0: h_y and the wrapped d_acc / h_ya, used if it attaches so
     FreshOla spec_ola;
     bool spec_y = false;     // computed with this batch
     bool spec_used = false;  // the attached object is the one it was computed for
+    bool single() const { return cb == 0 && we == M; }  // one window holds every frame
+    size_t row(int64_t j) const { return size_t(j - cb); }
 };
+
+// objects.cpp: the attached object's state allows its overlap-add to continue
+// into the next window (every frame before `we` pushed and read up to `we`'s
+// position, no wrap); *first = the first frame whose unread contributions remain
+bool ola_can_continue(const crlot_ola* o, const BatchSpec* b);
 
 // abi.cpp fft_host, under sh->mu: a contiguous batch-1 real forward / inverse.
 // 1: served into `out`; 0: not (take the ordinary path); < 0: error.

@@ -24,6 +24,8 @@
 // transform instead of two, and no exchange for the real split.
 #pragma once
 
+#include <type_traits>
+
 #include "fft_wave.h"
 
 namespace crlot {
@@ -290,6 +292,49 @@ __device__ __forceinline__ pc pk_fma_mi(pc a, pc k, pc b) { return pk_fmasw<SEL,
 template <bool POS>
 __device__ __forceinline__ pc pk_yform1(pc x) { return POS ? pk_add_sw_nl(x, x) : pk_add_sw_nh(x, x); }
 
+// The same two forms with a per-lane constant pair K in VGPRs.
+template <int SEL, bool NEG>
+__device__ __forceinline__ pc pk_fmak_v(pc a, pc k, pc b) {
+    pc r;
+    if constexpr (SEL == 0 && !NEG)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    else if constexpr (SEL == 0 && NEG)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    else if constexpr (SEL == 1 && !NEG)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[0,1,0] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    return r;
+}
+template <int SEL, bool NL, bool NH>
+__device__ __forceinline__ pc pk_fmasw_v(pc a, pc k, pc b) {
+    static_assert(NL != NH, "one half negated");
+    pc r;
+    if constexpr (SEL == 0 && NL)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    else if constexpr (SEL == 0 && NH)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    else if constexpr (SEL == 1 && NL)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]" : "=v"(r) : "v"(a), "v"(k), "v"(b));
+    return r;
+}
+// a * K.y (both halves)
+__device__ __forceinline__ pc pk_mul_hi_v(pc a, pc k) {
+    pc r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(k));
+    return r;
+}
+// twiddle w = C (1 + i T) held as K = (T, C): y = x + T (i x) (CONJ: x - T (i x))
+template <bool CONJ>
+__device__ __forceinline__ pc pk_yform_v(pc x, pc tc) { return pk_fmasw_v<0, !CONJ, CONJ>(x, tc, x); }
+// x * w (CONJ: x * conj w) with w held as (T, C): two operations, as pc_mul
+template <bool CONJ>
+__device__ __forceinline__ pc pk_tw_tc(pc x, pc tc) { return pk_mul_hi_v(pk_yform_v<CONJ>(x, tc), tc); }
+// (T, C) of a unit twiddle given as (cos, sin); C != 0 for every table entry it is used on
+__device__ __forceinline__ pc tw_tc(pc w) { return (pc){w.y / w.x, w.x}; }
+
 // 16-point DFT constants: cos(pi/8), sin(pi/8); tan(pi/8), tan(3 pi/8); sqrt(1/2)
 __device__ __forceinline__ pc k16_cs() { return (pc){0.92387953251128675613f, 0.38268343236508977173f}; }
 __device__ __forceinline__ pc k16_tt() { return (pc){0.41421356237309504880f, 2.41421356237309504880f}; }
@@ -303,10 +348,10 @@ __device__ __forceinline__ pc k16_h() { return (pc){0.70710678118654752440f, 0.7
 //   k1 = 2: W^2 (x9 + m x11), W^4 = m (free), as h (1 -+ i)
 //   k1 = 3: W^3, W^6 = -h (1 +- i), W^9 = -C1 (1 -+ i t8)
 // (upper signs forward; C1 = cos pi/8, S1 = sin pi/8, t8 = tan pi/8, t38 = tan 3pi/8)
+// the second layer of pdft16_fma (inputs a[n2][k1] at x[n2 + 4 k1]) and the
+// output renaming
 template <bool INV>
-__device__ __forceinline__ void pdft16_fma(pc (&x)[16]) {
-#pragma unroll
-    for (int n2 = 0; n2 < 4; ++n2) pdft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
+__device__ __forceinline__ void pdft16_fma_l2(pc (&x)[16]) {
     const pc kcs = k16_cs(), ktt = k16_tt(), kh = k16_h();
     // the twiddled inputs' forms: k1 = 1 (x5, x6, x7), k1 = 3 (x13, x14, x15), k1 = 2 (x9 +- m x11)
     const pc y5 = pk_yform<0, INV>(x[5], ktt);   // T = -+ t8
@@ -345,6 +390,12 @@ __device__ __forceinline__ void pdft16_fma(pc (&x)[16]) {
         for (int k2 = 0; k2 < 4; ++k2) y[k1 + 4 * k2] = x[4 * k1 + k2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = y[i];
+}
+template <bool INV>
+__device__ __forceinline__ void pdft16_fma(pc (&x)[16]) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) pdft4<INV>(x[n2], x[n2 + 4], x[n2 + 8], x[n2 + 12]);
+    pdft16_fma_l2<INV>(x);
 }
 
 // The same DFT with explicit rotations (80 packed operations); kept for A/B
@@ -527,9 +578,130 @@ __device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const PairTw& tw, int
 __device__ __forceinline__ pc pair_t2(const pc* t2, int c) { return t2[16 * (c - 1)]; }
 __device__ __forceinline__ pc pair_t2(const PairTw& tw, int c) { return tw.w2[c - 1]; }
 
+// The same twiddles in the FMA-fused form (the release layout at H = 256).  The
+// inverse runs decimation in time, so its twiddles sit on the INPUTS of the next
+// radix-4 butterflies and fuse into them (Goedecker): per butterfly the input of
+// index 2 keeps an explicit rotation (its C can be 0: W64^16 = -i at lane 8),
+// inputs 1 and 3 become y = x - T (i x) with C1 pending and the ratio C3 / C1
+// folded into the add -- 12 packed operations per radix-4 instead of 14.  The
+// forward (decimation in frequency) applies the same twiddles explicitly, two
+// operations each, as before.
+// 15 per-lane twiddles w_k = W^{k}, k = 1..15 (geometric in k), FMA form:
+// k in {1, 2, 3, 8, 9, 10, 11} as (cos, sin) in e[], k in {4..7, 12..15} as
+// (T, C) in y[], r = C_{n+12} / C_{n+4} (n = 0..3); 34 VGPRs instead of 30.
+struct Tw15F {
+    pc e[7];
+    pc y[8];
+    pc r[2];
+};
+__host__ __device__ constexpr int tw15_e_slot(int k) { return k < 8 ? k - 1 : k - 5; }   // k in {1,2,3,8..11}
+__host__ __device__ constexpr int tw15_y_slot(int k) { return k < 8 ? k - 4 : k - 8; }   // k in {4..7, 12..15}
+__host__ __device__ constexpr bool tw15_is_e(int k) { return (k & 4) == 0; }
+// w(k): (cos, sin) of w_k
+template <typename WF>
+__device__ __forceinline__ void tw15_load(Tw15F& tw, WF w) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+        if (tw15_is_e(k))
+            tw.e[tw15_e_slot(k)] = w(k);
+        else
+            tw.y[tw15_y_slot(k)] = tw_tc(w(k));
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) tw.r[n >> 1][n & 1] = tw.y[tw15_y_slot(n + 12)].y / tw.y[tw15_y_slot(n + 4)].y;
+}
+// forward (explicit, two operations each): v[k] *= w_k
+__device__ __forceinline__ void tw15_apply_fwd(pc (&v)[16], const Tw15F& tw) {
+#pragma unroll
+    for (int k = 1; k < 16; ++k)
+        v[k] = tw15_is_e(k) ? pc_mul(v[k], tw.e[tw15_e_slot(k)]) : pk_tw_tc<false>(v[k], tw.y[tw15_y_slot(k)]);
+}
+// inverse: conj(w_k) on register k fused with pdft16<true>'s first layer (one
+// radix-4 over registers n, n+4, n+8, n+12 per n: inputs n and n+8 rotated
+// explicitly, n+4 and n+12 in the y = x - T (i x) form, C_{n+4} pending), then
+// pdft16<true>'s second layer.  54 + 40 packed operations instead of 30 + 72.
+__device__ __forceinline__ void tw15_pdft16_inv(pc (&v)[16], const Tw15F& tw) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        const pc u0 = n ? pc_mulc(v[n], tw.e[tw15_e_slot(n)]) : v[0];
+        const pc u2 = pc_mulc(v[n + 8], tw.e[tw15_e_slot(n + 8)]);
+        const pc tc = tw.y[tw15_y_slot(n + 4)];
+        const pc y1 = pk_yform_v<true>(v[n + 4], tc);
+        const pc y3 = pk_yform_v<true>(v[n + 12], tw.y[tw15_y_slot(n + 12)]);
+        const pc s0 = u0 + u2, s1 = u0 - u2;
+        pc s2, d3;
+        if (n & 1) {
+            s2 = pk_fmak_v<1, false>(y3, tw.r[n >> 1], y1);
+            d3 = pk_fmak_v<1, true>(y3, tw.r[n >> 1], y1);
+        } else {
+            s2 = pk_fmak_v<0, false>(y3, tw.r[n >> 1], y1);
+            d3 = pk_fmak_v<0, true>(y3, tw.r[n >> 1], y1);
+        }
+        v[n] = pk_fmak_v<1, false>(s2, tc, s0);
+        v[n + 8] = pk_fmak_v<1, true>(s2, tc, s0);
+        v[n + 4] = pk_fmasw_v<1, true, false>(d3, tc, s1);   // s1 + C (i d3)
+        v[n + 12] = pk_fmasw_v<1, false, true>(d3, tc, s1);  // s1 - C (i d3)
+    }
+    pdft16_fma_l2<true>(v);
+}
+
+// K_pair's register twiddles in the FMA form: t1 = W1024^{l k} as a Tw15F; t2 =
+// W64^{x c} (x = lane & 15): c = 2 as (cos, sin), c = 1, 3 as (T, C), rb.x = C3 / C1.
+// Every C used as a divisor or pending factor is nonzero: cos(2 pi l k / 1024)
+// for l < 64 and k in {4..7, 12..15} never meets a quarter turn (nor do the
+// W4096 / W2048 / W256 / W128 tables of K_pair4k / K_pair2k), nor does
+// cos(2 pi x c / 64) for x < 16 and c in {1, 3}; |T| <= 163 here (<= 652 at 4096).
+struct PairTwF {
+    Tw15F t1;
+    pc w2, tc1, tc3, rb;
+};
+__device__ __forceinline__ void pair_tw_load(PairTwF& tw, const pc* t1, const pc* t2, int lane) {
+    tw15_load(tw.t1, [&](int k) { return t1[pair_t1_index(k, lane)]; });
+    const pc w1 = t2[0], w3 = t2[32];
+    tw.w2 = t2[16];
+    tw.tc1 = tw_tc(w1);
+    tw.tc3 = tw_tc(w3);
+    tw.rb = (pc){w3.x / w1.x, 0.f};
+}
+template <bool INV>
+__device__ __forceinline__ void pair_t1_apply(pc (&v)[16], const PairTwF& tw, int) {
+    static_assert(!INV, "the inverse fuses its t1 twiddles (tw15_pdft16_inv)");
+    tw15_apply_fwd(v, tw.t1);
+}
+// forward t2: v[j + 4 c] *= W64^{x c}
+__device__ __forceinline__ void pair_t2_fwd(pc (&v)[16], const PairTwF& tw) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        v[4 + j] = pk_tw_tc<false>(v[4 + j], tw.tc1);
+        v[8 + j] = pc_mul(v[8 + j], tw.w2);
+        v[12 + j] = pk_tw_tc<false>(v[12 + j], tw.tc3);
+    }
+}
+// inverse: conj W64^{x c} on v[j + 4 c] fused into the radix-4 over c
+__device__ __forceinline__ void pair_t2_dft4_inv(pc (&v)[16], const PairTwF& tw) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const pc u2 = pc_mulc(v[j + 8], tw.w2);
+        const pc y1 = pk_yform_v<true>(v[j + 4], tw.tc1);
+        const pc y3 = pk_yform_v<true>(v[j + 12], tw.tc3);
+        const pc s0 = v[j] + u2, s1 = v[j] - u2;
+        const pc s2 = pk_fmak_v<0, false>(y3, tw.rb, y1), d3 = pk_fmak_v<0, true>(y3, tw.rb, y1);
+        v[j] = pk_fmak_v<1, false>(s2, tw.tc1, s0);
+        v[j + 8] = pk_fmak_v<1, true>(s2, tw.tc1, s0);
+        v[j + 4] = pk_fmasw_v<1, true, false>(d3, tw.tc1, s1);
+        v[j + 12] = pk_fmasw_v<1, false, true>(d3, tw.tc1, s1);
+    }
+}
+
+#ifdef CRLOT_PAIR_TW_CLASSIC
+using PairTwReg = PairTw;
+#else
+using PairTwReg = PairTwF;
+#endif
+
 // Forward: natural z[lane + 64 m] -> bin-scrambled X (pair_bin).
 //   t1: W1024^{l k1} (pair_t1_index), t2[16 (c - 1)] = W64^{(lane & 15) c} (LDS),
-//   or both from a PairTw (T1 = PairTw, t2 unused).
+//   or both from a PairTw / PairTwF (T1 = the struct, t2 unused).
 template <typename T1, typename T2>
 __device__ __forceinline__ void pair_fft_fwd(pc (&v)[16], pc* buf, const T1& t1, const T2& t2, int lane) {
     pdft16<false>(v);
@@ -537,7 +709,9 @@ __device__ __forceinline__ void pair_fft_fwd(pc (&v)[16], pc* buf, const T1& t1,
     lane_reg_swap_any<CRLOT_PAIR_SWAP_LDS>(v, buf, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j) pdft4<false>(v[j], v[j + 4], v[j + 8], v[j + 12]);
-    {
+    if constexpr (std::is_same_v<T2, PairTwF>) {
+        pair_t2_fwd(v, t2);
+    } else {
         constexpr int idx[12] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
         pc_tw_run<false>(v, idx, [&](int i) { return pair_t2(t2, 1 + i / 4); });
     }
@@ -550,15 +724,23 @@ template <typename T1, typename T2>
 __device__ __forceinline__ void pair_fft_inv(pc (&v)[16], pc* buf, const T1& t1, const T2& t2, int lane) {
     pdft16<true>(v);
     transpose16(v, buf, lane);
-    {
-        constexpr int idx[12] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-        pc_tw_run<true>(v, idx, [&](int i) { return pair_t2(t2, 1 + i / 4); });
-    }
+    if constexpr (std::is_same_v<T2, PairTwF>) {
+        pair_t2_dft4_inv(v, t2);
+    } else {
+        {
+            constexpr int idx[12] = {4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+            pc_tw_run<true>(v, idx, [&](int i) { return pair_t2(t2, 1 + i / 4); });
+        }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) pdft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
+        for (int j = 0; j < 4; ++j) pdft4<true>(v[j], v[j + 4], v[j + 8], v[j + 12]);
+    }
     lane_reg_swap_any<CRLOT_PAIR_SWAP_LDS>(v, buf, lane);
-    pair_t1_apply<true>(v, t1, lane);
-    pdft16<true>(v);
+    if constexpr (std::is_same_v<T1, PairTwF>) {
+        tw15_pdft16_inv(v, t1.t1);
+    } else {
+        pair_t1_apply<true>(v, t1, lane);
+        pdft16<true>(v);
+    }
 }
 
 }  // namespace dev

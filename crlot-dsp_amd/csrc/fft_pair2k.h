@@ -97,10 +97,44 @@ __device__ __forceinline__ void pdft8_halves(pc (&v)[16]) {
     }
 }
 
-__device__ __forceinline__ void pair2k_fwd(pc (&v)[16], pc* xb, pc* tb, const Pair2kTw& tw, int t) {
-    pdft16<false>(v);
+// FMA form (fft_pair.h Tw15F) for the first-stage twiddles W2048^{t k1} only:
+// the inverse's last twiddle stage fuses into its last radix-16 (-8 packed
+// operations per inverse, +4 VGPRs; both stages would spill the hot walker).
+struct Pair2kTwF {
+    Tw15F w1;
+    pc w2[15];
+};
+__device__ __forceinline__ void pair2k_tw_load(Pair2kTwF& tw, const pc* g, int t) {
+    tw15_load(tw.w1, [&](int k) { return g[(k - 1) * 128 + t]; });
+#pragma unroll
+    for (int k = 1; k < 16; ++k) tw.w2[k - 1] = g[15 * 128 + (k - 1) * 8 + (t & 7)];
+}
+// The walkers' choice (SH = H / 128), as Pair4kTwFor: the FMA form at H = 512
+// without a gain only.
+#ifdef CRLOT_PAIR_TW_CLASSIC
+template <int SH, bool GAIN>
+using Pair2kTwFor = Pair2kTw;
+#else
+template <int SH, bool GAIN>
+using Pair2kTwFor = std::conditional_t<SH == 4, Pair2kTwF, Pair2kTw>;
+#endif
+__device__ __forceinline__ void pair2k_tw1_fwd(pc (&v)[16], const Pair2kTw& tw) {
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) v[k1] = pc_mul(v[k1], tw.w1[k1 - 1]);
+}
+__device__ __forceinline__ void pair2k_tw1_fwd(pc (&v)[16], const Pair2kTwF& tw) { tw15_apply_fwd(v, tw.w1); }
+// conj first-stage twiddles, then the inverse's last radix-16
+__device__ __forceinline__ void pair2k_tw1_pdft16_inv(pc (&v)[16], const Pair2kTw& tw) {
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) v[k1] = pc_mulc(v[k1], tw.w1[k1 - 1]);
+    pdft16<true>(v);
+}
+__device__ __forceinline__ void pair2k_tw1_pdft16_inv(pc (&v)[16], const Pair2kTwF& tw) { tw15_pdft16_inv(v, tw.w1); }
+
+template <typename TW>
+__device__ __forceinline__ void pair2k_fwd(pc (&v)[16], pc* xb, pc* tb, const TW& tw, int t) {
+    pdft16<false>(v);
+    pair2k_tw1_fwd(v, tw);
     pair2k_xchg_fwd(v, xb, t);
     pdft16<false>(v);
 #pragma unroll
@@ -109,16 +143,15 @@ __device__ __forceinline__ void pair2k_fwd(pc (&v)[16], pc* xb, pc* tb, const Pa
     pdft8_halves<false>(v);
 }
 
-__device__ __forceinline__ void pair2k_inv(pc (&v)[16], pc* xb, pc* tb, const Pair2kTw& tw, int t) {
+template <typename TW>
+__device__ __forceinline__ void pair2k_inv(pc (&v)[16], pc* xb, pc* tb, const TW& tw, int t) {
     pdft8_halves<true>(v);
     pair2k_t8(v, tb, t & 63);
 #pragma unroll
     for (int k2 = 1; k2 < 16; ++k2) v[k2] = pc_mulc(v[k2], tw.w2[k2 - 1]);
     pdft16<true>(v);
     pair2k_xchg_inv(v, xb, t);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) v[k1] = pc_mulc(v[k1], tw.w1[k1 - 1]);
-    pdft16<true>(v);
+    pair2k_tw1_pdft16_inv(v, tw);
 }
 
 }  // namespace dev

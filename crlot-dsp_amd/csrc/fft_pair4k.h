@@ -71,6 +71,31 @@ __device__ __forceinline__ void pair4k_tw_load(Pair4kTw& tw, const pc* g, int t)
     }
 }
 
+// The same twiddles in the FMA form (fft_pair.h Tw15F): the inverse's two
+// twiddle stages fuse into the first layer of the radix-16 that follows them
+// (-16 packed operations per inverse, +8 VGPRs).
+struct Pair4kTwF {
+    Tw15F w1, w2;
+};
+__device__ __forceinline__ void pair4k_tw_load(Pair4kTwF& tw, const pc* g, int t) {
+    tw15_load(tw.w1, [&](int k) { return g[(k - 1) * 256 + t]; });
+    tw15_load(tw.w2, [&](int k) { return g[15 * 256 + (k - 1) * 16 + (t & 15)]; });
+}
+// The walkers' choice, by hop (SH = H / 256) and gain, the same in the hot and
+// the two-regime walker so their paired bits agree: the FMA form at H = 1024
+// without a gain (config 3).  Elsewhere its registers spill the hot walk -- the
+// gain-carrying one by 54 VGPRs even with only the first stage fused (-7.6 % at
+// 4096/1024 with a gain, profiles/r05c_ab.log) -- so a plan with a gain rounds
+// its transforms the classic way: equal to the no-gain plan within the FFT
+// tolerance, not bit for bit, at N = 4096.
+#ifdef CRLOT_PAIR_TW_CLASSIC
+template <int SH, bool GAIN>
+using Pair4kTwFor = Pair4kTw;
+#else
+template <int SH, bool GAIN>
+using Pair4kTwFor = std::conditional_t<SH == 4 && !GAIN, Pair4kTwF, Pair4kTw>;
+#endif
+
 // Forward: natural z[t + 256 m] -> bin-scrambled X (pair4k_bin).
 __device__ __forceinline__ void pair4k_fwd(pc (&v)[16], pc* xb, pc* qb, const Pair4kTw& tw, int t) {
     pdft16<false>(v);
@@ -80,6 +105,15 @@ __device__ __forceinline__ void pair4k_fwd(pc (&v)[16], pc* xb, pc* qb, const Pa
     pdft16<false>(v);
 #pragma unroll
     for (int k2 = 1; k2 < 16; ++k2) v[k2] = pc_mul(v[k2], tw.w2[k2 - 1]);
+    transpose16(v, qb, t & 63);
+    pdft16<false>(v);
+}
+__device__ __forceinline__ void pair4k_fwd(pc (&v)[16], pc* xb, pc* qb, const Pair4kTwF& tw, int t) {
+    pdft16<false>(v);
+    tw15_apply_fwd(v, tw.w1);
+    pair4k_xchg_fwd(v, xb, t);
+    pdft16<false>(v);
+    tw15_apply_fwd(v, tw.w2);
     transpose16(v, qb, t & 63);
     pdft16<false>(v);
 }
@@ -95,6 +129,13 @@ __device__ __forceinline__ void pair4k_inv(pc (&v)[16], pc* xb, pc* qb, const Pa
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) v[k1] = pc_mulc(v[k1], tw.w1[k1 - 1]);
     pdft16<true>(v);
+}
+__device__ __forceinline__ void pair4k_inv(pc (&v)[16], pc* xb, pc* qb, const Pair4kTwF& tw, int t) {
+    pdft16<true>(v);
+    transpose16(v, qb, t & 63);
+    tw15_pdft16_inv(v, tw.w2);
+    pair4k_xchg_inv(v, xb, t);
+    tw15_pdft16_inv(v, tw.w1);
 }
 
 }  // namespace dev

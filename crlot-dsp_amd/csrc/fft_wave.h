@@ -620,7 +620,8 @@ __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, int voff, int 
 }
 __device__ __forceinline__ void bstore2(float2 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-    u2 w = {__builtin_bit_cast(unsigned, v.x), __builtin_bit_cast(unsigned, v.y)};
+    const float lo = v.x, hi = v.y;  // (scalars first: tools/bitcast_lint.py)
+    u2 w = {__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi)};
     __builtin_amdgcn_raw_buffer_store_b64(w, r, voff, soff, 0);
 }
 

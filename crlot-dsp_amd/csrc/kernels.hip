@@ -444,7 +444,7 @@ __global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const Fuse
     const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
-    dev::Pair512Tw tw;
+    dev::Pair512TwReg tw;
     dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
     float wa[E], ws[E];
 #pragma unroll
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
     const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
-    dev::Pair4kTw tw;
+    dev::Pair4kTwFor<SH, HAS_GAIN> tw;
     dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw4), t);
     float wa[E], ws[E];
 #pragma unroll
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
     const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
-    dev::Pair2kTw tw;
+    dev::Pair2kTwFor<SH, HAS_GAIN> tw;
     dev::pair2k_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw4), t);
     float wa[E], ws[E];
 #pragma unroll

@@ -85,17 +85,22 @@ struct crlot_framer {
 };
 
 namespace {
-// the Framer that popped last (batch.h framer_last_signal); cleared when it changes or dies
+// the Framer that popped last (batch.h framer_last_signal); cleared when it changes
+// or dies.  framer_last_signal reads that Framer's buffers from whatever thread runs
+// an FFT forward, so every Framer mutation (push, pop and its compaction,
+// set_params, reset, destroy) holds g_pop_mu too: a reader never sees a buffer
+// mid-reallocation.  The sections are short and uncontended unless
+// several threads push or pop at once.
 std::mutex g_pop_mu;
 const crlot_framer* g_last_pop = nullptr;
-void forget_framer(const crlot_framer* f) {
-    std::lock_guard<std::mutex> lk(g_pop_mu);
+void forget_framer_locked(const crlot_framer* f) {
     if (g_last_pop == f) g_last_pop = nullptr;
 }
 }  // namespace
 
 namespace crlot {
-bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_t* frames) {
+bool framer_last_signal(int64_t n, int64_t max_frames, const std::function<bool(const float*, int64_t)>& accept,
+                        std::vector<float>* sig, int64_t* hop, int64_t* frames, int64_t* total, uint64_t* source) {
     std::lock_guard<std::mutex> lk(g_pop_mu);
     const crlot_framer* f = g_last_pop;
     if (!f || f->c != 1 || f->n != n || int64_t(f->last.size()) != n) return false;
@@ -103,13 +108,22 @@ bool framer_last_signal(int64_t n, std::vector<float>* sig, int64_t* hop, int64_
     // unread buffer, which begins H samples into frame 0 (framer.cc:164-167)
     const int64_t h = f->h, rest = f->wr - f->rd;
     if (h > n) return false;
-    *hop = h;
     // frame j exists while j H < L (ZERO_PAD, padded) or j H + N <= L (DROP)
     const int64_t L = h + rest;
-    *frames = f->mode == CRLOT_ZERO_PAD ? (L + h - 1) / h : (L >= n ? (L - n) / h + 1 : 1);
-    sig->resize(size_t(L));
-    std::memcpy(sig->data(), f->last.data(), sizeof(float) * size_t(h));
-    if (rest > 0) std::memcpy(sig->data() + h, f->buf.data() + f->rd, sizeof(float) * size_t(rest));
+    const int64_t all = f->mode == CRLOT_ZERO_PAD ? (L + h - 1) / h : (L >= n ? (L - n) / h + 1 : 1);
+    // the cheap test first (frame 0 against the caller's input), then a copy of
+    // the first max_frames frames only: an unpredicted forward costs O(n), not
+    // O(remaining signal)
+    if (!accept(f->last.data(), h)) return false;
+    const int64_t F = std::min(all, std::max<int64_t>(1, max_frames));
+    const int64_t len = std::min(L, (F - 1) * h + n);
+    *hop = h;
+    *frames = F;
+    *total = all;
+    *source = reinterpret_cast<uintptr_t>(f);
+    sig->resize(size_t(len));
+    std::memcpy(sig->data(), f->last.data(), sizeof(float) * size_t(std::min(h, len)));
+    if (len > h) std::memcpy(sig->data() + h, f->buf.data() + f->rd, sizeof(float) * size_t(len - h));
     return true;
 }
 }  // namespace crlot
@@ -123,7 +137,10 @@ int crlot_framer_create(crlot_framer** out) {
 }
 
 void crlot_framer_destroy(crlot_framer* f) {
-    forget_framer(f);
+    {
+        std::lock_guard<std::mutex> lk(g_pop_mu);
+        forget_framer_locked(f);
+    }
     delete f;
 }
 
@@ -135,13 +152,14 @@ int crlot_framer_set_params(crlot_framer* f, int64_t frame_size, int64_t hop_siz
     if (channels <= 0) return fail(CRLOT_EINVAL, "Channels must be greater than 0");
     if (boundary_mode != CRLOT_ZERO_PAD && boundary_mode != CRLOT_DROP)
         return fail(CRLOT_EINVAL, "Unknown boundary mode");
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    forget_framer_locked(f);
     f->n = frame_size;
     f->h = hop_size;
     f->c = channels;
     f->mode = boundary_mode;
     f->ready = true;
     f->clear();
-    forget_framer(f);
     return CRLOT_OK;
 }
 
@@ -151,18 +169,21 @@ int crlot_framer_push(crlot_framer* f, const float* interleaved, int64_t frames)
     if (!interleaved && frames > 0) return 0;
     const int64_t add = frames * f->c;
     if (add == 0) return 1;
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    forget_framer_locked(f);  // the frames after the last pop change
     const int64_t need = f->wr + add;
     if (int64_t(f->buf.size()) < need)  // doubling growth (framer.cc:120-126)
         f->buf.resize(size_t(std::max<int64_t>(need, 2 * int64_t(f->buf.size()))), 0.0f);
     std::memcpy(f->buf.data() + f->wr, interleaved, sizeof(float) * size_t(add));
     f->wr = need;
-    forget_framer(f);  // the frames after the last pop changed
     return 1;
 }
 
 int crlot_framer_pop(crlot_framer* f, float* out) {
     if (!f) return fail(CRLOT_EINVAL, "null framer");
-    if (!f->ready || !out || f->available() == 0) return 0;
+    if (!f->ready || !out) return 0;
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    if (f->available() == 0) return 0;
     const int64_t len = f->n * f->c;     // extract_frame (framer.cc:128-181)
     const int64_t have = f->wr - f->rd;
     if (have >= len) {
@@ -174,8 +195,9 @@ int crlot_framer_pop(crlot_framer* f, float* out) {
     }
     if (f->c == 1) {  // kept for the batched speculation (batch.h)
         f->last.assign(out, out + len);
-        std::lock_guard<std::mutex> lk(g_pop_mu);
         g_last_pop = f;
+    } else {
+        forget_framer_locked(f);
     }
     f->rd = std::min(f->rd + f->h * f->c, f->wr);
     if (f->rd > int64_t(f->buf.size()) / 2) {  // compaction once half the buffer is consumed
@@ -194,8 +216,9 @@ int64_t crlot_framer_available(const crlot_framer* f) {
 
 int crlot_framer_reset(crlot_framer* f) {
     if (!f) return fail(CRLOT_EINVAL, "null framer");
+    std::lock_guard<std::mutex> lk(g_pop_mu);
+    forget_framer_locked(f);
     f->clear();
-    forget_framer(f);
     return CRLOT_OK;
 }
 
@@ -612,7 +635,7 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
     if (!b || crlot::spec_mode() < 2 || b->pushed < 0 || o->C() != 1 || b->n != o->N()) return 0;
     const int64_t j = b->pushed, N = o->N();
     if (start_off != 0 || eff != N || caller_win || !o->cfg.apply_window_inside || o->window.empty() ||
-        o->flushing || std::memcmp(frame, b->h_r + size_t(j) * size_t(N), sizeof(float) * size_t(N)) != 0)
+        o->flushing || std::memcmp(frame, b->h_r + b->row(j) * size_t(N), sizeof(float) * size_t(N)) != 0)
         return 0;
     if (o->vb) {
         if (o->vb != b || b->ola != o || o->vgen != b->gen || j != o->vlast + 1 ||
@@ -623,8 +646,9 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
         // batch's overlap-add does not alias, the ring does.  Before any produce
         // the wrapped ring is still a function of the frames (batch_alias);
         // after one, leave it to the ring
+        // (a batch of several windows holds only the current one's frames: the ring's path)
         if (start_sample + N > o->vread + o->R) {
-            if (o->vread != 0) return 0;
+            if (o->vread != 0 || !b->single()) return 0;
             o->valias = true;
         }
     } else {
@@ -664,7 +688,7 @@ int batch_produce(crlot_ola* o, float* out, int64_t n) {
         // t mod R, already read and cleared once t >= R).  A read longer than
         // the ring (e2e_benchmark.cc's produce(T)) is clamped to it by
         // RingBuffer::split: R outputs, out[R, n) untouched, every slot cleared
-        if (o->vlast != b->M - 1) return 0;
+        if (o->vlast != b->M - 1 || !b->single()) return 0;
         if (!o->vya) {
             const int rc = crlot::batch_alias(b, o->R, o->d_win, o->d_den);
             if (rc != CRLOT_OK) return rc;
@@ -684,10 +708,10 @@ int batch_produce(crlot_ola* o, float* out, int64_t n) {
     const int64_t final_end =
         (o->vlast - b->j0 + 1) * b->h + (o->vlast == b->M - 1 ? std::max<int64_t>(0, b->n - b->h) : 0);
     // (a read longer than the ring is clamped by RingBuffer::split: the ring's path)
-    if (n > o->R || o->vread + n > final_end) return 0;
+    if (n > o->R || o->vread + n > final_end || o->vread < b->y_lo) return 0;
     const int rc = crlot::batch_wait_y(b);
     if (rc != CRLOT_OK) return rc;
-    std::memcpy(out, b->h_y + o->vread, sizeof(float) * size_t(n));
+    std::memcpy(out, b->h_y + (o->vread - b->y_base), sizeof(float) * size_t(n));
     o->vread += n;
     crlot::spec_count(crlot::kStatProduce);
     return 1;
@@ -720,7 +744,9 @@ int ola_materialize(crlot_ola* o) {
     for (int64_t k = b->j0; k <= o->vlast; ++k) {
         const int64_t rel = (k - b->j0) * h, off = std::max<int64_t>(0, o->vread - rel);
         if (off >= N) continue;
-        const hipError_t e = crlot::launch_ola_add(o->d_ring, 1, o->R, b->d_r + size_t(k) * size_t(N) + off, N, 1,
+        if (k < b->cb)  // (a continuing object never needs a frame the window dropped: batch.cpp continue_window)
+            return fail(CRLOT_ERUNTIME, "OLA object: batched speculation lost a frame it needs");
+        const hipError_t e = crlot::launch_ola_add(o->d_ring, 1, o->R, b->d_r + b->row(k) * size_t(N) + off, N, 1,
                                                    o->d_win + off, (rel + off) % o->R, N - off, b->gain, o->own);
         if (e != hipSuccess) return hip_fail(e, "OLA rebuild");
     }
@@ -742,6 +768,12 @@ int ensure_real(crlot_ola* o) {
 
 namespace crlot {
 int ola_materialize_locked(crlot_ola* o) { return ola_materialize(o); }
+// the object read up to the window end's position with every frame before it
+// pushed, so only frames from we - (ceil(N / H) - 1) on reach its unread positions
+bool ola_can_continue(const crlot_ola* o, const BatchSpec* b) {
+    return o->vb == b && b->ola == o && o->vgen == b->gen && o->vlast == b->we - 1 && !o->valias && !o->flushing &&
+           o->vread >= (b->we - b->j0) * b->h;
+}
 }  // namespace crlot
 
 extern "C" {
@@ -1203,19 +1235,25 @@ bool fresh_ola(int64_t n, int64_t h, int device, hipStream_t s, FreshOla* out) {
     return true;
 }
 
-bool framequeue_last_rows(int64_t n, int64_t* hop, int64_t* frames, int* device,
-                          const std::function<float*(size_t)>& dst) {
+bool framequeue_last_rows(int64_t n, int64_t max_frames, const std::function<bool(const float*)>& accept,
+                          int64_t* hop, int64_t* frames, int64_t* total, int* device, uint64_t* source,
+                          int64_t* first, const std::function<float*(size_t)>& dst) {
     std::lock_guard<std::mutex> lk(g_pop_mu);
     const crlot_framequeue* q = g_last_fq;
     if (!q || q->n != n || g_last_fq_idx < 0 || g_last_fq_idx >= q->f) return false;
     const int64_t i = g_last_fq_idx;
-    const size_t floats = size_t(q->f - i) * size_t(n);
+    if (!accept(q->frames + size_t(i) * size_t(n))) return false;  // (row 0 first: no copy for a miss)
+    const int64_t F = std::min(q->f - i, std::max<int64_t>(1, max_frames));
+    const size_t floats = size_t(F) * size_t(n);
     float* d = dst(floats);
     if (!d) return false;
     std::memcpy(d, q->frames + size_t(i) * size_t(n), sizeof(float) * floats);
     *hop = q->h;
-    *frames = q->f - i;
+    *frames = F;
+    *total = q->f - i;
     *device = q->device;
+    *source = reinterpret_cast<uintptr_t>(q);
+    *first = i;
     return true;
 }
 }  // namespace crlot

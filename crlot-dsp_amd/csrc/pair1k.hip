@@ -137,10 +137,12 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     dev::pc* buf = reinterpret_cast<dev::pc*>(smem + PairLds<W>::bufs) + wave * dev::kPairXbuf;
     const dev::pc* t2 = t2s + (lane & 15);  // t2[16 (c-1)] = W64^{(lane & 15) c}
 #if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
-    dev::PairTw tw;
+    // FMA-form twiddles (fft_pair.h PairTwF) at H = 256 only: at H = 128 and 512
+    // their 6 extra VGPRs spill the walk (-5 % / -19 %, profiles/r05b_pairtw_ab.log)
+    std::conditional_t<SH == 4, dev::PairTwReg, dev::PairTw> tw;
     dev::pair_tw_load(tw, t1, t2, lane);
-    const dev::PairTw& tw1 = tw;
-    const dev::PairTw& tw2 = tw;
+    const auto& tw1 = tw;
+    const auto& tw2 = tw;
 #else
     const dev::pc* const tw1 = t1;
     const dev::pc* const tw2 = t2;
@@ -622,10 +624,12 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     };
 
 #if CRLOT_PAIR_REG_TW  // twiddles held in registers (3 waves per SIMD)
-    dev::PairTw tw;
+    // FMA-form twiddles (fft_pair.h PairTwF) at H = 256 only: at H = 128 and 512
+    // their 6 extra VGPRs spill the walk (-5 % / -19 %, profiles/r05b_pairtw_ab.log)
+    std::conditional_t<SH == 4, dev::PairTwReg, dev::PairTw> tw;
     dev::pair_tw_load(tw, t1, t2, lane);
-    const dev::PairTw& tw1 = tw;
-    const dev::PairTw& tw2 = tw;
+    const auto& tw1 = tw;
+    const auto& tw2 = tw;
 #else
     const dev::pc* const tw1 = t1;
     const dev::pc* const tw2 = t2;

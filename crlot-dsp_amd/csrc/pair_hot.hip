@@ -83,33 +83,44 @@ __device__ __forceinline__ void tw_all(dev::pc (&v)[16], const TW& w) {
     constexpr int idx[15] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15};
     dev::pc_tw_run<INV>(v, idx, [&](int i) { return w[i]; });
 }
+// a twiddle stage, explicit (pc[15]) or in the FMA form (Tw15F), then for the
+// inverse the radix-16 that follows it (fused with the twiddles in the FMA form)
+__device__ __forceinline__ void tw_fwd(dev::pc (&v)[16], const dev::pc (&w)[15]) { tw_all<false>(v, w); }
+__device__ __forceinline__ void tw_fwd(dev::pc (&v)[16], const dev::Tw15F& w) { dev::tw15_apply_fwd(v, w); }
+__device__ __forceinline__ void tw_pdft16_inv(dev::pc (&v)[16], const dev::pc (&w)[15]) {
+    tw_all<true>(v, w);
+    dev::pdft16<true>(v);
+}
+__device__ __forceinline__ void tw_pdft16_inv(dev::pc (&v)[16], const dev::Tw15F& w) { dev::tw15_pdft16_inv(v, w); }
 
 // N = 4096: 256 lanes (fft_pair4k.h), rows of 304, a wave's own rows 4w .. 4w+3
 struct Geo4k {
     static constexpr int N = 4096, L = 256, KS = 304, ROWS_PER_WAVE = 4, SIDE = 16, MIN_EXP = -87;  // 1e-30 N = 2^-87.66
-    using Tw = dev::Pair4kTw;
+    template <int SH, bool GAIN>
+    using Tw = dev::Pair4kTwFor<SH, GAIN>;
     using X = XchgRows<SIDE>;
-    static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
+    template <typename TW>
+    static __device__ __forceinline__ void tw_load(TW& tw, const float* g, int t) {
         dev::pair4k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
     }
     static constexpr __device__ int bin(int t, int d) { return dev::pair4k_bin(t, d); }
-    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const Tw& tw, int t, int wave) {
+    template <typename TW>
+    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const TW& tw, int t, int wave) {
         dev::pdft16<false>(v);
-        tw_all<false>(v, tw.w1);
+        tw_fwd(v, tw.w1);
         X::fwd<KS>(v, A, t);
         dev::pdft16<false>(v);
-        tw_all<false>(v, tw.w2);
+        tw_fwd(v, tw.w2);
         dev::transpose16(v, A + KS * ROWS_PER_WAVE * wave, t & 63);
         dev::pdft16<false>(v);
     }
-    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const Tw& tw, int t, int wave) {
+    template <typename TW>
+    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const TW& tw, int t, int wave) {
         dev::pdft16<true>(v);
         dev::transpose16(v, B + KS * ROWS_PER_WAVE * wave, t & 63);
-        tw_all<true>(v, tw.w2);
-        dev::pdft16<true>(v);
+        tw_pdft16_inv(v, tw.w2);
         X::inv<KS>(v, B, t);
-        tw_all<true>(v, tw.w1);
-        dev::pdft16<true>(v);
+        tw_pdft16_inv(v, tw.w1);
     }
     // the wave-local parts of fwd / inv (after / before the workgroup exchange),
     // second-stage twiddles from a getter
@@ -134,28 +145,30 @@ struct Geo4k {
 // N = 2048: 128 lanes (fft_pair2k.h), rows of 152, a wave's own rows 8w .. 8w+7
 struct Geo2k {
     static constexpr int N = 2048, L = 128, KS = 152, ROWS_PER_WAVE = 8, SIDE = 8, MIN_EXP = -88;  // 1e-30 N = 2^-88.66
-    using Tw = dev::Pair2kTw;
+    template <int SH, bool GAIN>
+    using Tw = dev::Pair2kTwFor<SH, GAIN>;
     using X = XchgRows<SIDE>;
-    static __device__ __forceinline__ void tw_load(Tw& tw, const float* g, int t) {
+    template <typename TW>
+    static __device__ __forceinline__ void tw_load(TW& tw, const float* g, int t) {
         dev::pair2k_tw_load(tw, reinterpret_cast<const dev::pc*>(g), t);
     }
-    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const Tw& tw, int t, int wave) {
+    template <typename TW>
+    static __device__ __forceinline__ void fwd(dev::pc (&v)[16], dev::pc* A, const TW& tw, int t, int wave) {
         dev::pdft16<false>(v);
-        tw_all<false>(v, tw.w1);
+        tw_fwd(v, tw.w1);
         X::fwd<KS>(v, A, t);
         dev::pdft16<false>(v);
-        tw_all<false>(v, tw.w2);
+        tw_fwd(v, tw.w2);
         dev::pair2k_t8(v, A + KS * ROWS_PER_WAVE * wave, t & 63);
         dev::pdft8_halves<false>(v);
     }
-    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const Tw& tw, int t, int wave) {
+    template <typename TW>
+    static __device__ __forceinline__ void inv(dev::pc (&v)[16], dev::pc* B, const TW& tw, int t, int wave) {
         dev::pdft8_halves<true>(v);
         dev::pair2k_t8(v, B + KS * ROWS_PER_WAVE * wave, t & 63);
-        tw_all<true>(v, tw.w2);
-        dev::pdft16<true>(v);
+        tw_pdft16_inv(v, tw.w2);
         X::inv<KS>(v, B, t);
-        tw_all<true>(v, tw.w1);
-        dev::pdft16<true>(v);
+        tw_pdft16_inv(v, tw.w1);
     }
     template <typename WF>
     static __device__ __forceinline__ void fwd_tail(dev::pc (&v)[16], dev::pc* own, WF w2, int lane) {
@@ -247,7 +260,7 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
     const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
-    typename G::Tw tw;
+    typename G::template Tw<SH, HAS_GAIN> tw;
     G::tw_load(tw, a.t.ptw4, t);
     float wa[E], ws[E];
 #pragma unroll
@@ -478,7 +491,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) { 
     const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
-    dev::Pair512Tw tw;
+    dev::Pair512TwReg tw;
     dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
     float wa[E], ws[E];
 #pragma unroll

@@ -155,6 +155,23 @@ int crlot_set_call_speculation(int32_t mode);
  * forwards, [2] inverses, [3] pushes, [4] produces served from a batch, [5] OLA
  * rings rebuilt after a call the batch did not predict. */
 int crlot_call_speculation_stats(int64_t* out6);
+/* The same counters and more, out[0 .. count): [0..5] as above, [6] frames the
+ * batches transformed, [7] window continuations (a batch is bounded: at most
+ * `window_frames` frames per chain, below; the next window starts at the
+ * forward of the first frame past it), [8] speculations declined because a
+ * buffer or launch failed (the call then took the ordinary path); entries past
+ * the known ones are 0.  Negative: CRLOT_EINVAL. */
+int crlot_call_speculation_stats_ex(int64_t* out, int32_t count);
+/* Bounds of the batched speculation: frames per window, and the device and
+ * pinned host bytes the batches hold now, with the pinned peak since load. */
+int crlot_call_batch_capacity(int64_t* window_frames, int64_t* device_bytes, int64_t* pinned_bytes,
+                              int64_t* pinned_peak);
+/* Test-only fault injection: CRLOT_INJECT_BATCH_ALLOC makes the next `count`
+ * buffer allocations of the batched speculation fail (a speculation that cannot
+ * allocate declines and the call takes its ordinary path).  Other `what`:
+ * CRLOT_EINVAL. */
+#define CRLOT_INJECT_BATCH_ALLOC 1
+int crlot_test_inject(int32_t what, int32_t count);
 /* What the plan's last call on `stream` launched: kernels in launch order
  * (CRLOT_K_* ids below; the first 8 are kept, n_kernels counts all), the
  * workgroups of each launch, and the chunks per stream of the walk (0 when the

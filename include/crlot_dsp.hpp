@@ -31,12 +31,16 @@
 #include <exception>
 #include <complex>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "crlot_dsp.h"
@@ -288,6 +292,116 @@ class WavWriter {
 }  // namespace io
 
 namespace dsp {
+
+// dsp::base (base/span.h, base/aligned_alloc.h) and dsp::ring::RingBuffer
+// (ring/ring_buffer.h:17-117): the host containers the reference's OLA object is
+// built on.  The drop-in OLAAccumulator keeps its rings in HBM; these exist so
+// code written against the reference's headers (its RingBuffer tests, harness
+// helpers) builds and behaves the same.  Semantics per ring_buffer.cc: split()
+// clamps the length to the capacity and wraps once; a shadow ring allocates
+// twice the capacity and mirrors the head after a wrapping write.
+namespace base {
+template <typename T>
+class Span {
+public:
+    Span() = default;
+    Span(T* p, size_t n) : p_(p), n_(n) {}
+    T* data() const { return p_; }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    T& operator[](size_t i) const { return p_[i]; }
+    T* begin() const { return p_; }
+    T* end() const { return p_ + n_; }
+
+private:
+    T* p_ = nullptr;
+    size_t n_ = 0;
+};
+// 64-byte aligned storage (aligned_alloc.h:18-45); nullptr for n == 0, bad_alloc on failure
+template <typename T>
+T* AllocateAligned(size_t n) {
+    if (n == 0) return nullptr;
+    if (n > SIZE_MAX / sizeof(T)) throw std::bad_alloc();
+    void* p = nullptr;
+    if (posix_memalign(&p, 64, n * sizeof(T)) != 0) throw std::bad_alloc();
+    return static_cast<T*>(p);
+}
+inline void DeallocateAligned(void* p) { std::free(p); }
+}  // namespace base
+
+namespace ring {
+template <typename T>
+class RingBuffer {
+    static_assert(std::is_trivially_copyable<T>::value, "RingBuffer elements are copied bytewise");
+
+public:
+    explicit RingBuffer(size_t capacity, bool shadow = false) : cap_(capacity), shadow_(shadow) {
+        if (capacity == 0) throw std::invalid_argument("RingBuffer capacity must be > 0");
+        const size_t phys = physical_capacity();
+        buf_ = base::AllocateAligned<T>(phys);
+        std::fill(buf_, buf_ + phys, T{});
+    }
+    ~RingBuffer() { base::DeallocateAligned(buf_); }
+    RingBuffer(const RingBuffer&) = delete;
+    RingBuffer& operator=(const RingBuffer&) = delete;
+
+    size_t capacity() const noexcept { return cap_; }
+    size_t physical_capacity() const noexcept { return shadow_ ? 2 * cap_ : cap_; }
+    bool has_shadow() const noexcept { return shadow_; }
+    size_t write_pos() const noexcept { return wpos_; }
+    T* data() noexcept { return buf_; }
+    const T* data() const noexcept { return buf_; }
+
+    std::pair<base::Span<T>, base::Span<T>> split(size_t start, size_t len) noexcept {
+        const auto r = spans(start, len);
+        return {base::Span<T>(r.a, r.na), base::Span<T>(r.b, r.nb)};
+    }
+    std::pair<base::Span<const T>, base::Span<const T>> split(size_t start, size_t len) const noexcept {
+        const auto r = spans(start, len);
+        return {base::Span<const T>(r.a, r.na), base::Span<const T>(r.b, r.nb)};
+    }
+    // mirror elements [0, n) of the ring past its end (shadow rings only)
+    void shadow_sync(size_t n) {
+        if (shadow_ && n > 0) std::memcpy(buf_ + cap_, buf_, std::min(n, cap_) * sizeof(T));
+    }
+    T* contiguous_read_ptr(size_t pos) noexcept { return buf_ + (shadow_ ? pos : pos % cap_); }
+    const T* contiguous_read_ptr(size_t pos) const noexcept { return buf_ + (shadow_ ? pos : pos % cap_); }
+    // n elements at the write position, wrapping once to the head
+    size_t write(const T* src, size_t n) {
+        if (!src || n == 0) return 0;
+        const size_t room = cap_ - wpos_;
+        if (n <= room) {
+            std::memcpy(buf_ + wpos_, src, n * sizeof(T));
+            wpos_ = (wpos_ + n == cap_) ? 0 : wpos_ + n;
+            return n;
+        }
+        std::memcpy(buf_ + wpos_, src, room * sizeof(T));
+        const size_t head = std::min(n - room, cap_);
+        std::memcpy(buf_, src + room, head * sizeof(T));
+        wpos_ = head;
+        shadow_sync(head);
+        return room + head;
+    }
+
+private:
+    struct Spans {
+        T* a;
+        size_t na;
+        T* b;
+        size_t nb;
+    };
+    Spans spans(size_t start, size_t len) const noexcept {
+        if (len == 0) return {nullptr, 0, nullptr, 0};
+        len = std::min(std::min(len, SIZE_MAX - start), cap_);
+        start %= cap_;
+        if (start + len <= cap_) return {buf_ + start, len, nullptr, 0};
+        return {buf_ + start, cap_ - start, buf_, len - (cap_ - start)};
+    }
+    T* buf_ = nullptr;
+    size_t cap_ = 0, wpos_ = 0;
+    bool shadow_ = false;
+};
+}  // namespace ring
 
 enum class WindowType { HANN, HAMMING, BLACKMAN, RECT, BLACKMAN_HARRIS };
 enum class NormalizationType { NONE, SUM_TO_ONE, L2_NORM, OLA_UNITY_GAIN, OLA_SUM_WSQ };

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "../../../crlot_dsp.hpp"
+#include "../ring/ring_buffer.h"  // (the reference header includes it: OLAAccumulator.h:7)
 
 namespace dsp {
 using crlot::dsp::OLAAccumulator;  // OLAAccumulator.h:55-217

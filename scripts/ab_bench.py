@@ -40,6 +40,10 @@ for path in libs:
     d = Desc(N, H, 0, 0, 0, 0, 1, 1, 1e-8, 1.0, 0, -1)
     h = C.c_void_p()
     assert L.crlot_plan_create(C.byref(d), C.byref(h)) == 0
+    if os.environ.get("AB_GAIN") == "1":  # a smooth per-bin gain (the spectral hook)
+        gain = (0.5 + 0.5 * torch.cos(torch.linspace(0, 3.14159, N // 2 + 1))).float().numpy()
+        L.crlot_plan_set_spectral_gain.argtypes = [C.c_void_p, C.c_void_p]
+        assert L.crlot_plan_set_spectral_gain(h, gain.ctypes.data) == 0
     handles[path], plans[path] = L, h
     ys[path] = torch.empty((S, F * H), device="cuda")
 

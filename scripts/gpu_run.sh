@@ -7,6 +7,7 @@
 #   tests[:PYTEST_K]  python -m pytest tests -m gpu [-k PYTEST_K]
 #   smoke             __graft_entry__.smoke()
 #   ab[:N/H]          scripts/ab_bench.py at N/H (default 1024/256) over abtmp/*.so
+#   abgain:N/H        the same with a spectral gain
 #   bench             bench.py (driver flags: --steps 20 --warmup 5)
 #   configs           scripts/bench_configs.py
 #   suite:NAME        bench.py --suite NAME
@@ -40,6 +41,9 @@ for s in "$@"; do
     ab)
       n=${arg%%/*}; h=${arg#*/}; [ -z "$arg" ] && n=1024 && h=256
       AB_N=$n AB_H=$h AB_GLOB="abtmp/*.so" AB_ROUNDS=${AB_ROUNDS:-8} run "ab_${n}_${h}" 400 python -u scripts/ab_bench.py ;;
+    abgain)
+      n=${arg%%/*}; h=${arg#*/}
+      AB_GAIN=1 AB_N=$n AB_H=$h AB_GLOB="abtmp/*.so" AB_ROUNDS=${AB_ROUNDS:-8} run "abgain_${n}_${h}" 400 python -u scripts/ab_bench.py ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     configs) run configs 600 python scripts/bench_configs.py ;;
     suite) run "suite_$arg" 600 python bench.py --suite "$arg" ;;

@@ -868,3 +868,149 @@ def test_batched_loop_keeps_ring_aliasing_of_the_harness_order(pkg, oracle, torc
     r = np.full(48_000, 7.0, np.float32)
     got = ref.produce_into(48_000, [r])
     assert np.array_equal(bits(yb[:got]), bits(r[:got]))
+
+
+# ---- bounded batches: windows of at most kBatchWindow frames
+
+def _e2e_digest(pkg, x, n, h, breaks=None, limit=None):
+    """The e2e loop (streaming-interleaved) without keeping its outputs: a digest
+    of every spectrum, inverse frame and produced block, and the frame count.
+    `breaks`: frame -> "input" (forward input one ulp off); `limit`: frames run."""
+    import hashlib
+    breaks = breaks or {}
+    w = pkg.window_table(pkg.HANN, n)
+    fr = pkg.Framer()
+    fr.set_params(n, h, 1, pkg.ZERO_PAD)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                                           apply_window_inside=True))
+    ola.set_window(w)
+    fr.push(x)
+    dig = hashlib.sha256()
+    k = 0
+    while limit is None or k < limit:
+        f = fr.pop()
+        if f is None:
+            break
+        p = (f * w).astype(np.float32)
+        if breaks.get(k) == "input":
+            p[k % n] = np.nextafter(p[k % n], np.float32(np.inf))
+        X = fft.forward_host(p[None])
+        y = fft.inverse_host(X)[0]
+        ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+        got, chans = ola.produce(h)
+        for a in (np.asarray(X), y, chans[0][:got]):
+            dig.update(np.ascontiguousarray(a).view(np.uint32).tobytes())
+        k += 1
+    ola.close()
+    fft.close()
+    fr.close()
+    return dig.hexdigest(), k
+
+
+def _spec_delta(pkg, run):
+    s0 = pkg.call_speculation_stats_ex()
+    out = run()
+    s1 = pkg.call_speculation_stats_ex()
+    return out, {key: s1[key] - s0[key] for key in s1}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,T", [(1024, 256, 160_000), (960, 240, 130_000), (1024, 512, 300_000)])
+def test_batched_loop_spans_windows(pkg, oracle, torch_cuda, n, h, T):
+    """A signal longer than one batch window: the batch runs window after window
+    (each continuation carries the last frames' inverse outputs over for the OLA
+    object), and every call still gives the per-call path's bits and the oracle
+    OLAAccumulator's blocks."""
+    x = oracle.synth(T, n + 3 * h)
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_loop(pkg, oracle, x, n, h)
+        pkg.set_call_speculation(2)
+        b, served = _spec_delta(pkg, lambda: _e2e_loop(pkg, oracle, x, n, h))
+    finally:
+        pkg.set_call_speculation(2)
+    F = len(a[0])
+    K = pkg.call_batch_capacity()["window_frames"]
+    assert F > K and len(b[0]) == F
+    for k in range(F):
+        assert np.array_equal(bits(a[0][k]), bits(b[0][k])), ("spectrum", k)
+        assert np.array_equal(bits(a[1][k]), bits(b[1][k])), ("inverse", k)
+        assert np.array_equal(bits(a[2][k]), bits(b[2][k])), ("produce", k)
+    ref = _oracle_outputs(oracle, n, h, pkg.window_table(pkg.HANN, n), b[3])
+    for k in range(F):
+        assert np.array_equal(bits(b[2][k]), bits(ref[k])), ("oracle", k)
+    assert served["batches"] == 1 and served["windows"] == (F - 1) // K, served
+    assert served["forwards"] == F and served["inverses"] == F and served["pushes"] == F, served
+    assert served["produces"] == F and served["rebuilds"] == 0 and served["frames"] == F, served
+
+
+@pytest.mark.gpu
+def test_batched_loop_ten_minutes_bounded_memory(pkg, oracle, torch_cuda):
+    """bench/e2e_benchmark.cc:144 pushes one second of audio whole into the
+    Framer; here ten minutes (28.8 M samples, 112 500 frames at 1024/256).  The
+    batch works window by window: the pinned and device memory it holds stay at
+    one window's worth (an unbounded batch would pin ~0.9 GB here), and every
+    spectrum, inverse frame and produced block equals the per-call path's."""
+    n, h, T = 1024, 256, 48_000 * 600
+    rng = np.random.default_rng(600)
+    x = (rng.standard_normal(T) * 0.1).astype(np.float32)
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_digest(pkg, x, n, h)
+        pkg.set_call_speculation(2)
+        b, served = _spec_delta(pkg, lambda: _e2e_digest(pkg, x, n, h))
+    finally:
+        pkg.set_call_speculation(2)
+    assert a == b, (a, b)
+    F = a[1]
+    cap = pkg.call_batch_capacity()
+    K = cap["window_frames"]
+    assert served["frames"] == F and served["windows"] == (F - 1) // K and served["rebuilds"] == 0, served
+    whole = F * (2 * n + 2) * 4  # spectra + inverse frames of the whole signal
+    assert cap["pinned_peak"] <= 128 << 20 < whole, cap
+    assert cap["pinned_bytes"] <= 40 << 20 and cap["device_bytes"] <= 64 << 20, cap
+    print(f"\n10-minute loop: {F} frames, {served['windows']} window continuations, batch memory {cap}")
+
+
+@pytest.mark.gpu
+def test_batched_loop_broken_at_frame_2_does_bounded_work(pkg, oracle, torch_cuda):
+    """A caller that breaks the rhythm at frame 2 of a long signal pays for at most
+    one window per batch start, not for the whole signal."""
+    n, h = 1024, 256
+    x = oracle.synth(48_000 * 60, 5)
+    (dig, k), served = _spec_delta(pkg, lambda: _e2e_digest(pkg, x, n, h, breaks={2: "input"}, limit=12))
+    K = pkg.call_batch_capacity()["window_frames"]
+    assert k == 12 and served["batches"] == 2 and served["rebuilds"] == 1, served
+    assert served["frames"] <= 2 * K < (x.size // h), served
+    try:
+        pkg.set_call_speculation(1)
+        ref = _e2e_digest(pkg, x, n, h, breaks={2: "input"}, limit=12)
+    finally:
+        pkg.set_call_speculation(2)
+    assert ref == (dig, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,count", [(2000, 500, 1), (2200, 550, 1000)])
+def test_batched_loop_declines_when_allocation_fails(pkg, oracle, torch_cuda, n, h, count):
+    """An allocation failure inside the speculation (injected: the next `count`
+    batch buffer allocations fail) is not the caller's error: the forward takes
+    the ordinary path and returns the right spectrum.  Frame sizes no other test
+    batches, so their buffers are allocated here."""
+    x = oracle.synth(40_000, 13)
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_digest(pkg, x, n, h)
+        pkg.set_call_speculation(2)
+        pkg.test_inject(pkg.INJECT_BATCH_ALLOC, count)
+        b, served = _spec_delta(pkg, lambda: _e2e_digest(pkg, x, n, h))
+    finally:
+        pkg.test_inject(pkg.INJECT_BATCH_ALLOC, 0)
+        pkg.set_call_speculation(2)
+    assert a == b
+    assert served["declined"] >= 1, served
+    if count == 1:  # the next frame's forward starts the batch
+        assert served["batches"] == 1 and served["forwards"] == a[1] - 1, served
+    else:
+        assert served["batches"] == 0 and served["forwards"] == 0, served

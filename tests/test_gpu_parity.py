@@ -1098,7 +1098,11 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     two-regime walker over every chunk, mode 1 through the hot walker; a burst of
     out-of-range samples exercises the flagged chunks' fix-up inside the hot run.
     A spectral gain of exactly 1 (x * 1 is exact) gives the same bits again, through
-    K_pair's gain-carrying hot walker or the others' two-regime walkers."""
+    K_pair's gain-carrying hot walker or the others' two-regime walkers -- except at
+    N = 4096, whose gain plans keep the classic twiddle rotations (the FMA form
+    spills the gain-carrying walker, fft_pair4k.h): there the gain-1 plan equals
+    the no-gain plan within the FFT tolerance, and its own hot and two-regime
+    walkers agree bit for bit."""
     torch = torch_cuda
     x = oracle.synth_streams(6, T, config_id=71)
     x[2, T // 3:T // 3 + 5] = 1e25   # unpaired regime: that chunk is redone
@@ -1113,7 +1117,14 @@ def test_pair_hot_walker_equals_two_regime_walker(pkg, oracle, torch_cuda, n, h,
     plan.set_frame_pairing(1)
     plan.set_spectral_gain(np.ones(n // 2 + 1, np.float32))
     y_gain1 = host(plan.roundtrip(xd))
-    assert np.array_equal(bits(y_hot), bits(y_gain1))
+    if n != 4096:
+        assert np.array_equal(bits(y_hot), bits(y_gain1))
+    else:
+        ok = np.isfinite(y_hot).all(axis=1)
+        assert rel_l2(y_gain1[ok], y_hot[ok]) <= REL_L2
+        plan.set_frame_pairing(2)
+        assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(y_gain1))
+        plan.set_frame_pairing(1)
 
 
 def quiet_with_zeros(row, at, length):
