@@ -170,15 +170,53 @@ def load_pmc_traffic(workload_key: str):
     return (None if stale else best.get("hbm_bytes_per_launch")), meta
 
 
-def valu_block(fps, achieved_tf, issue, kern_ms):
+ISSUE_CYCLES = {"packed": 4, "permlane": 8, "other": 2}  # per wave64 instruction
+
+
+def isa_issue_model(pairs_per_simd, kernel_cycles):
+    """The main loop's VALU issue cost from its instruction classes (the newest
+    profiles/*_isa_hist.json of these kernel sources): cycles per frame pair per
+    wave = 4 x packed + 8 x permlane + 2 x other VALU; times the pairs a SIMD
+    runs per launch, over the kernel's cycles (PMC GRBM_GUI_ACTIVE / 8)."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_isa_hist.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("src_hash") == src_hash():
+            best = (f, d)
+    if best is None:
+        return None
+    f, d = best
+    k = next((k for k in d["kernels"] if k.get("label", "").startswith("K_pair 1024/256")), None)
+    if not k or not k.get("pairs_per_iteration"):
+        return None
+    ppi = k["pairs_per_iteration"]
+    packed, perm = k["loop_packed"] / ppi, k["loop_permlane"] / ppi
+    other = k["loop_valu"] / ppi - packed - perm
+    cyc = ISSUE_CYCLES["packed"] * packed + ISSUE_CYCLES["permlane"] * perm + ISSUE_CYCLES["other"] * other
+    out = {"file": os.path.relpath(f, ROOT), "valu_per_pair": round(k["loop_valu"] / ppi, 1),
+           "packed_per_pair": round(packed, 1), "permlane_per_pair": round(perm, 1), "other_per_pair": round(other, 1),
+           "issue_cycles_per_pair": round(cyc, 1), "cycles_per_instruction": ISSUE_CYCLES}
+    if kernel_cycles:
+        out["issue_frac"] = round(cyc * pairs_per_simd / kernel_cycles, 4)
+    return out
+
+
+def valu_block(fps, achieved_tf, issue, kern_ms, pairs_per_simd=None):
     """roofline.valu: the launches priced in SURVEY 8d flops against the FP32
-    vector peak, plus -- from the same kernel sources' PMC profile -- the VALU
-    busy fraction (instruction cycles per SIMD / kernel cycles) and the FP32
+    vector peak, plus -- from the same kernel sources' PMC profile -- the cycles
+    the SIMDs had a VALU instruction active (SQ_ACTIVE_INST_VALU-based: issue
+    plus the dependency latency it waits out, not issue alone) over the kernel's
+    cycles, the issue cost from the loop's instruction classes, and the FP32
     flops the hardware counted (SQ_INSTS_VALU_FLOPS_FP32) at this run's time."""
     v = {"flop_per_sample": round(fps, 1), "achieved_tflops": round(achieved_tf, 2),
          "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(achieved_tf / VALU_PEAK_TFLOPS, 4)}
+    if pairs_per_simd:
+        v["issue_model"] = isa_issue_model(pairs_per_simd, (issue or {}).get("kernel_cycles"))
     if issue:
-        v["busy_frac_pmc"] = None if issue.get("busy_frac") is None else round(issue["busy_frac"], 4)
+        v["active_inst_frac_pmc"] = None if issue.get("busy_frac") is None else round(issue["busy_frac"], 4)
         if issue.get("fp32_flops_per_launch"):
             tf = issue["fp32_flops_per_launch"] / (kern_ms * 1e-3) / 1e12
             v["counted_fp32_tflops"] = round(tf, 2)
@@ -186,16 +224,19 @@ def valu_block(fps, achieved_tf, issue, kern_ms):
     return v
 
 
+SIMDS = 1024  # 256 CUs x 4 SIMDs
 RAMP_S = 0.25  # untimed clock ramp before the warm-up steps (reported as clock_ramp_steps)
 
 
-def timed_phase(plan, x, y, steps: int, warmup: int, D, dev, torch, ramp: dict = None):
+def timed_phase(plan, x, y, steps: int, warmup: int, D, dev, torch, ramp: dict = None, timings: dict = None):
     """Clock ramp (untimed round trips for RAMP_S seconds: an idle MI355X takes
     ~100-200 ms to reach its loaded clock, longer than a few warm-up steps), then
     `warmup` untimed steps, then `steps` round trips bracketed by barrier +
     synchronize; returns (wall seconds max over ranks, mean kernel ms on the
     launch stream)."""
     stream = torch.cuda.current_stream(dev)
+    slow = float(os.environ.get("CRLOT_BENCH_SLOW_RANK_FACTOR", "0") or 0) if D.env_rank_world()[0] == int(
+        os.environ.get("CRLOT_BENCH_SLOW_RANK", "-1")) else 0.0  # (rehearsal of a straggler: tests only)
     n_ramp, t_end = 0, time.perf_counter() + RAMP_S
     while time.perf_counter() < t_end:
         plan.roundtrip(x, y)
@@ -216,9 +257,15 @@ def timed_phase(plan, x, y, steps: int, warmup: int, D, dev, torch, ramp: dict =
         plan.roundtrip(x, y)
         ev[i][1].record(stream)
     torch.cuda.synchronize(dev)
+    own = time.perf_counter() - t0  # this rank's own time, before the closing barrier
+    if slow > 1.0:
+        time.sleep(own * (slow - 1.0))
+        own *= slow
     D.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    if timings is not None:
+        timings["own_ms"] = own * 1e3 / steps
     return D.max_over_ranks(elapsed, dev), kern_ms
 
 
@@ -486,6 +533,23 @@ def _cpu_loop_us(O, native, x, n, h, reps=5, **ex):
     return ts[len(ts) // 2] * 1e6, F
 
 
+def _cpu_gain_loop_us(O, native, x, n, h, reps=5):
+    """Median microseconds of the oracle's e2e loop with the spectral step (every
+    bin scaled by the e2e harness's gain 0.5 + 0.5 cos(pi k / (N/2))), one thread."""
+    L = O.lib(native)
+    g = (0.5 + 0.5 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2))).astype(np.float32)
+    T = x.size
+    F = O.frames_for(T, n, h, O.ZERO_PAD, True)
+    y = np.zeros(max(F * h, 1), np.float32)
+    ts = []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        L.or_roundtrip_gain(x, T, n, h, O.HANN, 0, O.ZERO_PAD, g.ctypes.data, y, F * h)
+        ts.append(time.perf_counter() - t0)
+    ts = sorted(ts[1:])
+    return ts[len(ts) // 2] * 1e6, F
+
+
 def suite_e2e(pkg, torch, dev):
     """bench/e2e_benchmark.cc counterpart: the per-frame drop-in loop through the
     C++ classes (harness/e2e_bench: Framer -> window -> IFftPlan::forward ->
@@ -504,6 +568,9 @@ def suite_e2e(pkg, torch, dev):
         cpu_us, F = _cpu_loop_us(O, native, x, n, h)
         g["cpu_oracle_1thread"] = {"ms_per_iteration": round(cpu_us / 1e3, 4), "us_per_frame": round(cpu_us / F, 3),
                                    "x_realtime": round(1e6 / cpu_us, 1)}
+        gus, _ = _cpu_gain_loop_us(O, native, x, n, h)
+        g["spectral_gain"]["cpu_oracle_1thread"] = {"ms_per_iteration": round(gus / 1e3, 4),
+                                                    "us_per_frame": round(gus / F, 3)}
         res["runs"].append(g)
     res["cpu_native_build"] = native
     return res
@@ -613,9 +680,13 @@ def main():
     # ---- weak phase (headline): S streams per rank
     x = synth_device(torch, S, T, dev, 0xC0FFEE + rank)
     y = torch.empty((S, L), dtype=torch.float32, device=dev)
-    ramp = {}
-    elapsed_max, kern_ms = timed_phase(plan, x, y, args.steps, args.warmup, D, dev, torch, ramp)
+    ramp, mine = {}, {}
+    elapsed_max, kern_ms = timed_phase(plan, x, y, args.steps, args.warmup, D, dev, torch, ramp, mine)
     del x, y
+    # every rank's device, kernel time and own wall time: who set the max (a first
+    # 8-GPU run names its straggler)
+    per = D.gather_over_ranks([kern_ms, mine["own_ms"]], dev)
+    ranks = D.rank_report([p[0] for p in per], [p[1] for p in per], observed["device_keys"])
 
     samples_step_rank = S * T
     value = samples_step_rank * world * args.steps / elapsed_max / 1e6
@@ -692,12 +763,14 @@ def main():
                 "traffic_source": traffic_meta,
                 "kernel_ms": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": BYTES_PER_SAMPLE * samples_step_rank,
-                "valu": valu_block(fps, achieved_tf, traffic_meta.get("valu_issue"), kern_ms),
+                "valu": valu_block(fps, achieved_tf, traffic_meta.get("valu_issue"), kern_ms,
+                                   S * plan.frame_count(T) / 2 / SIMDS),
                 "note": "frac is the metric's HBM-roofline fraction (8 B/sample); the kernel "
                         "is bound on the VALU issue (DESIGN.md section 5), valu.frac prices "
                         "the same launches in SURVEY 8d flops",
             },
             "strong_scaling": strong,
+            "ranks_report": ranks,
             "dist": {
                 "backend": observed["backend"],
                 "world_observed": observed["world"],

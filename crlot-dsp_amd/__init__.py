@@ -235,7 +235,8 @@ def call_speculation_stats() -> dict:
     return dict(zip(("batches", "forwards", "inverses", "pushes", "produces", "rebuilds"), list(v)))
 
 
-SPEC_STATS = ("batches", "forwards", "inverses", "pushes", "produces", "rebuilds", "frames", "windows", "declined")
+SPEC_STATS = ("batches", "forwards", "inverses", "pushes", "produces", "rebuilds", "frames", "windows", "declined",
+              "gains")
 
 
 def call_speculation_stats_ex() -> dict:
@@ -256,6 +257,7 @@ def call_batch_capacity() -> dict:
 
 
 INJECT_BATCH_ALLOC = 1
+INJECT_CALL_TIMEOUT = 2
 
 
 def test_inject(what: int, count: int):

@@ -1281,7 +1281,8 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     // a call the running batch serves touches no device state: no device switch
     if (p->sh && kind < 2 && batch == 1 && inc_in == 1 && inc_out == 1 && crlot::spec_mode() >= 2) {
         std::lock_guard<std::mutex> slk(p->sh->mu);
-        const int brc = kind == 0 ? crlot::batch_serve_forward(p->sh, n, in, out) : crlot::batch_inverse(p->sh, n, in, out);
+        const int brc = kind == 0 ? crlot::batch_serve_forward(p->sh, n, in, out)
+                                  : crlot::batch_inverse(p->sh, nullptr, n, in, out);
         if (brc != 0) return brc < 0 ? brc : CRLOT_OK;
     }
     DeviceGuard g(p->device);
@@ -1307,7 +1308,8 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
             crlot_plan* inner = fft_inner(p, &irc);
             brc = inner ? crlot::batch_forward(sh, inner, n, in, out) : 0;
         } else {
-            brc = crlot::batch_inverse(sh, n, in, out);
+            int irc = CRLOT_OK;
+            brc = crlot::batch_inverse(sh, fft_inner(p, &irc), n, in, out);
         }
         if (brc != 0) return brc < 0 ? brc : CRLOT_OK;
     }

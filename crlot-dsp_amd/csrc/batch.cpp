@@ -233,12 +233,13 @@ hipError_t launch_spec_ola(BatchSpec* b, int dev, bool zc_out) {
 // first ones)
 hipError_t launch_ola_window(BatchSpec* b, bool zc_out) {
     const size_t N = size_t(b->n), rows = b->rows_cap, row = N + 2;
-    const int64_t F = b->we - b->cb;
+    const int64_t first = std::max(b->cb, b->j0);  // the object's frames in the buffers
+    const int64_t F = b->we - first;
     const size_t ylen = y_floats(b, size_t(F));
-    // the gather divides position p by den[p mod R] from its own origin, frame cb's
-    // start, which sits (cb - j0) H into the object's ring: a rotated copy of the
-    // divisors puts that origin at index 0
-    const size_t R = size_t(b->ola_R), off = size_t((b->cb - b->j0) * b->h) % R;
+    // the gather divides position p by den[p mod R] from its own origin, frame
+    // first's start, which sits (first - j0) H into the object's ring: a rotated
+    // copy of the divisors puts that origin at index 0
+    const size_t R = size_t(b->ola_R), off = size_t((first - b->j0) * b->h) % R;
     hipError_t e;
     if ((e = dgrow(&b->d_den_rot, &b->c_den_rot, R)) ||
         (e = hipMemcpyAsync(b->d_den_rot, b->ola_den + off, sizeof(float) * (R - off), hipMemcpyDeviceToDevice, b->s)) ||
@@ -254,11 +255,12 @@ hipError_t launch_ola_window(BatchSpec* b, bool zc_out) {
     t.ws = b->ola_ws;
     t.den = b->d_den_rot;
     float* yout = zc_out ? b->m_blk + (rows * row + rows * N) : b->d_y;
-    if ((e = launch_ola_gather(g, t, b->d_r, b->n, yout, 1, F, int64_t(ylen), int64_t(ylen), b->s)) ||
+    if ((e = launch_ola_gather(g, t, b->d_r + b->row(first) * N, b->n, yout, 1, F, int64_t(ylen), int64_t(ylen),
+                               b->s)) ||
         (!zc_out && (e = hipMemcpyAsync(b->h_y, b->d_y, sizeof(float) * ylen, hipMemcpyDeviceToHost, b->s))))
         return e;
-    b->y_base = (b->cb - b->j0) * b->h;
-    b->y_lo = (b->wb - b->j0) * b->h;
+    b->y_base = (first - b->j0) * b->h;
+    b->y_lo = (std::max(b->wb, first) - b->j0) * b->h;
     b->y_ready = true;
     b->y_waited = false;
     return hipSuccess;
@@ -302,21 +304,32 @@ int launch_chain(BatchSpec* b, crlot_plan* inner, int64_t carry) {
             return hip_fail(e, "batch frames");
     }
     CRLOT_LAP(2);
-    // forward + inverse: one launch where the plan has the fused kernel
+    // forward + inverse: one launch where the plan has the fused kernel; with a
+    // learned spectral gain, forward, the gain and inverse as three
     const size_t c = size_t(carry);
     float* spec_dev = b->d_spec + c * row;
     float* r_dev = b->d_r + c * N;
+    const bool gained = !b->sgain.empty();
     bool spec_r_host = false;
-    int rc = fuse_fft() ? plan_rfft_irfft(inner, d_in, zc_out ? b->m_blk + c * row : spec_dev, r_dev,
-                                          zc_out ? b->m_blk + rows * row + c * N : nullptr, int32_t(F), b->s)
-                        : CRLOT_EUNSUPPORTED;
+    int rc = fuse_fft() && !gained
+                 ? plan_rfft_irfft(inner, d_in, zc_out ? b->m_blk + c * row : spec_dev, r_dev,
+                                   zc_out ? b->m_blk + rows * row + c * N : nullptr, int32_t(F), b->s)
+                 : CRLOT_EUNSUPPORTED;
     if (rc == CRLOT_OK) {
         spec_r_host = zc_out;
     } else if (rc == CRLOT_EUNSUPPORTED) {
         rc = crlot_rfft_batched(inner, d_in, spec_dev, int32_t(F), int64_t(N), 1, int64_t(row), 1, b->s);
         CRLOT_LAP(3);
+        const float* inv_in = spec_dev;
+        if (rc == CRLOT_OK && gained) {
+            if ((e = dgrow(&b->d_specg, &b->c_specg, rows * row)) ||
+                (e = launch_bin_gain(spec_dev, b->d_specg, b->d_sgain, int64_t(F), int64_t(row), int64_t(N / 2 + 1),
+                                     b->s)))
+                return hip_fail(e, "batch spectral gain");
+            inv_in = b->d_specg;
+        }
         if (rc == CRLOT_OK)
-            rc = crlot_irfft_batched(inner, spec_dev, r_dev, int32_t(F), int64_t(row), 1, int64_t(N), 1, b->s);
+            rc = crlot_irfft_batched(inner, inv_in, r_dev, int32_t(F), int64_t(row), 1, int64_t(N), 1, b->s);
     }
     if (rc != CRLOT_OK) return rc;
     CRLOT_LAP(4);
@@ -572,6 +585,15 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     b->next_fwd = 0;
     b->y_ready = b->y_waited = false;
     b->ola = nullptr;
+    b->sgain_from = 0;  // (a gain learned earlier is applied from the start: the likeliest caller)
+    b->learn_after = -1;
+    if (!b->sgain.empty()) {
+        const size_t bins = size_t(n) / 2 + 1;
+        hipError_t ge = b->sgain.size() == bins ? dgrow(&b->d_sgain, &b->c_sgain, bins) : hipErrorInvalidValue;
+        if (ge == hipSuccess && b->s)
+            ge = hipMemcpyAsync(b->d_sgain, b->sgain.data(), sizeof(float) * bins, hipMemcpyHostToDevice, b->s);
+        if (ge != hipSuccess || !b->s) b->sgain.clear();
+    }
     CRLOT_LAP(0);
     // buffers for one window, plus the frames a continuing object carries over
     // when the batch has more than one
@@ -589,12 +611,107 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     return 1;
 }
 
-int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out) {
+namespace {
+// the inverse input the batch predicts for frame j: its spectrum, or the
+// products with the learned gain (the caller's std::complex<float> *= float)
+bool inverse_input_matches(const BatchSpec* b, int64_t j, const float* in) {
+    const size_t row = size_t(b->n) + 2;
+    const float* X = b->h_spec + b->row(j) * row;
+    if (b->sgain.empty() || j < b->sgain_from) return std::memcmp(in, X, sizeof(float) * row) == 0;
+    thread_local std::vector<float> pred;
+    pred.resize(row);
+    const float* g = b->sgain.data();
+    for (size_t k = 0; k < row / 2; ++k) {
+        pred[2 * k] = X[2 * k] * g[k];
+        pred[2 * k + 1] = X[2 * k + 1] * g[k];
+    }
+    return std::memcmp(in, pred.data(), sizeof(float) * row) == 0;
+}
+
+// A real gain per bin that maps frame j's spectrum X onto the caller's input Y
+// bit for bit (Y = X * g in float): g[k] = Y / X, checked, with its float
+// neighbours as a fallback for the rounding of the division.  Bins where X is
+// zero keep the previous gain (or 1): any gain reproduces them.
+bool learn_gain(const BatchSpec* b, int64_t j, const float* Y, std::vector<float>* g) {
+    const size_t bins = size_t(b->n) / 2 + 1;
+    const float* X = b->h_spec + b->row(j) * (size_t(b->n) + 2);
+    g->resize(bins);
+    auto same = [](float a, float c) { return std::memcmp(&a, &c, sizeof(float)) == 0; };
+    for (size_t k = 0; k < bins; ++k) {
+        const float xr = X[2 * k], xi = X[2 * k + 1], yr = Y[2 * k], yi = Y[2 * k + 1];
+        float q = b->sgain.size() == bins ? b->sgain[k] : 1.0f;
+        if (xr != 0.0f)
+            q = yr / xr;
+        else if (xi != 0.0f)
+            q = yi / xi;
+        if (!std::isfinite(q)) return false;
+        const float cand[3] = {q, std::nextafter(q, INFINITY), std::nextafter(q, -INFINITY)};
+        bool ok = false;
+        for (float c : cand)
+            if (same(xr * c, yr) && same(xi * c, yi)) {
+                (*g)[k] = c;
+                ok = true;
+                break;
+            }
+        if (!ok) return false;
+    }
+    return true;
+}
+
+// the inverses of frames j .. we-1 of the buffers redone with the gain (and the
+// attached object's produce blocks over them), waited for
+int apply_gain(BatchSpec* b, crlot_plan* inner, int64_t j) {
+    const size_t N = size_t(b->n), row = N + 2, bins = N / 2 + 1, F = size_t(b->we - j);
+    hipError_t e;
+    if ((e = dgrow(&b->d_sgain, &b->c_sgain, bins)) || (e = dgrow(&b->d_specg, &b->c_specg, b->rows_cap * row)) ||
+        (e = hipMemcpyAsync(b->d_sgain, b->sgain.data(), sizeof(float) * bins, hipMemcpyHostToDevice, b->s)) ||
+        (e = launch_bin_gain(b->d_spec + b->row(j) * row, b->d_specg, b->d_sgain, int64_t(F), int64_t(row),
+                             int64_t(bins), b->s)))
+        return hip_fail(e, "batch spectral gain");
+    float* r_dev = b->d_r + b->row(j) * N;
+    int rc = crlot_irfft_batched(inner, b->d_specg, r_dev, int32_t(F), int64_t(row), 1, int64_t(N), 1, b->s);
+    if (rc != CRLOT_OK) return rc;
+    if ((e = hipMemcpyAsync(b->h_r + b->row(j) * N, r_dev, sizeof(float) * F * N, hipMemcpyDeviceToHost, b->s)))
+        return hip_fail(e, "batch spectral gain");
+    if (b->ola) {
+        if ((e = launch_ola_window(b, false))) return hip_fail(e, "batch overlap-add");
+    } else {
+        b->spec_y = false;  // a fresh object's blocks were of the inverses without the gain
+    }
+    if ((e = hipEventRecord(b->ev, b->s)) || (e = hipEventSynchronize(b->ev))) return hip_fail(e, "batch spectral gain");
+    if (b->ola) b->y_waited = true;
+    return CRLOT_OK;
+}
+}  // namespace
+
+int batch_inverse(SharedServer* sh, crlot_plan* inner, int64_t n, const float* in, float* out) {
     BatchSpec* b = sh->batch;
     if (!b || spec_mode() < 2 || b->n != n || b->inv_ready < 0) return 0;
     const int64_t j = b->inv_ready;
-    const size_t row = size_t(n) + 2;
-    if (std::memcmp(in, b->h_spec + b->row(j) * row, sizeof(float) * row) != 0) return 0;
+    if (!inverse_input_matches(b, j, in)) {
+        // a spectral step the batch does not know: learn it if it is a fixed real
+        // gain per bin, and redo this window's remaining inverses with it
+        if (!inner || j < b->learn_after) return 0;
+        std::vector<float> g;
+        if (!learn_gain(b, j, in, &g)) {
+            b->learn_after = j + 16;
+            return 0;
+        }
+        const std::vector<float> old = b->sgain;
+        const int64_t old_from = b->sgain_from;
+        b->sgain.swap(g);
+        b->sgain_from = j;
+        if (apply_gain(b, inner, j) != CRLOT_OK) {  // nothing served: the buffers hold the old inverses
+            b->sgain = old;
+            b->sgain_from = old_from;
+            b->learn_after = j + 16;
+            return decline(b);
+        }
+        spec_count(kStatGains);
+        if (std::all_of(b->sgain.begin(), b->sgain.end(), [](float v) { return v == 1.0f; }))
+            b->sgain.clear();  // the identity again (x * 1 is exact: the rows redone are its bits)
+        if (!inverse_input_matches(b, j, in)) return 0;
+    }
     std::memcpy(out, b->h_r + b->row(j) * size_t(n), sizeof(float) * size_t(n));
     b->inv_ready = -1;
     b->pushed = j;
@@ -705,8 +822,14 @@ extern "C" int crlot_call_batch_capacity(int64_t* window_frames, int64_t* device
 }
 
 extern "C" int crlot_test_inject(int32_t what, int32_t count) {
-    if (what != CRLOT_INJECT_BATCH_ALLOC || count < 0) return crlot::set_error(CRLOT_EINVAL, "unknown injection");
-    crlot::g_fail_alloc.store(count, std::memory_order_relaxed);
+    if (count < 0) return crlot::set_error(CRLOT_EINVAL, "negative injection count");
+    if (what == CRLOT_INJECT_BATCH_ALLOC) {
+        crlot::g_fail_alloc.store(count, std::memory_order_relaxed);
+    } else if (what == CRLOT_INJECT_CALL_TIMEOUT) {
+        crlot::test_inject_timeouts(count);
+    } else {
+        return crlot::set_error(CRLOT_EINVAL, "unknown injection");
+    }
     return CRLOT_OK;
 }
 

@@ -83,7 +83,7 @@ std::vector<std::vector<float>> windows_of_size(int64_t n);
 // speculation of the whole loop too (crlot_set_call_speculation)
 int spec_mode();
 enum { kStatStart = 0, kStatForward, kStatInverse, kStatPush, kStatProduce, kStatRebuild, kStatFrames, kStatWindows,
-       kStatDeclined, kStatCount };
+       kStatDeclined, kStatGains, kStatCount };
 void spec_count(int what);
 
 struct BatchSpec {
@@ -146,6 +146,16 @@ struct BatchSpec {
     FreshOla spec_ola;
     bool spec_y = false;     // computed with this batch
     bool spec_used = false;  // the attached object is the one it was computed for
+    // the caller's spectral step, when it is a fixed real gain per bin (learned
+    // from an inverse input the batch did not predict, batch_inverse): the
+    // inverses of frames from sgain_from on are those of fl(gain * spectrum), and
+    // an inverse is served only if its input is those products bit for bit
+    std::vector<float> sgain;  // [N/2 + 1]; empty: the identity step
+    int64_t sgain_from = 0;
+    int64_t learn_after = -1;  // no new learning attempt before this frame (after a failed one)
+    float* d_sgain = nullptr;
+    float* d_specg = nullptr;  // [rows][N + 2] gained spectra (the inverse's input)
+    size_t c_sgain = 0, c_specg = 0;
     bool single() const { return cb == 0 && we == M; }  // one window holds every frame
     size_t row(int64_t j) const { return size_t(j - cb); }
 };
@@ -158,7 +168,9 @@ bool ola_can_continue(const crlot_ola* o, const BatchSpec* b);
 // abi.cpp fft_host, under sh->mu: a contiguous batch-1 real forward / inverse.
 // 1: served into `out`; 0: not (take the ordinary path); < 0: error.
 int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* in, float* out);
-int batch_inverse(SharedServer* sh, int64_t n, const float* in, float* out);
+// inner: the FFT plan (null: serve only, never learn a spectral gain -- the
+// early path before the device guard)
+int batch_inverse(SharedServer* sh, crlot_plan* inner, int64_t n, const float* in, float* out);
 // ends the batch (a call it does not predict); an attached OLA object is
 // materialized first (objects.cpp ola_materialize_locked)
 int batch_abort(SharedServer* sh);

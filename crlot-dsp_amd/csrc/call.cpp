@@ -18,6 +18,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -213,6 +214,19 @@ int CallServer::stop() {
     return e == hipSuccess ? CRLOT_OK : hip_fail(e, "call server");
 }
 
+namespace {
+// crlot_test_inject(CRLOT_INJECT_CALL_TIMEOUT, k): the next k waits take the
+// timeout path at their first check (the request itself completes normally)
+std::atomic<int> g_timeout_inject{0};
+}  // namespace
+bool test_timeout_now() {
+    int v = g_timeout_inject.load(std::memory_order_relaxed);
+    while (v > 0)
+        if (g_timeout_inject.compare_exchange_weak(v, v - 1, std::memory_order_relaxed)) return true;
+    return false;
+}
+void test_inject_timeouts(int count) { g_timeout_inject.store(count, std::memory_order_relaxed); }
+
 int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
@@ -231,11 +245,13 @@ int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
             }
             const auto us =
                 std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
-            if (us > 5000000) {
+            if (us > 5000000 || test_timeout_now()) {
                 // the request is still in flight in the resident kernel: no later call
-                // may read a slot or speculation it could still write
+                // may read a slot or speculation it could still write -- until every
+                // request submitted so far has completed (submit re-checks)
                 broken_ = true;
-                return fail(CRLOT_EHIP, "call server: request timed out (server disabled)");
+                broken_at_ = q_;
+                return fail(CRLOT_EHIP, "call server: request timed out (server paused)");
             }
         }
         _mm_pause();
@@ -315,7 +331,11 @@ void CallServer::put(float* dst, const float* src, size_t n) {
 }
 
 int CallServer::submit(CallReq& r, const CallSlot& sl) {
-    if (broken_) return fail(CRLOT_EHIP, "call server: disabled after a timed-out request");
+    if (broken_) {  // a timed-out request: serve again once everything submitted has completed
+        if (done() < broken_at_) return fail(CRLOT_EHIP, "call server: a timed-out request is still in flight");
+        broken_ = false;
+        acquire_next_ = true;  // (the kernel's view of host memory is refreshed with the next request)
+    }
     r.in_off = sl.in_off;
     r.out_off = sl.out_off;
     r.spec_off = sl.spec_off;

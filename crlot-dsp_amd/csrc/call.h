@@ -89,7 +89,8 @@ class CallServer {
     size_t in_cap_ = 0, out_cap_ = 0, spec_cap_ = 0;
     uint64_t q_ = 0;                   // requests submitted
     uint64_t gen_ = 0;                 // arena generation (bumped by every allocation)
-    bool broken_ = false;              // a request timed out: the server refuses new work
+    bool broken_ = false;              // a request timed out: the server refuses new work ...
+    uint64_t broken_at_ = 0;           // ... until done() reaches the requests submitted by then
     std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
     uint64_t last_chain_ = 0;          // the last request with a chained produce
     CallReq::Pend pend_{};             // deferred ring work (flags 0: none)
@@ -146,6 +147,9 @@ struct SharedServer {
     ChainTarget target;     // the OLA object that pushed the last speculated inverse
     struct BatchSpec* batch = nullptr;  // batched speculation of the whole loop (batch.h)
 };
+// test-only (crlot_test_inject CRLOT_INJECT_CALL_TIMEOUT): the next k waits time out
+bool test_timeout_now();
+void test_inject_timeouts(int count);
 // the shared server of (device, e) (created on first use; never destroyed);
 // e < 0: the FFT-only server of complex size P = -e (any size, call_any_waves)
 SharedServer* shared_server(int device, int e, int* rc);

@@ -349,6 +349,10 @@ hipError_t launch_normalize_and_clear(float* out, int64_t ld_out, float* acc, in
 // products for the batched drop-in speculation (batch.cpp)
 hipError_t launch_windowed_frames(const float* x, int64_t T, const float* w, float* p, int64_t F, int64_t N,
                                   int64_t H, hipStream_t s);
+// out[k][2b + c] = spec[k][2b + c] * g[b] (k < rows, b < bins, rows ld floats apart):
+// a caller's per-bin real spectral gain (batch.cpp), one plain multiply
+hipError_t launch_bin_gain(const float* spec, float* out, const float* g, int64_t rows, int64_t ld, int64_t bins,
+                           hipStream_t s);
 // dsp::FrameQueue frames on the device: [stream][F][N] from x [stream][ld_x]
 hipError_t launch_fq_frames(const float* x, int64_t T, int64_t ld_x, int n_streams, float* frames, int64_t F,
                             int64_t N, int64_t H, int64_t pad, int pad_mode, hipStream_t s);

@@ -231,7 +231,33 @@ __global__ void __launch_bounds__(256) k_windowed_frames(const float* __restrict
     p[e] = (idx < T ? x[idx] : 0.0f) * w[j];
 }
 
+// ... and the spectral step a caller applies between forward and inverse when
+// it is a fixed real gain per bin (batch.cpp learns it): out[k][2b + c] =
+// spec[k][2b + c] * g[b], one plain multiply (std::complex<float> *= float).
+__global__ void __launch_bounds__(256) k_bin_gain(const float* __restrict__ spec, float* __restrict__ out,
+                                                  const float* __restrict__ g, int64_t rows, int64_t ld,
+                                                  int64_t bins) {
+    const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (e >= rows * bins) return;
+    const int64_t k = e / bins, b = e - k * bins;
+    const float gb = g[b];
+    const float2 v = *reinterpret_cast<const float2*>(spec + k * ld + 2 * b);
+    float2 o;
+    o.x = v.x * gb;
+    o.y = v.y * gb;
+    *reinterpret_cast<float2*>(out + k * ld + 2 * b) = o;
+}
+
 }  // namespace
+
+hipError_t launch_bin_gain(const float* spec, float* out, const float* g, int64_t rows, int64_t ld, int64_t bins,
+                           hipStream_t s) {
+    if (rows <= 0 || bins <= 0) return hipSuccess;
+    if (rows * bins > (int64_t(1) << 40) || (ld & 1)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bin_gain, dim3(unsigned((rows * bins + 255) / 256)), dim3(256), 0, s, spec, out, g, rows, ld,
+                       bins);
+    return hipGetLastError();
+}
 
 hipError_t launch_windowed_frames(const float* x, int64_t T, const float* w, float* p, int64_t F, int64_t N,
                                   int64_t H, hipStream_t s) {

@@ -122,6 +122,44 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(values, device=None) -> list:
+    """Every rank's list of floats, in rank order (an all-gather; one rank: [values])."""
+    import torch
+    import torch.distributed as dist
+    vals = [float(v) for v in values]
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [vals]
+    t = torch.tensor(vals, dtype=torch.float64, device=reduce_device(device))
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.cpu().tolist()] for o in out]
+
+
+STRAGGLER_RATIO = 1.25  # a rank this much slower than the median is named
+
+
+def rank_report(kernel_ms, wall_ms, device_keys) -> dict:
+    """Per-rank timings of a weak-scaling phase and who set the max: each rank's
+    device key, mean kernel time and wall time; the slowest rank by wall time, its
+    ratio to the median, and `stragglers` (ranks >= STRAGGLER_RATIO x the median
+    wall time, worst first) -- so a first multi-GPU run says which GPU held it back."""
+    n = len(wall_ms)
+    order = sorted(range(n), key=lambda r: wall_ms[r])
+    med = wall_ms[order[n // 2]] if n % 2 else 0.5 * (wall_ms[order[n // 2 - 1]] + wall_ms[order[n // 2]])
+    slow = order[-1]
+    ratio = (wall_ms[slow] / med) if med > 0 else 1.0
+    strag = sorted((r for r in range(n) if med > 0 and wall_ms[r] >= STRAGGLER_RATIO * med),
+                   key=lambda r: -wall_ms[r])
+    return {
+        "per_rank": [{"rank": r, "device_key": int(device_keys[r]) if r < len(device_keys) else None,
+                      "kernel_ms": round(float(kernel_ms[r]), 4), "wall_ms": round(float(wall_ms[r]), 4)}
+                     for r in range(n)],
+        "slowest_rank": slow,
+        "slowest_vs_median": round(ratio, 3),
+        "stragglers": strag,
+    }
+
+
 def finalize():
     import torch.distributed as dist
     if dist.is_initialized():
@@ -152,7 +190,8 @@ def _stop(procs, grace: float = 5.0):
 
 def launch(n: int, argv: list[str], timeout: float | None = None, poll_s: float = 0.1) -> int:
     """Run `python argv...` as n ranks on this node; returns 0 when every rank
-    succeeded, else the exit code of the first rank that failed.
+    succeeded, else the exit code of the first failure seen (ranks exiting in the
+    same poll interval: the lowest rank; a rank killed by signal k: 128 + k).
 
     All children are polled together: the first non-zero exit stops the other
     ranks at once (they would otherwise wait in a collective for the dead rank),
@@ -169,7 +208,9 @@ def launch(n: int, argv: list[str], timeout: float | None = None, poll_s: float 
             procs.append(subprocess.Popen([sys.executable] + argv, env=e))
         while True:
             codes = [p.poll() for p in procs]
-            bad = [c for c in codes if c not in (None, 0)]
+            # the first failure seen (in rank order within one poll); a rank killed by
+            # signal k (returncode -k) reports 128 + k, as a shell does
+            bad = [c if c > 0 else 128 - c for c in codes if c not in (None, 0)]
             if bad:
                 return bad[0]
             if all(c == 0 for c in codes):

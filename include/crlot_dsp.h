@@ -159,8 +159,11 @@ int crlot_call_speculation_stats(int64_t* out6);
  * batches transformed, [7] window continuations (a batch is bounded: at most
  * `window_frames` frames per chain, below; the next window starts at the
  * forward of the first frame past it), [8] speculations declined because a
- * buffer or launch failed (the call then took the ordinary path); entries past
- * the known ones are 0.  Negative: CRLOT_EINVAL. */
+ * buffer or launch failed (the call then took the ordinary path), [9] spectral
+ * gains learned (an inverse input that was the served spectrum times a fixed
+ * real gain per bin, bit for bit: the batch's remaining inverses are then those
+ * of the gained spectra, each still served only after a bitwise check); entries
+ * past the known ones are 0.  Negative: CRLOT_EINVAL. */
 int crlot_call_speculation_stats_ex(int64_t* out, int32_t count);
 /* Bounds of the batched speculation: frames per window, and the device and
  * pinned host bytes the batches hold now, with the pinned peak since load. */
@@ -168,9 +171,13 @@ int crlot_call_batch_capacity(int64_t* window_frames, int64_t* device_bytes, int
                               int64_t* pinned_peak);
 /* Test-only fault injection: CRLOT_INJECT_BATCH_ALLOC makes the next `count`
  * buffer allocations of the batched speculation fail (a speculation that cannot
- * allocate declines and the call takes its ordinary path).  Other `what`:
+ * allocate declines and the call takes its ordinary path);
+ * CRLOT_INJECT_CALL_TIMEOUT makes the next `count` waits on the resident call
+ * kernel take their timeout path (the call fails with CRLOT_EHIP; the server
+ * serves again once every request submitted before completed).  Other `what`:
  * CRLOT_EINVAL. */
 #define CRLOT_INJECT_BATCH_ALLOC 1
+#define CRLOT_INJECT_CALL_TIMEOUT 2
 int crlot_test_inject(int32_t what, int32_t count);
 /* What the plan's last call on `stream` launched: kernels in launch order
  * (CRLOT_K_* ids below; the first 8 are kept, n_kernels counts all), the

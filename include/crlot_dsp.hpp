@@ -327,6 +327,21 @@ T* AllocateAligned(size_t n) {
     return static_cast<T*>(p);
 }
 inline void DeallocateAligned(void* p) { std::free(p); }
+// std::allocator with 64-byte alignment (the window tables the reference hands
+// out are 32-byte aligned for its SIMD loads: window_lut_test.cc:285-330)
+template <typename T>
+struct AlignedAllocator {
+    using value_type = T;
+    AlignedAllocator() = default;
+    template <typename U>
+    AlignedAllocator(const AlignedAllocator<U>&) {}
+    T* allocate(size_t n) { return n ? AllocateAligned<T>(n) : nullptr; }
+    void deallocate(T* p, size_t) { DeallocateAligned(p); }
+    template <typename U>
+    bool operator==(const AlignedAllocator<U>&) const { return true; }
+    template <typename U>
+    bool operator!=(const AlignedAllocator<U>&) const { return false; }
+};
 }  // namespace base
 
 namespace ring {
@@ -413,7 +428,7 @@ enum class NormalizationType { NONE, SUM_TO_ONE, L2_NORM, OLA_UNITY_GAIN, OLA_SU
 // pointer valid until clearCache().  Tables are the reference's, bit-exact
 // (crlot_window_table, host code).
 struct WindowData {
-    std::vector<float> values;
+    std::vector<float, base::AlignedAllocator<float>> values;  // 64-byte aligned
     size_t size = 0;
     WindowType type = WindowType::HANN;
     bool periodic = false;

@@ -884,9 +884,29 @@ long or_roundtrip(const float* x, size_t T, size_t n, size_t h, int wtype, int p
                            spec_out);
 }
 
+static long or_roundtrip_impl(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
+                              int framing, int center, int pad_mode, int analysis_window, const float* bin_gain,
+                              float* y, size_t y_cap, float* frames_out, float* spec_out);
+
 long or_roundtrip_ex(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
                      int framing, int center, int pad_mode, int analysis_window, float* y,
                      size_t y_cap, float* frames_out, float* spec_out) {
+    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, center, pad_mode, analysis_window, NULL, y,
+                             y_cap, frames_out, spec_out);
+}
+
+/* The same loop with a spectral step where e2e_benchmark.cc:161-162 puts one
+ * ("filtering or other processing could go here"): every bin of each frame's
+ * spectrum scaled by bin_gain[k] (n/2+1 real gains; re and im multiplied, as a
+ * caller editing the interleaved complex spectrum on the host would). */
+long or_roundtrip_gain(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic, int framing,
+                       const float* bin_gain, float* y, size_t y_cap) {
+    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, 0, 0, 1, bin_gain, y, y_cap, NULL, NULL);
+}
+
+static long or_roundtrip_impl(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
+                              int framing, int center, int pad_mode, int analysis_window, const float* bin_gain,
+                              float* y, size_t y_cap, float* frames_out, float* spec_out) {
     if (n == 0 || h == 0 || (n & 1)) return -1;
     if (framing < 0 || framing > 2) return -3;
     float* w = (float*)malloc(sizeof(float) * n);
@@ -924,6 +944,11 @@ long or_roundtrip_ex(const float* x, size_t T, size_t n, size_t h, int wtype, in
         for (size_t i = 0; i < n; ++i) /* e2e_benchmark.cc:154-156 (analysis window) */
             proc[i] = analysis_window ? frame[i] * w[i] : frame[i];
         or_adapter_forward(fwd, (int)n, proc, spec);
+        if (bin_gain)
+            for (size_t b = 0; b <= n / 2; ++b) {
+                spec[2 * b] *= bin_gain[b];
+                spec[2 * b + 1] *= bin_gain[b];
+            }
         if (spec_out) memcpy(spec_out + k * (n + 2), spec, sizeof(float) * (n + 2));
         or_adapter_inverse(inv, (int)n, spec, proc);
         if (frames_out) memcpy(frames_out + k * n, proc, sizeof(float) * n);

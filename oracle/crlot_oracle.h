@@ -143,6 +143,10 @@ size_t or_fq_frames(const float* x, size_t T, size_t frame_size, size_t hop, int
 long or_roundtrip_ex(const float* x, size_t T, size_t frame_size, size_t hop, int window_type,
                      int periodic, int framing, int center, int pad_mode, int analysis_window,
                      float* y, size_t y_cap, float* frames_out, float* spec_out);
+/* or_roundtrip with a per-bin real gain applied to every frame's spectrum
+ * between the transforms (the spectral step of e2e_benchmark.cc:161-162). */
+long or_roundtrip_gain(const float* x, size_t T, size_t n, size_t h, int window_type, int periodic, int framing,
+                       const float* bin_gain, float* y, size_t y_cap);
 long or_roundtrip_batch_ex(const float* x, size_t n_streams, size_t T, size_t ld_x,
                            size_t frame_size, size_t hop, int window_type, int periodic,
                            int framing, int center, int pad_mode, int analysis_window, float* y,

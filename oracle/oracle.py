@@ -118,6 +118,8 @@ def lib(native: bool = False):
     L.or_roundtrip_ex.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, _f32p, sz, C.c_void_p, C.c_void_p]
     L.or_roundtrip_ex.restype = C.c_long
+    L.or_roundtrip_gain.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, C.c_void_p, _f32p, sz]
+    L.or_roundtrip_gain.restype = C.c_long
     L.or_roundtrip_batch_ex.argtypes = [_f32p, sz, sz, sz, sz, sz, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, C.c_int, _f32p, sz, C.c_int]
     L.or_roundtrip_batch_ex.restype = C.c_long
@@ -451,6 +453,22 @@ def roundtrip_ex(x, n, h, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT, ana
         raise ValueError(f"or_roundtrip_ex rc={r}")
     assert r == F, (r, F)
     return (y[:F * h], frames[:F]) if want_frames else y[:F * h]
+
+
+def roundtrip_gain(x, n, h, bin_gain, mode=ZERO_PAD, wtype=HANN, periodic=False):
+    """or_roundtrip_gain: the e2e loop with every spectrum bin k scaled by
+    bin_gain[k] (n/2+1 real gains) between forward and inverse."""
+    x = np.ascontiguousarray(x, np.float32)
+    g = np.ascontiguousarray(bin_gain, np.float32)
+    assert g.size == n // 2 + 1
+    T = x.size
+    F = frames_for(T, n, h, mode, True)
+    y = np.zeros(max(F * h, 1), np.float32)
+    r = lib().or_roundtrip_gain(x if T else np.zeros(1, np.float32), T, n, h, wtype, int(periodic), mode,
+                                g.ctypes.data, y, F * h)
+    if r < 0:
+        raise ValueError(f"or_roundtrip_gain rc={r}")
+    return y[:F * h]
 
 
 def roundtrip_batch_ex(x2d, n, h, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT,

@@ -53,9 +53,22 @@ def loop_hist(asm, pat):
     return m.group(1), c
 
 
+def src_hash() -> str:
+    """bench.py's src_hash: the kernel sources and the Makefile (the histogram
+    describes that build only)."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h")) +
+                    [os.path.join(CSRC, "Makefile")]):
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
-    out = {"tag": tag, "note": "main loop = the longest backward branch span of the kernel; "
+    out = {"tag": tag, "src_hash": src_hash(), "note": "main loop = the longest backward branch span of the kernel; "
            "counts are static instructions in it (every one issues once per iteration), except the "
            "exact sanitize test inside the frexp_min_if asm blocks, which runs only when the output "
            "screen fails (loop_valu_fallback_skipped, not in loop_valu)", "kernels": []}

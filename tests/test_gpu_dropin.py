@@ -1014,3 +1014,144 @@ def test_batched_loop_declines_when_allocation_fails(pkg, oracle, torch_cuda, n,
         assert served["batches"] == 1 and served["forwards"] == a[1] - 1, served
     else:
         assert served["batches"] == 0 and served["forwards"] == 0, served
+
+
+@pytest.mark.gpu
+def test_call_server_recovers_after_a_timed_out_request(pkg, oracle, torch_cuda):
+    """a request that times out used to disable its (device, size)
+    server for the rest of the process.  The timeout path (injected: the wait
+    gives up at once while the request completes normally) fails that call
+    loudly; once every request submitted before has completed, the server serves
+    again, with the right bits."""
+    import time
+    n = 1024
+    rng = np.random.default_rng(77)
+    x = rng.standard_normal((1, n)).astype(np.float32)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    try:
+        pkg.set_call_speculation(1)
+        ref = np.asarray(fft.forward_host(x)).copy()
+        pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 1)
+        with pytest.raises(Exception):
+            fft.forward_host(x)
+        time.sleep(0.05)  # the timed-out request finishes on the device
+        again = np.asarray(fft.forward_host(x)).copy()
+        inv = fft.inverse_host(again)[0]
+    finally:
+        pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 0)
+        pkg.set_call_speculation(2)
+        fft.close()
+    assert np.array_equal(bits(again), bits(ref))
+    assert np.allclose(inv / n, x[0], atol=1e-5)
+
+
+def _e2e_gain_loop(pkg, x, n, h, g):
+    """The e2e loop with a spectral step on the host: every bin of each spectrum
+    scaled by g[k] between forward and inverse (e2e_benchmark.cc:161-162)."""
+    w = pkg.window_table(pkg.HANN, n)
+    fr = pkg.Framer()
+    fr.set_params(n, h, 1, pkg.ZERO_PAD)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                                           apply_window_inside=True))
+    ola.set_window(w)
+    fr.push(x)
+    outs, k = [], 0
+    while True:
+        f = fr.pop()
+        if f is None:
+            break
+        X = np.asarray(fft.forward_host((f * w).astype(np.float32)[None])).copy()
+        X[0].real *= g
+        X[0].imag *= g
+        y = fft.inverse_host(X)[0]
+        ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+        got, chans = ola.produce(h)
+        outs.append(chans[0][:got].copy())
+        k += 1
+    ola.close()
+    fft.close()
+    fr.close()
+    return np.concatenate(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h", [(1024, 256), (960, 240)])
+def test_e2e_loop_with_host_spectral_gain(pkg, oracle, torch_cuda, n, h):
+    """A real spectral step in the per-frame loop (bench --suite e2e's
+    spectral_gain row): the caller scales every bin on the host between forward
+    and inverse.  The batch learns the fixed per-bin gain from the first edited
+    inverse input (bit for bit: input == spectrum * g), redoes its inverses with
+    it, and serves every call; the result is the per-call path's bits, and both
+    match the oracle's loop with the same gain within the FFT tolerance."""
+    x = oracle.synth(48_000, 21)
+    g = (0.5 + 0.5 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2))).astype(np.float32)
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_gain_loop(pkg, x, n, h, g)
+        pkg.set_call_speculation(2)
+        b, served = _spec_delta(pkg, lambda: _e2e_gain_loop(pkg, x, n, h, g))
+    finally:
+        pkg.set_call_speculation(2)
+    assert np.array_equal(bits(a), bits(b))
+    ref = oracle.roundtrip_gain(x, n, h, g)
+    assert a.shape == ref.shape
+    d = (a.astype(np.float64) - ref)
+    assert np.linalg.norm(d) <= 1e-6 * max(np.linalg.norm(ref), np.linalg.norm(x))  # the parity bar (DESIGN 4)
+    assert np.abs(d).max() <= 4e-6 * np.abs(x).max()
+    F = a.size // h
+    assert served["gains"] == 1 and served["batches"] == 1 and served["rebuilds"] == 0, served
+    assert served["inverses"] == F and served["pushes"] == F and served["produces"] == F, served
+
+
+@pytest.mark.gpu
+def test_e2e_loop_gain_changes_midstream(pkg, oracle, torch_cuda):
+    """The spectral gain changes half-way (another fixed gain) and, in a second
+    run, turns into an edit that is no per-bin real gain (one bin rotated): the
+    batch relearns or falls back, and every call keeps the per-call path's bits."""
+    n, h = 1024, 256
+    x = oracle.synth(48_000 * 3, 23)
+    g1 = (0.5 + 0.5 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2))).astype(np.float32)
+    g2 = np.linspace(1.5, 0.25, n // 2 + 1).astype(np.float32)
+
+    def run(kind):
+        w = pkg.window_table(pkg.HANN, n)
+        fr = pkg.Framer()
+        fr.set_params(n, h, 1, pkg.ZERO_PAD)
+        fft = pkg.FftPlan(n, pkg.FFT_REAL)
+        ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                                               apply_window_inside=True))
+        ola.set_window(w)
+        fr.push(x)
+        outs, k = [], 0
+        while True:
+            f = fr.pop()
+            if f is None:
+                break
+            X = np.asarray(fft.forward_host((f * w).astype(np.float32)[None])).copy()
+            g = g1 if k < 300 else g2
+            X[0].real *= g
+            X[0].imag *= g
+            if kind == "rotate" and k >= 300:
+                X[0][5] = X[0][5] * np.complex64(1j)
+            y = fft.inverse_host(X)[0]
+            ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+            got, chans = ola.produce(h)
+            outs.append(chans[0][:got].copy())
+            k += 1
+        ola.close()
+        fft.close()
+        fr.close()
+        return np.concatenate(outs)
+
+    for kind in ("regain", "rotate"):
+        try:
+            pkg.set_call_speculation(1)
+            a = run(kind)
+            pkg.set_call_speculation(2)
+            b, served = _spec_delta(pkg, lambda: run(kind))
+        finally:
+            pkg.set_call_speculation(2)
+        assert np.array_equal(bits(a), bits(b)), kind
+        if kind == "regain":
+            assert served["gains"] == 2, served

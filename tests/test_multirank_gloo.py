@@ -190,3 +190,52 @@ def test_observed_world_counts_ranks_and_devices(tmp_path):
         o = json.load(open(tmp_path / f"obs_{r}.json"))
         assert o["world"] == 2 and o["backend"] == "gloo" and o["devices"] == 2, o
         assert o["device_keys"] == [0, 1], o
+
+
+SLOW_WORKER = r'''
+import os, sys, json, time
+import importlib.util
+spec = importlib.util.spec_from_file_location("crlot_dist", os.path.join(ROOT, "crlot-dsp_amd", "dist.py"))
+D = importlib.util.module_from_spec(spec); spec.loader.exec_module(D)
+rank, world = D.init("gloo")
+D.barrier()
+t0 = time.perf_counter()
+time.sleep(0.2 * (3.0 if rank == SLOW else 1.0))   # rank SLOW is 3x slower
+own_ms = (time.perf_counter() - t0) * 1e3
+D.barrier()
+per = D.gather_over_ranks([own_ms * 0.9, own_ms])   # (kernel ms, wall ms) as bench.py reports them
+rep = D.rank_report([p[0] for p in per], [p[1] for p in per], [100 + r for r in range(world)])
+json.dump(rep, open(os.path.join(OUT, f"rep_{rank}.json"), "w"))
+D.finalize()
+'''
+
+
+def test_slow_rank_is_named_gloo(tmp_path):
+    """bench.py's ranks_report (dist.rank_report over an all-gather): with one of
+    three ranks made 3x slower, every rank's report names it as the slowest and as
+    a straggler, with its device key and times."""
+    import json
+    world, slow = 3, 1
+    script = tmp_path / "worker.py"
+    script.write_text(f"ROOT = {ROOT!r}\nOUT = {str(tmp_path)!r}\nSLOW = {slow}\n" + SLOW_WORKER)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world))
+    procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(world)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    reps = [json.load(open(tmp_path / f"rep_{r}.json")) for r in range(world)]
+    assert all(r == reps[0] for r in reps)
+    rep = reps[0]
+    assert rep["slowest_rank"] == slow and rep["stragglers"] == [slow], rep
+    assert 2.5 <= rep["slowest_vs_median"] <= 3.5, rep
+    assert [e["device_key"] for e in rep["per_rank"]] == [100, 101, 102]
+    assert rep["per_rank"][slow]["wall_ms"] > 2.5 * rep["per_rank"][0]["wall_ms"]
+
+
+def test_launch_reports_signal_exit_as_128_plus_signal(tmp_path):
+    """dist.launch: a rank killed by a signal (returncode -k) reports 128 + k."""
+    D = _load_dist()
+    script = tmp_path / "die.py"
+    script.write_text("import os, signal\nif os.environ['RANK'] == '1':\n    os.kill(os.getpid(), signal.SIGKILL)\n"
+                      "import time\ntime.sleep(30)\n")
+    assert D.launch(2, [str(script)], timeout=60) == 128 + 9
