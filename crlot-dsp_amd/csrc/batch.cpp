@@ -640,6 +640,10 @@ bool learn_gain(const BatchSpec* b, int64_t j, const float* Y, std::vector<float
     for (size_t k = 0; k < bins; ++k) {
         const float xr = X[2 * k], xi = X[2 * k + 1], yr = Y[2 * k], yi = Y[2 * k + 1];
         float q = b->sgain.size() == bins ? b->sgain[k] : 1.0f;
+        if (same(xr * q, yr) && same(xi * q, yi)) {  // one frame need not pin a gain: keep the one
+            (*g)[k] = q;                              // that reproduces the earlier frames too
+            continue;
+        }
         if (xr != 0.0f)
             q = yr / xr;
         else if (xi != 0.0f)
@@ -663,9 +667,13 @@ bool learn_gain(const BatchSpec* b, int64_t j, const float* Y, std::vector<float
 int apply_gain(BatchSpec* b, crlot_plan* inner, int64_t j) {
     const size_t N = size_t(b->n), row = N + 2, bins = N / 2 + 1, F = size_t(b->we - j);
     hipError_t e;
+    // the spectra as served (h_spec): the fused zero-copy chain wrote them to the
+    // mapped host block only, so d_spec's rows may be stale
+    float* spec = b->d_spec + b->row(j) * row;
     if ((e = dgrow(&b->d_sgain, &b->c_sgain, bins)) || (e = dgrow(&b->d_specg, &b->c_specg, b->rows_cap * row)) ||
+        (e = hipMemcpyAsync(spec, b->h_spec + b->row(j) * row, sizeof(float) * F * row, hipMemcpyHostToDevice, b->s)) ||
         (e = hipMemcpyAsync(b->d_sgain, b->sgain.data(), sizeof(float) * bins, hipMemcpyHostToDevice, b->s)) ||
-        (e = launch_bin_gain(b->d_spec + b->row(j) * row, b->d_specg, b->d_sgain, int64_t(F), int64_t(row),
+        (e = launch_bin_gain(spec, b->d_specg, b->d_sgain, int64_t(F), int64_t(row),
                              int64_t(bins), b->s)))
         return hip_fail(e, "batch spectral gain");
     float* r_dev = b->d_r + b->row(j) * N;

@@ -228,6 +228,11 @@ bool test_timeout_now() {
 void test_inject_timeouts(int count) { g_timeout_inject.store(count, std::memory_order_relaxed); }
 
 int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
+    if (test_timeout_now()) {  // (test-only: the timeout path below, taken at once)
+        broken_ = true;
+        broken_at_ = q_;
+        return fail(CRLOT_EHIP, "call server: request timed out (server paused)");
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t spin = 0;; ++spin) {
         if (load_acq(ctr) >= target) return CRLOT_OK;
@@ -245,7 +250,7 @@ int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
             }
             const auto us =
                 std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
-            if (us > 5000000 || test_timeout_now()) {
+            if (us > 5000000) {
                 // the request is still in flight in the resident kernel: no later call
                 // may read a slot or speculation it could still write -- until every
                 // request submitted so far has completed (submit re-checks)
