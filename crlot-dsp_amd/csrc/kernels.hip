@@ -441,7 +441,6 @@ __global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const Fuse
         dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
-    const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
     dev::Pair512TwReg tw;
@@ -450,7 +449,7 @@ __global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const Fuse
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         wa[m] = a.t.wa[lane + 64 * m];
-        ws[m] = a.t.wsn[lane + 64 * m];
+        ws[m] = a.t.wsn[lane + 64 * m] * a.gain;  // (ws g: ola_pair.h ola_pair_push_w)
     }
 
     float xin[E + SH];
@@ -472,7 +471,7 @@ __global__ __launch_bounds__(64 * kP512Waves) void k_stft_ola_pair512(const Fuse
             const float x = imag ? v[m].y : v[m].x;
             const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
             float& r = acc[m / SH][m % SH];
-            r = __builtin_fmaf(__builtin_fmaf(o, ws[m], 0.0f), g, r);
+            r = __builtin_fmaf(o, ws[m], r);  // (ws g: the hot walker's ola_pair_push_w)
         }
     };
     auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
@@ -626,7 +625,6 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
         dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
-    const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
     dev::Pair4kTwFor<SH, HAS_GAIN> tw;
@@ -635,7 +633,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         wa[m] = a.t.wa[t + 256 * m];
-        ws[m] = a.t.wsn[t + 256 * m];
+        ws[m] = a.t.wsn[t + 256 * m] * a.gain;  // (ws g: ola_pair.h ola_pair_push_w)
     }
 
     // xin[h*SH + q]: hop (k + h), h = 0..NB; bit h of hopok: hop k + h keeps the paired regime
@@ -658,7 +656,7 @@ __global__ __launch_bounds__(256, 2) void k_stft_ola_pair4k(const FusedArgs a) {
             const float x = imag ? v[m].y : v[m].x;
             const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
             float& r = acc[m / SH][m % SH];
-            r = __builtin_fmaf(__builtin_fmaf(o, ws[m], 0.0f), g, r);
+            r = __builtin_fmaf(o, ws[m], r);  // (ws g: the hot walker's ola_pair_push_w)
         }
     };
     auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift
@@ -778,7 +776,7 @@ __device__ __forceinline__ void load_den2k(float (&dr)[2 * SH], __amdgpu_buffer_
 constexpr size_t kPair2kLds = sizeof(cf) * (dev::kP2Xbuf + 2 * dev::kP2Tbuf);
 
 template <int SH, int NB, bool HAS_GAIN>
-__global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
+__global__ __launch_bounds__(128, 2) void k_stft_ola_pair2k(const FusedArgs a) {
     constexpr int E = 16, N = 2048, H = 128 * SH;
     static_assert(NB * SH == E, "N = NB * H");
     static_assert(SH >= 2, "den rows are read 16 bytes at a time");
@@ -800,7 +798,6 @@ __global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
         dev::make_rsrc(a.y + int64_t(s) * a.ld_y, uint32_t(a.out_len) * 4u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
-    const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
     dev::Pair2kTwFor<SH, HAS_GAIN> tw;
@@ -809,7 +806,7 @@ __global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         wa[m] = a.t.wa[t + 128 * m];
-        ws[m] = a.t.wsn[t + 128 * m];
+        ws[m] = a.t.wsn[t + 128 * m] * a.gain;  // (ws g: ola_pair.h ola_pair_push_w)
     }
 
     // xin[h*SH + q]: hop (k + h), h = 0..NB; bit h of hopok: hop k + h keeps the paired regime
@@ -832,7 +829,7 @@ __global__ __launch_bounds__(128) void k_stft_ola_pair2k(const FusedArgs a) {
             const float x = imag ? v[m].y : v[m].x;
             const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
             float& r = acc[m / SH][m % SH];
-            r = __builtin_fmaf(__builtin_fmaf(o, ws[m], 0.0f), g, r);
+            r = __builtin_fmaf(o, ws[m], r);  // (ws g: the hot walker's ola_pair_push_w)
         }
     };
     auto emit = [&](int k, const float (&dr)[2 * SH]) {  // produce(H) of block k, then shift

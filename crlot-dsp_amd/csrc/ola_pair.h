@@ -58,6 +58,41 @@ __device__ __forceinline__ void ola_pair_open(dev::pc (&acc2)[NB / 2][SH], const
     for (int m = (NB - 1) * SH; m < E; ++m) acc2[B0 / 2][m % SH][0] = __builtin_fmaf(v[m].y, g, 0.0f);
 }
 
+// steps 1-3 and 5 with the synthesis window and the OLA gain folded into the
+// adds: acc = fma(v, ws[m] g, acc), one rounding where push_frame_AoS has two
+// (fma(fma(o, w, 0), g, acc)); the walkers stage ws * g (exactly ws when g = 1)
+// and every walker of the kernel uses this form, so their bits still agree
+template <int E, int SH, int NB, int B0>
+__device__ __forceinline__ void ola_pair_push_w(dev::pc (&acc2)[NB / 2][SH], const dev::pc (&v)[E],
+                                                const float (&wg)[E]) {
+    static_assert(NB % 2 == 0 && B0 % 2 == 0 && NB * SH == E, "block pairs");
+#pragma unroll
+    for (int m = 0; m < E; ++m)
+        if ((m / SH) % 2 == 1) {
+            const int b = (B0 + m / SH) % NB;
+            acc2[b / 2][m % SH][b % 2] =
+                __builtin_fmaf(v[m].x, wg[m], m / SH == NB - 1 ? 0.0f : acc2[b / 2][m % SH][b % 2]);
+        }
+#pragma unroll
+    for (int m = 0; m < E; ++m)
+        if ((m / SH) % 2 == 0) {
+            dev::pc& r = acc2[((B0 + m / SH) % NB) / 2][m % SH];
+            r = __builtin_elementwise_fma(v[m], dev::pc{wg[m], wg[m]}, r);
+        }
+#pragma unroll
+    for (int m = 0; m < E; ++m)
+        if ((m / SH) % 2 == 1 && m / SH != NB - 1) {
+            const int b = (B0 + 1 + m / SH) % NB;
+            acc2[b / 2][m % SH][b % 2] = __builtin_fmaf(v[m].y, wg[m], acc2[b / 2][m % SH][b % 2]);
+        }
+}
+template <int E, int SH, int NB, int B0>
+__device__ __forceinline__ void ola_pair_open_w(dev::pc (&acc2)[NB / 2][SH], const dev::pc (&v)[E],
+                                                const float (&wg)[E]) {
+#pragma unroll
+    for (int m = (NB - 1) * SH; m < E; ++m) acc2[B0 / 2][m % SH][0] = __builtin_fmaf(v[m].y, wg[m], 0.0f);
+}
+
 // {den, rden} of blocks k and k+1 as register pairs (DevTables::pden2 rows of L lanes)
 template <int L, int SH>
 __device__ __forceinline__ void load_den_pair(dev::pc (&d2)[SH], dev::pc (&r2)[SH], __amdgpu_buffer_rsrc_t rp2,

@@ -110,6 +110,13 @@ struct PairRot {
     static_assert(R >= NB + 3 && (2 * U) % NB == 0, "ring");
 };
 
+// the synthesis window and gain folded into the OLA adds (ola_pair.h
+// ola_pair_push_w: +1.9 % at H = 256, +1.4 % at H = 512) except at H = 128, where
+// the 16 live window values double the walk's spills (-5.6 %): there the window
+// product and fma(., g, acc) stay separate.  Both walkers follow the same choice.
+template <int SH>
+constexpr bool kPairFoldWs = SH != 2;
+
 template <int SH, int NB, int W, bool ILV, bool HAS_GAIN>
 __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(const FusedArgs a) {
     constexpr int E = 16, N = 1024, H = 64 * SH;
@@ -128,7 +135,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             const int l = i & 63, m = i >> 6;  // tap n = l + 64 m
             const int d = (m >> 2) * 256 + l * 4 + (m & 3);
             wa4[d] = a.t.wa[i];
-            ws4[d] = a.t.wsn[i];
+            ws4[d] = kPairFoldWs<SH> ? a.t.wsn[i] * a.gain : a.t.wsn[i];  // (ws g: ola_pair.h ola_pair_push_w)
         }
         __syncthreads();
     }
@@ -186,7 +193,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
 #endif
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
-    const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
     // XR(slot, q): sample lane + 64 q of the hop in that slot; bit j of hopok:
@@ -313,12 +319,17 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int m = 4 * m4 + u, s = (S0 + m / SH) % R;
+#ifdef CRLOT_ABL_NOANAWIN  // timing-only ablation: wrong results
+                    (void)wv;
+                    v[m] = dev::pc_mk(XR(s, m % SH), XR((s + 1) % R, m % SH));
+#else
 #if CRLOT_PAIR_PKX
                     if ((m / SH) % 2 == 0)  // hops k + 2i, k + 2i + 1 share a register pair
                         v[m] = xr2[s / 2][m % SH] * dev::pc{wv[u], wv[u]};
                     else
 #endif
                         v[m] = dev::pc_mk(XR(s, m % SH) * wv[u], XR((s + 1) % R, m % SH) * wv[u]);
+#endif
                 }
             }
             // (frame k+1 = F past the last frame of an odd count still transforms
@@ -347,7 +358,8 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
             // one such value sends the walk to k_stft_ola_pair_fix (a value in
             // [1e-30 N, 2^-89) too, harmlessly), otherwise the sanitize is the identity.
             static_assert(N == 1024, "threshold exponent");
-#if CRLOT_PAIR_OSCREEN  // (the same test, screened: fft_pair.h)
+#if defined(CRLOT_ABL_NOOSAN)  // timing-only ablation
+#elif CRLOT_PAIR_OSCREEN  // (the same test, screened: fft_pair.h)
             bad |= dev::out_min_exp_screened<E>(v, 0x1p-89f) <= -89;
 #else
             {
@@ -358,34 +370,42 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
                 bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -89;
             }
 #endif
-            // push_frame_AoS of both frames: fma(fma(o, w, 0), g, acc), the window
-            // product of both parts in one packed multiply (v * (w, w) gives -0
-            // only where fma(o, w, 0) gives +0, and fma(-0, g, acc) == fma(+0, g, acc))
+            // push_frame_AoS of both frames with the window and gain folded into
+            // the adds, fma(v, ws g, acc) (ola_pair.h ola_pair_push_w); at H = 128
+            // fma(fma(o, w, 0), g, acc) with the window product of both parts in one
+            // packed multiply (v * (w, w) gives -0 only where fma(o, w, 0) gives +0,
+            // and fma(-0, g, acc) == fma(+0, g, acc)) and wg = g
+            float wg[E];
 #pragma unroll
             for (int m4 = 0; m4 < E / 4; ++m4) {
-                const dev::pc* w2 = reinterpret_cast<const dev::pc*>(ws4 + m4 * 256 + lane * 4);
-                const dev::pc wl = w2[0], wh = w2[1];
-                v[4 * m4 + 0] = v[4 * m4 + 0] * dev::pc{wl.x, wl.x};
-                v[4 * m4 + 1] = v[4 * m4 + 1] * dev::pc{wl.y, wl.y};
-                v[4 * m4 + 2] = v[4 * m4 + 2] * dev::pc{wh.x, wh.x};
-                v[4 * m4 + 3] = v[4 * m4 + 3] * dev::pc{wh.y, wh.y};
+                const float4 w = *reinterpret_cast<const float4*>(ws4 + m4 * 256 + lane * 4);
+                const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if constexpr (kPairFoldWs<SH>) {
+                        wg[4 * m4 + u] = wv[u];
+                    } else {
+                        v[4 * m4 + u] = v[4 * m4 + u] * dev::pc{wv[u], wv[u]};
+                        wg[4 * m4 + u] = a.gain;
+                    }
+                }
             }
 #if CRLOT_PAIR_PKA
             // (ola_pair.h: both frames' adds, then the produce of blocks k and k+1)
-            ola_pair_push<E, SH, NB, B0>(acc2, v, g);
+            ola_pair_push_w<E, SH, NB, B0>(acc2, v, wg);
             {
                 float o0[SH], o1[SH];
                 bad |= !mk_div_pair<SH>(acc2[B0 / 2], d2, r2, o0, o1);
                 store_block(k, o0);
                 store_block(k + 1 < f1 ? k + 1 : -1, o1);  // (past the chunk when k+1 == f1)
             }
-            ola_pair_open<E, SH, NB, B0>(acc2, v, g);
+            ola_pair_open_w<E, SH, NB, B0>(acc2, v, wg);
 #else
             // frame k -> blocks k .. k+NB-1 (the last opens), produce block k
 #pragma unroll
             for (int m = 0; m < E; ++m) {
                 CRLOT_ACC((B0 + m / SH) % NB, m % SH) =
-                    __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : CRLOT_ACC((B0 + m / SH) % NB, m % SH));
+                    __builtin_fmaf(v[m].x, wg[m], m / SH == NB - 1 ? 0.0f : CRLOT_ACC((B0 + m / SH) % NB, m % SH));
             }
             emit(B0, k, dr0);
             // frame k+1 -> blocks k+1 .. k+NB (k+NB opens in acc[B0]), produce block k+1
@@ -393,7 +413,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair(
 #pragma unroll
             for (int m = 0; m < E; ++m) {
                 CRLOT_ACC((B0 + 1 + m / SH) % NB, m % SH) =
-                    __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : CRLOT_ACC((B0 + 1 + m / SH) % NB, m % SH));
+                    __builtin_fmaf(v[m].y, wg[m], m / SH == NB - 1 ? 0.0f : CRLOT_ACC((B0 + 1 + m / SH) % NB, m % SH));
             }
             emit((B0 + 1) % NB, k + 1 < f1 ? k + 1 : -1, dr1);
 #endif
@@ -504,7 +524,7 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
             const int l = i & 63, m = i >> 6;  // tap n = l + 64 m
             const int d = (m >> 2) * 256 + l * 4 + (m & 3);
             wa4[d] = a.t.wa[i];
-            ws4[d] = a.t.wsn[i];
+            ws4[d] = kPairFoldWs<SH> ? a.t.wsn[i] * a.gain : a.t.wsn[i];  // (ws g: ola_pair.h ola_pair_push_w)
         }
         __syncthreads();
     }
@@ -549,7 +569,6 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
     };
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
-    const float g = a.gain;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
 
     for (int r = 0; r < 2; ++r) {
@@ -584,7 +603,10 @@ __global__ __launch_bounds__(64 * W, CRLOT_PAIR_MIN_WAVES) void k_stft_ola_pair_
                 const float x = imag ? v[m].y : v[m].x;
                 const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
                 float& r = acc[m / SH][m % SH];
-                r = __builtin_fmaf(__builtin_fmaf(o, wv[u], 0.0f), g, r);
+                if constexpr (kPairFoldWs<SH>)
+                    r = __builtin_fmaf(o, wv[u], r);  // (ws g staged: ola_pair.h ola_pair_push_w)
+                else
+                    r = __builtin_fmaf(__builtin_fmaf(o, wv[u], 0.0f), a.gain, r);
             }
         }
     };

@@ -257,7 +257,6 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #else
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden4, uint32_t(a.ring_blocks * H) * 8u);
 #endif
-    const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
     typename G::template Tw<SH, HAS_GAIN> tw;
@@ -266,7 +265,7 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         wa[m] = a.t.wa[t + L * m];
-        ws[m] = a.t.wsn[t + L * m];
+        ws[m] = a.t.wsn[t + L * m] * a.gain;  // (ws g: ola_pair.h ola_pair_push_w)
     }
     // spectral gain of this lane's bins (the two-regime walker's operation), in registers
     float gr[HAS_GAIN ? E : 1];
@@ -373,28 +372,27 @@ __global__ __launch_bounds__(G::L) __attribute__((amdgpu_waves_per_eu(2, 2))) vo
             bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= G::MIN_EXP;
         }
 #endif
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
+        // push_frame_AoS of both frames, window and gain folded into the adds
 #if CRLOT_HOT_PK
-        ola_pair_push<E, SH, NB, B0>(acc2, v, g);
+        ola_pair_push_w<E, SH, NB, B0>(acc2, v, ws);
         {
             float o0[SH], o1[SH];
             bad |= !mk_div_pair<SH>(acc2[B0 / 2], d2, r2, o0, o1);
             store_block(k, o0);
             store_block(k + 1 < f1 ? k + 1 : -1, o1);
         }
-        ola_pair_open<E, SH, NB, B0>(acc2, v, g);
+        ola_pair_open_w<E, SH, NB, B0>(acc2, v, ws);
 #else
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + m / SH) % NB][m % SH];
-            r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
+            r = __builtin_fmaf(v[m].x, ws[m], m / SH == NB - 1 ? 0.0f : r);
         }
         emit(acc[B0], k, dr0);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
-            r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
+            r = __builtin_fmaf(v[m].y, ws[m], m / SH == NB - 1 ? 0.0f : r);
         }
         emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
 #endif
@@ -488,7 +486,6 @@ __global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) { 
 #else
     const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
 #endif
-    const float g = a.gain;
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
     dev::Pair512TwReg tw;
@@ -497,7 +494,7 @@ __global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) { 
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         wa[m] = a.t.wa[lane + 64 * m];
-        ws[m] = a.t.wsn[lane + 64 * m];
+        ws[m] = a.t.wsn[lane + 64 * m] * a.gain;  // (ws g: ola_pair.h ola_pair_push_w)
     }
     bool bad = false;
     auto hop_check = [&](const float (&h)[SH]) {
@@ -583,28 +580,27 @@ __global__ __launch_bounds__(64 * W, 4) void k_pair512_hot(const FusedArgs a) { 
             bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -90;
         }
 #endif
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{ws[m], ws[m]};
+        // push_frame_AoS of both frames, window and gain folded into the adds
 #if CRLOT_HOT_PK
-        ola_pair_push<E, SH, NB, B0>(acc2, v, g);
+        ola_pair_push_w<E, SH, NB, B0>(acc2, v, ws);
         {
             float o0[SH], o1[SH];
             bad |= !mk_div_pair<SH>(acc2[B0 / 2], d2, r2, o0, o1);
             store_block(k, o0);
             store_block(k + 1 < f1 ? k + 1 : -1, o1);
         }
-        ola_pair_open<E, SH, NB, B0>(acc2, v, g);
+        ola_pair_open_w<E, SH, NB, B0>(acc2, v, ws);
 #else
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + m / SH) % NB][m % SH];
-            r = __builtin_fmaf(v[m].x, g, m / SH == NB - 1 ? 0.0f : r);
+            r = __builtin_fmaf(v[m].x, ws[m], m / SH == NB - 1 ? 0.0f : r);
         }
         emit(acc[B0], k, dr0);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float& r = acc[(B0 + 1 + m / SH) % NB][m % SH];
-            r = __builtin_fmaf(v[m].y, g, m / SH == NB - 1 ? 0.0f : r);
+            r = __builtin_fmaf(v[m].y, ws[m], m / SH == NB - 1 ? 0.0f : r);
         }
         emit(acc[(B0 + 1) % NB], k + 1 < f1 ? k + 1 : -1, dr1);
 #endif
