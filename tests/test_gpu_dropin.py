@@ -1157,3 +1157,58 @@ def test_e2e_loop_gain_changes_midstream(pkg, oracle, torch_cuda):
         assert np.array_equal(bits(a), bits(b)), kind
         if kind == "regain":
             assert 2 <= served["gains"] <= 16, served
+
+
+def _framer_forward_loop(pkg, x, n, h, chunks):
+    """Push x into a Framer in `chunks` pieces, popping after each push, and take
+    every popped frame (times the Hann table) through IFftPlan::forward: the
+    per-frame loop whose pops the batched speculation watches."""
+    w = pkg.window_table(pkg.HANN, n)
+    fr = pkg.Framer()
+    fr.set_params(n, h, 1, pkg.ZERO_PAD)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    specs = []
+    for piece in np.array_split(x, chunks):
+        fr.push(np.ascontiguousarray(piece))
+        while True:
+            f = fr.pop()
+            if f is None:
+                break
+            specs.append(np.asarray(fft.forward_host((f * w).astype(np.float32)[None])).copy())
+    fft.close()
+    fr.close()
+    return specs
+
+
+@pytest.mark.gpu
+def test_framers_on_two_threads_while_forwards_speculate(pkg, oracle, torch_cuda):
+    """the speculation reads the process-wide last-popped
+    Framer from any thread's forward while its owner pushes (reallocating the
+    buffer), pops (compacting it) or resets it.  Every Framer mutation now holds
+    the last-pop lock.  Two threads, each with its own Framer and FFT plan of the
+    same size, run the push/pop/forward loop at once; each thread's spectra are the
+    bits the same loop gives alone."""
+    import threading
+    n, h = 1024, 256
+    xs = [oracle.synth(48_000, 31 + t) for t in range(2)]
+    alone = [_framer_forward_loop(pkg, xs[t], n, h, 24) for t in range(2)]
+    for rep in range(3):
+        got = [None, None]
+        errs = []
+
+        def run(t):
+            try:
+                got[t] = _framer_forward_loop(pkg, xs[t], n, h, 24)
+            except Exception as e:  # reported below: a thread's exception would be lost
+                errs.append(e)
+
+        th = [threading.Thread(target=run, args=(t,)) for t in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        for t in range(2):
+            assert len(got[t]) == len(alone[t]), (rep, t)
+            for k, (a, b) in enumerate(zip(alone[t], got[t])):
+                assert np.array_equal(bits(a), bits(b)), (rep, t, k)
