@@ -113,7 +113,7 @@ void k_pair15_hot(const FusedArgs a) {
         const int l = i % L, m = i / L;
         const int d = (m >> 2) * (4 * L) + l * 4 + (m & 3);
         wa4[d] = m < E ? a.t.wa[i] : 0.0f;
-        ws4[d] = m < E ? a.t.ws[i] : 0.0f;
+        ws4[d] = m < E ? a.t.ws[i] * a.inv_n * a.gain : 0.0f;  // (1/N, ws and g folded: push)
     }
     __syncthreads();
     float* ring = rings + (wave * HALVES + half) * RL;
@@ -134,7 +134,6 @@ void k_pair15_hot(const FusedArgs a) {
     const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s0) * a.ld_y, span_y);
     const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
     const int xo = half * int(a.ld_x), yo = half * int(a.ld_y);  // < 2^27 (host-checked)
-    const float g = a.gain, inv_n = a.inv_n;
     const int ring_blocks = a.ring_blocks;  // ring_len / H (the den table's blocks)
     const uint32_t xlo_b = __builtin_bit_cast(uint32_t, a.t.px_lo), xhi_b = __builtin_bit_cast(uint32_t, a.t.px_hi);
 
@@ -145,7 +144,7 @@ void k_pair15_hot(const FusedArgs a) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             war[m] = a.t.wa[hl + L * m];
-            wsr[m] = a.t.ws[hl + L * m];
+            wsr[m] = a.t.ws[hl + L * m] * a.inv_n * a.gain;
         }
     }
     auto win4 = [&](const float* w4, const float* wr, int m4, float (&wv)[4]) {
@@ -190,13 +189,17 @@ void k_pair15_hot(const FusedArgs a) {
         }
         bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
     };
-    // push one frame's window-weighted output into the ring at block k's position
-    auto push = [&](const float (&p)[E], int k) {
+    // push one frame's inverse output into the ring at block k's position: the
+    // 1/N scale, the synthesis window and the gain folded into one factor per tap,
+    // fma(v, ws / N g, ring) (one rounding where the staged path's o = v / N,
+    // fma(fma(o, w, 0), g, acc) has three: inside the FFT tolerance; a flagged
+    // stream is redone whole by the per-frame walker, so no walker has to agree)
+    auto push = [&](const float (&p)[E], const float (&wg)[E], int k) {
         const int base = k * H + hl;  // k H < 2^27 (host-checked)
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int pos = (base + L * m) & RM;
-            ring[pos] = __builtin_fmaf(p[m], g, ring[pos]);
+            ring[pos] = __builtin_fmaf(p[m], wg[m], ring[pos]);
         }
         dev::wave_lds_fence();
     };
@@ -324,13 +327,15 @@ void k_pair15_hot(const FusedArgs a) {
             }
         }
         P15<L>::inv(v, buf, tw, lane);
-        // o = v / N; its sanitize threshold 1e-30 = 2^-99.66: frexp exponents <= -99 flag the walk
-#pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = v[m] * dev::pc{inv_n, inv_n};
+        // the output sanitize acts on o = v / N below 1e-30, i.e. on |v| < 1e-30 N =
+        // 2^-89.75 (N = 960) / 2^-90.75 (480): frexp exponents <= -89 / -90 (|v| <
+        // 2^-89 / 2^-90) flag the walk -- every such v and a few harmless others.
         // (screened: fft_pair.h out_min_exp_screened; the window-edge taps n < L and
         // n >= N - L sit in registers 0 and E-1)
-        bad |= dev::out_min_exp_screened<E>(v, 0x1p-99f) <= -99;
-        float p[E];
+        static_assert(N == 960 || N == 480, "threshold exponent");
+        constexpr int kSanExp = N == 960 ? -89 : -90;
+        bad |= dev::out_min_exp_screened<E>(v, N == 960 ? 0x1p-89f : 0x1p-90f) <= kSanExp;
+        float p[E], wg[E];
 #pragma unroll
         for (int m4 = 0; m4 < 4; ++m4) {
             float wv[4];
@@ -339,7 +344,7 @@ void k_pair15_hot(const FusedArgs a) {
             for (int q = 0; q < 4; ++q) {
                 const int m = 4 * m4 + q;
                 if (m < E) {
-                    v[m] = v[m] * dev::pc{wv[q], wv[q]};
+                    wg[m] = wv[q];
                     p[m] = v[m].x;
                 }
             }
@@ -351,21 +356,21 @@ void k_pair15_hot(const FusedArgs a) {
             // VGPRs at L = 64, no spill)
             float2 d0[JF], d1[JF];
             if constexpr (L == 64) den_fetch(k, d0);
-            push(p, k);
+            push(p, wg, k);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (L != 64) den_fetch(k, d0);  // L = 32: after the push (167 VGPRs before)
             den_fetch(k + 1, d1);
             produce_pre(k, d0);
 #pragma unroll
             for (int m = 0; m < E; ++m) p[m] = v[m].y;
-            push(p, k + 1);
+            push(p, wg, k + 1);
             if (k + 1 < f1) produce_pre(k + 1, d1);
         } else {
-            push(p, k);
+            push(p, wg, k);
             produce(k);
 #pragma unroll
             for (int m = 0; m < E; ++m) p[m] = v[m].y;
-            push(p, k + 1);
+            push(p, wg, k + 1);
             if (k + 1 < f1) produce(k + 1);
         }
     }
