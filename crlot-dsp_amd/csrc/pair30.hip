@@ -92,7 +92,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         war[m] = a.t.wa[2 * (lane + 64 * m) + w];
-        if constexpr (WSREG) wsr[m] = a.t.ws[2 * (lane + 64 * m) + w];
+        if constexpr (WSREG) wsr[m] = a.t.ws[2 * (lane + 64 * m) + w] * a.inv_n * a.gain;  // (folded: the push)
     }
     for (int i = threadIdx.x; i < RL; i += 128) ring[i] = 0.0f;
     __syncthreads();
@@ -116,12 +116,16 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         bad |= (mx > xhi_b) | (mn < xlo_b - 1u);
     };
     // push: this wave's samples of the frame at block k's position (its parity's ring slots)
+    // (WSREG: p is the unscaled inverse output and the push multiplies by the staged
+    // factor ws / N g, one rounding for three -- inside the FFT tolerance; a flagged
+    // stream is redone whole by the per-frame walker.  Else p = (v / N) ws and the
+    // push is fma(p, g, ring).)
     auto push = [&](const float (&p)[E], int k) {
         const int base = k * H + 2 * lane + w;  // k H < 2^27 (host-checked)
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int pos = (base + 128 * m) & RM;
-            ring[pos] = __builtin_fmaf(p[m], g, ring[pos]);
+            ring[pos] = __builtin_fmaf(p[m], WSREG ? wsr[m] : g, ring[pos]);
         }
         dev::wave_lds_fence();
     };
@@ -207,21 +211,26 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WPE))) void
         }
         __syncthreads();  // both read before either transposes into its buffer again
         dev::pair15_inv(v, buf, tw, lane);
-        // o = v / N; its sanitize threshold 1e-30 = 2^-99.66: frexp exponents <= -99 flag the walk
+        // the output sanitize acts on o = v / N below 1e-30 = 2^-99.66: on o, frexp
+        // exponents <= -99 flag the walk; on the unscaled v (WSREG), |v| < 2^-88
+        // covers every |v / N| < 1e-30 N / N = 2^-88.75 (and a few harmless others)
         {
+            constexpr int kSanExp = WSREG ? -88 : -99;
             int e[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int m = 0; m < E; ++m) {
-                v[m] = v[m] * dev::pc{inv_n, inv_n};
+                if constexpr (!WSREG) v[m] = v[m] * dev::pc{inv_n, inv_n};
                 e[m & 3] = min(e[m & 3], min(__builtin_amdgcn_frexp_expf(v[m].x), __builtin_amdgcn_frexp_expf(v[m].y)));
             }
-            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= -99;
+            bad |= min(min(e[0], e[1]), min(e[2], e[3])) <= kSanExp;
         }
         float p[E];
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const float wsm = WSREG ? wsr[m] : a.t.ws[2 * (lane + 64 * m) + w];
-            v[m] = v[m] * dev::pc{wsm, wsm};
+            if constexpr (!WSREG) {
+                const float wsm = a.t.ws[2 * (lane + 64 * m) + w];
+                v[m] = v[m] * dev::pc{wsm, wsm};
+            }
             p[m] = v[m].x;
         }
         push(p, k);

@@ -113,6 +113,21 @@ constexpr int pn_wpe(int key) {
     return n <= 400 * halves ? 4 : n <= 1000 * halves ? 3 : 2;
 }
 
+// The frexp exponent bound of the output sanitize on an unscaled inverse output v
+// of an N-point transform: |v| < 2^e for every v with |v / N| < 1e-30 (the
+// reference's threshold), e = floor(log2(1e-30 N)) + 1, with room for the
+// roundings of v / N (a few more values flag a walk, harmlessly)
+constexpr int pn_san_exp(int n) {
+    double t = 1e-30 * n;
+    int e = 0;
+    while (t < 1.0) {
+        t *= 2.0;
+        --e;
+    }
+    return t * (1.0 + 0x1p-20) < 2.0 ? e + 1 : e + 2;
+}
+static_assert(pn_san_exp(1024) == -89 && pn_san_exp(960) == -89 && pn_san_exp(480) == -90, "san exp");
+
 template <int K, bool HAS_GAIN>  // K: plan key (fft_pairn.h pn_factor), N = K % 100000
 __global__ __launch_bounds__(256 * pn_wpe(K)) __attribute__((amdgpu_waves_per_eu(pn_wpe(K))))
 void k_pairn(const FusedArgs a) {
@@ -155,7 +170,7 @@ void k_pairn(const FusedArgs a) {
         if constexpr (!LEAN)
             for (int i = threadIdx.x; i < N; i += blockDim.x) {
                 wl[i] = a.t.wa[i];
-                wl[N + i] = a.t.ws[i];
+                wl[N + i] = a.t.ws[i] * a.inv_n * a.gain;  // (1/N, ws and g folded: the pushes below)
             }
     }
     __syncthreads();
@@ -295,11 +310,16 @@ void k_pairn(const FusedArgs a) {
         }
         dev::pn_passes<true, K, 0, FAC.n - 1>(buf, tw, ln);
         // the last inverse pass into registers, pushed from there: frame k the real
-        // part, frame k+1 the imaginary part; o = v (1/N), then o * ws; the output
-        // sanitize threshold 1e-30 = 2^-99.66: exponents <= -99 flag the walk
+        // part, frame k+1 the imaginary part.  Lean walks: o = v (1/N), then o * ws,
+        // fma(., g, ring); the output sanitize threshold 1e-30 = 2^-99.66: exponents
+        // <= -99 flag the walk.  Otherwise 1/N, ws and g are one staged factor,
+        // fma(v, ws / N g, ring) (one rounding for three: inside the FFT tolerance; a
+        // flagged stream is redone whole by the per-frame walker), and the threshold
+        // test acts on v: |v| < 2^kSanExp covers every |v / N| < 1e-30 (pn_san_exp)
         dev::pc y[PL::ITS][PL::R];
         dev::pn_pass_compute<true, K, FAC.n - 1>(buf, tw, ln, y);
         const int kb0 = rbase(k), kb1 = rbase(k + 1);
+        constexpr int kSanExp = LEAN ? -99 : pn_san_exp(N);
         {
             int e = 0;
 #pragma unroll
@@ -308,16 +328,17 @@ void k_pairn(const FusedArgs a) {
                 if (PL::live(it, j)) {
 #pragma unroll
                     for (int q = 0; q < PL::R; ++q) {
-                        y[it][q] = y[it][q] * dev::pc{inv_n, inv_n};
+                        if constexpr (LEAN) y[it][q] = y[it][q] * dev::pc{inv_n, inv_n};
                         e = min(e, min(__builtin_amdgcn_frexp_expf(y[it][q].x),
                                        __builtin_amdgcn_frexp_expf(y[it][q].y)));
                         const int n = PL::out(j, q);
                         const int pos = rpos(kb0, n);
-                        ring[pos] = __builtin_fmaf(y[it][q].x * ws[n], g, ring[pos]);
+                        ring[pos] = LEAN ? __builtin_fmaf(y[it][q].x * ws[n], g, ring[pos])
+                                         : __builtin_fmaf(y[it][q].x, ws[n], ring[pos]);
                     }
                 }
             }
-            bad |= e <= -99;
+            bad |= e <= kSanExp;
         }
         dev::pn_fence<K>();
         produce(k);
@@ -329,7 +350,8 @@ void k_pairn(const FusedArgs a) {
                 for (int q = 0; q < PL::R; ++q) {
                     const int n = PL::out(j, q);
                     const int pos = rpos(kb1, n);
-                    ring[pos] = __builtin_fmaf(y[it][q].y * ws[n], g, ring[pos]);
+                    ring[pos] = LEAN ? __builtin_fmaf(y[it][q].y * ws[n], g, ring[pos])
+                                     : __builtin_fmaf(y[it][q].y, ws[n], ring[pos]);
                 }
             }
         }
