@@ -1212,3 +1212,77 @@ def test_framers_on_two_threads_while_forwards_speculate(pkg, oracle, torch_cuda
             assert len(got[t]) == len(alone[t]), (rep, t)
             for k, (a, b) in enumerate(zip(alone[t], got[t])):
                 assert np.array_equal(bits(a), bits(b)), (rep, t, k)
+
+
+def _random_rhythm_loop(pkg, x, n, h, seed, frames_max=None):
+    """The e2e loop with random deviations from the harness rhythm, drawn from
+    `seed` (the same script in every mode): a fixed per-bin gain from some frame
+    on, one-off spectrum edits (a bin rotated, a bin scaled), a forward asked
+    twice, a frame whose push is skipped, produce sizes other than H.  Returns
+    every array a call handed back, in call order."""
+    rng = np.random.default_rng(seed)
+    w = pkg.window_table(pkg.HANN, n)
+    fr = pkg.Framer()
+    fr.set_params(n, h, 1, pkg.ZERO_PAD)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                                           apply_window_inside=True))
+    ola.set_window(w)
+    fr.push(x)
+    g = (0.5 + 0.5 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2))).astype(np.float32)
+    gain_from = int(rng.integers(20, 200)) if rng.random() < 0.5 else None
+    got, k = [], 0
+    while frames_max is None or k < frames_max:
+        f = fr.pop()
+        if f is None:
+            break
+        p = (f * w).astype(np.float32)[None]
+        X = np.asarray(fft.forward_host(p)).copy()
+        r = rng.random()
+        if r < 0.03:  # the same forward again
+            X = np.asarray(fft.forward_host(p)).copy()
+        got.append(X.copy())
+        if gain_from is not None and k >= gain_from:
+            X[0].real *= g
+            X[0].imag *= g
+        r = rng.random()
+        if r < 0.03:
+            X[0][int(rng.integers(1, n // 2))] *= np.complex64(1j)
+        elif r < 0.05:
+            X[0][int(rng.integers(0, n // 2 + 1))] *= np.float32(1.5)
+        y = np.asarray(fft.inverse_host(X))[0].copy()
+        got.append(y)
+        if rng.random() >= 0.02:  # (else the frame's push is skipped)
+            ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+        r = rng.random()
+        m = h if r < 0.9 else (h // 2 if r < 0.95 else 2 * h)
+        cnt, chans = ola.produce(m)
+        got.append(chans[0][:cnt].copy())
+        k += 1
+    ola.close()
+    fft.close()
+    fr.close()
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_random_rhythm_loop_batch_equals_per_call(pkg, oracle, torch_cuda, seed):
+    """Property test of the batched speculation as a state machine: the e2e loop
+    with random deviations from the harness rhythm gives, call for call, the bits
+    the per-call path gives with the batch off (crlot_set_call_speculation(1)).
+    Signals of 1.5 windows and more, so deviations land inside windows and on
+    their seams."""
+    n, h = (1024, 256) if seed % 2 else (960, 240)
+    x = oracle.synth(int(48_000 * 3.2), 40 + seed)
+    try:
+        pkg.set_call_speculation(1)
+        a = _random_rhythm_loop(pkg, x, n, h, seed)
+        pkg.set_call_speculation(2)
+        b, served = _spec_delta(pkg, lambda: _random_rhythm_loop(pkg, x, n, h, seed))
+    finally:
+        pkg.set_call_speculation(2)
+    assert len(a) == len(b)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert u.shape == v.shape and np.array_equal(bits(u), bits(v)), (seed, i // 3, i % 3)
+    assert served["forwards"] > len(a) // 6, served  # the batch served a good part of the loop
