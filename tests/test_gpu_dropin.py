@@ -1286,3 +1286,65 @@ def test_random_rhythm_loop_batch_equals_per_call(pkg, oracle, torch_cuda, seed)
     for i, (u, v) in enumerate(zip(a, b)):
         assert u.shape == v.shape and np.array_equal(bits(u), bits(v)), (seed, i // 3, i % 3)
     assert served["forwards"] > len(a) // 6, served  # the batch served a good part of the loop
+
+
+def _random_pipeline_loop(pkg, x, n, h, seed):
+    """performance_benchmark.cc's loop (FrameQueue frames, add_frame_SoA) with
+    random deviations drawn from `seed`: a frame read twice, a frame read out of
+    order, a forward input nudged by one ulp, a spectrum edit, produce sizes
+    other than H.  Returns every array a call handed back, in call order."""
+    rng = np.random.default_rng(seed)
+    q = pkg.FrameQueue(x, n, h, center=True)
+    w = pkg.window_table(pkg.HANN, n)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                                           apply_window_inside=True))
+    ola.set_window(w)
+    got = []
+    F = q.getNumFrames()
+    for i in range(F):
+        r = rng.random()
+        if r < 0.02 and i + 3 < F:
+            q.getFrame(i + 3)  # a read ahead, then the frame itself
+        f = q.getFrame(i)
+        if rng.random() < 0.02:
+            f = q.getFrame(i)  # read twice
+        if rng.random() < 0.02:
+            f = f.copy()
+            f[int(rng.integers(0, n))] = np.nextafter(f[0], np.float32(np.inf))
+        X = np.asarray(fft.forward_host(f[None])).copy()
+        got.append(X.copy())
+        if rng.random() < 0.03:
+            X[0][int(rng.integers(1, n // 2))] *= np.complex64(1j)
+        y = np.asarray(fft.inverse_host(X))[0].copy()
+        got.append(y)
+        ola.add_frame_SoA([y], w, i * h, 0, n, 1.0)
+        r = rng.random()
+        m = h if r < 0.9 else (h // 2 if r < 0.95 else 3 * h)
+        cnt, chans = ola.produce(m)
+        got.append(chans[0][:cnt].copy())
+    ola.close()
+    fft.close()
+    q.close()
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_random_pipeline_loop_batch_equals_per_call(pkg, oracle, torch_cuda, seed):
+    """The FrameQueue source of the batched speculation under random deviations
+    from performance_benchmark.cc's rhythm: every call gives the per-call path's
+    bits with the batch on."""
+    n, h = (1024, 256) if seed % 2 else (2048, 512)
+    x = oracle.synth(int(48_000 * 3.2), 60 + seed)
+    try:
+        pkg.set_call_speculation(1)
+        a = _random_pipeline_loop(pkg, x, n, h, seed)
+        pkg.set_call_speculation(2)
+        b, served = _spec_delta(pkg, lambda: _random_pipeline_loop(pkg, x, n, h, seed))
+    finally:
+        pkg.set_call_speculation(2)
+    assert len(a) == len(b)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert u.shape == v.shape and np.array_equal(bits(u), bits(v)), (seed, i // 3, i % 3)
+    assert served["forwards"] > len(a) // 6, served
