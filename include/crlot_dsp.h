@@ -144,12 +144,16 @@ int crlot_plan_set_chunks(crlot_plan* plan, int32_t chunks_per_stream);
  * OLAAccumulator push / produce), process-wide.  1: each forward also computes
  * the inverse and the produce block that follow it on the call kernel.  2
  * (default): in addition, when a forward's input is bit for bit the frame a
- * dsp::Framer just popped times a window table the library built, the whole
- * remaining loop of that Framer's signal runs as one batch on the device and
- * the following calls are served from it after a bitwise check of each call's
- * input and arguments; the first call that differs ends the batch and the OLA
- * object's ring is rebuilt from the frames it was served.  Results are the
- * same bits in both modes.  Other values: CRLOT_EINVAL. */
+ * dsp::Framer just popped times a window table the library built (or the
+ * dsp::FrameQueue frame read last), the loop over that signal runs as batches
+ * on the device, windows of at most `window_frames` frames
+ * (crlot_call_batch_capacity), and the following calls are served from them
+ * after a bitwise check of each call's input and arguments; an inverse input
+ * that is the served spectrum times a fixed real gain per bin teaches the batch
+ * that gain.  The first call that differs otherwise ends the batch and the OLA
+ * object's ring is rebuilt from the frames it was served; a batch that cannot
+ * allocate or launch declines and the call takes its ordinary path.  Results
+ * are the same bits in both modes.  Other values: CRLOT_EINVAL. */
 int crlot_set_call_speculation(int32_t mode);
 /* Process-wide counters of the batched speculation: [0] batches started, [1]
  * forwards, [2] inverses, [3] pushes, [4] produces served from a batch, [5] OLA
