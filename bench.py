@@ -571,6 +571,9 @@ def suite_e2e(pkg, torch, dev):
         gus, _ = _cpu_gain_loop_us(O, native, x, n, h)
         g["spectral_gain"]["cpu_oracle_1thread"] = {"ms_per_iteration": round(gus / 1e3, 4),
                                                     "us_per_frame": round(gus / F, 3)}
+        if "spectral_mask" in g:  # (the CPU does the same per-bin multiply per frame whichever mask it is)
+            g["spectral_mask"]["cpu_oracle_1thread"] = dict(g["spectral_gain"]["cpu_oracle_1thread"],
+                                                            note="the spectral_gain row's oracle loop")
         res["runs"].append(g)
     res["cpu_native_build"] = native
     return res

@@ -236,7 +236,7 @@ def call_speculation_stats() -> dict:
 
 
 SPEC_STATS = ("batches", "forwards", "inverses", "pushes", "produces", "rebuilds", "frames", "windows", "declined",
-              "gains")
+              "gains", "gain_backoffs")
 
 
 def call_speculation_stats_ex() -> dict:

@@ -1327,10 +1327,14 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
     sh->chain.valid = false;
     const bool spec = kind == 0 && (p->e < 0 ? batch <= sh->any_waves : batch <= 4 && p->e <= 16);
     // chained speculation: a single frame whose inverse an OLA object pushed last time
+    // (a forward: the speculated inverse's push and produce; an inverse -- the
+    // caller edited the spectrum -- the push and produce of its own output; the
+    // power-of-two servers up to N = 2048 and the any-size server keep the frame in LDS)
     crlot::ChainPred pred;
-    const bool chain = spec && batch == 1 && sh->target.predict && sh->target.predict(sh->target.owner, &pred) &&
-                       pred.N == n && pred.n > 0;
-    if ((rc = sv->grow(nin, nout, spec ? size_t(batch) * size_t(n) + (chain ? size_t(pred.n) : 0) : 0)) !=
+    const bool ichain_ok = kind == 1 && batch == 1 && (p->e < 0 || p->e <= 16);
+    const bool chain = (spec || ichain_ok) && batch == 1 && sh->target.predict &&
+                       sh->target.predict(sh->target.owner, &pred) && pred.N == n && pred.n > 0;
+    if ((rc = sv->grow(nin, nout, spec || chain ? size_t(batch) * size_t(n) + (chain ? size_t(pred.n) : 0) : 0)) !=
         CRLOT_OK)
         return rc;
     crlot::CallSlot sl;
@@ -1370,7 +1374,12 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
         sh->chain.index = sl.index;
         sh->chain.pred = pred;
         sh->chain.slot = sl;
+        sh->chain.frame = kind == 1 ? sl.out : sl.spec;
+        sh->chain.frame_off = kind == 1 ? sl.out_off : sl.spec_off;
     }
+    sh->inv.valid = kind == 1 && batch == 1;
+    sh->inv.index = sl.index;
+    sh->inv.slot = sl;
     return CRLOT_OK;
 }
 

@@ -705,6 +705,24 @@ int batch_inverse(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
             b->learn_after = j + 16;
             return 0;
         }
+        // A new gain right after the last one, different in many bins: the edit
+        // changes from frame to frame (a time-varying mask), so redoing the
+        // window's inverses for each would cost a chain per frame.  Those frames
+        // take the per-call path; learning resumes after a backoff that doubles
+        // each time (up to a window).  A gain that changes in a few bins only is
+        // the same gain settling (bins one frame does not pin), applied at once.
+        if (!b->sgain.empty() && b->gain_served < kGainMinRun) {
+            size_t changed = 0;
+            for (size_t k = 0; k < g.size(); ++k) changed += g[k] != b->sgain[k];
+            if (changed * 8 > g.size()) {
+                b->learn_after = j + b->learn_backoff;
+                b->learn_backoff = std::min<int64_t>(2 * b->learn_backoff, kBatchWindow);
+                g_stats[kStatGainBackoffs].fetch_add(1, std::memory_order_relaxed);
+                return 0;
+            }
+        } else {
+            b->learn_backoff = 16;
+        }
         const std::vector<float> old = b->sgain;
         const int64_t old_from = b->sgain_from;
         b->sgain.swap(g);
@@ -716,6 +734,7 @@ int batch_inverse(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
             return decline(b);
         }
         spec_count(kStatGains);
+        b->gain_served = 0;
         if (std::all_of(b->sgain.begin(), b->sgain.end(), [](float v) { return v == 1.0f; }))
             b->sgain.clear();  // the identity again (x * 1 is exact: the rows redone are its bits)
         if (!inverse_input_matches(b, j, in)) return 0;
@@ -723,6 +742,7 @@ int batch_inverse(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     std::memcpy(out, b->h_r + b->row(j) * size_t(n), sizeof(float) * size_t(n));
     b->inv_ready = -1;
     b->pushed = j;
+    if (!b->sgain.empty()) b->gain_served += 1;
     spec_count(kStatInverse);
     return 1;
 }

@@ -41,6 +41,7 @@ struct SharedServer;
 // attached OLA object's overlap-add continues across the seam; device and pinned
 // buffers therefore hold at most kBatchWindow + kBatchWarm frames.
 constexpr int64_t kBatchWindow = 512;
+constexpr int64_t kGainMinRun = 4;  // inverses a learned gain must serve to count as fixed
 constexpr int64_t kBatchWarm = 63;  // warm-up frames kept: ceil(N / H) - 1 for H >= N / 64
 
 // The most recently popped mono Framer: accept(frame 0, hop) decides on the frame
@@ -83,7 +84,7 @@ std::vector<std::vector<float>> windows_of_size(int64_t n);
 // speculation of the whole loop too (crlot_set_call_speculation)
 int spec_mode();
 enum { kStatStart = 0, kStatForward, kStatInverse, kStatPush, kStatProduce, kStatRebuild, kStatFrames, kStatWindows,
-       kStatDeclined, kStatGains, kStatCount };
+       kStatDeclined, kStatGains, kStatGainBackoffs, kStatCount };
 void spec_count(int what);
 
 struct BatchSpec {
@@ -153,6 +154,8 @@ struct BatchSpec {
     std::vector<float> sgain;  // [N/2 + 1]; empty: the identity step
     int64_t sgain_from = 0;
     int64_t learn_after = -1;  // no new learning attempt before this frame (after a failed one)
+    int64_t gain_served = 0;   // inverses served with the gain learned last
+    int64_t learn_backoff = 16;  // frames without learning after a gain that did not last
     float* d_sgain = nullptr;
     float* d_specg = nullptr;  // [rows][N + 2] gained spectra (the inverse's input)
     size_t c_sgain = 0, c_specg = 0;

@@ -143,7 +143,17 @@ struct SharedServer {
         uint64_t index = 0;
         ChainPred pred;
         CallSlot slot;      // chained produce block at slot.spec + N
+        // the frame the push must equal (host) and its arena offset (the deferred
+        // commit's source after a relaunch): a chained forward's speculated inverse
+        // (slot.spec), or a chained inverse request's own output (slot.out)
+        const float* frame = nullptr;
+        int64_t frame_off = 0;
     } chain;
+    struct LastInverse {    // the last single-frame inverse request (the OLA association)
+        bool valid = false;
+        uint64_t index = 0;
+        CallSlot slot;      // slot.out: the frame it returned
+    } inv;
     ChainTarget target;     // the OLA object that pushed the last speculated inverse
     struct BatchSpec* batch = nullptr;  // batched speculation of the whole loop (batch.h)
 };

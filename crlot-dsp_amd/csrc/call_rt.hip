@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     cf* const ast = atw + (ANY ? a.any_tw : 0);
     float* const achain = reinterpret_cast<float*>(ast + (ANY ? a.any_p : 0));
     cf* const awaves = reinterpret_cast<cf*>(achain + (ANY ? 2 * a.any_p : 0));
-    float* const chainp = ANY ? achain : chainbuf;  // the kept frame of a chained forward
+    float* const chainp = ANY ? achain : chainbuf;  // the kept frame of a chained forward or inverse
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     cf* buf = bufs + wave * P;
@@ -390,13 +390,16 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 }
                 });
             } else if (r.op == kCallIrfft) {
+                // a chained inverse (a single frame an OLA object will push) also
+                // keeps its output in LDS for the produce block after the publish
+                const bool ich = CallLds<E>::CH > 0 && (r.flags & kCallChain) != 0 && r.batch == 1;
                 with_in([&](const auto& cin) {
                 for (int b = wave; b < r.batch; b += kCallWaves) {
                     const int64_t x = int64_t(b) * (2 * P + 2);
                     call_irfft<E>([&](int k) {
                         const float2 v = cin.at2(x + 2 * k);
                         return cf{v.x, v.y};
-                    }, out + int64_t(b) * 2 * P, buf, tw, st, r.f0, lane);
+                    }, out + int64_t(b) * 2 * P, buf, tw, st, r.f0, lane, ich ? chainp : nullptr);
                 }
                 });
             } else if (r.op == kCallCfft || r.op == kCallIcfft) {
@@ -471,9 +474,12 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                             const cf* z = wg ? any_fft<true, true>(A, B, aplan, gtw, t)
                                              : any_fft<true, false>(A, B, aplan, gtw, lane);
                             float* o = out + int64_t(b) * 2 * Pn;
-                            for (int i = tid; i < Pn; i += nth)
-                                *reinterpret_cast<float2*>(o + 2 * i) =
-                                    make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0));
+                            const bool ich = wg && (r.flags & kCallChain) != 0;  // (kept for the chained produce)
+                            for (int i = tid; i < Pn; i += nth) {
+                                const float2 v = make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0));
+                                *reinterpret_cast<float2*>(o + 2 * i) = v;
+                                if (ich) *reinterpret_cast<float2*>(chainp + 2 * i) = v;
+                            }
                         } else {
                             const int64_t x = int64_t(b) * 2 * Pn;
                             for (int i = tid; i < Pn; i += nth) {
@@ -646,6 +652,36 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             CALL_PH(1);
             __syncthreads();
             if (t == 0) st_sys64(&a.hctl->done, my);
+        }
+
+        // ---- a chained inverse (the caller edited the spectrum it pushes): the
+        // produce(n) block at rp after pushing the frame just returned at start --
+        // the forward chain's arithmetic below, on the frame kept in LDS -- into the
+        // speculation slot after one frame's floats
+        if constexpr (CallLds<E>::CH > 0 || ANY) {
+            if (r.op == kCallIrfft && (r.flags & kCallChain) != 0 && r.batch == 1) {
+                chain_req = my;
+                float* ring = r.p2;
+                const float* den = r.p3;
+                const float* wobj = r.p4;
+                const int64_t R = r.j[0], start = r.j[1], rp = r.j[2], n = r.j[3], Nf = 2 * Pr;
+                float* co = a.out_arena + r.spec_off + Nf;
+                for (int64_t q = t; q < n; q += kCallBlock) {
+                    int64_t p = rp + q;
+                    if (p >= R) p -= R;
+                    float v = ring[p];
+                    int64_t d = p - start;
+                    if (d < 0) d += R;
+                    if (d < Nf) {
+                        const float s0 = chainp[d];
+                        v = wobj ? __builtin_fmaf(__builtin_fmaf(s0, wobj[d], 0.0f), r.f1, v) : __builtin_fmaf(s0, r.f1, v);
+                    }
+                    co[q] = v / den[p];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                __syncthreads();
+                if (t == 0) st_sys64(&a.hctl->chain_done, my);
+            }
         }
 
         // ---- speculation after the publish (the host is already running)

@@ -523,8 +523,13 @@ int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, i
     crlot::CallServer* sv = sh->srv;
     const int64_t N = o->N();
     // learn the association: this object pushes the frames the server speculates
-    if (sh->target.owner != o && sh->fft.index + 4 > sv->submitted() && start_off == 0 && eff == N &&
-        sh->fft.slot.spec && sv->live(sh->fft.slot) && std::memcmp(frame, sh->fft.slot.spec, sizeof(float) * size_t(N)) == 0) {
+    // (or the output of the last single-frame inverse request: a caller that edits
+    // the spectrum pushes what the inverse call returned)
+    if (sh->target.owner != o && start_off == 0 && eff == N &&
+        ((sh->fft.index + 4 > sv->submitted() && sh->fft.slot.spec && sv->live(sh->fft.slot) &&
+          std::memcmp(frame, sh->fft.slot.spec, sizeof(float) * size_t(N)) == 0) ||
+         (sh->inv.valid && sh->inv.index + 4 > sv->submitted() && sv->live(sh->inv.slot) &&
+          std::memcmp(frame, sh->inv.slot.out, sizeof(float) * size_t(N)) == 0))) {
         sh->target.owner = o;
         sh->target.predict = ola_predict;
         return 0;
@@ -533,7 +538,8 @@ int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, i
     const float* want_win = (uw && !caller_win) ? o->d_win : nullptr;
     if (!(sh->chain.valid && sh->chain.index == sv->submitted() && sh->target.owner == o && start_off == 0 &&
           eff == N && start_sample == pd.start && gain == pd.gain && !caller_win && want_win == pd.win &&
-          pd.rp == o->read_pos && sv->live(sh->chain.slot) && std::memcmp(frame, sh->chain.slot.spec, sizeof(float) * size_t(N)) == 0))
+          pd.rp == o->read_pos && sv->live(sh->chain.slot) && sh->chain.frame &&
+          std::memcmp(frame, sh->chain.frame, sizeof(float) * size_t(N)) == 0))
         return 0;
     sh->chain.valid = false;
     // the push itself rides on the next request (the server keeps the frame in LDS)
@@ -546,7 +552,7 @@ int try_chain_push(crlot_ola* o, const float* frame, bool uw, bool caller_win, i
     pe.len = N;
     pe.gain = gain;
     pe.src_index = sh->chain.index;
-    pe.src_off = sh->chain.slot.spec_off;  // the speculated inverse = the frame pushed
+    pe.src_off = sh->chain.frame_off;  // the frame pushed, in the output arena
     int rc = sv->defer(pe);
     if (rc != CRLOT_OK) return rc;
     o->spec.valid = true;

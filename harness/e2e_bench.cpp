@@ -17,6 +17,8 @@
 //                   here"): every bin k of each spectrum scaled by the real gain
 //                   0.5 + 0.5 cos(pi k / (N/2)) on the host, between forward
 //                   and inverse -- ms per iteration, us per frame, per-call p50
+//   spectral_mask   the same with a time-varying mask: frame k scaled by mask
+//                   k mod 8, 0.5 + 0.5 cos(pi k / (N/2) + 0.7 j) (no fixed gain)
 //   fft1024         IFftPlan::forward alone, p50 us (:187-205, 10000 calls)
 //   quality         SNR and cross-correlation delay exactly as :77-128 compute
 //                   them, on the streaming-interleaved output
@@ -174,41 +176,57 @@ int main(int argc, char** argv) {
         y.resize(T, 0.0f);
         const double snr = calculate_snr(x, y), delay = calculate_delay(x, y, sr);
 
-        // the spectral step (a per-bin gain on the host between the transforms)
+        // the spectral step on the host between the transforms: frame k's bins
+        // scaled by masks[k % masks.size()] (one mask: a fixed per-bin gain)
+        struct SpecRun {
+            std::vector<double> it, fwd, inv, push, prod;
+        };
+        auto spectral_loop = [&](const std::vector<std::vector<float>>& masks) {
+            SpecRun r;
+            for (int it = -3; it < std::max(iters / 2, 20); ++it) {
+                size_t produced = 0, k = 0;
+                float* ch_out[1] = {output.data()};
+                const auto t_begin = clk::now();
+                p.framer.push(x.data(), T);
+                while (p.framer.pop(frame.data())) {
+                    for (size_t i = 0; i < N; ++i) processed[i] = frame[i] * p.window[i];
+                    auto t1 = clk::now();
+                    p.plan->forward(processed.data(), spectrum.data());
+                    auto t2 = clk::now();
+                    const std::vector<float>& g = masks[k % masks.size()];
+                    for (size_t b = 0; b <= N / 2; ++b) spectrum[b] *= g[b];
+                    p.plan->inverse(spectrum.data(), processed.data());
+                    auto t3 = clk::now();
+                    p.ola->push_frame_AoS(processed.data(), nullptr, k * H, 0, N, 1.0f);
+                    auto t4 = clk::now();
+                    ch_out[0] = output.data() + produced;
+                    produced += p.ola->produce(ch_out, H);
+                    auto t5 = clk::now();
+                    if (it >= 0 && it % 4 == 0) {
+                        r.fwd.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
+                        r.inv.push_back(std::chrono::duration<double, std::micro>(t3 - t2).count());
+                        r.push.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
+                        r.prod.push_back(std::chrono::duration<double, std::micro>(t5 - t4).count());
+                    }
+                    ++k;
+                }
+                if (it >= 0) r.it.push_back(us_since(t_begin));
+                p.ola->reset();
+                p.ola->set_window(p.window, int(N));
+                p.framer.reset();
+            }
+            return r;
+        };
         std::vector<float> bin_gain(N / 2 + 1);
         for (size_t k = 0; k <= N / 2; ++k) bin_gain[k] = float(0.5 + 0.5 * std::cos(M_PI * double(k) / double(N / 2)));
-        std::vector<double> g_it, g_fwd, g_inv, g_push, g_prod;
-        for (int it = -3; it < std::max(iters / 2, 20); ++it) {
-            size_t produced = 0, k = 0;
-            float* ch_out[1] = {output.data()};
-            const auto t_begin = clk::now();
-            p.framer.push(x.data(), T);
-            while (p.framer.pop(frame.data())) {
-                for (size_t i = 0; i < N; ++i) processed[i] = frame[i] * p.window[i];
-                auto t1 = clk::now();
-                p.plan->forward(processed.data(), spectrum.data());
-                auto t2 = clk::now();
-                for (size_t b = 0; b <= N / 2; ++b) spectrum[b] *= bin_gain[b];
-                p.plan->inverse(spectrum.data(), processed.data());
-                auto t3 = clk::now();
-                p.ola->push_frame_AoS(processed.data(), nullptr, k * H, 0, N, 1.0f);
-                auto t4 = clk::now();
-                ch_out[0] = output.data() + produced;
-                produced += p.ola->produce(ch_out, H);
-                auto t5 = clk::now();
-                if (it >= 0 && it % 4 == 0) {
-                    g_fwd.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
-                    g_inv.push_back(std::chrono::duration<double, std::micro>(t3 - t2).count());
-                    g_push.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
-                    g_prod.push_back(std::chrono::duration<double, std::micro>(t5 - t4).count());
-                }
-                ++k;
-            }
-            if (it >= 0) g_it.push_back(us_since(t_begin));
-            p.ola->reset();
-            p.ola->set_window(p.window, int(N));
-            p.framer.reset();
-        }
+        const SpecRun gain_run = spectral_loop({bin_gain});
+        // a time-varying mask (a noise suppressor's shape): eight masks in turn,
+        // 0.5 + 0.5 cos(pi k / (N/2) + 0.7 j) -- no fixed gain to learn
+        std::vector<std::vector<float>> masks(8, std::vector<float>(N / 2 + 1));
+        for (size_t j = 0; j < masks.size(); ++j)
+            for (size_t k = 0; k <= N / 2; ++k)
+                masks[j][k] = float(0.5 + 0.5 * std::cos(M_PI * double(k) / double(N / 2) + 0.7 * double(j)));
+        const SpecRun mask_run = spectral_loop(masks);
 
         // the harness's literal order: every push, then the produce loop (ring aliasing, Q3)
         std::vector<double> ho_us;
@@ -260,14 +278,19 @@ int main(int argc, char** argv) {
             "\"spectral_gain\": {\"order\": \"streaming-interleaved\", \"ms_p50\": %.4f, \"us_per_frame\": %.3f, "
             "\"per_call_us_p50\": {\"forward\": %.3f, \"gain_and_inverse\": %.3f, \"push_frame_AoS\": %.3f, "
             "\"produce\": %.3f}}, "
+            "\"spectral_mask\": {\"order\": \"streaming-interleaved\", \"masks\": 8, \"ms_p50\": %.4f, "
+            "\"us_per_frame\": %.3f, \"per_call_us_p50\": {\"forward\": %.3f, \"mask_and_inverse\": %.3f, "
+            "\"push_frame_AoS\": %.3f, \"produce\": %.3f}}, "
             "\"quality\": {\"snr_db\": %.4f, \"delay_ms\": %.4f}}\n",
             // 1 s of audio per iteration: x real-time = 1 s / iteration time; the
             // reference's reporter prints (48000 / ms) * 1000 under that name (:311-317)
             N, H, T, frames, iters, it_p50 / 1e3, 1e6 / it_p50, 48000.0 / (it_p50 / 1e3) * 1000.0,
             it_p50 / double(frames), double(T) / it_p50, ho_p50 / 1e3, 1e6 / ho_p50, ho_p50 / double(frames), p50(t_pop),
             p50(t_fwd), p50(t_inv), p50(t_push), p50(t_prod), pct(t_fwd, 0.1), pct(t_fwd, 0.9), pct(t_inv, 0.1),
-            pct(t_inv, 0.9), p50(f_us), p50(g_it) / 1e3, p50(g_it) / double(frames), p50(g_fwd), p50(g_inv),
-            p50(g_push), p50(g_prod), snr, delay);
+            pct(t_inv, 0.9), p50(f_us), p50(gain_run.it) / 1e3, p50(gain_run.it) / double(frames), p50(gain_run.fwd),
+            p50(gain_run.inv), p50(gain_run.push), p50(gain_run.prod), p50(mask_run.it) / 1e3,
+            p50(mask_run.it) / double(frames), p50(mask_run.fwd), p50(mask_run.inv), p50(mask_run.push),
+            p50(mask_run.prod), snr, delay);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "exception: %s\n", e.what());
         return 4;

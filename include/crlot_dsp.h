@@ -166,8 +166,11 @@ int crlot_call_speculation_stats(int64_t* out6);
  * buffer or launch failed (the call then took the ordinary path), [9] spectral
  * gains learned (an inverse input that was the served spectrum times a fixed
  * real gain per bin, bit for bit: the batch's remaining inverses are then those
- * of the gained spectra, each still served only after a bitwise check); entries
- * past the known ones are 0.  Negative: CRLOT_EINVAL. */
+ * of the gained spectra, each still served only after a bitwise check), [10]
+ * learned gains not applied because the previous one served fewer than four
+ * inverses and differed in more than an eighth of the bins (a time-varying
+ * edit: those frames take the per-call path, learning backs off for 16, 32, ..
+ * frames); entries past the known ones are 0.  Negative: CRLOT_EINVAL. */
 int crlot_call_speculation_stats_ex(int64_t* out, int32_t count);
 /* Bounds of the batched speculation: frames per window, and the device and
  * pinned host bytes the batches hold now, with the pinned peak since load. */

@@ -1348,3 +1348,67 @@ def test_random_pipeline_loop_batch_equals_per_call(pkg, oracle, torch_cuda, see
     for i, (u, v) in enumerate(zip(a, b)):
         assert u.shape == v.shape and np.array_equal(bits(u), bits(v)), (seed, i // 3, i % 3)
     assert served["forwards"] > len(a) // 6, served
+
+
+def _e2e_mask_loop(pkg, x, n, h, masks, pushed=None):
+    """The e2e loop with a time-varying spectral step: frame k's bins scaled by
+    masks[k % len(masks)] on the host between forward and inverse."""
+    w = pkg.window_table(pkg.HANN, n)
+    fr = pkg.Framer()
+    fr.set_params(n, h, 1, pkg.ZERO_PAD)
+    fft = pkg.FftPlan(n, pkg.FFT_REAL)
+    ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8,
+                                           apply_window_inside=True))
+    ola.set_window(w)
+    fr.push(x)
+    outs, k = [], 0
+    while True:
+        f = fr.pop()
+        if f is None:
+            break
+        X = np.asarray(fft.forward_host((f * w).astype(np.float32)[None])).copy()
+        g = masks[k % len(masks)]
+        X[0].real *= g
+        X[0].imag *= g
+        y = fft.inverse_host(X)[0]
+        ola.push_frame_AoS(y, None, k * h, 0, n, 1.0)
+        got, chans = ola.produce(h)
+        outs.append(chans[0][:got].copy())
+        if pushed is not None:
+            pushed.append((np.array(y, copy=True), k * h, 1.0, h))
+        k += 1
+    ola.close()
+    fft.close()
+    fr.close()
+    return (np.concatenate(outs), outs) if pushed is not None else np.concatenate(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h", [(1024, 256), (960, 240), (2048, 512)])
+def test_e2e_loop_with_time_varying_mask_backs_off(pkg, oracle, torch_cuda, n, h):
+    """A per-frame mask (a noise suppressor's shape: eight masks in turn) is no
+    fixed gain: after the first learned gain is replaced within a few frames by a
+    very different one, the batch stops redoing its window's inverses (each would
+    be a chain per frame) and backs off; the inverses take the per-call path, the
+    forwards are still served, and every bit equals the per-call path's."""
+    x = oracle.synth(48_000 * 2, 29)
+    masks = [(0.5 + 0.5 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2) + 0.7 * j)).astype(np.float32)
+             for j in range(8)]
+    try:
+        pkg.set_call_speculation(1)
+        a = _e2e_mask_loop(pkg, x, n, h, masks)
+        pkg.set_call_speculation(2)
+        b, served = _spec_delta(pkg, lambda: _e2e_mask_loop(pkg, x, n, h, masks))
+    finally:
+        pkg.set_call_speculation(2)
+    assert np.array_equal(bits(a), bits(b))
+    F = a.size // h
+    assert served["gains"] <= 2 and served["gain_backoffs"] >= 1, served
+    assert served["forwards"] == F, served
+    # the produce blocks (served from the chained inverse's speculation once the OLA
+    # object is off the batch) are the oracle OLAAccumulator's fed the same frames
+    pushed = []
+    _, blocks = _e2e_mask_loop(pkg, x, n, h, masks, pushed)
+    ref = _oracle_outputs(oracle, n, h, pkg.window_table(pkg.HANN, n), pushed)
+    for k in range(len(blocks)):
+        assert np.array_equal(bits(blocks[k]), bits(ref[k])), ("oracle", k)
