@@ -338,6 +338,25 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
             __syncthreads();
         }
         CALL_PH(4);  // deferred ring work done
+        // a chained inverse's produce block reads the ring (after the deferred work
+        // above) and the divisors: loaded now, in flight during the transform
+        constexpr int KI = 2;
+        float irv[KI], idv[KI];
+        if constexpr (CallLds<E>::CH > 0 || ANY) {
+            if (r.op == kCallIrfft && (r.flags & kCallChain) != 0 && r.batch == 1) {
+#pragma unroll
+                for (int k = 0; k < KI; ++k) {
+                    const int64_t q = t + int64_t(k) * kCallBlock;
+                    irv[k] = idv[k] = 1.0f;
+                    if (q < r.j[3]) {
+                        int64_t p = r.j[2] + q;
+                        if (p >= r.j[0]) p -= r.j[0];
+                        irv[k] = r.p2[p];
+                        idv[k] = r.p3[p];
+                    }
+                }
+            }
+        }
         const float* in = a.in_arena + r.in_off;  // r.in_off is the slot's start
         // the input floats this request reads: when they fit the prefetched 4 KB,
         // every read comes from LDS
@@ -666,17 +685,26 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 const float* wobj = r.p4;
                 const int64_t R = r.j[0], start = r.j[1], rp = r.j[2], n = r.j[3], Nf = 2 * Pr;
                 float* co = a.out_arena + r.spec_off + Nf;
-                for (int64_t q = t; q < n; q += kCallBlock) {
+                auto one = [&](int64_t q, float v, float dn) {
                     int64_t p = rp + q;
                     if (p >= R) p -= R;
-                    float v = ring[p];
                     int64_t d = p - start;
                     if (d < 0) d += R;
                     if (d < Nf) {
                         const float s0 = chainp[d];
                         v = wobj ? __builtin_fmaf(__builtin_fmaf(s0, wobj[d], 0.0f), r.f1, v) : __builtin_fmaf(s0, r.f1, v);
                     }
-                    co[q] = v / den[p];
+                    co[q] = v / dn;
+                };
+#pragma unroll
+                for (int k = 0; k < KI; ++k) {
+                    const int64_t q = t + int64_t(k) * kCallBlock;
+                    if (q < n) one(q, irv[k], idv[k]);
+                }
+                for (int64_t q = t + int64_t(KI) * kCallBlock; q < n; q += kCallBlock) {
+                    int64_t p = rp + q;
+                    if (p >= R) p -= R;
+                    one(q, ring[p], den[p]);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                 __syncthreads();
