@@ -204,6 +204,8 @@ int main() {
             pe.gain = 1.0f;
             pe.rp = r.j[2];
             pe.n = Hh;
+            pe.src_index = sl.index;     // the frame this request kept in LDS (the e2e loop's case)
+            pe.src_off = sl.spec_off;
             if (as->defer(pe) != CRLOT_OK) return 23;
         }
         std::printf("{\"chained_rfft%d\": {\"window\": %d, \"host_done_us_p50\": %.2f, \"dev_pend_end_us\": %.2f, "
