@@ -618,14 +618,14 @@ bool inverse_input_matches(const BatchSpec* b, int64_t j, const float* in) {
     const size_t row = size_t(b->n) + 2;
     const float* X = b->h_spec + b->row(j) * row;
     if (b->sgain.empty() || j < b->sgain_from) return std::memcmp(in, X, sizeof(float) * row) == 0;
-    thread_local std::vector<float> pred;
-    pred.resize(row);
+    // bin by bin, stopping at the first difference (an edit that changes every
+    // frame differs in the first bins: no full product row per call)
     const float* g = b->sgain.data();
     for (size_t k = 0; k < row / 2; ++k) {
-        pred[2 * k] = X[2 * k] * g[k];
-        pred[2 * k + 1] = X[2 * k + 1] * g[k];
+        const float p[2] = {X[2 * k] * g[k], X[2 * k + 1] * g[k]};
+        if (std::memcmp(p, in + 2 * k, sizeof(p)) != 0) return false;
     }
-    return std::memcmp(in, pred.data(), sizeof(float) * row) == 0;
+    return true;
 }
 
 // A real gain per bin that maps frame j's spectrum X onto the caller's input Y
