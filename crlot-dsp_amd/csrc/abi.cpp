@@ -1313,10 +1313,16 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
         }
         if (brc != 0) return brc < 0 ? brc : CRLOT_OK;
     }
-    p->pack.resize(std::max(nin, nout));
-    gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
+    // the request's input, dense: the caller's own buffer for one contiguous
+    // transform (no staging copy), else gathered
+    const float* dense = in;
+    if (!(batch == 1 && inc_in == 1)) {
+        p->pack.resize(std::max(nin, nout));
+        gather(in, p->pack.data(), batch, in_len, in_w, ld_in, inc_in);
+        dense = p->pack.data();
+    }
     if (kind == 1 && sh->fft.valid && sh->fft.index == sv->submitted() && sh->fft.batch == batch &&
-        sv->live(sh->fft.slot) && std::memcmp(p->pack.data(), sh->fft.slot.out, sizeof(float) * nin) == 0) {
+        sv->live(sh->fft.slot) && std::memcmp(dense, sh->fft.slot.out, sizeof(float) * nin) == 0) {
         // the spectrum the last forward returned, unchanged: its inverse is in the speculation slot
         sh->fft.valid = false;
         if ((rc = sv->wait_spec(sh->fft.index)) != CRLOT_OK) return rc;
@@ -1339,7 +1345,7 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
         return rc;
     crlot::CallSlot sl;
     if ((rc = sv->next_slot(&sl)) != CRLOT_OK) return rc;
-    sv->put(sl.in, p->pack.data(), nin);
+    sv->put(sl.in, dense, nin);
     crlot::CallReq r{};
     r.op = kind == 0 ? crlot::kCallRfft : kind == 1 ? crlot::kCallIrfft : kind == 2 ? crlot::kCallCfft : crlot::kCallIcfft;
     r.batch = batch;
