@@ -170,7 +170,7 @@ int CallServer::grow(size_t in_cap, size_t out_cap, size_t spec_cap) {
     rc = alloc(std::max(in_cap, in_cap_), std::max(out_cap, out_cap_), std::max(spec_cap, spec_cap_));
     if (rc != CRLOT_OK) return rc;
     q_ = q;
-    hctl_->done = hctl_->spec_done = hctl_->chain_done = q;
+    hctl_->done = hctl_->spec_done = hctl_->chain_done = hctl_->ring_done = q;
     store_ctl(&ctl_->seq, q);
     return CRLOT_OK;
 }
@@ -297,6 +297,7 @@ int CallServer::drain() {
     if (q_ == 0) return CRLOT_OK;
     if ((rc = wait_counter(&hctl_->done, q_)) != CRLOT_OK) return rc;
     if (last_chain_ && (rc = wait_counter(&hctl_->chain_done, last_chain_)) != CRLOT_OK) return rc;
+    if (last_late_ && (rc = wait_counter(&hctl_->ring_done, last_late_)) != CRLOT_OK) return rc;
     for (int i = 0; i < depth_; ++i)
         if (spec_req_[size_t(i)]) {
             rc = wait_counter(&hctl_->spec_done, spec_req_[size_t(i)]);
@@ -351,6 +352,7 @@ int CallServer::submit(CallReq& r, const CallSlot& sl) {
     r.pend = pend_;
     pend_ = CallReq::Pend{};
     if (r.flags & kCallChain) last_chain_ = q_ + 1;
+    if (r.flags & kCallPendLate) last_late_ = q_ + 1;
     const int k = int(q_ % uint64_t(depth_));
     if (wc_inputs_)
         copy_wc(reinterpret_cast<float*>(reqs_ + k), reinterpret_cast<const float*>(&r), sizeof(CallReq) / 4);

@@ -54,6 +54,7 @@ class CallServer {
     // state was written by kernels on other streams since the last request)
     void acquire_next() { acquire_next_ = true; }
     uint64_t submitted() const { return q_; }
+    const CallReq::Pend& pending() const { return pend_; }  // the ring work the next request carries
     // the slot's views still point into the current arenas (grow() reallocates
     // them: a speculation recorded before a grow is gone)
     bool live(const CallSlot& s) const { return s.gen == gen_ && gen_ != 0; }
@@ -94,6 +95,7 @@ class CallServer {
     std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
     uint64_t last_chain_ = 0;          // the last request with a chained produce
     CallReq::Pend pend_{};             // deferred ring work (flags 0: none)
+    uint64_t last_late_ = 0;           // the last request that ran its ring work late (kCallPendLate)
     uint64_t idle_ticks_ = 0;
     double tick_ns_ = 10.0;
 };

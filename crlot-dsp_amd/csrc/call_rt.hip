@@ -97,9 +97,11 @@ struct CallLds {
     static constexpr int TW = E > 0 ? dev::twiddle_table_size(E) : 1;
     static constexpr bool SPEC = E > 0 && E <= 16;
     static constexpr int SP = SPEC ? P + 1 : 0;
-    static constexpr int CH = SPEC ? 2 * P : 0;  // the chained frame (one speculated inverse, floats)
+    static constexpr int CH = SPEC ? 2 * P : 0;  // a chained frame (one inverse output, floats)
+    // two of them, by request parity: a late commit (kCallPendLate) reads the
+    // previous request's frame while this request keeps its own
     static constexpr size_t bytes = sizeof(cf) * (size_t(TW) + 2 * P + size_t(kCallWaves) * (P + SP)) +
-                                    sizeof(float) * (kCallPre + CH) + sizeof(CallReq) + 16;
+                                    sizeof(float) * (kCallPre + 2 * CH) + sizeof(CallReq) + 16;
 };
 
 // ---- FFTs, one wave per transform (k_rfft / k_irfft / k_cfft's arithmetic)
@@ -237,7 +239,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     constexpr bool ANY = E < 0;
     float* pre = ANY ? reinterpret_cast<float*>(smem) : reinterpret_cast<float*>(specs + kCallWaves * CallLds<E>::SP);
     float* chainbuf = pre + kCallPre;  // the frame a chained forward kept for the push that follows
-    CallReq* rq = reinterpret_cast<CallReq*>(chainbuf + CallLds<E>::CH);
+    CallReq* rq = reinterpret_cast<CallReq*>(chainbuf + 2 * CallLds<E>::CH);
     uint32_t* cmd = reinterpret_cast<uint32_t*>(rq + 1);
     // ANY: [plan][tw any_tw cf][st P cf][chain frame 2P f][per wave A, B (P cf), S (P + 1 cf)]
     dev::any::Plan* const aplan = reinterpret_cast<dev::any::Plan*>(reinterpret_cast<char*>(cmd) + 16);
@@ -246,7 +248,10 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
     cf* const ast = atw + (ANY ? a.any_tw : 0);
     float* const achain = reinterpret_cast<float*>(ast + (ANY ? a.any_p : 0));
     cf* const awaves = reinterpret_cast<cf*>(achain + (ANY ? 2 * a.any_p : 0));
-    float* const chainp = ANY ? achain : chainbuf;  // the kept frame of a chained forward or inverse
+    // the frame kept by chained request q (a forward's speculated inverse or an
+    // inverse request's output): buffer q % 2 (any size: one buffer, whose commits
+    // never run late)
+    auto chain_buf = [&](uint64_t q) -> float* { return ANY ? achain : chainbuf + ((q & 1) ? CallLds<E>::CH : 0); };
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     cf* buf = bufs + wave * P;
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
 
     uint64_t my = a.first;
     uint64_t t_last = wall_clock64();
-    uint64_t chain_req = 0;  // the chained forward (1-based) whose kept frame this launch holds in LDS
+    uint64_t chain_req[2] = {0, 0};  // the chained requests (1-based) whose frames this launch holds, by parity
     for (;;) {
         // ---- wait for request `my` (thread 0 polls device memory, the workgroup follows)
         if (t == 0) {
@@ -305,7 +310,8 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         }
         if (r.flags & kCallAcquire)  // device-form calls ran on streams since the last request
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (r.pend.flags) {
+        auto run_pend = [&]() {
+            if (!r.pend.flags) return;
             // deferred ring work: the push of the kept frame (the push's arithmetic on
             // the frame bits the host compared), then a served produce's clear
             float* ring = r.pend.ring;
@@ -316,7 +322,8 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                     // the LDS copy only survives within the launch that kept it (the
                     // kernel may have idled out and been relaunched since); else the
                     // same bits from the forward's speculation slot in host memory
-                    const bool lds = chain_req != 0 && chain_req == r.pend.src_index;
+                    const bool lds = r.pend.src_index != 0 && chain_req[r.pend.src_index & 1] == r.pend.src_index;
+                    const float* const chainp = chain_buf(r.pend.src_index);
                     const float* hsrc = a.out_arena + r.pend.src_off;
                     for (int64_t j = t; j < r.pend.len; j += kCallBlock) {
                         int64_t p = r.pend.start + j;
@@ -336,7 +343,46 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 }
             }
             __syncthreads();
+        };
+        // kCallPendLate: the ring work waits until this request's chained produce
+        // block (which adds the committed frame itself) is published
+        // (only where this request computes a chained produce block and then runs
+        // late_ring_work: a single-frame chained inverse, or forward with its
+        // speculation; a flag set anywhere else runs the work now and still
+        // publishes ring_done, so no host wait can miss it)
+        const bool late = CallLds<E>::CH > 0 && (r.flags & kCallPendLate) != 0 && (r.pend.flags & kPendCommit) != 0 &&
+                          (r.flags & kCallChain) != 0 && r.batch == 1 &&
+                          (r.op == kCallIrfft || (r.op == kCallRfft && (r.flags & kCallSpec) != 0));
+        if (!late) {
+            run_pend();
+            if (r.flags & kCallPendLate) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                __syncthreads();
+                if (t == 0) st_sys64(&a.hctl->ring_done, my + 1);
+            }
         }
+        // the late commit's frame added to a produce value at ring position p: the
+        // commit's own arithmetic on the ring value before it (bit for bit what the
+        // produce would read after the commit)
+        auto prev_add = [&](int64_t p, float v) -> float {
+            if (!late) return v;
+            int64_t d = p - r.pend.start;
+            if (d < 0) d += r.pend.R;
+            if (d < r.pend.len) {
+                const bool lds = r.pend.src_index != 0 && chain_req[r.pend.src_index & 1] == r.pend.src_index;
+                const float s0 = lds ? chain_buf(r.pend.src_index)[d] : ld_sys32(a.out_arena + r.pend.src_off + d);
+                v = r.pend.win ? __builtin_fmaf(__builtin_fmaf(s0, r.pend.win[d], 0.0f), r.pend.gain, v)
+                               : __builtin_fmaf(s0, r.pend.gain, v);
+            }
+            return v;
+        };
+        auto late_ring_work = [&]() {
+            if (!late) return;
+            run_pend();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            __syncthreads();
+            if (t == 0) st_sys64(&a.hctl->ring_done, my);
+        };
         CALL_PH(4);  // deferred ring work done
         // a chained inverse's produce block reads the ring (after the deferred work
         // above) and the divisors: loaded now, in flight during the transform
@@ -418,7 +464,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                     call_irfft<E>([&](int k) {
                         const float2 v = cin.at2(x + 2 * k);
                         return cf{v.x, v.y};
-                    }, out + int64_t(b) * 2 * P, buf, tw, st, r.f0, lane, ich ? chainp : nullptr);
+                    }, out + int64_t(b) * 2 * P, buf, tw, st, r.f0, lane, ich ? chain_buf(my + 1) : nullptr);
                 }
                 });
             } else if (r.op == kCallCfft || r.op == kCallIcfft) {
@@ -497,7 +543,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                             for (int i = tid; i < Pn; i += nth) {
                                 const float2 v = make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0));
                                 *reinterpret_cast<float2*>(o + 2 * i) = v;
-                                if (ich) *reinterpret_cast<float2*>(chainp + 2 * i) = v;
+                                if (ich) *reinterpret_cast<float2*>(chain_buf(my + 1) + 2 * i) = v;
                             }
                         } else {
                             const int64_t x = int64_t(b) * 2 * Pn;
@@ -679,7 +725,8 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
         // speculation slot after one frame's floats
         if constexpr (CallLds<E>::CH > 0 || ANY) {
             if (r.op == kCallIrfft && (r.flags & kCallChain) != 0 && r.batch == 1) {
-                chain_req = my;
+                chain_req[my & 1] = my;
+                const float* const chainp = chain_buf(my);
                 float* ring = r.p2;
                 const float* den = r.p3;
                 const float* wobj = r.p4;
@@ -688,6 +735,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 auto one = [&](int64_t q, float v, float dn) {
                     int64_t p = rp + q;
                     if (p >= R) p -= R;
+                    v = prev_add(p, v);  // (a late commit's frame first, as the ring would hold it)
                     int64_t d = p - start;
                     if (d < 0) d += R;
                     if (d < Nf) {
@@ -709,6 +757,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                 __syncthreads();
                 if (t == 0) st_sys64(&a.hctl->chain_done, my);
+                late_ring_work();
             }
         }
 
@@ -740,7 +789,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                 if constexpr (E > 0) {
                     for (int b = wave; b < r.batch; b += kCallWaves)
                         call_irfft<E>([&](int k) { return spb[k]; }, so + int64_t(b) * 2 * P, buf, tw, st, r.f0,
-                                      lane, chain ? chainp : nullptr);
+                                      lane, chain ? chain_buf(my) : nullptr);
                 }
                 if constexpr (ANY) {
                     const bool wg = r.batch == 1;  // as the forward: its S buffer
@@ -759,14 +808,15 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                             for (int i = tid; i < Pn; i += nth) {
                                 const float2 v = make_float2(dev::sanit(z[i].r * r.f0), dev::sanit(z[i].i * r.f0));
                                 *reinterpret_cast<float2*>(o + 2 * i) = v;
-                                if (chain) *reinterpret_cast<float2*>(chainp + 2 * i) = v;
+                                if (chain) *reinterpret_cast<float2*>(chain_buf(my) + 2 * i) = v;
                             }
                             any_sync(wg);
                         }
                     }
                 }
                 if (chain) {
-                    chain_req = my;
+                    chain_req[my & 1] = my;
+                    const float* const chainp = chain_buf(my);
                     // publish the inverse first: the host's inverse call waits for it
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                     __syncthreads();
@@ -782,6 +832,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                     auto one = [&](int64_t q, float v, float dn) {
                         int64_t p = rp + q;
                         if (p >= R) p -= R;
+                        v = prev_add(p, v);  // (a late commit's frame first, as the ring would hold it)
                         int64_t d = p - start;
                         if (d < 0) d += R;
                         if (d < Nf) {
@@ -804,6 +855,7 @@ __global__ __launch_bounds__(kCallBlock) void k_call(const CallArgs a) {
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
                     __syncthreads();
                     if (t == 0) st_sys64(&a.hctl->chain_done, my);
+                    late_ring_work();
                 }
             }
             CALL_PH(2);

@@ -270,7 +270,11 @@ enum : uint32_t {
 };  // op 0: nothing but the request's deferred ring work (CallPend)
 // kCallChain (on a speculating forward): also keep the speculated inverse frame
 // and compute the produce block the target OLA object would give after pushing it
-enum : uint32_t { kCallSpec = 1, kCallClearOnly = 2, kCallAcquire = 4, kCallChain = 8 };
+// kCallPendLate (on a chained single-frame request whose deferred commit pushes
+// into the chain's own ring, its clear disjoint from the produce block): the
+// produce block adds that commit's frame itself, and the deferred ring work runs
+// after chain_done, published as ring_done
+enum : uint32_t { kCallSpec = 1, kCallClearOnly = 2, kCallAcquire = 4, kCallChain = 8, kCallPendLate = 16 };
 struct alignas(512) CallReq {
     uint32_t op, flags;
     int32_t batch, channels;
@@ -319,6 +323,8 @@ struct alignas(64) CallHostCtl {  // pinned host memory, written by the kernel
     uint64_t pad1[7];
     uint64_t chain_done;          // forwards whose chained produce block is written
     uint64_t pad2[7];
+    uint64_t ring_done;           // requests whose late deferred ring work (kCallPendLate) is done
+    uint64_t pad3[7];
     uint64_t ph[8];               // -DCRLOT_CALL_PHASES builds: the last request's phase stamps
 };
 struct CallArgs {
