@@ -148,20 +148,23 @@ def cpu_baseline(n_streams: int = 1024, reps: int = CPU_REPS):
 
 
 def load_pmc_traffic(workload_key: str):
-    """HBM bytes per launch from the newest profiles/*pmc_summary.json of this
-    workload; null (stale) unless it was taken of the same kernel sources."""
+    """HBM bytes per launch from the profiles/*pmc_summary.json of this workload
+    taken of the same kernel sources (else the last by name, reported stale:
+    null)."""
     pdir = os.path.join(ROOT, "profiles")
-    best, best_f = None, None
+    cur = src_hash()
+    best, best_f, match = None, None, False
     for f in sorted(glob.glob(os.path.join(pdir, "*pmc_summary.json"))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
         if d.get("workload_key") == workload_key:
-            best, best_f = d, f
+            same = d.get("src_hash") == cur
+            if same or not match:
+                best, best_f, match = d, f, same
     if best is None:
         return None, {"file": None, "stale": True, "note": "no PMC profile of this workload"}
-    cur = src_hash()
     stale = best.get("src_hash") != cur
     meta = {"file": os.path.relpath(best_f, ROOT), "kernel": best.get("kernel"),
             "profile_src_hash": best.get("src_hash"), "src_hash": cur, "stale": stale,

@@ -1367,15 +1367,15 @@ int fft_host(crlot_fft_plan* p, int kind, const float* in, float* out, int32_t b
         r.f1 = pred.gain;
         // the previous frame's deferred push (riding on this request) into the same
         // ring: the chained produce block adds it itself and the ring work runs
-        // after the block is published (kCallPendLate; the power-of-two servers,
-        // whose LDS keeps both frames), unless the deferred clear meets the block
+        // after the block is published (kCallPendLate; where the server's LDS keeps
+        // both frames), unless the deferred clear meets the block
         const crlot::CallReq::Pend& pe = sv->pending();
         const int64_t R = pred.R;
         auto apart = [R](int64_t a0, int64_t an, int64_t b0, int64_t bn) {  // disjoint ring intervals
             const int64_t ab = ((b0 - a0) % R + R) % R, ba = ((a0 - b0) % R + R) % R;
             return ab >= an && ba >= bn;
         };
-        if (p->e > 0 && (pe.flags & crlot::kPendCommit) && pe.ring == pred.ring && pe.R == R &&
+        if ((p->e > 0 || sh->any_two) && (pe.flags & crlot::kPendCommit) && pe.ring == pred.ring && pe.R == R &&
             pe.src_index == sv->submitted() && pe.len <= R &&
             (!(pe.flags & crlot::kPendClear) || apart(pe.rp, pe.n, pred.rp % R, pred.n)))
             r.flags |= crlot::kCallPendLate;

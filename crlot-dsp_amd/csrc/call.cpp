@@ -442,6 +442,7 @@ SharedServer* shared_server_any(int device, int P, int* rc) {
         SharedServer* n = new SharedServer();
         n->e = -P;
         n->any_waves = waves;
+        n->any_two = call_any_two(P);
         const std::vector<float> tw = build_any_twiddles(P);
         const std::vector<uint8_t> plan = build_any_plan_blob(P);
         std::vector<float> st(2 * size_t(P));

@@ -134,6 +134,7 @@ struct SharedServer {
     float* d_st = nullptr;
     void* d_plan = nullptr; // e < 0 (any size): the Stockham pass plan (device, owned)
     int any_waves = 0;      // ... and how many transforms one request runs at once
+    bool any_two = false;   // ... and whether its LDS keeps two chained frames (late commits)
     struct FftSpec {        // the inverse speculated after the last forward
         bool valid = false;
         uint64_t index = 0;

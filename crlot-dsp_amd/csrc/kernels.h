@@ -338,11 +338,13 @@ struct CallArgs {
     uint64_t first = 0;             // requests completed before this launch
     uint64_t idle_ticks = 0;
     int any_p = 0, any_waves = 0, any_tw = 0;  // e < 0: complex points, FFT waves, twiddles (launch_call)
+    int any_two = 0;                           // e < 0: two chained frames in LDS (call_any_two)
 };
 // e = 0 (OLA / kernel ops only), the FFT's E = P / 64 in {2, 4, 8, 16, 32}, or
 // -P for any other complex size P (fft_any.h; call_any_waves(P) > 0)
 size_t call_lds_bytes(int e);
 int call_any_waves(int p);
+bool call_any_two(int p);
 hipError_t launch_call(int e, const CallArgs& a, hipStream_t s);
 
 // dsp::axpy / axpy_windowed (win != nullptr) / normalize_and_clear over `batch`
