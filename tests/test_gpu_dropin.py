@@ -1384,13 +1384,15 @@ def _e2e_mask_loop(pkg, x, n, h, masks, pushed=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,h", [(1024, 256), (960, 240), (2048, 512)])
+@pytest.mark.parametrize("n,h", [(1024, 256), (960, 240), (2048, 512), (3840, 960), (4000, 1000)])
 def test_e2e_loop_with_time_varying_mask_backs_off(pkg, oracle, torch_cuda, n, h):
     """A per-frame mask (a noise suppressor's shape: eight masks in turn) is no
     fixed gain: after the first learned gain is replaced within a few frames by a
     very different one, the batch stops redoing its window's inverses (each would
     be a chain per frame) and backs off; the inverses take the per-call path, the
-    forwards are still served, and every bit equals the per-call path's."""
+    forwards are still served, and every bit equals the per-call path's.
+    (3840: the any-size server keeps two chained frames and runs its ring commits
+    late; 4000: its LDS keeps one, the commits run before the transform.)"""
     x = oracle.synth(48_000 * 2, 29)
     masks = [(0.5 + 0.5 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2) + 0.7 * j)).astype(np.float32)
              for j in range(8)]
