@@ -632,8 +632,133 @@ def suite_pipeline(pkg, torch, dev):
     return res
 
 
+def stft_bytes_per_sample(n: int, h: int) -> float:
+    """Algorithmic HBM bytes per input sample of crlot_stft (4 read + the spectra,
+    8 (N/2+1) per frame written) -- and of crlot_istft_ola, the other way round."""
+    return 4.0 + 8.0 * (n // 2 + 1) / h
+
+
+def suite_stft(pkg, torch, dev):
+    """the round trip split at its spectral step
+    (bench/e2e_benchmark.cc:160-162).  At 1024 streams x 480 000 per shape:
+    crlot_stft (x -> spectra), crlot_istft_ola (spectra -> y), both back to back,
+    the round trip with a per-frame mask shared by the streams and with one per
+    stream and frame (crlot_plan_set_spectral_mask: one walk over HBM), and the
+    unmasked round trip beside them; each priced against HBM with its algorithmic
+    bytes.  Then the e2e harness's time-varying mask on one 1 s window of 48 kHz
+    audio (188 frames at 1024/256): host x -> device -> masked round trip (and
+    stft -> a torch edit -> istft_ola) -> host y, per frame, next to the oracle's
+    single-thread masked loop."""
+    O, native = _oracle()
+    res = {"suite": "stft", "reference": "bench/e2e_benchmark.cc:160-162", "shapes": []}
+    S, T = STREAMS, T_LEN
+    g = torch.Generator(device=dev).manual_seed(41)
+    x = (torch.rand((S, T), generator=g, device=dev) * 2 - 1) * 0.5
+    for n, h in ((1024, 256), (4096, 1024), (512, 128)):
+        plan = pkg.Plan(frame_size=n, hop_size=h, device=dev.index)
+        F, bins = plan.frame_count(T), n // 2 + 1
+        spec = torch.empty((S, F, bins), dtype=torch.complex64, device=dev)
+        y = torch.empty((S, F * h), device=dev)
+        samples = S * T
+        b1 = stft_bytes_per_sample(n, h)
+
+        def row(name, ms, bps, kern=None):
+            gbs = bps * samples / (ms * 1e-3) / 1e9
+            r = {"op": name, "ms": round(ms, 4), "msamples_s": round(samples / ms / 1e3, 1),
+                 "bytes_per_sample": round(bps, 3), "gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+            if kern:
+                r["kernels"] = kern
+            return r
+
+        t_st = _ev_time(torch, lambda: plan.stft(x, spec), 10)
+        k_st = plan.last_launch()["kernels"]
+        t_is = _ev_time(torch, lambda: plan.istft_ola(spec, y), 10)
+        k_is = plan.last_launch()["kernels"]
+        t_both = _ev_time(torch, lambda: (plan.stft(x, spec), plan.istft_ola(spec, y)), 10)
+        shape = {"frame": n, "hop": h, "streams": S, "samples_per_stream": T, "frames_per_stream": F, "runs": [
+            row("stft", t_st, b1, k_st), row("istft_ola", t_is, b1, k_is),
+            row("stft+istft_ola", t_both, 2 * b1)]}
+        del spec
+        mask = torch.rand((F, bins), generator=g, device=dev)
+        plan.set_spectral_mask(mask)
+        t_m = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)
+        shape["runs"].append(row("roundtrip, mask shared by the streams", t_m, 8.0, plan.last_launch()["kernels"]))
+        del mask
+        mask = torch.rand((S, F, bins), generator=g, device=dev)
+        plan.set_spectral_mask(mask)
+        t_ms = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)
+        shape["runs"].append(row("roundtrip, mask per stream and frame", t_ms, 8.0 + 4.0 * bins / h,
+                                 plan.last_launch()["kernels"]))
+        plan.set_spectral_mask(None)
+        del mask
+        t_r = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)
+        shape["runs"].append(row("roundtrip (no mask)", t_r, 8.0, plan.last_launch()["kernels"]))
+        res["shapes"].append(shape)
+        del y
+        torch.cuda.empty_cache()
+    del x
+    torch.cuda.empty_cache()
+    # the e2e harness's spectral_mask row on one window: 1 s of the 3-tone signal,
+    # 8 masks in turn (frame k takes mask k % 8), as harness/e2e_bench does per call
+    n, h = 1024, 256
+    t = np.arange(48000) / 48000.0
+    xh = (0.5 * np.sin(2 * np.pi * 440 * t) + 0.3 * np.sin(2 * np.pi * 880 * t)
+          + 0.2 * np.sin(2 * np.pi * 1320 * t)).astype(np.float32)
+    plan = pkg.Plan(frame_size=n, hop_size=h, device=dev.index)
+    F, bins = plan.frame_count(xh.size), n // 2 + 1
+    kk = np.arange(bins) / (bins - 1)
+    masks = np.stack([(0.5 + 0.5 * np.cos(np.pi * kk * (1 + j / 8.0))) for j in range(8)]).astype(np.float32)
+    rows = masks[np.arange(F) % 8]
+    mask_d = torch.from_numpy(rows).to(dev)
+    x_pin = torch.from_numpy(xh[None].copy()).pin_memory()
+    y_pin = torch.empty((1, F * h)).pin_memory()
+    xd = torch.empty((1, xh.size), device=dev)
+    yd = torch.empty((1, F * h), device=dev)
+    specd = torch.empty((1, F, bins), dtype=torch.complex64, device=dev)
+
+    def masked_walk():
+        xd.copy_(x_pin, non_blocking=True)
+        plan.roundtrip(xd, yd)
+        y_pin.copy_(yd, non_blocking=True)
+
+    def split_edit():
+        xd.copy_(x_pin, non_blocking=True)
+        plan.stft(xd, specd)
+        specd.mul_(mask_d[None])  # any device-side edit between the halves
+        plan.istft_ola(specd, yd)
+        y_pin.copy_(yd, non_blocking=True)
+
+    plan.set_spectral_mask(mask_d)
+    us_walk = _sync_latency_us(torch, masked_walk, 300)
+    y_walk = y_pin.numpy().copy()
+    plan.set_spectral_mask(None)
+    us_split = _sync_latency_us(torch, split_edit, 300)
+    y_split = y_pin.numpy().copy()
+    L = O.lib(native)
+    yc = np.zeros(F * h, np.float32)
+    ts = []
+    for _ in range(6):
+        t0 = time.perf_counter()
+        L.or_roundtrip_mask(xh, xh.size, n, h, O.HANN, 0, O.ZERO_PAD, 1, O.PAD_CONSTANT, 1, None,
+                            np.ascontiguousarray(rows).ctypes.data, bins, yc, F * h, None)
+        ts.append(time.perf_counter() - t0)
+    cpu_us = sorted(ts[1:])[2] * 1e6
+    d = y_walk[0].astype(np.float64) - yc
+    res["e2e_window"] = {
+        "frame": n, "hop": h, "samples": int(xh.size), "frames": F, "masks": 8,
+        "masked_roundtrip_us_per_window_p50": us_walk, "masked_roundtrip_us_per_frame": round(us_walk / F, 3),
+        "stft_edit_istft_us_per_window_p50": us_split, "stft_edit_istft_us_per_frame": round(us_split / F, 3),
+        "includes": "H2D of x and D2H of y (pinned), launch and synchronize",
+        "cpu_oracle_1thread": {"us_per_window": round(cpu_us, 1), "us_per_frame": round(cpu_us / F, 3)},
+        "rel_l2_vs_oracle": float(np.linalg.norm(d) / np.linalg.norm(yc)),
+        "split_equals_walk_bits": bool(np.array_equal(y_walk.view(np.uint32), y_split.view(np.uint32)))}
+    res["cpu_native_build"] = native
+    return res
+
+
 SUITES = {"ola": suite_ola, "multichannel": suite_multichannel, "fft": suite_fft, "streaming": suite_streaming,
-          "config1": suite_config1, "e2e": suite_e2e, "kernels": suite_kernels, "pipeline": suite_pipeline}
+          "config1": suite_config1, "e2e": suite_e2e, "kernels": suite_kernels, "pipeline": suite_pipeline,
+          "stft": suite_stft}
 
 
 def run_suite(name):

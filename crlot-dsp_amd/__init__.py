@@ -133,6 +133,9 @@ def lib():
         "crlot_ola_gather": ([vp, vp, vp, i32, i64, i64, i64, vp], C.c_int),
         "crlot_rfft_batched": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
         "crlot_irfft_batched": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_plan_set_spectral_mask": ([vp, vp, i64, i64], C.c_int),
+        "crlot_stft": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
+        "crlot_istft_ola": ([vp, vp, vp, i32, i64, i64, i64, i64, vp], C.c_int),
         "crlot_fft_plan_create": ([C.POINTER(FftDesc), C.POINTER(vp)], C.c_int),
         "crlot_fft_plan_destroy": ([vp], None),
         "crlot_fft_plan_info": ([vp, C.POINTER(i32), C.POINTER(i32)], C.c_int),
@@ -454,6 +457,63 @@ class Plan:
             raise ValueError("gain needs N/2+1 bins")
         _check(lib().crlot_plan_set_spectral_gain_async(self._h, None if g is None else g.ctypes.data,
                                                         self._cur_stream()))
+
+    def set_spectral_mask(self, mask=None):
+        """Time-varying spectral step (crlot_plan_set_spectral_mask): mask is a
+        float32 device tensor (S, F, N/2+1) -- one real row per stream and frame --
+        or (F, N/2+1), one row per frame shared by every stream; None clears it.
+        The plan keeps a reference to the tensor until it is replaced."""
+        if mask is None:
+            self._mask = None
+            _check(lib().crlot_plan_set_spectral_mask(self._h, None, 0, 0), "crlot_plan_set_spectral_mask")
+            return
+        bins = self.frame_size // 2 + 1
+        if not mask.is_cuda or mask.shape[-1] != bins or mask.stride(-1) != 1 or mask.dim() not in (2, 3):
+            raise ValueError("mask must be a (S, F, N/2+1) or (F, N/2+1) device tensor with contiguous rows")
+        ld_frame = _ld(mask, -2, bins)
+        ld_stream = 0 if mask.dim() == 2 else _ld(mask, 0, mask.shape[1] * ld_frame)
+        self._mask = mask
+        _check(lib().crlot_plan_set_spectral_mask(self._h, mask.data_ptr(), ld_frame, ld_stream),
+               "crlot_plan_set_spectral_mask")
+
+    def stft(self, x, spec=None, stream: int | None = None):
+        """x: (S, T) float32 device tensor -> spec: (S, F, N/2+1) complex64, frame *
+        analysis window then IFftPlan::forward per frame (crlot_stft)."""
+        torch = _torch()
+        if x.dim() == 1:
+            return self.stft(x[None], None if spec is None else spec[None], stream)[0]
+        S, T = x.shape
+        if x.dtype != torch.float32 or not x.is_cuda or x.stride(1) != 1:
+            raise ValueError("x must be a float32 device tensor with contiguous rows")
+        F, bins = self.frame_count(T), self.frame_size // 2 + 1
+        if spec is None:
+            spec = torch.empty((S, F, bins), dtype=torch.complex64, device=x.device)
+        if spec.dtype != torch.complex64 or spec.shape != (S, F, bins) or spec.stride(2) != 1:
+            raise ValueError("spec must be (S, F, N/2+1) complex64 with contiguous rows")
+        s = _stream_handle(x) if stream is None else stream
+        _check(lib().crlot_stft(self._h, x.data_ptr(), spec.data_ptr(), S, T, _ld(x, 0, T),
+                                2 * _ld(spec, 0, F * bins), 2 * _ld(spec, 1, bins), s), "crlot_stft")
+        return spec
+
+    def istft_ola(self, spec, y=None, stream: int | None = None):
+        """spec: (S, F, N/2+1) complex64 device tensor -> y: (S, F*H): the spectral
+        step, IFftPlan::inverse, overlap-add and produce (crlot_istft_ola)."""
+        torch = _torch()
+        if spec.dim() == 2:
+            return self.istft_ola(spec[None], None if y is None else y[None], stream)[0]
+        S, F, bins = spec.shape
+        if spec.dtype != torch.complex64 or not spec.is_cuda or bins != self.frame_size // 2 + 1 or \
+                spec.stride(2) != 1:
+            raise ValueError("spec must be (S, F, N/2+1) complex64 with contiguous rows")
+        L = F * self.hop_size
+        if y is None:
+            y = torch.empty((S, L), dtype=torch.float32, device=spec.device)
+        if y.shape[0] != S or y.shape[1] < L or y.stride(1) != 1:
+            raise ValueError("bad y shape")
+        s = _stream_handle(spec) if stream is None else stream
+        _check(lib().crlot_istft_ola(self._h, spec.data_ptr(), y.data_ptr(), S, F, 2 * _ld(spec, 0, F * bins),
+                                     2 * _ld(spec, 1, bins), _ld(y, 0, L), s), "crlot_istft_ola")
+        return y
 
     # -- hot path
     def roundtrip(self, x, y=None, stream: int | None = None):

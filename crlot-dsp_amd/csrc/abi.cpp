@@ -69,6 +69,8 @@ struct crlot_plan {
     float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024: 64 lanes, N = 4096: 256)
     float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
+    // per-frame spectral mask (crlot_plan_set_spectral_mask): caller-owned device rows
+    crlot::SpecMask mask;
     bool pairing = true;      // crlot_plan_set_frame_pairing
     bool hot = true;          // ... 2: pairing with the two-regime walkers only
     std::atomic<int> chunks{0};  // crlot_plan_set_chunks (0: the library's chunking)
@@ -439,6 +441,19 @@ int64_t frames_for(const crlot_plan* p, int64_t T) {
 bool aligned8(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 7u) == 0; }
 bool aligned4(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 3u) == 0; }
 
+// the walk of K_istft: power-of-two N, H % 128 == 0, N % H == 0, the exact-rewrite
+// tables, whole ring blocks and 8-byte aligned output rows
+bool istft_walk_ok(const crlot_plan* p, const float* y, int64_t ld_y) {
+    return !p->generic && crlot::istft_walk_supported(p->geo.n, p->geo.h) && p->geo.ring_len % p->geo.h == 0 &&
+           p->fast_ok && aligned8(y) && ld_y % 2 == 0;
+}
+
+// (x rows may be 4-byte aligned only: the walk's frame loads check the alignment per frame)
+bool masked_walk_ok(const crlot_plan* p, const float* y, int64_t ld_y) {
+    return istft_walk_ok(p, y, ld_y) && (p->geo.pad & 1) == 0;
+}
+
+
 }  // namespace
 
 namespace crlot {
@@ -753,6 +768,9 @@ static void scratch_need(const crlot_plan* p, int32_t n_streams, int64_t T, int3
     const bool fused = use_fused(p, probe, const_cast<float*>(probe), T + (T & 1), L + (L & 1), int32_t(S), T, L);
     const bool any = p->generic && crlot::fused_any_fits(p->geo.n, p->geo.h);
     *work = (fused || any) ? 0 : S * F * p->geo.n * int64_t(sizeof(float));
+    if (p->mask.p)  // the masked round trip: one walk, or spectra + frames through HBM
+        *work = masked_walk_ok(p, probe, L + (L & 1)) ? 0
+                                                                        : S * F * (2 * p->geo.n + 2) * int64_t(sizeof(float));
 }
 
 int crlot_plan_reserve_stream(crlot_plan* p, int32_t n_streams, int64_t T, int32_t channels, void* stream) {
@@ -775,8 +793,12 @@ int crlot_plan_reserve_stream(crlot_plan* p, int32_t n_streams, int64_t T, int32
     return rc;
 }
 
+static int masked_roundtrip(crlot_plan* p, crlot::Scratch* sc, const float* d_x, float* d_y, int32_t n_streams,
+                            int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, hipStream_t s);
+
 static int roundtrip_impl(crlot_plan* p, crlot::Scratch* sc, const float* d_x, float* d_y, int32_t n_streams,
                           int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, hipStream_t s) {
+    if (p->mask.p) return masked_roundtrip(p, sc, d_x, d_y, n_streams, T, ld_x, ld_y, F, s);
     const int64_t out_len = F * p->geo.h;
     hipError_t e;
     const bool fused = use_fused(p, d_x, d_y, ld_x, ld_y, n_streams, T, out_len);
@@ -900,7 +922,7 @@ int crlot_roundtrip_interleaved(crlot_plan* p, const float* d_x, float* d_y, int
         const char* v = crlot::ab_env("CRLOT_ILV_3PASS");  // A/B: always deinterleave -> planes -> interleave
         return v && v[0] == '1';
     }();
-    if (!three_pass && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0 && aligned4(d_x) &&
+    if (!three_pass && !p->mask.p && channels <= 5 && p->geo.n == 1024 && p->geo.pad_mode == 0 && aligned4(d_x) &&
         aligned4(d_y)) {
         const int rcf = ensure_pair_flags(p, sc, int32_t(n_groups * C), F);
         if (rcf != CRLOT_OK) return rcf;
@@ -997,6 +1019,170 @@ int crlot_irfft_batched(crlot_plan* p, const float* d_in, float* d_out, int32_t 
     if (e != hipSuccess) return hip_fail(e, "irfft kernel launch");
     return CRLOT_OK;
 }
+
+// ------------------------------------------------------------------ the spectral step
+// crlot_stft / crlot_istft_ola split the round trip at the spectral step
+// (e2e_benchmark.cc:160-162) so device-side processing can sit between the
+// halves; crlot_plan_set_spectral_mask makes the step time-varying (stft.hip).
+// The plan's per-bin gain, then the mask row of the frame, scale the spectrum
+// in crlot_istft_ola and in the masked crlot_roundtrip, which equals
+// crlot_istft_ola(crlot_stft(x)) bit for bit.
+namespace {
+
+// x -> spectra; `work` holds S F N floats of windowed frames when the frame size
+// takes the mixed-radix rfft (else unused)
+int stft_impl(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams, int64_t T, int64_t ld_x, int64_t F,
+              int64_t ld_spec, int64_t ld_frame, float* work, hipStream_t s) {
+    const crlot::DevTables t = tables(p);
+    hipError_t e;
+    if (!p->generic && crlot::stft_supported(p->geo.n)) {
+        e = crlot::launch_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft kernel launch");
+    }
+    // other sizes: the windowed frames, then IFftPlan::forward on each (crlot_rfft_batched's kernel)
+    e = crlot::launch_frames_windowed(p->geo, t, d_x, n_streams, T, ld_x, F, work, s);
+    if (e != hipSuccess) return hip_fail(e, "frames kernel launch");
+    const int P = p->geo.n / 2, n = p->geo.n;
+    const int64_t rows = int64_t(n_streams) * F;
+    if (ld_spec == F * ld_frame && rows <= INT32_MAX) {
+        e = crlot::launch_fft_any(0, P, p->geo.inv_n, t, p->d_twany, work, d_spec, int(rows), n, 1, ld_frame, 1, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "rfft kernel launch");
+    }
+    for (int32_t i = 0; i < n_streams; ++i) {
+        e = crlot::launch_fft_any(0, P, p->geo.inv_n, t, p->d_twany, work + int64_t(i) * F * n,
+                                  d_spec + int64_t(i) * ld_spec, int(F), n, 1, ld_frame, 1, s);
+        if (e != hipSuccess) return hip_fail(e, "rfft kernel launch");
+    }
+    return CRLOT_OK;
+}
+
+// spectra -> step -> y.  Staged (no K_istft walk): `specw` receives the stepped
+// spectra as flat rows of N+2 floats (may be d_spec itself when that already
+// has this layout: the step runs in place), `frames` S F N floats.
+int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams, int64_t F, int64_t ld_spec,
+               int64_t ld_frame, int64_t ld_y, float* specw, float* frames, hipStream_t s) {
+    const crlot::DevTables t = tables(p);
+    hipError_t e;
+    if (istft_walk_ok(p, d_y, ld_y)) {
+        e = crlot::launch_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft kernel launch");
+    }
+    const int n = p->geo.n, bins = n / 2 + 1;
+    const int64_t rows = int64_t(n_streams) * F;
+    if (rows > INT32_MAX) return fail(CRLOT_EUNSUPPORTED, "too many frames for one call");
+    const float* src = d_spec;
+    int64_t ldf = ld_frame;
+    if (t.gain || p->mask.p || ld_spec != F * ld_frame) {
+        e = crlot::launch_spec_step(t, p->mask, d_spec, ld_spec, ld_frame, specw, n_streams, F, bins, s);
+        if (e != hipSuccess) return hip_fail(e, "spectral step kernel launch");
+        src = specw;
+        ldf = 2 * bins;
+    }
+    e = p->generic ? crlot::launch_fft_any(1, n / 2, p->geo.inv_n, t, p->d_twany, src, frames, int(rows), ldf, 1, n,
+                                           1, s)
+                   : crlot::launch_irfft(p->geo, t, src, frames, int(rows), ldf, 1, n, 1, s);
+    if (e != hipSuccess) return hip_fail(e, "irfft kernel launch");
+    e = crlot::launch_ola_gather(p->geo, t, frames, n, d_y, n_streams, F, ld_y, F * p->geo.h, s);
+    return e == hipSuccess ? CRLOT_OK : hip_fail(e, "gather kernel launch");
+}
+
+}  // namespace
+
+static int masked_roundtrip(crlot_plan* p, crlot::Scratch* sc, const float* d_x, float* d_y, int32_t n_streams,
+                            int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, hipStream_t s) {
+    if (masked_walk_ok(p, d_y, ld_y)) {
+        const hipError_t e = crlot::launch_roundtrip_masked(p->geo, tables(p), p->mask, d_x, d_y, n_streams, T, ld_x,
+                                                            ld_y, F, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "masked round trip kernel launch");
+    }
+    // through HBM: spectra (flat rows of N+2 floats), then the synthesis half
+    const int64_t row = p->geo.n + 2, sp = int64_t(n_streams) * F * row;
+    int rc = ensure_workspace(sc, (sp + int64_t(n_streams) * F * p->geo.n) * int64_t(sizeof(float)));
+    if (rc != CRLOT_OK) return rc;
+    float* spec = sc->work;
+    float* frames = sc->work + sp;
+    rc = stft_impl(p, d_x, spec, n_streams, T, ld_x, F, F * row, row, frames, s);
+    if (rc != CRLOT_OK) return rc;
+    return istft_impl(p, spec, d_y, n_streams, F, F * row, row, ld_y, spec, frames, s);
+}
+
+extern "C" {
+
+int crlot_plan_set_spectral_mask(crlot_plan* p, const float* d_mask, int64_t ld_frame, int64_t ld_stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!d_mask) {
+        p->mask = crlot::SpecMask{};
+        return CRLOT_OK;
+    }
+    if (ld_frame < p->geo.n / 2 + 1 || ld_stream < 0) return fail(CRLOT_EINVAL, "mask leading dimension too small");
+    if (!aligned4(d_mask)) return fail(CRLOT_EINVAL, "mask rows must be 4-byte aligned floats");
+    p->mask.p = d_mask;
+    p->mask.ld_frame = ld_frame;
+    p->mask.ld_stream = ld_stream;
+    return CRLOT_OK;
+}
+
+int crlot_stft(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams, int64_t T, int64_t ld_x,
+               int64_t ld_spec, int64_t ld_frame, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_streams < 0 || T < 0) return fail(CRLOT_EINVAL, "negative size");
+    LaunchScope ls(p, stream);
+    const int64_t F = frames_for(p, T);
+    if (n_streams == 0 || F == 0) return CRLOT_OK;
+    if ((!d_x && T > 0) || !d_spec) return fail(CRLOT_EINVAL, "null buffer");
+    const int64_t row = p->geo.n + 2;
+    if (ld_x < T || ld_frame < row || (n_streams > 1 && ld_spec < (F - 1) * ld_frame + row))
+        return fail(CRLOT_EINVAL, "leading dimension too small");
+    if (!aligned8(d_spec) || (ld_frame & 1) || (n_streams > 1 && (ld_spec & 1)))
+        return fail(CRLOT_EINVAL, "spectra are complex float pairs: 8-byte aligned rows");
+    if (F > INT32_MAX) return fail(CRLOT_EUNSUPPORTED, "too many frames per stream");
+    DeviceGuard g(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(p->mu);
+    crlot::Scratch* sc = scratch_slot(p, s);
+    if (!sc) return fail(CRLOT_EHIP, "scratch slot");
+    float* work = nullptr;
+    if (p->generic || !crlot::stft_supported(p->geo.n)) {
+        const int rc = ensure_workspace(sc, int64_t(n_streams) * F * p->geo.n * int64_t(sizeof(float)));
+        if (rc != CRLOT_OK) return rc;
+        work = sc->work;
+    }
+    return stft_impl(p, d_x, d_spec, n_streams, T, ld_x, F, ld_spec, ld_frame, work, s);
+}
+
+int crlot_istft_ola(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams, int64_t F, int64_t ld_spec,
+                    int64_t ld_frame, int64_t ld_y, void* stream) {
+    if (!p) return fail(CRLOT_EINVAL, "null plan");
+    if (n_streams < 0 || F < 0) return fail(CRLOT_EINVAL, "negative size");
+    LaunchScope ls(p, stream);
+    if (n_streams == 0 || F == 0) return CRLOT_OK;
+    if (!d_spec || !d_y) return fail(CRLOT_EINVAL, "null buffer");
+    const int64_t row = p->geo.n + 2;
+    if (ld_frame < row || (n_streams > 1 && ld_spec < (F - 1) * ld_frame + row) ||
+        (n_streams > 1 && ld_y < F * p->geo.h))
+        return fail(CRLOT_EINVAL, "leading dimension too small");
+    if (!aligned8(d_spec) || (ld_frame & 1) || (n_streams > 1 && (ld_spec & 1)))
+        return fail(CRLOT_EINVAL, "spectra are complex float pairs: 8-byte aligned rows");
+    if (F > INT32_MAX) return fail(CRLOT_EUNSUPPORTED, "too many frames per stream");
+    DeviceGuard g(p->device);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(p->mu);
+    crlot::Scratch* sc = scratch_slot(p, s);
+    if (!sc) return fail(CRLOT_EHIP, "scratch slot");
+    float* specw = nullptr;
+    float* frames = nullptr;
+    if (!istft_walk_ok(p, d_y, ld_y)) {
+        const int64_t sp = int64_t(n_streams) * F * row;
+        const int rc = ensure_workspace(sc, (sp + int64_t(n_streams) * F * p->geo.n) * int64_t(sizeof(float)));
+        if (rc != CRLOT_OK) return rc;
+        specw = sc->work;
+        frames = sc->work + sp;
+    }
+    return istft_impl(p, d_spec, d_y, n_streams, F, ld_spec, ld_frame, ld_y, specw, frames, s);
+}
+
+}  // extern "C"
 
 // ------------------------------------------------------------------ FFT plans
 // A real plan of nfft points owns an STFT plan of frame nfft; a complex plan of

@@ -361,6 +361,36 @@ hipError_t launch_windowed_frames(const float* x, int64_t T, const float* w, flo
 // a caller's per-bin real spectral gain (batch.cpp), one plain multiply
 hipError_t launch_bin_gain(const float* spec, float* out, const float* g, int64_t rows, int64_t ld, int64_t bins,
                            hipStream_t s);
+// ---- stft.hip: the round trip split at the spectral step (crlot_stft / crlot_istft_ola)
+// Per-frame real mask rows: row (stream s, frame k) at p + s ld_stream + k ld_frame,
+// N/2+1 floats (ld_stream 0: one row per frame for every stream).
+struct SpecMask {
+    const float* p = nullptr;
+    int64_t ld_frame = 0, ld_stream = 0;
+};
+// K_stft: power-of-two N 256..4096, any hop and framing; spectra (s, k) at
+// spec + s ld_spec + k ld_frame, N/2+1 float pairs (8-byte aligned rows)
+bool stft_supported(int n);
+hipError_t launch_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
+                       int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame, hipStream_t s);
+// K_istft walker shapes: stft_supported(n), H % 128 == 0, N % H == 0; also needs the
+// exact-rewrite tables (t.wsn, t.rden), ring_len % H == 0 and 8-byte aligned y rows
+bool istft_walk_supported(int n, int h);
+hipError_t launch_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
+                        int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
+                        hipStream_t s);
+// The round trip with the spectral step (gain, mask) on K_istft's walk from x
+// (8-byte aligned x rows as well): bit-identical to launch_istft(launch_stft(x))
+hipError_t launch_roundtrip_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x,
+                                   float* y, int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
+                                   hipStream_t s);
+// staged forms: frames[s F + k][N] = x frame * analysis window; out rows (s F + k) of
+// 2 bins floats = spectrum * gain * mask (in place when out aliases the same layout)
+hipError_t launch_frames_windowed(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
+                                  int64_t ld_x, int64_t F, float* frames, hipStream_t s);
+hipError_t launch_spec_step(const DevTables& t, const SpecMask& m, const float* spec, int64_t ld_spec,
+                            int64_t ld_frame, float* out, int n_streams, int64_t F, int bins, hipStream_t s);
+
 // dsp::FrameQueue frames on the device: [stream][F][N] from x [stream][ld_x]
 hipError_t launch_fq_frames(const float* x, int64_t T, int64_t ld_x, int n_streams, float* frames, int64_t F,
                             int64_t N, int64_t H, int64_t pad, int pad_mode, hipStream_t s);

@@ -62,6 +62,11 @@ extern "C" const char* crlot_kernel_name(int32_t id) {
         case CRLOT_K_INTERLEAVE: return "k_interleave";
         case CRLOT_K_FFT: return "k_fft";
         case CRLOT_K_FFT_ANY: return "k_fft_any";
+        case CRLOT_K_STFT: return "k_stft";
+        case CRLOT_K_ISTFT: return "k_istft";
+        case CRLOT_K_STFT_MASKED: return "k_stft_masked";
+        case CRLOT_K_SPEC_STEP: return "k_spec_step";
+        case CRLOT_K_FRAMES_W: return "k_frames_w";
         case CRLOT_K_EXPERIMENT: return "k_experiment";
         default: return "unknown";
     }

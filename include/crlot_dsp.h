@@ -216,6 +216,11 @@ int crlot_test_inject(int32_t what, int32_t count);
 #define CRLOT_K_INTERLEAVE 21
 #define CRLOT_K_FFT 22           /* batched rfft / irfft / cfft */
 #define CRLOT_K_FFT_ANY 23
+#define CRLOT_K_STFT 24          /* crlot_stft: x -> spectra */
+#define CRLOT_K_ISTFT 25         /* crlot_istft_ola: spectra -> step -> y */
+#define CRLOT_K_STFT_MASKED 26   /* crlot_roundtrip with a spectral mask: one walk x -> y */
+#define CRLOT_K_SPEC_STEP 27     /* staged spectral step (gain, mask) over spectra in HBM */
+#define CRLOT_K_FRAMES_W 28      /* staged windowed frames (mixed-radix stft) */
 #define CRLOT_K_EXPERIMENT 99    /* experiment builds only */
 typedef struct crlot_launch_info {
     int32_t n_kernels;
@@ -284,6 +289,47 @@ int crlot_roundtrip_stages(crlot_plan* plan, const float* d_x, int32_t n_streams
  * d_y[s*ld_y + n], n < F*H.  Bit-exact with the reference given equal frames. */
 int crlot_ola_gather(crlot_plan* plan, const float* d_frames, float* d_y, int32_t n_streams,
                      int64_t F, int64_t ld_frames, int64_t ld_y, void* stream);
+
+/* ---------------------------------------------------------------- the spectral step
+ * The round trip split where the reference's harness leaves its spectral
+ * processing step (e2e_benchmark.cc:160-162, identity there), so any
+ * device-side processing -- masks, Wiener gains, a model -- can sit between
+ * the halves with the spectra in HBM.
+ *
+ * crlot_stft: the analysis half.  Per stream and frame (framing exactly as
+ * crlot_roundtrip: Framer ZERO_PAD / DROP or FrameQueue), frame * analysis
+ * window, then IFftPlan::forward (sanitize, kiss_fftr; kissfft_adapter.cc
+ * :83-122): spectrum k of stream s, N/2+1 complex bins as float pairs, at
+ * d_spec[s*ld_spec + k*ld_frame + 2*b], b <= N/2.  ld_frame >= N+2 floats;
+ * d_spec 8-byte aligned, ld_frame and ld_spec even.  F = crlot_frame_count(T)
+ * frames per stream.  Bit-identical to crlot_rfft_batched on the windowed
+ * frames.
+ *
+ * crlot_istft_ola: the synthesis half.  Spectra in that layout (F frames per
+ * stream) -> the plan's spectral step (the per-bin gain of
+ * crlot_plan_set_spectral_gain, then row k of the mask below) ->
+ * IFftPlan::inverse (kiss_fftri, *1/N, sanitize; kissfft_adapter.cc:124-168)
+ * -> push_frame_AoS(k*H) with the synthesis window and gain -> produce(H)
+ * (OLAAccumulator.cc:124-221): d_y[s*ld_y + n], n < F*H.  Bit-identical to
+ * crlot_irfft_batched of the stepped spectra + crlot_ola_gather.  The imaginary
+ * parts of bins 0 and N/2 are ignored, as kiss_fftri ignores them.
+ *
+ * crlot_plan_set_spectral_mask: a time-varying spectral step.  Row (s, k) of
+ * N/2+1 real floats at d_mask[s*ld_stream + k*ld_frame] multiplies frame k of
+ * stream s after the per-bin gain (ld_stream = 0: one row per frame, shared by
+ * every stream).  Device memory owned by the caller, read by every later
+ * crlot_roundtrip, crlot_roundtrip_interleaved (stream = channel plane
+ * g*C + c) and crlot_istft_ola on the plan until it is replaced or cleared
+ * (NULL); it must hold a row for every frame those calls run.  With a mask,
+ * crlot_roundtrip(x) equals crlot_istft_ola(crlot_stft(x)) bit for bit (one
+ * walk over HBM where the shape allows it: power-of-two N, H % 128 == 0,
+ * N % H == 0, 8-byte aligned output rows).  The streaming objects, the host-pointer
+ * calls and crlot_roundtrip_stages keep the per-bin gain only. */
+int crlot_plan_set_spectral_mask(crlot_plan* plan, const float* d_mask, int64_t ld_frame, int64_t ld_stream);
+int crlot_stft(crlot_plan* plan, const float* d_x, float* d_spec, int32_t n_streams, int64_t T, int64_t ld_x,
+               int64_t ld_spec, int64_t ld_frame, void* stream);
+int crlot_istft_ola(crlot_plan* plan, const float* d_spec, float* d_y, int32_t n_streams, int64_t F,
+                    int64_t ld_spec, int64_t ld_frame, int64_t ld_y, void* stream);
 
 /* Batched IFftPlan::forward / inverse with the adapter's semantics
  * (kissfft_adapter.cc:83-168): forward sanitizes its input, inverse scales by

@@ -886,13 +886,14 @@ long or_roundtrip(const float* x, size_t T, size_t n, size_t h, int wtype, int p
 
 static long or_roundtrip_impl(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
                               int framing, int center, int pad_mode, int analysis_window, const float* bin_gain,
-                              float* y, size_t y_cap, float* frames_out, float* spec_out);
+                              const float* mask, size_t mask_ld, float* y, size_t y_cap, float* frames_out,
+                              float* spec_out, float* raw_spec_out);
 
 long or_roundtrip_ex(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
                      int framing, int center, int pad_mode, int analysis_window, float* y,
                      size_t y_cap, float* frames_out, float* spec_out) {
-    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, center, pad_mode, analysis_window, NULL, y,
-                             y_cap, frames_out, spec_out);
+    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, center, pad_mode, analysis_window, NULL, NULL, 0,
+                             y, y_cap, frames_out, spec_out, NULL);
 }
 
 /* The same loop with a spectral step where e2e_benchmark.cc:161-162 puts one
@@ -901,12 +902,27 @@ long or_roundtrip_ex(const float* x, size_t T, size_t n, size_t h, int wtype, in
  * caller editing the interleaved complex spectrum on the host would). */
 long or_roundtrip_gain(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic, int framing,
                        const float* bin_gain, float* y, size_t y_cap) {
-    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, 0, 0, 1, bin_gain, y, y_cap, NULL, NULL);
+    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, 0, 0, 1, bin_gain, NULL, 0, y, y_cap, NULL, NULL,
+                             NULL);
+}
+
+/* The same loop with a time-varying spectral step (crlot_plan_set_spectral_mask):
+ * frame k's spectrum is scaled by bin_gain[b] (nullable), then by mask row k,
+ * mask[k * mask_ld + b] (nullable), b <= n/2 -- re and im each multiplied, as in
+ * or_roundtrip_gain.  raw_spec_out (nullable, rows of n + 2 floats) receives the
+ * forward spectra before the step: IFftPlan::forward of frame * w, what
+ * crlot_stft writes. */
+long or_roundtrip_mask(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic, int framing,
+                       int center, int pad_mode, int analysis_window, const float* bin_gain, const float* mask,
+                       size_t mask_ld, float* y, size_t y_cap, float* raw_spec_out) {
+    return or_roundtrip_impl(x, T, n, h, wtype, periodic, framing, center, pad_mode, analysis_window, bin_gain,
+                             mask, mask_ld, y, y_cap, NULL, NULL, raw_spec_out);
 }
 
 static long or_roundtrip_impl(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic,
                               int framing, int center, int pad_mode, int analysis_window, const float* bin_gain,
-                              float* y, size_t y_cap, float* frames_out, float* spec_out) {
+                              const float* mask, size_t mask_ld, float* y, size_t y_cap, float* frames_out,
+                              float* spec_out, float* raw_spec_out) {
     if (n == 0 || h == 0 || (n & 1)) return -1;
     if (framing < 0 || framing > 2) return -3;
     float* w = (float*)malloc(sizeof(float) * n);
@@ -944,10 +960,16 @@ static long or_roundtrip_impl(const float* x, size_t T, size_t n, size_t h, int 
         for (size_t i = 0; i < n; ++i) /* e2e_benchmark.cc:154-156 (analysis window) */
             proc[i] = analysis_window ? frame[i] * w[i] : frame[i];
         or_adapter_forward(fwd, (int)n, proc, spec);
+        if (raw_spec_out) memcpy(raw_spec_out + k * (n + 2), spec, sizeof(float) * (n + 2));
         if (bin_gain)
             for (size_t b = 0; b <= n / 2; ++b) {
                 spec[2 * b] *= bin_gain[b];
                 spec[2 * b + 1] *= bin_gain[b];
+            }
+        if (mask)
+            for (size_t b = 0; b <= n / 2; ++b) {
+                spec[2 * b] *= mask[k * mask_ld + b];
+                spec[2 * b + 1] *= mask[k * mask_ld + b];
             }
         if (spec_out) memcpy(spec_out + k * (n + 2), spec, sizeof(float) * (n + 2));
         or_adapter_inverse(inv, (int)n, spec, proc);

@@ -147,6 +147,11 @@ long or_roundtrip_ex(const float* x, size_t T, size_t frame_size, size_t hop, in
  * between the transforms (the spectral step of e2e_benchmark.cc:161-162). */
 long or_roundtrip_gain(const float* x, size_t T, size_t n, size_t h, int window_type, int periodic, int framing,
                        const float* bin_gain, float* y, size_t y_cap);
+/* the loop with bin_gain then mask row k scaling frame k's spectrum; raw_spec_out:
+ * the forward spectra before the step (rows of n + 2 floats) */
+long or_roundtrip_mask(const float* x, size_t T, size_t n, size_t h, int window_type, int periodic, int framing,
+                       int center, int pad_mode, int analysis_window, const float* bin_gain, const float* mask,
+                       size_t mask_ld, float* y, size_t y_cap, float* raw_spec_out);
 long or_roundtrip_batch_ex(const float* x, size_t n_streams, size_t T, size_t ld_x,
                            size_t frame_size, size_t hop, int window_type, int periodic,
                            int framing, int center, int pad_mode, int analysis_window, float* y,

@@ -120,6 +120,9 @@ def lib(native: bool = False):
     L.or_roundtrip_ex.restype = C.c_long
     L.or_roundtrip_gain.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, C.c_void_p, _f32p, sz]
     L.or_roundtrip_gain.restype = C.c_long
+    L.or_roundtrip_mask.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_void_p, C.c_void_p, sz, _f32p, sz, C.c_void_p]
+    L.or_roundtrip_mask.restype = C.c_long
     L.or_roundtrip_batch_ex.argtypes = [_f32p, sz, sz, sz, sz, sz, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, C.c_int, _f32p, sz, C.c_int]
     L.or_roundtrip_batch_ex.restype = C.c_long
@@ -469,6 +472,32 @@ def roundtrip_gain(x, n, h, bin_gain, mode=ZERO_PAD, wtype=HANN, periodic=False)
     if r < 0:
         raise ValueError(f"or_roundtrip_gain rc={r}")
     return y[:F * h]
+
+
+def roundtrip_mask(x, n, h, bin_gain=None, mask=None, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT,
+                   analysis_window=True, wtype=HANN, periodic=False, want_spec=False):
+    """or_roundtrip_mask: the e2e loop with a time-varying spectral step -- frame
+    k's spectrum scaled by bin_gain (n/2+1, optional), then by mask[k] (rows of
+    n/2+1, optional).  Returns y (F*H) [, the forward spectra before the step,
+    (F, n/2+1) complex64: crlot_stft's output]."""
+    x = np.ascontiguousarray(x, np.float32)
+    T = x.size
+    F = frames_for(T, n, h, mode, center)
+    bins = n // 2 + 1
+    g = None if bin_gain is None else np.ascontiguousarray(bin_gain, np.float32)
+    m = None if mask is None else np.ascontiguousarray(mask, np.float32).reshape(-1, bins)
+    if m is not None and m.shape[0] < F:
+        raise ValueError("mask needs a row per frame")
+    y = np.zeros(max(F * h, 1), np.float32)
+    spec = np.zeros((max(F, 1), bins), np.complex64) if want_spec else None
+    r = lib().or_roundtrip_mask(x if T else np.zeros(1, np.float32), T, n, h, wtype, int(periodic), mode,
+                                int(center), pad_mode, int(analysis_window),
+                                None if g is None else g.ctypes.data, None if m is None else m.ctypes.data,
+                                bins, y, F * h, None if spec is None else spec.ctypes.data)
+    if r < 0:
+        raise ValueError(f"or_roundtrip_mask rc={r}")
+    assert r == F, (r, F)
+    return (y[:F * h], spec[:F]) if want_spec else y[:F * h]
 
 
 def roundtrip_batch_ex(x2d, n, h, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT,

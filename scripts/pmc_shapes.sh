@@ -16,6 +16,8 @@ run() {
 }
 SHAPES="$*"
 run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE
+# stall split: parked (s_waitcnt / s_barrier) vs issue stalls, LDS bank conflicts
+run sq2 --pmc SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 echo "== done"

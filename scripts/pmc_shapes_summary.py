@@ -7,13 +7,17 @@ import collections
 import csv
 import json
 import statistics
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import src_hash  # noqa: E402
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "r03"
 src = f"gpurun_out/pmcs_{tag}"
 per = collections.defaultdict(lambda: collections.defaultdict(list))  # kernel -> counter -> [per dispatch]
 dur = collections.defaultdict(list)
-for part in ("sq", "fetch", "write"):
+for part in ("sq", "sq2", "fetch", "write"):
     acc = collections.defaultdict(float)  # (kernel, dispatch, counter) -> sum over agents/dims
     try:
         rows = list(csv.DictReader(open(f"{src}/{part}/run_counter_collection.csv")))
@@ -30,7 +34,7 @@ for part in ("sq", "fetch", "write"):
             if "crlot" in r["Kernel_Name"]:
                 dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 
-out = {"tag": tag, "source": "scripts/pmc_shapes.sh (rocprofv3 --pmc, one group per run) over scripts/bench_shapes.py "
+out = {"tag": tag, "src_hash": src_hash(), "source": "scripts/pmc_shapes.sh (rocprofv3 --pmc, one group per run) over scripts/bench_shapes.py "
        "at 1024 streams x 480000; medians per launch", "kernels": {}}
 for k, cs in per.items():
     d = {c: statistics.median(v) for c, v in cs.items()}

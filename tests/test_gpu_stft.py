@@ -1,0 +1,320 @@
+"""The round trip split at its spectral step: crlot_stft,
+crlot_istft_ola and the per-frame spectral mask, through the C ABI.
+
+The reference leaves the step as the identity (bench/e2e_benchmark.cc:160-162);
+the oracle applies the same edit in its e2e loop (oracle/crlot_oracle.c
+or_roundtrip_mask: kissfft_adapter.cc forward -> spectrum * gain * mask row k ->
+inverse -> OLAAccumulator push / produce), so the masked results are pinned to
+the oracle's restatement of the reference chain ("parity unpinned" for the edit
+itself: the reference has no non-identity step).
+
+Bars (tests/test_gpu_parity.py):
+  * spectra and outputs vs the oracle: the float32 FFT tolerance
+    (rel-L2 <= 1e-6, max-abs <= 4e-6 of the input / spectrum scale);
+  * bit-exact: crlot_stft vs crlot_rfft_batched of the windowed frames,
+    crlot_istft_ola vs crlot_irfft_batched of the stepped spectra +
+    crlot_ola_gather, the masked crlot_roundtrip vs crlot_istft_ola(crlot_stft),
+    the walkers vs their staged fallbacks, and every chunking.
+"""
+import numpy as np
+import pytest
+
+from test_gpu_parity import assert_close, bits, dev, host, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(1024, 256), (4096, 1024), (512, 128)]
+
+
+def assert_spec_close(X, ref, what=""):
+    X = np.asarray(X, np.complex64)
+    ref = np.asarray(ref, np.complex64)
+    assert X.shape == ref.shape, (what, X.shape, ref.shape)
+    assert np.all(np.isfinite(X.view(np.float32))), what
+    scale = float(np.max(np.abs(ref))) if ref.size else 0.0
+    r = rel_l2(X, ref)
+    m = float(np.max(np.abs(X.astype(np.complex128) - ref))) if X.size else 0.0
+    assert r <= 1e-6 or np.linalg.norm(ref) < 1e-20, f"{what}: rel-L2 {r:.3e}"
+    assert m <= 4e-6 * max(scale, 1e-30), f"{what}: max-abs {m:.3e} (scale {scale:.3e})"
+
+
+def frames_np(oracle, x, n, h, mode, center=True, pad_mode=0):
+    """Raw frames of one stream: the Framer (whole push) or the FrameQueue."""
+    if mode == oracle.FRAMEQUEUE:
+        return oracle.fq_frames(x, n, h, center, pad_mode).reshape(-1, n)
+    T = x.size
+    F = oracle.frame_count(T, n, h, mode)
+    out = np.zeros((F, n), np.float32)
+    for k in range(F):
+        seg = x[k * h:k * h + n]
+        out[k, :seg.size] = seg
+    return out
+
+
+def special(x):
+    """NaN / Inf bursts, sub-threshold and denormal stretches, a huge sample."""
+    x = x.copy()
+    T = x.shape[1]
+    x[0, 100:110] = np.nan
+    x[0, min(2000, T - 1)] = np.inf
+    x[0, min(2100, T - 2)] = -np.inf
+    if x.shape[0] > 1:
+        x[1, 300:900] = 1e-35
+        x[1, 1000:1010] = 1e-42
+        x[1, min(5000, T - 3)] = 3e30
+    return x
+
+
+def finite_scale(xs):
+    """(max |x|, ||x||) over the finite samples: the tolerance scale of a stream."""
+    f = np.where(np.isfinite(xs), xs, 0).astype(np.float64)
+    return float(np.max(np.abs(f))) if f.size else 0.0, float(np.linalg.norm(f))
+
+
+def stepped(spec, gain=None, mask=None):
+    """spectrum * gain[b] then * mask[k, b] in float32, re and im each (the oracle's step)."""
+    f = np.ascontiguousarray(spec, np.complex64).view(np.float32).reshape(spec.shape + (2,)).copy()
+    if gain is not None:
+        f *= np.asarray(gain, np.float32)[..., None]
+    if mask is not None:
+        f *= np.asarray(mask, np.float32)[..., None]
+    return f.view(np.complex64).reshape(spec.shape)
+
+
+@pytest.mark.parametrize("n,h", SHAPES + [(256, 128), (2048, 512), (1024, 300)])
+@pytest.mark.parametrize("mode", [0, 1, 2])  # ZERO_PAD, DROP, FRAMEQUEUE (centre, reflect)
+def test_stft_vs_oracle_and_rfft(pkg, oracle, torch_cuda, n, h, mode):
+    torch = torch_cuda
+    S, T = 3, 9 * n + 77
+    x = special(oracle.synth_streams(S, T, config_id=61))
+    kw = dict(center=True, pad_mode=pkg.PAD_REFLECT) if mode == 2 else {}
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode, **kw)
+    xd = dev(torch, x)
+    spec = host(plan.stft(xd))
+    assert plan.last_launch()["kernels"] == ["k_stft"]
+    F = plan.frame_count(T)
+    assert spec.shape == (S, F, n // 2 + 1)
+    w = oracle.window(oracle.HANN, n)
+    for s in range(S):
+        _, ref = oracle.roundtrip_mask(x[s], n, h, mode=mode, pad_mode=kw.get("pad_mode", 0), want_spec=True)
+        assert_spec_close(spec[s], ref, f"{n}/{h} mode {mode} stream {s}")
+        assert np.all(spec[s][:, 0].imag == 0) and np.all(spec[s][:, -1].imag == 0)
+        fr = frames_np(oracle, x[s], n, h, mode, True, kw.get("pad_mode", 0))
+        direct = host(plan.rfft(dev(torch, (fr * w).astype(np.float32))))
+        assert np.array_equal(bits(spec[s].view(np.float32)), bits(direct.view(np.float32))), (n, h, mode, s)
+
+
+@pytest.mark.parametrize("n,h", SHAPES + [(2048, 1024), (1024, 128)])
+def test_istft_ola_bit_exact_vs_irfft_gather(pkg, oracle, torch_cuda, n, h):
+    torch = torch_cuda
+    S, T = 3, 11 * n + 5
+    bins = n // 2 + 1
+    x = oracle.synth_streams(S, T, config_id=62)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    spec = plan.stft(dev(torch, x))
+    F = spec.shape[1]
+    rng = np.random.default_rng(n + h)
+    gain = rng.uniform(0.0, 2.0, bins).astype(np.float32)
+    mask = rng.uniform(-1.5, 1.5, (S, F, bins)).astype(np.float32)
+    for g, m in ((None, None), (gain, None), (None, mask), (gain, mask)):
+        plan.set_spectral_gain(g)
+        plan.set_spectral_mask(None if m is None else dev(torch, m))
+        y = host(plan.istft_ola(spec))
+        assert plan.last_launch()["kernels"] == ["k_istft"]
+        X = dev(torch, stepped(host(spec), g, m))
+        fr = plan.irfft(X.reshape(S * F, bins)).reshape(S, F, n)
+        ref = host(plan.ola_gather(fr))
+        assert np.array_equal(bits(y), bits(ref)), (n, h, g is not None, m is not None)
+    plan.set_spectral_gain(None)
+    plan.set_spectral_mask(None)
+
+
+@pytest.mark.parametrize("n,h", SHAPES)
+@pytest.mark.parametrize("shared", [False, True])
+def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared):
+    """crlot_roundtrip with a per-frame mask: one walk over HBM, bit-identical to
+    crlot_istft_ola(crlot_stft(x)), and the oracle's masked e2e loop within the
+    FFT tolerance -- with NaN, Inf, tiny and huge samples in the input."""
+    torch = torch_cuda
+    S, T = 4, 13 * n + 31
+    bins = n // 2 + 1
+    x = special(oracle.synth_streams(S, T, config_id=63))
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    F = plan.frame_count(T)
+    rng = np.random.default_rng(7 * n + h)
+    m = rng.uniform(0.0, 1.0, (F, bins) if shared else (S, F, bins)).astype(np.float32)
+    m[..., ::17] = 0.0
+    plan.set_spectral_mask(dev(torch, m))
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    assert plan.last_launch()["kernels"] == ["k_stft_masked"]
+    y2 = host(plan.istft_ola(plan.stft(xd)))
+    assert np.array_equal(bits(y), bits(y2))
+    assert np.all(np.isfinite(y))
+    for s in range(S):
+        ms = m if shared else m[s]
+        ref = oracle.roundtrip_mask(x[s], n, h, mask=ms)
+        xmax, xnorm = finite_scale(x[s])
+        assert_close(y[s], ref, xmax, f"{n}/{h} masked stream {s}", xnorm)
+    plan.set_spectral_mask(None)
+
+
+@pytest.mark.parametrize("n,h", SHAPES)
+def test_masked_roundtrip_chunking_and_fallbacks(pkg, oracle, torch_cuda, n, h):
+    """The bits do not depend on the chunking, nor on whether the walk or the
+    staged path (spectra through HBM, k_spec_step + irfft + gather) runs."""
+    torch = torch_cuda
+    S, T = 3, 17 * n + 9
+    bins = n // 2 + 1
+    x = oracle.synth_streams(S, T, config_id=64)
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    F = plan.frame_count(T)
+    m = np.random.default_rng(3).uniform(0.2, 1.2, (S, F, bins)).astype(np.float32)
+    plan.set_spectral_mask(dev(torch, m))
+    plan.set_spectral_gain(np.linspace(0.5, 1.5, bins).astype(np.float32))
+    xd = dev(torch, x)
+    y0 = host(plan.roundtrip(xd))
+    for c in (1, 2, 5, F):
+        plan.set_chunks(c)
+        assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(y0)), c
+        assert np.array_equal(bits(host(plan.istft_ola(plan.stft(xd)))), bits(y0)), c
+    plan.set_chunks(0)
+    # x rows 4-byte aligned only: still the one walk (its frame loads check the alignment)
+    xo = torch.zeros((S, T + 1), device="cuda")
+    xo[:, :T] = xd
+    xv = xo[:, :T]
+    assert np.array_equal(bits(host(plan.roundtrip(xv))), bits(y0))
+    assert plan.last_launch()["kernels"] == ["k_stft_masked"]
+    # output rows 4-byte aligned only: spectra through HBM, k_spec_step + irfft + gather
+    yo = torch.zeros((S, F * h + 1), device="cuda")
+    plan.roundtrip(xv, yo[:, :F * h])
+    ks = plan.last_launch()["kernels"]
+    assert ks[:2] == ["k_stft", "k_spec_step"] and "k_gather" in ks[-1], ks
+    assert np.array_equal(bits(host(yo[:, :F * h])), bits(y0))
+    spec = plan.stft(xv)
+    yo.zero_()
+    assert np.array_equal(bits(host(plan.istft_ola(spec, yo[:, :F * h]))), bits(y0))
+    assert plan.last_launch()["kernels"][0] == "k_spec_step"
+    plan.set_spectral_mask(None)
+    plan.set_spectral_gain(None)
+
+
+@pytest.mark.parametrize("n,h", [(960, 240), (882, 441), (1024, 200), (480, 120), (1000, 250)])
+def test_other_sizes(pkg, oracle, torch_cuda, n, h):
+    """Frame sizes / hops outside the walkers: the staged forms (windowed frames ->
+    mixed-radix rfft; spectral step -> irfft -> gather) against the oracle."""
+    torch = torch_cuda
+    S, T = 3, 12 * n + 13
+    bins = n // 2 + 1
+    x = special(oracle.synth_streams(S, T, config_id=65))
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    xd = dev(torch, x)
+    spec = plan.stft(xd)
+    F = spec.shape[1]
+    m = np.random.default_rng(n).uniform(0.0, 1.0, (S, F, bins)).astype(np.float32)
+    specn = host(spec)
+    for s in range(S):
+        _, ref = oracle.roundtrip_mask(x[s], n, h, want_spec=True)
+        assert_spec_close(specn[s], ref, f"{n}/{h} stream {s}")
+    plan.set_spectral_mask(dev(torch, m))
+    y = host(plan.istft_ola(spec))
+    yr = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(y), bits(yr))
+    for s in range(S):
+        xmax, xnorm = finite_scale(x[s])
+        ref = oracle.roundtrip_mask(x[s], n, h, mask=m[s])
+        assert_close(y[s], ref, xmax, f"{n}/{h} stream {s}", xnorm)
+    plan.set_spectral_mask(None)
+
+
+def test_framequeue_pipeline_masked(pkg, oracle, torch_cuda):
+    """performance_benchmark.cc:174-246's framing (FrameQueue, centre, reflect, no
+    analysis window) with a per-frame mask."""
+    torch = torch_cuda
+    n, h, S, T = 1024, 256, 2, 20000
+    x = oracle.synth_streams(S, T, config_id=66)
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=pkg.FRAMEQUEUE, analysis_window=False,
+                    pad_mode=pkg.PAD_REFLECT)
+    F = plan.frame_count(T)
+    m = np.random.default_rng(9).uniform(0.0, 1.0, (F, n // 2 + 1)).astype(np.float32)
+    plan.set_spectral_mask(dev(torch, m))
+    xd = dev(torch, x)
+    y = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(y), bits(host(plan.istft_ola(plan.stft(xd)))))
+    for s in range(S):
+        ref = oracle.roundtrip_mask(x[s], n, h, mask=m, mode=oracle.FRAMEQUEUE, pad_mode=oracle.PAD_REFLECT,
+                                    analysis_window=False)
+        assert_close(y[s], ref, 0.5, f"framequeue stream {s}")
+
+
+def test_short_and_empty_streams(pkg, oracle, torch_cuda):
+    torch = torch_cuda
+    n, h = 1024, 256
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    for T in (1, 2, 5, 255, 256, 257, 1023, 1025):
+        x = oracle.synth_streams(2, T, config_id=67)
+        xd = dev(torch, x)
+        spec = host(plan.stft(xd))
+        y = host(plan.istft_ola(plan.stft(xd)))
+        for s in range(2):
+            yr, ref = oracle.roundtrip_mask(x[s], n, h, want_spec=True)
+            assert_spec_close(spec[s], ref, f"T={T}")
+            assert_close(y[s], yr, 0.5, f"T={T}", float(np.linalg.norm(x[s])))
+    empty = torch.zeros((2, 0), device="cuda")
+    assert plan.stft(empty).shape == (2, 0, n // 2 + 1)
+
+
+def test_abi_validation(pkg, torch_cuda):
+    torch = torch_cuda
+    L = pkg.lib()
+    plan = pkg.Plan(frame_size=1024, hop_size=256)
+    x = torch.zeros((2, 4096), device="cuda")
+    R = 1026  # N + 2 floats: one spectrum row
+    spec = torch.zeros((2, 16, R), device="cuda")
+    y = torch.zeros((2, 4096), device="cuda")
+    xp, sp, yp = x.data_ptr(), spec.data_ptr(), y.data_ptr()
+    assert L.crlot_stft(None, xp, sp, 2, 4096, 4096, 16 * R, R, None) == pkg.EINVAL
+    assert L.crlot_stft(plan._h, xp, sp, 2, 4096, 4096, 16 * R, R - 2, None) == pkg.EINVAL
+    assert L.crlot_stft(plan._h, xp, sp + 4, 2, 4096, 4096, 16 * R, R, None) == pkg.EINVAL
+    assert L.crlot_stft(plan._h, xp, sp, 2, 4096, 4096, 15 * R, R, None) == pkg.EINVAL
+    assert L.crlot_stft(plan._h, xp, sp, 2, 4096, 4095, 16 * R, R, None) == pkg.EINVAL
+    assert L.crlot_istft_ola(plan._h, sp, yp, 2, 16, 16 * R, R + 1, 4096, None) == pkg.EINVAL
+    assert L.crlot_istft_ola(plan._h, sp, yp, 2, 16, 16 * R, R, 4095, None) == pkg.EINVAL
+    assert L.crlot_istft_ola(plan._h, None, yp, 2, 16, 16 * R, R, 4096, None) == pkg.EINVAL
+    assert L.crlot_plan_set_spectral_mask(plan._h, sp, 512, 0) == pkg.EINVAL
+    assert L.crlot_plan_set_spectral_mask(plan._h, sp, 513, -1) == pkg.EINVAL
+    assert L.crlot_plan_set_spectral_mask(plan._h, sp + 2, 513, 0) == pkg.EINVAL
+    assert L.crlot_stft(plan._h, xp, sp, 2, 4096, 4096, 16 * R, R, None) == 0
+    assert L.crlot_istft_ola(plan._h, sp, yp, 2, 16, 16 * R, R, 4096, None) == 0
+    assert L.crlot_stft(plan._h, xp, sp, 0, 4096, 4096, 16 * R, R, None) == 0  # nothing to do
+    torch.cuda.synchronize()
+
+
+def test_full_size_stft_istft(pkg, oracle, torch_cuda):
+    """At BASELINE scale (1024 x 480000, 1024/256; 7.9 GB of spectra):
+    istft_ola(stft(x)) within the parity bar of crlot_roundtrip(x) on sampled
+    streams and of the oracle; an all-ones shared mask gives the masked walk the
+    same bits; determinism."""
+    torch = torch_cuda
+    n, h, S, T = 1024, 256, 1024, 480_000
+    g = torch.Generator(device="cuda").manual_seed(4321)
+    x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    spec = plan.stft(x)
+    y = plan.istft_ola(spec)
+    assert torch.equal(y, plan.istft_ola(plan.stft(x)))
+    del spec
+    yr = plan.roundtrip(x)
+    F = plan.frame_count(T)
+    ones = torch.ones((F, n // 2 + 1), device="cuda")
+    plan.set_spectral_mask(ones)
+    ym = plan.roundtrip(x)
+    assert torch.equal(ym, y)
+    plan.set_spectral_mask(None)
+    for s in (0, 700, 1023):
+        xs = host(x[s])
+        ref = oracle.roundtrip(xs, n, h)
+        assert_close(host(y[s]), ref, 0.5, f"stft+istft stream {s}", float(np.linalg.norm(xs)))
+        assert_close(host(y[s]), host(yr[s]), 0.5, f"vs roundtrip stream {s}", float(np.linalg.norm(xs)))
+    del x, y, yr, ym
+    torch.cuda.empty_cache()

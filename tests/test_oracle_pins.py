@@ -392,3 +392,33 @@ def test_e2e_golden_reproduces(oracle, e2e_gold):
         for s in range(S):
             y = oracle.roundtrip(x[s], n, h, mode=mode)
             assert np.array_equal(bits(y), bits(e2e_gold[f"{name}/y"][s])), name
+
+
+@pytest.mark.parametrize("n,h,mode", [(1024, 256, 0), (4096, 1024, 1), (512, 128, 2), (960, 240, 0)])
+def test_oracle_spectral_step_reduces_to_pinned_loops(oracle, n, h, mode):
+    """or_roundtrip_mask (the checker of crlot_stft / crlot_istft_ola / the masked
+    round trip) on the pinned loops: a mask of ones is or_roundtrip_ex, mask rows
+    equal to one gain are or_roundtrip_gain (ZERO_PAD), and its raw spectra are
+    IFftPlan::forward (the adapter restatement) of the windowed frames."""
+    T = 7 * n + 33
+    x = oracle.synth(T, 5 + n)
+    F = oracle.frames_for(T, n, h, mode)
+    bins = n // 2 + 1
+    y0 = oracle.roundtrip_ex(x, n, h, mode=mode)
+    y1, spec = oracle.roundtrip_mask(x, n, h, mask=np.ones((F, bins), np.float32), mode=mode, want_spec=True)
+    assert np.array_equal(bits(y0), bits(y1))
+    w = oracle.window(oracle.HANN, n)
+    if mode == oracle.FRAMEQUEUE:
+        fr = oracle.fq_frames(x, n, h).reshape(-1, n)
+    else:
+        fr = np.zeros((F, n), np.float32)
+        for k in range(F):
+            seg = x[k * h:k * h + n]
+            fr[k, :seg.size] = seg
+    direct = oracle.bench_rfft((fr * w).astype(np.float32), n)
+    assert np.array_equal(bits(spec.view(np.float32)), bits(direct.view(np.float32)))
+    if mode == oracle.ZERO_PAD:
+        g = np.linspace(0.25, 1.75, bins).astype(np.float32)
+        yg = oracle.roundtrip_gain(x, n, h, g)
+        assert np.array_equal(bits(yg), bits(oracle.roundtrip_mask(x, n, h, bin_gain=g)))
+        assert np.array_equal(bits(yg), bits(oracle.roundtrip_mask(x, n, h, mask=np.tile(g, (F, 1)))))
