@@ -74,6 +74,19 @@ def src_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def build_check(pkg) -> dict:
+    """The loaded library's baked-in source hash against the tree's
+    (tools/src_hash.py lib_hash): a stale prebuilt .so fails the run."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import src_hash as SH
+    info = pkg.build_info()
+    tree = SH.lib_hash()
+    if info["src"] != tree:
+        raise SystemExit(f"stale library: {info['path']} was built from sources {info['src']}, the tree is {tree} "
+                         "(run __graft_entry__.build())")
+    return {"lib_src_hash": info["src"], "tree_src_hash": tree, "kernel_src_hash": src_hash(), "match": True}
+
+
 def cpu_share() -> int:
     """Threads this process may use: the pool's per-GPU share (OMP_NUM_THREADS on
     the GPU box) or the affinity mask, never the whole machine's os.cpu_count()."""
@@ -766,9 +779,10 @@ def run_suite(name):
     import torch
     from __graft_entry__ import load_pkg
     pkg = load_pkg()
+    build = build_check(pkg)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    print(json.dumps(SUITES[name](pkg, torch, dev)), flush=True)
+    print(json.dumps({**SUITES[name](pkg, torch, dev), "build": build}), flush=True)
 
 
 def main():
@@ -804,6 +818,7 @@ def main():
     observed = D.observed_world(dev)  # what the process group really holds (all ranks agree)
 
     pkg = load_pkg()
+    build = build_check(pkg)
     plan = pkg.Plan(frame_size=N_FFT, hop_size=HOP, device=dev.index)
     S, T = args.streams, T_LEN
     L = plan.output_length(T)
@@ -911,6 +926,7 @@ def main():
                         "size the group reports and the distinct devices (PCI ids) its ranks ran on",
             },
             "cpu_baseline": cpu,
+            "build": build,
         }
         print(json.dumps(out), flush=True)
     D.finalize()

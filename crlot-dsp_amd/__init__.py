@@ -108,6 +108,7 @@ def lib():
     sig = {
         "crlot_last_error": ([], C.c_char_p),
         "crlot_abi_version": ([], C.c_int),
+        "crlot_build_info": ([], C.c_char_p),
         "crlot_plan_create": ([C.POINTER(PlanDesc), C.POINTER(vp)], C.c_int),
         "crlot_plan_destroy": ([vp], None),
         "crlot_plan_upload_tables": ([vp, vp, vp], C.c_int),
@@ -223,6 +224,13 @@ def lib():
         fn.restype = rest
     _lib = L
     return L
+
+
+def build_info() -> dict:
+    """What the loaded library was built from (crlot_build_info): {"src": the
+    source hash baked in at build time, "arch": ...}."""
+    parts = dict(p.split(":", 1) for p in lib().crlot_build_info().decode().split())
+    return {"src": parts.get("src"), "arch": parts.get("arch"), "path": LIB_PATH}
 
 
 def set_call_speculation(mode: int):

@@ -416,7 +416,7 @@ int continue_window(SharedServer* sh, BatchSpec* b, crlot_plan* inner, int64_t n
         const bool got = framequeue_last_rows(n, kBatchWindow, accept, &hop, &F, &total, &qdev, &src, &first, dst);
         if (he != hipSuccess) return decline(b);
         if (!got) return 0;
-        if (src != b->source || first != b->src_first + b->we || hop != b->h) return 0;
+        if (src != b->source || first != b->src_first + b->we || hop != b->h || total != b->M - b->we) return 0;
     }
     // the attached object: carry its last frames' inverse outputs over, or rebuild
     // its ring now, while the frames it needs are still in the buffers
@@ -453,6 +453,9 @@ int continue_window(SharedServer* sh, BatchSpec* b, crlot_plan* inner, int64_t n
         if (b->ola) {  // the frames it still needs are the carried rows [0, carry)
             crlot_ola* o = b->ola;
             b->ola = nullptr;
+            // the carry copy above runs on b->s; the rebuild reads those rows on the
+            // object's own stream, which nothing orders after b->s
+            (void)hipStreamSynchronize(b->s);
             const int rc = ola_materialize_locked(o);
             if (rc != CRLOT_OK) return rc;
         }
@@ -682,6 +685,11 @@ int apply_gain(BatchSpec* b, crlot_plan* inner, int64_t j) {
     if ((e = hipMemcpyAsync(b->h_r + b->row(j) * N, r_dev, sizeof(float) * F * N, hipMemcpyDeviceToHost, b->s)))
         return hip_fail(e, "batch spectral gain");
     if (b->ola) {
+        // the attached object's produce blocks over the redone rows; its wrapped ring
+        // (the push-everything-first order) was precomputed from the inverses without
+        // the gain when it attached with the chain: batch_alias rebuilds it from d_r
+        b->spec_used = false;
+        b->spec_y = false;
         if ((e = launch_ola_window(b, false))) return hip_fail(e, "batch overlap-add");
     } else {
         b->spec_y = false;  // a fresh object's blocks were of the inverses without the gain

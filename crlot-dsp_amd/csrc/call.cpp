@@ -229,8 +229,7 @@ void test_inject_timeouts(int count) { g_timeout_inject.store(count, std::memory
 
 int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
     if (test_timeout_now()) {  // (test-only: the timeout path below, taken at once)
-        broken_ = true;
-        broken_at_ = q_;
+        timed_out(std::min(done(), target - 1));
         return fail(CRLOT_EHIP, "call server: request timed out (server paused)");
     }
     const auto t0 = std::chrono::steady_clock::now();
@@ -254,13 +253,25 @@ int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
                 // the request is still in flight in the resident kernel: no later call
                 // may read a slot or speculation it could still write -- until every
                 // request submitted so far has completed (submit re-checks)
-                broken_ = true;
-                broken_at_ = q_;
+                timed_out(load_acq(ctr) < target ? std::min(done(), target - 1) : done());
                 return fail(CRLOT_EHIP, "call server: request timed out (server paused)");
             }
         }
         _mm_pause();
     }
+}
+
+// A request timed out while still in flight: pause the server until every
+// request submitted so far has completed.  If one of those changes an OLA ring
+// (an add / produce, a chained produce, deferred push / clear work), the host's
+// bookkeeping of that object no longer matches what the device will do (a
+// produce that failed here still clears its slots there): that server is never
+// used again, so every later call on its objects fails loudly instead of
+// reading a ring the host cannot account for.
+void CallServer::timed_out(uint64_t done_seen) {
+    broken_ = true;
+    broken_at_ = q_;
+    if (stateful_q_ > done_seen) dead_ = true;
 }
 
 int CallServer::defer(const CallReq::Pend& p) {
@@ -337,6 +348,7 @@ void CallServer::put(float* dst, const float* src, size_t n) {
 }
 
 int CallServer::submit(CallReq& r, const CallSlot& sl) {
+    if (dead_) return fail(CRLOT_EHIP, "call server: a timed-out request left OLA ring state unknown (server disabled)");
     if (broken_) {  // a timed-out request: serve again once everything submitted has completed
         if (done() < broken_at_) return fail(CRLOT_EHIP, "call server: a timed-out request is still in flight");
         broken_ = false;
@@ -351,6 +363,9 @@ int CallServer::submit(CallReq& r, const CallSlot& sl) {
     }
     r.pend = pend_;
     pend_ = CallReq::Pend{};
+    if (r.op == kCallOlaAdd || r.op == kCallOlaProduce || r.pend.flags != 0 ||
+        (r.flags & (kCallChain | kCallPendLate)) != 0)
+        stateful_q_ = q_ + 1;
     if (r.flags & kCallChain) last_chain_ = q_ + 1;
     if (r.flags & kCallPendLate) last_late_ = q_ + 1;
     const int k = int(q_ % uint64_t(depth_));

@@ -92,6 +92,9 @@ class CallServer {
     uint64_t gen_ = 0;                 // arena generation (bumped by every allocation)
     bool broken_ = false;              // a request timed out: the server refuses new work ...
     uint64_t broken_at_ = 0;           // ... until done() reaches the requests submitted by then
+    uint64_t stateful_q_ = 0;          // the last request that changes OLA ring state (1-based)
+    bool dead_ = false;                // a timed-out request had ring work in flight: never again
+    void timed_out(uint64_t done_seen);  // the timeout paths of wait_counter (done_seen: < the target)
     std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
     uint64_t last_chain_ = 0;          // the last request with a chained produce
     CallReq::Pend pend_{};             // deferred ring work (flags 0: none)

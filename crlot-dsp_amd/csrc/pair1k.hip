@@ -772,7 +772,7 @@ constexpr bool pair_hot() {
 }
 
 #ifdef CRLOT_PAIR32_EXPERIMENT
-bool pair32_enabled();                                            // experiments/pair32.hip
+bool pair32_enabled();                                            // tools/experiments/pair32.hip
 hipError_t launch_pair32(const FusedArgs& a, hipStream_t stream);
 #endif
 

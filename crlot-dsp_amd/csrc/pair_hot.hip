@@ -451,9 +451,10 @@ hipError_t launch_wg_hot(int sh, const FusedArgs& a, int64_t grid, hipStream_t s
 }
 
 // ---- N = 4096 / 2048 at three waves per SIMD: a measured negative result kept
-// outside the release library (experiments/pair_wg_hot3.inc); stubs here.
+// outside the release library (tools/experiments/pair_wg_hot3.inc, on the include
+// path of `make experiments` only); stubs here.
 #ifdef CRLOT_PAIR_WG_HOT3_EXPERIMENT
-#include "experiments/pair_wg_hot3.inc"
+#include "pair_wg_hot3.inc"
 #else
 hipError_t launch_pair4k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { return hipErrorInvalidValue; }
 hipError_t launch_pair2k_hot3(int, const FusedArgs&, int64_t, hipStream_t) { return hipErrorInvalidValue; }

@@ -74,7 +74,7 @@ bool pn_lean(int n) {
 int pn_key(int n) {
     return n + 100000 * pn_variant(n) + 1000000 * (pn_halves(n) - 1) + 10000000 * (pn_lean(n) ? 1 : 0);
 }
-// N = 1764 as two 882-point halves on two waves (experiments/pairn_dit.inc,
+// N = 1764 as two 882-point halves on two waves (tools/experiments/pairn_dit.inc,
 // -DCRLOT_PN_DIT_EXPERIMENT builds only: measured 14 % slower than the two-wave
 // 1764-point transform)
 constexpr int kDitHalf = 882;  // the half transform's plan key (one wave, fft_pairn.h)
@@ -364,7 +364,7 @@ void k_pairn(const FusedArgs a) {
 }
 
 #ifdef CRLOT_PN_DIT_EXPERIMENT
-#include "experiments/pairn_dit.inc"
+#include "pairn_dit.inc"  // tools/experiments (`make experiments`)
 #endif
 
 namespace {

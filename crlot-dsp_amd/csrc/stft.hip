@@ -130,11 +130,17 @@ struct Cfg {
     // of K_stft in registers); N = 4096 reads them from L2, so the LDS holds only
     // the twiddles and the four exchange buffers
     static constexpr bool TL = E <= 16;
+    static constexpr bool WREG = E <= 8;  // K_stft: the analysis window in registers
 };
 
 // ------------------------------------------------------------------ K_stft
 template <int E>
-__global__ __launch_bounds__(64 * kW) void k_stft(const StftArgs a) {
+struct StftOcc {
+    static constexpr int value = E <= 2 ? 8 : E <= 4 ? 6 : E <= 8 ? 4 : E <= 16 ? 3 : 2;
+};
+
+template <int E>
+__global__ __launch_bounds__(64 * kW, StftOcc<E>::value) void k_stft(const StftArgs a) {
     using C = Cfg<E>;
     constexpr int P = C::P;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -163,8 +169,8 @@ __global__ __launch_bounds__(64 * kW) void k_stft(const StftArgs a) {
     const float* xs = a.x + int64_t(s) * a.ld_x;
     float* so = a.spec + int64_t(s) * a.ld_spec;
     const float2* wa2 = reinterpret_cast<const float2*>(a.t.wa);
-    float2 wr[C::TL ? E : 1];
-    if constexpr (C::TL) {
+    float2 wr[C::WREG ? E : 1];
+    if constexpr (C::WREG) {
 #pragma unroll
         for (int m = 0; m < E; ++m) wr[m] = wa2[lane + 64 * m];
     }
@@ -175,7 +181,7 @@ __global__ __launch_bounds__(64 * kW) void k_stft(const StftArgs a) {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             float2 w;
-            if constexpr (C::TL) w = wr[m];
+            if constexpr (C::WREG) w = wr[m];
             else w = wa2[lane + 64 * m];
             v[m].r = dev::sanit(xr[m].x * w.x);  // harness frame[i] * w[i], then the adapter's sanitize
             v[m].i = dev::sanit(xr[m].y * w.y);
@@ -202,18 +208,34 @@ __global__ __launch_bounds__(64 * kW) void k_stft(const StftArgs a) {
 }
 
 // ------------------------------------------------------------------ K_istft
+// Waves per SIMD the walkers are compiled for (registers: 512 / waves per lane).
+template <int E, bool XIN>
+struct IstftOcc {
+    static constexpr int value = E <= 2 ? 6 : E <= 4 ? 5 : E <= 8 ? 3 : 2;
+};
+
+// Per-wave LDS of K_istft: the spectrum of the frame (P + 2 float pairs, X[0..P];
+// the inverse FFT's exchange buffer once the merge has read it) and its mask row
+// (P + 2 floats).
+template <int E>
+constexpr int istft_wave_floats() {
+    return 2 * (64 * E + 2) + (64 * E + 2);
+}
+
 template <int E, int S, bool XIN>
-__global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
+__global__ __launch_bounds__(64 * kW, (IstftOcc<E, XIN>::value)) void k_istft(const StftArgs a) {
     using C = Cfg<E>;
     constexpr int P = C::P, N = C::N, H = 128 * S, NB = E / S;
     static_assert(NB * S == E, "N = NB * H");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     cf* tw = reinterpret_cast<cf*>(smem);
-    cf* st = tw + C::TW;                                  // [P] when TL
+    cf* st = tw + C::TW;                                          // [P] when TL
     float* wsn = reinterpret_cast<float*>(st + (C::TL ? P : 0));  // [N] when TL
-    float* wa = wsn + (C::TL ? N : 0);                    // [N] when TL and XIN
-    cf* bufs = reinterpret_cast<cf*>(wa + (C::TL && XIN ? N : 0));
+    float* wa = wsn + (C::TL ? N : 0);                            // [N] when TL and XIN
+    float* gl = wa + (C::TL && XIN ? N : 0);                      // [P + 2] when TL (gain)
+    float* wbase = gl + (C::TL ? P + 2 : 0);                      // per wave: istft_wave_floats
     const cf* gst = reinterpret_cast<const cf*>(a.t.st);
+    const bool has_gain = a.t.gain != nullptr;
     {
         const cf* gtw = reinterpret_cast<const cf*>(a.t.tw);
         for (int i = threadIdx.x; i < C::TW; i += 64 * kW) tw[i] = gtw[i];
@@ -223,14 +245,24 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
                 wsn[i] = a.t.wsn[i];
                 if constexpr (XIN) wa[i] = a.t.wa[i];
             }
+            // the gain table (ones without a gain: x * 1 == x, so the step is branch-free)
+            for (int i = threadIdx.x; i <= P; i += 64 * kW) gl[i] = has_gain ? a.t.gain[i] : 1.0f;
         }
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    cf* buf = bufs + wave * P;
+    cf* buf = reinterpret_cast<cf*>(wbase + wave * istft_wave_floats<E>());  // [P + 2]: spectrum / FFT exchange
+    float* mb = reinterpret_cast<float*>(buf + P + 2);                       // [P + 2]: mask row
     const int gw = blockIdx.x * kW + wave;
     if (gw >= a.n_streams * a.n_chunks) return;
+    if constexpr (C::TL) {
+        if (!a.mask.p) {  // no mask: a row of ones, set once (the step stays branch-free)
+#pragma unroll
+            for (int m = 0; m < E; ++m) mb[lane + 64 * m] = 1.0f;
+            if (lane == 0) mb[P] = 1.0f;
+        }
+    }
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M;
     const int f1 = min(a.F, f0 + a.M);
@@ -238,11 +270,30 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
     const float* xs = XIN ? a.x + int64_t(s) * a.ld_x : nullptr;
     const float* ss = XIN ? nullptr : a.sin + int64_t(s) * a.ld_spec;
     float* ys = a.y + int64_t(s) * a.ld_y;
-    const float* gain = a.t.gain;
+    const float* gain = C::TL ? gl : a.t.gain;
     const float* mbase = a.mask.p ? a.mask.p + int64_t(s) * a.mask.ld_stream : nullptr;
     const float g = a.gain;
     const float2* wa2 = reinterpret_cast<const float2*>(XIN && C::TL ? wa : a.t.wa);
     const float2* ws2 = reinterpret_cast<const float2*>(C::TL ? wsn : a.t.wsn);
+
+    // frame k's spectrum row X[0..P] (lane l: X[l + 64 m], lane 0 also X[P]) and mask
+    // row, into registers: issued one step ahead, stored to the wave's LDS when used
+    float2 ps[XIN ? 1 : E], pP = make_float2(0.f, 0.f);
+    float pm[E], pmP = 0.f;
+    auto load_rows = [&](int k) {
+        if constexpr (!XIN) {
+            const float2* row = reinterpret_cast<const float2*>(ss + int64_t(k) * a.ld_frame);
+#pragma unroll
+            for (int m = 0; m < E; ++m) ps[m] = row[lane + 64 * m];
+            if (lane == 0) pP = row[P];
+        }
+        if (mbase) {
+            const float* mr = mbase + int64_t(k) * a.mask.ld_frame;
+#pragma unroll
+            for (int m = 0; m < E; ++m) pm[m] = mr[lane + 64 * m];
+            if (lane == 0) pmP = mr[P];
+        }
+    };
 
     float2 acc[NB][S];
 #pragma unroll
@@ -250,7 +301,11 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
 #pragma unroll
         for (int q = 0; q < S; ++q) acc[j][q] = make_float2(0.f, 0.f);
     float2 xin[XIN ? E : 1];
-    if constexpr (XIN) load_part<0, E, E>(xin, xs, int64_t(fs) * H - a.pad, a.T, a.pad_mode, lane);
+    if constexpr (XIN) {
+        load_part<0, E, E>(xin, xs, int64_t(fs) * H - a.pad, a.T, a.pad_mode, lane);
+    } else {
+        load_rows(fs);
+    }
 
     for (int k = fs; k < f1; ++k) {
         // prefetch: frame k+1's new hop (XIN) and block k's divisors, consumed at the
@@ -258,6 +313,7 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
         float2 nxt[XIN ? E : 1];
         if constexpr (XIN) {
             if (k + 1 < f1) load_part<E - S, S, E>(nxt, xs, int64_t(k + 1) * H - a.pad, a.T, a.pad_mode, lane);
+            load_rows(k);  // the mask row: lands during the forward transform
         }
         float2 dn[S], rn[S];
         if (k >= f0) {
@@ -269,10 +325,8 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
                 rn[q] = r2[lane + 64 * q];
             }
         }
-        // the spectrum of frame k: X[b] and X[P-b] for b = lane + 64 m
-        cf xk[E], xp[E];
+        cf v[E];
         if constexpr (XIN) {
-            cf v[E];
 #pragma unroll
             for (int m = 0; m < E; ++m) {
                 const float2 w = wa2[lane + 64 * m];
@@ -282,10 +336,28 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
             dev::fft_wave<E, false>(v, buf, tw, lane);
 #pragma unroll
             for (int m = 0; m < E; ++m) buf[lane + 64 * m] = v[m];
-            dev::wave_lds_fence();
+        } else {
 #pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const int b = lane + 64 * m;
+            for (int m = 0; m < E; ++m) buf[lane + 64 * m] = cf{ps[m].x, ps[m].y};
+            if (lane == 0) buf[P] = cf{pP.x, pP.y};
+        }
+        if (mbase) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) mb[lane + 64 * m] = pm[m];
+            if (lane == 0) mb[P] = pmP;
+        }
+        dev::wave_lds_fence();
+        if constexpr (!XIN) {
+            if (k + 1 < f1) load_rows(k + 1);  // in flight during this frame's inverse
+        }
+        // per bin b = lane + 64 m: X[b] and X[P-b] (from the spectrum, or -- XIN -- as
+        // k_rfft's lanes b and P-b compute them from Z), the spectral step (the plan's
+        // gain, then row k of the mask), then kiss_fftri's merge into Z'[b]
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int b = lane + 64 * m;
+            cf xk, xp;
+            if constexpr (XIN) {
                 const cf zp = buf[(P - b) & (P - 1)];
                 cf h0, h1;
                 if constexpr (C::TL) {
@@ -295,50 +367,27 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
                     h0 = gst[b];
                     h1 = gst[(P - b) & (P - 1)];
                 }
-                // X[b] as k_rfft's lane b writes it, X[P-b] as lane P-b does (b > 0)
-                xk[m] = split_bin(v[m], zp, cf{h0.r * 0.5f, h0.i * 0.5f});
-                xp[m] = split_bin(zp, v[m], cf{h1.r * 0.5f, h1.i * 0.5f});
-                if (b == 0) dev::dc_split(v[m], xk[m], xp[m]);
+                xk = split_bin(v[m], zp, cf{h0.r * 0.5f, h0.i * 0.5f});
+                xp = split_bin(zp, v[m], cf{h1.r * 0.5f, h1.i * 0.5f});
+                if (b == 0) dev::dc_split(v[m], xk, xp);
+            } else {
+                xk = buf[b];
+                xp = buf[P - b];  // (b = 0: X[P])
             }
-            dev::wave_lds_fence();
-        } else {
-            const float2* row = reinterpret_cast<const float2*>(ss + int64_t(k) * a.ld_frame);
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const int b = lane + 64 * m;
-                const float2 u = row[b], w = row[P - b];  // (b = 0: X[P])
-                xk[m] = cf{u.x, u.y};
-                xp[m] = cf{w.x, w.y};
+            if (C::TL || has_gain) {
+                xk = scale(xk, gain[b]);
+                xp = scale(xp, gain[P - b]);
             }
-        }
-        // the spectral step: the plan's per-bin gain, then row k of the mask
-        if (gain) {
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const int b = lane + 64 * m;
-                xk[m] = scale(xk[m], gain[b]);
-                xp[m] = scale(xp[m], gain[P - b]);
+            if (C::TL || mbase) {
+                xk = scale(xk, mb[b]);
+                xp = scale(xp, mb[P - b]);
             }
-        }
-        if (mbase) {
-            const float* mr = mbase + int64_t(k) * a.mask.ld_frame;
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const int b = lane + 64 * m;
-                xk[m] = scale(xk[m], mr[b]);
-                xp[m] = scale(xp[m], mr[P - b]);
-            }
-        }
-        cf v[E];
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int b = lane + 64 * m;
             cf w;
             if constexpr (C::TL) w = st[b];
             else w = gst[b];
-            v[m] = merge_bin(xk[m], xp[m], w);
-            if (b == 0) v[m] = dev::dc_merge(xk[m], xp[m]);
+            v[m] = b == 0 ? dev::dc_merge(xk, xp) : merge_bin(xk, xp, w);
         }
+        dev::wave_lds_fence();
         dev::fft_wave<E, true>(v, buf, tw, lane);
         // *1/N and sanitize (folded: sanit_scaled, ws / N), synthesis window, OLA in ascending k
 #pragma unroll
@@ -379,6 +428,7 @@ __global__ __launch_bounds__(64 * kW) void k_istft(const StftArgs a) {
 #pragma unroll
             for (int m = E - S; m < E; ++m) xin[m] = nxt[m];
         }
+        dev::wave_lds_fence();  // (the next frame's stores to buf follow this one's reads)
     }
 }
 
@@ -432,8 +482,8 @@ size_t stft_lds() {
 template <int E, bool XIN>
 size_t istft_lds() {
     using C = Cfg<E>;
-    return sizeof(cf) * (C::TW + (C::TL ? C::P : 0) + kW * C::P) +
-           sizeof(float) * (C::TL ? (XIN ? 2 : 1) * C::N : 0);
+    return sizeof(cf) * (C::TW + (C::TL ? C::P : 0)) +
+           sizeof(float) * ((C::TL ? (XIN ? 2 : 1) * C::N + C::P + 2 : 0) + kW * istft_wave_floats<E>());
 }
 
 int cus() {

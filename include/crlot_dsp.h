@@ -97,6 +97,10 @@ typedef struct crlot_plan_desc {
 
 const char* crlot_last_error(void);
 int crlot_abi_version(void);
+/* What this binary was built from: "src:<hash> arch:gfx950", the hash being
+ * tools/src_hash.py's lib_hash() of the library's sources at build time (a
+ * prebuilt library older than the tree it ships in shows a different hash). */
+const char* crlot_build_info(void);
 
 /* ---------------------------------------------------------------- plan */
 int crlot_plan_create(const crlot_plan_desc* desc, crlot_plan** out);

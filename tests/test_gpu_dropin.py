@@ -1414,3 +1414,86 @@ def test_e2e_loop_with_time_varying_mask_backs_off(pkg, oracle, torch_cuda, n, h
     ref = _oracle_outputs(oracle, n, h, pkg.window_table(pkg.HANN, n), pushed)
     for k in range(len(blocks)):
         assert np.array_equal(bits(blocks[k]), bits(ref[k])), ("oracle", k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gain_from", [0, 5, 40])
+def test_harness_order_with_a_gain_learned_late(pkg, oracle, torch_cuda, gain_from):
+    """the harness's literal order (push every frame, then
+    produce) with a spectral gain that starts at frame `gain_from`.  The batch
+    learns the gain there and redoes the window's later inverses; the object's
+    wrapped ring (precomputed with the chain from the ungained inverses) must be
+    rebuilt from the redone rows.  Bits equal the per-call path's."""
+    n, h = 1024, 256
+    x = oracle.synth(48_000, 31)
+    w = pkg.window_table(pkg.HANN, n)
+    g = (0.25 + 0.75 * np.cos(np.pi * np.arange(n // 2 + 1) / (n // 2)) ** 2).astype(np.float32)
+
+    def run():
+        fr = pkg.Framer()
+        fr.set_params(n, h, 1, pkg.ZERO_PAD)
+        fft = pkg.FftPlan(n, pkg.FFT_REAL)
+        ola = pkg.OLAAccumulator(pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1,
+                                               eps=1e-8, apply_window_inside=True))
+        ola.set_window(w)
+        fr.push(x)
+        k = 0
+        while True:
+            f = fr.pop()
+            if f is None:
+                break
+            X = np.asarray(fft.forward_host((f * w).astype(np.float32)[None])).copy()
+            if k >= gain_from:
+                X[0].real *= g
+                X[0].imag *= g
+            ola.push_frame_AoS(fft.inverse_host(X)[0], None, k * h, 0, n, 1.0)
+            k += 1
+        got, chans = ola.produce(48_000, [np.full(48_000, 7.0, np.float32)])
+        out = chans[0].copy()
+        ola.close()
+        fft.close()
+        fr.close()
+        return got, out
+
+    try:
+        pkg.set_call_speculation(1)
+        ga, ya = run()
+        pkg.set_call_speculation(2)
+        s0 = pkg.call_speculation_stats_ex()
+        gb, yb = run()
+        s1 = pkg.call_speculation_stats_ex()
+    finally:
+        pkg.set_call_speculation(2)
+    assert ga == gb
+    assert np.array_equal(bits(ya), bits(yb))
+    assert s1["gains"] - s0["gains"] >= 1, (s0, s1)
+
+
+@pytest.mark.gpu
+def test_timed_out_ola_request_disables_its_server(pkg, torch_cuda):
+    """a timed-out request that changes an OLA ring (a push
+    or produce) has side effects the host never recorded, so the server that ran
+    it is not resumed: every later call on it fails loudly.  (Odd frame size: the
+    object runs on a private server, so no other test's server is touched.)"""
+    n, h = 255, 64
+    cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8, apply_window_inside=False)
+    fr = np.random.default_rng(5).standard_normal(n).astype(np.float32)
+    for op in ("push", "produce"):
+        ola = pkg.OLAAccumulator(cfg)
+        try:
+            ola.push_frame_AoS(fr, None, 0, 0, n, 1.0)
+            ola.produce(h)
+            pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 1)
+            with pytest.raises(Exception):  # (a push may ride on the next request: the produce waits)
+                if op == "push":
+                    ola.push_frame_AoS(fr, None, h, 0, n, 1.0)
+                ola.produce(h)
+            pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 0)
+            import time
+            time.sleep(0.05)
+            with pytest.raises(Exception, match="disabled"):
+                ola.push_frame_AoS(fr, None, 2 * h, 0, n, 1.0)
+                ola.produce(h)
+        finally:
+            pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 0)
+            ola.close()

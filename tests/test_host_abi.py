@@ -29,6 +29,18 @@ def test_library_exports_every_header_symbol(pkg):
     assert L.crlot_abi_version() == 2
 
 
+def test_library_built_from_this_tree(pkg):
+    """crlot_build_info: the source hash baked in at build time equals the tree's
+    (tools/src_hash.py lib_hash), so the library a run loads is the sources' build."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import src_hash
+    info = pkg.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["src"] == src_hash.lib_hash(), info
+
+
 def test_library_has_gfx950_code_object(pkg):
     data = open(pkg.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data

@@ -14,7 +14,7 @@
 #include <cmath>
 #include <cstdlib>
 
-#include "experiments/fft_pair32.h"
+#include "fft_pair32.h"
 #include "fused_common.h"
 
 namespace crlot {
