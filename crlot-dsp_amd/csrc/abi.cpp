@@ -1090,6 +1090,16 @@ int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams
 
 static int masked_roundtrip(crlot_plan* p, crlot::Scratch* sc, const float* d_x, float* d_y, int32_t n_streams,
                             int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, hipStream_t s) {
+    const int64_t out_len = F * p->geo.h, lim = int64_t(1) << 29;
+    const crlot::DevTables t = tables(p);
+    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && t.ptw && t.pden && t.wsn && t.rden &&
+        p->geo.ring_len % p->geo.h == 0 && aligned4(d_x) && aligned4(d_y) && T < lim && out_len + 2 * p->geo.n < lim &&
+        int64_t(n_streams) * (T / p->geo.h + 1) < lim) {
+        // N = 1024 frame pairs (pairing off: the per-frame walk below, bit-identical to istft(stft))
+        const hipError_t e = crlot::launch_pair_masked(p->geo, t, p->mask, d_x, d_y, n_streams, T, ld_x, ld_y, F,
+                                                       out_len, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "masked frame-pair kernel launch");
+    }
     if (masked_walk_ok(p, d_y, ld_y)) {
         const hipError_t e = crlot::launch_roundtrip_masked(p->geo, tables(p), p->mask, d_x, d_y, n_streams, T, ld_x,
                                                             ld_y, F, s);

@@ -151,6 +151,7 @@ int CallServer::alloc(size_t in_cap, size_t out_cap, size_t spec_cap) {
     _mm_sfence();
     q_ = 0;
     spec_req_.assign(size_t(depth_), 0);
+    slot_rings_.assign(2 * size_t(depth_), nullptr);
     return CRLOT_OK;
 }
 
@@ -262,16 +263,32 @@ int CallServer::wait_counter(const uint64_t* ctr, uint64_t target) {
 }
 
 // A request timed out while still in flight: pause the server until every
-// request submitted so far has completed.  If one of those changes an OLA ring
-// (an add / produce, a chained produce, deferred push / clear work), the host's
-// bookkeeping of that object no longer matches what the device will do (a
-// produce that failed here still clears its slots there): that server is never
-// used again, so every later call on its objects fails loudly instead of
-// reading a ring the host cannot account for.
+// request submitted so far has completed.  The OLA rings those requests change
+// (an add / produce, a chained produce, deferred push / clear work) are
+// poisoned: the host's bookkeeping of their objects no longer matches what the
+// device does (a produce that failed here still clears its slots there), so
+// those objects' calls fail loudly until reset() instead of reading a ring the
+// host cannot account for.  Stateless requests (FFTs) resume.
 void CallServer::timed_out(uint64_t done_seen) {
     broken_ = true;
     broken_at_ = q_;
-    if (stateful_q_ > done_seen) dead_ = true;
+    // requests (done_seen, q_] are in flight, at most depth_ of them (next_slot), so
+    // each still owns its slot's record
+    for (uint64_t i = done_seen + 1; i <= q_; ++i) {
+        const size_t k = size_t((i - 1) % uint64_t(depth_));
+        for (int j = 0; j < 2; ++j) {
+            const float* r = slot_rings_[2 * k + size_t(j)];
+            if (r && !poisoned(r) && ola_ring_live(r)) poisoned_.push_back(r);
+        }
+    }
+}
+
+bool CallServer::poisoned(const float* ring) const {
+    return std::find(poisoned_.begin(), poisoned_.end(), ring) != poisoned_.end();
+}
+
+void CallServer::unpoison(const float* ring) {
+    poisoned_.erase(std::remove(poisoned_.begin(), poisoned_.end(), ring), poisoned_.end());
 }
 
 int CallServer::defer(const CallReq::Pend& p) {
@@ -348,7 +365,6 @@ void CallServer::put(float* dst, const float* src, size_t n) {
 }
 
 int CallServer::submit(CallReq& r, const CallSlot& sl) {
-    if (dead_) return fail(CRLOT_EHIP, "call server: a timed-out request left OLA ring state unknown (server disabled)");
     if (broken_) {  // a timed-out request: serve again once everything submitted has completed
         if (done() < broken_at_) return fail(CRLOT_EHIP, "call server: a timed-out request is still in flight");
         broken_ = false;
@@ -363,12 +379,12 @@ int CallServer::submit(CallReq& r, const CallSlot& sl) {
     }
     r.pend = pend_;
     pend_ = CallReq::Pend{};
-    if (r.op == kCallOlaAdd || r.op == kCallOlaProduce || r.pend.flags != 0 ||
-        (r.flags & (kCallChain | kCallPendLate)) != 0)
-        stateful_q_ = q_ + 1;
     if (r.flags & kCallChain) last_chain_ = q_ + 1;
     if (r.flags & kCallPendLate) last_late_ = q_ + 1;
     const int k = int(q_ % uint64_t(depth_));
+    const bool ring_op = r.op == kCallOlaAdd || r.op == kCallOlaProduce || (r.flags & (kCallChain | kCallPendLate));
+    slot_rings_[2 * size_t(k)] = ring_op ? r.p2 : nullptr;
+    slot_rings_[2 * size_t(k) + 1] = r.pend.flags != 0 ? r.pend.ring : nullptr;
     if (wc_inputs_)
         copy_wc(reinterpret_cast<float*>(reqs_ + k), reinterpret_cast<const float*>(&r), sizeof(CallReq) / 4);
     else

@@ -62,6 +62,12 @@ class CallServer {
     int device() const { return device_; }
     const CallHostCtl* host_ctl() const { return hctl_; }  // diagnostics (phase stamps)
 
+    // An OLA ring a request that timed out still changes (or changed) on the device
+    // while the host gave up on it: its object's bookkeeping no longer matches the
+    // ring, so its calls fail until reset() (which zeroes the ring and unpoisons it).
+    bool poisoned(const float* ring) const;
+    void unpoison(const float* ring);
+
    private:
     CallServer() = default;
     int alloc(size_t in_cap, size_t out_cap, size_t spec_cap);
@@ -92,8 +98,11 @@ class CallServer {
     uint64_t gen_ = 0;                 // arena generation (bumped by every allocation)
     bool broken_ = false;              // a request timed out: the server refuses new work ...
     uint64_t broken_at_ = 0;           // ... until done() reaches the requests submitted by then
-    uint64_t stateful_q_ = 0;          // the last request that changes OLA ring state (1-based)
-    bool dead_ = false;                // a timed-out request had ring work in flight: never again
+    // per slot: the OLA rings the request there changes (its add / produce / chained
+    // produce ring, and the ring of the deferred work it carries)
+    std::vector<const float*> slot_rings_;
+    // rings a timed-out request changes behind the host's bookkeeping (poisoned())
+    std::vector<const float*> poisoned_;
     void timed_out(uint64_t done_seen);  // the timeout paths of wait_counter (done_seen: < the target)
     std::vector<uint64_t> spec_req_;   // per slot: request with a pending speculation (0: none)
     uint64_t last_chain_ = 0;          // the last request with a chained produce
@@ -169,5 +178,9 @@ void test_inject_timeouts(int count);
 // the shared server of (device, e) (created on first use; never destroyed);
 // e < 0: the FFT-only server of complex size P = -e (any size, call_any_waves)
 SharedServer* shared_server(int device, int e, int* rc);
+
+// The rings of the live OLA objects (objects.cpp): a timed-out request poisons
+// only those (a ring whose object is gone has no bookkeeping left to protect).
+bool ola_ring_live(const float* ring);
 
 }  // namespace crlot

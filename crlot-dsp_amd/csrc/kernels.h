@@ -384,6 +384,12 @@ hipError_t launch_istft(const Geometry& g, const DevTables& t, const SpecMask& m
 hipError_t launch_roundtrip_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x,
                                    float* y, int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F,
                                    hipStream_t s);
+// ... as frame pairs (K_pair_mask, pair_mask.hip: N = 1024, H = 128 / 256 / 512, the
+// pair tables; equal to the per-frame walk within float32 rounding)
+bool pair_mask_supported(int n, int h);
+hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
+                              int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
+                              hipStream_t s);
 // staged forms: frames[s F + k][N] = x frame * analysis window; out rows (s F + k) of
 // 2 bins floats = spectrum * gain * mask (in place when out aliases the same layout)
 hipError_t launch_frames_windowed(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,

@@ -2143,6 +2143,37 @@ int wg_chunk_target() {
 
 }  // namespace
 
+bool pair_mask_supported(int n, int h) { return n == 1024 && (h == 128 || h == 256 || h == 512); }
+
+// K_pair_mask: K_pair's chunking (whole resident rounds) over its own residency
+hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
+                              int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
+                              hipStream_t stream) {
+    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !m.p || !t.ptw || !t.pden || !t.wsn ||
+        !t.rden || g.ring_len % g.h != 0)
+        return hipErrorInvalidValue;
+    FusedArgs a;
+    a.t = t;
+    a.x = x;
+    a.y = y;
+    a.ld_x = ld_x;
+    a.ld_y = ld_y;
+    a.T = int(T);
+    a.out_len = int(out_len);
+    a.n_streams = n_streams;
+    a.F = int(F);
+    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * fk::pair_mask_walkers_per_cu(),
+                         a.n_chunks, a.M);
+    chunk_override(F, a);
+    note_chunks(a.n_chunks);
+    a.ring_blocks = g.ring_len / g.h;
+    a.pad = g.pad;
+    a.pad_mode = g.pad_mode;
+    a.inv_n = g.inv_n;
+    a.gain = g.gain;
+    return fk::launch_pair_mask(g.h, a, m, int64_t(n_streams) * a.n_chunks, stream);
+}
+
 std::vector<float> build_pair512_twiddles() {
     std::vector<float> t;
     for (int k1 = 1; k1 < 8; ++k1)

@@ -67,6 +67,7 @@ extern "C" const char* crlot_kernel_name(int32_t id) {
         case CRLOT_K_STFT_MASKED: return "k_stft_masked";
         case CRLOT_K_SPEC_STEP: return "k_spec_step";
         case CRLOT_K_FRAMES_W: return "k_frames_w";
+        case CRLOT_K_PAIR_MASK: return "k_pair_mask";
         case CRLOT_K_EXPERIMENT: return "k_experiment";
         default: return "unknown";
     }

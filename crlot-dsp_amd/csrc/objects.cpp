@@ -327,6 +327,18 @@ float peak_of(const float* x, int64_t n) {
 std::mutex g_fresh_mu;
 crlot_ola* g_fresh_ola = nullptr;
 
+// the rings of the live objects (call.h ola_ring_live)
+std::mutex g_rings_mu;
+std::vector<const float*> g_rings;
+void ring_register(const float* r) {
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    g_rings.push_back(r);
+}
+void ring_unregister(const float* r) {
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    g_rings.erase(std::remove(g_rings.begin(), g_rings.end(), r), g_rings.end());
+}
+
 void ola_free(crlot_ola* o) {
     if (!o) return;
     {
@@ -351,6 +363,8 @@ void ola_free(crlot_ola* o) {
         crlot::pool_event_put(o->device, s.ev);
         crlot::pool_pinned_put(s.h, s.cap * sizeof(float));
     }
+    if (o->d_ring) ring_unregister(o->d_ring);
+    if (o->srv) o->srv->unpoison(o->d_ring);  // (the block may serve a later object)
     if (o->own) {
         crlot::pool_free(o->d_ring, o->own);  // the object's one device block (crlot_ola_create)
     }
@@ -483,6 +497,8 @@ int to_server(crlot_ola* o) {
             if (rc != CRLOT_OK) return rc;
         }
     }
+    if (o->srv->poisoned(o->d_ring))
+        return fail(CRLOT_EHIP, "OLA object: a timed-out call left its ring state unknown; reset() it");
     if (o->mode == 1) {
         hipError_t e = o->last_set ? hipStreamSynchronize(o->last) : hipSuccess;
         if (e != hipSuccess) return hip_fail(e, "stream order");
@@ -637,6 +653,7 @@ int server_add(crlot_ola* o, const float* const* rows, int64_t ch, bool aos, con
 // every remaining frame with the object's window and divisors).  1: served.
 int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_sample, int64_t start_off,
                int64_t eff, float gain) {
+    if (o->srv && o->srv->poisoned(o->d_ring)) return 0;  // (the ordinary path reports it)
     crlot::BatchSpec* b = o->shared ? o->shared->batch : nullptr;
     if (!b || crlot::spec_mode() < 2 || b->pushed < 0 || o->C() != 1 || b->n != o->N()) return 0;
     const int64_t j = b->pushed, N = o->N();
@@ -684,6 +701,7 @@ int batch_push(crlot_ola* o, const float* frame, bool caller_win, int64_t start_
 // A mono host produce of n (already clamped to the available count) inside the
 // blocks the batch's pushes have finalised.  1: served into out.
 int batch_produce(crlot_ola* o, float* out, int64_t n) {
+    if (o->srv && o->srv->poisoned(o->d_ring)) return 0;
     crlot::BatchSpec* b = o->vb;
     if (!b || crlot::spec_mode() < 2 || b->ola != o || o->vgen != b->gen || o->flushing || o->C() != 1) return 0;
     if (o->read_pos != o->vread % o->R) return 0;
@@ -774,6 +792,10 @@ int ensure_real(crlot_ola* o) {
 
 namespace crlot {
 int ola_materialize_locked(crlot_ola* o) { return ola_materialize(o); }
+bool ola_ring_live(const float* ring) {
+    std::lock_guard<std::mutex> lk(g_rings_mu);
+    return std::find(g_rings.begin(), g_rings.end(), ring) != g_rings.end();
+}
 // the object read up to the window end's position with every frame before it
 // pushed, so only frames from we - (ceil(N / H) - 1) on reach its unread positions
 bool ola_can_continue(const crlot_ola* o, const BatchSpec* b) {
@@ -824,6 +846,7 @@ int crlot_ola_create(const crlot_ola_config* cfg, crlot_ola** out) {
     o->d_peak = reinterpret_cast<unsigned*>(base + b_ring);
     o->d_den = reinterpret_cast<float*>(base + b_ring + b_peak);
     o->d_win = reinterpret_cast<float*>(base + b_ring + b_peak + b_den);
+    ring_register(o->d_ring);
     if ((e = hipMemsetAsync(o->d_ring, 0, b_ring + sizeof(unsigned), o->own))) {
         ola_free(o);
         return hip_fail(e, "OLA object init");
@@ -1096,6 +1119,7 @@ int crlot_ola_reset(crlot_ola* o) {
     o->last_req_n = 0;
     o->spec.valid = false;
     o->pristine = true;
+    if (o->srv) o->srv->unpoison(o->d_ring);  // (the zeroed ring is known again)
     return upload_norm(o, o->own);
 }
 

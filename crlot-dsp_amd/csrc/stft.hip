@@ -432,6 +432,295 @@ __global__ __launch_bounds__(64 * kW, (IstftOcc<E, XIN>::value)) void k_istft(co
     }
 }
 
+// ------------------------------------------------------------------ workgroup walkers (N = 2048, 4096)
+// One frame on a workgroup of L lanes, E = 8 complex points per lane (lane t
+// holds z[t + L m]), so registers stay at the per-wave E = 8 budget.  The
+// Stockham passes are the per-wave schedule's (radix 8, 8, 8, 4 at P = 2048;
+// 8, 8, 4, ... identical radices and twiddle indices), exchanged through two LDS
+// buffers with one barrier each (fft_wave.h stockham_exchange_wg), so the bits
+// equal the per-wave kernels' (k_rfft / k_irfft) -- crlot_rfft_batched and
+// crlot_irfft_batched + crlot_ola_gather stay the checks.  Twiddles and
+// super-twiddles are staged in LDS (the walks are memory-bound: registers go to
+// the frames in flight).
+template <int E, int L, int NS, int XI, int TOFF, bool INV, typename TW>
+__device__ __forceinline__ void fft_passes_wg_t(cf (&v)[E], cf* buf0, cf* buf1, const cf* twp, int t,
+                                                const TW& tw) {
+    constexpr int P = L * E;
+    if constexpr (NS < P) {
+        constexpr int R = dev::radix_for(P / NS, E);
+        dev::stockham_compute<E, R, NS, INV>(v, tw);
+        if constexpr (NS * R < P) {
+            constexpr int NS2 = NS * R;
+            constexpr int R2 = dev::radix_for(P / NS2, E);
+            constexpr int TOFF2 = TOFF + (NS > 1 ? (R - 1) * NS : 0);
+            dev::PassTw<E, R2, NS2> tw2;
+            dev::load_pass_tw_wg<E, R2, NS2, L, TOFF2>(tw2, twp, t);
+            dev::stockham_exchange_wg<E, R, NS, L>(v, (XI & 1) ? buf1 : buf0, t);
+            fft_passes_wg_t<E, L, NS2, XI + 1, TOFF2, INV>(v, buf0, buf1, twp, t, tw2);
+        }
+    }
+}
+template <int L, bool INV>
+__device__ __forceinline__ void fft_wg(cf (&v)[8], cf* buf0, cf* buf1, const cf* twp, int t) {
+    constexpr int E = 8, R = dev::radix_for(L * E, E);
+    dev::PassTw<E, R, 1> none;
+    fft_passes_wg_t<E, L, 1, 0, 0, INV>(v, buf0, buf1, twp, t, none);
+}
+template <int L>
+struct WgCfg {
+    static constexpr int E = 8, P = L * E, N = 2 * P;
+    static constexpr int TW = dev::twiddle_table_size(P / 64);  // (the per-wave table of this P)
+};
+
+// frame part at origin o for the workgroup layout: r[m] = (x[o + 2i], x[o + 2i + 1]), i = t + L m
+template <int M0, int CNT, int L>
+__device__ __forceinline__ void load_part_wg(float2 (&r)[8], const float* xs, int64_t o, int64_t T, int mode,
+                                             int t) {
+    const int64_t lo = o + 2 * L * M0, hi = o + 2 * L * (M0 + CNT);
+    if (lo >= 0 && hi <= T) {
+        const float* p = xs + o;
+        if ((reinterpret_cast<uintptr_t>(p) & 7u) == 0) {
+#pragma unroll
+            for (int m = M0; m < M0 + CNT; ++m) r[m] = reinterpret_cast<const float2*>(p)[t + L * m];
+        } else {
+#pragma unroll
+            for (int m = M0; m < M0 + CNT; ++m) {
+                const int i = 2 * (t + L * m);
+                r[m] = make_float2(p[i], p[i + 1]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int m = M0; m < M0 + CNT; ++m) {
+            const int64_t j = o + 2 * (t + L * m);
+            r[m] = make_float2(xat(xs, j, T, mode), xat(xs, j + 1, T, mode));
+        }
+    }
+}
+
+// K_stft on a workgroup: blockIdx = (stream, chunk), frames k0 .. k1-1 in order.
+template <int L>
+__global__ __launch_bounds__(L) void k_stft_wg(const StftArgs a) {
+    using C = WgCfg<L>;
+    constexpr int E = 8, P = C::P;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* bufA = tw + C::TW;
+    cf* bufB = bufA + P;
+    const int t = threadIdx.x;
+    for (int i = t; i < C::TW; i += L) tw[i] = reinterpret_cast<const cf*>(a.t.tw)[i];
+    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
+    const int k0 = c * a.M, k1 = min(a.F, k0 + a.M);
+    const float* xs = a.x + int64_t(s) * a.ld_x;
+    float* so = a.spec + int64_t(s) * a.ld_spec;
+    const cf* gst = reinterpret_cast<const cf*>(a.t.st);
+    float2 wa[E];
+    cf sth[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = reinterpret_cast<const float2*>(a.t.wa)[t + L * m];
+        const cf w = gst[t + L * m];
+        sth[m] = cf{w.r * 0.5f, w.i * 0.5f};
+    }
+    float2 xr[E];
+    load_part_wg<0, E, L>(xr, xs, int64_t(k0) * a.h - a.pad, a.T, a.pad_mode, t);
+    __syncthreads();
+    for (int k = k0; k < k1; ++k) {
+        cf v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            v[m].r = dev::sanit(xr[m].x * wa[m].x);
+            v[m].i = dev::sanit(xr[m].y * wa[m].y);
+        }
+        if (k + 1 < k1) load_part_wg<0, E, L>(xr, xs, int64_t(k + 1) * a.h - a.pad, a.T, a.pad_mode, t);
+        // (exchanges A B A, then the split partner through B: 4 per frame, so the
+        // alternation holds across frames)
+        static_assert(dev::fft_exchanges(P, E) == 3, "buffer alternation");
+        fft_wg<L, false>(v, bufA, bufB, tw, t);
+        cf* bx = bufB;
+#pragma unroll
+        for (int m = 0; m < E; ++m) bx[t + L * m] = v[m];
+        __syncthreads();
+        float2* out = reinterpret_cast<float2*>(so + int64_t(k) * a.ld_frame);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int b = t + L * m;
+            cf xk = split_bin(v[m], bx[(P - b) & (P - 1)], sth[m]), xp;
+            if (b == 0) dev::dc_split(v[m], xk, xp);
+            out[b] = make_float2(xk.r, xk.i);
+            if (b == 0) out[P] = make_float2(xp.r, xp.i);
+        }
+    }
+}
+
+// K_istft on a workgroup (XIN: from x, the masked round trip).  The spectral
+// step is applied to each lane's own bins as the spectrum is staged in LDS
+// (X'[b] = X[b] * gain[b] * mask[b]), so the merge reads X'[b] and X'[P-b] with
+// no per-bin tables in LDS.  XIN computes its own bins' X[b] first, exactly as
+// K_stft's lane b does (split of Z[b], Z[P-b] through one exchange), then
+// stages X'[b].  LDS: the twiddles and the two exchange buffers.
+template <int L, int S, bool XIN>
+__global__ __launch_bounds__(L) void k_istft_wg(const StftArgs a) {
+    using C = WgCfg<L>;
+    constexpr int E = 8, P = C::P, N = C::N, H = 2 * L * S, NB = E / S;
+    static_assert(NB * S == E, "N = NB * H");
+    // exchanges per frame: XIN forward A B A, Z partner B, staging A, inverse B A B;
+    // else staging B, inverse A B A -- consecutive exchanges alternate buffers
+    // within and across frames (a buffer is rewritten only behind the barrier of
+    // the exchange that followed its last reads)
+    static_assert(dev::fft_exchanges(P, E) == 3, "buffer alternation");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    cf* tw = reinterpret_cast<cf*>(smem);
+    cf* bufA = tw + C::TW;     // [P + 2]
+    cf* bufB = bufA + P + 2;   // [P + 2]
+    const int t = threadIdx.x;
+    for (int i = t; i < C::TW; i += L) tw[i] = reinterpret_cast<const cf*>(a.t.tw)[i];
+    const int s = blockIdx.x / a.n_chunks, c = blockIdx.x - s * a.n_chunks;
+    const int f0 = c * a.M;
+    const int f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1));
+    const float* xs = XIN ? a.x + int64_t(s) * a.ld_x : nullptr;
+    const float* ss = XIN ? nullptr : a.sin + int64_t(s) * a.ld_spec;
+    float* ys = a.y + int64_t(s) * a.ld_y;
+    const float* mbase = a.mask.p ? a.mask.p + int64_t(s) * a.mask.ld_stream : nullptr;
+    const float g = a.gain;
+    const cf* gst = reinterpret_cast<const cf*>(a.t.st);
+    // this lane's bins b = t + L m: super-twiddle, gain (1 without one), windows
+    float2 wsn[E], wa[XIN ? E : 1];
+    cf st[E];
+    float gb[E], gP = 1.0f;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wsn[m] = reinterpret_cast<const float2*>(a.t.wsn)[t + L * m];
+        if constexpr (XIN) wa[m] = reinterpret_cast<const float2*>(a.t.wa)[t + L * m];
+        st[m] = gst[t + L * m];
+        gb[m] = a.t.gain ? a.t.gain[t + L * m] : 1.0f;
+    }
+    if (t == 0 && a.t.gain) gP = a.t.gain[P];
+    // frame k's spectrum and mask rows, this lane's bins (issued one frame ahead)
+    float2 ps[XIN ? 1 : E], pP = make_float2(0.f, 0.f);
+    float pm[E], pmP = 1.0f;
+#pragma unroll
+    for (int m = 0; m < E; ++m) pm[m] = 1.0f;
+    auto load_rows = [&](int k) {
+        if constexpr (!XIN) {
+            const float2* row = reinterpret_cast<const float2*>(ss + int64_t(k) * a.ld_frame);
+#pragma unroll
+            for (int m = 0; m < E; ++m) ps[m] = row[t + L * m];
+            if (t == 0) pP = row[P];
+        }
+        if (mbase) {
+            const float* mr = mbase + int64_t(k) * a.mask.ld_frame;
+#pragma unroll
+            for (int m = 0; m < E; ++m) pm[m] = mr[t + L * m];
+            if (t == 0) pmP = mr[P];
+        }
+    };
+    float2 acc[NB][S];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[j][q] = make_float2(0.f, 0.f);
+    float2 xin[E];
+    if constexpr (XIN) load_part_wg<0, E, L>(xin, xs, int64_t(fs) * H - a.pad, a.T, a.pad_mode, t);
+    load_rows(fs);
+    __syncthreads();
+
+    for (int k = fs; k < f1; ++k) {
+        float2 nxt[E];
+        if constexpr (XIN) {
+            if (k + 1 < f1) load_part_wg<E - S, S, L>(nxt, xs, int64_t(k + 1) * H - a.pad, a.T, a.pad_mode, t);
+        }
+        float2 dn[S], rn[S];
+        if (k >= f0) {
+            const float2* d2 = reinterpret_cast<const float2*>(a.t.den + (k % a.ring_blocks) * H);
+            const float2* r2 = reinterpret_cast<const float2*>(a.t.rden + (k % a.ring_blocks) * H);
+#pragma unroll
+            for (int q = 0; q < S; ++q) {
+                dn[q] = d2[t + L * q];
+                rn[q] = r2[t + L * q];
+            }
+        }
+        // this lane's X[b] (and lane 0's X[P])
+        cf xk[E], xP = cf{0.f, 0.f};
+        if constexpr (XIN) {
+            cf v[E];
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                v[m].r = dev::sanit(xin[m].x * wa[m].x);
+                v[m].i = dev::sanit(xin[m].y * wa[m].y);
+            }
+            fft_wg<L, false>(v, bufA, bufB, tw, t);
+#pragma unroll
+            for (int m = 0; m < E; ++m) bufB[t + L * m] = v[m];
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const int b = t + L * m;
+                xk[m] = split_bin(v[m], bufB[(P - b) & (P - 1)], cf{st[m].r * 0.5f, st[m].i * 0.5f});
+                if (b == 0) dev::dc_split(v[m], xk[m], xP);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < E; ++m) xk[m] = cf{ps[m].x, ps[m].y};
+            xP = cf{pP.x, pP.y};
+        }
+        // the spectral step on this lane's bins, staged for the merge
+        cf* bx = XIN ? bufA : bufB;
+#pragma unroll
+        for (int m = 0; m < E; ++m) bx[t + L * m] = scale(scale(xk[m], gb[m]), pm[m]);
+        if (t == 0) bx[P] = scale(scale(xP, gP), pmP);
+        __syncthreads();
+        if (k + 1 < f1) load_rows(k + 1);  // in flight during the merge and the inverse
+        cf v[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int b = t + L * m;
+            const cf x0 = bx[b], x1 = bx[P - b];  // (b = 0: X'[P])
+            v[m] = b == 0 ? dev::dc_merge(x0, x1) : merge_bin(x0, x1, st[m]);
+        }
+        if constexpr (XIN) fft_wg<L, true>(v, bufB, bufA, tw, t);
+        else fft_wg<L, true>(v, bufA, bufB, tw, t);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float o0 = dev::sanit_scaled<N>(v[m].r);
+            const float o1 = dev::sanit_scaled<N>(v[m].i);
+            float2& r = acc[m / S][m % S];
+            r.x = __builtin_fmaf(__builtin_fmaf(o0, wsn[m].x, 0.0f), g, r.x);
+            r.y = __builtin_fmaf(__builtin_fmaf(o1, wsn[m].y, 0.0f), g, r.y);
+        }
+        if (k >= f0) {
+            float2* yo = reinterpret_cast<float2*>(ys + int64_t(k) * H);
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < S; ++q) ok = ok && mk_ok(acc[0][q].x) && mk_ok(acc[0][q].y);
+            // (a per-wave choice: both divisions give the same bits where Markstein's is valid)
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+#pragma unroll
+                for (int q = 0; q < S; ++q)
+                    yo[t + L * q] = make_float2(mk_div(acc[0][q].x, dn[q].x, rn[q].x),
+                                                mk_div(acc[0][q].y, dn[q].y, rn[q].y));
+            } else {
+#pragma unroll
+                for (int q = 0; q < S; ++q)
+                    yo[t + L * q] = make_float2(acc[0][q].x / dn[q].x, acc[0][q].y / dn[q].y);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int q = 0; q < S; ++q) acc[j][q] = acc[j + 1][q];
+#pragma unroll
+        for (int q = 0; q < S; ++q) acc[NB - 1][q] = make_float2(0.f, 0.f);
+        if constexpr (XIN) {
+#pragma unroll
+            for (int m = 0; m < E - S; ++m) xin[m] = xin[m + S];
+#pragma unroll
+            for (int m = E - S; m < E; ++m) xin[m] = nxt[m];
+        }
+    }
+}
+
 // ------------------------------------------------------------------ staged forms
 // frames[r][i] = x[k H - pad + i] * wa[i] (padding rule outside [0, T)), r = s F + k:
 // the analysis products of every frame, for the mixed-radix rfft (which sanitizes).
@@ -485,6 +774,14 @@ size_t istft_lds() {
     return sizeof(cf) * (C::TW + (C::TL ? C::P : 0)) +
            sizeof(float) * ((C::TL ? (XIN ? 2 : 1) * C::N + C::P + 2 : 0) + kW * istft_wave_floats<E>());
 }
+template <int L>
+size_t stft_wg_lds() {
+    return sizeof(cf) * (WgCfg<L>::TW + 2 * WgCfg<L>::P);
+}
+template <int L>
+size_t istft_wg_lds() {
+    return sizeof(cf) * (WgCfg<L>::TW + 2 * (WgCfg<L>::P + 2));
+}
 
 int cus() {
     static const int v = [] {
@@ -497,15 +794,14 @@ int cus() {
     return v;
 }
 
-// Chunks per stream: enough waves for two resident rounds of the device
-// (`per_cu` workgroups of kW waves per CU), chunks of about 128 frames while the
-// grid stays that deep, at least `min_m` frames each (the istft walk recomputes
-// NB-1 warm-up frames per chunk); the plan's chunk knob overrides.
-void pick_chunks(int64_t F, int n_streams, int per_cu, int min_m, int& n_chunks, int& m) {
+// Chunks per stream: enough walkers for two resident rounds of the device
+// (`resident` walkers at once), chunks of about 128 frames while the grid stays
+// that deep, at least `min_m` frames each (the istft walk recomputes NB-1
+// warm-up frames per chunk); the plan's chunk knob overrides.
+void pick_chunks(int64_t F, int n_streams, int64_t resident, int min_m, int& n_chunks, int& m) {
     const int64_t S = std::max(1, n_streams);
-    const int64_t resident = int64_t(std::max(1, per_cu)) * kW * cus();
     int64_t n = (F + 127) / 128;
-    n = std::max<int64_t>(n, (2 * resident + S - 1) / S);
+    n = std::max<int64_t>(n, (2 * std::max<int64_t>(1, resident) + S - 1) / S);
     n = std::min<int64_t>(n, std::max<int64_t>(1, F / std::max(1, min_m)));
     if (const int64_t c = chunks_or(0, F); c > 0) n = c;
     n = std::max<int64_t>(1, std::min<int64_t>(n, F));
@@ -513,27 +809,28 @@ void pick_chunks(int64_t F, int n_streams, int per_cu, int min_m, int& n_chunks,
     n_chunks = int((F + m - 1) / m);
 }
 
+// walkers the device holds at once: workgroups per CU x walkers per workgroup x CUs
 template <typename K>
-int blocks_per_cu(K kernel, size_t lds) {
+int64_t resident_walkers(K kernel, int threads, size_t lds, int walkers_per_block) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel), 64 * kW, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kernel), threads, lds) !=
             hipSuccess ||
         nb <= 0)
         nb = 1;
-    return nb;
+    return int64_t(nb) * walkers_per_block * cus();
 }
 
-template <int E>
-hipError_t stft_e(StftArgs& a, hipStream_t stream) {
-    auto k = k_stft<E>;
-    const size_t lds = stft_lds<E>();
-    hipError_t e = set_lds(k, lds);
+// one launch of a walker kernel: `walkers` (stream, chunk) walks, `per_block` per workgroup
+template <typename K>
+hipError_t launch_walk(K kernel, int32_t id, int threads, int per_block, size_t lds, int min_m, StftArgs& a,
+                       hipStream_t stream) {
+    hipError_t e = set_lds(kernel, lds);
     if (e != hipSuccess) return e;
-    pick_chunks(a.F, a.n_streams, blocks_per_cu(k, lds), 1, a.n_chunks, a.M);
+    pick_chunks(a.F, a.n_streams, resident_walkers(kernel, threads, lds, per_block), min_m, a.n_chunks, a.M);
     note_chunks(a.n_chunks);
-    const int64_t grid = (int64_t(a.n_streams) * a.n_chunks + kW - 1) / kW;
-    note_launch(CRLOT_K_STFT, grid);
-    hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * kW), lds, stream, a);
+    const int64_t grid = (int64_t(a.n_streams) * a.n_chunks + per_block - 1) / per_block;
+    note_launch(id, grid);
+    hipLaunchKernelGGL(kernel, dim3(unsigned(grid)), dim3(threads), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -542,19 +839,10 @@ hipError_t istft_es(StftArgs& a, hipStream_t stream) {
     if constexpr (S > E) {
         return hipErrorInvalidValue;
     } else {
-        auto k = k_istft<E, S, XIN>;
-        const size_t lds = istft_lds<E, XIN>();
-        hipError_t e = set_lds(k, lds);
-        if (e != hipSuccess) return e;
-        pick_chunks(a.F, a.n_streams, blocks_per_cu(k, lds), std::max(4, E / S), a.n_chunks, a.M);
-        note_chunks(a.n_chunks);
-        const int64_t grid = (int64_t(a.n_streams) * a.n_chunks + kW - 1) / kW;
-        note_launch(XIN ? CRLOT_K_STFT_MASKED : CRLOT_K_ISTFT, grid);
-        hipLaunchKernelGGL(k, dim3(unsigned(grid)), dim3(64 * kW), lds, stream, a);
-        return hipGetLastError();
+        return launch_walk(k_istft<E, S, XIN>, XIN ? CRLOT_K_STFT_MASKED : CRLOT_K_ISTFT, 64 * kW, kW,
+                           istft_lds<E, XIN>(), std::max(4, E / S), a, stream);
     }
 }
-
 template <int E, bool XIN>
 hipError_t istft_e(int s, StftArgs& a, hipStream_t stream) {
     switch (s) {
@@ -562,20 +850,34 @@ hipError_t istft_e(int s, StftArgs& a, hipStream_t stream) {
         case 2: return istft_es<E, 2, XIN>(a, stream);
         case 4: return istft_es<E, 4, XIN>(a, stream);
         case 8: return istft_es<E, 8, XIN>(a, stream);
-        case 16: return istft_es<E, 16, XIN>(a, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+template <int L, int S, bool XIN>
+hipError_t istft_wg_s(StftArgs& a, hipStream_t stream) {
+    return launch_walk(k_istft_wg<L, S, XIN>, XIN ? CRLOT_K_STFT_MASKED : CRLOT_K_ISTFT, L, 1, istft_wg_lds<L>(),
+                       std::max(4, 8 / S), a, stream);
+}
+template <int L, bool XIN>
+hipError_t istft_wg(int s, StftArgs& a, hipStream_t stream) {
+    switch (s) {
+        case 1: return istft_wg_s<L, 1, XIN>(a, stream);
+        case 2: return istft_wg_s<L, 2, XIN>(a, stream);
+        case 4: return istft_wg_s<L, 4, XIN>(a, stream);
+        case 8: return istft_wg_s<L, 8, XIN>(a, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
+// N <= 1024: one frame per wave; N = 2048 / 4096: one frame per 128 / 256-lane workgroup
 template <bool XIN>
 hipError_t istft_dispatch(int n, int h, StftArgs& a, hipStream_t stream) {
-    const int s = h / 128;
-    switch (e_of_n(n)) {
-        case 2: return istft_e<2, XIN>(s, a, stream);
-        case 4: return istft_e<4, XIN>(s, a, stream);
-        case 8: return istft_e<8, XIN>(s, a, stream);
-        case 16: return istft_e<16, XIN>(s, a, stream);
-        case 32: return istft_e<32, XIN>(s, a, stream);
+    switch (n) {
+        case 256: return istft_e<2, XIN>(h / 128, a, stream);
+        case 512: return istft_e<4, XIN>(h / 128, a, stream);
+        case 1024: return istft_e<8, XIN>(h / 128, a, stream);
+        case 2048: return istft_wg<128, XIN>(h / 256, a, stream);
+        case 4096: return istft_wg<256, XIN>(h / 512, a, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -598,10 +900,11 @@ StftArgs base_args(const Geometry& g, const DevTables& t, int n_streams, int64_t
 bool stft_supported(int n) { return e_of_n(n) != 0; }
 
 bool istft_walk_supported(int n, int h) {
-    const int e = e_of_n(n);
-    if (e == 0 || h % 128 != 0 || n % h != 0) return false;
-    const int s = h / 128;
-    return s <= e && (s == 1 || s == 2 || s == 4 || s == 8 || s == 16);
+    if (e_of_n(n) == 0 || h <= 0 || n % h != 0) return false;
+    const int unit = n <= 1024 ? 128 : n / 8;  // per-wave: 2 x 64 lanes; workgroup: 2 x n / 16 lanes
+    if (h % unit != 0) return false;
+    const int s = h / unit;
+    return s == 1 || s == 2 || s == 4 || s == 8;
 }
 
 hipError_t launch_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
@@ -614,12 +917,12 @@ hipError_t launch_stft(const Geometry& g, const DevTables& t, const float* x, in
     a.spec = spec;
     a.ld_spec = ld_spec;
     a.ld_frame = ld_frame;
-    switch (e_of_n(g.n)) {
-        case 2: return stft_e<2>(a, stream);
-        case 4: return stft_e<4>(a, stream);
-        case 8: return stft_e<8>(a, stream);
-        case 16: return stft_e<16>(a, stream);
-        case 32: return stft_e<32>(a, stream);
+    switch (g.n) {
+        case 256: return launch_walk(k_stft<2>, CRLOT_K_STFT, 64 * kW, kW, stft_lds<2>(), 1, a, stream);
+        case 512: return launch_walk(k_stft<4>, CRLOT_K_STFT, 64 * kW, kW, stft_lds<4>(), 1, a, stream);
+        case 1024: return launch_walk(k_stft<8>, CRLOT_K_STFT, 64 * kW, kW, stft_lds<8>(), 1, a, stream);
+        case 2048: return launch_walk(k_stft_wg<128>, CRLOT_K_STFT, 128, 1, stft_wg_lds<128>(), 1, a, stream);
+        case 4096: return launch_walk(k_stft_wg<256>, CRLOT_K_STFT, 256, 1, stft_wg_lds<256>(), 1, a, stream);
         default: return hipErrorInvalidValue;
     }
 }

@@ -1470,30 +1470,41 @@ def test_harness_order_with_a_gain_learned_late(pkg, oracle, torch_cuda, gain_fr
 
 
 @pytest.mark.gpu
-def test_timed_out_ola_request_disables_its_server(pkg, torch_cuda):
+def test_timed_out_ola_request_poisons_its_object(pkg, torch_cuda):
     """a timed-out request that changes an OLA ring (a push
-    or produce) has side effects the host never recorded, so the server that ran
-    it is not resumed: every later call on it fails loudly.  (Odd frame size: the
-    object runs on a private server, so no other test's server is touched.)"""
-    n, h = 255, 64
+    or produce) has side effects the host never recorded.  The object's ring is
+    poisoned: every later call on it fails loudly until reset(), which zeroes the
+    ring; after that its calls give the bits of a fresh object.  Stateless FFT
+    calls on the same server resume (test_call_server_recovers_...)."""
+    import time
+    n, h = 1024, 256
     cfg = pkg.OLAConfig(sample_rate=48000, frame_size=n, hop_size=h, channels=1, eps=1e-8, apply_window_inside=False)
     fr = np.random.default_rng(5).standard_normal(n).astype(np.float32)
+
+    def fresh_run(ola):
+        ola.push_frame_AoS(fr, None, 0, 0, n, 1.0)
+        got, ch = ola.produce(h)
+        return ch[0][:got].copy()
+
+    ref_ola = pkg.OLAAccumulator(cfg)
+    ref = fresh_run(ref_ola)
+    ref_ola.close()
     for op in ("push", "produce"):
         ola = pkg.OLAAccumulator(cfg)
         try:
-            ola.push_frame_AoS(fr, None, 0, 0, n, 1.0)
-            ola.produce(h)
+            fresh_run(ola)
             pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 1)
             with pytest.raises(Exception):  # (a push may ride on the next request: the produce waits)
                 if op == "push":
                     ola.push_frame_AoS(fr, None, h, 0, n, 1.0)
                 ola.produce(h)
             pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 0)
-            import time
-            time.sleep(0.05)
-            with pytest.raises(Exception, match="disabled"):
+            time.sleep(0.05)  # the timed-out request completes on the device
+            with pytest.raises(Exception, match="reset"):
                 ola.push_frame_AoS(fr, None, 2 * h, 0, n, 1.0)
                 ola.produce(h)
+            ola.reset()
+            assert np.array_equal(bits(fresh_run(ola)), bits(ref))
         finally:
             pkg.test_inject(pkg.INJECT_CALL_TIMEOUT, 0)
             ola.close()

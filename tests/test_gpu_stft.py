@@ -13,8 +13,11 @@ Bars (tests/test_gpu_parity.py):
     (rel-L2 <= 1e-6, max-abs <= 4e-6 of the input / spectrum scale);
   * bit-exact: crlot_stft vs crlot_rfft_batched of the windowed frames,
     crlot_istft_ola vs crlot_irfft_batched of the stepped spectra +
-    crlot_ola_gather, the masked crlot_roundtrip vs crlot_istft_ola(crlot_stft),
-    the walkers vs their staged fallbacks, and every chunking.
+    crlot_ola_gather, the per-frame masked crlot_roundtrip vs
+    crlot_istft_ola(crlot_stft), the walkers vs their staged fallbacks, every
+    chunking, and the N = 1024 frame-pair masked walk under a mask of ones vs
+    the unmasked frame-pair round trip;
+  * the frame-pair masked walk vs the per-frame one: the FFT tolerance.
 """
 import numpy as np
 import pytest
@@ -131,15 +134,21 @@ def test_istft_ola_bit_exact_vs_irfft_gather(pkg, oracle, torch_cuda, n, h):
 
 @pytest.mark.parametrize("n,h", SHAPES)
 @pytest.mark.parametrize("shared", [False, True])
-def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared):
-    """crlot_roundtrip with a per-frame mask: one walk over HBM, bit-identical to
-    crlot_istft_ola(crlot_stft(x)), and the oracle's masked e2e loop within the
-    FFT tolerance -- with NaN, Inf, tiny and huge samples in the input."""
+@pytest.mark.parametrize("pairing", [True, False])
+def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared, pairing):
+    """crlot_roundtrip with a per-frame mask: one walk over HBM -- per frame
+    (k_stft_masked) bit-identical to crlot_istft_ola(crlot_stft(x)); at N = 1024
+    with frame pairing (the default) as frame pairs (k_pair_mask) within the FFT
+    tolerance of it -- and the oracle's masked e2e loop within the FFT tolerance,
+    with NaN, Inf, tiny and huge samples in the input."""
+    if n != 1024 and not pairing:
+        pytest.skip("frame pairing only changes the N = 1024 walk")
     torch = torch_cuda
     S, T = 4, 13 * n + 31
     bins = n // 2 + 1
     x = special(oracle.synth_streams(S, T, config_id=63))
     plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_frame_pairing(pairing)
     F = plan.frame_count(T)
     rng = np.random.default_rng(7 * n + h)
     m = rng.uniform(0.0, 1.0, (F, bins) if shared else (S, F, bins)).astype(np.float32)
@@ -147,16 +156,72 @@ def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared):
     plan.set_spectral_mask(dev(torch, m))
     xd = dev(torch, x)
     y = host(plan.roundtrip(xd))
-    assert plan.last_launch()["kernels"] == ["k_stft_masked"]
+    paired = pairing and n == 1024
+    assert plan.last_launch()["kernels"] == ["k_pair_mask" if paired else "k_stft_masked"]
     y2 = host(plan.istft_ola(plan.stft(xd)))
-    assert np.array_equal(bits(y), bits(y2))
     assert np.all(np.isfinite(y))
+    if not paired:
+        assert np.array_equal(bits(y), bits(y2))
     for s in range(S):
         ms = m if shared else m[s]
         ref = oracle.roundtrip_mask(x[s], n, h, mask=ms)
         xmax, xnorm = finite_scale(x[s])
         assert_close(y[s], ref, xmax, f"{n}/{h} masked stream {s}", xnorm)
+        assert_close(y[s], y2[s], xmax, f"{n}/{h} masked vs istft(stft) stream {s}", xnorm)
     plan.set_spectral_mask(None)
+
+
+@pytest.mark.parametrize("h", [128, 256, 512])
+def test_pair_mask_walk(pkg, oracle, torch_cuda, h):
+    """K_pair_mask (N = 1024): frames 2j, 2j+1 share one transform and the step
+    separates them (c1 Z + c2 conj Z[-k]).  A mask of ones gives K_pair's own bits
+    (with and without a spectral gain, NaN / Inf / huge samples included); a
+    time-varying signed mask with zero, NaN, tiny and huge (unpaired regime)
+    values matches the oracle and the per-frame walk within the FFT tolerance;
+    the bits do not depend on the chunking; odd frame counts."""
+    torch = torch_cuda
+    n, S = 1024, 4
+    T = 29 * n + 17
+    bins = n // 2 + 1
+    x = special(oracle.synth_streams(S, T, config_id=68))
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    F = plan.frame_count(T)
+    xd = dev(torch, x)
+    gain = np.linspace(0.5, 1.5, bins).astype(np.float32)
+    ones = dev(torch, np.ones((F, bins), np.float32))
+    for g in (None, gain):
+        plan.set_spectral_gain(g)
+        plan.set_spectral_mask(None)
+        y0 = host(plan.roundtrip(xd))
+        plan.set_spectral_mask(ones)
+        y1 = host(plan.roundtrip(xd))
+        assert plan.last_launch()["kernels"] == ["k_pair_mask"]
+        assert np.array_equal(bits(y1), bits(y0)), (h, g is not None)
+    rng = np.random.default_rng(h)
+    m = rng.uniform(-1.0, 1.5, (S, F, bins)).astype(np.float32)
+    m[..., ::13] = 0.0
+    m[1, 5, 40] = np.nan
+    m[1, 20, :] = 1e-30
+    m[2, 9, 100] = 1e25
+    m[3, F - 1, 3] = 2.0 ** 21  # the last frame's (odd F: its own pair)
+    plan.set_spectral_mask(dev(torch, m))
+    y = host(plan.roundtrip(xd))
+    assert plan.last_launch()["kernels"] == ["k_pair_mask"]
+    for c in (1, 2, 5, F):
+        plan.set_chunks(c)
+        assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(y)), c
+    plan.set_chunks(0)
+    plan.set_frame_pairing(False)
+    yf = host(plan.roundtrip(xd))
+    assert plan.last_launch()["kernels"] == ["k_stft_masked"]
+    plan.set_frame_pairing(True)
+    for s in range(S):
+        ref = oracle.roundtrip_mask(x[s], n, h, bin_gain=gain, mask=m[s])
+        ymax, ynorm = finite_scale(ref)
+        assert_close(y[s], ref, ymax, f"{h} pair mask stream {s}", ynorm)
+        assert_close(y[s], yf[s], ymax, f"{h} pair vs per-frame stream {s}", ynorm)
+    plan.set_spectral_mask(None)
+    plan.set_spectral_gain(None)
 
 
 @pytest.mark.parametrize("n,h", SHAPES)
@@ -168,6 +233,7 @@ def test_masked_roundtrip_chunking_and_fallbacks(pkg, oracle, torch_cuda, n, h):
     bins = n // 2 + 1
     x = oracle.synth_streams(S, T, config_id=64)
     plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_frame_pairing(False)  # (the per-frame walk; test_pair_mask_walk covers K_pair_mask)
     F = plan.frame_count(T)
     m = np.random.default_rng(3).uniform(0.2, 1.2, (S, F, bins)).astype(np.float32)
     plan.set_spectral_mask(dev(torch, m))
@@ -240,8 +306,12 @@ def test_framequeue_pipeline_masked(pkg, oracle, torch_cuda):
     plan.set_spectral_mask(dev(torch, m))
     xd = dev(torch, x)
     y = host(plan.roundtrip(xd))
-    assert np.array_equal(bits(y), bits(host(plan.istft_ola(plan.stft(xd)))))
+    assert plan.last_launch()["kernels"] == ["k_pair_mask"]
+    plan.set_frame_pairing(False)
+    yf = host(plan.roundtrip(xd))
+    assert np.array_equal(bits(yf), bits(host(plan.istft_ola(plan.stft(xd)))))
     for s in range(S):
+        assert_close(y[s], yf[s], 0.5, f"framequeue pair vs per-frame stream {s}")
         ref = oracle.roundtrip_mask(x[s], n, h, mask=m, mode=oracle.FRAMEQUEUE, pad_mode=oracle.PAD_REFLECT,
                                     analysis_window=False)
         assert_close(y[s], ref, 0.5, f"framequeue stream {s}")
@@ -308,8 +378,12 @@ def test_full_size_stft_istft(pkg, oracle, torch_cuda):
     F = plan.frame_count(T)
     ones = torch.ones((F, n // 2 + 1), device="cuda")
     plan.set_spectral_mask(ones)
-    ym = plan.roundtrip(x)
+    ym = plan.roundtrip(x)  # frame pairs (K_pair_mask): K_pair's bits
+    assert torch.equal(ym, yr)
+    plan.set_frame_pairing(False)
+    ym = plan.roundtrip(x)  # per frame: istft(stft)'s bits
     assert torch.equal(ym, y)
+    plan.set_frame_pairing(True)
     plan.set_spectral_mask(None)
     for s in (0, 700, 1023):
         xs = host(x[s])
