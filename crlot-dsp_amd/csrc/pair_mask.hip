@@ -43,25 +43,36 @@ struct MaskWalkArgs {
 namespace {
 
 constexpr int kMW = 4;  // waves per workgroup, each walking its own chunk
+#ifndef CRLOT_PAIR_MASK_WAVES
+#define CRLOT_PAIR_MASK_WAVES 2  // waves per SIMD
+#endif
 
 // LDS: the twiddle tables (loaded into registers, then overlaid by the gain
-// table [N], symmetric) | wa4 [1024] | ws4 [1024] | per-wave transpose buffers
+// table [N], symmetric) | wa4 [1024] | ws4 [1024] | per-wave transpose buffers |
+// per-wave step coefficients (c1, c2) [513] (69.7 KB: two workgroups per CU)
 struct MaskLds {
     static constexpr size_t t1 = 0;
     static constexpr size_t t2 = t1 + sizeof(dev::pc) * 15 * 64;
     static constexpr size_t wa = t2 + sizeof(dev::pc) * 3 * 16;
     static constexpr size_t ws = wa + sizeof(float) * 1024;
     static constexpr size_t bufs = ws + sizeof(float) * 1024;
-    static constexpr size_t bytes = bufs + sizeof(dev::pc) * dev::kPairXbuf * kMW;
+    static constexpr int kCst = 514;  // per wave: (c1, c2) of the staged pair by real bin 0 .. 512
+    static constexpr size_t cst = bufs + sizeof(dev::pc) * dev::kPairXbuf * kMW;
+    static constexpr size_t bytes = cst + sizeof(dev::pc) * kCst * kMW;
 };
 static_assert(sizeof(dev::pc) * (15 * 64 + 3 * 16) >= sizeof(float) * 1024, "the gain table overlays the twiddles");
 
+// (both take the value as a scalar: a bit cast applied to an ext_vector element
+// directly is miscompiled by this clang)
+__device__ __forceinline__ float lane0(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+}
 __device__ __forceinline__ float bperm(int src_lane, float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src_lane * 4, __builtin_bit_cast(int, v)));
 }
 
 template <int SH, int NB>
-__global__ __launch_bounds__(64 * kMW, 2) void k_pair_mask(const MaskWalkArgs ma) {
+__global__ __launch_bounds__(64 * kMW, CRLOT_PAIR_MASK_WAVES) void k_pair_mask(const MaskWalkArgs ma) {
     const FusedArgs& a = ma.f;
     constexpr int E = 16, N = 1024, H = 64 * SH, P2 = N / 2;
     static_assert(NB * SH == E, "N = NB * H");
@@ -174,25 +185,52 @@ __global__ __launch_bounds__(64 * kMW, 2) void k_pair_mask(const MaskWalkArgs ma
         for (int q = 0; q < SH; ++q) acc[j][q] = 0.f;
 
     constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;
+    // The step's coefficients for a pair, staged one pair ahead: the mask rows load
+    // coalesced (real bin kr = lane + 64 i; i = 8 is bin 512, lane 0's) while the
+    // previous pair transforms, then c1 = (g ma + g mb) / 2, c2 = (g ma - g mb) / 2
+    // go to this wave's LDS rows, read back by the step in the scrambled order
+    // (in-order LDS: the writes follow the previous step's reads)
+    dev::pc* cst = reinterpret_cast<dev::pc*>(smem + MaskLds::cst) + wave * MaskLds::kCst;
+    constexpr int MI = 9;
+    float mra[MI], mrb[MI];
+    auto row_a = [&](int k) { return mrow0 + int64_t(k) * ma.mask.ld_frame; };
+    auto row_b = [&](int k) { return k + 1 < a.F ? row_a(k) + ma.mask.ld_frame : row_a(k); };  // (past F: unused)
+    auto load_rows = [&](int k) {
+        const float* ra = row_a(k);
+        const float* rb = row_b(k);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = i < 8 ? lane + 64 * i : P2;
+            mra[i] = ra[kr];
+            mrb[i] = rb[kr];
+        }
+    };
+    auto stage_rows = [&]() -> bool {  // true: every value keeps the paired regime
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = i < 8 ? lane + 64 * i : P2;
+            bad |= !(__builtin_fabsf(mra[i]) <= 0x1p20f) | !(__builtin_fabsf(mrb[i]) <= 0x1p20f);  // (NaN too)
+            const float g = gl[kr];
+            const float ga = g * mra[i], gb = g * mrb[i];
+            if (i < 8 || lane == 0) cst[kr] = dev::pc_mk(0.5f * (ga + gb), 0.5f * (ga - gb));
+        }
+        return __builtin_amdgcn_ballot_w64(bad) == 0;
+    };
+    // bin kb = pbl + 64 d: real bin kr = kb (d < 8), N - kb (d >= 8; d = 8, pbl = 0: 512 both ways)
+    const dev::pc* const cb1 = cst + pbl;
+    const dev::pc* const cb2 = cst - pbl;
+    load_rows(fs);
+    bool mok = stage_rows();
     for (int k = fs; k < f1; k += 2) {
         float nxt[2 * SH];
         load_hop(nxt, (k + NB + 1) * H - a.pad);
         load_hop(nxt + SH, (k + NB + 2) * H - a.pad);
-        // both frames' mask values at this lane's bins (frame k+1 past the last
-        // frame -- never produced -- takes frame k's row)
-        const float* ra = mrow0 + int64_t(k) * ma.mask.ld_frame;
-        const float* rb = k + 1 < a.F ? ra + ma.mask.ld_frame : ra;
-        float mva[E], mvb[E];
-        bool mbad = false;
-#pragma unroll
-        for (int d = 0; d < E; ++d) {
-            const int kb = pbl + 64 * d, kr = kb <= P2 ? kb : N - kb;
-            mva[d] = ra[kr];
-            mvb[d] = rb[kr];
-        }
-        const bool paired_hops = (hopok & kPairHops) == kPairHops;
+        const bool more = k + 2 < f1;
+        if (more) load_rows(k + 2);  // (in flight during this pair)
+        const bool paired = mok && (hopok & kPairHops) == kPairHops;
         dev::pc v[E];
-        if (paired_hops) {
+        if (paired) {
 #pragma unroll
             for (int m4 = 0; m4 < E / 4; ++m4) {
                 const float4 w = *reinterpret_cast<const float4*>(wa4 + m4 * 256 + lane * 4);
@@ -204,28 +242,28 @@ __global__ __launch_bounds__(64 * kMW, 2) void k_pair_mask(const MaskWalkArgs ma
                 }
             }
             dev::pair_fft_fwd(v, buf, tw, tw, lane);
+            // the step, Z' = c1 Z + c2 conj Z[-k], registers d and 15 - d together so
+            // both update in place; lane 0's partners are its own registers
+            // (16 - d) mod 16, read into SGPRs before any update
+            float own_r[E], own_i[E];
 #pragma unroll
             for (int d = 0; d < E; ++d) {
-                const float ta = __builtin_fabsf(mva[d]), tb = __builtin_fabsf(mvb[d]);
-                mbad |= !(ta <= 0x1p20f) | !(tb <= 0x1p20f);  // (NaN fails the test)
-            }
-        }
-        const bool paired = paired_hops && __builtin_amdgcn_ballot_w64(mbad) == 0;
-        if (paired) {
-            // the step: Z' = c1 Z + c2 conj Z[-k]
-            dev::pc zp[E];
-#pragma unroll
-            for (int d = 0; d < E; ++d) {
-                const float pr = bperm(partner, v[15 - d].x), pi = bperm(partner, v[15 - d].y);
-                const dev::pc own = v[(16 - d) & 15];
-                zp[d] = lane == 0 ? own : dev::pc_mk(pr, pi);
+                const float re = v[(16 - d) & 15].x, im = v[(16 - d) & 15].y;
+                own_r[d] = lane0(re);
+                own_i[d] = lane0(im);
             }
 #pragma unroll
-            for (int d = 0; d < E; ++d) {
-                const float g = gl[pbl + 64 * d];
-                const float ga = g * mva[d], gb = g * mvb[d];
-                const float c1 = 0.5f * (ga + gb), c2 = 0.5f * (ga - gb);
-                v[d] = dev::pc_mk(__builtin_fmaf(c2, zp[d].x, c1 * v[d].x), __builtin_fmaf(-c2, zp[d].y, c1 * v[d].y));
+            for (int d = 0; d < E / 2; ++d) {
+                const int e = 15 - d;
+                dev::pc zd = dev::pc_mk(bperm(partner, v[e].x), bperm(partner, v[e].y));
+                dev::pc ze = dev::pc_mk(bperm(partner, v[d].x), bperm(partner, v[d].y));
+                if (lane == 0) {
+                    zd = dev::pc_mk(own_r[d], own_i[d]);
+                    ze = dev::pc_mk(own_r[e], own_i[e]);
+                }
+                const dev::pc cd = cb1[64 * d], ce = cb2[N - 64 * e];
+                v[d] = dev::pc_mk(__builtin_fmaf(cd.y, zd.x, cd.x * v[d].x), __builtin_fmaf(-cd.y, zd.y, cd.x * v[d].y));
+                v[e] = dev::pc_mk(__builtin_fmaf(ce.y, ze.x, ce.x * v[e].x), __builtin_fmaf(-ce.y, ze.y, ce.x * v[e].y));
             }
             dev::pair_fft_inv(v, buf, tw, tw, lane);
             float dr0[2 * SH], dr1[2 * SH];
@@ -237,7 +275,7 @@ __global__ __launch_bounds__(64 * kMW, 2) void k_pair_mask(const MaskWalkArgs ma
                 accumulate(v, true, true);
                 emit(k + 1, dr1);
             }
-        } else {  // each frame alone, full sanitize, its own gain g m
+        } else {  // each frame alone, full sanitize, its own gain g m (rows read again)
             const int npass = min(2, f1 - k);
             for (int p = 0; p < npass; ++p) {
 #pragma unroll
@@ -251,8 +289,12 @@ __global__ __launch_bounds__(64 * kMW, 2) void k_pair_mask(const MaskWalkArgs ma
                     }
                 }
                 dev::pair_fft_fwd(v, buf, tw, tw, lane);
+                const float* r = p ? row_b(k) : row_a(k);
 #pragma unroll
-                for (int d = 0; d < E; ++d) v[d] = v[d] * (gl[pbl + 64 * d] * (p ? mvb[d] : mva[d]));
+                for (int d = 0; d < E; ++d) {
+                    const int kb = pbl + 64 * d, kr = kb <= P2 ? kb : N - kb;
+                    v[d] = v[d] * (gl[kb] * r[kr]);
+                }
                 dev::pair_fft_inv(v, buf, tw, tw, lane);
                 float dr[2 * SH];
                 load_den<SH>(dr, rp, lane, (k + p) % a.ring_blocks);
@@ -260,6 +302,7 @@ __global__ __launch_bounds__(64 * kMW, 2) void k_pair_mask(const MaskWalkArgs ma
                 emit(k + p, dr);
             }
         }
+        if (more) mok = stage_rows();
         hopok = (hopok | hop_ok<SH>(nxt, xlo, xhi) << (NB + 1) | hop_ok<SH>(nxt + SH, xlo, xhi) << (NB + 2)) >> 2;
 #pragma unroll
         for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];

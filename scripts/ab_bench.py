@@ -44,6 +44,13 @@ for path in libs:
         gain = (0.5 + 0.5 * torch.cos(torch.linspace(0, 3.14159, N // 2 + 1))).float().numpy()
         L.crlot_plan_set_spectral_gain.argtypes = [C.c_void_p, C.c_void_p]
         assert L.crlot_plan_set_spectral_gain(h, gain.ctypes.data) == 0
+    if os.environ.get("AB_MASK") in ("1", "2"):  # a per-frame spectral mask: 1 shared, 2 per stream
+        shape = (F, N // 2 + 1) if os.environ["AB_MASK"] == "1" else (S, F, N // 2 + 1)
+        mk = torch.rand(shape, generator=torch.Generator(device="cuda").manual_seed(4), device="cuda")
+        L.crlot_plan_set_spectral_mask.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64]
+        assert L.crlot_plan_set_spectral_mask(h, mk.data_ptr(), N // 2 + 1,
+                                              0 if mk.dim() == 2 else F * (N // 2 + 1)) == 0
+        ys[path + "#mask"] = mk  # (kept alive)
     handles[path], plans[path] = L, h
     ys[path] = torch.empty((S, F * H), device="cuda")
 

@@ -741,11 +741,12 @@ def test_fft_plan_domains(pkg, oracle, torch_cuda):
 
 
 # ------------------------------------------------------------------ size-independent properties
-def test_full_size_properties(pkg, oracle, torch_cuda):
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024)])  # the headline; config 3 (K_pair4k)
+def test_full_size_properties(pkg, oracle, torch_cuda, n, h):
     """At BASELINE scale (1024 streams x 480000, 2 GB in + 2 GB out): determinism,
     stream independence, exact power-of-two linearity, sampled oracle parity."""
     torch = torch_cuda
-    n, h, S, T = 1024, 256, 1024, 480_000
+    S, T = 1024, 480_000
     g = torch.Generator(device="cuda").manual_seed(1234)
     x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
     plan = pkg.Plan(frame_size=n, hop_size=h)
