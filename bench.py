@@ -566,6 +566,21 @@ def _cpu_gain_loop_us(O, native, x, n, h, reps=5):
     return ts[len(ts) // 2] * 1e6, F
 
 
+def _cpu_harness_order_us(O, native, x, n, h, reps=5):
+    """Median microseconds of the oracle's loop in e2e_benchmark.cc:152-179's
+    literal order (every push, then the produce loop), one thread."""
+    L = O.lib(native)
+    T = x.size
+    y = np.zeros(T, np.float32)
+    ts = []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        L.or_roundtrip_harness_order(x, T, n, h, O.HANN, 0, y, T)
+        ts.append(time.perf_counter() - t0)
+    ts = sorted(ts[1:])
+    return ts[len(ts) // 2] * 1e6
+
+
 def suite_e2e(pkg, torch, dev):
     """bench/e2e_benchmark.cc counterpart: the per-frame drop-in loop through the
     C++ classes (harness/e2e_bench: Framer -> window -> IFftPlan::forward ->
@@ -584,6 +599,10 @@ def suite_e2e(pkg, torch, dev):
         cpu_us, F = _cpu_loop_us(O, native, x, n, h)
         g["cpu_oracle_1thread"] = {"ms_per_iteration": round(cpu_us / 1e3, 4), "us_per_frame": round(cpu_us / F, 3),
                                    "x_realtime": round(1e6 / cpu_us, 1)}
+        hus = _cpu_harness_order_us(O, native, x, n, h)
+        g["harness_order"]["cpu_oracle_1thread"] = {"ms_per_iteration": round(hus / 1e3, 4),
+                                                    "us_per_frame": round(hus / F, 3),
+                                                    "order": "every push, then the produce loop"}
         gus, _ = _cpu_gain_loop_us(O, native, x, n, h)
         g["spectral_gain"]["cpu_oracle_1thread"] = {"ms_per_iteration": round(gus / 1e3, 4),
                                                     "us_per_frame": round(gus / F, 3)}

@@ -229,7 +229,9 @@ int main(int argc, char** argv) {
         const SpecRun mask_run = spectral_loop(masks);
 
         // the harness's literal order: every push, then the produce loop (ring aliasing, Q3)
-        std::vector<double> ho_us;
+        std::vector<double> ho_us, ho_frames_us, ho_produce_us;
+        int64_t st0[11] = {0}, st1[11] = {0};
+        (void)crlot_call_speculation_stats_ex(st0, 11);
         for (int it = 0; it < std::max(iters / 4, 10); ++it) {
             auto t0 = clk::now();
             p.framer.push(x.data(), T);
@@ -241,6 +243,7 @@ int main(int argc, char** argv) {
                 p.ola->push_frame_AoS(processed.data(), nullptr, k * H, 0, N, 1.0f);
                 ++k;
             }
+            const auto t1 = clk::now();
             size_t got = 0;
             float* ch_out[1] = {output.data()};
             while (got < T) {
@@ -250,10 +253,13 @@ int main(int argc, char** argv) {
                 got += s;
             }
             ho_us.push_back(us_since(t0));  // the reset below re-arms the objects, untimed
+            ho_frames_us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+            ho_produce_us.push_back(us_since(t1));
             p.ola->reset();
             p.ola->set_window(p.window, int(N));
             p.framer.reset();
         }
+        (void)crlot_call_speculation_stats_ex(st1, 11);
 
         // FFT1024Performance (:187-205): forward alone
         std::vector<double> f_us;
@@ -270,7 +276,10 @@ int main(int argc, char** argv) {
             "\"samples\": %zu, \"frames_per_iteration\": %zu, \"iterations\": %d, "
             "\"full_pipeline\": {\"order\": \"streaming-interleaved\", \"ms_p50\": %.4f, \"x_realtime\": %.2f, "
             "\"reference_reporter_value\": %.1f, \"us_per_frame\": %.3f, \"msamples_s\": %.3f}, "
-            "\"harness_order\": {\"ms_p50\": %.4f, \"x_realtime\": %.2f, \"us_per_frame\": %.3f}, "
+            "\"harness_order\": {\"ms_p50\": %.4f, \"x_realtime\": %.2f, \"us_per_frame\": %.3f, "
+            "\"frames_loop_us_p50\": %.1f, \"produce_loop_us_p50\": %.1f, \"speculation_delta\": "
+            "{\"starts\": %lld, \"forwards\": %lld, \"inverses\": %lld, \"pushes\": %lld, \"produces\": %lld, "
+            "\"rebuilds\": %lld, \"windows\": %lld, \"declined\": %lld}}, "
             "\"per_call_us_p50\": {\"pop_window\": %.3f, \"forward\": %.3f, \"inverse\": %.3f, \"push_frame_AoS\": "
             "%.3f, \"produce\": %.3f}, "
             "\"forward_us_p10_p90\": [%.3f, %.3f], \"inverse_us_p10_p90\": [%.3f, %.3f], "
@@ -285,7 +294,10 @@ int main(int argc, char** argv) {
             // 1 s of audio per iteration: x real-time = 1 s / iteration time; the
             // reference's reporter prints (48000 / ms) * 1000 under that name (:311-317)
             N, H, T, frames, iters, it_p50 / 1e3, 1e6 / it_p50, 48000.0 / (it_p50 / 1e3) * 1000.0,
-            it_p50 / double(frames), double(T) / it_p50, ho_p50 / 1e3, 1e6 / ho_p50, ho_p50 / double(frames), p50(t_pop),
+            it_p50 / double(frames), double(T) / it_p50, ho_p50 / 1e3, 1e6 / ho_p50, ho_p50 / double(frames),
+            p50(ho_frames_us), p50(ho_produce_us), (long long)(st1[0] - st0[0]), (long long)(st1[1] - st0[1]),
+            (long long)(st1[2] - st0[2]), (long long)(st1[3] - st0[3]), (long long)(st1[4] - st0[4]),
+            (long long)(st1[5] - st0[5]), (long long)(st1[7] - st0[7]), (long long)(st1[8] - st0[8]), p50(t_pop),
             p50(t_fwd), p50(t_inv), p50(t_push), p50(t_prod), pct(t_fwd, 0.1), pct(t_fwd, 0.9), pct(t_inv, 0.1),
             pct(t_inv, 0.9), p50(f_us), p50(gain_run.it) / 1e3, p50(gain_run.it) / double(frames), p50(gain_run.fwd),
             p50(gain_run.inv), p50(gain_run.push), p50(gain_run.prod), p50(mask_run.it) / 1e3,

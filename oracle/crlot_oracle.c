@@ -997,6 +997,57 @@ static long or_roundtrip_impl(const float* x, size_t T, size_t n, size_t h, int 
     return (long)k;
 }
 
+/* bench/e2e_benchmark.cc:152-179 in its literal order: every frame pushed
+ * (pop -> window -> forward -> inverse -> push_frame_AoS(k H)), THEN the produce
+ * loop asking for what is left of T each call -- the ring aliases when the
+ * signal outruns the ring, as the reference's does.  Returns the
+ * samples produced (at most y_cap are stored). */
+long or_roundtrip_harness_order(const float* x, size_t T, size_t n, size_t h, int wtype, int periodic, float* y,
+                                size_t y_cap) {
+    if (n == 0 || h == 0 || (n & 1)) return -1;
+    float* w = (float*)malloc(sizeof(float) * n);
+    if (or_window(wtype, n, periodic, OR_NORM_NONE, w) != 0) {
+        free(w);
+        return -2;
+    }
+    or_framer* fr = or_framer_new(n, h, 1, OR_ZERO_PAD);
+    or_framer_push(fr, x, T);
+    or_ola* ola = or_ola_new(n, h, 1, 1e-8f, 1);
+    or_ola_set_window(ola, w);
+    or_kfftr_cfg* fwd = or_kfftr_alloc((int)n, 0);
+    or_kfftr_cfg* inv = or_kfftr_alloc((int)n, 1);
+    float* frame = (float*)malloc(sizeof(float) * n);
+    float* proc = (float*)malloc(sizeof(float) * n);
+    float* spec = (float*)malloc(sizeof(float) * (n + 2));
+    size_t k = 0;
+    while (or_framer_pop(fr, frame)) {
+        for (size_t i = 0; i < n; ++i) proc[i] = frame[i] * w[i];
+        or_adapter_forward(fwd, (int)n, proc, spec);
+        or_adapter_inverse(inv, (int)n, spec, proc);
+        or_ola_push_frame_aos(ola, proc, NULL, k * h, 0, n, 1.0f);
+        ++k;
+    }
+    size_t got = 0;
+    float* tmp = (float*)calloc(T + 1, sizeof(float)); /* (a clamped read leaves its tail as it was) */
+    while (got < T) {
+        float* chp[1] = {tmp};
+        const size_t s = or_ola_produce(ola, chp, T - got);
+        if (s == 0) break;
+        if (got < y_cap) memcpy(y + got, tmp, sizeof(float) * (y_cap - got < s ? y_cap - got : s));
+        got += s;
+    }
+    free(tmp);
+    free(frame);
+    free(proc);
+    free(spec);
+    free(w);
+    or_kfftr_free(fwd);
+    or_kfftr_free(inv);
+    or_ola_free(ola);
+    or_framer_free(fr);
+    return (long)got;
+}
+
 typedef struct {
     const float* x;
     float* y;

@@ -149,6 +149,9 @@ long or_roundtrip_gain(const float* x, size_t T, size_t n, size_t h, int window_
                        const float* bin_gain, float* y, size_t y_cap);
 /* the loop with bin_gain then mask row k scaling frame k's spectrum; raw_spec_out:
  * the forward spectra before the step (rows of n + 2 floats) */
+/* e2e_benchmark.cc:152-179's literal order: every push, then the produce loop (ring aliasing) */
+long or_roundtrip_harness_order(const float* x, size_t T, size_t n, size_t h, int window_type, int periodic,
+                                float* y, size_t y_cap);
 long or_roundtrip_mask(const float* x, size_t T, size_t n, size_t h, int window_type, int periodic, int framing,
                        int center, int pad_mode, int analysis_window, const float* bin_gain, const float* mask,
                        size_t mask_ld, float* y, size_t y_cap, float* raw_spec_out);

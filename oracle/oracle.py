@@ -123,6 +123,8 @@ def lib(native: bool = False):
     L.or_roundtrip_mask.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                     C.c_void_p, C.c_void_p, sz, _f32p, sz, C.c_void_p]
     L.or_roundtrip_mask.restype = C.c_long
+    L.or_roundtrip_harness_order.argtypes = [_f32p, sz, sz, sz, C.c_int, C.c_int, _f32p, sz]
+    L.or_roundtrip_harness_order.restype = C.c_long
     L.or_roundtrip_batch_ex.argtypes = [_f32p, sz, sz, sz, sz, sz, C.c_int, C.c_int, C.c_int,
                                         C.c_int, C.c_int, C.c_int, _f32p, sz, C.c_int]
     L.or_roundtrip_batch_ex.restype = C.c_long
@@ -498,6 +500,18 @@ def roundtrip_mask(x, n, h, bin_gain=None, mask=None, mode=ZERO_PAD, center=True
         raise ValueError(f"or_roundtrip_mask rc={r}")
     assert r == F, (r, F)
     return (y[:F * h], spec[:F]) if want_spec else y[:F * h]
+
+
+def roundtrip_harness_order(x, n, h, wtype=HANN, periodic=False):
+    """or_roundtrip_harness_order: e2e_benchmark.cc:152-179 in its literal order
+    (every push, then the produce loop); returns the samples produced."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.zeros(max(x.size, 1), np.float32)
+    r = lib().or_roundtrip_harness_order(x if x.size else np.zeros(1, np.float32), x.size, n, h, wtype,
+                                         int(periodic), y, x.size)
+    if r < 0:
+        raise ValueError(f"or_roundtrip_harness_order rc={r}")
+    return y[:r]
 
 
 def roundtrip_batch_ex(x2d, n, h, mode=ZERO_PAD, center=True, pad_mode=PAD_CONSTANT,

@@ -422,3 +422,32 @@ def test_oracle_spectral_step_reduces_to_pinned_loops(oracle, n, h, mode):
         yg = oracle.roundtrip_gain(x, n, h, g)
         assert np.array_equal(bits(yg), bits(oracle.roundtrip_mask(x, n, h, bin_gain=g)))
         assert np.array_equal(bits(yg), bits(oracle.roundtrip_mask(x, n, h, mask=np.tile(g, (F, 1)))))
+
+
+def test_oracle_harness_order_loop_replays_the_objects(oracle):
+    """or_roundtrip_harness_order (bench.py's CPU leg for e2e_benchmark.cc:152-179's
+    literal order) equals the oracle's Framer / kissfft adapter / OLAAccumulator
+    objects driven call by call in that order: every push, then produce(T - got)
+    until it returns 0 -- ring aliasing and the clamped first read included."""
+    n, h = 1024, 256
+    x = oracle.synth(12_000, 5)
+    T = x.size
+    y = oracle.roundtrip_harness_order(x, n, h)
+    w = oracle.window(oracle.HANN, n)
+    fr, _ = oracle.framer_run(x, T, 1, n, h, oracle.ZERO_PAD)
+    kr = oracle.KissR(n)
+    ola = oracle.Ola(n, h, 1, eps=1e-8, inside=True)
+    ola.set_window(w)
+    for k, f in enumerate(fr.reshape(-1, n)):
+        ola.push_frame_aos(kr.inverse(kr.forward(f * w)), k * h, 0, n, 1.0)
+    out = np.zeros(T, np.float32)
+    got = 0
+    while got < T:
+        buf = np.zeros(T - got, np.float32)
+        s = ola.produce_into(T - got, [buf])
+        if s == 0:
+            break
+        out[got:got + s] = buf[:s]
+        got += s
+    assert y.size == got
+    assert np.array_equal(y.view(np.uint32), out[:got].view(np.uint32))
