@@ -124,7 +124,7 @@ class StftEngine {
         bool center = true;                  // boundary_mode == CRLOT_FRAMEQUEUE
         int pad_mode = CRLOT_PAD_CONSTANT;   // (dsp::FrameQueue defaults)
     };
-    explicit StftEngine(const Config& c) : plan_(desc(c)) {}
+    explicit StftEngine(const Config& c) : plan_(desc(c)), n_(c.frame_size) {}
     int64_t frame_count(int64_t T) const { return crlot_frame_count(plan_.get(), T); }
     int64_t output_length(int64_t T) const { return crlot_output_length(plan_.get(), T); }
     // d_x [n_streams][ld_x], d_y [n_streams][ld_y] device pointers
@@ -159,6 +159,26 @@ class StftEngine {
     void set_frame_pairing(bool enable) {
         check(crlot_plan_set_frame_pairing(plan_.get(), enable ? 1 : 0), "set_frame_pairing");
     }
+    // The round trip split at its spectral step (e2e_benchmark.cc:160-162).
+    // Spectra: complex64 rows of frame_size/2 + 1 bins, frame k of stream s at
+    // d_spec + s*ld_spec + k*ld_frame floats (ld_frame >= frame_size + 2, even).
+    int64_t bins() const { return n_ / 2 + 1; }
+    void stft_device(const float* d_x, float* d_spec, int n_streams, int64_t T, int64_t ld_x, int64_t ld_spec,
+                     int64_t ld_frame, hipStream_t s = nullptr) {
+        check(crlot_stft(plan_.get(), d_x, d_spec, n_streams, T, ld_x, ld_spec, ld_frame, s), "crlot_stft");
+    }
+    // spectra (F frames per stream) -> gain / mask step -> irfft -> OLA -> y [F * hop]
+    void istft_ola_device(const float* d_spec, float* d_y, int n_streams, int64_t F, int64_t ld_spec,
+                          int64_t ld_frame, int64_t ld_y, hipStream_t s = nullptr) {
+        check(crlot_istft_ola(plan_.get(), d_spec, d_y, n_streams, F, ld_spec, ld_frame, ld_y, s),
+              "crlot_istft_ola");
+    }
+    // per-frame real mask rows of bins(): frame k of stream s at d_mask + s*ld_stream + k*ld_frame
+    // (ld_stream 0: one mask shared by the streams); nullptr clears it
+    void set_spectral_mask(const float* d_mask_or_null, int64_t ld_frame = 0, int64_t ld_stream = 0) {
+        check(crlot_plan_set_spectral_mask(plan_.get(), d_mask_or_null, ld_frame ? ld_frame : bins(), ld_stream),
+              "set_spectral_mask");
+    }
     crlot_plan* plan() const { return plan_.get(); }
 
    private:
@@ -179,6 +199,7 @@ class StftEngine {
         return d;
     }
     Plan plan_;
+    int n_;
     DeviceBuffer<float> dx_, dy_;
 };
 

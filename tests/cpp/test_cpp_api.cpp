@@ -252,6 +252,33 @@ int main() {
             }
             EXPECT(std::sqrt(num / den) < 1e-6 && mx < 2e-6, "stream %d rel %g max %g", s, std::sqrt(num / den), mx);
         }
+        // the split round trip (stft_device -> istft_ola_device) and a per-frame mask
+        // through the same engine: within the FFT tolerance of the round trip, and
+        // the masked round trip of the oracle's masked loop
+        const int64_t F = eng.frame_count(T), B = eng.bins(), R = 1024 + 2;
+        crlot::DeviceBuffer<float> dx(S * T), dy(S * L), dspec(S * F * R), dmask(F * B);
+        crlot::hip_check(hipMemcpy(dx.get(), x.data(), sizeof(float) * S * T, hipMemcpyHostToDevice), "up");
+        eng.stft_device(dx.get(), dspec.get(), S, T, T, F * R, R);
+        eng.istft_ola_device(dspec.get(), dy.get(), S, F, F * R, R, L);
+        std::vector<float> y2(S * L), mask(F * B), ym(L);
+        crlot::hip_check(hipMemcpy(y2.data(), dy.get(), sizeof(float) * S * L, hipMemcpyDeviceToHost), "down");
+        double mx2 = 0;
+        for (int64_t i = 0; i < S * L; ++i) mx2 = std::fmax(mx2, std::fabs(double(y2[i]) - y[i]));
+        EXPECT(mx2 < 2e-6, "istft_ola(stft) vs roundtrip max %g", mx2);
+        for (int64_t k = 0; k < F; ++k)
+            for (int64_t b = 0; b < B; ++b) mask[k * B + b] = float(0.5 + 0.5 * std::cos(0.01 * double(b) + 0.3 * double(k)));
+        crlot::hip_check(hipMemcpy(dmask.get(), mask.data(), sizeof(float) * F * B, hipMemcpyHostToDevice), "up");
+        eng.set_spectral_mask(dmask.get());
+        eng.roundtrip_device(dx.get(), dy.get(), S, T, T, L);
+        eng.set_spectral_mask(nullptr);
+        crlot::hip_check(hipMemcpy(y2.data(), dy.get(), sizeof(float) * S * L, hipMemcpyDeviceToHost), "down");
+        for (int s = 0; s < S; ++s) {
+            or_roundtrip_mask(x.data() + s * T, T, 1024, 256, OR_HANN, 0, OR_ZERO_PAD, 1, 0, 1, nullptr, mask.data(),
+                              size_t(B), ym.data(), L, nullptr);
+            double mxm = 0;
+            for (int64_t i = 0; i < L; ++i) mxm = std::fmax(mxm, std::fabs(double(y2[s * L + i]) - ym[i]));
+            EXPECT(mxm < 2e-6, "masked stream %d max %g", s, mxm);
+        }
     }
     // io::WavReader / WavWriter (wav_io_test.cc WriteAndRead) + the oboe fixture
     {
