@@ -233,6 +233,13 @@ def valu_block(fps, achieved_tf, issue, kern_ms, pairs_per_simd=None):
         v["issue_model"] = isa_issue_model(pairs_per_simd, (issue or {}).get("kernel_cycles"))
     if issue:
         v["active_inst_frac_pmc"] = None if issue.get("busy_frac") is None else round(issue["busy_frac"], 4)
+        if issue.get("kernel_cycles"):
+            # GRBM_GUI_ACTIVE / 8 over the profile's average kernel duration, and the same
+            # cycles over this run's kernel time (cycles, not time, are what the
+            # instruction trims move; the clock is power-capped)
+            v["clock_ghz"] = None if issue.get("clock_ghz") is None else round(issue["clock_ghz"], 3)
+            v["clock_ghz_this_run"] = round(issue["kernel_cycles"] / (kern_ms * 1e6), 3)
+            v["kernel_cycles_pmc"] = round(issue["kernel_cycles"])
         if issue.get("fp32_flops_per_launch"):
             tf = issue["fp32_flops_per_launch"] / (kern_ms * 1e-3) / 1e12
             v["counted_fp32_tflops"] = round(tf, 2)

@@ -590,6 +590,10 @@ int batch_forward(SharedServer* sh, crlot_plan* inner, int64_t n, const float* i
     b->ola = nullptr;
     b->sgain_from = 0;  // (a gain learned earlier is applied from the start: the likeliest caller)
     b->learn_after = -1;
+    // a different gain at a new signal's first frames is a new caller's gain, not a
+    // per-frame edit: it is learned at once (churn is judged within a signal)
+    b->gain_served = kGainMinRun;
+    b->learn_backoff = 16;
     if (!b->sgain.empty()) {
         const size_t bins = size_t(n) / 2 + 1;
         hipError_t ge = b->sgain.size() == bins ? dgrow(&b->d_sgain, &b->c_sgain, bins) : hipErrorInvalidValue;

@@ -2162,8 +2162,18 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
     a.out_len = int(out_len);
     a.n_streams = n_streams;
     a.F = int(F);
-    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, fused_resident_waves() / 16 * fk::pair_mask_walkers_per_cu(),
-                         a.n_chunks, a.M);
+    const int resident = fused_resident_waves() / 16 * fk::pair_mask_walkers_per_cu();
+    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.n_chunks, a.M);
+    // a batch below one resident round (one window of a few streams: the per-call
+    // latency case) walks chunks of >= 16 frames instead, as many as fit the round
+    const int64_t S = std::max(1, n_streams);
+    if (S * a.n_chunks < resident) {
+        const int64_t n = std::min<int64_t>(F / 16, (resident + S - 1) / S);
+        if (n > a.n_chunks) {
+            a.M = int((F + n - 1) / n);
+            a.n_chunks = int((F + a.M - 1) / a.M);
+        }
+    }
     chunk_override(F, a);
     note_chunks(a.n_chunks);
     a.ring_blocks = g.ring_len / g.h;

@@ -147,5 +147,10 @@ out = {
     "aux_kernels": aux,
     "note": __doc__.strip(),
 }
+# the clock the kernel ran at: its cycles (GRBM_GUI_ACTIVE / 8, PMC pass) over its
+# average duration in the trace pass of the same lease (the cycle count barely
+# moves with the clock: DESIGN.md section 5)
+if out["valu_issue"] and dur:
+    out["valu_issue"]["clock_ghz"] = out["valu_issue"]["kernel_cycles"] / dur
 json.dump(out, open(f"profiles/{tag}_pmc_summary.json", "w"), indent=1)
 print(json.dumps({k: v for k, v in out.items() if k not in ("note", "pmc_per_launch")}, indent=1))
