@@ -1035,6 +1035,12 @@ int stft_impl(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams,
               int64_t ld_spec, int64_t ld_frame, float* work, hipStream_t s) {
     const crlot::DevTables t = tables(p);
     hipError_t e;
+    const int64_t lim = int64_t(1) << 29;
+    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && t.ptw && t.wa && aligned4(d_x) && T < lim) {
+        // N = 1024 frame pairs (pairing off: K_stft, bit-identical to crlot_rfft_batched)
+        e = crlot::launch_pair_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft (frame pairs) kernel launch");
+    }
     if (!p->generic && crlot::stft_supported(p->geo.n)) {
         e = crlot::launch_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft kernel launch");
@@ -1063,6 +1069,12 @@ int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams
                int64_t ld_frame, int64_t ld_y, float* specw, float* frames, hipStream_t s) {
     const crlot::DevTables t = tables(p);
     hipError_t e;
+    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && t.ptw && t.pden && t.wsn && t.rden &&
+        p->geo.ring_len % p->geo.h == 0 && aligned4(d_y) && F * p->geo.h + 2 * p->geo.n < (int64_t(1) << 29)) {
+        // N = 1024 frame pairs (pairing off: K_istft, bit-identical to irfft + gather)
+        e = crlot::launch_pair_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft (frame pairs) kernel launch");
+    }
     if (istft_walk_ok(p, d_y, ld_y)) {
         e = crlot::launch_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft kernel launch");

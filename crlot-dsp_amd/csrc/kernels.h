@@ -387,6 +387,13 @@ hipError_t launch_roundtrip_masked(const Geometry& g, const DevTables& t, const 
 // ... as frame pairs (K_pair_mask, pair_mask.hip: N = 1024, H = 128 / 256 / 512, the
 // pair tables; equal to the per-frame walk within float32 rounding)
 bool pair_mask_supported(int n, int h);
+// crlot_stft / crlot_istft_ola as frame pairs (K_pair_stft / K_pair_istft, pair_stft.hip:
+// N = 1024, H = 128 / 256 / 512, the pair tables; within float32 rounding of the per-frame kernels)
+hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
+                            int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame, hipStream_t s);
+hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
+                             int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
+                             hipStream_t s);
 hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
                               int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
                               hipStream_t s);

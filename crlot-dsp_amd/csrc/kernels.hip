@@ -2184,6 +2184,72 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
     return fk::launch_pair_mask(g.h, a, m, int64_t(n_streams) * a.n_chunks, stream);
 }
 
+// K_pair_stft: chunks of an even number of frames (pairs start on even frames), about
+// 128 per walk, at least two resident rounds of walks (no warm-up frames to amortise)
+hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
+                            int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
+                            hipStream_t stream) {
+    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.wa) return hipErrorInvalidValue;
+    fk::PairSpecArgs a{};
+    a.f.t = t;
+    a.f.x = x;
+    a.f.ld_x = ld_x;
+    a.f.T = int(T);
+    a.f.n_streams = n_streams;
+    a.f.F = int(F);
+    a.f.pad = g.pad;
+    a.f.pad_mode = g.pad_mode;
+    a.spec = spec;
+    a.ld_spec = ld_spec;
+    a.ld_frame = ld_frame;
+    const int64_t S = std::max(1, n_streams), resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu();
+    int64_t n = std::max<int64_t>((F + 127) / 128, (2 * resident + S - 1) / S);
+    n = std::max<int64_t>(1, std::min<int64_t>(n, (F + 15) / 16));
+    if (const int64_t c = chunks_or(0, F); c > 0) n = std::min(c, F);
+    int64_t m = (F + n - 1) / n;
+    m += m & 1;
+    a.f.M = int(m);
+    a.f.n_chunks = int((F + m - 1) / m);
+    note_chunks(a.f.n_chunks);
+    return fk::launch_pair_stft(g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
+}
+
+// K_pair_istft: K_pair_mask's chunking (whole resident rounds; small batches in >= 16-frame chunks)
+hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
+                             int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
+                             hipStream_t stream) {
+    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.pden || !t.wsn || !t.rden ||
+        g.ring_len % g.h != 0)
+        return hipErrorInvalidValue;
+    fk::PairSpecArgs a{};
+    a.f.t = t;
+    a.f.y = y;
+    a.f.ld_y = ld_y;
+    a.f.out_len = int(F * g.h);
+    a.f.n_streams = n_streams;
+    a.f.F = int(F);
+    a.f.ring_blocks = g.ring_len / g.h;
+    a.f.inv_n = g.inv_n;
+    a.f.gain = g.gain;
+    a.sin = spec;
+    a.ld_spec = ld_spec;
+    a.ld_frame = ld_frame;
+    a.mask = m;
+    const int resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu();
+    choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.f.n_chunks, a.f.M);
+    const int64_t S = std::max(1, n_streams);
+    if (S * a.f.n_chunks < resident) {
+        const int64_t n = std::min<int64_t>(F / 16, (resident + S - 1) / S);
+        if (n > a.f.n_chunks) {
+            a.f.M = int((F + n - 1) / n);
+            a.f.n_chunks = int((F + a.f.M - 1) / a.f.M);
+        }
+    }
+    chunk_override(F, a.f);
+    note_chunks(a.f.n_chunks);
+    return fk::launch_pair_istft(g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
+}
+
 std::vector<float> build_pair512_twiddles() {
     std::vector<float> t;
     for (int k1 = 1; k1 < 8; ++k1)

@@ -68,6 +68,8 @@ extern "C" const char* crlot_kernel_name(int32_t id) {
         case CRLOT_K_SPEC_STEP: return "k_spec_step";
         case CRLOT_K_FRAMES_W: return "k_frames_w";
         case CRLOT_K_PAIR_MASK: return "k_pair_mask";
+        case CRLOT_K_PAIR_STFT: return "k_pair_stft";
+        case CRLOT_K_PAIR_ISTFT: return "k_pair_istft";
         case CRLOT_K_EXPERIMENT: return "k_experiment";
         default: return "unknown";
     }

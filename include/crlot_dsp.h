@@ -226,6 +226,8 @@ int crlot_test_inject(int32_t what, int32_t count);
 #define CRLOT_K_SPEC_STEP 27     /* staged spectral step (gain, mask) over spectra in HBM */
 #define CRLOT_K_FRAMES_W 28      /* staged windowed frames (mixed-radix stft) */
 #define CRLOT_K_PAIR_MASK 29     /* N = 1024 frame-pair walk with the per-frame mask */
+#define CRLOT_K_PAIR_STFT 30     /* crlot_stft as frame pairs (N = 1024) */
+#define CRLOT_K_PAIR_ISTFT 31    /* crlot_istft_ola as frame pairs (N = 1024) */
 #define CRLOT_K_EXPERIMENT 99    /* experiment builds only */
 typedef struct crlot_launch_info {
     int32_t n_kernels;

@@ -93,18 +93,27 @@ def test_stft_vs_oracle_and_rfft(pkg, oracle, torch_cuda, n, h, mode):
     kw = dict(center=True, pad_mode=pkg.PAD_REFLECT) if mode == 2 else {}
     plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode, **kw)
     xd = dev(torch, x)
+    paired = n == 1024 and h in (128, 256, 512)  # K_pair_stft (frame pairing on, the default)
     spec = host(plan.stft(xd))
-    assert plan.last_launch()["kernels"] == ["k_stft"]
+    assert plan.last_launch()["kernels"] == ["k_pair_stft" if paired else "k_stft"]
+    if paired:  # ... and the per-frame kernel beside it, the one the bit-exact check below holds for
+        plan.set_frame_pairing(False)
+        spec_pf = host(plan.stft(xd))
+        assert plan.last_launch()["kernels"] == ["k_stft"]
+        plan.set_frame_pairing(True)
+    else:
+        spec_pf = spec
     F = plan.frame_count(T)
     assert spec.shape == (S, F, n // 2 + 1)
     w = oracle.window(oracle.HANN, n)
     for s in range(S):
         _, ref = oracle.roundtrip_mask(x[s], n, h, mode=mode, pad_mode=kw.get("pad_mode", 0), want_spec=True)
         assert_spec_close(spec[s], ref, f"{n}/{h} mode {mode} stream {s}")
+        assert_spec_close(spec_pf[s], ref, f"{n}/{h} mode {mode} stream {s} per frame")
         assert np.all(spec[s][:, 0].imag == 0) and np.all(spec[s][:, -1].imag == 0)
         fr = frames_np(oracle, x[s], n, h, mode, True, kw.get("pad_mode", 0))
         direct = host(plan.rfft(dev(torch, (fr * w).astype(np.float32))))
-        assert np.array_equal(bits(spec[s].view(np.float32)), bits(direct.view(np.float32))), (n, h, mode, s)
+        assert np.array_equal(bits(spec_pf[s].view(np.float32)), bits(direct.view(np.float32))), (n, h, mode, s)
 
 
 @pytest.mark.parametrize("n,h", SHAPES + [(2048, 1024), (1024, 128)])
@@ -119,15 +128,24 @@ def test_istft_ola_bit_exact_vs_irfft_gather(pkg, oracle, torch_cuda, n, h):
     rng = np.random.default_rng(n + h)
     gain = rng.uniform(0.0, 2.0, bins).astype(np.float32)
     mask = rng.uniform(-1.5, 1.5, (S, F, bins)).astype(np.float32)
+    paired = n == 1024 and h in (128, 256, 512)  # K_pair_istft (frame pairing on, the default)
     for g, m in ((None, None), (gain, None), (None, mask), (gain, mask)):
         plan.set_spectral_gain(g)
         plan.set_spectral_mask(None if m is None else dev(torch, m))
-        y = host(plan.istft_ola(spec))
-        assert plan.last_launch()["kernels"] == ["k_istft"]
         X = dev(torch, stepped(host(spec), g, m))
         fr = plan.irfft(X.reshape(S * F, bins)).reshape(S, F, n)
         ref = host(plan.ola_gather(fr))
+        if paired:
+            yp = host(plan.istft_ola(spec))
+            assert plan.last_launch()["kernels"] == ["k_pair_istft"]
+            for s in range(S):
+                assert_close(yp[s], ref[s], float(np.max(np.abs(ref[s]))), f"{n}/{h} pair istft stream {s}",
+                             float(np.linalg.norm(ref[s])))
+            plan.set_frame_pairing(False)
+        y = host(plan.istft_ola(spec))
+        assert plan.last_launch()["kernels"] == ["k_istft"]
         assert np.array_equal(bits(y), bits(ref)), (n, h, g is not None, m is not None)
+        plan.set_frame_pairing(True)
     plan.set_spectral_gain(None)
     plan.set_spectral_mask(None)
 
@@ -370,9 +388,13 @@ def test_full_size_stft_istft(pkg, oracle, torch_cuda):
     g = torch.Generator(device="cuda").manual_seed(4321)
     x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
     plan = pkg.Plan(frame_size=n, hop_size=h)
-    spec = plan.stft(x)
+    spec = plan.stft(x)  # frame pairs (K_pair_stft / K_pair_istft)
     y = plan.istft_ola(spec)
     assert torch.equal(y, plan.istft_ola(plan.stft(x)))
+    plan.set_frame_pairing(False)  # per frame (K_stft / K_istft)
+    spec = plan.stft(x)
+    y_pf = plan.istft_ola(spec)
+    plan.set_frame_pairing(True)
     del spec
     yr = plan.roundtrip(x)
     F = plan.frame_count(T)
@@ -382,13 +404,83 @@ def test_full_size_stft_istft(pkg, oracle, torch_cuda):
     assert torch.equal(ym, yr)
     plan.set_frame_pairing(False)
     ym = plan.roundtrip(x)  # per frame: istft(stft)'s bits
-    assert torch.equal(ym, y)
+    assert torch.equal(ym, y_pf)
     plan.set_frame_pairing(True)
     plan.set_spectral_mask(None)
     for s in (0, 700, 1023):
         xs = host(x[s])
         ref = oracle.roundtrip(xs, n, h)
-        assert_close(host(y[s]), ref, 0.5, f"stft+istft stream {s}", float(np.linalg.norm(xs)))
-        assert_close(host(y[s]), host(yr[s]), 0.5, f"vs roundtrip stream {s}", float(np.linalg.norm(xs)))
-    del x, y, yr, ym
+        for yy, what in ((y, "pairs"), (y_pf, "per frame")):
+            assert_close(host(yy[s]), ref, 0.5, f"stft+istft ({what}) stream {s}", float(np.linalg.norm(xs)))
+            assert_close(host(yy[s]), host(yr[s]), 0.5, f"vs roundtrip ({what}) stream {s}", float(np.linalg.norm(xs)))
+    del x, y, y_pf, yr, ym
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("h", [128, 256, 512])
+def test_pair_stft_istft(pkg, oracle, torch_cuda, h):
+    """K_pair_stft / K_pair_istft (N = 1024, frame pairing on): spectra and the
+    split round trip vs the oracle and vs the per-frame kernels within the FFT
+    tolerance, with NaN / Inf / tiny / huge samples (the forward's per-frame
+    regime) and NaN / Inf / 1e30 spectrum values (the inverse's); the bits do not
+    depend on the chunking; odd frame counts; gain + mask."""
+    torch = torch_cuda
+    n, S = 1024, 4
+    T = 23 * n + 57
+    bins = n // 2 + 1
+    x = special(oracle.synth_streams(S, T, config_id=69))
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    F = plan.frame_count(T)
+    xd = dev(torch, x)
+    spec = plan.stft(xd)
+    assert plan.last_launch()["kernels"] == ["k_pair_stft"]
+    sh = host(spec)
+    for c in (1, 2, 5, F):
+        plan.set_chunks(c)
+        assert np.array_equal(bits(host(plan.stft(xd)).view(np.float32)), bits(sh.view(np.float32))), c
+    plan.set_chunks(0)
+    plan.set_frame_pairing(False)
+    spf = host(plan.stft(xd))
+    plan.set_frame_pairing(True)
+    for s in range(S):
+        _, ref = oracle.roundtrip_mask(x[s], n, h, want_spec=True)
+        assert_spec_close(sh[s], ref, f"{h} pair stft stream {s}")
+        assert_spec_close(sh[s], spf[s], f"{h} pair vs per-frame stft stream {s}")
+    # the inverse: a gain, a signed mask, and edited spectra that leave the paired regime
+    rng = np.random.default_rng(h + 1)
+    gain = np.linspace(0.5, 1.5, bins).astype(np.float32)
+    m = rng.uniform(-1.0, 1.5, (S, F, bins)).astype(np.float32)
+    se = sh.copy()
+    se[1, 3, 17] = np.nan
+    se[2, 8, 100] = np.inf
+    se[3, 11, 40] = 1e30
+    se[3, F - 1, 5] = 1e25
+    sed = dev(torch, se)
+    for g, mm in ((None, None), (gain, None), (gain, m)):
+        plan.set_spectral_gain(g)
+        plan.set_spectral_mask(None if mm is None else dev(torch, mm))
+        y = host(plan.istft_ola(sed))
+        assert plan.last_launch()["kernels"] == ["k_pair_istft"]
+        for c in (1, 3, F):
+            plan.set_chunks(c)
+            assert np.array_equal(bits(host(plan.istft_ola(sed))), bits(y)), c
+        plan.set_chunks(0)
+        plan.set_frame_pairing(False)
+        ypf = host(plan.istft_ola(sed))
+        assert plan.last_launch()["kernels"] == ["k_istft"]
+        plan.set_frame_pairing(True)
+        assert np.all(np.isfinite(y))
+        for s in range(S):
+            ymax, ynorm = finite_scale(ypf[s])
+            assert_close(y[s], ypf[s], ymax, f"{h} pair vs per-frame istft stream {s}", ynorm)
+    plan.set_spectral_gain(None)
+    plan.set_spectral_mask(None)
+    # the split round trip of plain input vs the fused one and the oracle
+    xp = oracle.synth_streams(S, T, config_id=70)
+    xpd = dev(torch, xp)
+    y2 = host(plan.istft_ola(plan.stft(xpd)))
+    yr = host(plan.roundtrip(xpd))
+    for s in range(S):
+        ref = oracle.roundtrip(xp[s], n, h)
+        assert_close(y2[s], ref, 0.5, f"{h} pair split vs oracle stream {s}", float(np.linalg.norm(xp[s])))
+        assert_close(y2[s], yr[s], 0.5, f"{h} pair split vs roundtrip stream {s}", float(np.linalg.norm(xp[s])))
