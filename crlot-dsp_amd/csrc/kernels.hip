@@ -2165,10 +2165,10 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
     const int resident = fused_resident_waves() / 16 * fk::pair_mask_walkers_per_cu();
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.n_chunks, a.M);
     // a batch below one resident round (one window of a few streams: the per-call
-    // latency case) walks chunks of >= 16 frames instead, as many as fit the round
+    // latency case) walks chunks of >= 8 frames instead, as many as fit the round
     const int64_t S = std::max(1, n_streams);
     if (S * a.n_chunks < resident) {
-        const int64_t n = std::min<int64_t>(F / 16, (resident + S - 1) / S);
+        const int64_t n = std::min<int64_t>(F / 8, (resident + S - 1) / S);
         if (n > a.n_chunks) {
             a.M = int((F + n - 1) / n);
             a.n_chunks = int((F + a.M - 1) / a.M);
@@ -2204,7 +2204,7 @@ hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* 
     a.ld_frame = ld_frame;
     const int64_t S = std::max(1, n_streams), resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu();
     int64_t n = std::max<int64_t>((F + 127) / 128, (2 * resident + S - 1) / S);
-    n = std::max<int64_t>(1, std::min<int64_t>(n, (F + 15) / 16));
+    n = std::max<int64_t>(1, std::min<int64_t>(n, (F + 1) / 2));  // (down to one pair per walk: small batches)
     if (const int64_t c = chunks_or(0, F); c > 0) n = std::min(c, F);
     int64_t m = (F + n - 1) / n;
     m += m & 1;
@@ -2214,7 +2214,7 @@ hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* 
     return fk::launch_pair_stft(g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
 }
 
-// K_pair_istft: K_pair_mask's chunking (whole resident rounds; small batches in >= 16-frame chunks)
+// K_pair_istft: K_pair_mask's chunking (whole resident rounds; small batches in >= 8-frame chunks)
 hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
                              int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
                              hipStream_t stream) {
@@ -2238,8 +2238,8 @@ hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMa
     const int resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu();
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.f.n_chunks, a.f.M);
     const int64_t S = std::max(1, n_streams);
-    if (S * a.f.n_chunks < resident) {
-        const int64_t n = std::min<int64_t>(F / 16, (resident + S - 1) / S);
+    if (S * a.f.n_chunks < resident) {  // (small batches: chunks of >= 8 frames, as the mask walker)
+        const int64_t n = std::min<int64_t>(F / 8, (resident + S - 1) / S);
         if (n > a.f.n_chunks) {
             a.f.M = int((F + n - 1) / n);
             a.f.n_chunks = int((F + a.f.M - 1) / a.f.M);
