@@ -1036,8 +1036,8 @@ int stft_impl(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams,
     const crlot::DevTables t = tables(p);
     hipError_t e;
     const int64_t lim = int64_t(1) << 29;
-    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && t.ptw && t.wa && aligned4(d_x) && T < lim) {
-        // N = 1024 frame pairs (pairing off: K_stft, bit-identical to crlot_rfft_batched)
+    if (p->pairing && crlot::pair_spec_supported(p->geo.n, p->geo.h) && t.ptw && t.wa && aligned4(d_x) && T < lim) {
+        // N = 1024 / 512 frame pairs (pairing off: K_stft, bit-identical to crlot_rfft_batched)
         e = crlot::launch_pair_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft (frame pairs) kernel launch");
     }
@@ -1069,9 +1069,9 @@ int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams
                int64_t ld_frame, int64_t ld_y, float* specw, float* frames, hipStream_t s) {
     const crlot::DevTables t = tables(p);
     hipError_t e;
-    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && t.ptw && t.pden && t.wsn && t.rden &&
+    if (p->pairing && crlot::pair_spec_supported(p->geo.n, p->geo.h) && t.ptw && t.pden && t.wsn && t.rden &&
         p->geo.ring_len % p->geo.h == 0 && aligned4(d_y) && F * p->geo.h + 2 * p->geo.n < (int64_t(1) << 29)) {
-        // N = 1024 frame pairs (pairing off: K_istft, bit-identical to irfft + gather)
+        // N = 1024 / 512 frame pairs (pairing off: K_istft, bit-identical to irfft + gather)
         e = crlot::launch_pair_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft (frame pairs) kernel launch");
     }

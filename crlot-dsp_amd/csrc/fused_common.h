@@ -214,7 +214,7 @@ hipError_t launch_pair2k_hot(int sh, const FusedArgs& a, int64_t grid, hipStream
 hipError_t launch_pair2k_hot3(int sh, const FusedArgs& a, int64_t grid, hipStream_t stream);
 // ... and K_pair512's (H = 64 * sh, sh = 2 or 4; w waves per workgroup, flags per wave)
 hipError_t launch_pair512_hot(int sh, const FusedArgs& a, int64_t waves, int w, hipStream_t stream);
-// K_pair_stft / K_pair_istft (pair_stft.hip): N = 1024, H = 128, 256, 512
+// K_pair_stft / K_pair_istft (pair_stft.hip): N = 1024, H = 128, 256, 512; N = 512, H = 128, 256
 struct PairSpecArgs {
     FusedArgs f;       // stft: x, T, ld_x; istft: y, out_len, ld_y, the OLA tables
     float* spec;       // stft output rows
@@ -223,8 +223,8 @@ struct PairSpecArgs {
     SpecMask mask;     // istft: the per-frame mask (p null: none)
 };
 int pair_spec_walkers_per_cu();
-hipError_t launch_pair_stft(int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
-hipError_t launch_pair_istft(int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
+hipError_t launch_pair_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
+hipError_t launch_pair_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
 // K_pair_mask (pair_mask.hip): walkers a CU holds, and the launch (H = 128, 256, 512)
 int pair_mask_walkers_per_cu();
 hipError_t launch_pair_mask(int h, const FusedArgs& f, const SpecMask& m, int64_t walkers, hipStream_t stream);

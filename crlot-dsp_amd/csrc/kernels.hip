@@ -2144,6 +2144,7 @@ int wg_chunk_target() {
 }  // namespace
 
 bool pair_mask_supported(int n, int h) { return n == 1024 && (h == 128 || h == 256 || h == 512); }
+bool pair_spec_supported(int n, int h) { return pair_mask_supported(n, h) || (n == 512 && (h == 128 || h == 256)); }
 
 // K_pair_mask: K_pair's chunking (whole resident rounds) over its own residency
 hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
@@ -2189,7 +2190,7 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
 hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
                             int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
                             hipStream_t stream) {
-    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.wa) return hipErrorInvalidValue;
+    if (!pair_spec_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.wa) return hipErrorInvalidValue;
     fk::PairSpecArgs a{};
     a.f.t = t;
     a.f.x = x;
@@ -2211,14 +2212,14 @@ hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* 
     a.f.M = int(m);
     a.f.n_chunks = int((F + m - 1) / m);
     note_chunks(a.f.n_chunks);
-    return fk::launch_pair_stft(g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
+    return fk::launch_pair_stft(g.n, g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
 }
 
 // K_pair_istft: K_pair_mask's chunking (whole resident rounds; small batches in >= 8-frame chunks)
 hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
                              int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
                              hipStream_t stream) {
-    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.pden || !t.wsn || !t.rden ||
+    if (!pair_spec_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.pden || !t.wsn || !t.rden ||
         g.ring_len % g.h != 0)
         return hipErrorInvalidValue;
     fk::PairSpecArgs a{};
@@ -2247,7 +2248,7 @@ hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMa
     }
     chunk_override(F, a.f);
     note_chunks(a.f.n_chunks);
-    return fk::launch_pair_istft(g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
+    return fk::launch_pair_istft(g.n, g.h, a, int64_t(n_streams) * a.f.n_chunks, stream);
 }
 
 std::vector<float> build_pair512_twiddles() {

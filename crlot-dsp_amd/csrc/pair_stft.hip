@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "fft_pair.h"
+#include "fft_pair512.h"
 #include "fused_common.h"
 
 namespace crlot {
@@ -397,6 +398,276 @@ __global__ __launch_bounds__(64 * kSW, (PairIstftOcc<SH, MASK>::value)) void k_p
     }
 }
 
+// ------------------------------------------------------------------ N = 512 (fft_pair512.h)
+// The same two kernels on K_pair512's transform: lane l holds z[l + 64 m], m < 8;
+// the spectrum sits at bin q(l) + 64 d, q(l) = (l >> 3) + 8 (l & 7) (pair512_bin:
+// an involution), so the partner of (l, d) is register 7 - d of lane
+// q(64 - q(l)) and lane 0's partners its own registers (8 - d) mod 8.  Windows,
+// twiddles in registers; LDS only the per-wave exchange buffer (576 complex),
+// which also stages the inverse's rows (2 x 257 complex).
+__device__ __forceinline__ int p512_q(int l) { return (l >> 3) + 8 * (l & 7); }
+struct Spec512Lds {
+    static constexpr size_t bytes = sizeof(dev::pc) * dev::kP512Buf * kSW;
+};
+
+template <int SH>
+__global__ __launch_bounds__(64 * kSW) void k_pair512_stft(const PairSpecArgs pa) {
+    const FusedArgs& a = pa.f;
+    constexpr int E = 8, H = 64 * SH, NB = 8 / SH, P2 = 256;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kP512Buf;
+    const int gw = blockIdx.x * kSW + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M, f1 = min(a.F, f0 + a.M);  // (M even)
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, span_bytes(a.T, 1));
+    float* so = pa.spec + int64_t(s) * pa.ld_spec;
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi;
+    const int q = p512_q(lane);
+    const int partner = p512_q((64 - q) & 63);
+    dev::Pair512TwReg tw;
+    dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
+    float wa[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) wa[m] = a.t.wa[lane + 64 * m];
+    auto load_hop = [&](float* dst, int origin) { load_hop1<SH>(dst, rx, lane, origin, a.T, a.pad_mode); };
+    float xin[E + SH];
+    uint32_t hopok = 0;
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop(xin + h * SH, (f0 + h) * H - a.pad);
+        hopok |= hop_ok<SH>(xin + h * SH, xlo, xhi) << h;
+    }
+    auto store_bins = [&](float* row, auto valfn) {  // bins q + 64 d <= N/2: d < 4, and d = 4 in lane 0
+        float2* r2 = reinterpret_cast<float2*>(row);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const dev::pc o = valfn(d);
+            st2(r2 + q + 64 * d, o.x, o.y);
+        }
+        if (lane == 0) {
+            const dev::pc o = valfn(4);
+            st2(r2 + P2, o.x, o.y);
+        }
+    };
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;
+    for (int k = f0; k < f1; k += 2) {
+        float nxt[2 * SH];
+        load_hop(nxt, (k + NB + 1) * H - a.pad);
+        load_hop(nxt + SH, (k + NB + 2) * H - a.pad);
+        const bool two = k + 1 < f1;
+        float* ra = so + int64_t(k) * pa.ld_frame;
+        float* rb = ra + pa.ld_frame;
+        dev::pc v[E];
+        if ((hopok & kPairHops) == kPairHops) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(xin[m] * wa[m], xin[m + SH] * wa[m]);
+            dev::wave_lds_fence();
+            dev::pair512_fwd(v, buf, tw, lane);
+            dev::pc zp[5];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                const float px = v[(7 - d) & 7].x, py = v[(7 - d) & 7].y;
+                zp[d] = dev::pc_mk(bperm_f(partner, px), bperm_f(partner, py));
+                if (lane == 0) zp[d] = v[(8 - d) & 7];
+            }
+            store_bins(ra, [&](int d) {
+                return dev::pc_mk(0.5f * (v[d].x + zp[d].x), 0.5f * (v[d].y - zp[d].y));
+            });
+            if (two)
+                store_bins(rb, [&](int d) {
+                    return dev::pc_mk(0.5f * (v[d].y + zp[d].y), 0.5f * (zp[d].x - v[d].x));
+                });
+        } else {  // each frame alone, full input sanitize
+            for (int p = 0; p < (two ? 2 : 1); ++p) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(dev::sanit((p ? xin[m + SH] : xin[m]) * wa[m]), 0.0f);
+                dev::wave_lds_fence();
+                dev::pair512_fwd(v, buf, tw, lane);
+                store_bins(p ? rb : ra, [&](int d) {
+                    return dev::pc_mk(v[d].x, (lane == 0 && (d == 0 || d == 4)) ? 0.0f : v[d].y);
+                });
+            }
+        }
+        hopok = (hopok | hop_ok<SH>(nxt, xlo, xhi) << (NB + 1) | hop_ok<SH>(nxt + SH, xlo, xhi) << (NB + 2)) >> 2;
+#pragma unroll
+        for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
+#pragma unroll
+        for (int qq = 0; qq < 2 * SH; ++qq) xin[E - SH + qq] = nxt[qq];
+    }
+}
+
+template <int SH, int NB, bool MASK>
+__global__ __launch_bounds__(64 * kSW) void k_pair512_istft(const PairSpecArgs pa) {
+    const FusedArgs& a = pa.f;
+    constexpr int E = 8, N = 512, H = 64 * SH, P2 = 256;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * dev::kP512Buf;
+    const int gw = blockIdx.x * kSW + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M, f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, span_bytes(a.out_len, 1));
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const float* sb = pa.sin + int64_t(s) * pa.ld_spec;
+    const int q = p512_q(lane);
+    dev::Pair512TwReg tw;
+    dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
+    float ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) ws[m] = a.t.wsn[lane + 64 * m] * a.gain;  // (ws g: K_pair512's OLA form)
+    float acc[NB][SH];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) acc[j][qq] = 0.f;
+    auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float x = imag ? v[m].y : v[m].x;
+            const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
+            float& r = acc[m / SH][m % SH];
+            r = __builtin_fmaf(o, ws[m], r);
+        }
+    };
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {
+        float mx = 0.0f, mn = 0x1p127f;
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) {
+            const float t = __builtin_fabsf(acc[0][qq]);
+            mx = __builtin_fmaxf(mx, t);
+            mn = __builtin_fminf(mn, t);
+        }
+        const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
+        float o[SH];
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) o[qq] = mk_div(acc[0][qq], dr[qq], dr[SH + qq]);
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+#pragma unroll
+            for (int qq = 0; qq < SH; ++qq) o[qq] = acc[0][qq] / dr[qq];
+        }
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[qq]), rk, lane * 4,
+                                                  k * (4 * H) + qq * 256, 0);
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int qq = 0; qq < SH; ++qq) acc[j][qq] = acc[j + 1][qq];
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) acc[NB - 1][qq] = 0.f;
+    };
+    constexpr int MI = 5;  // natural-order bins lane + 64 i (i = 4: bin N/2, lane 0's)
+    float2 ra_[MI], rb_[MI];
+    float ma_[MASK ? MI : 1], mb_[MASK ? MI : 1];
+    const float* mrow0 = MASK ? pa.mask.p + int64_t(s) * pa.mask.ld_stream : nullptr;
+    auto load_rows = [&](int k) {
+        const float2* ra = reinterpret_cast<const float2*>(sb + int64_t(k) * pa.ld_frame);
+        const float2* rb = reinterpret_cast<const float2*>(sb + int64_t(k + 1) * pa.ld_frame);
+        const bool two = k + 1 < a.F;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = i < 4 ? lane + 64 * i : P2;
+            ra_[i] = ld2(ra + kr);
+            rb_[i] = two ? ld2(rb + kr) : make_float2(0.f, 0.f);
+        }
+        if constexpr (MASK) {
+            const float* m0 = mrow0 + int64_t(k) * pa.mask.ld_frame;
+            const float* m1 = two ? m0 + pa.mask.ld_frame : m0;
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                const int kr = i < 4 ? lane + 64 * i : P2;
+                ma_[i] = m0[kr];
+                mb_[i] = m1[kr];
+            }
+        }
+    };
+    auto stage = [&]() -> bool {
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = i < 4 ? lane + 64 * i : P2;
+            const float g = a.t.gain ? a.t.gain[kr] : 1.0f;
+            float ax = ra_[i].x * g, ay = ra_[i].y * g, bx = rb_[i].x * g, by = rb_[i].y * g;
+            if constexpr (MASK) {
+                ax *= ma_[i];
+                ay *= ma_[i];
+                bx *= mb_[i];
+                by *= mb_[i];
+            }
+            if (kr == 0 || kr == P2) ay = by = 0.0f;
+            const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ax), __builtin_fabsf(ay)),
+                                            __builtin_fmaxf(__builtin_fabsf(bx), __builtin_fabsf(by)));
+            bad |= !(m <= 0x1p60f) | (ax != ax) | (ay != ay) | (bx != bx) | (by != by);
+            if (i < 4 || lane == 0) {
+                buf[kr] = dev::pc_mk(ax, ay);
+                buf[P2 + 1 + kr] = dev::pc_mk(bx, by);
+            }
+        }
+        return __builtin_amdgcn_ballot_w64(bad) == 0;
+    };
+    const dev::pc* const ca = buf + q;
+    const dev::pc* const cb = buf - q;
+    load_rows(fs);
+    for (int k = fs; k < f1; k += 2) {
+        const bool paired = stage();
+        dev::wave_lds_fence();
+        const bool more = k + 2 < f1;
+        dev::pc v[E];
+        if (paired) {
+#pragma unroll
+            for (int d = 0; d < E; ++d) {
+                const dev::pc A = d < 4 ? ca[64 * d] : cb[N - 64 * d];
+                const dev::pc B = d < 4 ? ca[P2 + 1 + 64 * d] : cb[P2 + 1 + N - 64 * d];
+                v[d] = d < 4 ? dev::pc_mk(A.x - B.y, A.y + B.x) : dev::pc_mk(A.x + B.y, B.x - A.y);
+            }
+            dev::wave_lds_fence();
+            if (more) load_rows(k + 2);
+            dev::pair512_inv(v, buf, tw, lane);
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
+            load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+            accumulate(v, false, true);
+            emit(k, dr0);
+            if (k + 1 < f1) {
+                accumulate(v, true, true);
+                emit(k + 1, dr1);
+            }
+        } else {
+            const int npass = min(2, f1 - k);
+            for (int p = 0; p < npass; ++p) {
+                if (p) {
+                    dev::wave_lds_fence();
+                    (void)stage();
+                    dev::wave_lds_fence();
+                }
+#pragma unroll
+                for (int d = 0; d < E; ++d) {
+                    const dev::pc X = d < 4 ? ca[(p ? P2 + 1 : 0) + 64 * d] : cb[(p ? P2 + 1 : 0) + N - 64 * d];
+                    v[d] = d < 4 ? X : dev::pc_mk(X.x, -X.y);
+                }
+                dev::wave_lds_fence();
+                dev::pair512_inv(v, buf, tw, lane);
+                float dr[2 * SH];
+                load_den<SH>(dr, rp, lane, (k + p) % a.ring_blocks);
+                accumulate(v, false, false);
+                emit(k + p, dr);
+            }
+            if (more) load_rows(k + 2);
+        }
+        dev::wave_lds_fence();
+    }
+}
+
 template <typename K>
 hipError_t launch_spec(K kernel, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
     hipError_t e = set_lds(kernel, SpecLds::bytes);
@@ -420,8 +691,22 @@ int pair_spec_walkers_per_cu() {
     return v;
 }
 
-hipError_t launch_pair_stft(int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
+template <typename K>
+hipError_t launch_spec512(K kernel, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
+    const int64_t grid = (walkers + kSW - 1) / kSW;
+    hipLaunchKernelGGL(kernel, dim3(unsigned(grid)), dim3(64 * kSW), Spec512Lds::bytes, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
     note_launch(CRLOT_K_PAIR_STFT, (walkers + kSW - 1) / kSW);
+    if (n == 512) {
+        switch (h) {
+            case 128: return launch_spec512(k_pair512_stft<2>, a, walkers, stream);
+            case 256: return launch_spec512(k_pair512_stft<4>, a, walkers, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (h) {
         case 128: return launch_spec(k_pair_stft<2>, a, walkers, stream);
         case 256: return launch_spec(k_pair_stft<4>, a, walkers, stream);
@@ -440,8 +725,19 @@ hipError_t pair_istft_m(int h, const PairSpecArgs& a, int64_t walkers, hipStream
     }
 }
 
-hipError_t launch_pair_istft(int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
+template <bool MASK>
+hipError_t pair512_istft_m(int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
+    switch (h) {
+        case 128: return launch_spec512(k_pair512_istft<2, 4, MASK>, a, walkers, stream);
+        case 256: return launch_spec512(k_pair512_istft<4, 2, MASK>, a, walkers, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_pair_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
     note_launch(CRLOT_K_PAIR_ISTFT, (walkers + kSW - 1) / kSW);
+    if (n == 512)
+        return a.mask.p ? pair512_istft_m<true>(h, a, walkers, stream) : pair512_istft_m<false>(h, a, walkers, stream);
     return a.mask.p ? pair_istft_m<true>(h, a, walkers, stream) : pair_istft_m<false>(h, a, walkers, stream);
 }
 
