@@ -486,3 +486,52 @@ def test_pair_stft_istft(pkg, oracle, torch_cuda, n, h):
         ref = oracle.roundtrip(xp[s], n, h)
         assert_close(y2[s], ref, 0.5, f"{h} pair split vs oracle stream {s}", float(np.linalg.norm(xp[s])))
         assert_close(y2[s], yr[s], 0.5, f"{h} pair split vs roundtrip stream {s}", float(np.linalg.norm(xp[s])))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
+    """Random shapes through crlot_stft / crlot_istft_ola / the masked round trip:
+    frame sizes with and without frame-pair kernels, every framing, stream counts
+    and lengths (short streams, odd frame counts), leading dimensions with slack;
+    frame pairs vs per frame within the FFT tolerance, per frame bit-exact between
+    the split and the fused masked walk, one stream vs the oracle."""
+    torch = torch_cuda
+    rng = np.random.default_rng(1000 + seed)
+    n, h = [(1024, 256), (1024, 128), (1024, 512), (512, 128), (512, 256), (2048, 512), (256, 128),
+            (4096, 1024)][int(rng.integers(8))]
+    mode = int(rng.integers(3))
+    kw = dict(center=bool(rng.integers(2)), pad_mode=int(rng.integers(3))) if mode == 2 else {}
+    S = int(rng.integers(1, 6))
+    T = int(rng.integers(n // 2, 9 * n))
+    plan = pkg.Plan(frame_size=n, hop_size=h, boundary_mode=mode, **kw)
+    F = plan.frame_count(T)
+    if F == 0:
+        pytest.skip("no frames")
+    bins = n // 2 + 1
+    x = oracle.synth_streams(S, T, config_id=80 + seed)
+    ldx = T + int(rng.integers(0, 5))
+    xs = torch.zeros((S, ldx), device="cuda")
+    xs[:, :T] = dev(torch, x)
+    xv = xs[:, :T]
+    m = rng.uniform(0.0, 1.2, (S, F, bins)).astype(np.float32)
+    outs = {}
+    for pairing in (True, False):
+        plan.set_frame_pairing(pairing)
+        spec = plan.stft(xv)
+        plan.set_spectral_mask(dev(torch, m))
+        y_split = host(plan.istft_ola(spec))
+        y_walk = host(plan.roundtrip(xv))
+        plan.set_spectral_mask(None)
+        outs[pairing] = (host(spec), y_split, y_walk)
+    sp, ysp, ywp = outs[True]
+    sf, ysf, ywf = outs[False]
+    assert np.array_equal(bits(ysf), bits(ywf)), (n, h, mode, S, T)  # per frame: split == fused walk
+    for s in range(S):
+        assert_spec_close(sp[s], sf[s], f"{n}/{h} pairs vs per frame, stream {s}")
+        ymax, ynorm = finite_scale(ysf[s])
+        for yy, what in ((ysp, "split"), (ywp, "walk")):
+            assert_close(yy[s], ysf[s], max(ymax, 1e-30), f"{n}/{h} {what} vs per frame, stream {s}", ynorm)
+    ref = oracle.roundtrip_mask(x[0], n, h, mask=m[0], mode=mode, center=kw.get("center", True),
+                                pad_mode=kw.get("pad_mode", 0))
+    assert_close(ysf[0], ref, max(finite_scale(ref)[0], 1e-30), f"{n}/{h} mode {mode} vs oracle",
+                 finite_scale(ref)[1])
