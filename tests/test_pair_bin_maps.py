@@ -1,0 +1,47 @@
+"""The index maps the frame-pair spectral kernels rely on (CPU; restated from
+csrc/fft_pair.h pair_bin_lane, csrc/fft_pair512.h pair512_bin and the comments of
+csrc/pair_mask.hip / csrc/pair_stft.hip), checked exhaustively:
+
+  * the bin of (lane l, register d) is q(l) + 64 d with q an involution;
+  * its partner bin N - k sits in register E-1-d of lane q(64 - q(l)), except in
+    lane 0, where it is register (E - d) mod E of lane 0 (ds_bpermute + readlane);
+  * the forward split stores every real bin 0 .. N/2 exactly once (registers
+    d < E/2 in every lane, register E/2 in lane 0);
+  * the inverse's scrambled reads (buf + q + 64 d for d < E/2, buf - q + N - 64 d
+    above) land on the real bin min(k, N - k), conjugated above N/2.
+"""
+import pytest
+
+
+def q1024(l):
+    return (l & 3) + 4 * (l >> 4) + 16 * ((l >> 2) & 3)
+
+
+def q512(l):
+    return (l >> 3) + 8 * (l & 7)
+
+
+@pytest.mark.parametrize("n,E,q", [(1024, 16, q1024), (512, 8, q512)])
+def test_pair_bin_maps(n, E, q):
+    lanes = range(64)
+    assert sorted(q(l) for l in lanes) == list(range(64))
+    assert all(q(q(l)) == l for l in lanes)  # involution
+    where = {q(l) + 64 * d: (l, d) for l in lanes for d in range(E)}
+    assert sorted(where) == list(range(n))
+    for l in lanes:
+        partner = q((64 - q(l)) & 63)
+        for d in range(E):
+            kb = q(l) + 64 * d
+            want = where[(n - kb) % n]
+            got = (0, (E - d) % E) if l == 0 else (partner, E - 1 - d)
+            assert got == want, (n, l, d)
+    # the forward split's stores: bins 0 .. N/2, each once
+    stored = [q(l) + 64 * d for l in lanes for d in range(E // 2)] + [q(0) + 64 * (E // 2)]
+    assert sorted(stored) == list(range(n // 2 + 1))
+    # the inverse's scrambled reads of the staged real bins
+    for l in lanes:
+        for d in range(E):
+            kb = q(l) + 64 * d
+            idx = q(l) + 64 * d if d < E // 2 else -q(l) + n - 64 * d
+            assert idx == min(kb, n - kb), (n, l, d)
+            assert 0 <= idx <= n // 2
