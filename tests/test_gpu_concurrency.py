@@ -247,3 +247,47 @@ def test_stream_rt_idle_exit_is_grid_wide(pkg, oracle, torch_cuda):
             assert np.array_equal(bits(out), bits(want[q])), q
     st.close()
     assert len(slow) <= 1, slow
+
+
+@pytest.mark.parametrize("pairing", [True, False])
+def test_two_streams_spectral_entries(pkg, oracle, torch_cuda, pairing):
+    """crlot_stft / crlot_istft_ola and the masked round trip of one plan on two
+    streams at once (the staged fallbacks take per-stream scratch: unaligned
+    output rows force them for half the calls): bits equal the serial runs."""
+    torch = torch_cuda
+    n, h, S, T = 1024, 256, 3, 20_000
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_frame_pairing(pairing)
+    F = plan.frame_count(T)
+    xa = dev(torch, bursty(oracle, S, T, h, 91))
+    xb = dev(torch, oracle.synth_streams(S, T, config_id=92))
+    m = torch.from_numpy(np.random.default_rng(5).uniform(0, 1, (F, n // 2 + 1)).astype(np.float32)).cuda()
+
+    def work(x, yo):
+        spec = plan.stft(x)
+        y1 = plan.istft_ola(spec)
+        plan.roundtrip(x, yo[:, :F * h])  # (odd row stride: per frame the staged path)
+        return spec, y1
+
+    serial = []
+    plan.set_spectral_mask(m)
+    for x in (xa, xb):
+        yo = torch.zeros((S, F * h + 1), device="cuda")
+        spec, y1 = work(x, yo)
+        serial.append((host(spec), host(y1), host(yo[:, :F * h])))
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    for it in range(3):
+        outs = []
+        yoa = torch.zeros((S, F * h + 1), device="cuda")
+        yob = torch.zeros((S, F * h + 1), device="cuda")
+        with torch.cuda.stream(sa):
+            ra = work(xa, yoa)
+        with torch.cuda.stream(sb):
+            rb = work(xb, yob)
+        torch.cuda.synchronize()
+        outs = [(host(ra[0]), host(ra[1]), host(yoa[:, :F * h])), (host(rb[0]), host(rb[1]), host(yob[:, :F * h]))]
+        for got, want in zip(outs, serial):
+            for g_, w_ in zip(got, want):
+                assert np.array_equal(bits(g_.view(np.float32) if g_.dtype == np.complex64 else g_),
+                                      bits(w_.view(np.float32) if w_.dtype == np.complex64 else w_)), (pairing, it)
+    plan.set_spectral_mask(None)
