@@ -225,9 +225,10 @@ struct PairSpecArgs {
 int pair_spec_walkers_per_cu();
 hipError_t launch_pair_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
 hipError_t launch_pair_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
-// K_pair_mask (pair_mask.hip): walkers a CU holds, and the launch (H = 128, 256, 512)
-int pair_mask_walkers_per_cu();
-hipError_t launch_pair_mask(int h, const FusedArgs& f, const SpecMask& m, int64_t walkers, hipStream_t stream);
+// K_pair_mask (pair_mask.hip): walkers a CU holds, and the launch (N = 1024: H = 128, 256, 512; N = 512: H = 128, 256)
+int pair_mask_walkers_per_cu(int n);
+hipError_t launch_pair_mask(int n, int h, const FusedArgs& f, const SpecMask& m, int64_t walkers,
+                            hipStream_t stream);
 
 }  // namespace fk
 }  // namespace crlot

@@ -2143,8 +2143,10 @@ int wg_chunk_target() {
 
 }  // namespace
 
-bool pair_mask_supported(int n, int h) { return n == 1024 && (h == 128 || h == 256 || h == 512); }
-bool pair_spec_supported(int n, int h) { return pair_mask_supported(n, h) || (n == 512 && (h == 128 || h == 256)); }
+bool pair_mask_supported(int n, int h) {
+    return (n == 1024 && (h == 128 || h == 256 || h == 512)) || (n == 512 && (h == 128 || h == 256));
+}
+bool pair_spec_supported(int n, int h) { return pair_mask_supported(n, h); }
 
 // K_pair_mask: K_pair's chunking (whole resident rounds) over its own residency
 hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
@@ -2163,7 +2165,7 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
     a.out_len = int(out_len);
     a.n_streams = n_streams;
     a.F = int(F);
-    const int resident = fused_resident_waves() / 16 * fk::pair_mask_walkers_per_cu();
+    const int resident = fused_resident_waves() / 16 * fk::pair_mask_walkers_per_cu(g.n);
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.n_chunks, a.M);
     // a batch below one resident round (one window of a few streams: the per-call
     // latency case) walks chunks of >= 8 frames instead, as many as fit the round
@@ -2182,7 +2184,7 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
     a.pad_mode = g.pad_mode;
     a.inv_n = g.inv_n;
     a.gain = g.gain;
-    return fk::launch_pair_mask(g.h, a, m, int64_t(n_streams) * a.n_chunks, stream);
+    return fk::launch_pair_mask(g.n, g.h, a, m, int64_t(n_streams) * a.n_chunks, stream);
 }
 
 // K_pair_stft: chunks of an even number of frames (pairs start on even frames), about

@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "fft_pair.h"
+#include "fft_pair512.h"
 #include "fused_common.h"
 
 namespace crlot {
@@ -311,6 +312,213 @@ __global__ __launch_bounds__(64 * kMW, CRLOT_PAIR_MASK_WAVES) void k_pair_mask(c
     }
 }
 
+// ------------------------------------------------------------------ N = 512
+// The same walk on K_pair512's transform (fft_pair512.h): bins q(l) + 64 d with
+// q(l) = (l >> 3) + 8 (l & 7), the partner of (l, d) register 7 - d of lane
+// q(64 - q(l)) (lane 0: its own register (8 - d) mod 8); windows, twiddles in
+// registers, the gain from L2; per wave the exchange buffer and the staged
+// (c1, c2) of bins 0 .. 256.
+struct Mask512Lds {
+    static constexpr int kCst = 258;
+    static constexpr int per_wave = dev::kP512Buf + kCst;  // complex elements
+    static constexpr size_t bytes = sizeof(dev::pc) * per_wave * kMW;
+};
+__device__ __forceinline__ int m512_q(int l) { return (l >> 3) + 8 * (l & 7); }
+
+template <int SH, int NB>
+__global__ __launch_bounds__(64 * kMW) void k_pair512_mask(const MaskWalkArgs ma) {
+    const FusedArgs& a = ma.f;
+    constexpr int E = 8, N = 512, H = 64 * SH, P2 = N / 2;
+    static_assert(NB * SH == E, "N = NB * H");
+    static_assert(SH >= 2, "den rows are read 16 bytes at a time");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    dev::pc* buf = reinterpret_cast<dev::pc*>(smem) + wave * Mask512Lds::per_wave;
+    dev::pc* cst = buf + dev::kP512Buf;
+    const int gw = blockIdx.x * kMW + wave;
+    if (gw >= a.n_streams * a.n_chunks) return;
+    const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
+    const int f0 = c * a.M, f1 = min(a.F, f0 + a.M);
+    const int fs = max(0, f0 - (NB - 1)) & ~1;
+    const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(s) * a.ld_x, span_bytes(a.T, 1));
+    const __amdgpu_buffer_rsrc_t ry = dev::make_rsrc(a.y + int64_t(s) * a.ld_y, span_bytes(a.out_len, 1));
+    const __amdgpu_buffer_rsrc_t rp = dev::make_rsrc(a.t.pden, uint32_t(a.ring_blocks * H) * 8u);
+    const __amdgpu_buffer_rsrc_t ry_null = dev::make_rsrc(a.y, 0u);
+    const float xlo = a.t.px_lo, xhi = a.t.px_hi * 0x1p-20f;  // (mask values up to 2^20)
+    const float* mrow0 = ma.mask.p + int64_t(s) * ma.mask.ld_stream;
+    const int q = m512_q(lane);
+    const int partner = m512_q((64 - q) & 63);
+    dev::Pair512TwReg tw;
+    dev::pair512_tw_load(tw, reinterpret_cast<const dev::pc*>(a.t.ptw), lane);
+    float wa[E], ws[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        wa[m] = a.t.wa[lane + 64 * m];
+        ws[m] = a.t.wsn[lane + 64 * m] * a.gain;  // (ws g: K_pair512's OLA form)
+    }
+    auto gain_at = [&](int kr) { return a.t.gain ? a.t.gain[kr] : 1.0f; };
+    float xin[E + SH];
+    auto load_hop = [&](float* dst, int origin) { load_hop1<SH>(dst, rx, lane, origin, a.T, a.pad_mode); };
+    float acc[NB][SH];
+    auto accumulate = [&](const dev::pc (&v)[E], bool imag, bool paired) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const float x = imag ? v[m].y : v[m].x;
+            const float o = paired ? dev::sanit_scaled_finite<N>(x) : dev::sanit_scaled<N>(x);
+            float& r = acc[m / SH][m % SH];
+            r = __builtin_fmaf(o, ws[m], r);
+        }
+    };
+    auto emit = [&](int k, const float (&dr)[2 * SH]) {
+        float mx = 0.0f, mn = 0x1p127f;
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) {
+            const float t = __builtin_fabsf(acc[0][qq]);
+            mx = __builtin_fmaxf(mx, t);
+            mn = __builtin_fminf(mn, t);
+        }
+        const bool ok = (mx <= 0x1p64f) & ((mn >= 0x1p-64f) | (mx == 0.0f));
+        float o[SH];
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) o[qq] = mk_div(acc[0][qq], dr[qq], dr[SH + qq]);
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
+#pragma unroll
+            for (int qq = 0; qq < SH; ++qq) o[qq] = acc[0][qq] / dr[qq];
+        }
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o[qq]), rk, lane * 4,
+                                                  k * (4 * H) + qq * 256, 0);
+#pragma unroll
+        for (int j = 0; j < NB - 1; ++j)
+#pragma unroll
+            for (int qq = 0; qq < SH; ++qq) acc[j][qq] = acc[j + 1][qq];
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) acc[NB - 1][qq] = 0.f;
+    };
+    uint32_t hopok = 0;
+#pragma unroll
+    for (int h = 0; h <= NB; ++h) {
+        load_hop(xin + h * SH, (fs + h) * H - a.pad);
+        hopok |= hop_ok<SH>(xin + h * SH, xlo, xhi) << h;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int qq = 0; qq < SH; ++qq) acc[j][qq] = 0.f;
+
+    constexpr uint32_t kPairHops = (1u << (NB + 1)) - 1;
+    constexpr int MI = 5;  // real bins lane + 64 i (i = 4: bin 256, lane 0's)
+    float mra[MI], mrb[MI];
+    auto row_a = [&](int k) { return mrow0 + int64_t(k) * ma.mask.ld_frame; };
+    auto row_b = [&](int k) { return k + 1 < a.F ? row_a(k) + ma.mask.ld_frame : row_a(k); };
+    auto load_rows = [&](int k) {
+        const float* ra = row_a(k);
+        const float* rb = row_b(k);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = i < 4 ? lane + 64 * i : P2;
+            mra[i] = ra[kr];
+            mrb[i] = rb[kr];
+        }
+    };
+    auto stage_rows = [&]() -> bool {
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = i < 4 ? lane + 64 * i : P2;
+            bad |= !(__builtin_fabsf(mra[i]) <= 0x1p20f) | !(__builtin_fabsf(mrb[i]) <= 0x1p20f);  // (NaN too)
+            const float g = gain_at(kr);
+            const float ga = g * mra[i], gb = g * mrb[i];
+            if (i < 4 || lane == 0) cst[kr] = dev::pc_mk(0.5f * (ga + gb), 0.5f * (ga - gb));
+        }
+        return __builtin_amdgcn_ballot_w64(bad) == 0;
+    };
+    const dev::pc* const cb1 = cst + q;
+    const dev::pc* const cb2 = cst - q;
+    load_rows(fs);
+    bool mok = stage_rows();
+    for (int k = fs; k < f1; k += 2) {
+        float nxt[2 * SH];
+        load_hop(nxt, (k + NB + 1) * H - a.pad);
+        load_hop(nxt + SH, (k + NB + 2) * H - a.pad);
+        const bool more = k + 2 < f1;
+        if (more) load_rows(k + 2);
+        const bool paired = mok && (hopok & kPairHops) == kPairHops;
+        dev::pc v[E];
+        if (paired) {
+#pragma unroll
+            for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(xin[m] * wa[m], xin[m + SH] * wa[m]);
+            dev::wave_lds_fence();
+            dev::pair512_fwd(v, buf, tw, lane);
+            float own_r[E], own_i[E];
+#pragma unroll
+            for (int d = 0; d < E; ++d) {
+                const float re = v[(8 - d) & 7].x, im = v[(8 - d) & 7].y;
+                own_r[d] = lane0(re);
+                own_i[d] = lane0(im);
+            }
+#pragma unroll
+            for (int d = 0; d < E / 2; ++d) {
+                const int e = 7 - d;
+                dev::pc zd = dev::pc_mk(bperm(partner, v[e].x), bperm(partner, v[e].y));
+                dev::pc ze = dev::pc_mk(bperm(partner, v[d].x), bperm(partner, v[d].y));
+                if (lane == 0) {
+                    zd = dev::pc_mk(own_r[d], own_i[d]);
+                    ze = dev::pc_mk(own_r[e], own_i[e]);
+                }
+                const dev::pc cd = cb1[64 * d], ce = cb2[N - 64 * e];
+                v[d] = dev::pc_mk(__builtin_fmaf(cd.y, zd.x, cd.x * v[d].x), __builtin_fmaf(-cd.y, zd.y, cd.x * v[d].y));
+                v[e] = dev::pc_mk(__builtin_fmaf(ce.y, ze.x, ce.x * v[e].x), __builtin_fmaf(-ce.y, ze.y, ce.x * v[e].y));
+            }
+            dev::pair512_inv(v, buf, tw, lane);
+            float dr0[2 * SH], dr1[2 * SH];
+            load_den<SH>(dr0, rp, lane, k % a.ring_blocks);
+            load_den<SH>(dr1, rp, lane, (k + 1) % a.ring_blocks);
+            accumulate(v, false, true);
+            emit(k, dr0);
+            if (k + 1 < f1) {
+                accumulate(v, true, true);
+                emit(k + 1, dr1);
+            }
+        } else {  // each frame alone, full sanitize, its own gain g m
+            const int npass = min(2, f1 - k);
+            for (int p = 0; p < npass; ++p) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) v[m] = dev::pc_mk(dev::sanit((p ? xin[m + SH] : xin[m]) * wa[m]), 0.0f);
+                dev::wave_lds_fence();
+                dev::pair512_fwd(v, buf, tw, lane);
+                const float* r = p ? row_b(k) : row_a(k);
+#pragma unroll
+                for (int d = 0; d < E; ++d) {
+                    const int kb = q + 64 * d, kr = kb <= P2 ? kb : N - kb;
+                    v[d] = v[d] * (gain_at(kr) * r[kr]);
+                }
+                dev::pair512_inv(v, buf, tw, lane);
+                float dr[2 * SH];
+                load_den<SH>(dr, rp, lane, (k + p) % a.ring_blocks);
+                accumulate(v, false, false);
+                emit(k + p, dr);
+            }
+        }
+        if (more) mok = stage_rows();
+        hopok = (hopok | hop_ok<SH>(nxt, xlo, xhi) << (NB + 1) | hop_ok<SH>(nxt + SH, xlo, xhi) << (NB + 2)) >> 2;
+#pragma unroll
+        for (int m = 0; m < E + SH - 2 * SH; ++m) xin[m] = xin[m + 2 * SH];
+#pragma unroll
+        for (int qq = 0; qq < 2 * SH; ++qq) xin[E - SH + qq] = nxt[qq];
+    }
+}
+
+template <int SH>
+hipError_t pair512_mask_sh(const MaskWalkArgs& a, int64_t grid, hipStream_t stream) {
+    constexpr int NB = 8 / SH;
+    hipLaunchKernelGGL((k_pair512_mask<SH, NB>), dim3(unsigned(grid)), dim3(64 * kMW), Mask512Lds::bytes, stream, a);
+    return hipGetLastError();
+}
+
 template <int SH>
 hipError_t pair_mask_sh(const MaskWalkArgs& a, int64_t grid, hipStream_t stream) {
     constexpr int NB = 16 / SH;
@@ -323,8 +531,8 @@ hipError_t pair_mask_sh(const MaskWalkArgs& a, int64_t grid, hipStream_t stream)
 
 }  // namespace
 
-int pair_mask_walkers_per_cu() {
-    static const int v = [] {
+int pair_mask_walkers_per_cu(int n) {
+    static const int v1k = [] {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_pair_mask<4, 4>),
                                                          64 * kMW, MaskLds::bytes) != hipSuccess ||
@@ -332,15 +540,31 @@ int pair_mask_walkers_per_cu() {
             nb = 1;
         return nb * kMW;
     }();
-    return v;
+    static const int v512 = [] {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_pair512_mask<2, 4>),
+                                                         64 * kMW, Mask512Lds::bytes) != hipSuccess ||
+            nb <= 0)
+            nb = 1;
+        return nb * kMW;
+    }();
+    return n == 512 ? v512 : v1k;
 }
 
-hipError_t launch_pair_mask(int h, const FusedArgs& f, const SpecMask& m, int64_t walkers, hipStream_t stream) {
+hipError_t launch_pair_mask(int n, int h, const FusedArgs& f, const SpecMask& m, int64_t walkers,
+                            hipStream_t stream) {
     MaskWalkArgs a;
     a.f = f;
     a.mask = m;
     const int64_t grid = (walkers + kMW - 1) / kMW;
     note_launch(CRLOT_K_PAIR_MASK, grid);
+    if (n == 512) {
+        switch (h) {
+            case 128: return pair512_mask_sh<2>(a, grid, stream);
+            case 256: return pair512_mask_sh<4>(a, grid, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (h) {
         case 128: return pair_mask_sh<2>(a, grid, stream);
         case 256: return pair_mask_sh<4>(a, grid, stream);

@@ -176,7 +176,7 @@ def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared, pairing):
     plan.set_spectral_mask(dev(torch, m))
     xd = dev(torch, x)
     y = host(plan.roundtrip(xd))
-    paired = pairing and n == 1024
+    paired = pairing and (n, h) in PAIR_SPEC  # (the frame-pair masked walk takes the same shapes)
     assert plan.last_launch()["kernels"] == ["k_pair_mask" if paired else "k_stft_masked"]
     y2 = host(plan.istft_ola(plan.stft(xd)))
     assert np.all(np.isfinite(y))
@@ -191,17 +191,17 @@ def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared, pairing):
     plan.set_spectral_mask(None)
 
 
-@pytest.mark.parametrize("h", [128, 256, 512])
-def test_pair_mask_walk(pkg, oracle, torch_cuda, h):
-    """K_pair_mask (N = 1024): frames 2j, 2j+1 share one transform and the step
+@pytest.mark.parametrize("n,h", sorted(PAIR_SPEC))
+def test_pair_mask_walk(pkg, oracle, torch_cuda, n, h):
+    """K_pair_mask (N = 1024 and 512): frames 2j, 2j+1 share one transform and the step
     separates them (c1 Z + c2 conj Z[-k]).  A mask of ones gives K_pair's own bits
     (with and without a spectral gain, NaN / Inf / huge samples included); a
     time-varying signed mask with zero, NaN, tiny and huge (unpaired regime)
     values matches the oracle and the per-frame walk within the FFT tolerance;
     the bits do not depend on the chunking; odd frame counts."""
     torch = torch_cuda
-    n, S = 1024, 4
-    T = 29 * n + 17
+    S = 4
+    T = 29 * n + 18  # (even rows: the unmasked N = 512 round trip takes K_pair512; F odd at every hop here)
     bins = n // 2 + 1
     x = special(oracle.synth_streams(S, T, config_id=68))
     plan = pkg.Plan(frame_size=n, hop_size=h)
@@ -213,6 +213,7 @@ def test_pair_mask_walk(pkg, oracle, torch_cuda, h):
         plan.set_spectral_gain(g)
         plan.set_spectral_mask(None)
         y0 = host(plan.roundtrip(xd))
+        assert plan.last_launch()["kernels"][0].startswith("k_pair"), plan.last_launch()
         plan.set_spectral_mask(ones)
         y1 = host(plan.roundtrip(xd))
         assert plan.last_launch()["kernels"] == ["k_pair_mask"]
