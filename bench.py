@@ -693,7 +693,7 @@ def suite_stft(pkg, torch, dev):
     S, T = STREAMS, T_LEN
     g = torch.Generator(device=dev).manual_seed(41)
     x = (torch.rand((S, T), generator=g, device=dev) * 2 - 1) * 0.5
-    for n, h in ((1024, 256), (4096, 1024), (512, 128)):
+    for n, h in ((1024, 256), (4096, 1024), (512, 128), (2048, 512)):
         plan = pkg.Plan(frame_size=n, hop_size=h, device=dev.index)
         F, bins = plan.frame_count(T), n // 2 + 1
         spec = torch.empty((S, F, bins), dtype=torch.complex64, device=dev)
@@ -714,9 +714,16 @@ def suite_stft(pkg, torch, dev):
         t_is = _ev_time(torch, lambda: plan.istft_ola(spec, y), 10)
         k_is = plan.last_launch()["kernels"]
         t_both = _ev_time(torch, lambda: (plan.stft(x, spec), plan.istft_ola(spec, y)), 10)
+        plan.set_frame_pairing(False)  # the per-frame kernels beside the frame-pair ones
+        t_stf = _ev_time(torch, lambda: plan.stft(x, spec), 10)
+        k_stf = plan.last_launch()["kernels"]
+        t_isf = _ev_time(torch, lambda: plan.istft_ola(spec, y), 10)
+        k_isf = plan.last_launch()["kernels"]
+        plan.set_frame_pairing(True)
         shape = {"frame": n, "hop": h, "streams": S, "samples_per_stream": T, "frames_per_stream": F, "runs": [
             row("stft", t_st, b1, k_st), row("istft_ola", t_is, b1, k_is),
-            row("stft+istft_ola", t_both, 2 * b1)]}
+            row("stft+istft_ola", t_both, 2 * b1),
+            row("stft, per frame", t_stf, b1, k_stf), row("istft_ola, per frame", t_isf, b1, k_isf)]}
         del spec
         mask = torch.rand((F, bins), generator=g, device=dev)
         plan.set_spectral_mask(mask)
@@ -728,12 +735,11 @@ def suite_stft(pkg, torch, dev):
         t_ms = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)
         shape["runs"].append(row("roundtrip, mask per stream and frame", t_ms, 8.0 + 4.0 * bins / h,
                                  plan.last_launch()["kernels"]))
-        if n == 1024:  # the per-frame walk beside the frame-pair one
-            plan.set_frame_pairing(False)
-            t_mf = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)
-            shape["runs"].append(row("roundtrip, mask per stream and frame, per-frame walk", t_mf,
-                                     8.0 + 4.0 * bins / h, plan.last_launch()["kernels"]))
-            plan.set_frame_pairing(True)
+        plan.set_frame_pairing(False)  # the per-frame walk beside the frame-pair one
+        t_mf = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)
+        shape["runs"].append(row("roundtrip, mask per stream and frame, per-frame walk", t_mf,
+                                 8.0 + 4.0 * bins / h, plan.last_launch()["kernels"]))
+        plan.set_frame_pairing(True)
         plan.set_spectral_mask(None)
         del mask
         t_r = _ev_time(torch, lambda: plan.roundtrip(x, y), 10)

@@ -1036,8 +1036,8 @@ int stft_impl(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams,
     const crlot::DevTables t = tables(p);
     hipError_t e;
     const int64_t lim = int64_t(1) << 29;
-    if (p->pairing && crlot::pair_spec_supported(p->geo.n, p->geo.h) && t.ptw && t.wa && aligned4(d_x) && T < lim) {
-        // N = 1024 / 512 frame pairs (pairing off: K_stft, bit-identical to crlot_rfft_batched)
+    if (p->pairing && crlot::pair_spec_supported(p->geo.n, p->geo.h) && crlot::pair_tables(p->geo, t) && aligned4(d_x) && T < lim) {
+        // N = 512 - 4096 frame pairs (pairing off: K_stft, bit-identical to crlot_rfft_batched)
         e = crlot::launch_pair_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft (frame pairs) kernel launch");
     }
@@ -1069,9 +1069,9 @@ int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams
                int64_t ld_frame, int64_t ld_y, float* specw, float* frames, hipStream_t s) {
     const crlot::DevTables t = tables(p);
     hipError_t e;
-    if (p->pairing && crlot::pair_spec_supported(p->geo.n, p->geo.h) && t.ptw && t.pden && t.wsn && t.rden &&
+    if (p->pairing && crlot::pair_spec_supported(p->geo.n, p->geo.h) && crlot::pair_tables(p->geo, t) &&
         p->geo.ring_len % p->geo.h == 0 && aligned4(d_y) && F * p->geo.h + 2 * p->geo.n < (int64_t(1) << 29)) {
-        // N = 1024 / 512 frame pairs (pairing off: K_istft, bit-identical to irfft + gather)
+        // N = 512 - 4096 frame pairs (pairing off: K_istft, bit-identical to irfft + gather)
         e = crlot::launch_pair_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft (frame pairs) kernel launch");
     }
@@ -1104,10 +1104,10 @@ static int masked_roundtrip(crlot_plan* p, crlot::Scratch* sc, const float* d_x,
                             int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, hipStream_t s) {
     const int64_t out_len = F * p->geo.h, lim = int64_t(1) << 29;
     const crlot::DevTables t = tables(p);
-    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && t.ptw && t.pden && t.wsn && t.rden &&
+    if (p->pairing && crlot::pair_mask_supported(p->geo.n, p->geo.h) && crlot::pair_tables(p->geo, t) &&
         p->geo.ring_len % p->geo.h == 0 && aligned4(d_x) && aligned4(d_y) && T < lim && out_len + 2 * p->geo.n < lim &&
         int64_t(n_streams) * (T / p->geo.h + 1) < lim) {
-        // N = 1024 frame pairs (pairing off: the per-frame walk below, bit-identical to istft(stft))
+        // frame pairs (pairing off: the per-frame walk below, bit-identical to istft(stft))
         const hipError_t e = crlot::launch_pair_masked(p->geo, t, p->mask, d_x, d_y, n_streams, T, ld_x, ld_y, F,
                                                        out_len, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "masked frame-pair kernel launch");

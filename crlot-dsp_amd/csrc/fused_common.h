@@ -222,9 +222,16 @@ struct PairSpecArgs {
     int64_t ld_spec, ld_frame;
     SpecMask mask;     // istft: the per-frame mask (p null: none)
 };
-int pair_spec_walkers_per_cu();
+int pair_spec_walkers_per_cu(int n);
 hipError_t launch_pair_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
 hipError_t launch_pair_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
+// ... at N = 4096 (H = 512, 1024) and 2048 (H = 256, 512): one workgroup per walk
+// (pair_wg_spec.hip), the masked round trip too
+bool pair_wg_supported(int n, int h);
+int pair_wg_walkers_per_cu(int n);
+hipError_t launch_pairwg_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
+hipError_t launch_pairwg_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
+hipError_t launch_pairwg_mask(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream);
 // K_pair_mask (pair_mask.hip): walkers a CU holds, and the launch (N = 1024: H = 128, 256, 512; N = 512: H = 128, 256)
 int pair_mask_walkers_per_cu(int n);
 hipError_t launch_pair_mask(int n, int h, const FusedArgs& f, const SpecMask& m, int64_t walkers,

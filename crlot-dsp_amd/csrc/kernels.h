@@ -387,7 +387,9 @@ hipError_t launch_roundtrip_masked(const Geometry& g, const DevTables& t, const 
 // ... as frame pairs (K_pair_mask, pair_mask.hip: N = 1024, H = 128 / 256 / 512, the
 // pair tables; equal to the per-frame walk within float32 rounding)
 bool pair_mask_supported(int n, int h);
-bool pair_spec_supported(int n, int h);  // K_pair_stft / K_pair_istft: N = 1024 (H 128-512), N = 512 (H 128, 256)
+bool pair_spec_supported(int n, int h);  // K_pair_stft / K_pair_istft: N = 1024 (H 128-512), 512 (H 128, 256),
+                                         // 2048 (H 256, 512), 4096 (H 512, 1024)
+bool pair_tables(const Geometry& g, const DevTables& t);  // the tables those kernels read are there
 // crlot_stft / crlot_istft_ola as frame pairs (K_pair_stft / K_pair_istft, pair_stft.hip:
 // N = 1024, H = 128 / 256 / 512, the pair tables; within float32 rounding of the per-frame kernels)
 hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,

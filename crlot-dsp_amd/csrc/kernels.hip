@@ -2144,16 +2144,21 @@ int wg_chunk_target() {
 }  // namespace
 
 bool pair_mask_supported(int n, int h) {
-    return (n == 1024 && (h == 128 || h == 256 || h == 512)) || (n == 512 && (h == 128 || h == 256));
+    return (n == 1024 && (h == 128 || h == 256 || h == 512)) || (n == 512 && (h == 128 || h == 256)) ||
+           fk::pair_wg_supported(n, h);
 }
 bool pair_spec_supported(int n, int h) { return pair_mask_supported(n, h); }
+// the frame-pair kernels' tables (N = 2048 / 4096 keep theirs in ptw4 / pden4)
+bool pair_tables(const Geometry& g, const DevTables& t) {
+    return (g.n >= 2048 ? (t.ptw4 && t.pden4) : (t.ptw && t.pden)) && t.wa && t.wsn && t.rden;
+}
 
 // K_pair_mask: K_pair's chunking (whole resident rounds) over its own residency
 hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
                               int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
                               hipStream_t stream) {
-    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !m.p || !t.ptw || !t.pden || !t.wsn ||
-        !t.rden || g.ring_len % g.h != 0)
+    if (!pair_mask_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !m.p || !pair_tables(g, t) ||
+        g.ring_len % g.h != 0)
         return hipErrorInvalidValue;
     FusedArgs a;
     a.t = t;
@@ -2192,7 +2197,7 @@ hipError_t launch_pair_masked(const Geometry& g, const DevTables& t, const SpecM
 hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
                             int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
                             hipStream_t stream) {
-    if (!pair_spec_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.wa) return hipErrorInvalidValue;
+    if (!pair_spec_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !pair_tables(g, t)) return hipErrorInvalidValue;
     fk::PairSpecArgs a{};
     a.f.t = t;
     a.f.x = x;
@@ -2205,7 +2210,7 @@ hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* 
     a.spec = spec;
     a.ld_spec = ld_spec;
     a.ld_frame = ld_frame;
-    const int64_t S = std::max(1, n_streams), resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu();
+    const int64_t S = std::max(1, n_streams), resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu(g.n);
     int64_t n = std::max<int64_t>((F + 127) / 128, (2 * resident + S - 1) / S);
     n = std::max<int64_t>(1, std::min<int64_t>(n, (F + 1) / 2));  // (down to one pair per walk: small batches)
     if (const int64_t c = chunks_or(0, F); c > 0) n = std::min(c, F);
@@ -2221,8 +2226,7 @@ hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* 
 hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
                              int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
                              hipStream_t stream) {
-    if (!pair_spec_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !t.ptw || !t.pden || !t.wsn || !t.rden ||
-        g.ring_len % g.h != 0)
+    if (!pair_spec_supported(g.n, g.h) || F <= 0 || n_streams <= 0 || !pair_tables(g, t) || g.ring_len % g.h != 0)
         return hipErrorInvalidValue;
     fk::PairSpecArgs a{};
     a.f.t = t;
@@ -2238,7 +2242,7 @@ hipError_t launch_pair_istft(const Geometry& g, const DevTables& t, const SpecMa
     a.ld_spec = ld_spec;
     a.ld_frame = ld_frame;
     a.mask = m;
-    const int resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu();
+    const int resident = fused_resident_waves() / 16 * fk::pair_spec_walkers_per_cu(g.n);
     choose_chunks_rounds(F, n_streams, g.n / g.h + 1, resident, a.f.n_chunks, a.f.M);
     const int64_t S = std::max(1, n_streams);
     if (S * a.f.n_chunks < resident) {  // (small batches: chunks of >= 8 frames, as the mask walker)

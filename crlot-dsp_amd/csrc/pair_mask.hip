@@ -532,6 +532,7 @@ hipError_t pair_mask_sh(const MaskWalkArgs& a, int64_t grid, hipStream_t stream)
 }  // namespace
 
 int pair_mask_walkers_per_cu(int n) {
+    if (n >= 2048) return pair_wg_walkers_per_cu(n);
     static const int v1k = [] {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_pair_mask<4, 4>),
@@ -553,6 +554,12 @@ int pair_mask_walkers_per_cu(int n) {
 
 hipError_t launch_pair_mask(int n, int h, const FusedArgs& f, const SpecMask& m, int64_t walkers,
                             hipStream_t stream) {
+    if (n >= 2048) {  // one workgroup per walk (pair_wg_spec.hip)
+        PairSpecArgs pa{};
+        pa.f = f;
+        pa.mask = m;
+        return launch_pairwg_mask(n, h, pa, walkers, stream);
+    }
     MaskWalkArgs a;
     a.f = f;
     a.mask = m;

@@ -679,7 +679,8 @@ hipError_t launch_spec(K kernel, const PairSpecArgs& a, int64_t walkers, hipStre
 
 }  // namespace
 
-int pair_spec_walkers_per_cu() {
+int pair_spec_walkers_per_cu(int n) {
+    if (n >= 2048) return pair_wg_walkers_per_cu(n);
     static const int v = [] {
         int nb = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(k_pair_istft<4, 4, false>),
@@ -699,6 +700,7 @@ hipError_t launch_spec512(K kernel, const PairSpecArgs& a, int64_t walkers, hipS
 }
 
 hipError_t launch_pair_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
+    if (n >= 2048) return launch_pairwg_stft(n, h, a, walkers, stream);
     note_launch(CRLOT_K_PAIR_STFT, (walkers + kSW - 1) / kSW);
     if (n == 512) {
         switch (h) {
@@ -735,6 +737,7 @@ hipError_t pair512_istft_m(int h, const PairSpecArgs& a, int64_t walkers, hipStr
 }
 
 hipError_t launch_pair_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
+    if (n >= 2048) return launch_pairwg_istft(n, h, a, walkers, stream);
     note_launch(CRLOT_K_PAIR_ISTFT, (walkers + kSW - 1) / kSW);
     if (n == 512)
         return a.mask.p ? pair512_istft_m<true>(h, a, walkers, stream) : pair512_istft_m<false>(h, a, walkers, stream);

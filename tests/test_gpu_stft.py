@@ -15,7 +15,7 @@ Bars (tests/test_gpu_parity.py):
     crlot_istft_ola vs crlot_irfft_batched of the stepped spectra +
     crlot_ola_gather, the per-frame masked crlot_roundtrip vs
     crlot_istft_ola(crlot_stft), the walkers vs their staged fallbacks, every
-    chunking, and the N = 1024 frame-pair masked walk under a mask of ones vs
+    chunking, and the frame-pair masked walk under a mask of ones vs
     the unmasked frame-pair round trip;
   * the frame-pair masked walk vs the per-frame one: the FFT tolerance.
 """
@@ -28,7 +28,8 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [(1024, 256), (4096, 1024), (512, 128)]
 # the spectral entries as frame pairs (K_pair_stft / K_pair_istft, frame pairing on: the default)
-PAIR_SPEC = {(1024, 128), (1024, 256), (1024, 512), (512, 128), (512, 256)}
+PAIR_SPEC = {(1024, 128), (1024, 256), (1024, 512), (512, 128), (512, 256),
+             (2048, 256), (2048, 512), (4096, 512), (4096, 1024)}  # (N >= 2048: one workgroup per walk)
 
 
 def assert_spec_close(X, ref, what=""):
@@ -157,12 +158,12 @@ def test_istft_ola_bit_exact_vs_irfft_gather(pkg, oracle, torch_cuda, n, h):
 @pytest.mark.parametrize("pairing", [True, False])
 def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared, pairing):
     """crlot_roundtrip with a per-frame mask: one walk over HBM -- per frame
-    (k_stft_masked) bit-identical to crlot_istft_ola(crlot_stft(x)); at N = 1024
+    (k_stft_masked) bit-identical to crlot_istft_ola(crlot_stft(x)); at the PAIR_SPEC shapes
     with frame pairing (the default) as frame pairs (k_pair_mask) within the FFT
     tolerance of it -- and the oracle's masked e2e loop within the FFT tolerance,
     with NaN, Inf, tiny and huge samples in the input."""
-    if n != 1024 and not pairing:
-        pytest.skip("frame pairing only changes the N = 1024 walk")
+    if not pairing and (n, h) not in PAIR_SPEC:
+        pytest.skip("frame pairing only changes the frame-pair shapes' walk")
     torch = torch_cuda
     S, T = 4, 13 * n + 31
     bins = n // 2 + 1
@@ -193,7 +194,7 @@ def test_masked_roundtrip(pkg, oracle, torch_cuda, n, h, shared, pairing):
 
 @pytest.mark.parametrize("n,h", sorted(PAIR_SPEC))
 def test_pair_mask_walk(pkg, oracle, torch_cuda, n, h):
-    """K_pair_mask (N = 1024 and 512): frames 2j, 2j+1 share one transform and the step
+    """K_pair_mask (N = 512 - 4096): frames 2j, 2j+1 share one transform and the step
     separates them (c1 Z + c2 conj Z[-k]).  A mask of ones gives K_pair's own bits
     (with and without a spectral gain, NaN / Inf / huge samples included); a
     time-varying signed mask with zero, NaN, tiny and huge (unpaired regime)
@@ -422,7 +423,7 @@ def test_full_size_stft_istft(pkg, oracle, torch_cuda):
 
 @pytest.mark.parametrize("n,h", sorted(PAIR_SPEC))
 def test_pair_stft_istft(pkg, oracle, torch_cuda, n, h):
-    """K_pair_stft / K_pair_istft (N = 1024 and 512, frame pairing on): spectra and the
+    """K_pair_stft / K_pair_istft (N = 512 - 4096, frame pairing on): spectra and the
     split round trip vs the oracle and vs the per-frame kernels within the FFT
     tolerance, with NaN / Inf / tiny / huge samples (the forward's per-frame
     regime) and NaN / Inf / 1e30 spectrum values (the inverse's); the bits do not
