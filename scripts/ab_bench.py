@@ -1,7 +1,9 @@
 """A/B timing of library variants (crlot-dsp_amd/variants/*.so) in ONE process,
 interleaved rounds (cdna_hip_programming.md 5.4 rule 24), the
 order rotated every round so that no library always holds the first slot.  Each variant is
-loaded through its own ctypes handle; the workload is the headline one."""
+loaded through its own ctypes handle; the workload is the headline one.  AB_OP=stft /
+istft times crlot_stft / crlot_istft_ola instead of crlot_roundtrip (spectra in one
+shared buffer; the istft input is the base library's stft of the signal)."""
 import ctypes as C
 import glob
 import json
@@ -55,17 +57,39 @@ for path in libs:
     ys[path] = torch.empty((S, F * H), device="cuda")
 
 stream = torch.cuda.current_stream()
+OP = os.environ.get("AB_OP", "roundtrip")
+R = N + 2  # floats per spectrum row
+if OP in ("stft", "istft"):
+    spec = torch.empty((S, F, R), device="cuda")
+    for p in libs:
+        L = handles[p]
+        L.crlot_stft.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_int64,
+                                 C.c_int64, C.c_void_p]
+        L.crlot_istft_ola.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64,
+                                      C.c_int64, C.c_int64, C.c_void_p]
+    assert handles[base].crlot_stft(plans[base], x.data_ptr(), spec.data_ptr(), S, T, T, F * R, R,
+                                    stream.cuda_stream) == 0
+
+
+def call(L, h, y):
+    if OP == "stft":
+        return L.crlot_stft(h, x.data_ptr(), spec.data_ptr(), S, T, T, F * R, R, stream.cuda_stream)
+    if OP == "istft":
+        return L.crlot_istft_ola(h, spec.data_ptr(), y.data_ptr(), S, F, F * R, R, F * H, stream.cuda_stream)
+    return L.crlot_roundtrip(h, x.data_ptr(), y.data_ptr(), S, T, T, F * H, stream.cuda_stream)
+
+
 times = {p: [] for p in libs}
 for rnd in range(int(os.environ.get("AB_ROUNDS", len(libs) * 2))):
     # rotate the order each round: the first slot of a round can run 2-4 % slow
     for p in libs[rnd % len(libs):] + libs[:rnd % len(libs)]:
         L, h, y = handles[p], plans[p], ys[p]
         for _ in range(2):
-            L.crlot_roundtrip(h, x.data_ptr(), y.data_ptr(), S, T, T, F * H, stream.cuda_stream)
+            call(L, h, y)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
-            L.crlot_roundtrip(h, x.data_ptr(), y.data_ptr(), S, T, T, F * H, stream.cuda_stream)
+            call(L, h, y)
         e1.record()
         torch.cuda.synchronize()
         times[p].append(e0.elapsed_time(e1) / 5)
@@ -74,6 +98,6 @@ for p in libs:
     t = sorted(times[p])
     same = bool(torch.equal(ys[p], ref))
     maxd = float((ys[p] - ref).abs().max())
-    print(json.dumps({"lib": os.path.relpath(p, ROOT), "ms_median": round(t[len(t) // 2], 4),
+    print(json.dumps({"lib": os.path.relpath(p, ROOT), "op": OP, "ms_median": round(t[len(t) // 2], 4),
                       "ms_min": round(t[0], 4), "Msamples_s": round(S * T / t[len(t) // 2] / 1e3, 1),
                       "bitexact_vs_base": same, "maxdiff": maxd}))
