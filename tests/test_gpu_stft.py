@@ -339,19 +339,28 @@ def test_framequeue_pipeline_masked(pkg, oracle, torch_cuda):
         assert_close(y[s], ref, 0.5, f"framequeue stream {s}")
 
 
-def test_short_and_empty_streams(pkg, oracle, torch_cuda):
+@pytest.mark.parametrize("n,h", [(1024, 256), (4096, 1024), (2048, 256)])
+def test_short_and_empty_streams(pkg, oracle, torch_cuda, n, h):
+    """Streams of one or two frames, a hop either side of the frame edges, an
+    empty batch; the masked walk as well (one pair, a lone last frame)."""
     torch = torch_cuda
-    n, h = 1024, 256
     plan = pkg.Plan(frame_size=n, hop_size=h)
-    for T in (1, 2, 5, 255, 256, 257, 1023, 1025):
+    for T in (1, 2, 5, h - 1, h, h + 1, n - 1, n + 1):
         x = oracle.synth_streams(2, T, config_id=67)
         xd = dev(torch, x)
         spec = host(plan.stft(xd))
         y = host(plan.istft_ola(plan.stft(xd)))
+        F = plan.frame_count(T)
+        m = np.random.default_rng(T).uniform(0.0, 1.0, (F, n // 2 + 1)).astype(np.float32)
+        plan.set_spectral_mask(dev(torch, m))
+        ym = host(plan.roundtrip(xd))
+        plan.set_spectral_mask(None)
         for s in range(2):
             yr, ref = oracle.roundtrip_mask(x[s], n, h, want_spec=True)
-            assert_spec_close(spec[s], ref, f"T={T}")
-            assert_close(y[s], yr, 0.5, f"T={T}", float(np.linalg.norm(x[s])))
+            assert_spec_close(spec[s], ref, f"{n}/{h} T={T}")
+            assert_close(y[s], yr, 0.5, f"{n}/{h} T={T}", float(np.linalg.norm(x[s])))
+            assert_close(ym[s], oracle.roundtrip_mask(x[s], n, h, mask=m), 0.5, f"{n}/{h} masked T={T}",
+                         float(np.linalg.norm(x[s])))
     empty = torch.zeros((2, 0), device="cuda")
     assert plan.stft(empty).shape == (2, 0, n // 2 + 1)
 
