@@ -390,6 +390,17 @@ bool pair_mask_supported(int n, int h);
 bool pair_spec_supported(int n, int h);  // K_pair_stft / K_pair_istft: N = 1024 (H 128-512), 512 (H 128, 256),
                                          // 2048 (H 256, 512), 4096 (H 512, 1024)
 bool pair_tables(const Geometry& g, const DevTables& t);  // the tables those kernels read are there
+// ... and at N = 960 (K_pair15's transform, any hop >= 32 with ring_len % H == 0; pair15_spec.hip)
+bool pair15_spec_supported(int n, int h, int ring_len);
+hipError_t launch_pair15_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
+                              int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
+                              hipStream_t stream);
+hipError_t launch_pair15_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
+                               int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
+                               hipStream_t stream);
+hipError_t launch_pair15_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
+                                int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
+                                hipStream_t stream);
 // crlot_stft / crlot_istft_ola as frame pairs (K_pair_stft / K_pair_istft, pair_stft.hip:
 // N = 1024, H = 128 / 256 / 512, the pair tables; within float32 rounding of the per-frame kernels)
 hipError_t launch_pair_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,

@@ -290,12 +290,14 @@ def test_masked_roundtrip_chunking_and_fallbacks(pkg, oracle, torch_cuda, n, h):
 @pytest.mark.parametrize("n,h", [(960, 240), (882, 441), (1024, 200), (480, 120), (1000, 250)])
 def test_other_sizes(pkg, oracle, torch_cuda, n, h):
     """Frame sizes / hops outside the walkers: the staged forms (windowed frames ->
-    mixed-radix rfft; spectral step -> irfft -> gather) against the oracle."""
+    mixed-radix rfft; spectral step -> irfft -> gather) against the oracle (frame
+    pairing off: 960 has frame-pair kernels, test_pair15_spectral_entries)."""
     torch = torch_cuda
     S, T = 3, 12 * n + 13
     bins = n // 2 + 1
     x = special(oracle.synth_streams(S, T, config_id=65))
     plan = pkg.Plan(frame_size=n, hop_size=h)
+    plan.set_frame_pairing(False)
     xd = dev(torch, x)
     spec = plan.stft(xd)
     F = spec.shape[1]
@@ -510,7 +512,7 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
     torch = torch_cuda
     rng = np.random.default_rng(1000 + seed)
     n, h = [(1024, 256), (1024, 128), (1024, 512), (512, 128), (512, 256), (2048, 512), (256, 128),
-            (4096, 1024)][int(rng.integers(8))]
+            (4096, 1024), (960, 240), (960, 320)][int(rng.integers(10))]
     mode = int(rng.integers(3))
     kw = dict(center=bool(rng.integers(2)), pad_mode=int(rng.integers(3))) if mode == 2 else {}
     S = int(rng.integers(1, 6))
@@ -547,3 +549,94 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
                                 pad_mode=kw.get("pad_mode", 0))
     assert_close(ysf[0], ref, max(finite_scale(ref)[0], 1e-30), f"{n}/{h} mode {mode} vs oracle",
                  finite_scale(ref)[1])
+
+
+@pytest.mark.parametrize("h", [240, 480, 320, 100])
+def test_pair15_spectral_entries(pkg, oracle, torch_cuda, h):
+    """N = 960 (20 ms at 48 kHz) frame pairs on K_pair15's transform (any hop):
+    crlot_stft, crlot_istft_ola and the masked round trip vs the oracle and vs the
+    per-frame staged forms (frame pairing off) within the FFT tolerance, with NaN /
+    Inf / tiny / huge samples (the per-frame regime), edited spectra and signed /
+    NaN / huge mask values; the bits do not depend on the chunking; odd F."""
+    torch = torch_cuda
+    n, S = 960, 3
+    T = 21 * n + 37
+    bins = n // 2 + 1
+    x = special(oracle.synth_streams(S, T, config_id=71))
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    F = plan.frame_count(T)
+    xd = dev(torch, x)
+    spec = plan.stft(xd)
+    assert plan.last_launch()["kernels"] == ["k_pair_stft"]
+    sh = host(spec)
+    for c in (1, 3, F):
+        plan.set_chunks(c)
+        assert np.array_equal(bits(host(plan.stft(xd)).view(np.float32)), bits(sh.view(np.float32))), c
+    plan.set_chunks(0)
+    plan.set_frame_pairing(False)
+    spf = host(plan.stft(xd))
+    plan.set_frame_pairing(True)
+    for s in range(S):
+        _, ref = oracle.roundtrip_mask(x[s], n, h, want_spec=True)
+        assert_spec_close(sh[s], ref, f"960/{h} pair stft stream {s}")
+        assert_spec_close(sh[s], spf[s], f"960/{h} pair vs per-frame stft stream {s}")
+        assert np.all(sh[s][:, 0].imag == 0) and np.all(sh[s][:, -1].imag == 0)
+    # the inverse: gain, signed mask, edited spectra that leave the paired regime
+    rng = np.random.default_rng(h)
+    gain = np.linspace(0.5, 1.5, bins).astype(np.float32)
+    m = rng.uniform(-1.0, 1.5, (S, F, bins)).astype(np.float32)
+    se = sh.copy()
+    se[1, 3, 17] = np.nan
+    se[2, 8, 100] = np.inf
+    se[2, F - 1, 5] = 1e25
+    sed = dev(torch, se)
+    for g, mm in ((None, None), (gain, None), (gain, m)):
+        plan.set_spectral_gain(g)
+        plan.set_spectral_mask(None if mm is None else dev(torch, mm))
+        y = host(plan.istft_ola(sed))
+        assert plan.last_launch()["kernels"] == ["k_pair_istft"]
+        for c in (1, 3, F):
+            plan.set_chunks(c)
+            assert np.array_equal(bits(host(plan.istft_ola(sed))), bits(y)), c
+        plan.set_chunks(0)
+        plan.set_frame_pairing(False)
+        ypf = host(plan.istft_ola(sed))
+        plan.set_frame_pairing(True)
+        assert np.all(np.isfinite(y))
+        for s in range(S):
+            ymax, ynorm = finite_scale(ypf[s])
+            assert_close(y[s], ypf[s], ymax, f"960/{h} pair vs per-frame istft stream {s}", ynorm)
+    plan.set_spectral_gain(None)
+    # the masked round trip: one walk, vs the oracle's masked loop and the per-frame form
+    m[..., ::13] = 0.0
+    m[1, 5, 40] = np.nan
+    m[1, 9, :] = 1e-30
+    m[2, 2, 100] = 1e25
+    m[0, F - 1, 3] = 2.0 ** 21
+    plan.set_spectral_mask(dev(torch, m))
+    plan.set_spectral_gain(gain)
+    y = host(plan.roundtrip(xd))
+    assert plan.last_launch()["kernels"] == ["k_pair_mask"]
+    for c in (1, 2, 5, F):
+        plan.set_chunks(c)
+        assert np.array_equal(bits(host(plan.roundtrip(xd))), bits(y)), c
+    plan.set_chunks(0)
+    plan.set_frame_pairing(False)
+    yf = host(plan.roundtrip(xd))
+    plan.set_frame_pairing(True)
+    for s in range(S):
+        ref = oracle.roundtrip_mask(x[s], n, h, bin_gain=gain, mask=m[s])
+        ymax, ynorm = finite_scale(ref)
+        assert_close(y[s], ref, ymax, f"960/{h} pair mask stream {s}", ynorm)
+        assert_close(y[s], yf[s], ymax, f"960/{h} pair vs per-frame mask stream {s}", ynorm)
+    plan.set_spectral_mask(None)
+    plan.set_spectral_gain(None)
+    # plain input: the split round trip vs the fused one and the oracle
+    xp = oracle.synth_streams(S, T, config_id=72)
+    xpd = dev(torch, xp)
+    y2 = host(plan.istft_ola(plan.stft(xpd)))
+    yr = host(plan.roundtrip(xpd))
+    for s in range(S):
+        ref = oracle.roundtrip(xp[s], n, h)
+        assert_close(y2[s], ref, 0.5, f"960/{h} pair split vs oracle stream {s}", float(np.linalg.norm(xp[s])))
+        assert_close(y2[s], yr[s], 0.5, f"960/{h} pair split vs roundtrip stream {s}", float(np.linalg.norm(xp[s])))

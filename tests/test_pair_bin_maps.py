@@ -45,3 +45,39 @@ def test_pair_bin_maps(n, E, q):
             idx = q(l) + 64 * d if d < E // 2 else -q(l) + n - 64 * d
             assert idx == min(kb, n - kb), (n, l, d)
             assert 0 <= idx <= n // 2
+
+
+def test_pair15_bin_map():
+    """N = 960 (csrc/fft_pair15.h pair15_bin, csrc/pair15_spec.hip q15_partner): bin
+    k1 + 15 k' in lane l, register d, k1 = (l & 3) + 4 (l >> 4) (15: the zero row),
+    k' = ((l >> 2) & 3) + 4 d; the partner N - k in register 15 - d of
+    q15_partner(l), lane 0 its own register (16 - d) mod 16; the stores of bins
+    0 .. N/2 (registers d < 8 of the bin lanes, register 8 of lane 0) each once."""
+    n = 960
+
+    def k1(l):
+        return (l & 3) + 4 * (l >> 4)
+
+    def b15(l, d):
+        return k1(l) + 15 * (((l >> 2) & 3) + 4 * d)
+
+    def partner(l):
+        j = (l >> 2) & 3
+        if k1(l) == 15:
+            return l
+        if k1(l) == 0:
+            return 0 if j == 0 else 4 * (4 - j)
+        kp = 15 - k1(l)
+        return (kp & 3) + 4 * (3 - j) + 16 * (kp >> 2)
+
+    live = [l for l in range(64) if k1(l) != 15]
+    assert len(live) == 60
+    where = {b15(l, d): (l, d) for l in live for d in range(16)}
+    assert sorted(where) == list(range(n))
+    for l in live:
+        for d in range(16):
+            want = where[(n - b15(l, d)) % n]
+            got = (0, (16 - d) % 16) if l == 0 else (partner(l), 15 - d)
+            assert got == want, (l, d)
+    stored = [b15(l, d) for l in live for d in range(8)] + [b15(0, 8)]
+    assert sorted(stored) == list(range(n // 2 + 1))
