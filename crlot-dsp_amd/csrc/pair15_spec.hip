@@ -26,7 +26,8 @@
 // finite and within 2^20) and its stepped spectra are finite and below 2^60;
 // otherwise each frame alone with the full sanitize.  The inverse output is
 // scaled and sanitized as kissfft_adapter.cc:154-163 does (o = sanit(v / N)) and
-// pushed with fma(o, ws g, ring); produce divides by the plan's den (IEEE).
+// pushed with fma(o, ws g, ring); produce divides by the plan's den (IEEE; the
+// divisors of both blocks fetched ahead when H <= 256).
 // Results equal the per-frame kissfft formulation within float32 rounding.
 #include <algorithm>
 #include <type_traits>
@@ -113,7 +114,7 @@ struct Q15Ola {
     float* ring;
     int H, RM, ring_blocks, f0;
     const float* den;
-    __amdgpu_buffer_rsrc_t ry, ry_null;
+    __amdgpu_buffer_rsrc_t ry, ry_null, rd;  // (rd: den, ring_blocks H floats)
     __device__ __forceinline__ void clear(int lane) {
         for (int i = lane; i <= RM; i += 64) ring[i] = 0.0f;
         dev::wave_lds_fence();
@@ -129,6 +130,47 @@ struct Q15Ola {
             ring[pos] = __builtin_fmaf(o, wsg[m], ring[pos]);
         }
         dev::wave_lds_fence();
+    }
+    // H <= 256: a block is at most 4 rows of the walk; its divisors are fetched
+    // before the pushes (a divisor load waits on every earlier store too: one
+    // vmcnt counter), as K_pair15's DPRE form does
+    __device__ __forceinline__ void den4(int k, float (&d)[4], int lane) const {
+        const int dbase = (k % ring_blocks) * H;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[i] = dev::bload1(rd, (lane + 64 * i) * 4, dbase * 4);  // (past the table: 0, unused)
+    }
+    __device__ __forceinline__ void produce4(int k, const float (&d)[4], int lane) {
+        const int base = k * H;
+        const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = lane + 64 * i;
+            if (j < H) {
+                const int pos = (base + j) & RM;
+                const float s = ring[pos];
+                ring[pos] = 0.0f;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s / d[i]), rk, (base + j) * 4, 0, 0);
+            }
+        }
+        dev::wave_lds_fence();
+    }
+    // a pair's two frames: push k, produce k, push k+1, produce k+1 (when k+1 < f1)
+    __device__ __forceinline__ void pair(const dev::pc (&v)[16], const float (&wsg)[kQE], float inv_n, int k, int f1,
+                                         int lane) {
+        if (H <= 256) {
+            float d0[4], d1[4];
+            den4(k, d0, lane);
+            den4(k + 1, d1, lane);
+            push<false>(v, wsg, inv_n, k, lane);
+            produce4(k, d0, lane);
+            push<true>(v, wsg, inv_n, k + 1, lane);
+            if (k + 1 < f1) produce4(k + 1, d1, lane);
+        } else {
+            push<false>(v, wsg, inv_n, k, lane);
+            produce(k, lane);
+            push<true>(v, wsg, inv_n, k + 1, lane);
+            if (k + 1 < f1) produce(k + 1, lane);
+        }
     }
     __device__ __forceinline__ void produce(int k, int lane) {
         const int base = k * H;
@@ -240,7 +282,9 @@ __device__ __forceinline__ bool q15_walk(const FusedArgs& a, int gw, int NB, Q15
 }
 
 // ------------------------------------------------------------------ K_pair_istft
-template <bool MASK>
+// PF: the next pair's rows and both blocks' divisors fetched ahead (H <= 256; 180-204
+// VGPRs, 2 waves/SIMD: +16 % at 960/240), else at use (3 waves/SIMD: +9 % at 960/480)
+template <bool MASK, bool PF>
 __global__ __launch_bounds__(64 * kQW, 2) void k_p15_istft(const PairSpecArgs pa) {
     const FusedArgs& a = pa.f;
     constexpr int N = kQN, E = kQE, P2 = kQP2, OB = P2 + 1, MI = 8;
@@ -258,6 +302,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void k_p15_istft(const PairSpecArgs pa
     ola.ring_blocks = a.ring_blocks;
     ola.f0 = w.f0;
     ola.den = a.t.den;
+    ola.rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
     ola.ry = dev::make_rsrc(a.y + int64_t(w.s) * a.ld_y, span_bytes(a.out_len, 1));
     ola.ry_null = dev::make_rsrc(a.y, 0u);
     ola.clear(lane);
@@ -269,29 +314,43 @@ __global__ __launch_bounds__(64 * kQW, 2) void k_p15_istft(const PairSpecArgs pa
     const bool live = q15_k1(lane) != 15;
     const float* sb = pa.sin + int64_t(w.s) * pa.ld_spec;
     const float* mrow0 = MASK ? pa.mask.p + int64_t(w.s) * pa.mask.ld_stream : nullptr;
-    // the pair's rows (and mask rows) by real bin kr = lane + 64 i <= N/2, coalesced;
-    // stepped -- (X g) m, re and im each; DC and Nyquist imaginary parts dropped --
-    // and staged at buf[kr] (frame k) and buf[OB + kr] (frame k+1, zeros past the last)
-    auto stage = [&](int k) -> bool {
+    // the pair's rows (and mask rows) by real bin kr = lane + 64 i <= N/2, coalesced,
+    // loaded during the previous pair's OLA stage; stepped -- (X g) m, re and im
+    // each; DC and Nyquist imaginary parts dropped -- and staged at buf[kr] (frame
+    // k) and buf[OB + kr] (frame k+1, zeros past the last)
+    float2 ra_[MI], rb_[MI];
+    float ma_[MASK ? MI : 1], mb_[MASK ? MI : 1];
+    auto load_rows = [&](int k) {
         const float2* ra = reinterpret_cast<const float2*>(sb + int64_t(k) * pa.ld_frame);
         const float2* rb = reinterpret_cast<const float2*>(sb + int64_t(k + 1) * pa.ld_frame);
         const bool two = k + 1 < a.F;
         const float* m0 = MASK ? mrow0 + int64_t(k) * pa.mask.ld_frame : nullptr;
         const float* m1 = MASK && two ? m0 + pa.mask.ld_frame : m0;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int kr = lane + 64 * i;
+            const bool on = kr <= P2;
+            ra_[i] = on ? ra[kr] : make_float2(0.f, 0.f);
+            rb_[i] = on && two ? rb[kr] : make_float2(0.f, 0.f);
+            if constexpr (MASK) {
+                ma_[i] = on ? m0[kr] : 0.f;
+                mb_[i] = on ? m1[kr] : 0.f;
+            }
+        }
+    };
+    auto stage = [&]() -> bool {
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             const int kr = lane + 64 * i;
             if (kr <= P2) {
-                const float2 xa = ra[kr], xb = two ? rb[kr] : make_float2(0.f, 0.f);
                 const float g = a.t.gain ? a.t.gain[kr] : 1.0f;
-                float ax = xa.x * g, ay = xa.y * g, bx = xb.x * g, by = xb.y * g;
+                float ax = ra_[i].x * g, ay = ra_[i].y * g, bx = rb_[i].x * g, by = rb_[i].y * g;
                 if constexpr (MASK) {
-                    const float ma = m0[kr], mb = m1[kr];
-                    ax *= ma;
-                    ay *= ma;
-                    bx *= mb;
-                    by *= mb;
+                    ax *= ma_[i];
+                    ay *= ma_[i];
+                    bx *= mb_[i];
+                    by *= mb_[i];
                 }
                 if (kr == 0 || kr == P2) ay = by = 0.0f;
                 const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(ax), __builtin_fabsf(ay)),
@@ -322,27 +381,36 @@ __global__ __launch_bounds__(64 * kQW, 2) void k_p15_istft(const PairSpecArgs pa
         }
         dev::wave_lds_fence();  // (the reads before the inverse's transpose rewrites buf)
     };
+    if (PF) load_rows(w.fs);
     for (int k = w.fs; k < w.f1; k += 2) {
         dev::pc v[16];
-        if (stage(k)) {
+        const bool more = k + 2 < w.f1;
+        if (!PF) load_rows(k);
+        if (stage()) {
             gather(v, true, 0);
             dev::pair15_inv(v, buf, tw, lane);
-            ola.push<false>(v, wsg, a.inv_n, k, lane);
-            ola.produce(k, lane);
-            ola.push<true>(v, wsg, a.inv_n, k + 1, lane);
-            if (k + 1 < w.f1) ola.produce(k + 1, lane);
+            if constexpr (PF) {
+                if (more) load_rows(k + 2);  // (in flight during the OLA stage)
+                ola.pair(v, wsg, a.inv_n, k, w.f1, lane);
+            } else {
+                ola.push<false>(v, wsg, a.inv_n, k, lane);
+                ola.produce(k, lane);
+                ola.push<true>(v, wsg, a.inv_n, k + 1, lane);
+                if (k + 1 < w.f1) ola.produce(k + 1, lane);
+            }
         } else {  // each frame alone, full sanitize (staged again for frame k+1: the inverse used buf)
             gather(v, false, 0);
             dev::pair15_inv(v, buf, tw, lane);
             ola.push<false>(v, wsg, a.inv_n, k, lane);
             ola.produce(k, lane);
             if (k + 1 < w.f1) {
-                (void)stage(k);
+                (void)stage();
                 gather(v, false, OB);
                 dev::pair15_inv(v, buf, tw, lane);
                 ola.push<false>(v, wsg, a.inv_n, k + 1, lane);
                 ola.produce(k + 1, lane);
             }
+            if (PF && more) load_rows(k + 2);
         }
     }
 }
@@ -365,6 +433,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void k_p15_mask(const PairSpecArgs pa)
     ola.ring_blocks = a.ring_blocks;
     ola.f0 = w.f0;
     ola.den = a.t.den;
+    ola.rd = dev::make_rsrc(a.t.den, uint32_t(a.ring_blocks * H) * 4u);
     ola.ry = dev::make_rsrc(a.y + int64_t(w.s) * a.ld_y, span_bytes(a.out_len, 1));
     ola.ry_null = dev::make_rsrc(a.y, 0u);
     ola.clear(lane);
@@ -441,7 +510,7 @@ __global__ __launch_bounds__(64 * kQW, 2) void k_p15_mask(const PairSpecArgs pa)
             }
             dev::wave_lds_fence();  // (the coefficient reads before the inverse's transpose rewrites buf)
             dev::pair15_inv(v, buf, tw, lane);
-            ola.push<false>(v, wsg, a.inv_n, k, lane);
+            ola.push<false>(v, wsg, a.inv_n, k, lane);  // (the divisors fetched ahead would spill here)
             ola.produce(k, lane);
             ola.push<true>(v, wsg, a.inv_n, k + 1, lane);
             if (k + 1 < w.f1) ola.produce(k + 1, lane);
@@ -553,8 +622,11 @@ hipError_t launch_pair15_istft(const Geometry& g, const DevTables& t, const Spec
     a.mask = m;
     fk::q15_chunks(a.f, F, n_streams, 48);
     const int64_t walkers = int64_t(n_streams) * a.f.n_chunks;
-    return m.p ? fk::q15_launch(fk::k_p15_istft<true>, a, walkers, CRLOT_K_PAIR_ISTFT, true, stream)
-               : fk::q15_launch(fk::k_p15_istft<false>, a, walkers, CRLOT_K_PAIR_ISTFT, true, stream);
+    if (g.h <= 256)
+        return m.p ? fk::q15_launch(fk::k_p15_istft<true, true>, a, walkers, CRLOT_K_PAIR_ISTFT, true, stream)
+                   : fk::q15_launch(fk::k_p15_istft<false, true>, a, walkers, CRLOT_K_PAIR_ISTFT, true, stream);
+    return m.p ? fk::q15_launch(fk::k_p15_istft<true, false>, a, walkers, CRLOT_K_PAIR_ISTFT, true, stream)
+               : fk::q15_launch(fk::k_p15_istft<false, false>, a, walkers, CRLOT_K_PAIR_ISTFT, true, stream);
 }
 
 // crlot_roundtrip at N = 960 with a per-frame mask, one walk
