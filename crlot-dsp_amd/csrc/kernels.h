@@ -390,8 +390,9 @@ bool pair_mask_supported(int n, int h);
 bool pair_spec_supported(int n, int h);  // K_pair_stft / K_pair_istft: N = 1024 (H 128-512), 512 (H 128, 256),
                                          // 2048 (H 256, 512), 4096 (H 512, 1024)
 bool pair_tables(const Geometry& g, const DevTables& t);  // the tables those kernels read are there
-// ... and at N = 960 (K_pair15's transform, any hop >= 32 with ring_len % H == 0; pair15_spec.hip)
+// ... and at N = 960 / 480 (K_pair15's transforms, any hop >= 32 with ring_len % H == 0; pair15_spec.hip)
 bool pair15_spec_supported(int n, int h, int ring_len);
+bool pair15_spec_fits(int n, int64_t ld, int64_t len);  // the walks' 32-bit buffer offsets cover (ld, len)
 hipError_t launch_pair15_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
                               int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
                               hipStream_t stream);

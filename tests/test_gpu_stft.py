@@ -512,7 +512,7 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
     torch = torch_cuda
     rng = np.random.default_rng(1000 + seed)
     n, h = [(1024, 256), (1024, 128), (1024, 512), (512, 128), (512, 256), (2048, 512), (256, 128),
-            (4096, 1024), (960, 240), (960, 320)][int(rng.integers(10))]
+            (4096, 1024), (960, 240), (960, 320), (480, 120)][int(rng.integers(11))]
     mode = int(rng.integers(3))
     kw = dict(center=bool(rng.integers(2)), pad_mode=int(rng.integers(3))) if mode == 2 else {}
     S = int(rng.integers(1, 6))
@@ -551,15 +551,16 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
                  finite_scale(ref)[1])
 
 
-@pytest.mark.parametrize("h", [240, 480, 320, 100])
-def test_pair15_spectral_entries(pkg, oracle, torch_cuda, h):
-    """N = 960 (20 ms at 48 kHz) frame pairs on K_pair15's transform (any hop):
+@pytest.mark.parametrize("n,h", [(960, 240), (960, 480), (960, 320), (960, 100), (480, 120), (480, 240), (480, 100)])
+def test_pair15_spectral_entries(pkg, oracle, torch_cuda, n, h):
+    """N = 960 / 480 (20 / 10 ms at 48 kHz) frame pairs on K_pair15's transforms (any
+    hop; at 480 the two halves of a wave walk two streams, an odd stream count here):
     crlot_stft, crlot_istft_ola and the masked round trip vs the oracle and vs the
     per-frame staged forms (frame pairing off) within the FFT tolerance, with NaN /
     Inf / tiny / huge samples (the per-frame regime), edited spectra and signed /
     NaN / huge mask values; the bits do not depend on the chunking; odd F."""
     torch = torch_cuda
-    n, S = 960, 3
+    S = 3
     T = 21 * n + 37
     bins = n // 2 + 1
     x = special(oracle.synth_streams(S, T, config_id=71))
@@ -578,8 +579,8 @@ def test_pair15_spectral_entries(pkg, oracle, torch_cuda, h):
     plan.set_frame_pairing(True)
     for s in range(S):
         _, ref = oracle.roundtrip_mask(x[s], n, h, want_spec=True)
-        assert_spec_close(sh[s], ref, f"960/{h} pair stft stream {s}")
-        assert_spec_close(sh[s], spf[s], f"960/{h} pair vs per-frame stft stream {s}")
+        assert_spec_close(sh[s], ref, f"{n}/{h} pair stft stream {s}")
+        assert_spec_close(sh[s], spf[s], f"{n}/{h} pair vs per-frame stft stream {s}")
         assert np.all(sh[s][:, 0].imag == 0) and np.all(sh[s][:, -1].imag == 0)
     # the inverse: gain, signed mask, edited spectra that leave the paired regime
     rng = np.random.default_rng(h)
@@ -605,7 +606,7 @@ def test_pair15_spectral_entries(pkg, oracle, torch_cuda, h):
         assert np.all(np.isfinite(y))
         for s in range(S):
             ymax, ynorm = finite_scale(ypf[s])
-            assert_close(y[s], ypf[s], ymax, f"960/{h} pair vs per-frame istft stream {s}", ynorm)
+            assert_close(y[s], ypf[s], ymax, f"{n}/{h} pair vs per-frame istft stream {s}", ynorm)
     plan.set_spectral_gain(None)
     # the masked round trip: one walk, vs the oracle's masked loop and the per-frame form
     m[..., ::13] = 0.0
@@ -627,8 +628,8 @@ def test_pair15_spectral_entries(pkg, oracle, torch_cuda, h):
     for s in range(S):
         ref = oracle.roundtrip_mask(x[s], n, h, bin_gain=gain, mask=m[s])
         ymax, ynorm = finite_scale(ref)
-        assert_close(y[s], ref, ymax, f"960/{h} pair mask stream {s}", ynorm)
-        assert_close(y[s], yf[s], ymax, f"960/{h} pair vs per-frame mask stream {s}", ynorm)
+        assert_close(y[s], ref, ymax, f"{n}/{h} pair mask stream {s}", ynorm)
+        assert_close(y[s], yf[s], ymax, f"{n}/{h} pair vs per-frame mask stream {s}", ynorm)
     plan.set_spectral_mask(None)
     plan.set_spectral_gain(None)
     # plain input: the split round trip vs the fused one and the oracle
@@ -638,5 +639,5 @@ def test_pair15_spectral_entries(pkg, oracle, torch_cuda, h):
     yr = host(plan.roundtrip(xpd))
     for s in range(S):
         ref = oracle.roundtrip(xp[s], n, h)
-        assert_close(y2[s], ref, 0.5, f"960/{h} pair split vs oracle stream {s}", float(np.linalg.norm(xp[s])))
-        assert_close(y2[s], yr[s], 0.5, f"960/{h} pair split vs roundtrip stream {s}", float(np.linalg.norm(xp[s])))
+        assert_close(y2[s], ref, 0.5, f"{n}/{h} pair split vs oracle stream {s}", float(np.linalg.norm(xp[s])))
+        assert_close(y2[s], yr[s], 0.5, f"{n}/{h} pair split vs roundtrip stream {s}", float(np.linalg.norm(xp[s])))
