@@ -81,3 +81,35 @@ def test_pair15_bin_map():
             assert got == want, (l, d)
     stored = [b15(l, d) for l in live for d in range(8)] + [b15(0, 8)]
     assert sorted(stored) == list(range(n // 2 + 1))
+
+
+def test_pair15h_bin_map():
+    """N = 480 (csrc/fft_pair15.h pair15h_bin, csrc/pair15_spec.hip Q15<32>::partner):
+    half-lane h holds bin k1 + 15 (c + 2 e), k1 = (h & 7) + 8 (h >> 4) (15: the zero
+    row), c = (h >> 3) & 1; the partner N - k in register 15 - e of partner(h)
+    (half-lane 0: its own register (16 - e) mod 16); bins 0 .. N/2 stored once."""
+    n = 480
+
+    def k1(h):
+        return (h & 7) + 8 * (h >> 4)
+
+    def b(h, e):
+        return k1(h) + 15 * (((h >> 3) & 1) + 2 * e)
+
+    def partner(h):
+        if k1(h) in (0, 15):
+            return h
+        c, kp = (h >> 3) & 1, 15 - k1(h)
+        return (kp & 7) + 8 * (1 - c) + 16 * (kp >> 3)
+
+    live = [h for h in range(32) if k1(h) != 15]
+    assert len(live) == 30
+    where = {b(h, e): (h, e) for h in live for e in range(16)}
+    assert sorted(where) == list(range(n))
+    for h in live:
+        for e in range(16):
+            want = where[(n - b(h, e)) % n]
+            got = (0, (16 - e) % 16) if h == 0 else (partner(h), 15 - e)
+            assert got == want, (h, e)
+    stored = [b(h, e) for h in live for e in range(8)] + [b(0, 8)]
+    assert sorted(stored) == list(range(n // 2 + 1))
