@@ -1047,6 +1047,12 @@ int stft_impl(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams,
         e = crlot::launch_pair15_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft (frame pairs, N = 960 / 480) kernel launch");
     }
+    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptw && t.wa &&
+        aligned4(d_x) && T < (int64_t(1) << 27)) {
+        // K_pairN's one-wave sizes (882, 1000, 640, 400, 320) as frame pairs (pairing off: the mixed-radix rfft below)
+        e = crlot::launch_pairn_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft (frame pairs, K_pairN sizes) kernel launch");
+    }
     if (!p->generic && crlot::stft_supported(p->geo.n)) {
         e = crlot::launch_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft kernel launch");
@@ -1086,6 +1092,12 @@ int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams
         // N = 960 / 480 frame pairs (pairing off: the staged irfft + gather below)
         e = crlot::launch_pair15_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft (frame pairs, N = 960 / 480) kernel launch");
+    }
+    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptw && t.ws && t.den &&
+        aligned4(d_y) && F * p->geo.h + p->geo.n < (int64_t(1) << 27)) {
+        // K_pairN's one-wave sizes as frame pairs (pairing off: the staged irfft + gather below)
+        e = crlot::launch_pairn_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft (frame pairs, K_pairN sizes) kernel launch");
     }
     if (istft_walk_ok(p, d_y, ld_y)) {
         e = crlot::launch_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
@@ -1131,6 +1143,13 @@ static int masked_roundtrip(crlot_plan* p, crlot::Scratch* sc, const float* d_x,
         const hipError_t e = crlot::launch_pair15_masked(p->geo, t, p->mask, d_x, d_y, n_streams, T, ld_x, ld_y, F,
                                                          out_len, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "masked frame-pair kernel launch (N = 960 / 480)");
+    }
+    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptw && t.wa && t.ws &&
+        t.den && aligned4(d_x) && aligned4(d_y) && T < (int64_t(1) << 27) && out_len + p->geo.n < (int64_t(1) << 27)) {
+        // K_pairN's one-wave sizes as frame pairs, one walk (pairing off: spectra through HBM below)
+        const hipError_t e = crlot::launch_pairn_masked(p->geo, t, p->mask, d_x, d_y, n_streams, T, ld_x, ld_y, F,
+                                                        out_len, s);
+        return e == hipSuccess ? CRLOT_OK : hip_fail(e, "masked frame-pair kernel launch (K_pairN sizes)");
     }
     if (masked_walk_ok(p, d_y, ld_y)) {
         const hipError_t e = crlot::launch_roundtrip_masked(p->geo, tables(p), p->mask, d_x, d_y, n_streams, T, ld_x,

@@ -393,6 +393,17 @@ bool pair_tables(const Geometry& g, const DevTables& t);  // the tables those ke
 // ... and at N = 960 / 480 (K_pair15's transforms, any hop >= 32 with ring_len % H == 0; pair15_spec.hip)
 bool pair15_spec_supported(int n, int h, int ring_len);
 bool pair15_spec_fits(int n, int64_t ld, int64_t len);  // the walks' 32-bit buffer offsets cover (ld, len)
+// ... and at K_pairN's one-wave sizes 882, 1000, 640, 400, 320 (pairn_spec.hip)
+bool pairn_spec_supported(int n, int h, int ring_len);
+hipError_t launch_pairn_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
+                             int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
+                             hipStream_t stream);
+hipError_t launch_pairn_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
+                              int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
+                              hipStream_t stream);
+hipError_t launch_pairn_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
+                               int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
+                               hipStream_t stream);
 hipError_t launch_pair15_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
                               int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
                               hipStream_t stream);

@@ -291,7 +291,7 @@ def test_masked_roundtrip_chunking_and_fallbacks(pkg, oracle, torch_cuda, n, h):
 def test_other_sizes(pkg, oracle, torch_cuda, n, h):
     """Frame sizes / hops outside the walkers: the staged forms (windowed frames ->
     mixed-radix rfft; spectral step -> irfft -> gather) against the oracle (frame
-    pairing off: 960 has frame-pair kernels, test_pair15_spectral_entries)."""
+    pairing off: these sizes have frame-pair kernels, test_anysize_pair_spectral_entries)."""
     torch = torch_cuda
     S, T = 3, 12 * n + 13
     bins = n // 2 + 1
@@ -512,7 +512,7 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
     torch = torch_cuda
     rng = np.random.default_rng(1000 + seed)
     n, h = [(1024, 256), (1024, 128), (1024, 512), (512, 128), (512, 256), (2048, 512), (256, 128),
-            (4096, 1024), (960, 240), (960, 320), (480, 120)][int(rng.integers(11))]
+            (4096, 1024), (960, 240), (960, 320), (480, 120), (882, 441)][int(rng.integers(12))]
     mode = int(rng.integers(3))
     kw = dict(center=bool(rng.integers(2)), pad_mode=int(rng.integers(3))) if mode == 2 else {}
     S = int(rng.integers(1, 6))
@@ -551,10 +551,12 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
                  finite_scale(ref)[1])
 
 
-@pytest.mark.parametrize("n,h", [(960, 240), (960, 480), (960, 320), (960, 100), (480, 120), (480, 240), (480, 100)])
-def test_pair15_spectral_entries(pkg, oracle, torch_cuda, n, h):
-    """N = 960 / 480 (20 / 10 ms at 48 kHz) frame pairs on K_pair15's transforms (any
-    hop; at 480 the two halves of a wave walk two streams, an odd stream count here):
+@pytest.mark.parametrize("n,h", [(960, 240), (960, 480), (960, 320), (960, 100), (480, 120), (480, 240), (480, 100),
+                                 (882, 441), (882, 220), (1000, 250), (640, 320), (400, 160), (320, 160)])
+def test_anysize_pair_spectral_entries(pkg, oracle, torch_cuda, n, h):
+    """The any-size frame pairs: N = 960 / 480 (20 / 10 ms at 48 kHz) on K_pair15's
+    transforms (at 480 the two halves of a wave walk two streams, an odd stream
+    count here) and 882 (20 ms at 44.1 kHz), 1000, 640, 400, 320 on K_pairN's (any hop):
     crlot_stft, crlot_istft_ola and the masked round trip vs the oracle and vs the
     per-frame staged forms (frame pairing off) within the FFT tolerance, with NaN /
     Inf / tiny / huge samples (the per-frame regime), edited spectra and signed /
