@@ -686,7 +686,10 @@ int wg_per_cu(K kernel) {
 
 }  // namespace
 
-bool pair_wg_supported(int n, int h) { return (n == 4096 && (h == 512 || h == 1024)) || (n == 2048 && (h == 256 || h == 512)); }
+// N = 4096: H 512, 1024, 2048; N = 2048: H 256, 512, 1024 (SH = H / L = 2, 4, 8)
+bool pair_wg_supported(int n, int h) {
+    return (n == 4096 && (h == 512 || h == 1024 || h == 2048)) || (n == 2048 && (h == 256 || h == 512 || h == 1024));
+}
 
 int pair_wg_walkers_per_cu(int n) {
     static const int v4 = wg_per_cu<W4k>(k_pairwg_mask<W4k, 4, 4, false>);
@@ -697,16 +700,21 @@ int pair_wg_walkers_per_cu(int n) {
 hipError_t launch_pairwg_stft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
     if (!pair_wg_supported(n, h) || !a.f.t.ptw4 || !a.f.t.wa) return hipErrorInvalidValue;
     note_launch(CRLOT_K_PAIR_STFT, walkers);
-    if (n == 4096) return h == 512 ? launch_wg<W4k>(k_pairwg_stft<W4k, 2>, a, walkers, stream)
-                                   : launch_wg<W4k>(k_pairwg_stft<W4k, 4>, a, walkers, stream);
-    return h == 256 ? launch_wg<W2k>(k_pairwg_stft<W2k, 2>, a, walkers, stream)
-                    : launch_wg<W2k>(k_pairwg_stft<W2k, 4>, a, walkers, stream);
+    auto go = [&](auto g) {
+        using G = decltype(g);
+        const int sh = h / G::L;
+        return sh == 2 ? launch_wg<G>(k_pairwg_stft<G, 2>, a, walkers, stream)
+                       : sh == 4 ? launch_wg<G>(k_pairwg_stft<G, 4>, a, walkers, stream)
+                                 : launch_wg<G>(k_pairwg_stft<G, 8>, a, walkers, stream);
+    };
+    return n == 4096 ? go(W4k{}) : go(W2k{});
 }
 
 template <typename G, bool MASK>
 hipError_t pairwg_istft_m(int sh, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
-    return sh == 2 ? launch_wg<G>(k_pairwg_istft<G, 2, 8, MASK>, a, walkers, stream)
-                   : launch_wg<G>(k_pairwg_istft<G, 4, 4, MASK>, a, walkers, stream);
+    return sh == 2   ? launch_wg<G>(k_pairwg_istft<G, 2, 8, MASK>, a, walkers, stream)
+           : sh == 4 ? launch_wg<G>(k_pairwg_istft<G, 4, 4, MASK>, a, walkers, stream)
+                     : launch_wg<G>(k_pairwg_istft<G, 8, 2, MASK>, a, walkers, stream);
 }
 
 hipError_t launch_pairwg_istft(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
@@ -724,8 +732,9 @@ hipError_t launch_pairwg_istft(int n, int h, const PairSpecArgs& a, int64_t walk
 
 template <typename G, bool GAIN>
 hipError_t pairwg_mask_g(int sh, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {
-    return sh == 2 ? launch_wg<G>(k_pairwg_mask<G, 2, 8, GAIN>, a, walkers, stream)
-                   : launch_wg<G>(k_pairwg_mask<G, 4, 4, GAIN>, a, walkers, stream);
+    return sh == 2   ? launch_wg<G>(k_pairwg_mask<G, 2, 8, GAIN>, a, walkers, stream)
+           : sh == 4 ? launch_wg<G>(k_pairwg_mask<G, 4, 4, GAIN>, a, walkers, stream)
+                     : launch_wg<G>(k_pairwg_mask<G, 8, 2, GAIN>, a, walkers, stream);
 }
 
 hipError_t launch_pairwg_mask(int n, int h, const PairSpecArgs& a, int64_t walkers, hipStream_t stream) {

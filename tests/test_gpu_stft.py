@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(1024, 256), (4096, 1024), (512, 128)]
 # the spectral entries as frame pairs (K_pair_stft / K_pair_istft, frame pairing on: the default)
 PAIR_SPEC = {(1024, 128), (1024, 256), (1024, 512), (512, 128), (512, 256),
-             (2048, 256), (2048, 512), (4096, 512), (4096, 1024)}  # (N >= 2048: one workgroup per walk)
+             (2048, 256), (2048, 512), (2048, 1024), (4096, 512), (4096, 1024), (4096, 2048)}  # (N >= 2048: one workgroup per walk)
 
 
 def assert_spec_close(X, ref, what=""):

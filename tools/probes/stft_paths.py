@@ -32,11 +32,12 @@ def main():
         [(256, 128), (512, 128), (1024, 256), (2048, 512), (4096, 1024)]
     for n, h in shapes:
         plan = pkg.Plan(frame_size=n, hop_size=h)
+        plan.set_frame_pairing(os.environ.get("PROBE_PAIRING", "1") == "1")  # (0: the per-frame / staged forms)
         F, bins = plan.frame_count(T), n // 2 + 1
         spec = torch.empty((S, F, bins), dtype=torch.complex64, device="cuda")
         y = torch.empty((S, F * h), device="cuda")
         yo = torch.empty((S, F * h + 1), device="cuda")
-        r = {"n": n, "h": h}
+        r = {"n": n, "h": h, "pairing": os.environ.get("PROBE_PAIRING", "1") == "1"}
         r["stft_ms"] = ev(lambda: plan.stft(x, spec))
         r["istft_walk_ms"] = ev(lambda: plan.istft_ola(spec, y))
         r["istft_staged_ms"] = ev(lambda: plan.istft_ola(spec, yo[:, :F * h]))
