@@ -1,17 +1,19 @@
 // pairn_spec.hip -- the spectral entries and the masked round trip as frame
-// pairs at K_pairN's one-wave sizes: 882 (20 ms at 44.1 kHz), 1000, 640, 400,
-// 320, any hop H >= 32 whose ring the plan allows:
+// pairs at K_pairN's sizes 882 (20 ms at 44.1 kHz), 1000, 640, 400, 320 (one wave
+// per transform) and 1764 (40 ms at 44.1 kHz; two waves, one walk per
+// workgroup), any hop H >= 32 whose ring the plan allows:
 //   K_pair_stft   k_pn_stft<K>        (crlot_stft)
 //   K_pair_istft  k_pn_istft<K,MASK>  (crlot_istft_ola)
 //   K_pair_mask   k_pn_mask<K>        (crlot_roundtrip with a per-frame mask)
 // on fft_pairn.h's transform (compile-time Stockham passes over composite
-// radices in one LDS buffer per wave, natural order in and out), one walk per
-// wave, frames loaded whole and the overlap-add in a per-walk LDS ring, as K_pairN
-// (pair_n.hip).
+// radices in one LDS buffer per transform, natural order in and out), frames
+// loaded whole and the overlap-add in a per-walk LDS ring, as K_pairN
+// (pair_n.hip).  At 1764 the transform spans the two waves of a workgroup (its
+// fences are barriers) and the regime verdicts are shared through LDS.
 //
 // The spectrum of the pair z = a w + i b w is in natural order in the wave's
 // buffer after the forward passes, so each lane works on its own real bins
-// kr = t + 64 i <= N/2 and their partners N - kr, with no bin map:
+// kr = t + L i <= N/2 and their partners N - kr, with no bin map:
 //   stft:  A[k] = (Z[k] + conj Z[-k]) / 2, B[k] = (Z[k] - conj Z[-k]) / 2i;
 //   istft: Z[k] = A' + i B' and Z[N-k] = conj A' + i conj B' written from the
 //          stepped rows, then the inverse passes;
@@ -34,14 +36,16 @@ namespace fk {
 
 namespace {
 
-constexpr int kNW = 4;  // walks (waves) per workgroup
+constexpr int kNW = 4;  // waves per workgroup at the one-wave sizes (one walk each)
 
 template <int K>
 struct QN {
-    static constexpr int N = K % 100000, E = (N + 63) / 64, LAST = N - 64 * (E - 1), P2 = N / 2;
-    static constexpr int IB = (P2 + 1 + 63) / 64;  // natural real-bin rows per lane
+    static constexpr int N = K % 100000, L = dev::pn_lanes(K);  // lanes per transform
+    static constexpr int WALKS = L == 64 ? kNW : 1, THREADS = WALKS * L;  // per workgroup
+    static constexpr int E = (N + L - 1) / L, LAST = N - L * (E - 1), P2 = N / 2;
+    static constexpr int IB = (P2 + 1 + L - 1) / L;  // natural real-bin rows per lane
     static constexpr dev::PnFac FAC = dev::pn_factor(K);
-    static_assert(FAC.rest == 1 && dev::pn_lanes(K) == 64 && N % 2 == 0, "one-wave plan of an even N");
+    static_assert(FAC.rest == 1 && N % 2 == 0, "a plan of an even N");
     static __device__ __forceinline__ bool valid(int m, int t) { return m + 1 < E || t < LAST; }
     static __device__ __forceinline__ void fwd(dev::pc* buf, const dev::pc* tw, int t) {
         dev::pn_passes<false, K, 0, FAC.n>(buf, tw, dev::pn_opaque(t));
@@ -57,35 +61,53 @@ __host__ __device__ inline int qn_ring(int n, int h) {
     while (r < span) r <<= 1;
     return r;
 }
-// LDS: [twiddles tw_len cf] | per wave [buffer N cf] | per wave [ring RL f] (synthesis kernels)
-struct QNLds {
-    static size_t tw(int tw_len) { return sizeof(dev::pc) * size_t(tw_len); }
-    static size_t bytes(int n, int tw_len, int h, bool ring) {
-        return tw(tw_len) + sizeof(dev::pc) * size_t(n) * kNW + (ring ? sizeof(float) * qn_ring(n, h) * kNW : 0);
-    }
-};
+// LDS: [twiddles tw_len cf] | per walk [buffer N cf] | per walk [ring RL f]
+// (synthesis kernels) | the verdicts of the walk's waves (two-wave walks)
+template <int K>
+size_t qn_lds(int h, bool ring) {
+    using G = QN<K>;
+    return sizeof(dev::pc) * size_t(G::FAC.tw_len + G::WALKS * G::N) +
+           (ring ? sizeof(float) * qn_ring(G::N, h) * G::WALKS : 0) + 16;
+}
 
 template <int K>
 struct QNSmem {
     dev::pc* tw;
     dev::pc* buf;
     float* ring;
-    __device__ QNSmem(char* smem, int wave, int RL) {
-        constexpr int N = QN<K>::N, TL = QN<K>::FAC.tw_len;
+    uint32_t* votes;
+    __device__ QNSmem(char* smem, int pw, int RL) {
+        using G = QN<K>;
         tw = reinterpret_cast<dev::pc*>(smem);
-        buf = tw + TL + wave * N;
-        ring = reinterpret_cast<float*>(tw + TL + kNW * N) + wave * RL;
+        buf = tw + G::FAC.tw_len + pw * G::N;
+        float* rings = reinterpret_cast<float*>(tw + G::FAC.tw_len + G::WALKS * G::N);
+        ring = rings + pw * RL;
+        votes = reinterpret_cast<uint32_t*>(rings + G::WALKS * RL);
+    }
+    // the walk's verdict: the wave's ballot (one-wave walks), or both waves' (two-wave
+    // walks: posted in LDS between barriers, which the transform's fences are anyway)
+    __device__ __forceinline__ bool all(bool wave_ok) const {
+        if constexpr (QN<K>::L == 64) {
+            return wave_ok;
+        } else {
+            const int wave = threadIdx.x >> 6;
+            if ((threadIdx.x & 63) == 0) votes[wave] = wave_ok ? 1u : 0u;
+            __syncthreads();
+            const bool r = (votes[0] & votes[1]) != 0u;
+            __syncthreads();  // (both read before the next post)
+            return r;
+        }
     }
 };
 // the plan's pass twiddles into LDS (the whole workgroup), then a barrier
 template <int K>
 __device__ __forceinline__ void qn_stage_tw(dev::pc* tw, const float* g) {
     const dev::pc* gp = reinterpret_cast<const dev::pc*>(g);
-    for (int i = threadIdx.x; i < QN<K>::FAC.tw_len; i += 64 * kNW) tw[i] = gp[i];
+    for (int i = threadIdx.x; i < QN<K>::FAC.tw_len; i += QN<K>::THREADS) tw[i] = gp[i];
     __syncthreads();
 }
 
-// frame at `origin`: x[origin + t + 64 m] (m < E, the last row partial), the
+// frame at `origin`: x[origin + t + L m] (m < E, the last row partial), the
 // plan's padding outside [0, T)
 template <int K>
 __device__ __forceinline__ void qn_load(float (&f)[QN<K>::E], __amdgpu_buffer_rsrc_t rx, int t, int origin, int T,
@@ -93,10 +115,11 @@ __device__ __forceinline__ void qn_load(float (&f)[QN<K>::E], __amdgpu_buffer_rs
     using G = QN<K>;
     if (origin >= 0 && origin + G::N <= T) {
 #pragma unroll
-        for (int m = 0; m < G::E; ++m) f[m] = G::valid(m, t) ? dev::bload1(rx, (origin + t) * 4 + m * 256, 0) : 0.0f;
+        for (int m = 0; m < G::E; ++m)
+            f[m] = G::valid(m, t) ? dev::bload1(rx, (origin + t) * 4 + m * (4 * G::L), 0) : 0.0f;
     } else {
 #pragma unroll
-        for (int m = 0; m < G::E; ++m) f[m] = G::valid(m, t) ? fetch_x(rx, origin + t + 64 * m, T, mode) : 0.0f;
+        for (int m = 0; m < G::E; ++m) f[m] = G::valid(m, t) ? fetch_x(rx, origin + t + G::L * m, T, mode) : 0.0f;
     }
 }
 template <int E>
@@ -115,14 +138,14 @@ __device__ __forceinline__ bool qn_ok(const float (&f)[E], float lo, float hi) {
 // block k (ring / den, clear; stored when k >= f0).
 template <int K>
 struct QNOla {
-    static constexpr int N = QN<K>::N, E = QN<K>::E;
+    static constexpr int N = QN<K>::N, E = QN<K>::E, L = QN<K>::L;
     float* ring;
     int H, RM, ring_blocks, f0, t;
     const float* den;
     __amdgpu_buffer_rsrc_t ry, ry_null;
     __device__ __forceinline__ void clear() {
-        for (int i = t; i <= RM; i += 64) ring[i] = 0.0f;
-        dev::wave_lds_fence();
+        for (int i = t; i <= RM; i += L) ring[i] = 0.0f;
+        dev::pn_fence<K>();
     }
     template <bool IMAG>
     __device__ __forceinline__ void push(const dev::pc* buf, const float (&wsg)[E], float inv_n, int k) {
@@ -130,25 +153,25 @@ struct QNOla {
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             if (QN<K>::valid(m, t)) {
-                const dev::pc v = buf[t + 64 * m];
-                const int pos = (base + 64 * m) & RM;
+                const dev::pc v = buf[t + L * m];
+                const int pos = (base + L * m) & RM;
                 const float o = dev::sanit((IMAG ? v.y : v.x) * inv_n);
                 ring[pos] = __builtin_fmaf(o, wsg[m], ring[pos]);
             }
         }
-        dev::wave_lds_fence();
+        dev::pn_fence<K>();
     }
     __device__ __forceinline__ void produce(int k) {
         const int base = k * H;
         const float* dk = den + (k % ring_blocks) * H;
         const __amdgpu_buffer_rsrc_t rk = k >= f0 ? ry : ry_null;
-        for (int j = t; j < H; j += 64) {
+        for (int j = t; j < H; j += L) {
             const int pos = (base + j) & RM;
             const float s = ring[pos];
             ring[pos] = 0.0f;
             __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, s / dk[j]), rk, (base + j) * 4, 0, 0);
         }
-        dev::wave_lds_fence();
+        dev::pn_fence<K>();
     }
 };
 
@@ -181,16 +204,16 @@ __device__ __forceinline__ void qn_ola_init(QNOla<K>& o, const FusedArgs& a, flo
 
 // ------------------------------------------------------------------ K_pair_stft
 template <int K>
-__global__ __launch_bounds__(64 * kNW, 2) void k_pn_stft(const PairSpecArgs pa) {
+__global__ __launch_bounds__(QN<K>::THREADS, 2) void k_pn_stft(const PairSpecArgs pa) {
     using G = QN<K>;
     const FusedArgs& a = pa.f;
     constexpr int N = G::N, E = G::E, P2 = G::P2, IB = G::IB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    QNSmem<K> sm(smem, wave, 0);
+    const int t = threadIdx.x % G::L;
+    const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x / G::L);  // the walk in the workgroup
+    QNSmem<K> sm(smem, pw, 0);
     qn_stage_tw<K>(sm.tw, a.t.ptw);
-    const int gw = blockIdx.x * kNW + wave;
+    const int gw = blockIdx.x * G::WALKS + pw;
     if (gw >= a.n_streams * a.n_chunks) return;
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
     const int f0 = c * a.M, f1 = min(a.F, f0 + a.M);  // (M even: chunks start on even frames)
@@ -199,7 +222,7 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_stft(const PairSpecArgs pa) 
     float* so = pa.spec + int64_t(s) * pa.ld_spec;
     float wa[E];
 #pragma unroll
-    for (int m = 0; m < E; ++m) wa[m] = G::valid(m, t) ? a.t.wa[t + 64 * m] : 0.0f;
+    for (int m = 0; m < E; ++m) wa[m] = G::valid(m, t) ? a.t.wa[t + G::L * m] : 0.0f;
     const float xlo = a.t.px_lo, xhi = a.t.px_hi;
     float fa[E], fb[E];
     auto load = [&](float (&f)[E], int k) { qn_load<K>(f, rx, t, k * H - a.pad, a.T, a.pad_mode); };
@@ -209,19 +232,19 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_stft(const PairSpecArgs pa) 
         const bool two = k + 1 < f1;
         float2* ra = reinterpret_cast<float2*>(so + int64_t(k) * pa.ld_frame);
         float2* rb = reinterpret_cast<float2*>(so + int64_t(k + 1) * pa.ld_frame);
-        const bool paired = qn_ok(fa, xlo, xhi) && qn_ok(fb, xlo, xhi);
+        const bool paired = sm.all(qn_ok(fa, xlo, xhi) && qn_ok(fb, xlo, xhi));
         auto pass = [&](auto pc_) {  // P = 0 / 1: frame k / k+1 alone; paired: both (P = 0)
             constexpr int P = decltype(pc_)::value;
 #pragma unroll
             for (int m = 0; m < E; ++m)
                 if (G::valid(m, t))
-                    sm.buf[t + 64 * m] = paired ? dev::pc_mk(fa[m] * wa[m], fb[m] * wa[m])
+                    sm.buf[t + G::L * m] = paired ? dev::pc_mk(fa[m] * wa[m], fb[m] * wa[m])
                                                 : dev::pc_mk(dev::sanit((P ? fb[m] : fa[m]) * wa[m]), 0.0f);
-            dev::wave_lds_fence();
+            dev::pn_fence<K>();
             G::fwd(sm.buf, sm.tw, t);
 #pragma unroll
             for (int i = 0; i < IB; ++i) {
-                const int kr = t + 64 * i;
+                const int kr = t + G::L * i;
                 if (kr <= P2) {
                     const dev::pc z = sm.buf[kr];
                     if (paired) {
@@ -233,7 +256,7 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_stft(const PairSpecArgs pa) 
                     }
                 }
             }
-            dev::wave_lds_fence();  // (the reads before the next transform's writes)
+            dev::pn_fence<K>();  // (the reads before the next transform's writes)
         };
         pass(std::integral_constant<int, 0>());
         if (!paired && two) pass(std::integral_constant<int, 1>());
@@ -244,26 +267,26 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_stft(const PairSpecArgs pa) 
 
 // ------------------------------------------------------------------ K_pair_istft
 template <int K, bool MASK>
-__global__ __launch_bounds__(64 * kNW, 2) void k_pn_istft(const PairSpecArgs pa) {
+__global__ __launch_bounds__(QN<K>::THREADS, 2) void k_pn_istft(const PairSpecArgs pa) {
     using G = QN<K>;
     const FusedArgs& a = pa.f;
     constexpr int N = G::N, E = G::E, P2 = G::P2, IB = G::IB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = threadIdx.x % G::L;
+    const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x / G::L);  // the walk in the workgroup
     const int H = a.hop, NB = (N + H - 1) / H, RL = qn_ring(N, H);
-    QNSmem<K> sm(smem, wave, RL);
+    QNSmem<K> sm(smem, pw, RL);
     qn_stage_tw<K>(sm.tw, a.t.ptw);
     QNWalk w;
-    if (!qn_walk(a, blockIdx.x * kNW + wave, NB, w)) return;
+    if (!qn_walk(a, blockIdx.x * G::WALKS + pw, NB, w)) return;
     QNOla<K> ola;
     qn_ola_init<K>(ola, a, sm.ring, RL, w, t);
     float wsg[E];
 #pragma unroll
-    for (int m = 0; m < E; ++m) wsg[m] = G::valid(m, t) ? a.t.ws[t + 64 * m] * a.gain : 0.0f;
+    for (int m = 0; m < E; ++m) wsg[m] = G::valid(m, t) ? a.t.ws[t + G::L * m] * a.gain : 0.0f;
     const float* sb = pa.sin + int64_t(w.s) * pa.ld_spec;
     const float* mrow0 = MASK ? pa.mask.p + int64_t(w.s) * pa.mask.ld_stream : nullptr;
-    // the pair's rows (and mask rows) by real bin kr = t + 64 i <= N/2, coalesced;
+    // the pair's rows (and mask rows) by real bin kr = t + L i <= N/2, coalesced;
     // stepped -- (X g) m, re and im each; DC and Nyquist imaginary parts dropped
     float2 ra_[IB], rb_[IB];
     auto load_rows = [&](int k) -> bool {
@@ -275,7 +298,7 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_istft(const PairSpecArgs pa)
         bool bad = false;
 #pragma unroll
         for (int i = 0; i < IB; ++i) {
-            const int kr = t + 64 * i;
+            const int kr = t + G::L * i;
             const bool on = kr <= P2;
             const float2 xa = on ? ra[kr] : make_float2(0.f, 0.f);
             const float2 xb = on && two ? rb[kr] : make_float2(0.f, 0.f);
@@ -302,7 +325,7 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_istft(const PairSpecArgs pa)
     auto put = [&](int form) {
 #pragma unroll
         for (int i = 0; i < IB; ++i) {
-            const int kr = t + 64 * i;
+            const int kr = t + G::L * i;
             if (kr <= P2) {
                 const float2 A = ra_[i], B = rb_[i];
                 dev::pc lo, hi;
@@ -318,10 +341,10 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_istft(const PairSpecArgs pa)
                 if (kr != 0 && kr != P2) sm.buf[N - kr] = hi;
             }
         }
-        dev::wave_lds_fence();
+        dev::pn_fence<K>();
     };
     for (int k = w.fs; k < w.f1; k += 2) {
-        if (load_rows(k)) {
+        if (sm.all(load_rows(k))) {
             put(0);
             G::inv(sm.buf, sm.tw, t);
             ola.template push<false>(sm.buf, wsg, a.inv_n, k);
@@ -345,38 +368,38 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_istft(const PairSpecArgs pa)
 
 // ------------------------------------------------------------------ K_pair_mask
 template <int K>
-__global__ __launch_bounds__(64 * kNW, 2) void k_pn_mask(const PairSpecArgs pa) {
+__global__ __launch_bounds__(QN<K>::THREADS, 2) void k_pn_mask(const PairSpecArgs pa) {
     using G = QN<K>;
     const FusedArgs& a = pa.f;
     constexpr int N = G::N, E = G::E, P2 = G::P2, IB = G::IB;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int t = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int t = threadIdx.x % G::L;
+    const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x / G::L);  // the walk in the workgroup
     const int H = a.hop, NB = (N + H - 1) / H, RL = qn_ring(N, H);
-    QNSmem<K> sm(smem, wave, RL);
+    QNSmem<K> sm(smem, pw, RL);
     qn_stage_tw<K>(sm.tw, a.t.ptw);
     QNWalk w;
-    if (!qn_walk(a, blockIdx.x * kNW + wave, NB, w)) return;
+    if (!qn_walk(a, blockIdx.x * G::WALKS + pw, NB, w)) return;
     QNOla<K> ola;
     qn_ola_init<K>(ola, a, sm.ring, RL, w, t);
     const __amdgpu_buffer_rsrc_t rx = dev::make_rsrc(a.x + int64_t(w.s) * a.ld_x, span_bytes(a.T, 1));
     float wa[E], wsg[E];
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        wa[m] = G::valid(m, t) ? a.t.wa[t + 64 * m] : 0.0f;
-        wsg[m] = G::valid(m, t) ? a.t.ws[t + 64 * m] * a.gain : 0.0f;
+        wa[m] = G::valid(m, t) ? a.t.wa[t + G::L * m] : 0.0f;
+        wsg[m] = G::valid(m, t) ? a.t.ws[t + G::L * m] * a.gain : 0.0f;
     }
     const float xlo = a.t.px_lo, xhi = a.t.px_hi * 0x1p-20f;  // (mask values up to 2^20)
     const float* mrow0 = pa.mask.p + int64_t(w.s) * pa.mask.ld_stream;
     auto row_a = [&](int k) { return mrow0 + int64_t(k) * pa.mask.ld_frame; };
     auto row_b = [&](int k) { return k + 1 < a.F ? row_a(k) + pa.mask.ld_frame : row_a(k); };  // (past F: unused)
-    float ma[IB], mb[IB];  // the pair's mask rows by real bin t + 64 i (<= N/2; 1 beyond)
+    float ma[IB], mb[IB];  // the pair's mask rows by real bin t + L i (<= N/2; 1 beyond)
     auto load_rows = [&](int k) {
         const float* r0 = row_a(k);
         const float* r1 = row_b(k);
 #pragma unroll
         for (int i = 0; i < IB; ++i) {
-            const int kr = t + 64 * i;
+            const int kr = t + G::L * i;
             ma[i] = kr <= P2 ? r0[kr] : 1.0f;
             mb[i] = kr <= P2 ? r1[kr] : 1.0f;
         }
@@ -394,18 +417,18 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_mask(const PairSpecArgs pa) 
     load(fb, w.fs + 1);
     load_rows(w.fs);
     for (int k = w.fs; k < w.f1; k += 2) {
-        const bool paired = qn_ok(fa, xlo, xhi) && qn_ok(fb, xlo, xhi) && rows_ok();
+        const bool paired = sm.all(qn_ok(fa, xlo, xhi) && qn_ok(fb, xlo, xhi) && rows_ok());
         const bool partner_frame = k + 1 < a.F;  // frame k+1 past the last: imaginary part 0
         if (paired) {
 #pragma unroll
             for (int m = 0; m < E; ++m)
-                if (G::valid(m, t)) sm.buf[t + 64 * m] = dev::pc_mk(fa[m] * wa[m], partner_frame ? fb[m] * wa[m] : 0.0f);
-            dev::wave_lds_fence();
+                if (G::valid(m, t)) sm.buf[t + G::L * m] = dev::pc_mk(fa[m] * wa[m], partner_frame ? fb[m] * wa[m] : 0.0f);
+            dev::pn_fence<K>();
             G::fwd(sm.buf, sm.tw, t);
             // the step on this lane's bin pairs {kr, N - kr}, in place
 #pragma unroll
             for (int i = 0; i < IB; ++i) {
-                const int kr = t + 64 * i;
+                const int kr = t + G::L * i;
                 if (kr <= P2) {
                     const int jr = kr == 0 ? 0 : N - kr;
                     const float g = a.t.gain ? a.t.gain[kr] : 1.0f;
@@ -417,7 +440,7 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_mask(const PairSpecArgs pa) 
                         sm.buf[jr] = dev::pc_mk(__builtin_fmaf(c2, z.x, c1 * zp.x), __builtin_fmaf(-c2, z.y, c1 * zp.y));
                 }
             }
-            dev::wave_lds_fence();
+            dev::pn_fence<K>();
             load(fa, k + 2);  // (in flight during the inverse and the OLA)
             load(fb, k + 3);
             if (k + 2 < w.f1) load_rows(k + 2);
@@ -430,17 +453,17 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_mask(const PairSpecArgs pa) 
             auto pass = [&](const float (&f)[E], const float* r, int kk) {
 #pragma unroll
                 for (int m = 0; m < E; ++m)
-                    if (G::valid(m, t)) sm.buf[t + 64 * m] = dev::pc_mk(dev::sanit(f[m] * wa[m]), 0.0f);
-                dev::wave_lds_fence();
+                    if (G::valid(m, t)) sm.buf[t + G::L * m] = dev::pc_mk(dev::sanit(f[m] * wa[m]), 0.0f);
+                dev::pn_fence<K>();
                 G::fwd(sm.buf, sm.tw, t);
 #pragma unroll
                 for (int m = 0; m < E; ++m) {
                     if (G::valid(m, t)) {
-                        const int n = t + 64 * m, kr = n <= P2 ? n : N - n;
+                        const int n = t + G::L * m, kr = n <= P2 ? n : N - n;
                         sm.buf[n] = sm.buf[n] * ((a.t.gain ? a.t.gain[kr] : 1.0f) * r[kr]);
                     }
                 }
-                dev::wave_lds_fence();
+                dev::pn_fence<K>();
                 G::inv(sm.buf, sm.tw, t);
                 ola.template push<false>(sm.buf, wsg, a.inv_n, kk);
                 ola.produce(kk);
@@ -454,15 +477,15 @@ __global__ __launch_bounds__(64 * kNW, 2) void k_pn_mask(const PairSpecArgs pa) 
     }
 }
 
-template <typename K>
-hipError_t qn_launch(K kernel, const PairSpecArgs& a, int n, int tw_len, int64_t waves, int32_t kind, bool ring,
-                     hipStream_t stream) {
-    const size_t lds = QNLds::bytes(n, tw_len, a.f.hop, ring);
+template <int K, typename KF>
+hipError_t qn_launch(KF kernel, const PairSpecArgs& a, int64_t walks, int32_t kind, bool ring, hipStream_t stream) {
+    using G = QN<K>;
+    const size_t lds = qn_lds<K>(a.f.hop, ring);
     hipError_t e = set_lds(kernel, lds);
     if (e != hipSuccess) return e;
-    const int64_t grid = (waves + kNW - 1) / kNW;
+    const int64_t grid = (walks + G::WALKS - 1) / G::WALKS;
     note_launch(kind, grid);
-    hipLaunchKernelGGL(kernel, dim3(unsigned(grid)), dim3(64 * kNW), lds, stream, a);
+    hipLaunchKernelGGL(kernel, dim3(unsigned(grid)), dim3(G::THREADS), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -472,7 +495,7 @@ int64_t qn_chunks(FusedArgs& f, int64_t F, int n_streams, int64_t min_m) {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
         cus = 256;
-    const int64_t resident = int64_t(cus) * 2 * kNW, S = std::max(1, n_streams);
+    const int64_t resident = int64_t(cus) * 8, S = std::max(1, n_streams);  // (walks a CU holds, about)
     int64_t c = std::max<int64_t>(1, std::min<int64_t>(F / min_m, (2 * resident + S - 1) / S));
     c = chunks_or(c, F);
     int64_t m = (F + c - 1) / c;
@@ -483,10 +506,11 @@ int64_t qn_chunks(FusedArgs& f, int64_t F, int n_streams, int64_t min_m) {
     return S * f.n_chunks;
 }
 
-// the one-wave plan keys (fft_pairn.h pn_factor; the release plans' radix lists)
+// the plan keys (fft_pairn.h pn_factor; the release plans' radix lists; 1764: two waves)
 template <typename F>
 bool qn_dispatch(int n, F&& f) {
     switch (n) {
+        case 1764: f(std::integral_constant<int, 1001764>{}); return true;
         case 320: f(std::integral_constant<int, 320>{}); return true;
         case 400: f(std::integral_constant<int, 400>{}); return true;
         case 640: f(std::integral_constant<int, 640>{}); return true;
@@ -528,7 +552,7 @@ hipError_t launch_pairn_stft(const Geometry& g, const DevTables& t, const float*
     hipError_t e = hipErrorInvalidValue;
     fk::qn_dispatch(g.n, [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        e = fk::qn_launch(fk::k_pn_stft<K>, a, g.n, fk::QN<K>::FAC.tw_len, waves, CRLOT_K_PAIR_STFT, false, stream);
+        e = fk::qn_launch<K>(fk::k_pn_stft<K>, a, waves, CRLOT_K_PAIR_STFT, false, stream);
     });
     return e;
 }
@@ -559,9 +583,8 @@ hipError_t launch_pairn_istft(const Geometry& g, const DevTables& t, const SpecM
     hipError_t e = hipErrorInvalidValue;
     fk::qn_dispatch(g.n, [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        constexpr int TL = fk::QN<K>::FAC.tw_len;
-        e = m.p ? fk::qn_launch(fk::k_pn_istft<K, true>, a, g.n, TL, waves, CRLOT_K_PAIR_ISTFT, true, stream)
-                : fk::qn_launch(fk::k_pn_istft<K, false>, a, g.n, TL, waves, CRLOT_K_PAIR_ISTFT, true, stream);
+        e = m.p ? fk::qn_launch<K>(fk::k_pn_istft<K, true>, a, waves, CRLOT_K_PAIR_ISTFT, true, stream)
+                : fk::qn_launch<K>(fk::k_pn_istft<K, false>, a, waves, CRLOT_K_PAIR_ISTFT, true, stream);
     });
     return e;
 }
@@ -594,7 +617,7 @@ hipError_t launch_pairn_masked(const Geometry& g, const DevTables& t, const Spec
     hipError_t e = hipErrorInvalidValue;
     fk::qn_dispatch(g.n, [&](auto kc) {
         constexpr int K = decltype(kc)::value;
-        e = fk::qn_launch(fk::k_pn_mask<K>, a, g.n, fk::QN<K>::FAC.tw_len, waves, CRLOT_K_PAIR_MASK, true, stream);
+        e = fk::qn_launch<K>(fk::k_pn_mask<K>, a, waves, CRLOT_K_PAIR_MASK, true, stream);
     });
     return e;
 }
