@@ -66,6 +66,7 @@ struct crlot_plan {
     float* d_wsn = nullptr;   // ws * (1/N)
     float* d_rden = nullptr;  // RN(1 / den) [ring], then {den, RN(1 / den)} pairs [ring][2]
     float* d_ptw = nullptr;   // frame-pair transform twiddles (N = 1024)
+    float* d_ptwn = nullptr;  // K_pairN's pass twiddles where d_ptw holds another transform's (1920 at even hops)
     float* d_pden = nullptr;  // K_pair per-block den | rden rows (N = 1024: 64 lanes, N = 4096: 256)
     float px_lo = 0.f, px_hi = 0.f;  // K_pair paired-regime sample range
     float gain_max = 1.f;     // max |spectral gain| (1 without one)
@@ -180,6 +181,7 @@ crlot::DevTables tables(const crlot_plan* p, const crlot::Scratch* sc = nullptr)
             t.ptw = p->d_ptw;
             t.pden = p->d_pden;
         }
+        if (crlot::pairn_size(p->geo.n)) t.ptwn = p->d_ptwn ? p->d_ptwn : p->d_ptw;
         const int n = p->geo.n;
         if (p->d_pden && (n == 512 || n == 1024 || n == 2048 || n == 4096)) t.pden2 = p->d_pden + 2 * p->geo.ring_len;
         if (sc) {
@@ -213,7 +215,7 @@ void free_plan(crlot_plan* p) {
         (void)hipStreamSynchronize(nullptr);
     }
     for (float* q : {p->d_wa, p->d_ws, p->d_den, p->d_tw, p->d_st, p->d_gain, p->d_wsn,
-                     p->d_rden, p->d_twany_own, p->d_ptw, p->d_pden})  // d_twany aliases d_tw or d_twany_own
+                     p->d_rden, p->d_twany_own, p->d_ptw, p->d_ptwn, p->d_pden})  // d_twany aliases d_tw or d_twany_own
         if (q) (void)hipFree(q);
     if (p->stage_pending) (void)hipEventSynchronize(p->stage_ev);
     if (p->stage_ev) (void)hipEventDestroy(p->stage_ev);
@@ -573,6 +575,14 @@ int crlot_plan_create(const crlot_plan_desc* desc_in, crlot_plan** out) {
             (e = hipMemcpy(p->d_ptw, ptw.data(), sizeof(float) * ptw.size(), hipMemcpyHostToDevice))) {
             free_plan(p);
             return hip_fail(e, "pair twiddles");
+        }
+        if (p->pair30 && crlot::pairn_size(n)) {  // the spectral entries' K_pairN transform (pairn_spec.hip)
+            const std::vector<float> pn = crlot::build_pairn_twiddles(n);
+            if ((e = hipMalloc(&p->d_ptwn, sizeof(float) * pn.size())) ||
+                (e = hipMemcpy(p->d_ptwn, pn.data(), sizeof(float) * pn.size(), hipMemcpyHostToDevice))) {
+                free_plan(p);
+                return hip_fail(e, "pair twiddles (K_pairN)");
+            }
         }
     }
     if (generic) p->d_twany = p->d_tw;  // the same allocation: W_P^k
@@ -1047,7 +1057,7 @@ int stft_impl(crlot_plan* p, const float* d_x, float* d_spec, int32_t n_streams,
         e = crlot::launch_pair15_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "stft (frame pairs, N = 960 / 480) kernel launch");
     }
-    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptw && t.wa &&
+    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptwn && t.wa &&
         aligned4(d_x) && T < (int64_t(1) << 27)) {
         // K_pairN's one-wave sizes (882, 1000, 640, 400, 320) as frame pairs (pairing off: the mixed-radix rfft below)
         e = crlot::launch_pairn_stft(p->geo, t, d_x, n_streams, T, ld_x, F, d_spec, ld_spec, ld_frame, s);
@@ -1093,7 +1103,7 @@ int istft_impl(crlot_plan* p, const float* d_spec, float* d_y, int32_t n_streams
         e = crlot::launch_pair15_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "istft (frame pairs, N = 960 / 480) kernel launch");
     }
-    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptw && t.ws && t.den &&
+    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptwn && t.ws && t.den &&
         aligned4(d_y) && F * p->geo.h + p->geo.n < (int64_t(1) << 27)) {
         // K_pairN's one-wave sizes as frame pairs (pairing off: the staged irfft + gather below)
         e = crlot::launch_pairn_istft(p->geo, t, p->mask, d_spec, ld_spec, ld_frame, d_y, n_streams, F, ld_y, s);
@@ -1144,7 +1154,7 @@ static int masked_roundtrip(crlot_plan* p, crlot::Scratch* sc, const float* d_x,
                                                          out_len, s);
         return e == hipSuccess ? CRLOT_OK : hip_fail(e, "masked frame-pair kernel launch (N = 960 / 480)");
     }
-    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptw && t.wa && t.ws &&
+    if (p->pairing && crlot::pairn_spec_supported(p->geo.n, p->geo.h, p->geo.ring_len) && t.ptwn && t.wa && t.ws &&
         t.den && aligned4(d_x) && aligned4(d_y) && T < (int64_t(1) << 27) && out_len + p->geo.n < (int64_t(1) << 27)) {
         // K_pairN's one-wave sizes as frame pairs, one walk (pairing off: spectra through HBM below)
         const hipError_t e = crlot::launch_pairn_masked(p->geo, t, p->mask, d_x, d_y, n_streams, T, ld_x, ld_y, F,

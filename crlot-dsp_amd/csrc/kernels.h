@@ -46,6 +46,10 @@ struct DevTables {
     // L = 256 / 128, SH = H/L.
     const float* ptw4 = nullptr;
     const float* pden4 = nullptr;
+    // K_pairN's pass twiddles for the spectral entries (pairn_spec.hip): ptw at its
+    // sizes, a table of their own where ptw holds another transform's (1920 at even
+    // hops: K_pair30's)
+    const float* ptwn = nullptr;
     // K_pair (N = 1024): one flag per walker wave, written by the paired-only
     // walker (1 = a pair of its chunk left the paired regime) and read by the
     // fix-up walker that redoes those chunks; pflags_len flags of capacity.

@@ -1,6 +1,6 @@
 // pairn_spec.hip -- the spectral entries and the masked round trip as frame
 // pairs at K_pairN's sizes 882 (20 ms at 44.1 kHz), 1000, 640, 400, 320 (one wave
-// per transform) and 1764 (40 ms at 44.1 kHz; two waves, one walk per
+// per transform) and 1764, 1920 (40 ms at 44.1 / 48 kHz; two waves, one walk per
 // workgroup), any hop H >= 32 whose ring the plan allows:
 //   K_pair_stft   k_pn_stft<K>        (crlot_stft)
 //   K_pair_istft  k_pn_istft<K,MASK>  (crlot_istft_ola)
@@ -8,7 +8,7 @@
 // on fft_pairn.h's transform (compile-time Stockham passes over composite
 // radices in one LDS buffer per transform, natural order in and out), frames
 // loaded whole and the overlap-add in a per-walk LDS ring, as K_pairN
-// (pair_n.hip).  At 1764 the transform spans the two waves of a workgroup (its
+// (pair_n.hip).  At 1764 and 1920 the transform spans the two waves of a workgroup (its
 // fences are barriers) and the regime verdicts are shared through LDS.
 //
 // The spectrum of the pair z = a w + i b w is in natural order in the wave's
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(QN<K>::THREADS, 2) void k_pn_stft(const PairSpecArg
     const int t = threadIdx.x % G::L;
     const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x / G::L);  // the walk in the workgroup
     QNSmem<K> sm(smem, pw, 0);
-    qn_stage_tw<K>(sm.tw, a.t.ptw);
+    qn_stage_tw<K>(sm.tw, a.t.ptwn);
     const int gw = blockIdx.x * G::WALKS + pw;
     if (gw >= a.n_streams * a.n_chunks) return;
     const int s = gw / a.n_chunks, c = gw - s * a.n_chunks;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(QN<K>::THREADS, 2) void k_pn_istft(const PairSpecAr
     const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x / G::L);  // the walk in the workgroup
     const int H = a.hop, NB = (N + H - 1) / H, RL = qn_ring(N, H);
     QNSmem<K> sm(smem, pw, RL);
-    qn_stage_tw<K>(sm.tw, a.t.ptw);
+    qn_stage_tw<K>(sm.tw, a.t.ptwn);
     QNWalk w;
     if (!qn_walk(a, blockIdx.x * G::WALKS + pw, NB, w)) return;
     QNOla<K> ola;
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(QN<K>::THREADS, 2) void k_pn_mask(const PairSpecArg
     const int pw = __builtin_amdgcn_readfirstlane(threadIdx.x / G::L);  // the walk in the workgroup
     const int H = a.hop, NB = (N + H - 1) / H, RL = qn_ring(N, H);
     QNSmem<K> sm(smem, pw, RL);
-    qn_stage_tw<K>(sm.tw, a.t.ptw);
+    qn_stage_tw<K>(sm.tw, a.t.ptwn);
     QNWalk w;
     if (!qn_walk(a, blockIdx.x * G::WALKS + pw, NB, w)) return;
     QNOla<K> ola;
@@ -506,11 +506,12 @@ int64_t qn_chunks(FusedArgs& f, int64_t F, int n_streams, int64_t min_m) {
     return S * f.n_chunks;
 }
 
-// the plan keys (fft_pairn.h pn_factor; the release plans' radix lists; 1764: two waves)
+// the plan keys (fft_pairn.h pn_factor; the release plans' radix lists; 1764, 1920: two waves)
 template <typename F>
 bool qn_dispatch(int n, F&& f) {
     switch (n) {
         case 1764: f(std::integral_constant<int, 1001764>{}); return true;
+        case 1920: f(std::integral_constant<int, 1001920>{}); return true;
         case 320: f(std::integral_constant<int, 320>{}); return true;
         case 400: f(std::integral_constant<int, 400>{}); return true;
         case 640: f(std::integral_constant<int, 640>{}); return true;
@@ -532,7 +533,7 @@ bool pairn_spec_supported(int n, int h, int ring_len) {
 hipError_t launch_pairn_stft(const Geometry& g, const DevTables& t, const float* x, int n_streams, int64_t T,
                              int64_t ld_x, int64_t F, float* spec, int64_t ld_spec, int64_t ld_frame,
                              hipStream_t stream) {
-    if (!pairn_spec_supported(g.n, g.h, g.ring_len) || F <= 0 || n_streams <= 0 || !t.ptw || !t.wa ||
+    if (!pairn_spec_supported(g.n, g.h, g.ring_len) || F <= 0 || n_streams <= 0 || !t.ptwn || !t.wa ||
         T >= (int64_t(1) << 27))
         return hipErrorInvalidValue;
     fk::PairSpecArgs a{};
@@ -561,7 +562,7 @@ hipError_t launch_pairn_stft(const Geometry& g, const DevTables& t, const float*
 hipError_t launch_pairn_istft(const Geometry& g, const DevTables& t, const SpecMask& m, const float* spec,
                               int64_t ld_spec, int64_t ld_frame, float* y, int n_streams, int64_t F, int64_t ld_y,
                               hipStream_t stream) {
-    if (!pairn_spec_supported(g.n, g.h, g.ring_len) || F <= 0 || n_streams <= 0 || !t.ptw || !t.ws || !t.den ||
+    if (!pairn_spec_supported(g.n, g.h, g.ring_len) || F <= 0 || n_streams <= 0 || !t.ptwn || !t.ws || !t.den ||
         F * g.h + g.n >= (int64_t(1) << 27))
         return hipErrorInvalidValue;
     fk::PairSpecArgs a{};
@@ -593,7 +594,7 @@ hipError_t launch_pairn_istft(const Geometry& g, const DevTables& t, const SpecM
 hipError_t launch_pairn_masked(const Geometry& g, const DevTables& t, const SpecMask& m, const float* x, float* y,
                                int n_streams, int64_t T, int64_t ld_x, int64_t ld_y, int64_t F, int64_t out_len,
                                hipStream_t stream) {
-    if (!pairn_spec_supported(g.n, g.h, g.ring_len) || F <= 0 || n_streams <= 0 || !m.p || !t.ptw || !t.wa ||
+    if (!pairn_spec_supported(g.n, g.h, g.ring_len) || F <= 0 || n_streams <= 0 || !m.p || !t.ptwn || !t.wa ||
         !t.ws || !t.den || T >= (int64_t(1) << 27) || out_len + g.n >= (int64_t(1) << 27))
         return hipErrorInvalidValue;
     fk::PairSpecArgs a{};

@@ -553,12 +553,13 @@ def test_spectral_entries_random_shapes(pkg, oracle, torch_cuda, seed):
 
 @pytest.mark.parametrize("n,h", [(960, 240), (960, 480), (960, 320), (960, 100), (480, 120), (480, 240), (480, 100),
                                  (882, 441), (882, 220), (1000, 250), (640, 320), (400, 160), (320, 160),
-                                 (1764, 441)])
+                                 (1764, 441), (1920, 480), (1920, 455)])
 def test_anysize_pair_spectral_entries(pkg, oracle, torch_cuda, n, h):
     """The any-size frame pairs: N = 960 / 480 (20 / 10 ms at 48 kHz) on K_pair15's
     transforms (at 480 the two halves of a wave walk two streams, an odd stream
-    count here) and 882 (20 ms at 44.1 kHz), 1000, 640, 400, 320, 1764 (two waves per
-    transform) on K_pairN's (any hop):
+    count here) and 882 (20 ms at 44.1 kHz), 1000, 640, 400, 320, 1764, 1920 (two waves
+    per transform; 1920 at an even hop with a twiddle table of its own beside K_pair30's)
+    on K_pairN's (any hop):
     crlot_stft, crlot_istft_ola and the masked round trip vs the oracle and vs the
     per-frame staged forms (frame pairing off) within the FFT tolerance, with NaN /
     Inf / tiny / huge samples (the per-frame regime), edited spectra and signed /
