@@ -433,6 +433,40 @@ def test_full_size_stft_istft(pkg, oracle, torch_cuda, n, h):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("n,h", [(960, 240), (1920, 480), (882, 441)])
+def test_full_size_anysize_stft_istft(pkg, oracle, torch_cuda, n, h):
+    """The any-size frame-pair entries (K_pair15's / K_pairN's transforms) at
+    1024 x 480000: istft_ola(stft(x)) deterministic, within the parity bar of the
+    per-frame entries, of crlot_roundtrip(x) and of the oracle on sampled streams;
+    the masked walk under an all-ones shared mask within the bar of the round trip."""
+    torch = torch_cuda
+    S, T = 1024, 480_000
+    g = torch.Generator(device="cuda").manual_seed(8765)
+    x = (torch.rand((S, T), generator=g, device="cuda") * 2 - 1) * 0.5
+    plan = pkg.Plan(frame_size=n, hop_size=h)
+    y = plan.istft_ola(plan.stft(x))
+    assert torch.equal(y, plan.istft_ola(plan.stft(x)))
+    plan.set_frame_pairing(False)
+    y_pf = plan.istft_ola(plan.stft(x))
+    plan.set_frame_pairing(True)
+    yr = plan.roundtrip(x)
+    F = plan.frame_count(T)
+    plan.set_spectral_mask(torch.ones((F, n // 2 + 1), device="cuda"))  # (one row per frame, shared)
+    ym = plan.roundtrip(x)
+    plan.set_spectral_mask(None)
+    assert bool(torch.isfinite(y).all()) and bool(torch.isfinite(ym).all())
+    for s in (0, 511, 1023):
+        xs = host(x[s])
+        nx = float(np.linalg.norm(xs))
+        ref = oracle.roundtrip(xs, n, h)
+        assert_close(host(y[s]), ref, 0.5, f"stft+istft pairs stream {s}", nx)
+        assert_close(host(y[s]), host(y_pf[s]), 0.5, f"pairs vs per frame stream {s}", nx)
+        assert_close(host(y[s]), host(yr[s]), 0.5, f"pairs vs roundtrip stream {s}", nx)
+        assert_close(host(ym[s]), host(yr[s]), 0.5, f"masked (ones) vs roundtrip stream {s}", nx)
+    del x, y, y_pf, yr, ym
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("n,h", sorted(PAIR_SPEC))
 def test_pair_stft_istft(pkg, oracle, torch_cuda, n, h):
     """K_pair_stft / K_pair_istft (N = 512 - 4096, frame pairing on): spectra and the
