@@ -693,7 +693,8 @@ def suite_stft(pkg, torch, dev):
     S, T = STREAMS, T_LEN
     g = torch.Generator(device=dev).manual_seed(41)
     x = (torch.rand((S, T), generator=g, device=dev) * 2 - 1) * 0.5
-    for n, h in ((1024, 256), (4096, 1024), (512, 128), (2048, 512), (960, 240), (480, 120)):
+    for n, h in ((1024, 256), (4096, 1024), (512, 128), (2048, 512), (960, 240), (480, 120),
+                 (882, 441), (1764, 441), (1920, 480)):  # (the last three: K_pairN's transforms)
         plan = pkg.Plan(frame_size=n, hop_size=h, device=dev.index)
         F, bins = plan.frame_count(T), n // 2 + 1
         spec = torch.empty((S, F, bins), dtype=torch.complex64, device=dev)
